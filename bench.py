@@ -1,0 +1,195 @@
+"""bench.py -- get_rows()/s on a Kingsford-shaped Multi-BRWT (BASELINE.json).
+
+Workload (config.workload): BASELINE.json configs[3] shape on one GPU per rank
+-- a 3.7 B x 2,652 Multi-BRWT (i.i.d. d = 0.3 % columns, basic arity-8
+partitioner, generated top-down on the device: DESIGN.md "Synthetic
+matrices"), replicated on every GPU; each rank queries its own 8 M-row batch
+(uniform 64-bit row ids, seed 42 + rank).  One step = one batched get_rows
+over the rank's batch, device-resident row ids -> CSR in HBM, plus (N > 1)
+the RCCL all-gatherv that reassembles the global CSR on every rank.
+
+Prints ONE JSON line (rank 0).  roofline: algorithmic bytes of the traversal
+kernel per launch (64 B x V + 8 + 8 + 4 B x L per row, V and
+L counted exactly on the device for the batch) / its HIP-event-timed average
+duration.  cpu_baseline: the oracle's restatement of BRWT::get_row on the
+same structure (generated on the host from the same spec), timed on a bounded
+row sample on all host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "get_rows()/s on Multi-BRWT, 3.7B×2,652 Kingsford-shape @1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level table (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--rows", type=int, default=3_700_000_000)
+    ap.add_argument("--cols", type=int, default=2652)
+    ap.add_argument("--density", type=float, default=0.003)
+    ap.add_argument("--arity", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=8_000_000, help="query rows per GPU")
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--no-gather", action="store_true", help="N>1: skip the all-gatherv reassembly")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--cpu-sample", type=int, default=400_000, help="rows timed on the CPU")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host cores")
+    ap.add_argument("--check-rows", type=int, default=20_000, help="GPU rows checked against the oracle")
+    ap.add_argument("--sort-rows", type=int, default=-1, help="-1 library default, 0/1 force")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    from genome_graph_annotation_amd import BRWTDevice, _lib as L
+    from genome_graph_annotation_amd.dist import allgatherv_csr
+
+    dev_t = torch.device("cuda", local)
+    t0 = time.time()
+    mat = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, device=local)
+    setup_s = time.time() - t0
+    if a.sort_rows >= 0:
+        mat.set_option(L.MBRWT_OPT_SORT_ROWS, a.sort_rows)
+
+    rows_np = np.random.default_rng(a.seed + 1000 * rank).integers(0, a.rows, a.batch, dtype=np.uint64)
+    rows_t = torch.from_numpy(rows_np.view(np.int64)).to(dev_t)
+    off_t = torch.empty(a.batch + 1, dtype=torch.int64, device=dev_t)
+    stream = torch.cuda.current_stream(dev_t)
+    sptr = stream.cuda_stream
+    # size the label buffer once (capacity protocol), outside the timed region
+    probe = torch.empty(1, dtype=torch.int32, device=dev_t)
+    try:
+        need = mat.get_rows_device(rows_t, off_t, probe, sptr)
+    except L.MBRWTError as e:
+        if e.status != L.MBRWT_ERR_CAPACITY:
+            raise
+        need = e.needed
+    cols_t = torch.empty(int(need * 1.02) + 1024, dtype=torch.int32, device=dev_t)
+
+    def step():
+        n_lab = mat.get_rows_device(rows_t, off_t, cols_t, sptr)
+        if world > 1 and not a.no_gather:
+            allgatherv_csr(off_t, cols_t[:n_lab])
+        return n_lab
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    mat.take_timing()
+    mat.set_option(L.MBRWT_OPT_TIMING, 1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        n_lab = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    mat.set_option(L.MBRWT_OPT_TIMING, 0)
+    kern_ms_total, launches = mat.take_timing()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # exact work accounting for the roofline (untimed diagnostic pass)
+    visits, labels = mat.count_work_device(rows_t, sptr)
+    assert labels == n_lab, (labels, n_lab)
+    alg_bytes = 64 * visits + 16 * a.batch + 4 * labels
+    kern_ms = kern_ms_total / max(1, launches)
+    achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+
+    # GPU result sample for the parity spot-check
+    chk = min(a.check_rows, a.batch)
+    off_h = off_t[: chk + 1].cpu().numpy().view(np.uint64)
+    cols_h = cols_t[: int(off_h[-1])].cpu().numpy().view(np.uint32)
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O  # CPU baseline leg only
+
+        threads = a.cpu_threads or len(os.sched_getaffinity(0))
+        threads = min(threads, 16)
+        g0 = time.time()
+        ref = O.OracleTree.topdown(a.rows, a.cols, a.density, a.arity, a.seed, threads)
+        gen_s = time.time() - g0
+        off_o, cols_o = ref.get_rows(rows_np[:chk], threads)
+        parity = bool(np.array_equal(off_o, off_h) and np.array_equal(cols_o, cols_h))
+        sample = rows_np[: a.cpu_sample]
+        c0 = time.perf_counter()
+        ref.time_rows(sample, threads)
+        cpu_s = time.perf_counter() - c0
+        cpu = {"value": len(sample) / cpu_s, "unit": "rows/s", "cores": threads, "kind": "port",
+               "sample": f"first {len(sample):,} rows of the rank-0 batch on the same {a.rows:,} x {a.cols:,} "
+                         f"structure (oracle restatement of BRWT::get_row, plain rank/select; host build {gen_s:.0f} s)"}
+        del ref
+
+    value = world * a.batch * a.steps / elapsed
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "rows/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32/u64",
+        "data": "synthetic (top-down i.i.d. Bernoulli columns, seed 42; uniform random rows)",
+        "config": {
+            "workload": f"Multi-BRWT {a.rows:,} x {a.cols:,}, d={a.density}, arity {a.arity} "
+                        f"(Kingsford shape, BASELINE configs[3]); batch {a.batch:,} rows per GPU",
+            "num_rows": a.rows, "num_columns": a.cols, "density": a.density, "arity": a.arity,
+            "batch_per_gpu": a.batch, "global_batch": a.batch * world,
+            "parallelism": f"batch-sharded x{world}, tree replicated" + ("" if world == 1 or a.no_gather
+                                                                         else ", RCCL all-gatherv"),
+            "structure_bytes": mat.device_bytes(), "setup_s": round(setup_s, 2),
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "kernel": "k_traverse", "kernel_ms": kern_ms,
+            "alg_bytes_per_launch": alg_bytes, "visits_per_row": visits / a.batch,
+            "labels_per_row": labels / a.batch,
+        },
+        "cpu_baseline": cpu,
+        "parity": None if parity is None else f"{'bit-exact' if parity else 'MISMATCH'} on {chk:,} rows vs oracle",
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,109 @@
+"""ctypes binding of libmbrwt.so (include/mbrwt.h).
+
+The binding is exactly what a reference-side maintainer would write (see
+INTEGRATION.md).  There is no fallback: if the HIP library is missing the
+import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmbrwt.so")
+
+MBRWT_OK = 0
+MBRWT_ERR_INVALID = 1
+MBRWT_ERR_RANGE = 2
+MBRWT_ERR_CAPACITY = 3
+MBRWT_ERR_UNSUPPORTED = 4
+MBRWT_ERR_DEVICE = 5
+MBRWT_ERR_NOMEM = 6
+
+MBRWT_OPT_TIMING = 1
+MBRWT_OPT_SLOT_LABELS = 2
+MBRWT_OPT_SORT_ROWS = 3
+
+u64p = C.POINTER(C.c_uint64)
+u32p = C.POINTER(C.c_uint32)
+u8p = C.POINTER(C.c_uint8)
+
+
+class TreeDesc(C.Structure):
+    _fields_ = [
+        ("num_rows", C.c_uint64),
+        ("num_columns", C.c_uint64),
+        ("num_nodes", C.c_uint32),
+        ("num_children", u32p),
+        ("first_child", u32p),
+        ("leaf_column", u32p),
+        ("vec_size", u64p),
+        ("vec_words", C.POINTER(u64p)),
+    ]
+
+
+class SynthDesc(C.Structure):
+    _fields_ = [
+        ("num_rows", C.c_uint64),
+        ("num_columns", C.c_uint64),
+        ("density", C.c_double),
+        ("arity", C.c_uint32),
+        ("seed", C.c_uint64),
+    ]
+
+
+# every symbol include/mbrwt.h declares, with its signature
+SIGNATURES = {
+    "mbrwt_create": (C.c_int, [C.POINTER(TreeDesc), C.c_int, C.POINTER(C.c_void_p)]),
+    "mbrwt_create_synthetic": (C.c_int, [C.POINTER(SynthDesc), C.c_int, C.POINTER(C.c_void_p)]),
+    "mbrwt_destroy": (None, [C.c_void_p]),
+    "mbrwt_num_rows": (C.c_uint64, [C.c_void_p]),
+    "mbrwt_num_columns": (C.c_uint64, [C.c_void_p]),
+    "mbrwt_num_relations": (C.c_uint64, [C.c_void_p]),
+    "mbrwt_num_nodes": (C.c_uint64, [C.c_void_p]),
+    "mbrwt_device_bytes": (C.c_uint64, [C.c_void_p]),
+    "mbrwt_device": (C.c_int, [C.c_void_p]),
+    "mbrwt_get_rows": (C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p, u32p, C.c_uint64, u64p]),
+    "mbrwt_get_rows_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
+                                        u64p, C.c_void_p]),
+    "mbrwt_get_batch": (C.c_int, [C.c_void_p, u64p, u64p, C.c_uint64, u8p]),
+    "mbrwt_get_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
+    "mbrwt_count_labels_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
+    "mbrwt_count_work_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, u64p, u64p, C.c_void_p]),
+    "mbrwt_set_option": (C.c_int, [C.c_void_p, C.c_int, C.c_int64]),
+    "mbrwt_take_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), u64p]),
+    "mbrwt_strerror": (C.c_char_p, [C.c_int]),
+    "mbrwt_last_error_message": (C.c_char_p, []),
+}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(there is no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+class MBRWTError(RuntimeError):
+    def __init__(self, status, where=""):
+        L = lib()
+        msg = L.mbrwt_strerror(status).decode()
+        detail = (L.mbrwt_last_error_message() or b"").decode()
+        super().__init__(f"{where}: {msg} ({detail})" if where else f"{msg} ({detail})")
+        self.status = status
+
+
+def check(status, where=""):
+    if status != MBRWT_OK:
+        raise MBRWTError(status, where)

@@ -1,0 +1,167 @@
+"""Python mirror of the reference's BinaryMatrix surface over the HIP engine.
+
+`BRWTDevice` answers the reference's BRWT queries (BinaryMatrix,
+common/binary_matrix.hpp:9-29; BRWT, annotation/hierarchical_annotation/
+BRWT.hpp:33-51) from a device-resident image through include/mbrwt.h.
+The C++ mirror used by C++ callers is csrc/brwt_device.hpp; this module is
+what the Python tests and bench.py drive.  Device-buffer entry points take
+torch tensors only as plumbing for device memory and streams.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+class BRWTDevice:
+    """A BRWT held in HBM; every query runs the HIP traversal kernels."""
+
+    def __init__(self, handle, keepalive=None):
+        self._h = handle
+        self._keep = keepalive
+
+    # -- construction -------------------------------------------------------
+    @classmethod
+    def from_tree(cls, tree, device=0):
+        """`tree`: BFS description (keys as include/mbrwt.h mbrwt_tree_desc:
+        num_rows, num_columns, num_children, first_child, leaf_column,
+        vec_size, words = list of uint64 arrays)."""
+        lib = L.lib()
+        N = int(len(tree["num_children"]))
+        nc = np.ascontiguousarray(tree["num_children"], dtype=np.uint32)
+        fc = np.ascontiguousarray(tree["first_child"], dtype=np.uint32)
+        lc = np.ascontiguousarray(tree["leaf_column"], dtype=np.uint32)
+        vs = np.ascontiguousarray(tree["vec_size"], dtype=np.uint64)
+        words = [np.ascontiguousarray(w, dtype=np.uint64) for w in tree["words"]]
+        ptrs = (L.u64p * max(1, N))()
+        for u, w in enumerate(words):
+            ptrs[u] = _p(w, C.c_uint64) if w.size else None
+        d = L.TreeDesc()
+        d.num_rows = int(tree["num_rows"])
+        d.num_columns = int(tree["num_columns"])
+        d.num_nodes = N
+        d.num_children = _p(nc, C.c_uint32)
+        d.first_child = _p(fc, C.c_uint32)
+        d.leaf_column = _p(lc, C.c_uint32)
+        d.vec_size = _p(vs, C.c_uint64)
+        d.vec_words = ptrs
+        h = C.c_void_p()
+        L.check(lib.mbrwt_create(C.byref(d), device, C.byref(h)), "mbrwt_create")
+        return cls(h)
+
+    @classmethod
+    def synthetic(cls, num_rows, num_columns, density, arity=8, seed=42, device=0):
+        lib = L.lib()
+        d = L.SynthDesc(num_rows, num_columns, float(density), arity, seed)
+        h = C.c_void_p()
+        L.check(lib.mbrwt_create_synthetic(C.byref(d), device, C.byref(h)), "mbrwt_create_synthetic")
+        return cls(h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            L.lib().mbrwt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- properties -----------------------------------------------------------
+    def num_rows(self):
+        return L.lib().mbrwt_num_rows(self._h)
+
+    def num_columns(self):
+        return L.lib().mbrwt_num_columns(self._h)
+
+    def num_relations(self):
+        return L.lib().mbrwt_num_relations(self._h)
+
+    def num_nodes(self):
+        return L.lib().mbrwt_num_nodes(self._h)
+
+    def device_bytes(self):
+        return L.lib().mbrwt_device_bytes(self._h)
+
+    # -- host-buffer queries --------------------------------------------------
+    def get_rows(self, rows):
+        """Batched BRWT::get_row (BRWT.cpp:26-53) -> (offsets[n+1], cols)."""
+        lib = L.lib()
+        rows = np.ascontiguousarray(rows, dtype=np.uint64)
+        n = len(rows)
+        offsets = np.zeros(n + 1, dtype=np.uint64)
+        need = C.c_uint64(0)
+        cap = max(16, n * 16)
+        while True:
+            cols = np.zeros(cap, dtype=np.uint32)
+            st = lib.mbrwt_get_rows(self._h, _p(rows, C.c_uint64), n, _p(offsets, C.c_uint64),
+                                    _p(cols, C.c_uint32), cap, C.byref(need))
+            if st == L.MBRWT_ERR_CAPACITY:
+                cap = int(need.value)
+                continue
+            L.check(st, "mbrwt_get_rows")
+            return offsets, cols[: need.value]
+
+    def get_row(self, row):
+        off, cols = self.get_rows(np.array([row], dtype=np.uint64))
+        return cols.tolist()
+
+    def get_batch(self, rows, cols):
+        """Batched BRWT::get (BRWT.cpp:9-24)."""
+        rows = np.ascontiguousarray(rows, dtype=np.uint64)
+        cols = np.ascontiguousarray(cols, dtype=np.uint64)
+        out = np.zeros(max(1, len(rows)), dtype=np.uint8)
+        L.check(L.lib().mbrwt_get_batch(self._h, _p(rows, C.c_uint64), _p(cols, C.c_uint64), len(rows),
+                                        _p(out, C.c_uint8)), "mbrwt_get_batch")
+        return out[: len(rows)].astype(bool)
+
+    def get(self, row, col):
+        return bool(self.get_batch([row], [col])[0])
+
+    # -- device-buffer queries (torch tensors as plumbing) ---------------------
+    def get_rows_device(self, rows_t, offsets_t, cols_t, stream=None):
+        """rows_t: uint64/int64 cuda tensor [n]; offsets_t: [n+1] 64-bit; cols_t:
+        int32 [cap].  Returns the number of labels; raises on capacity."""
+        need = C.c_uint64(0)
+        st = L.lib().mbrwt_get_rows_device(self._h, rows_t.data_ptr(), rows_t.numel(), offsets_t.data_ptr(),
+                                           cols_t.data_ptr(), cols_t.numel(), C.byref(need),
+                                           stream if stream is not None else None)
+        if st == L.MBRWT_ERR_CAPACITY:
+            e = L.MBRWTError(st, "mbrwt_get_rows_device")
+            e.needed = int(need.value)
+            raise e
+        L.check(st, "mbrwt_get_rows_device")
+        return int(need.value)
+
+    def get_batch_device(self, rows_t, cols_t, out_t, stream=None):
+        L.check(L.lib().mbrwt_get_batch_device(self._h, rows_t.data_ptr(), cols_t.data_ptr(), rows_t.numel(),
+                                               out_t.data_ptr(), stream), "mbrwt_get_batch_device")
+
+    def count_labels_device(self, rows_t, counts_t, stream=None):
+        L.check(L.lib().mbrwt_count_labels_device(self._h, rows_t.data_ptr(), rows_t.numel(), counts_t.data_ptr(),
+                                                  stream), "mbrwt_count_labels_device")
+
+    def count_work_device(self, rows_t, stream=None):
+        v = C.c_uint64(0)
+        lab = C.c_uint64(0)
+        L.check(L.lib().mbrwt_count_work_device(self._h, rows_t.data_ptr(), rows_t.numel(), C.byref(v),
+                                                C.byref(lab), stream), "mbrwt_count_work_device")
+        return int(v.value), int(lab.value)
+
+    # -- options / measurement ------------------------------------------------
+    def set_option(self, option, value):
+        L.check(L.lib().mbrwt_set_option(self._h, option, int(value)), "mbrwt_set_option")
+
+    def take_timing(self):
+        ms = C.c_double(0)
+        k = C.c_uint64(0)
+        L.check(L.lib().mbrwt_take_timing(self._h, C.byref(ms), C.byref(k)), "mbrwt_take_timing")
+        return ms.value, int(k.value)

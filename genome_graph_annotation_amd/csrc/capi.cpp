@@ -1,0 +1,303 @@
+// capi.cpp -- the extern "C" boundary of libmbrwt (include/mbrwt.h).
+// Never throws across the ABI; every failure is an MBRWT_* status plus a
+// thread-local message (mbrwt_last_error_message).
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "mbrwt_internal.hpp"
+
+namespace mbrwt {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string &msg) { g_last_error = msg; }
+
+int hip_fail(hipError_t e, const char *what) {
+    g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+    (void)hipGetLastError();  // clear the sticky non-fatal error
+    return (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) ? MBRWT_ERR_NOMEM : MBRWT_ERR_DEVICE;
+}
+
+static int upload_tables(Ctx &c) {
+    Tree &t = c.tree;
+    if (!t.nodes.empty()) {
+        MBRWT_HIP(hipMalloc(&c.d_nodes, t.nodes.size() * sizeof(DevNode)));
+        MBRWT_HIP(hipMemcpy(c.d_nodes, t.nodes.data(), t.nodes.size() * sizeof(DevNode), hipMemcpyHostToDevice));
+    }
+    if (!t.col_path.empty()) {
+        MBRWT_HIP(hipMalloc(&c.d_col_path, t.col_path.size()));
+        MBRWT_HIP(hipMemcpy(c.d_col_path, t.col_path.data(), t.col_path.size(), hipMemcpyHostToDevice));
+    }
+    if (!t.col_leaf.empty()) {
+        MBRWT_HIP(hipMalloc(&c.d_col_leaf, t.col_leaf.size() * 4));
+        MBRWT_HIP(hipMemcpy(c.d_col_leaf, t.col_leaf.data(), t.col_leaf.size() * 4, hipMemcpyHostToDevice));
+    }
+    MBRWT_HIP(hipHostMalloc(reinterpret_cast<void **>(&c.h_scalars), 8 * sizeof(uint64_t), hipHostMallocDefault));
+    MBRWT_HIP(hipMalloc(&c.d_scalars, 8 * sizeof(uint64_t)));
+    MBRWT_HIP(hipEventCreate(&c.ev0));
+    MBRWT_HIP(hipEventCreate(&c.ev1));
+    return MBRWT_OK;
+}
+
+static void release(Ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    free_tree(c->tree);
+    for (Workspace *w : {&c->ws_temp, &c->ws_counts, &c->ws_ovf, &c->ws_scan, &c->ws_rows, &c->ws_out, &c->ws_sort})
+        if (w->buf) (void)hipFree(w->buf);
+    if (c->d_nodes) (void)hipFree(c->d_nodes);
+    if (c->d_col_path) (void)hipFree(c->d_col_path);
+    if (c->d_col_leaf) (void)hipFree(c->d_col_leaf);
+    if (c->d_scalars) (void)hipFree(c->d_scalars);
+    if (c->h_scalars) (void)hipHostFree(c->h_scalars);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+template <class Build>
+static int create_common(int device, mbrwt_ctx **out, Build &&build) {
+    if (!out) {
+        set_error("null output pointer");
+        return MBRWT_ERR_INVALID;
+    }
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        set_error("no HIP device available");
+        return MBRWT_ERR_DEVICE;
+    }
+    if (device < 0 || device >= ndev) {
+        set_error("device index out of range");
+        return MBRWT_ERR_INVALID;
+    }
+    Ctx *c = new (std::nothrow) Ctx();
+    if (!c) return MBRWT_ERR_NOMEM;
+    c->device = device;
+    int rc = MBRWT_OK;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        rc = hip_fail(hipGetLastError(), "stream creation");
+    }
+    if (!rc) rc = build(*c);
+    if (!rc) rc = upload_tables(*c);
+    if (rc) {
+        release(c);
+        return rc;
+    }
+    *out = reinterpret_cast<mbrwt_ctx *>(c);
+    return MBRWT_OK;
+}
+
+static Ctx *C(mbrwt_ctx *p) { return reinterpret_cast<Ctx *>(p); }
+static const Ctx *C(const mbrwt_ctx *p) { return reinterpret_cast<const Ctx *>(p); }
+
+}  // namespace mbrwt
+
+using namespace mbrwt;
+
+extern "C" {
+
+int mbrwt_create(const mbrwt_tree_desc *desc, int device, mbrwt_ctx **out) {
+    if (!desc) {
+        set_error("null tree description");
+        return MBRWT_ERR_INVALID;
+    }
+    try {
+        return create_common(device, out, [&](Ctx &c) { return build_from_desc(*desc, device, c.tree); });
+    } catch (const std::bad_alloc &) {
+        set_error("host allocation failed");
+        return MBRWT_ERR_NOMEM;
+    } catch (...) {
+        set_error("unexpected exception in mbrwt_create");
+        return MBRWT_ERR_INVALID;
+    }
+}
+
+int mbrwt_create_synthetic(const mbrwt_synth_desc *desc, int device, mbrwt_ctx **out) {
+    if (!desc) {
+        set_error("null synthetic description");
+        return MBRWT_ERR_INVALID;
+    }
+    try {
+        return create_common(device, out,
+                             [&](Ctx &c) { return build_synthetic(*desc, device, c.tree, c.stream); });
+    } catch (const std::bad_alloc &) {
+        set_error("host allocation failed");
+        return MBRWT_ERR_NOMEM;
+    } catch (...) {
+        set_error("unexpected exception in mbrwt_create_synthetic");
+        return MBRWT_ERR_INVALID;
+    }
+}
+
+void mbrwt_destroy(mbrwt_ctx *ctx) { release(C(ctx)); }
+
+uint64_t mbrwt_num_rows(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.num_rows : 0; }
+uint64_t mbrwt_num_columns(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.num_columns : 0; }
+uint64_t mbrwt_num_relations(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.num_relations : 0; }
+uint64_t mbrwt_num_nodes(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.num_nodes : 0; }
+uint64_t mbrwt_device_bytes(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.image_bytes : 0; }
+int mbrwt_device(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->device : -1; }
+
+int mbrwt_get_rows_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols,
+                          uint64_t cols_cap, uint64_t *cols_needed, void *stream) {
+    if (!ctx || (n && (!d_rows || !d_offsets)) || (!n && !d_offsets)) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    try {
+        if (hipSetDevice(c.device) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
+        return run_get_rows(c, d_rows, n, d_offsets, d_cols, d_cols ? cols_cap : 0, cols_needed,
+                            reinterpret_cast<hipStream_t>(stream));
+    } catch (...) {
+        set_error("unexpected exception in mbrwt_get_rows_device");
+        return MBRWT_ERR_INVALID;
+    }
+}
+
+int mbrwt_get_rows(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n, uint64_t *offsets, uint32_t *cols,
+                   uint64_t cols_cap, uint64_t *cols_needed) {
+    if (!ctx || !offsets || (n && !rows)) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    try {
+        MBRWT_HIP(hipSetDevice(c.device));
+        int rc;
+        if ((rc = ensure(c.ws_rows, (n + 1) * sizeof(uint64_t) * 2))) return rc;
+        uint64_t *d_rows = reinterpret_cast<uint64_t *>(c.ws_rows.buf);
+        uint64_t *d_off = d_rows + n;
+        if (n) MBRWT_HIP(hipMemcpyAsync(d_rows, rows, n * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+        uint64_t needed = 0;
+        // size the output buffer from a first pass over the batch, then fill
+        uint64_t cap = cols_cap;
+        if ((rc = ensure(c.ws_out, std::max<uint64_t>(cap, 1) * sizeof(uint32_t)))) return rc;
+        rc = run_get_rows(c, d_rows, n, d_off, reinterpret_cast<uint32_t *>(c.ws_out.buf), cap, &needed, c.stream);
+        if (cols_needed) *cols_needed = needed;
+        if (rc) return rc;
+        MBRWT_HIP(hipMemcpyAsync(offsets, d_off, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+        if (needed)
+            MBRWT_HIP(hipMemcpyAsync(cols, c.ws_out.buf, needed * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+        MBRWT_HIP(hipStreamSynchronize(c.stream));
+        return MBRWT_OK;
+    } catch (...) {
+        set_error("unexpected exception in mbrwt_get_rows");
+        return MBRWT_ERR_INVALID;
+    }
+}
+
+int mbrwt_get_batch_device(mbrwt_ctx *ctx, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n,
+                           uint8_t *d_out, void *stream) {
+    if (!ctx || (n && (!d_rows || !d_cols || !d_out))) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    MBRWT_HIP(hipSetDevice(c.device));
+    return run_get_batch(c, d_rows, d_cols, n, d_out, reinterpret_cast<hipStream_t>(stream));
+}
+
+int mbrwt_get_batch(mbrwt_ctx *ctx, const uint64_t *rows, const uint64_t *cols, uint64_t n, uint8_t *out) {
+    if (!ctx || (n && (!rows || !cols || !out))) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    MBRWT_HIP(hipSetDevice(c.device));
+    if (!n) return MBRWT_OK;
+    int rc;
+    if ((rc = ensure(c.ws_rows, n * sizeof(uint64_t) * 2 + n))) return rc;
+    uint64_t *d_r = reinterpret_cast<uint64_t *>(c.ws_rows.buf);
+    uint64_t *d_c = d_r + n;
+    uint8_t *d_o = reinterpret_cast<uint8_t *>(d_c + n);
+    MBRWT_HIP(hipMemcpyAsync(d_r, rows, n * 8, hipMemcpyHostToDevice, c.stream));
+    MBRWT_HIP(hipMemcpyAsync(d_c, cols, n * 8, hipMemcpyHostToDevice, c.stream));
+    rc = run_get_batch(c, d_r, d_c, n, d_o, c.stream);
+    if (rc) return rc;
+    MBRWT_HIP(hipMemcpyAsync(out, d_o, n, hipMemcpyDeviceToHost, c.stream));
+    MBRWT_HIP(hipStreamSynchronize(c.stream));
+    return MBRWT_OK;
+}
+
+int mbrwt_count_labels_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts,
+                              void *stream) {
+    if (!ctx || (n && !d_rows) || !d_counts) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    MBRWT_HIP(hipSetDevice(c.device));
+    return run_count_labels(c, d_rows, n, d_counts, reinterpret_cast<hipStream_t>(stream));
+}
+
+int mbrwt_count_work_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, uint64_t *sum_visits,
+                            uint64_t *sum_labels, void *stream) {
+    if (!ctx || (n && !d_rows)) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    MBRWT_HIP(hipSetDevice(c.device));
+    return run_count_work(c, d_rows, n, sum_visits, sum_labels, reinterpret_cast<hipStream_t>(stream));
+}
+
+int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value) {
+    if (!ctx) return MBRWT_ERR_INVALID;
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    switch (option) {
+    case MBRWT_OPT_TIMING:
+        c.timing = value != 0;
+        return MBRWT_OK;
+    case MBRWT_OPT_SLOT_LABELS:
+        if (value < 0 || value > 4096) return MBRWT_ERR_INVALID;
+        c.slot_labels = (uint32_t)value;
+        return MBRWT_OK;
+    case MBRWT_OPT_SORT_ROWS:
+        c.sort_rows = value != 0;
+        return MBRWT_OK;
+    default:
+        set_error("unknown option");
+        return MBRWT_ERR_INVALID;
+    }
+}
+
+int mbrwt_take_timing(mbrwt_ctx *ctx, double *kernel_ms, uint64_t *launches) {
+    if (!ctx) return MBRWT_ERR_INVALID;
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (kernel_ms) *kernel_ms = c.timing_ms;
+    if (launches) *launches = c.timing_launches;
+    c.timing_ms = 0;
+    c.timing_launches = 0;
+    return MBRWT_OK;
+}
+
+const char *mbrwt_strerror(int status) {
+    switch (status) {
+    case MBRWT_OK: return "ok";
+    case MBRWT_ERR_INVALID: return "invalid argument";
+    case MBRWT_ERR_RANGE: return "row or column out of range";
+    case MBRWT_ERR_CAPACITY: return "output capacity too small";
+    case MBRWT_ERR_UNSUPPORTED: return "unsupported tree shape";
+    case MBRWT_ERR_DEVICE: return "HIP device error";
+    case MBRWT_ERR_NOMEM: return "out of memory";
+    default: return "unknown status";
+    }
+}
+
+const char *mbrwt_last_error_message(void) { return g_last_error.c_str(); }
+
+}  // extern "C"

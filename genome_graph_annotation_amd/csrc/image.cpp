@@ -1,0 +1,260 @@
+// image.cpp -- builds the device image of a BRWT from a tree description
+// (include/mbrwt.h mbrwt_tree_desc), replacing BRWT::load (BRWT.cpp:87-111)
+// as the way structure enters the engine.  Layout: mbrwt_internal.hpp.
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mbrwt_internal.hpp"
+
+namespace mbrwt {
+
+namespace {
+
+inline uint64_t popc(uint64_t x) { return (uint64_t)__builtin_popcountll(x); }
+
+inline bool bit_at(const uint64_t *w, uint64_t i) { return (w[i >> 6] >> (i & 63)) & 1; }
+
+uint64_t count_ones(const uint64_t *w, uint64_t size) {
+    uint64_t c = 0, W = size / 64;
+    for (uint64_t k = 0; k < W; ++k) c += popc(w[k]);
+    if (size & 63) c += popc(w[W] & ((1ull << (size & 63)) - 1));
+    return c;
+}
+
+// 32-bit chunk b of a bit vector, tail bits past `size` cleared
+inline uint32_t chunk32(const uint64_t *w, uint64_t size, uint64_t b) {
+    uint64_t lo = b * 32;
+    if (lo >= size) return 0;
+    uint32_t v = (uint32_t)(w[b >> 1] >> (32 * (b & 1)));
+    uint64_t valid = size - lo;
+    if (valid < 32) v &= (1u << valid) - 1;
+    return v;
+}
+
+// Build the children image of one internal dnode: children vectors are
+// child_words[c] (length L each).
+int upload_image(const std::vector<const uint64_t *> &child_words, const std::vector<bool> &child_is_leaf,
+                 uint64_t L, DevNode &dn, std::vector<void *> &images, uint64_t &image_bytes) {
+    const uint32_t a = (uint32_t)child_words.size();
+    bool all_leaves = std::all_of(child_is_leaf.begin(), child_is_leaf.end(), [](bool b) { return b; });
+    std::vector<uint8_t> host;
+    if (all_leaves) {
+        dn.kind = mask_kind(a);
+        const uint32_t w = mask_bytes(dn.kind);
+        host.assign(L * w + kImagePad, 0);
+        for (uint32_t c = 0; c < a; ++c) {
+            const uint64_t *cw = child_words[c];
+            const uint64_t W = (L + 63) / 64;
+            for (uint64_t k = 0; k < W; ++k) {
+                uint64_t x = cw[k];
+                if (k == W - 1 && (L & 63)) x &= (1ull << (L & 63)) - 1;
+                while (x) {
+                    uint64_t j = k * 64 + (uint64_t)__builtin_ctzll(x);
+                    x &= x - 1;
+                    uint8_t *p = &host[j * w];
+                    uint64_t m = 0;
+                    std::memcpy(&m, p, w);
+                    m |= 1ull << c;
+                    std::memcpy(p, &m, w);
+                }
+            }
+        }
+    } else {
+        dn.kind = KIND_PLANE;
+        dn.stride = plane_stride(a);
+        const uint64_t blocks = (L + 31) / 32;
+        host.assign(blocks * dn.stride + kImagePad, 0);
+        for (uint32_t c = 0; c < a; ++c) {
+            uint32_t rank = 0;
+            for (uint64_t b = 0; b < blocks; ++b) {
+                uint32_t bits = chunk32(child_words[c], L, b);
+                uint8_t *p = &host[b * dn.stride + 8ull * c];
+                std::memcpy(p, &rank, 4);
+                std::memcpy(p + 4, &bits, 4);
+                rank += (uint32_t)__builtin_popcount(bits);
+            }
+        }
+    }
+    dn.arity = (uint16_t)a;
+    dn.length = L;
+    void *d = nullptr;
+    MBRWT_HIP(hipMalloc(&d, host.size()));
+    images.push_back(d);
+    MBRWT_HIP(hipMemcpy(d, host.data(), host.size(), hipMemcpyHostToDevice));
+    dn.base = (uint64_t)(uintptr_t)d;
+    image_bytes += host.size();
+    return MBRWT_OK;
+}
+
+}  // namespace
+
+int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
+    MBRWT_HIP(hipSetDevice(device));
+    tree = Tree();
+    tree.num_rows = desc.num_rows;
+    tree.num_columns = desc.num_columns;
+    const uint32_t N = desc.num_nodes;
+    tree.num_nodes = N;
+    if (N == 0) {  // BRWT(): no columns, no rows (test_BRWT.cpp:15-19)
+        if (desc.num_columns != 0 || desc.num_rows != 0) {
+            set_error("empty tree description with nonzero shape");
+            return MBRWT_ERR_INVALID;
+        }
+        return finalize_tree(tree);
+    }
+    if (!desc.num_children || !desc.first_child || !desc.leaf_column || !desc.vec_size || !desc.vec_words) {
+        set_error("null array in tree description");
+        return MBRWT_ERR_INVALID;
+    }
+    if (desc.num_rows > kMaxRows) {
+        set_error("num_rows >= 2^32 is not supported by this build");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
+    if (desc.vec_size[0] != desc.num_rows) {
+        set_error("root index column length != num_rows");
+        return MBRWT_ERR_INVALID;
+    }
+    // structural validation: BFS numbering, children contiguous, each child
+    // column as long as its parent's popcount (BRWT invariant, BRWT.cpp:43)
+    std::vector<uint8_t> seen(N, 0);
+    std::vector<uint64_t> ones(N);
+    uint64_t leaves = 0;
+    for (uint32_t u = 0; u < N; ++u) {
+        if (!desc.vec_words[u] && desc.vec_size[u]) {
+            set_error("null index column");
+            return MBRWT_ERR_INVALID;
+        }
+        ones[u] = desc.vec_size[u] ? count_ones(desc.vec_words[u], desc.vec_size[u]) : 0;
+    }
+    std::vector<uint8_t> col_seen(desc.num_columns, 0);
+    for (uint32_t u = 0; u < N; ++u) {
+        const uint32_t a = desc.num_children[u];
+        if (a == 0) {
+            ++leaves;
+            uint32_t col = desc.leaf_column[u];
+            if (col >= desc.num_columns || col_seen[col]) {
+                set_error("leaf column out of range or duplicated");
+                return MBRWT_ERR_INVALID;
+            }
+            col_seen[col] = 1;
+            continue;
+        }
+        if (a > kMaxArity) {
+            set_error("node arity > 64 is not supported by this build");
+            return MBRWT_ERR_UNSUPPORTED;
+        }
+        const uint64_t fc = desc.first_child[u];
+        if (fc <= u || fc + a > N) {
+            set_error("children not in BFS order");
+            return MBRWT_ERR_INVALID;
+        }
+        for (uint32_t c = 0; c < a; ++c) {
+            if (seen[fc + c]++) {
+                set_error("node has two parents");
+                return MBRWT_ERR_INVALID;
+            }
+            if (desc.vec_size[fc + c] != ones[u]) {
+                set_error("child index column length != parent popcount");
+                return MBRWT_ERR_INVALID;
+            }
+        }
+    }
+    if (leaves != desc.num_columns) {
+        set_error("number of leaves != num_columns");
+        return MBRWT_ERR_INVALID;
+    }
+
+    tree.nodes.assign(N + 1, DevNode{});
+    // leaves and node wiring
+    for (uint32_t u = 0; u < N; ++u) {
+        DevNode &dn = tree.nodes[u + 1];
+        if (desc.num_children[u] == 0) {
+            dn.kind = KIND_LEAF;
+            dn.label = desc.leaf_column[u];
+            tree.num_relations += ones[u];
+        } else {
+            dn.first_child = desc.first_child[u] + 1;
+            dn.label = UINT32_MAX;
+        }
+        tree.max_arity = std::max<uint32_t>(tree.max_arity, desc.num_children[u]);
+    }
+    // super-root: its single child is the root
+    {
+        DevNode &sr = tree.nodes[0];
+        sr.first_child = 1;
+        sr.label = UINT32_MAX;
+        int rc = upload_image({desc.vec_words[0]}, {desc.num_children[0] == 0}, desc.num_rows, sr, tree.images,
+                              tree.image_bytes);
+        if (rc) return rc;
+    }
+    for (uint32_t u = 0; u < N; ++u) {
+        const uint32_t a = desc.num_children[u];
+        if (!a) continue;
+        std::vector<const uint64_t *> cw(a);
+        std::vector<bool> leaf(a);
+        for (uint32_t c = 0; c < a; ++c) {
+            cw[c] = desc.vec_words[desc.first_child[u] + c];
+            leaf[c] = desc.num_children[desc.first_child[u] + c] == 0;
+        }
+        int rc = upload_image(cw, leaf, ones[u], tree.nodes[u + 1], tree.images, tree.image_bytes);
+        if (rc) return rc;
+    }
+    return finalize_tree(tree);
+}
+
+int finalize_tree(Tree &tree) {
+    const uint32_t D = (uint32_t)tree.nodes.size();
+    if (D == 0) return MBRWT_OK;
+    // consecutive-label flag for MASK nodes
+    for (uint32_t v = 0; v < D; ++v) {
+        DevNode &dn = tree.nodes[v];
+        if (dn.kind < KIND_MASK8) continue;
+        bool consec = true;
+        for (uint32_t c = 0; c < dn.arity; ++c)
+            if (tree.nodes[dn.first_child + c].label != tree.nodes[dn.first_child].label + c) consec = false;
+        if (consec) {
+            dn.flags |= FLAG_CONSEC_LABELS;
+            dn.label = tree.nodes[dn.first_child].label;
+        }
+    }
+    // depth-first walk: stack depth (KIND_PLANE frames) and column paths
+    std::vector<uint32_t> parent(D, UINT32_MAX), cidx(D, 0), depth(D, 0), planes(D, 0);
+    uint32_t max_depth = 0;
+    for (uint32_t v = 0; v < D; ++v) {
+        const DevNode &dn = tree.nodes[v];
+        if (dn.kind == KIND_LEAF) continue;
+        for (uint32_t c = 0; c < dn.arity; ++c) {
+            uint32_t w = dn.first_child + c;
+            parent[w] = v;
+            cidx[w] = c;
+            depth[w] = depth[v] + 1;
+            planes[w] = planes[v] + (dn.kind == KIND_PLANE ? 1 : 0);
+            max_depth = std::max(max_depth, depth[w]);
+            tree.stack_depth = std::max(tree.stack_depth, planes[w]);
+        }
+    }
+    tree.path_len = std::max<uint32_t>(1, max_depth);
+    tree.col_path.assign(tree.num_columns * tree.path_len, 0);
+    tree.col_leaf.assign(tree.num_columns, 0);
+    for (uint32_t v = 0; v < D; ++v) {
+        const DevNode &dn = tree.nodes[v];
+        if (dn.kind != KIND_LEAF || v == 0) continue;
+        uint32_t col = dn.label;
+        tree.col_leaf[col] = v;
+        // path from the super-root down to the leaf
+        std::vector<uint8_t> rev;
+        for (uint32_t w = v; parent[w] != UINT32_MAX; w = parent[w]) rev.push_back((uint8_t)cidx[w]);
+        std::reverse(rev.begin(), rev.end());
+        for (size_t k = 0; k < rev.size(); ++k) tree.col_path[(uint64_t)col * tree.path_len + k] = rev[k];
+    }
+    return MBRWT_OK;
+}
+
+void free_tree(Tree &tree) {
+    for (void *p : tree.images) (void)hipFree(p);
+    tree.images.clear();
+}
+
+}  // namespace mbrwt

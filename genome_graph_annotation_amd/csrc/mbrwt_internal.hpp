@@ -1,0 +1,138 @@
+// mbrwt_internal.hpp -- device image format and context of libmbrwt.
+//
+// Device image of a BRWT (DESIGN.md "Data layout in HBM"):
+//   * dnode 0 is a virtual super-root with one child, the BRWT root; dnode
+//     u+1 is tree node u (BFS numbering of mbrwt_tree_desc).  Visiting the
+//     super-root at position `row` reads the root's index bit and rank, so
+//     get_row(row) is one uniform descent (BRWT.cpp:30 + :43).
+//   * An internal node u does not store its own index column; it stores the
+//     columns of ALL its children interleaved ("sibling-interleaved"): every
+//     child of u is probed at the same index j = rank1(u, i) - 1
+//     (BRWT.cpp:43-51), so one block read answers every child's
+//     operator[] and rank1 at j:
+//       KIND_PLANE : per 32-position block, for each child c an 8-byte
+//                    {u32 rank of child c before the block, u32 bits of child
+//                    c in the block}; block stride = pow2ceil(8 * arity).
+//       KIND_MASK* : (all children are leaves) one arity-bit mask per position,
+//                    1/2/4/8 bytes wide; leaves need no rank.
+//   * Leaves have no image; their global column (RangePartition::get composed
+//     along the path, utils.cpp:689-691) is in DevNode::label.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mbrwt.h"
+
+namespace mbrwt {
+
+enum : uint8_t {
+    KIND_LEAF = 0,
+    KIND_PLANE = 1,
+    KIND_MASK8 = 2,
+    KIND_MASK16 = 3,
+    KIND_MASK32 = 4,
+    KIND_MASK64 = 5,
+};
+enum : uint8_t { FLAG_CONSEC_LABELS = 1 };
+
+struct alignas(32) DevNode {
+    uint64_t base;         // device address of the children image (internal nodes)
+    uint32_t first_child;  // dnode id of child 0 (internal nodes)
+    uint32_t label;        // leaf: global column; MASK with FLAG_CONSEC_LABELS: label of child 0
+    uint32_t stride;       // KIND_PLANE: bytes per 32-position block
+    uint16_t arity;
+    uint8_t kind;
+    uint8_t flags;
+    uint64_t length;       // positions in the image (= length of every child's index column)
+};
+static_assert(sizeof(DevNode) == 32, "DevNode must be 32 bytes");
+
+constexpr uint32_t kMaxArity = 64;       // child masks are held in <= 64 bits
+constexpr uint32_t kImagePad = 64;       // bytes of zero padding after every image
+constexpr uint64_t kMaxRows = 0xFFFFFFFFull;  // positions are 32-bit in the kernels
+
+inline uint32_t plane_stride(uint32_t arity) {  // >= 16: blocks are read as 16-byte pairs
+    uint32_t s = 16;
+    while (s < 8u * arity) s <<= 1;
+    return s;
+}
+inline uint8_t mask_kind(uint32_t arity) {
+    return arity <= 8 ? KIND_MASK8 : arity <= 16 ? KIND_MASK16 : arity <= 32 ? KIND_MASK32 : KIND_MASK64;
+}
+inline uint32_t mask_bytes(uint8_t kind) { return 1u << (kind - KIND_MASK8); }
+
+// Host-side mirror of the device node table plus ownership of the images.
+struct Tree {
+    std::vector<DevNode> nodes;             // dnode table (host copy)
+    std::vector<void *> images;             // device allocations, one per internal dnode
+    std::vector<uint8_t> col_path;          // [num_columns][max_depth] child index path per column
+    std::vector<uint32_t> col_leaf;         // dnode of the leaf holding each column
+    uint32_t path_len = 0;                  // max_depth stride of col_path
+    uint32_t stack_depth = 0;               // max KIND_PLANE dnodes on a root path (incl. super)
+    uint32_t max_arity = 0;
+    uint64_t num_rows = 0, num_columns = 0, num_relations = 0, num_nodes = 0;
+    uint64_t image_bytes = 0;
+};
+
+struct Workspace {
+    void *buf = nullptr;
+    size_t bytes = 0;
+};
+
+struct Ctx {
+    int device = 0;
+    Tree tree;
+    DevNode *d_nodes = nullptr;
+    uint8_t *d_col_path = nullptr;
+    uint32_t *d_col_leaf = nullptr;
+    hipStream_t stream = nullptr;       // stream of the host-buffer API
+    std::mutex mu;
+
+    // reusable device workspace (grown on demand, never inside a timed call
+    // once warmed up)
+    Workspace ws_temp, ws_counts, ws_ovf, ws_scan, ws_rows, ws_out, ws_sort;
+    uint64_t *h_scalars = nullptr;      // pinned: [0] total, [1] overflow count, [2] error
+    uint64_t *d_scalars = nullptr;      // device twin
+
+    // options
+    bool timing = false;
+    uint32_t slot_labels = 0;           // 0 = auto
+    bool sort_rows = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double timing_ms = 0;
+    uint64_t timing_launches = 0;
+    int grid_cache = 0;
+};
+
+// status helpers ---------------------------------------------------------
+void set_error(const std::string &msg);
+int hip_fail(hipError_t e, const char *what);
+
+#define MBRWT_HIP(call)                                          \
+    do {                                                         \
+        hipError_t _e = (call);                                  \
+        if (_e != hipSuccess) return ::mbrwt::hip_fail(_e, #call); \
+    } while (0)
+
+int ensure(Workspace &w, size_t bytes);
+
+// image construction (image.cpp / synth.hip)
+int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree);
+int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStream_t stream);
+void free_tree(Tree &tree);
+// finish a Tree whose nodes/images are set: column paths, stack depth
+int finalize_tree(Tree &tree);
+
+// queries (query.hip)
+int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
+                 uint64_t *needed, hipStream_t s);
+int run_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n, uint8_t *d_out, hipStream_t s);
+int run_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts, hipStream_t s);
+int run_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s);
+
+}  // namespace mbrwt

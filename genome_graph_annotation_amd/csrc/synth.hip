@@ -1,0 +1,491 @@
+// synth.hip -- top-down synthetic Multi-BRWT generated straight into the
+// device image (DESIGN.md "Synthetic matrices").
+//
+// Law: a BRWT of the basic arity-k partitioner shape (BRWT_builders.cpp:20-31,
+// pass-through of singleton groups :74-76) built from i.i.d. Bernoulli(d)
+// columns (experiments/data_generation.cpp:20-29).  Given that row r reaches
+// node u (u's index bit set), the children's "subtree nonzero" indicators are
+// independent Bernoulli(q_c), q_c = 1 - (1-d)^cols(c), conditioned on not all
+// being zero -- the conditional law of OR-ed i.i.d. columns.  The root bit is
+// Bernoulli(q_root).  Each position draws ONE 64-bit hash of (seed, node,
+// position) and maps it through the node's inverse-CDF table over nonzero
+// child masks, so the structure is a pure function of the seed; the CPU
+// oracle implements the same spec independently (oracle/brwt_oracle.cpp).
+//
+// The 3.7 B x 2,652 Kingsford shape (~77 G mask draws, ~127 GB image) is
+// generated level by level in a few seconds; the reference's column-major
+// mt19937 path would need ~1.2 TB of raw bits.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <vector>
+
+#include "mbrwt_internal.hpp"
+
+namespace mbrwt {
+
+namespace {
+
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t node_key(uint64_t seed, uint64_t key) {
+    return mix64(seed ^ ((key + 1) * 0x9E3779B97F4A7C15ull));
+}
+__host__ __device__ __forceinline__ uint64_t draw(uint64_t k, uint64_t pos) {
+    return mix64(k + pos * 0xD1B54A32D192ED03ull);
+}
+constexpr uint64_t kRootKey = 0xFFFFFFFFull;
+constexpr uint32_t kSynthMaxArity = 12;
+
+uint64_t prob_to_threshold(double p) {
+    if (!(p > 0.0)) return 0;
+    if (p >= 1.0) return UINT64_MAX;
+    return (uint64_t)(p * 18446744073709551616.0);
+}
+
+// inverse-CDF thresholds over nonzero masks 1..2^a-1 (same order of
+// floating-point operations as the spec; built with -ffp-contract=off)
+std::vector<uint64_t> mask_table(const std::vector<double> &q) {
+    const size_t a = q.size();
+    const size_t nm = (1ull << a) - 1;
+    std::vector<uint64_t> T(nm, UINT64_MAX);
+    double prod0 = 1.0;
+    for (size_t c = 0; c < a; ++c) prod0 = prod0 * (1.0 - q[c]);
+    const double Z = 1.0 - prod0;
+    if (!(Z > 0.0)) return T;
+    double cum = 0.0;
+    for (size_t k = 1; k <= nm; ++k) {
+        double p = 1.0;
+        for (size_t c = 0; c < a; ++c) p = p * (((k >> c) & 1) ? q[c] : (1.0 - q[c]));
+        cum = cum + p / Z;
+        T[k - 1] = (k == nm) ? UINT64_MAX : prob_to_threshold(cum);
+    }
+    return T;
+}
+
+__device__ __forceinline__ bool bern(uint64_t x, uint64_t t) { return x < t || t == UINT64_MAX; }
+
+__device__ __forceinline__ uint32_t draw_mask(const uint64_t *__restrict__ T, uint32_t nT, uint64_t x) {
+    uint32_t lo = 0, hi = nT - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (x < T[mid]) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo + 1;
+}
+
+// ---- image kernels -----------------------------------------------------
+
+// super-root as KIND_PLANE with one child (the internal root): bits of the
+// root index column, Bernoulli(q_root) per row
+__global__ __launch_bounds__(256) void k_gen_root_plane(uint8_t *img, uint64_t L, uint64_t K, uint64_t T,
+                                                         uint32_t stride) {
+    const uint64_t nb = (L + 31) / 32;
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gs) {
+        uint32_t bits = 0;
+        for (uint32_t t = 0; t < 32; ++t) {
+            const uint64_t j = b * 32 + t;
+            if (j < L && bern(draw(K, j), T)) bits |= 1u << t;
+        }
+        *reinterpret_cast<uint2 *>(img + b * stride) = make_uint2(0u, bits);
+    }
+}
+
+// super-root as KIND_MASK8 when the root is a leaf (one column)
+__global__ __launch_bounds__(256) void k_gen_root_mask(uint8_t *img, uint64_t L, uint64_t K, uint64_t T,
+                                                        unsigned long long *ones) {
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t local = 0;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < L; j += gs) {
+        const uint8_t b = bern(draw(K, j), T) ? 1 : 0;
+        img[j] = b;
+        local += b;
+    }
+    if (local) atomicAdd(ones, (unsigned long long)local);
+}
+
+// internal node with at least one internal child: KIND_PLANE blocks
+template <int A>
+__global__ __launch_bounds__(256) void k_gen_plane(uint8_t *img, uint64_t L, uint64_t K,
+                                                   const uint64_t *__restrict__ Tg, uint32_t nT, uint32_t stride) {
+    __shared__ uint64_t T[(1 << A) - 1];
+    for (uint32_t i = threadIdx.x; i < nT; i += blockDim.x) T[i] = Tg[i];
+    __syncthreads();
+    const uint64_t nb = (L + 31) / 32;
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gs) {
+        uint32_t bits[A];
+#pragma unroll
+        for (int c = 0; c < A; ++c) bits[c] = 0;
+        for (uint32_t t = 0; t < 32; ++t) {
+            const uint64_t j = b * 32 + t;
+            if (j >= L) break;
+            const uint32_t m = draw_mask(T, nT, draw(K, j));
+#pragma unroll
+            for (int c = 0; c < A; ++c) bits[c] |= ((m >> c) & 1u) << t;
+        }
+        uint8_t *blk = img + b * stride;
+#pragma unroll
+        for (int c = 0; c < A; ++c) *reinterpret_cast<uint2 *>(blk + 8 * c) = make_uint2(0u, bits[c]);
+    }
+}
+
+// internal node whose children are all leaves: one mask per position
+template <typename W, int A>
+__global__ __launch_bounds__(256) void k_gen_mask(W *img, uint64_t L, uint64_t K, const uint64_t *__restrict__ Tg,
+                                                  uint32_t nT, unsigned long long *ones) {
+    __shared__ uint64_t T[(1 << A) - 1];
+    for (uint32_t i = threadIdx.x; i < nT; i += blockDim.x) T[i] = Tg[i];
+    __syncthreads();
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t local = 0;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < L; j += gs) {
+        const uint32_t m = draw_mask(T, nT, draw(K, j));
+        img[j] = (W)m;
+        local += (uint64_t)__builtin_popcount(m);
+    }
+    // wave-level reduction before the atomic
+    for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off);
+    if ((threadIdx.x & 63) == 0 && local) atomicAdd(ones, (unsigned long long)local);
+}
+
+// ---- per-child rank scan over the blocks of a KIND_PLANE image ----------
+constexpr int kScanTile = 256;  // blocks per tile (one thread per block)
+
+__global__ __launch_bounds__(kScanTile) void k_tile_sums(const uint8_t *img, uint64_t nb, uint32_t a,
+                                                         uint32_t stride, uint64_t *tile_sums) {
+    typedef hipcub::BlockReduce<uint32_t, kScanTile> BR;
+    __shared__ typename BR::TempStorage tmp;
+    const uint64_t tile = blockIdx.x;
+    const uint64_t b = tile * kScanTile + threadIdx.x;
+    for (uint32_t c = 0; c < a; ++c) {
+        uint32_t v = 0;
+        if (b < nb) v = __builtin_popcount(reinterpret_cast<const uint2 *>(img + b * stride + 8 * c)->y);
+        const uint32_t s = BR(tmp).Sum(v);
+        if (threadIdx.x == 0) tile_sums[tile * a + c] = s;
+        __syncthreads();
+    }
+}
+
+// exclusive scan of tile sums per child (one workgroup per child), totals out
+__global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t *tile_sums, uint64_t ntiles, uint32_t a,
+                                                     uint64_t *totals) {
+    typedef hipcub::BlockScan<uint64_t, 1024> BS;
+    __shared__ typename BS::TempStorage tmp;
+    __shared__ uint64_t carry;
+    const uint32_t c = blockIdx.x;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint64_t base = 0; base < ntiles; base += 1024) {
+        const uint64_t t = base + threadIdx.x;
+        const uint64_t v = t < ntiles ? tile_sums[t * a + c] : 0;
+        uint64_t ex, agg;
+        BS(tmp).ExclusiveSum(v, ex, agg);
+        const uint64_t cr = carry;
+        if (t < ntiles) tile_sums[t * a + c] = cr + ex;
+        __syncthreads();
+        if (threadIdx.x == 0) carry = cr + agg;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) totals[c] = carry;
+}
+
+__global__ __launch_bounds__(kScanTile) void k_write_ranks(uint8_t *img, uint64_t nb, uint32_t a, uint32_t stride,
+                                                           const uint64_t *tile_offsets) {
+    typedef hipcub::BlockScan<uint32_t, kScanTile> BS;
+    __shared__ typename BS::TempStorage tmp;
+    const uint64_t tile = blockIdx.x;
+    const uint64_t b = tile * kScanTile + threadIdx.x;
+    for (uint32_t c = 0; c < a; ++c) {
+        uint2 *e = reinterpret_cast<uint2 *>(img + b * stride + 8 * c);
+        uint32_t v = 0;
+        if (b < nb) v = __builtin_popcount(e->y);
+        uint32_t ex;
+        BS(tmp).ExclusiveSum(v, ex);
+        if (b < nb) e->x = (uint32_t)(tile_offsets[tile * a + c] + ex);
+        __syncthreads();
+    }
+}
+
+int launch_grid(uint64_t items) { return (int)std::max<uint64_t>(1, std::min<uint64_t>((items + 255) / 256, 65536)); }
+
+// rank scan of a KIND_PLANE image; returns per-child totals (lengths of the
+// children's index columns)
+int plane_scan(uint8_t *img, uint64_t L, uint32_t a, uint32_t stride, std::vector<uint64_t> &totals,
+               hipStream_t s) {
+    const uint64_t nb = (L + 31) / 32;
+    const uint64_t ntiles = std::max<uint64_t>(1, (nb + kScanTile - 1) / kScanTile);
+    uint64_t *d_tiles = nullptr, *d_tot = nullptr;
+    MBRWT_HIP(hipMalloc(&d_tiles, ntiles * a * sizeof(uint64_t)));
+    MBRWT_HIP(hipMalloc(&d_tot, a * sizeof(uint64_t)));
+    if (nb) {
+        hipLaunchKernelGGL(k_tile_sums, dim3((unsigned)ntiles), dim3(kScanTile), 0, s, img, nb, a, stride, d_tiles);
+        MBRWT_HIP(hipGetLastError());
+    } else {
+        MBRWT_HIP(hipMemsetAsync(d_tiles, 0, ntiles * a * sizeof(uint64_t), s));
+    }
+    hipLaunchKernelGGL(k_scan_tiles, dim3(a), dim3(1024), 0, s, d_tiles, ntiles, a, d_tot);
+    MBRWT_HIP(hipGetLastError());
+    if (nb) {
+        hipLaunchKernelGGL(k_write_ranks, dim3((unsigned)ntiles), dim3(kScanTile), 0, s, img, nb, a, stride, d_tiles);
+        MBRWT_HIP(hipGetLastError());
+    }
+    totals.assign(a, 0);
+    MBRWT_HIP(hipMemcpyAsync(totals.data(), d_tot, a * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    MBRWT_HIP(hipStreamSynchronize(s));
+    MBRWT_HIP(hipFree(d_tiles));
+    MBRWT_HIP(hipFree(d_tot));
+    return MBRWT_OK;
+}
+
+struct ShapeNode {
+    std::vector<uint32_t> children;
+    uint64_t cols = 0;
+    uint32_t column = UINT32_MAX;  // leaves
+};
+
+// basic-partitioner shape in BFS numbering (node 0 = root)
+std::vector<ShapeNode> basic_shape(uint64_t m, uint32_t arity) {
+    std::vector<ShapeNode> all;
+    std::vector<uint32_t> cur;
+    for (uint64_t i = 0; i < m; ++i) {
+        ShapeNode s;
+        s.cols = 1;
+        s.column = (uint32_t)i;
+        all.push_back(s);
+        cur.push_back((uint32_t)i);
+    }
+    while (cur.size() > 1) {
+        std::vector<uint32_t> next;
+        for (size_t b = 0; b < cur.size(); b += arity) {
+            const size_t e = std::min<size_t>(cur.size(), b + arity);
+            if (e - b == 1) {
+                next.push_back(cur[b]);
+                continue;
+            }
+            ShapeNode p;
+            for (size_t i = b; i < e; ++i) {
+                p.children.push_back(cur[i]);
+                p.cols += all[cur[i]].cols;
+            }
+            all.push_back(p);
+            next.push_back((uint32_t)all.size() - 1);
+        }
+        cur.swap(next);
+    }
+    std::vector<uint32_t> order{cur[0]};
+    for (size_t h = 0; h < order.size(); ++h)
+        for (uint32_t c : all[order[h]].children) order.push_back(c);
+    std::vector<uint32_t> newid(all.size());
+    for (size_t i = 0; i < order.size(); ++i) newid[order[i]] = (uint32_t)i;
+    std::vector<ShapeNode> bfs;
+    bfs.reserve(order.size());
+    for (uint32_t o : order) {
+        ShapeNode s = all[o];
+        for (auto &c : s.children) c = newid[c];
+        bfs.push_back(s);
+    }
+    return bfs;
+}
+
+template <int A>
+void launch_plane(uint8_t *img, uint64_t L, uint64_t K, const uint64_t *T, uint32_t nT, uint32_t stride,
+                  hipStream_t s) {
+    hipLaunchKernelGGL(k_gen_plane<A>, dim3(launch_grid((L + 31) / 32)), dim3(256), 0, s, img, L, K, T, nT, stride);
+}
+template <typename W, int A>
+void launch_mask(uint8_t *img, uint64_t L, uint64_t K, const uint64_t *T, uint32_t nT, unsigned long long *ones,
+                 hipStream_t s) {
+    hipLaunchKernelGGL((k_gen_mask<W, A>), dim3(launch_grid(L)), dim3(256), 0, s, reinterpret_cast<W *>(img), L, K,
+                       T, nT, ones);
+}
+
+using PlaneFn = void (*)(uint8_t *, uint64_t, uint64_t, const uint64_t *, uint32_t, uint32_t, hipStream_t);
+using MaskFn = void (*)(uint8_t *, uint64_t, uint64_t, const uint64_t *, uint32_t, unsigned long long *, hipStream_t);
+
+PlaneFn plane_fn(uint32_t a) {
+    static const PlaneFn t[] = {nullptr, launch_plane<1>, launch_plane<2>, launch_plane<3>, launch_plane<4>,
+                                launch_plane<5>, launch_plane<6>, launch_plane<7>, launch_plane<8>, launch_plane<9>,
+                                launch_plane<10>, launch_plane<11>, launch_plane<12>};
+    return a <= kSynthMaxArity ? t[a] : nullptr;
+}
+MaskFn mask_fn(uint32_t a) {
+    static const MaskFn t[] = {nullptr,
+                               launch_mask<uint8_t, 1>,  launch_mask<uint8_t, 2>,   launch_mask<uint8_t, 3>,
+                               launch_mask<uint8_t, 4>,  launch_mask<uint8_t, 5>,   launch_mask<uint8_t, 6>,
+                               launch_mask<uint8_t, 7>,  launch_mask<uint8_t, 8>,   launch_mask<uint16_t, 9>,
+                               launch_mask<uint16_t, 10>, launch_mask<uint16_t, 11>, launch_mask<uint16_t, 12>};
+    return a <= kSynthMaxArity ? t[a] : nullptr;
+}
+
+}  // namespace
+
+int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStream_t s) {
+    MBRWT_HIP(hipSetDevice(device));
+    tree = Tree();
+    const uint64_t n = desc.num_rows, m = desc.num_columns;
+    const double d = desc.density;
+    if (desc.arity < 2 || desc.arity > kSynthMaxArity || !(d >= 0.0 && d <= 1.0)) {
+        set_error("synthetic: arity must be in [2,12] and density in [0,1]");
+        return MBRWT_ERR_INVALID;
+    }
+    if (n > kMaxRows) {
+        set_error("synthetic: num_rows >= 2^32 is not supported by this build");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
+    tree.num_rows = n;
+    tree.num_columns = m;
+    if (m == 0) {
+        tree.num_rows = 0;
+        return finalize_tree(tree);
+    }
+    const auto shape = basic_shape(m, desc.arity);
+    const uint32_t N = (uint32_t)shape.size();
+    tree.num_nodes = N;
+    std::vector<double> q(N);
+    for (uint32_t u = 0; u < N; ++u) q[u] = 1.0 - std::pow(1.0 - d, (double)shape[u].cols);
+
+    tree.nodes.assign(N + 1, DevNode{});
+    for (uint32_t u = 0; u < N; ++u) {
+        DevNode &dn = tree.nodes[u + 1];
+        const auto &sh = shape[u];
+        if (sh.children.empty()) {
+            dn.kind = KIND_LEAF;
+            dn.label = sh.column;
+            continue;
+        }
+        bool all_leaves = true;
+        for (uint32_t c : sh.children) all_leaves &= shape[c].children.empty();
+        dn.arity = (uint16_t)sh.children.size();
+        dn.first_child = sh.children[0] + 1;
+        dn.label = UINT32_MAX;
+        dn.kind = all_leaves ? mask_kind(dn.arity) : KIND_PLANE;
+        if (dn.kind == KIND_PLANE) dn.stride = std::max<uint32_t>(16, plane_stride(dn.arity));
+        tree.max_arity = std::max<uint32_t>(tree.max_arity, dn.arity);
+    }
+    // per-node inverse-CDF tables, deduplicated by the children's q profile
+    std::map<std::vector<double>, uint64_t *> tables;
+    std::vector<uint64_t *> node_T(N, nullptr);
+    int rc = MBRWT_OK;
+    auto cleanup = [&]() {
+        for (auto &kv : tables) (void)hipFree(kv.second);
+    };
+    for (uint32_t u = 0; u < N && !rc; ++u) {
+        const auto &sh = shape[u];
+        if (sh.children.empty()) continue;
+        std::vector<double> qc;
+        for (uint32_t c : sh.children) qc.push_back(q[c]);
+        auto it = tables.find(qc);
+        if (it == tables.end()) {
+            auto T = mask_table(qc);
+            uint64_t *dT = nullptr;
+            if (hipMalloc(&dT, T.size() * 8) != hipSuccess ||
+                hipMemcpy(dT, T.data(), T.size() * 8, hipMemcpyHostToDevice) != hipSuccess) {
+                rc = hip_fail(hipErrorOutOfMemory, "synthetic table upload");
+                break;
+            }
+            it = tables.emplace(qc, dT).first;
+        }
+        node_T[u] = it->second;
+    }
+    if (rc) {
+        cleanup();
+        return rc;
+    }
+    unsigned long long *d_ones = nullptr;
+    if (hipMalloc(&d_ones, sizeof(unsigned long long)) != hipSuccess) {
+        cleanup();
+        return hip_fail(hipErrorOutOfMemory, "hipMalloc");
+    }
+    (void)hipMemsetAsync(d_ones, 0, sizeof(unsigned long long), s);
+
+    auto alloc_image = [&](DevNode &dn, uint64_t bytes) -> uint8_t * {
+        void *p = nullptr;
+        if (hipMalloc(&p, bytes + kImagePad) != hipSuccess) return nullptr;
+        (void)hipMemsetAsync(p, 0, bytes + kImagePad, s);
+        tree.images.push_back(p);
+        tree.image_bytes += bytes + kImagePad;
+        dn.base = (uint64_t)(uintptr_t)p;
+        return reinterpret_cast<uint8_t *>(p);
+    };
+    auto fail = [&](int code, const char *what) {
+        cleanup();
+        (void)hipFree(d_ones);
+        set_error(what);
+        return code;
+    };
+
+    // super-root: the root's index column (Bernoulli(q_root) per row)
+    {
+        DevNode &sr = tree.nodes[0];
+        sr.first_child = 1;
+        sr.arity = 1;
+        sr.label = UINT32_MAX;
+        sr.length = n;
+        const uint64_t K = node_key(desc.seed, kRootKey);
+        const uint64_t T = prob_to_threshold(q[0]);
+        if (shape[0].children.empty()) {  // one column: the root is a leaf
+            sr.kind = KIND_MASK8;
+            uint8_t *img = alloc_image(sr, n);
+            if (!img) return fail(MBRWT_ERR_NOMEM, "device allocation failed");
+            hipLaunchKernelGGL(k_gen_root_mask, dim3(launch_grid(n)), dim3(256), 0, s, img, n, K, T, d_ones);
+            if (hipGetLastError() != hipSuccess) return fail(MBRWT_ERR_DEVICE, "root mask kernel");
+        } else {
+            sr.kind = KIND_PLANE;
+            sr.stride = 16;
+            uint8_t *img = alloc_image(sr, ((n + 31) / 32) * sr.stride);
+            if (!img) return fail(MBRWT_ERR_NOMEM, "device allocation failed");
+            hipLaunchKernelGGL(k_gen_root_plane, dim3(launch_grid((n + 31) / 32)), dim3(256), 0, s, img, n, K, T,
+                               sr.stride);
+            if (hipGetLastError() != hipSuccess) return fail(MBRWT_ERR_DEVICE, "root plane kernel");
+            std::vector<uint64_t> tot;
+            if ((rc = plane_scan(img, n, 1, sr.stride, tot, s))) return fail(rc, "root scan");
+            // tot[0] = popcount of the root column = length of the root's children columns
+            tree.nodes[1].length = tot[0];
+        }
+    }
+    // internal nodes in BFS order: parents are generated before children
+    for (uint32_t u = 0; u < N; ++u) {
+        const auto &sh = shape[u];
+        DevNode &dn = tree.nodes[u + 1];
+        if (sh.children.empty()) continue;
+        const uint64_t L = dn.length;  // positions = popcount of u's own column
+        const uint64_t K = node_key(desc.seed, u);
+        const uint32_t a = dn.arity, nT = (1u << a) - 1;
+        if (dn.kind == KIND_PLANE) {
+            uint8_t *img = alloc_image(dn, ((L + 31) / 32) * dn.stride);
+            if (!img) return fail(MBRWT_ERR_NOMEM, "device allocation failed");
+            plane_fn(a)(img, L, K, node_T[u], nT, dn.stride, s);
+            if (hipGetLastError() != hipSuccess) return fail(MBRWT_ERR_DEVICE, "plane kernel");
+            std::vector<uint64_t> tot;
+            if ((rc = plane_scan(img, L, a, dn.stride, tot, s))) return fail(rc, "plane scan");
+            for (uint32_t c = 0; c < a; ++c) {
+                DevNode &ch = tree.nodes[sh.children[c] + 1];
+                if (ch.kind == KIND_LEAF) tree.num_relations += tot[c];
+                else ch.length = tot[c];
+            }
+        } else {
+            uint8_t *img = alloc_image(dn, L * mask_bytes(dn.kind));
+            if (!img) return fail(MBRWT_ERR_NOMEM, "device allocation failed");
+            mask_fn(a)(img, L, K, node_T[u], nT, d_ones, s);
+            if (hipGetLastError() != hipSuccess) return fail(MBRWT_ERR_DEVICE, "mask kernel");
+        }
+    }
+    unsigned long long ones = 0;
+    if (hipMemcpyAsync(&ones, d_ones, sizeof(ones), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return fail(MBRWT_ERR_DEVICE, "synthetic finish");
+    tree.num_relations += ones;
+    cleanup();
+    (void)hipFree(d_ones);
+    return finalize_tree(tree);
+}
+
+}  // namespace mbrwt

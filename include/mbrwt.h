@@ -1,0 +1,162 @@
+/*
+ * mbrwt.h -- C ABI of the MI355X-native Multi-BRWT row-query engine
+ * (genome_graph_annotation_amd/libmbrwt.so).
+ *
+ * Drop-in boundary for the reference's BRWT query path
+ * (ratschlab/genome_graph_annotation; paths below are relative to its root):
+ *
+ *   reference                                        replaced by
+ *   -----------------------------------------------  -----------------------------------
+ *   BinaryMatrix::get_row        common/binary_matrix.hpp:21      mbrwt_get_rows / _device (batched)
+ *   BRWT::get_row                annotation/hierarchical_annotation/BRWT.cpp:26-53
+ *   BRWT::get                    BRWT.cpp:9-24                     mbrwt_get_batch / _device
+ *   bit_vector_rrr<63>::rank1    common/bit_vector.cpp:857-861     (inside the traversal kernel)
+ *   bit_vector_rrr<63>::operator[]  common/bit_vector.cpp:884-888  (inside the traversal kernel)
+ *   utils::RangePartition::get   common/utils.cpp:689-691          (leaf column table, composed)
+ *   BRWT::num_rows/num_columns   BRWT.hpp:33-34                    mbrwt_num_rows / mbrwt_num_columns
+ *   BRWT::num_relations          BRWT.cpp:130-140                  mbrwt_num_relations
+ *   BRWT::load (structure ingestion) BRWT.cpp:87-111               mbrwt_create (from a tree description)
+ *   StaticBinRelAnnotator::count_labels annotation/annotate_static.cpp:149-162
+ *                                                                  mbrwt_count_labels_device
+ *
+ * Conventions: plain pointers and sizes only; no C++ or torch types.  Every
+ * function returns an MBRWT_* status code; nothing throws across the ABI.
+ * Rows are uint64 (binary_matrix.hpp:11) and must be < mbrwt_num_rows().
+ * Columns are emitted as uint32 (the reference stores them as uint32,
+ * utils.hpp:442-444).  Output order per row is the reference's order: the
+ * pre-order (DFS) of the BRWT's leaves (BRWT.cpp:45-51).
+ *
+ * Threading: a context may be used from several host threads; calls on one
+ * context are serialised internally (the reference's get_row is const and
+ * called concurrently from a ThreadPool, main.cpp:462-497).
+ */
+#ifndef MBRWT_H
+#define MBRWT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define MBRWT_OK 0
+#define MBRWT_ERR_INVALID 1     /* bad argument or malformed tree description */
+#define MBRWT_ERR_RANGE 2       /* row or column out of range (reference: assert, BRWT.cpp:27) */
+#define MBRWT_ERR_CAPACITY 3    /* cols_cap too small; *cols_needed holds the size needed */
+#define MBRWT_ERR_UNSUPPORTED 4 /* tree beyond this build's limits */
+#define MBRWT_ERR_DEVICE 5      /* HIP runtime error (see mbrwt_last_error_message) */
+#define MBRWT_ERR_NOMEM 6       /* device or host allocation failed */
+
+typedef struct mbrwt_ctx mbrwt_ctx;
+
+/* ---- structure ingestion ---------------------------------------------- */
+/*
+ * A BRWT in breadth-first numbering: node 0 is the root; the children of node
+ * u are nodes [first_child[u], first_child[u] + num_children[u]) in the
+ * reference's child order (BRWT.hpp:60).  vec_words[u] points to node u's
+ * index column (BRWT.hpp:59 nonzero_rows_) as ceil(vec_size[u]/64) LSB-first
+ * uint64 words.  For a leaf, leaf_column[u] is the global column id obtained by
+ * composing RangePartition::get along the path (utils.cpp:689-691); internal
+ * nodes carry UINT32_MAX.  num_nodes == 0 describes the empty BRWT().
+ * Replaces BRWT::load (BRWT.cpp:87-111) as the way structure enters the engine.
+ */
+typedef struct mbrwt_tree_desc {
+    uint64_t num_rows;
+    uint64_t num_columns;
+    uint32_t num_nodes;
+    const uint32_t *num_children;
+    const uint32_t *first_child;
+    const uint32_t *leaf_column;
+    const uint64_t *vec_size;
+    const uint64_t *const *vec_words;
+} mbrwt_tree_desc;
+
+/* Build the device image of a BRWT on HIP device `device`. */
+int mbrwt_create(const mbrwt_tree_desc *desc, int device, mbrwt_ctx **out);
+
+/*
+ * Generate a synthetic Multi-BRWT directly in device memory: the law of a
+ * basic-partitioner (BRWT_builders.cpp:20-31) BRWT built from i.i.d.
+ * Bernoulli(density) columns (experiments/data_generation.cpp:20-29), drawn
+ * top-down from a counter-based hash (spec: DESIGN.md "Synthetic matrices").
+ * arity in [2, 12]; num_rows < 2^32.
+ */
+typedef struct mbrwt_synth_desc {
+    uint64_t num_rows;
+    uint64_t num_columns;
+    double density;
+    uint32_t arity;
+    uint64_t seed;
+} mbrwt_synth_desc;
+int mbrwt_create_synthetic(const mbrwt_synth_desc *desc, int device, mbrwt_ctx **out);
+
+void mbrwt_destroy(mbrwt_ctx *ctx);
+
+/* ---- properties (BRWT.hpp:33-51) -------------------------------------- */
+uint64_t mbrwt_num_rows(const mbrwt_ctx *ctx);
+uint64_t mbrwt_num_columns(const mbrwt_ctx *ctx);
+uint64_t mbrwt_num_relations(const mbrwt_ctx *ctx);
+uint64_t mbrwt_num_nodes(const mbrwt_ctx *ctx);
+uint64_t mbrwt_device_bytes(const mbrwt_ctx *ctx); /* HBM held by the structure image */
+int mbrwt_device(const mbrwt_ctx *ctx);
+
+/* ---- queries ----------------------------------------------------------- */
+/*
+ * Batched BRWT::get_row over rows[0..n): CSR result with offsets[0..n]
+ * (n+1 entries, offsets[0] = 0) and cols[offsets[i]..offsets[i+1]) = row i's
+ * column ids in the reference's order.  If the total exceeds cols_cap,
+ * returns MBRWT_ERR_CAPACITY with *cols_needed set and cols untouched (retry
+ * protocol).  cols_needed may be NULL.  Host buffers.
+ */
+int mbrwt_get_rows(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n, uint64_t *offsets, uint32_t *cols,
+                   uint64_t cols_cap, uint64_t *cols_needed);
+
+/*
+ * Same on device buffers (d_rows: n uint64; d_offsets: n+1 uint64; d_cols:
+ * cols_cap uint32), enqueued on HIP stream `stream` (hipStream_t, NULL =
+ * default stream).  The call synchronises `stream` once to learn the output
+ * size; the results are complete when `stream` is next synchronised.
+ */
+int mbrwt_get_rows_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets,
+                          uint32_t *d_cols, uint64_t cols_cap, uint64_t *cols_needed, void *stream);
+
+/* Batched BRWT::get (BRWT.cpp:9-24): out[i] = bit (rows[i], cols[i]). Host buffers. */
+int mbrwt_get_batch(mbrwt_ctx *ctx, const uint64_t *rows, const uint64_t *cols, uint64_t n, uint8_t *out);
+int mbrwt_get_batch_device(mbrwt_ctx *ctx, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n,
+                           uint8_t *d_out, void *stream);
+
+/*
+ * StaticBinRelAnnotator::count_labels (annotate_static.cpp:149-162) fused on
+ * the device: counts[c] (num_columns uint64, zeroed by the call) = number of
+ * rows among d_rows[0..n) that carry column c.  Device buffers.
+ */
+int mbrwt_count_labels_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts,
+                              void *stream);
+
+/* ---- measurement ------------------------------------------------------- */
+/*
+ * Roofline accounting (DESIGN.md "Measurement"): over rows[0..n) (device
+ * buffer) return sum V(row) (index-bit probes the reference recursion makes,
+ * BRWT.cpp:30) and sum L(row) (labels returned).  Untimed diagnostic pass.
+ */
+int mbrwt_count_work_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, uint64_t *sum_visits,
+                            uint64_t *sum_labels, void *stream);
+
+/* Options (mbrwt_set_option). */
+#define MBRWT_OPT_TIMING 1       /* 1: time the traversal kernel with HIP events */
+#define MBRWT_OPT_SLOT_LABELS 2  /* per-row label slots of the fast path (0 = auto) */
+#define MBRWT_OPT_SORT_ROWS 3    /* 1: process the batch in row order (radix sort) */
+int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value);
+
+/* Traversal-kernel time accumulated while MBRWT_OPT_TIMING is on (ms, launches); resets the sums. */
+int mbrwt_take_timing(mbrwt_ctx *ctx, double *kernel_ms, uint64_t *launches);
+
+const char *mbrwt_strerror(int status);
+const char *mbrwt_last_error_message(void); /* thread-local detail of the last failure */
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MBRWT_H */

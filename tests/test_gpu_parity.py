@@ -1,0 +1,211 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle.
+
+Every comparison is bit-exact on the ordered CSR (ints/indices, no
+tolerance).  The cases mirror the reference's own tests:
+  tests/test_BRWT.cpp:152-212        all grids 1..19 x 1..19: all-zero, all-one, mixed
+  tests/test_BRWT_optimizer.cpp:102-163  the same after BRWTOptimizer::relax
+  experiments/run_benchmarks.py:47   C1 densities (1M x 500, arity 2)
+  BASELINE.json configs[1..3]        C2 exact, C3/C4 shapes via the top-down generator
+"""
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU")]
+
+
+def _dev(tree):
+    from genome_graph_annotation_amd import BRWTDevice
+    return BRWTDevice.from_tree(tree.export())
+
+
+def _check_rows(oracle_tree, dev, rows):
+    off_o, cols_o = oracle_tree.get_rows(rows)
+    off_d, cols_d = dev.get_rows(rows)
+    np.testing.assert_array_equal(off_d, off_o)
+    np.testing.assert_array_equal(cols_d, cols_o)
+    return off_o, cols_o
+
+
+def _grid(kind, n, m):
+    if kind == "zero":
+        return np.zeros((n, m), dtype=bool)
+    if kind == "one":
+        return np.ones((n, m), dtype=bool)
+    i = np.arange(n)[:, None]
+    j = np.arange(m)[None, :]
+    return ((i + 2 * j) % 2).astype(bool)  # test_BRWT.cpp:200
+
+
+@pytest.mark.parametrize("kind", ["zero", "one", "mixed"])
+@pytest.mark.parametrize("build", [("basic", 2, 0), ("basic", 2, 2**64 - 1), ("greedy", 2, 0)])
+def test_reference_grids(oracle_mod, kind, build):
+    O = oracle_mod
+    part, arity, relax = build
+    for n in range(1, 20):
+        for m in range(1, 20):
+            dense = _grid(kind, n, m)
+            t = O.OracleTree.from_dense(dense, part, arity, relax)
+            d = _dev(t)
+            assert d.num_rows() == n and d.num_columns() == m
+            assert d.num_relations() == int(dense.sum())
+            off, cols = _check_rows(t, d, np.arange(n, dtype=np.uint64))
+            for i in range(n):  # the reference test compares as sets (test_BRWT.cpp:125-141)
+                assert sorted(cols[off[i]:off[i + 1]].tolist()) == np.nonzero(dense[i])[0].tolist()
+            ii, jj = np.meshgrid(np.arange(n), np.arange(m), indexing="ij")
+            got = d.get_batch(ii.ravel(), jj.ravel())
+            np.testing.assert_array_equal(got, dense.ravel())
+
+
+@pytest.mark.parametrize("n,m,d,part,arity,relax", [
+    (5000, 40, 0.1, "basic", 2, 0),
+    (5000, 40, 0.1, "basic", 3, 0),
+    (5000, 40, 0.1, "greedy", 2, 0),
+    (5000, 40, 0.1, "greedy", 2, 4),
+    (3000, 100, 0.05, "basic", 8, 0),
+    (3000, 100, 0.05, "basic", 2, 2**64 - 1),
+    (2000, 70, 0.3, "basic", 33, 0),   # MASK64 leaf parents, 64-bit masks
+    (2000, 64, 0.02, "basic", 64, 0),
+    (2000, 200, 0.02, "basic", 16, 0),
+    (1000, 7, 1.0, "basic", 2, 0),     # dense rows
+    (1000, 7, 0.0, "basic", 2, 0),     # empty matrix rows
+])
+def test_random_matrices(oracle_mod, n, m, d, part, arity, relax):
+    O = oracle_mod
+    rng = np.random.default_rng(n * 7 + m)
+    dense = rng.random((n, m)) < d
+    t = O.OracleTree.from_dense(dense, part, arity, relax)
+    dev = _dev(t)
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 5000)]).astype(np.uint64)
+    off, cols = _check_rows(t, dev, rows)
+    for k in range(0, len(rows), 97):
+        assert sorted(cols[off[k]:off[k + 1]].tolist()) == np.nonzero(dense[rows[k]])[0].tolist()
+
+
+def test_single_column_and_empty(oracle_mod):
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice, MBRWTError
+    dense = np.array([[1], [0], [1], [1]], dtype=bool)
+    t = O.OracleTree.from_dense(dense)
+    d = _dev(t)
+    _check_rows(t, d, np.arange(4, dtype=np.uint64))
+    # empty BRWT (test_BRWT.cpp:15-25): no rows, any query is out of range
+    e = BRWTDevice.from_tree(O.OracleTree.from_dense(np.zeros((0, 0), dtype=bool)).export())
+    assert e.num_rows() == 0 and e.num_columns() == 0
+    with pytest.raises(MBRWTError):
+        e.get_rows(np.array([0], dtype=np.uint64))
+
+
+def test_errors_and_capacity(oracle_mod):
+    O = oracle_mod
+    import ctypes as C
+    from genome_graph_annotation_amd import MBRWTError, _lib as L
+    rng = np.random.default_rng(3)
+    dense = rng.random((100, 20)) < 0.5
+    t = O.OracleTree.from_dense(dense, "basic", 4)
+    d = _dev(t)
+    with pytest.raises(MBRWTError) as ei:
+        d.get_rows(np.array([0, 100], dtype=np.uint64))
+    assert ei.value.status == L.MBRWT_ERR_RANGE
+    with pytest.raises(MBRWTError):
+        d.get_batch([0], [20])
+    # capacity retry protocol
+    rows = np.arange(100, dtype=np.uint64)
+    off = np.zeros(101, dtype=np.uint64)
+    cols = np.zeros(5, dtype=np.uint32)
+    need = C.c_uint64(0)
+    st = L.lib().mbrwt_get_rows(d._h, rows.ctypes.data_as(L.u64p), 100, off.ctypes.data_as(L.u64p),
+                                cols.ctypes.data_as(L.u32p), 5, C.byref(need))
+    assert st == L.MBRWT_ERR_CAPACITY and need.value == int(dense.sum())
+    # empty batch
+    o2, c2 = d.get_rows(np.zeros(0, dtype=np.uint64))
+    assert o2.tolist() == [0] and len(c2) == 0
+
+
+def test_overflow_rows_take_direct_path(oracle_mod):
+    """Rows with more labels than the fast path's slot take pass 2."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import _lib as L
+    rng = np.random.default_rng(5)
+    dense = rng.random((3000, 300)) < 0.2  # ~60 labels per row
+    t = O.OracleTree.from_dense(dense, "basic", 8)
+    d = _dev(t)
+    for k in (16, 32, 64, 1024):
+        d.set_option(L.MBRWT_OPT_SLOT_LABELS, k)
+        _check_rows(t, d, rng.integers(0, 3000, 20000).astype(np.uint64))
+
+
+@pytest.mark.parametrize("density", [0.0, 0.0058333, 0.01])
+def test_c1_norepl_arity2(oracle_mod, density):
+    """BASELINE configs[0] (C1): 1M x 500 norepl, arity 2, mt19937 seed 42;
+    queries = generate_random_ints(1000, 0, n) seed 42 (experiments/main.cpp:78-93)
+    plus a 200k-row random batch."""
+    O = oracle_mod
+    n, m = 1_000_000, 500
+    t = O.OracleTree.norepl(n, m, density, 42, "basic", 2)
+    d = _dev(t)
+    _check_rows(t, d, O.generate_random_ints(1000, 0, n, 42))
+    _check_rows(t, d, np.random.default_rng(42).integers(0, n, 200_000).astype(np.uint64))
+
+
+def test_c2_kingsford_small_exact(oracle_mod):
+    """BASELINE configs[1] (C2): 1M x 2,652, d=0.3%, arity 8, batch 1M --
+    the reference's own generator (column-major mt19937, seed 42) and
+    bottom-up builder; every row of the batch compared bit-exactly."""
+    O = oracle_mod
+    n, m = 1_000_000, 2652
+    t = O.OracleTree.norepl(n, m, 0.003, 42, "basic", 8)
+    d = _dev(t)
+    rows = np.random.default_rng(42).integers(0, n, 1_000_000).astype(np.uint64)
+    _check_rows(t, d, rows)
+
+
+@pytest.mark.parametrize("n,m,dens,arity", [
+    (2_000_000, 2652, 0.003, 8),   # Kingsford shape, reduced rows
+    (300_000, 3173, 0.038, 8),     # RefSeq shape, reduced rows
+    (100_000, 1, 0.3, 2),          # root is a leaf
+    (100_000, 2, 0.5, 2),
+    (200_000, 500, 0.01, 2),
+    (200_000, 1000, 0.02, 3),
+    (100_000, 700, 0.05, 12),      # MASK16 leaf parents
+])
+def test_synthetic_matches_oracle(oracle_mod, n, m, dens, arity):
+    """The device generator and the oracle's independent implementation of
+    the same spec produce the same BRWT (same answers on every sampled row)."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    t = O.OracleTree.topdown(n, m, dens, arity, 42)
+    d = BRWTDevice.synthetic(n, m, dens, arity, 42)
+    assert d.num_relations() == t.num_relations()
+    assert d.num_rows() == n and d.num_columns() == m
+    rows = np.random.default_rng(1).integers(0, n, 300_000).astype(np.uint64)
+    _check_rows(t, d, rows)
+
+
+def test_device_api_and_accounting(oracle_mod):
+    import torch
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    n, m = 500_000, 2652
+    t = O.OracleTree.topdown(n, m, 0.003, 8, 7)
+    d = BRWTDevice.synthetic(n, m, 0.003, 8, 7)
+    rows = np.random.default_rng(2).integers(0, n, 100_000).astype(np.uint64)
+    off_o, cols_o, vis = t.get_rows(rows, with_visits=True)
+    rt = torch.from_numpy(rows.view(np.int64)).cuda()
+    ot = torch.empty(len(rows) + 1, dtype=torch.int64, device="cuda")
+    ct = torch.empty(len(cols_o) + 10, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    got = d.get_rows_device(rt, ot, ct, s.cuda_stream)
+    torch.cuda.synchronize()
+    assert got == len(cols_o)
+    np.testing.assert_array_equal(ot.cpu().numpy().view(np.uint64), off_o)
+    np.testing.assert_array_equal(ct[:got].cpu().numpy().view(np.uint32), cols_o)
+    # V and L accounting used by the roofline (DESIGN.md "Measurement")
+    v, lab = d.count_work_device(rt, s.cuda_stream)
+    assert v == int(vis.sum()) and lab == len(cols_o)
+    # fused count_labels (annotate_static.cpp:149-162)
+    cnt = torch.empty(m, dtype=torch.int64, device="cuda")
+    d.count_labels_device(rt, cnt, s.cuda_stream)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(cnt.cpu().numpy(), np.bincount(cols_o, minlength=m))
