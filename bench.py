@@ -54,6 +54,10 @@ def parse():
     return ap.parse_args()
 
 
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -72,6 +76,7 @@ def main():
     t0 = time.time()
     mat = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, device=local)
     setup_s = time.time() - t0
+    log(f"device structure built in {setup_s:.1f} s ({mat.device_bytes() / 1e9:.1f} GB)")
     if a.sort_rows >= 0:
         mat.set_option(L.MBRWT_OPT_SORT_ROWS, a.sort_rows)
 
@@ -111,6 +116,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    log(f"timed {a.steps} steps: {elapsed / a.steps * 1e3:.3f} ms/step")
     mat.set_option(L.MBRWT_OPT_TIMING, 0)
     kern_ms_total, launches = mat.take_timing()
     if world > 1:
@@ -138,9 +144,11 @@ def main():
 
         threads = a.cpu_threads or len(os.sched_getaffinity(0))
         threads = min(threads, 16)
+        log(f"building the host oracle structure on {threads} threads")
         g0 = time.time()
         ref = O.OracleTree.topdown(a.rows, a.cols, a.density, a.arity, a.seed, threads)
         gen_s = time.time() - g0
+        log(f"host structure built in {gen_s:.1f} s; checking {chk} rows and timing {a.cpu_sample} rows")
         off_o, cols_o = ref.get_rows(rows_np[:chk], threads)
         parity = bool(np.array_equal(off_o, off_h) and np.array_equal(cols_o, cols_h))
         sample = rows_np[: a.cpu_sample]
