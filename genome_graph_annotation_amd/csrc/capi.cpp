@@ -268,6 +268,10 @@ int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value) {
     case MBRWT_OPT_SORT_ROWS:
         c.sort_rows = value != 0;
         return MBRWT_OK;
+    case MBRWT_OPT_KERNEL:
+        if (value < 0 || value > 4) return MBRWT_ERR_INVALID;
+        c.kernel_variant = (int)value;
+        return MBRWT_OK;
     default:
         set_error("unknown option");
         return MBRWT_ERR_INVALID;

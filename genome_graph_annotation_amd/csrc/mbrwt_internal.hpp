@@ -103,6 +103,7 @@ struct Ctx {
     bool timing = false;
     uint32_t slot_labels = 0;           // 0 = auto
     bool sort_rows = false;
+    int kernel_variant = 0;             // 0 group-per-row (default), 1 lane-per-row
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double timing_ms = 0;
     uint64_t timing_launches = 0;

@@ -240,6 +240,274 @@ __global__ __launch_bounds__(256) void k_traverse(TravParams p) {
     }
 }
 
+// ------------------------------------------------------------------------
+// k_traverse_group: G lanes cooperate on one row (G = pow2ceil(max arity)).
+// Visiting node u at position j, lane c of the group reads child c's
+// {rank, bits} pair: the G 8-byte reads of one block are adjacent, so the
+// memory pipeline sees ONE coalesced request per visit instead of one per
+// lane-load (random requests, not bytes, bound this path: tools/
+// gather_probe.hip).  Each stack level holds, per lane, the child index j_c
+// of child c and, uniform in the group, the parent's first child and the
+// mask of children still to visit.  Children are taken in order (DFS, the
+// reference's output order); the index of the next child comes from lane
+// c's register through a cross-lane shuffle.
+// ------------------------------------------------------------------------
+template <int MAXD, int CPL>
+struct GroupFrames {
+    uint32_t jc[MAXD][CPL];  // per lane: position of child c*CPL+k in its own image
+    uint32_t fc[MAXD];       // uniform: dnode of child 0
+    uint64_t pend[MAXD];     // uniform: children still to take (bit i = child i)
+    int sp;
+    __device__ __forceinline__ void push(const uint32_t (&j)[CPL], uint32_t f, uint64_t p) {
+#pragma unroll
+        for (int k = MAXD - 1; k > 0; --k) {
+#pragma unroll
+            for (int q = 0; q < CPL; ++q) jc[k][q] = jc[k - 1][q];
+            fc[k] = fc[k - 1];
+            pend[k] = pend[k - 1];
+        }
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) jc[0][q] = j[q];
+        fc[0] = f;
+        pend[0] = p;
+        ++sp;
+    }
+    __device__ __forceinline__ void pop() {
+#pragma unroll
+        for (int k = 0; k < MAXD - 1; ++k) {
+#pragma unroll
+            for (int q = 0; q < CPL; ++q) jc[k][q] = jc[k + 1][q];
+            fc[k] = fc[k + 1];
+            pend[k] = pend[k + 1];
+        }
+        --sp;
+    }
+};
+
+// Per-group label sink: the labels of the current row are staged in LDS
+// (kStageLabels per group) and written out once, contiguously, when the row
+// ends.  Stores count in vmcnt on CDNA4, so a store issued inside the
+// descent would hold up the wait of the next dependent block load; staging
+// keeps the descent free of global stores.  Labels past the stage go
+// straight to global memory (rare: rows with > kStageLabels labels).
+constexpr uint32_t kStageLabels = 32;
+
+template <int MODE>
+struct GroupSink {
+    uint32_t cnt;        // labels emitted so far (uniform)
+    uint64_t slot_base;  // MODE_SLOTS: bi*K ; MODE_DIRECT: offsets[bi]
+    uint64_t visits;
+    uint32_t *stage;     // this group's LDS stage
+    // lane-parallel emission: `label` goes to position cnt + rank
+    __device__ __forceinline__ void put(const TravParams &p, uint32_t rank, uint32_t label) {
+        const uint32_t pos = cnt + rank;
+        if constexpr (MODE == MODE_SLOTS || MODE == MODE_DIRECT) {
+            if (pos < kStageLabels) {
+                stage[pos] = label;
+                return;
+            }
+        }
+        if constexpr (MODE == MODE_SLOTS) {
+            if (pos < p.K) p.temp[slot_base + pos] = label;
+        } else if constexpr (MODE == MODE_DIRECT) {
+            p.cols[slot_base + pos] = label;
+        } else if constexpr (MODE == MODE_COUNT) {
+            atomicAdd(&p.label_counts[label], 1ull);
+        }
+    }
+    // end of row: the group's lanes copy the stage out, contiguously
+    __device__ __forceinline__ void flush(const TravParams &p, uint32_t c, uint32_t G) {
+        if constexpr (MODE == MODE_SLOTS || MODE == MODE_DIRECT) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint32_t lim = cnt < kStageLabels ? cnt : kStageLabels;
+            if constexpr (MODE == MODE_SLOTS) lim = lim < p.K ? lim : p.K;
+            for (uint32_t pos = c; pos < lim; pos += G) {
+                if constexpr (MODE == MODE_SLOTS) p.temp[slot_base + pos] = stage[pos];
+                else p.cols[slot_base + pos] = stage[pos];
+            }
+        }
+    }
+};
+
+// spread the low G bits of x to every CPL-th bit position
+template <int CPL>
+__device__ __forceinline__ uint64_t spread_bits(uint64_t x, uint32_t G) {
+    if constexpr (CPL == 1) return x;
+    uint64_t r = 0;
+    for (uint32_t i = 0; i < G; ++i) r |= ((x >> i) & 1ull) << (i * CPL);
+    return r;
+}
+
+template <int MAXD, int CPL, int MODE>
+__device__ __forceinline__ void group_visit(const TravParams &p, GroupFrames<MAXD, CPL> &st, GroupSink<MODE> &sk,
+                                            const DevNode &nd, uint32_t j, uint32_t c, uint32_t gbase,
+                                            uint64_t gmask, uint32_t G) {
+    const uint32_t a = nd.arity;
+    const uint8_t *base = reinterpret_cast<const uint8_t *>(nd.base);
+    if constexpr (MODE == MODE_WORK) sk.visits += a;  // operator[] on every child (BRWT.cpp:30)
+    if (nd.kind == KIND_PLANE) {
+        const uint32_t t = j & 31;
+        const uint32_t below = (1u << t) - 1u;
+        uint32_t bit[CPL], jc[CPL];
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) {
+            bit[q] = 0;
+            jc[q] = 0;
+        }
+        if (c * CPL < a) {
+            const uint8_t *blk = base + (uint64_t)(j >> 5) * nd.stride + 8u * CPL * c;
+            uint32_t rk[CPL], bw[CPL];
+            if constexpr (CPL == 1) {
+                const uint2 rb = *reinterpret_cast<const uint2 *>(blk);
+                rk[0] = rb.x;
+                bw[0] = rb.y;
+            } else {
+#pragma unroll
+                for (int h = 0; h < CPL / 2; ++h) {
+                    const uint4 q4 = *reinterpret_cast<const uint4 *>(blk + 16 * h);
+                    rk[2 * h] = q4.x;
+                    bw[2 * h] = q4.y;
+                    rk[2 * h + 1] = q4.z;
+                    bw[2 * h + 1] = q4.w;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < CPL; ++q) {
+                if (c * CPL + q < a) {
+                    bit[q] = (bw[q] >> t) & 1u;
+                    jc[q] = rk[q] + (uint32_t)__builtin_popcount(bw[q] & below);  // rank1(j) - 1
+                }
+            }
+        }
+        uint64_t P = 0;
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) P |= spread_bits<CPL>((__ballot(bit[q]) >> gbase) & gmask, G) << q;
+        if (P) {
+            if (st.sp >= MAXD) {
+                if (c == 0) atomicOr(&p.scalars[2], 2ull);
+                return;
+            }
+            st.push(jc, nd.first_child, P);
+        }
+        return;
+    }
+    uint64_t m;  // all children are leaves: one mask per position (uniform load)
+    if (nd.kind == KIND_MASK8) m = base[j];
+    else if (nd.kind == KIND_MASK16) m = reinterpret_cast<const uint16_t *>(base)[j];
+    else if (nd.kind == KIND_MASK32) m = reinterpret_cast<const uint32_t *>(base)[j];
+    else m = reinterpret_cast<const uint64_t *>(base)[j];
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+        const uint32_t cc = c * CPL + q;
+        if (cc < a && ((m >> cc) & 1u)) {
+            const uint32_t label =
+                (nd.flags & FLAG_CONSEC_LABELS) ? nd.label + cc : p.nodes[nd.first_child + cc].label;
+            sk.put(p, (uint32_t)__builtin_popcountll(m & ((1ull << cc) - 1ull)), label);
+        }
+    }
+    sk.cnt += (uint32_t)__builtin_popcountll(m);
+}
+
+template <int MAXD, int CPL, int MODE>
+__global__ __launch_bounds__(256) void k_traverse_group(TravParams p, uint32_t G) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t c = lane & (G - 1);
+    const uint32_t gbase = lane & ~(G - 1);
+    const uint64_t gmask = G >= 64 ? ~0ull : ((1ull << G) - 1ull);
+    const uint64_t groups_per_block = blockDim.x / G;
+    const uint64_t gstride = (uint64_t)gridDim.x * groups_per_block;
+    uint64_t s = (uint64_t)blockIdx.x * groups_per_block + threadIdx.x / G;
+
+    GroupFrames<MAXD, CPL> st;
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k) {
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) st.jc[k][q] = 0;
+        st.fc[k] = 0;
+        st.pend[k] = 0;
+    }
+    st.sp = 0;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_stage[];  // (256 / G) * kStageLabels
+    GroupSink<MODE> sk;
+    sk.cnt = 0;
+    sk.visits = 0;
+    sk.slot_base = 0;
+    sk.stage = lds_stage + (threadIdx.x / G) * kStageLabels;
+    uint64_t bi = 0;
+    unsigned long long acc_visits = 0, acc_labels = 0;
+
+    auto begin_row = [&]() {
+        bi = (MODE == MODE_DIRECT) ? (uint64_t)p.slot_list[s] : (p.order ? (uint64_t)p.order[s] : s);
+        const uint64_t row = p.rows[bi];
+        sk.cnt = 0;
+        sk.visits = 0;
+        if constexpr (MODE == MODE_SLOTS) sk.slot_base = bi * p.K;
+        if constexpr (MODE == MODE_DIRECT) sk.slot_base = p.offsets[bi];
+        if (row >= p.num_rows) {
+            if (c == 0) atomicOr(&p.scalars[2], 1ull);
+            return;
+        }
+        const DevNode nd = p.nodes[0];
+        group_visit<MAXD, CPL, MODE>(p, st, sk, nd, (uint32_t)row, c, gbase, gmask, G);
+    };
+    auto end_row = [&]() {
+        sk.flush(p, c, G);
+        if constexpr (MODE == MODE_SLOTS) {
+            if (c == 0) {
+                p.counts[bi] = sk.cnt;
+                if (sk.cnt > p.K) {
+                    const unsigned long long k = atomicAdd(&p.scalars[1], 1ull);
+                    p.ovf_list[k] = (uint32_t)bi;
+                }
+            }
+        }
+        if constexpr (MODE == MODE_WORK) {
+            if (c == 0) {
+                acc_visits += sk.visits;
+                acc_labels += sk.cnt;
+            }
+        }
+    };
+
+    bool active = s < p.n;
+    if (active) begin_row();
+    while (true) {
+        if (active && st.sp == 0) {
+            end_row();
+            s += gstride;
+            active = s < p.n;
+            if (active) begin_row();
+        }
+        if (!__any(active)) break;
+        if (active && st.sp > 0) {
+            uint64_t P = st.pend[0];
+            const uint32_t cs = (uint32_t)__builtin_ctzll(P);
+            P &= P - 1;
+            st.pend[0] = P;
+            const uint32_t w = st.fc[0] + cs;
+            uint32_t mine = st.jc[0][0];
+#pragma unroll
+            for (int q = 1; q < CPL; ++q)
+                if ((cs % CPL) == (uint32_t)q) mine = st.jc[0][q];
+            const uint32_t jw = (uint32_t)__shfl((int)mine, (int)(gbase + cs / CPL), 64);
+            if (P == 0) st.pop();  // no children left at this level: drop it before descending
+            const DevNode nd = p.nodes[w];
+            if (nd.kind == KIND_LEAF) {
+                if (c == 0) sk.put(p, 0, nd.label);
+                sk.cnt += 1;
+            } else {
+                group_visit<MAXD, CPL, MODE>(p, st, sk, nd, jw, c, gbase, gmask, G);
+            }
+        }
+    }
+    if constexpr (MODE == MODE_WORK) {
+        if (acc_visits) atomicAdd(&p.scalars[3], acc_visits);
+        if (acc_labels) atomicAdd(&p.scalars[4], acc_labels);
+    }
+}
+
 // CSR compaction of the label slots (rows with <= K labels).
 __global__ __launch_bounds__(256) void k_compact(const uint32_t *__restrict__ counts,
                                                  const uint64_t *__restrict__ offsets,
@@ -310,31 +578,76 @@ __global__ __launch_bounds__(256) void k_get(const DevNode *__restrict__ nodes, 
 namespace {
 
 using TravFn = void (*)(TravParams);
+using GroupFn = void (*)(TravParams, uint32_t);
+
+// A traversal launch: the lane-per-row kernel or the group kernel.
+struct Trav {
+    const void *fn = nullptr;
+    TravFn lane_fn = nullptr;
+    GroupFn group_fn = nullptr;
+    uint32_t G = 1;  // lanes per row
+    explicit operator bool() const { return fn != nullptr; }
+};
 
 template <int MODE>
-TravFn pick_traverse(uint32_t depth, uint32_t max_arity) {
-    const bool wide = max_arity > 32;
-#define PICK(D)                                                               \
-    if (depth <= D)                                                           \
-        return wide ? (TravFn)k_traverse<D, uint64_t, MODE> : (TravFn)k_traverse<D, uint32_t, MODE>;
-    PICK(4)
-    PICK(8)
-    PICK(16)
-    PICK(32)
+Trav pick_traverse(const Ctx &c) {
+    const uint32_t depth = c.tree.stack_depth, max_arity = c.tree.max_arity;
+    Trav t;
+    if (c.kernel_variant == 1) {  // lane-per-row kernel (kept for A/B measurement)
+        const bool wide = max_arity > 32;
+#define PICK(D)                                                                                      \
+    if (depth <= D) {                                                                                \
+        t.lane_fn = wide ? (TravFn)k_traverse<D, uint64_t, MODE> : (TravFn)k_traverse<D, uint32_t, MODE>; \
+        t.fn = reinterpret_cast<const void *>(t.lane_fn);                                            \
+        return t;                                                                                    \
+    }
+        PICK(4)
+        PICK(8)
+        PICK(16)
+        PICK(32)
 #undef PICK
-    return nullptr;
+        return t;
+    }
+    // group kernel: CPL children per lane, G = pow2ceil(ceil(max_arity / CPL)) lanes per row
+    const int cpl = c.kernel_variant == 2 ? 1 : c.kernel_variant == 4 ? 4 : 2;
+    const uint32_t need = (max_arity + cpl - 1) / cpl;
+    uint32_t G = 1;
+    while (G < need) G <<= 1;
+    t.G = G;
+#define PICKG(D, CPLV)                                                     \
+    if (depth <= D && cpl == CPLV) {                                       \
+        t.group_fn = (GroupFn)k_traverse_group<D, CPLV, MODE>;             \
+        t.fn = reinterpret_cast<const void *>(t.group_fn);                 \
+        return t;                                                          \
+    }
+#define PICKD(CPLV) PICKG(4, CPLV) PICKG(8, CPLV) PICKG(16, CPLV) PICKG(32, CPLV)
+    PICKD(1)
+    PICKD(2)
+    PICKD(4)
+#undef PICKD
+#undef PICKG
+    return t;
 }
 
-int grid_for(Ctx &c, TravFn fn, uint64_t n) {
+size_t lds_bytes(const Trav &t) { return t.group_fn ? (size_t)(256 / t.G) * kStageLabels * sizeof(uint32_t) : 0; }
+
+int grid_for(const Ctx &c, const Trav &t, uint64_t n) {
     int dev_cus = 0;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device);
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(fn), 256, 0) != hipSuccess ||
-        per_cu <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, t.fn, 256, lds_bytes(t)) != hipSuccess || per_cu <= 0)
         per_cu = 4;
-    uint64_t resident = (uint64_t)std::max(1, dev_cus) * (uint64_t)per_cu;
-    uint64_t need = (n + 255) / 256;
+    const uint64_t resident = (uint64_t)std::max(1, dev_cus) * (uint64_t)per_cu;
+    const uint64_t rows_per_block = 256 / t.G;
+    const uint64_t need = (n + rows_per_block - 1) / rows_per_block;
     return (int)std::max<uint64_t>(1, std::min(need, resident));
+}
+
+hipError_t launch(const Ctx &c, const Trav &t, uint64_t n, hipStream_t s, const TravParams &p) {
+    const int grid = grid_for(c, t, n);
+    if (t.group_fn) hipLaunchKernelGGL(t.group_fn, dim3(grid), dim3(256), lds_bytes(t), s, p, t.G);
+    else hipLaunchKernelGGL(t.lane_fn, dim3(grid), dim3(256), 0, s, p);
+    return hipGetLastError();
 }
 
 uint32_t auto_slots(const Ctx &c) {
@@ -383,8 +696,8 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
         return MBRWT_ERR_UNSUPPORTED;
     }
     const uint32_t K = auto_slots(c);
-    TravFn fn = pick_traverse<MODE_SLOTS>(c.tree.stack_depth, c.tree.max_arity);
-    TravFn fn_direct = pick_traverse<MODE_DIRECT>(c.tree.stack_depth, c.tree.max_arity);
+    const Trav fn = pick_traverse<MODE_SLOTS>(c);
+    const Trav fn_direct = pick_traverse<MODE_DIRECT>(c);
     if (!fn || !fn_direct) {
         set_error("tree deeper than 32 levels of internal nodes");
         return MBRWT_ERR_UNSUPPORTED;
@@ -409,10 +722,8 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
 
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
     MBRWT_HIP(hipMemsetAsync(p.counts + n, 0, sizeof(uint32_t), s));
-    const int grid = grid_for(c, fn, n);
     if (c.timing) MBRWT_HIP(hipEventRecord(c.ev0, s));
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, p);
-    MBRWT_HIP(hipGetLastError());
+    MBRWT_HIP(launch(c, fn, n, s, p));
     if (c.timing) MBRWT_HIP(hipEventRecord(c.ev1, s));
     MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_offsets, n + 1, s));
     MBRWT_HIP(hipMemcpyAsync(c.d_scalars, d_offsets + n, sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
@@ -449,25 +760,20 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
         q.slot_list = p.ovf_list;
         q.offsets = d_offsets;
         q.cols = d_cols;
-        const int g2 = grid_for(c, fn_direct, ovf);
-        hipLaunchKernelGGL(fn_direct, dim3(g2), dim3(256), 0, s, q);
-        MBRWT_HIP(hipGetLastError());
+        MBRWT_HIP(launch(c, fn_direct, ovf, s, q));
     }
     return MBRWT_OK;
 }
 
 int run_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s) {
     if (c.tree.nodes.empty()) return n ? MBRWT_ERR_RANGE : MBRWT_OK;
-    TravFn fn = pick_traverse<MODE_WORK>(c.tree.stack_depth, c.tree.max_arity);
+    const Trav fn = pick_traverse<MODE_WORK>(c);
     if (!fn) return MBRWT_ERR_UNSUPPORTED;
     TravParams p = base_params(c);
     p.rows = d_rows;
     p.n = n;
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
-    if (n) {
-        hipLaunchKernelGGL(fn, dim3(grid_for(c, fn, n)), dim3(256), 0, s, p);
-        MBRWT_HIP(hipGetLastError());
-    }
+    if (n) MBRWT_HIP(launch(c, fn, n, s, p));
     MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     MBRWT_HIP(hipStreamSynchronize(s));
     if (c.h_scalars[2] & 1) return MBRWT_ERR_RANGE;
@@ -480,17 +786,14 @@ int run_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits,
 int run_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts, hipStream_t s) {
     if (c.tree.num_columns) MBRWT_HIP(hipMemsetAsync(d_counts, 0, c.tree.num_columns * sizeof(uint64_t), s));
     if (c.tree.nodes.empty()) return n ? MBRWT_ERR_RANGE : MBRWT_OK;
-    TravFn fn = pick_traverse<MODE_COUNT>(c.tree.stack_depth, c.tree.max_arity);
+    const Trav fn = pick_traverse<MODE_COUNT>(c);
     if (!fn) return MBRWT_ERR_UNSUPPORTED;
     TravParams p = base_params(c);
     p.rows = d_rows;
     p.n = n;
     p.label_counts = reinterpret_cast<unsigned long long *>(d_counts);
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
-    if (n) {
-        hipLaunchKernelGGL(fn, dim3(grid_for(c, fn, n)), dim3(256), 0, s, p);
-        MBRWT_HIP(hipGetLastError());
-    }
+    if (n) MBRWT_HIP(launch(c, fn, n, s, p));
     MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     MBRWT_HIP(hipStreamSynchronize(s));
     if (c.h_scalars[2] & 1) return MBRWT_ERR_RANGE;

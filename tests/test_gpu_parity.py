@@ -20,11 +20,18 @@ def _dev(tree):
     return BRWTDevice.from_tree(tree.export())
 
 
-def _check_rows(oracle_tree, dev, rows):
+def _check_rows(oracle_tree, dev, rows, variants=(0, 1, 2, 4)):
+    """Every traversal kernel (1 lane-per-row; 2/3/4 group-cooperative with
+    1/2/4 children per lane; 0 the default) must
+    reproduce the oracle's ordered CSR exactly."""
+    from genome_graph_annotation_amd import _lib as L
     off_o, cols_o = oracle_tree.get_rows(rows)
-    off_d, cols_d = dev.get_rows(rows)
-    np.testing.assert_array_equal(off_d, off_o)
-    np.testing.assert_array_equal(cols_d, cols_o)
+    for v in variants:
+        dev.set_option(L.MBRWT_OPT_KERNEL, v)
+        off_d, cols_d = dev.get_rows(rows)
+        np.testing.assert_array_equal(off_d, off_o)
+        np.testing.assert_array_equal(cols_d, cols_o)
+    dev.set_option(L.MBRWT_OPT_KERNEL, 0)
     return off_o, cols_o
 
 
@@ -201,11 +208,14 @@ def test_device_api_and_accounting(oracle_mod):
     assert got == len(cols_o)
     np.testing.assert_array_equal(ot.cpu().numpy().view(np.uint64), off_o)
     np.testing.assert_array_equal(ct[:got].cpu().numpy().view(np.uint32), cols_o)
-    # V and L accounting used by the roofline (DESIGN.md "Measurement")
-    v, lab = d.count_work_device(rt, s.cuda_stream)
-    assert v == int(vis.sum()) and lab == len(cols_o)
-    # fused count_labels (annotate_static.cpp:149-162)
-    cnt = torch.empty(m, dtype=torch.int64, device="cuda")
-    d.count_labels_device(rt, cnt, s.cuda_stream)
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(cnt.cpu().numpy(), np.bincount(cols_o, minlength=m))
+    from genome_graph_annotation_amd import _lib as L
+    for variant in (0, 1, 2, 4):
+        d.set_option(L.MBRWT_OPT_KERNEL, variant)
+        # V and L accounting used by the roofline (DESIGN.md "Measurement")
+        v, lab = d.count_work_device(rt, s.cuda_stream)
+        assert v == int(vis.sum()) and lab == len(cols_o)
+        # fused count_labels (annotate_static.cpp:149-162)
+        cnt = torch.empty(m, dtype=torch.int64, device="cuda")
+        d.count_labels_device(rt, cnt, s.cuda_stream)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(cnt.cpu().numpy(), np.bincount(cols_o, minlength=m))

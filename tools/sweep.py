@@ -1,0 +1,58 @@
+"""A/B sweep of traversal-kernel variants on one structure, in one process
+(interleaved repetitions, HIP-event kernel times).  Calibration tool, not the
+bench: python tools/sweep.py --rows 3700000000 --batch 8000000"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from genome_graph_annotation_amd import BRWTDevice, _lib as L  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--rows", type=int, default=3_700_000_000)
+ap.add_argument("--cols", type=int, default=2652)
+ap.add_argument("--density", type=float, default=0.003)
+ap.add_argument("--arity", type=int, default=8)
+ap.add_argument("--batch", type=int, default=8_000_000)
+ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--variants", default="1,2,3,4")
+ap.add_argument("--sort", default="0")
+a = ap.parse_args()
+t0 = time.time()
+m = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, 42)
+print(f"built {m.device_bytes() / 1e9:.1f} GB in {time.time() - t0:.1f}s", flush=True)
+rows = torch.from_numpy(np.random.default_rng(42).integers(0, a.rows, a.batch, dtype=np.uint64).view(np.int64)).cuda()
+off = torch.empty(a.batch + 1, dtype=torch.int64, device="cuda")
+s = torch.cuda.current_stream().cuda_stream
+v, lab = m.count_work_device(rows, s)
+cols = torch.empty(lab + 1024, dtype=torch.int32, device="cuda")
+alg = 64 * v + 16 * a.batch + 4 * lab
+variants = [int(x) for x in a.variants.split(",")]
+sorts = [int(x) for x in a.sort.split(",")]
+res = {}
+for rep in range(a.reps):
+    for var in variants:
+        for so in sorts:
+            m.set_option(L.MBRWT_OPT_KERNEL, var)
+            m.set_option(L.MBRWT_OPT_SORT_ROWS, so)
+            m.get_rows_device(rows, off, cols, s)
+            m.take_timing()
+            m.set_option(L.MBRWT_OPT_TIMING, 1)
+            torch.cuda.synchronize()
+            w0 = time.perf_counter()
+            for _ in range(3):
+                m.get_rows_device(rows, off, cols, s)
+            torch.cuda.synchronize()
+            wall = (time.perf_counter() - w0) / 3
+            m.set_option(L.MBRWT_OPT_TIMING, 0)
+            ms, k = m.take_timing()
+            res.setdefault((var, so), []).append((ms / k, wall * 1e3))
+for (var, so), xs in sorted(res.items()):
+    kms = np.median([x[0] for x in xs])
+    wms = np.median([x[1] for x in xs])
+    print(f"variant {var} sort {so}: kernel {kms:.3f} ms  step {wms:.3f} ms  -> {a.batch / wms * 1e3 / 1e6:.1f} M rows/s, "
+          f"alg {alg / kms / 1e6:.0f} GB/s")
