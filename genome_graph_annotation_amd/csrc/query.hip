@@ -27,6 +27,29 @@ namespace mbrwt {
 
 enum { MODE_SLOTS = 0, MODE_DIRECT = 1, MODE_WORK = 2, MODE_COUNT = 3 };
 
+// Explicit address spaces: image addresses are rebuilt from integers and
+// would otherwise compile to flat_* loads, which CDNA4 retires out of order
+// (every wait becomes vmcnt(0) & lgkmcnt(0)).  Every hot access below is a
+// global_* (address space 1) or ds_* (address space 3) instruction.
+#define AS_GLOBAL __attribute__((address_space(1)))
+#define AS_LDS __attribute__((address_space(3)))
+// (the host pass of the same source only needs the declarations to parse)
+#if defined(__HIP_DEVICE_COMPILE__)
+template <class T>
+__device__ __forceinline__ T gld(const T *p) { return *(const AS_GLOBAL T *)(uintptr_t)p; }
+template <class T>
+__device__ __forceinline__ T gld_at(uint64_t addr) { return *(const AS_GLOBAL T *)addr; }
+template <class T>
+__device__ __forceinline__ void gst(T *p, T v) { *(AS_GLOBAL T *)(uintptr_t)p = v; }
+#else
+template <class T>
+__device__ T gld(const T *p) { return *p; }
+template <class T>
+__device__ T gld_at(uint64_t addr) { return *(const T *)addr; }
+template <class T>
+__device__ void gst(T *p, T v) { *p = v; }
+#endif
+
 struct TravParams {
     const DevNode *nodes;
     const uint64_t *rows;
@@ -87,9 +110,9 @@ struct Sink {
     uint64_t visits;
     __device__ __forceinline__ void emit(const TravParams &p, uint32_t label) {
         if constexpr (MODE == MODE_SLOTS) {
-            if (cnt < p.K) p.temp[slot_base + cnt] = label;
+            if (cnt < p.K) gst(p.temp + slot_base + cnt, label);
         } else if constexpr (MODE == MODE_DIRECT) {
-            p.cols[slot_base + cnt] = label;
+            gst(p.cols + slot_base + cnt, label);
         } else if constexpr (MODE == MODE_COUNT) {
             atomicAdd(&p.label_counts[label], 1ull);
         }
@@ -107,17 +130,17 @@ __device__ __forceinline__ MaskT arity_mask(uint32_t a) {
 template <int MAXD, typename MaskT, int MODE>
 __device__ __forceinline__ void enter(const TravParams &p, Frames<MAXD, MaskT> &st, Sink<MODE> &sk, uint32_t v,
                                       uint32_t j) {
-    const DevNode *nd = p.nodes + v;
-    const uint8_t kind = nd->kind;
-    const uint32_t a = nd->arity;
-    const uint8_t *base = reinterpret_cast<const uint8_t *>(nd->base);
+    const DevNode nd = gld(p.nodes + v);
+    const uint8_t kind = nd.kind;
+    const uint32_t a = nd.arity;
+    const uint64_t base = nd.base;
     if constexpr (MODE == MODE_WORK) sk.visits += a;  // operator[] on every child (BRWT.cpp:30)
     if (kind == KIND_PLANE) {
-        const uint8_t *blk = base + (uint64_t)(j >> 5) * nd->stride;
+        const uint64_t blk = base + (uint64_t)(j >> 5) * nd.stride;
         const uint32_t t = j & 31;
         MaskT m = 0;
         for (uint32_t c = 0; c < a; c += 2) {
-            const uint4 q = *reinterpret_cast<const uint4 *>(blk + 8u * c);
+            const uint4 q = gld_at<uint4>(blk + 8u * c);
             m |= (MaskT)((q.y >> t) & 1u) << c;
             m |= (MaskT)((q.w >> t) & 1u) << (c + 1);
         }
@@ -133,20 +156,20 @@ __device__ __forceinline__ void enter(const TravParams &p, Frames<MAXD, MaskT> &
     }
     // all children are leaves: one mask per position
     uint64_t m;
-    if (kind == KIND_MASK8) m = base[j];
-    else if (kind == KIND_MASK16) m = reinterpret_cast<const uint16_t *>(base)[j];
-    else if (kind == KIND_MASK32) m = reinterpret_cast<const uint32_t *>(base)[j];
-    else m = reinterpret_cast<const uint64_t *>(base)[j];
-    if (nd->flags & FLAG_CONSEC_LABELS) {
-        const uint32_t l0 = nd->label;
+    if (kind == KIND_MASK8) m = gld_at<uint8_t>(base + j);
+    else if (kind == KIND_MASK16) m = gld_at<uint16_t>(base + 2ull * j);
+    else if (kind == KIND_MASK32) m = gld_at<uint32_t>(base + 4ull * j);
+    else m = gld_at<uint64_t>(base + 8ull * j);
+    if (nd.flags & FLAG_CONSEC_LABELS) {
+        const uint32_t l0 = nd.label;
         while (m) {
             sk.emit(p, l0 + (uint32_t)__builtin_ctzll(m));
             m &= m - 1;
         }
     } else {
-        const uint32_t fc = nd->first_child;
+        const uint32_t fc = nd.first_child;
         while (m) {
-            sk.emit(p, p.nodes[fc + __builtin_ctzll(m)].label);
+            sk.emit(p, gld(p.nodes + fc + __builtin_ctzll(m)).label);
             m &= m - 1;
         }
     }
@@ -161,16 +184,16 @@ __device__ __forceinline__ void step(const TravParams &p, Frames<MAXD, MaskT> &s
     const int c = ctz_m(m);
     m &= m - 1;
     st.rem[0] = m;
-    const DevNode *nu = p.nodes + u;
-    const uint32_t v = nu->first_child + (uint32_t)c;
-    const uint8_t *blk = reinterpret_cast<const uint8_t *>(nu->base) + (uint64_t)(j >> 5) * nu->stride + 8u * c;
+    const DevNode nu = gld(p.nodes + u);
+    const uint32_t v = nu.first_child + (uint32_t)c;
+    const uint64_t blk = nu.base + (uint64_t)(j >> 5) * nu.stride + 8u * c;
     if (m == 0) st.pop();  // the frame has no children left: drop it before descending
-    const DevNode *nv = p.nodes + v;
-    if (nv->kind == KIND_LEAF) {
-        sk.emit(p, nv->label);
+    const DevNode nv = gld(p.nodes + v);
+    if (nv.kind == KIND_LEAF) {
+        sk.emit(p, nv.label);
         return;
     }
-    const uint2 rb = *reinterpret_cast<const uint2 *>(blk);  // {rank before block, bits}
+    const uint2 rb = gld_at<uint2>(blk);  // {rank before block, bits}
     const uint32_t below = (1u << (j & 31)) - 1u;
     const uint32_t jv = rb.x + (uint32_t)__builtin_popcount(rb.y & below);  // rank1(j) - 1
     enter<MAXD, MaskT, MODE>(p, st, sk, v, jv);
@@ -196,12 +219,12 @@ __global__ __launch_bounds__(256) void k_traverse(TravParams p) {
     unsigned long long acc_visits = 0, acc_labels = 0;
 
     auto begin_row = [&]() {
-        bi = (MODE == MODE_DIRECT) ? (uint64_t)p.slot_list[s] : (p.order ? (uint64_t)p.order[s] : s);
-        const uint64_t row = p.rows[bi];
+        bi = (MODE == MODE_DIRECT) ? (uint64_t)gld(p.slot_list + s) : (p.order ? (uint64_t)gld(p.order + s) : s);
+        const uint64_t row = gld(p.rows + bi);
         sk.cnt = 0;
         sk.visits = 0;
         if constexpr (MODE == MODE_SLOTS) sk.slot_base = bi * p.K;
-        if constexpr (MODE == MODE_DIRECT) sk.slot_base = p.offsets[bi];
+        if constexpr (MODE == MODE_DIRECT) sk.slot_base = gld(p.offsets + bi);
         if (row >= p.num_rows) {
             atomicOr(&p.scalars[2], 1ull);
             return;
@@ -210,10 +233,10 @@ __global__ __launch_bounds__(256) void k_traverse(TravParams p) {
     };
     auto end_row = [&]() {
         if constexpr (MODE == MODE_SLOTS) {
-            p.counts[bi] = sk.cnt;
+            gst(p.counts + bi, sk.cnt);
             if (sk.cnt > p.K) {
                 const unsigned long long k = atomicAdd(&p.scalars[1], 1ull);
-                p.ovf_list[k] = (uint32_t)bi;
+                gst(p.ovf_list + k, (uint32_t)bi);
             }
         }
         if constexpr (MODE == MODE_WORK) {
@@ -252,13 +275,13 @@ __global__ __launch_bounds__(256) void k_traverse(TravParams p) {
 // reference's output order); the index of the next child comes from lane
 // c's register through a cross-lane shuffle.
 // ------------------------------------------------------------------------
-template <int MAXD, int CPL>
+template <int MAXD, int CPL, typename MaskT>
 struct GroupFrames {
     uint32_t jc[MAXD][CPL];  // per lane: position of child c*CPL+k in its own image
     uint32_t fc[MAXD];       // uniform: dnode of child 0
-    uint64_t pend[MAXD];     // uniform: children still to take (bit i = child i)
+    MaskT pend[MAXD];        // uniform: children still to take (bit i = child i)
     int sp;
-    __device__ __forceinline__ void push(const uint32_t (&j)[CPL], uint32_t f, uint64_t p) {
+    __device__ __forceinline__ void push(const uint32_t (&j)[CPL], uint32_t f, MaskT p) {
 #pragma unroll
         for (int k = MAXD - 1; k > 0; --k) {
 #pragma unroll
@@ -297,7 +320,7 @@ struct GroupSink {
     uint32_t cnt;        // labels emitted so far (uniform)
     uint64_t slot_base;  // MODE_SLOTS: bi*K ; MODE_DIRECT: offsets[bi]
     uint64_t visits;
-    uint32_t *stage;     // this group's LDS stage
+    AS_LDS uint32_t *stage;  // this group's LDS stage
     // lane-parallel emission: `label` goes to position cnt + rank
     __device__ __forceinline__ void put(const TravParams &p, uint32_t rank, uint32_t label) {
         const uint32_t pos = cnt + rank;
@@ -308,9 +331,9 @@ struct GroupSink {
             }
         }
         if constexpr (MODE == MODE_SLOTS) {
-            if (pos < p.K) p.temp[slot_base + pos] = label;
+            if (pos < p.K) gst(p.temp + slot_base + pos, label);
         } else if constexpr (MODE == MODE_DIRECT) {
-            p.cols[slot_base + pos] = label;
+            gst(p.cols + slot_base + pos, label);
         } else if constexpr (MODE == MODE_COUNT) {
             atomicAdd(&p.label_counts[label], 1ull);
         }
@@ -324,8 +347,8 @@ struct GroupSink {
             uint32_t lim = cnt < kStageLabels ? cnt : kStageLabels;
             if constexpr (MODE == MODE_SLOTS) lim = lim < p.K ? lim : p.K;
             for (uint32_t pos = c; pos < lim; pos += G) {
-                if constexpr (MODE == MODE_SLOTS) p.temp[slot_base + pos] = stage[pos];
-                else p.cols[slot_base + pos] = stage[pos];
+                if constexpr (MODE == MODE_SLOTS) gst(p.temp + slot_base + pos, (uint32_t)stage[pos]);
+                else gst(p.cols + slot_base + pos, (uint32_t)stage[pos]);
             }
         }
     }
@@ -340,12 +363,12 @@ __device__ __forceinline__ uint64_t spread_bits(uint64_t x, uint32_t G) {
     return r;
 }
 
-template <int MAXD, int CPL, int MODE>
-__device__ __forceinline__ void group_visit(const TravParams &p, GroupFrames<MAXD, CPL> &st, GroupSink<MODE> &sk,
+template <int MAXD, int CPL, typename MaskT, int MODE>
+__device__ __forceinline__ void group_visit(const TravParams &p, GroupFrames<MAXD, CPL, MaskT> &st, GroupSink<MODE> &sk,
                                             const DevNode &nd, uint32_t j, uint32_t c, uint32_t gbase,
                                             uint64_t gmask, uint32_t G) {
     const uint32_t a = nd.arity;
-    const uint8_t *base = reinterpret_cast<const uint8_t *>(nd.base);
+    const uint64_t base = nd.base;
     if constexpr (MODE == MODE_WORK) sk.visits += a;  // operator[] on every child (BRWT.cpp:30)
     if (nd.kind == KIND_PLANE) {
         const uint32_t t = j & 31;
@@ -357,16 +380,16 @@ __device__ __forceinline__ void group_visit(const TravParams &p, GroupFrames<MAX
             jc[q] = 0;
         }
         if (c * CPL < a) {
-            const uint8_t *blk = base + (uint64_t)(j >> 5) * nd.stride + 8u * CPL * c;
+            const uint64_t blk = base + (uint64_t)(j >> 5) * nd.stride + 8u * CPL * c;
             uint32_t rk[CPL], bw[CPL];
             if constexpr (CPL == 1) {
-                const uint2 rb = *reinterpret_cast<const uint2 *>(blk);
+                const uint2 rb = gld_at<uint2>(blk);
                 rk[0] = rb.x;
                 bw[0] = rb.y;
             } else {
 #pragma unroll
                 for (int h = 0; h < CPL / 2; ++h) {
-                    const uint4 q4 = *reinterpret_cast<const uint4 *>(blk + 16 * h);
+                    const uint4 q4 = gld_at<uint4>(blk + 16 * h);
                     rk[2 * h] = q4.x;
                     bw[2 * h] = q4.y;
                     rk[2 * h + 1] = q4.z;
@@ -389,28 +412,28 @@ __device__ __forceinline__ void group_visit(const TravParams &p, GroupFrames<MAX
                 if (c == 0) atomicOr(&p.scalars[2], 2ull);
                 return;
             }
-            st.push(jc, nd.first_child, P);
+            st.push(jc, nd.first_child, (MaskT)P);
         }
         return;
     }
     uint64_t m;  // all children are leaves: one mask per position (uniform load)
-    if (nd.kind == KIND_MASK8) m = base[j];
-    else if (nd.kind == KIND_MASK16) m = reinterpret_cast<const uint16_t *>(base)[j];
-    else if (nd.kind == KIND_MASK32) m = reinterpret_cast<const uint32_t *>(base)[j];
-    else m = reinterpret_cast<const uint64_t *>(base)[j];
+    if (nd.kind == KIND_MASK8) m = gld_at<uint8_t>(base + j);
+    else if (nd.kind == KIND_MASK16) m = gld_at<uint16_t>(base + 2ull * j);
+    else if (nd.kind == KIND_MASK32) m = gld_at<uint32_t>(base + 4ull * j);
+    else m = gld_at<uint64_t>(base + 8ull * j);
 #pragma unroll
     for (int q = 0; q < CPL; ++q) {
         const uint32_t cc = c * CPL + q;
         if (cc < a && ((m >> cc) & 1u)) {
             const uint32_t label =
-                (nd.flags & FLAG_CONSEC_LABELS) ? nd.label + cc : p.nodes[nd.first_child + cc].label;
+                (nd.flags & FLAG_CONSEC_LABELS) ? nd.label + cc : gld(p.nodes + nd.first_child + cc).label;
             sk.put(p, (uint32_t)__builtin_popcountll(m & ((1ull << cc) - 1ull)), label);
         }
     }
     sk.cnt += (uint32_t)__builtin_popcountll(m);
 }
 
-template <int MAXD, int CPL, int MODE>
+template <int MAXD, int CPL, typename MaskT, int MODE>
 __global__ __launch_bounds__(256) void k_traverse_group(TravParams p, uint32_t G) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c = lane & (G - 1);
@@ -420,7 +443,7 @@ __global__ __launch_bounds__(256) void k_traverse_group(TravParams p, uint32_t G
     const uint64_t gstride = (uint64_t)gridDim.x * groups_per_block;
     uint64_t s = (uint64_t)blockIdx.x * groups_per_block + threadIdx.x / G;
 
-    GroupFrames<MAXD, CPL> st;
+    GroupFrames<MAXD, CPL, MaskT> st;
 #pragma unroll
     for (int k = 0; k < MAXD; ++k) {
 #pragma unroll
@@ -434,32 +457,32 @@ __global__ __launch_bounds__(256) void k_traverse_group(TravParams p, uint32_t G
     sk.cnt = 0;
     sk.visits = 0;
     sk.slot_base = 0;
-    sk.stage = lds_stage + (threadIdx.x / G) * kStageLabels;
+    sk.stage = (AS_LDS uint32_t *)lds_stage + (threadIdx.x / G) * kStageLabels;
     uint64_t bi = 0;
     unsigned long long acc_visits = 0, acc_labels = 0;
 
     auto begin_row = [&]() {
-        bi = (MODE == MODE_DIRECT) ? (uint64_t)p.slot_list[s] : (p.order ? (uint64_t)p.order[s] : s);
-        const uint64_t row = p.rows[bi];
+        bi = (MODE == MODE_DIRECT) ? (uint64_t)gld(p.slot_list + s) : (p.order ? (uint64_t)gld(p.order + s) : s);
+        const uint64_t row = gld(p.rows + bi);
         sk.cnt = 0;
         sk.visits = 0;
         if constexpr (MODE == MODE_SLOTS) sk.slot_base = bi * p.K;
-        if constexpr (MODE == MODE_DIRECT) sk.slot_base = p.offsets[bi];
+        if constexpr (MODE == MODE_DIRECT) sk.slot_base = gld(p.offsets + bi);
         if (row >= p.num_rows) {
             if (c == 0) atomicOr(&p.scalars[2], 1ull);
             return;
         }
-        const DevNode nd = p.nodes[0];
-        group_visit<MAXD, CPL, MODE>(p, st, sk, nd, (uint32_t)row, c, gbase, gmask, G);
+        const DevNode nd = gld(p.nodes);
+        group_visit<MAXD, CPL, MaskT, MODE>(p, st, sk, nd, (uint32_t)row, c, gbase, gmask, G);
     };
     auto end_row = [&]() {
         sk.flush(p, c, G);
         if constexpr (MODE == MODE_SLOTS) {
             if (c == 0) {
-                p.counts[bi] = sk.cnt;
+                gst(p.counts + bi, sk.cnt);
                 if (sk.cnt > p.K) {
                     const unsigned long long k = atomicAdd(&p.scalars[1], 1ull);
-                    p.ovf_list[k] = (uint32_t)bi;
+                    gst(p.ovf_list + k, (uint32_t)bi);
                 }
             }
         }
@@ -482,8 +505,8 @@ __global__ __launch_bounds__(256) void k_traverse_group(TravParams p, uint32_t G
         }
         if (!__any(active)) break;
         if (active && st.sp > 0) {
-            uint64_t P = st.pend[0];
-            const uint32_t cs = (uint32_t)__builtin_ctzll(P);
+            MaskT P = st.pend[0];
+            const uint32_t cs = (uint32_t)__builtin_ctzll((uint64_t)P);
             P &= P - 1;
             st.pend[0] = P;
             const uint32_t w = st.fc[0] + cs;
@@ -493,12 +516,12 @@ __global__ __launch_bounds__(256) void k_traverse_group(TravParams p, uint32_t G
                 if ((cs % CPL) == (uint32_t)q) mine = st.jc[0][q];
             const uint32_t jw = (uint32_t)__shfl((int)mine, (int)(gbase + cs / CPL), 64);
             if (P == 0) st.pop();  // no children left at this level: drop it before descending
-            const DevNode nd = p.nodes[w];
+            const DevNode nd = gld(p.nodes + w);
             if (nd.kind == KIND_LEAF) {
                 if (c == 0) sk.put(p, 0, nd.label);
                 sk.cnt += 1;
             } else {
-                group_visit<MAXD, CPL, MODE>(p, st, sk, nd, jw, c, gbase, gmask, G);
+                group_visit<MAXD, CPL, MaskT, MODE>(p, st, sk, nd, jw, c, gbase, gmask, G);
             }
         }
     }
@@ -544,11 +567,12 @@ __global__ __launch_bounds__(256) void k_get(const DevNode *__restrict__ nodes, 
         uint32_t v = 0, j = (uint32_t)row;
         uint8_t bit = 0;
         for (uint32_t k = 0; k < path_len; ++k) {
-            const DevNode *nd = nodes + v;
+            const DevNode ndv = gld(nodes + v);
+            const DevNode *nd = &ndv;
             const uint32_t c = col_path[col * path_len + k];
-            const uint8_t *base = reinterpret_cast<const uint8_t *>(nd->base);
+            const uint64_t base = nd->base;
             if (nd->kind == KIND_PLANE) {
-                const uint2 rb = *reinterpret_cast<const uint2 *>(base + (uint64_t)(j >> 5) * nd->stride + 8u * c);
+                const uint2 rb = gld_at<uint2>(base + (uint64_t)(j >> 5) * nd->stride + 8u * c);
                 const uint32_t t = j & 31;
                 if (!((rb.y >> t) & 1u)) break;
                 j = rb.x + (uint32_t)__builtin_popcount(rb.y & ((1u << t) - 1u));
@@ -559,10 +583,10 @@ __global__ __launch_bounds__(256) void k_get(const DevNode *__restrict__ nodes, 
                 }
             } else {
                 uint64_t m;
-                if (nd->kind == KIND_MASK8) m = base[j];
-                else if (nd->kind == KIND_MASK16) m = reinterpret_cast<const uint16_t *>(base)[j];
-                else if (nd->kind == KIND_MASK32) m = reinterpret_cast<const uint32_t *>(base)[j];
-                else m = reinterpret_cast<const uint64_t *>(base)[j];
+                if (nd->kind == KIND_MASK8) m = gld_at<uint8_t>(base + j);
+                else if (nd->kind == KIND_MASK16) m = gld_at<uint16_t>(base + 2ull * j);
+                else if (nd->kind == KIND_MASK32) m = gld_at<uint32_t>(base + 4ull * j);
+                else m = gld_at<uint64_t>(base + 8ull * j);
                 bit = (uint8_t)((m >> c) & 1u);
                 break;
             }
@@ -614,11 +638,12 @@ Trav pick_traverse(const Ctx &c) {
     uint32_t G = 1;
     while (G < need) G <<= 1;
     t.G = G;
-#define PICKG(D, CPLV)                                                     \
-    if (depth <= D && cpl == CPLV) {                                       \
-        t.group_fn = (GroupFn)k_traverse_group<D, CPLV, MODE>;             \
-        t.fn = reinterpret_cast<const void *>(t.group_fn);                 \
-        return t;                                                          \
+#define PICKG(D, CPLV)                                                                          \
+    if (depth <= D && cpl == CPLV) {                                                            \
+        t.group_fn = max_arity <= 32 ? (GroupFn)k_traverse_group<D, CPLV, uint32_t, MODE>       \
+                                     : (GroupFn)k_traverse_group<D, CPLV, uint64_t, MODE>;      \
+        t.fn = reinterpret_cast<const void *>(t.group_fn);                                      \
+        return t;                                                                               \
     }
 #define PICKD(CPLV) PICKG(4, CPLV) PICKG(8, CPLV) PICKG(16, CPLV) PICKG(32, CPLV)
     PICKD(1)
