@@ -269,7 +269,7 @@ int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value) {
         c.sort_rows = value != 0;
         return MBRWT_OK;
     case MBRWT_OPT_KERNEL:
-        if (value < 0 || value > 4) return MBRWT_ERR_INVALID;
+        if (value < 0 || value > 6) return MBRWT_ERR_INVALID;
         c.kernel_variant = (int)value;
         return MBRWT_OK;
     default:

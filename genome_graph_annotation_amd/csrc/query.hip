@@ -433,8 +433,8 @@ __device__ __forceinline__ void group_visit(const TravParams &p, GroupFrames<MAX
     sk.cnt += (uint32_t)__builtin_popcountll(m);
 }
 
-template <int MAXD, int CPL, typename MaskT, int MODE>
-__global__ __launch_bounds__(256) void k_traverse_group(TravParams p, uint32_t G) {
+template <int MAXD, int CPL, typename MaskT, int MODE, int WPE>
+__global__ __launch_bounds__(256, WPE) void k_traverse_group(TravParams p, uint32_t G) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c = lane & (G - 1);
     const uint32_t gbase = lane & ~(G - 1);
@@ -632,23 +632,28 @@ Trav pick_traverse(const Ctx &c) {
 #undef PICK
         return t;
     }
-    // group kernel: CPL children per lane, G = pow2ceil(ceil(max_arity / CPL)) lanes per row
-    const int cpl = c.kernel_variant == 2 ? 1 : c.kernel_variant == 4 ? 4 : 2;
+    // group kernel: CPL children per lane, G = pow2ceil(ceil(max_arity / CPL)) lanes per row;
+    // variants 5/6 request a higher occupancy (waves per SIMD) from the register allocator
+    const int v = c.kernel_variant;
+    const int cpl = v == 2 ? 1 : (v == 4 || v == 6) ? 4 : 2;
+    const int wpe = v == 5 ? 8 : v == 6 ? 6 : 1;
     const uint32_t need = (max_arity + cpl - 1) / cpl;
     uint32_t G = 1;
     while (G < need) G <<= 1;
     t.G = G;
-#define PICKG(D, CPLV)                                                                          \
-    if (depth <= D && cpl == CPLV) {                                                            \
-        t.group_fn = max_arity <= 32 ? (GroupFn)k_traverse_group<D, CPLV, uint32_t, MODE>       \
-                                     : (GroupFn)k_traverse_group<D, CPLV, uint64_t, MODE>;      \
-        t.fn = reinterpret_cast<const void *>(t.group_fn);                                      \
-        return t;                                                                               \
+#define PICKG(D, CPLV, W)                                                                          \
+    if (depth <= D && cpl == CPLV && wpe == W) {                                                   \
+        t.group_fn = max_arity <= 32 ? (GroupFn)k_traverse_group<D, CPLV, uint32_t, MODE, W>       \
+                                     : (GroupFn)k_traverse_group<D, CPLV, uint64_t, MODE, W>;      \
+        t.fn = reinterpret_cast<const void *>(t.group_fn);                                         \
+        return t;                                                                                  \
     }
-#define PICKD(CPLV) PICKG(4, CPLV) PICKG(8, CPLV) PICKG(16, CPLV) PICKG(32, CPLV)
-    PICKD(1)
-    PICKD(2)
-    PICKD(4)
+#define PICKD(CPLV, W) PICKG(4, CPLV, W) PICKG(8, CPLV, W) PICKG(16, CPLV, W) PICKG(32, CPLV, W)
+    PICKD(1, 1)
+    PICKD(2, 1)
+    PICKD(4, 1)
+    PICKD(2, 8)
+    PICKD(4, 6)
 #undef PICKD
 #undef PICKG
     return t;

@@ -38,6 +38,46 @@ __global__ __launch_bounds__(256) void k_probe(const uint4 *__restrict__ buf, ui
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) out[tid] = acc;
 }
 
+// groups of G lanes read one 16*G-byte segment of a random line together
+// (the coalesced shape of the group traversal kernel)
+template <int U>
+__global__ __launch_bounds__(256) void k_probe_group(const uint4 *__restrict__ buf, uint64_t nlines, uint32_t G,
+                                                      uint32_t iters, uint64_t seed, uint4 *out) {
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t grp = tid / G;
+    const uint32_t c = tid % G;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (uint32_t it = 0; it < iters; ++it) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t line = mix64(seed ^ (grp * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)(it * U + u) << 40)) % nlines;
+            v[u] = buf[line * 8 + c];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            acc.x ^= v[u].x; acc.y ^= v[u].y; acc.z ^= v[u].z; acc.w ^= v[u].w;
+        }
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) out[tid] = acc;
+}
+
+template <int U>
+double run_group(const uint4 *buf, uint64_t bytes_total, uint32_t G, int grid, uint32_t iters, uint4 *out) {
+    const uint64_t nlines = bytes_total / 128;
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipLaunchKernelGGL(k_probe_group<U>, dim3(grid), dim3(256), 0, 0, buf, nlines, G, iters, 1, out);
+    hipEventRecord(a);
+    hipLaunchKernelGGL(k_probe_group<U>, dim3(grid), dim3(256), 0, 0, buf, nlines, G, iters, 7, out);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    return (double)grid * 256 / G * iters * U / (ms / 1e3);
+}
+
 template <int VEC>
 double run(const uint4 *buf, uint64_t bytes_total, uint32_t line_bytes, int grid, uint32_t iters, uint4 *out) {
     const uint64_t nlines = bytes_total / line_bytes;
@@ -72,6 +112,13 @@ int main(int argc, char **argv) {
         double r64a = run<4>((const uint4 *)buf, total, 64, grid, iters, out);
         printf("buffer %.1f GiB grid %d: 16B-in-128B-line %.2f G/s | 64B(128-aligned) %.2f G/s | 128B %.2f G/s (%.2f TB/s) | 64B(64-aligned) %.2f G/s (%.2f TB/s)\n",
                gib, grid, r16 / 1e9, r64 / 1e9, r128 / 1e9, r128 * 128 / 1e12, r64a / 1e9, r64a * 64 / 1e12);
+    }
+    for (uint32_t G : {1u, 2u, 4u, 8u}) {
+        const int grid = 8192;
+        double u1 = run_group<1>((const uint4 *)buf, total, G, grid, 64, out);
+        double u4 = run_group<4>((const uint4 *)buf, total, G, grid, 64, out);
+        printf("buffer %.1f GiB group G=%u (%u B segment): 1 in flight %.2f G lines/s | 4 in flight %.2f G lines/s\n",
+               gib, G, 16 * G, u1 / 1e9, u4 / 1e9);
     }
     hipFree(buf);
     return 0;
