@@ -25,6 +25,16 @@ static int upload_tables(Ctx &c) {
     if (!t.nodes.empty()) {
         MBRWT_HIP(hipMalloc(&c.d_nodes, t.nodes.size() * sizeof(DevNode)));
         MBRWT_HIP(hipMemcpy(c.d_nodes, t.nodes.data(), t.nodes.size() * sizeof(DevNode), hipMemcpyHostToDevice));
+        std::vector<CNode> cn(t.nodes.size());
+        for (size_t i = 0; i < cn.size(); ++i) {
+            if (t.nodes[i].base >> 48) {
+                set_error("device address above 2^48");
+                return MBRWT_ERR_UNSUPPORTED;
+            }
+            cn[i] = compact(t.nodes[i]);
+        }
+        MBRWT_HIP(hipMalloc(&c.d_cnodes, cn.size() * sizeof(CNode)));
+        MBRWT_HIP(hipMemcpy(c.d_cnodes, cn.data(), cn.size() * sizeof(CNode), hipMemcpyHostToDevice));
     }
     if (!t.col_path.empty()) {
         MBRWT_HIP(hipMalloc(&c.d_col_path, t.col_path.size()));
@@ -48,6 +58,7 @@ static void release(Ctx *c) {
     for (Workspace *w : {&c->ws_temp, &c->ws_counts, &c->ws_ovf, &c->ws_scan, &c->ws_rows, &c->ws_out, &c->ws_sort})
         if (w->buf) (void)hipFree(w->buf);
     if (c->d_nodes) (void)hipFree(c->d_nodes);
+    if (c->d_cnodes) (void)hipFree(c->d_cnodes);
     if (c->d_col_path) (void)hipFree(c->d_col_path);
     if (c->d_col_leaf) (void)hipFree(c->d_col_leaf);
     if (c->d_scalars) (void)hipFree(c->d_scalars);

@@ -52,6 +52,28 @@ struct alignas(32) DevNode {
 };
 static_assert(sizeof(DevNode) == 32, "DevNode must be 32 bytes");
 
+// Compact 16-byte node record read by the group kernel (kept in LDS for the
+// first kLdsNodes dnodes -- in BFS numbering the internal nodes come first):
+//   w0 = base[0:48) | kind[48:51) | flags[51] | log2(stride)[52:56) | arity[56:64)
+struct alignas(16) CNode {
+    uint64_t w0;
+    uint32_t first_child;
+    uint32_t label;
+};
+static_assert(sizeof(CNode) == 16, "CNode must be 16 bytes");
+constexpr uint32_t kLdsNodes = 512;
+
+inline CNode compact(const DevNode &d) {
+    uint32_t lg = 0;
+    while (d.stride && (1u << lg) < d.stride) ++lg;
+    CNode c;
+    c.w0 = (d.base & ((1ull << 48) - 1)) | ((uint64_t)(d.kind & 7) << 48) | ((uint64_t)(d.flags & 1) << 51) |
+           ((uint64_t)(lg & 15) << 52) | ((uint64_t)(d.arity & 0xFF) << 56);
+    c.first_child = d.first_child;
+    c.label = d.label;
+    return c;
+}
+
 constexpr uint32_t kMaxArity = 64;       // child masks are held in <= 64 bits
 constexpr uint32_t kImagePad = 64;       // bytes of zero padding after every image
 constexpr uint64_t kMaxRows = 0xFFFFFFFFull;  // positions are 32-bit in the kernels
@@ -88,6 +110,7 @@ struct Ctx {
     int device = 0;
     Tree tree;
     DevNode *d_nodes = nullptr;
+    CNode *d_cnodes = nullptr;
     uint8_t *d_col_path = nullptr;
     uint32_t *d_col_leaf = nullptr;
     hipStream_t stream = nullptr;       // stream of the host-buffer API

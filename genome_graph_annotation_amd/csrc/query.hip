@@ -65,7 +65,31 @@ struct TravParams {
     const uint64_t *offsets;     // MODE_DIRECT
     uint32_t *cols;              // MODE_DIRECT
     unsigned long long *label_counts;  // MODE_COUNT: [num_columns]
+    const CNode *cnodes;         // compact node records (group kernel)
+    uint32_t n_lds;              // records [0, n_lds) are staged in LDS
 };
+
+// decoded node record
+struct NodeInfo {
+    uint64_t base;
+    uint32_t first_child;
+    uint32_t label;
+    uint32_t stride;
+    uint32_t arity;
+    uint32_t kind;
+    uint32_t flags;
+};
+__device__ __forceinline__ NodeInfo decode(uint64_t w0, uint64_t w1) {
+    NodeInfo n;
+    n.base = w0 & ((1ull << 48) - 1);
+    n.kind = (uint32_t)(w0 >> 48) & 7u;
+    n.flags = (uint32_t)(w0 >> 51) & 1u;
+    n.stride = 1u << ((uint32_t)(w0 >> 52) & 15u);
+    n.arity = (uint32_t)(w0 >> 56);
+    n.first_child = (uint32_t)w1;
+    n.label = (uint32_t)(w1 >> 32);
+    return n;
+}
 
 template <typename MaskT>
 __device__ __forceinline__ int ctz_m(MaskT m) {
@@ -365,7 +389,7 @@ __device__ __forceinline__ uint64_t spread_bits(uint64_t x, uint32_t G) {
 
 template <int MAXD, int CPL, typename MaskT, int MODE>
 __device__ __forceinline__ void group_visit(const TravParams &p, GroupFrames<MAXD, CPL, MaskT> &st, GroupSink<MODE> &sk,
-                                            const DevNode &nd, uint32_t j, uint32_t c, uint32_t gbase,
+                                            const NodeInfo &nd, uint32_t j, uint32_t c, uint32_t gbase,
                                             uint64_t gmask, uint32_t G) {
     const uint32_t a = nd.arity;
     const uint64_t base = nd.base;
@@ -426,7 +450,9 @@ __device__ __forceinline__ void group_visit(const TravParams &p, GroupFrames<MAX
         const uint32_t cc = c * CPL + q;
         if (cc < a && ((m >> cc) & 1u)) {
             const uint32_t label =
-                (nd.flags & FLAG_CONSEC_LABELS) ? nd.label + cc : gld(p.nodes + nd.first_child + cc).label;
+                (nd.flags & FLAG_CONSEC_LABELS) ? nd.label + cc
+                                                 : (uint32_t)(gld(reinterpret_cast<const uint64_t *>(p.cnodes) +
+                                                                  2 * (nd.first_child + cc) + 1) >> 32);
             sk.put(p, (uint32_t)__builtin_popcountll(m & ((1ull << cc) - 1ull)), label);
         }
     }
@@ -453,6 +479,15 @@ __global__ __launch_bounds__(256, WPE) void k_traverse_group(TravParams p, uint3
     }
     st.sp = 0;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_stage[];  // (256 / G) * kStageLabels
+    // node records [0, n_lds) after the label stages
+    AS_LDS uint64_t *lds_nodes = (AS_LDS uint64_t *)((AS_LDS uint32_t *)lds_stage + (blockDim.x / G) * kStageLabels);
+    const uint64_t *gnodes = reinterpret_cast<const uint64_t *>(p.cnodes);
+    for (uint32_t i = threadIdx.x; i < 2 * p.n_lds; i += blockDim.x) lds_nodes[i] = gld(gnodes + i);
+    __syncthreads();
+    auto node_info = [&](uint32_t w) -> NodeInfo {
+        if (w < p.n_lds) return decode(lds_nodes[2 * w], lds_nodes[2 * w + 1]);
+        return decode(gld(gnodes + 2 * w), gld(gnodes + 2 * w + 1));
+    };
     GroupSink<MODE> sk;
     sk.cnt = 0;
     sk.visits = 0;
@@ -472,7 +507,7 @@ __global__ __launch_bounds__(256, WPE) void k_traverse_group(TravParams p, uint3
             if (c == 0) atomicOr(&p.scalars[2], 1ull);
             return;
         }
-        const DevNode nd = gld(p.nodes);
+        const NodeInfo nd = node_info(0);
         group_visit<MAXD, CPL, MaskT, MODE>(p, st, sk, nd, (uint32_t)row, c, gbase, gmask, G);
     };
     auto end_row = [&]() {
@@ -516,7 +551,7 @@ __global__ __launch_bounds__(256, WPE) void k_traverse_group(TravParams p, uint3
                 if ((cs % CPL) == (uint32_t)q) mine = st.jc[0][q];
             const uint32_t jw = (uint32_t)__shfl((int)mine, (int)(gbase + cs / CPL), 64);
             if (P == 0) st.pop();  // no children left at this level: drop it before descending
-            const DevNode nd = gld(p.nodes + w);
+            const NodeInfo nd = node_info(w);
             if (nd.kind == KIND_LEAF) {
                 if (c == 0) sk.put(p, 0, nd.label);
                 sk.cnt += 1;
@@ -659,13 +694,17 @@ Trav pick_traverse(const Ctx &c) {
     return t;
 }
 
-size_t lds_bytes(const Trav &t) { return t.group_fn ? (size_t)(256 / t.G) * kStageLabels * sizeof(uint32_t) : 0; }
+size_t lds_bytes(const Ctx &c, const Trav &t) {
+    if (!t.group_fn) return 0;
+    const size_t nl = std::min<size_t>(c.tree.nodes.size(), kLdsNodes);
+    return (size_t)(256 / t.G) * kStageLabels * sizeof(uint32_t) + nl * sizeof(CNode);
+}
 
 int grid_for(const Ctx &c, const Trav &t, uint64_t n) {
     int dev_cus = 0;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device);
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, t.fn, 256, lds_bytes(t)) != hipSuccess || per_cu <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, t.fn, 256, lds_bytes(c, t)) != hipSuccess || per_cu <= 0)
         per_cu = 4;
     const uint64_t resident = (uint64_t)std::max(1, dev_cus) * (uint64_t)per_cu;
     const uint64_t rows_per_block = 256 / t.G;
@@ -675,7 +714,7 @@ int grid_for(const Ctx &c, const Trav &t, uint64_t n) {
 
 hipError_t launch(const Ctx &c, const Trav &t, uint64_t n, hipStream_t s, const TravParams &p) {
     const int grid = grid_for(c, t, n);
-    if (t.group_fn) hipLaunchKernelGGL(t.group_fn, dim3(grid), dim3(256), lds_bytes(t), s, p, t.G);
+    if (t.group_fn) hipLaunchKernelGGL(t.group_fn, dim3(grid), dim3(256), lds_bytes(c, t), s, p, t.G);
     else hipLaunchKernelGGL(t.lane_fn, dim3(grid), dim3(256), 0, s, p);
     return hipGetLastError();
 }
@@ -691,6 +730,8 @@ uint32_t auto_slots(const Ctx &c) {
 TravParams base_params(const Ctx &c) {
     TravParams p{};
     p.nodes = c.d_nodes;
+    p.cnodes = c.d_cnodes;
+    p.n_lds = (uint32_t)std::min<size_t>(c.tree.nodes.size(), kLdsNodes);
     p.num_rows = c.tree.num_rows;
     p.scalars = reinterpret_cast<unsigned long long *>(c.d_scalars);
     return p;
