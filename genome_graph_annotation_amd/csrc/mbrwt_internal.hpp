@@ -126,7 +126,7 @@ struct Ctx {
     bool timing = false;
     uint32_t slot_labels = 0;           // 0 = auto
     bool sort_rows = false;
-    int kernel_variant = 0;             // 0 group-per-row (default), 1 lane-per-row
+    int kernel_variant = 0;             // MBRWT_OPT_KERNEL (0 = default = 5)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double timing_ms = 0;
     uint64_t timing_launches = 0;

@@ -566,18 +566,35 @@ __global__ __launch_bounds__(256, WPE) void k_traverse_group(TravParams p, uint3
     }
 }
 
-// CSR compaction of the label slots (rows with <= K labels).
-__global__ __launch_bounds__(256) void k_compact(const uint32_t *__restrict__ counts,
-                                                 const uint64_t *__restrict__ offsets,
-                                                 const uint32_t *__restrict__ temp, uint32_t K,
-                                                 uint32_t *__restrict__ cols, uint64_t n) {
-    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
-        const uint32_t c = counts[i];
-        if (c > K) continue;
-        const uint64_t o = offsets[i];
-        const uint32_t *src = temp + i * K;
-        for (uint32_t k = 0; k < c; ++k) cols[o + k] = src[k];
+// CSR compaction of the label slots (rows with <= K labels).  A workgroup
+// takes 256 consecutive rows; its threads walk the tile's contiguous output
+// range [offsets[r0], offsets[r0+256]) so the stores are fully coalesced,
+// find each position's row by a binary search over the tile's offsets in
+// LDS, and read the slot labels (a row's labels are adjacent in its slot).
+constexpr int kCompactTile = 256;
+
+__global__ __launch_bounds__(kCompactTile) void k_compact(const uint64_t *__restrict__ offsets,
+                                                          const uint32_t *__restrict__ temp, uint32_t K,
+                                                          uint32_t *__restrict__ cols, uint64_t n) {
+    __shared__ uint64_t soff[kCompactTile + 1];
+    const uint32_t t = threadIdx.x;
+    for (uint64_t tile = blockIdx.x; tile * kCompactTile < n; tile += gridDim.x) {
+        const uint64_t r0 = tile * kCompactTile;
+        const uint32_t rn = (uint32_t)((n - r0) < kCompactTile ? (n - r0) : kCompactTile);
+        for (uint32_t i = t; i <= rn; i += kCompactTile) soff[i] = gld(offsets + r0 + i);
+        __syncthreads();
+        const uint64_t q0 = soff[0], q1 = soff[rn];
+        for (uint64_t q = q0 + t; q < q1; q += kCompactTile) {
+            uint32_t lo = 0, hi = rn;  // largest r with soff[r] <= q
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (soff[mid] <= q) lo = mid;
+                else hi = mid;
+            }
+            const uint64_t c = soff[lo + 1] - soff[lo];
+            if (c <= K) gst(cols + q, gld(temp + (r0 + lo) * K + (q - soff[lo])));
+        }
+        __syncthreads();
     }
 }
 
@@ -669,7 +686,7 @@ Trav pick_traverse(const Ctx &c) {
     }
     // group kernel: CPL children per lane, G = pow2ceil(ceil(max_arity / CPL)) lanes per row;
     // variants 5/6 request a higher occupancy (waves per SIMD) from the register allocator
-    const int v = c.kernel_variant;
+    const int v = c.kernel_variant ? c.kernel_variant : 5;  // default: 2 children per lane, 8 waves/SIMD
     const int cpl = v == 2 ? 1 : (v == 4 || v == 6) ? 4 : 2;
     const int wpe = v == 5 ? 8 : v == 6 ? 6 : 1;
     const uint32_t need = (max_arity + cpl - 1) / cpl;
@@ -722,8 +739,8 @@ hipError_t launch(const Ctx &c, const Trav &t, uint64_t n, hipStream_t s, const 
 uint32_t auto_slots(const Ctx &c) {
     if (c.slot_labels) return c.slot_labels;
     const double mean = c.tree.num_rows ? (double)c.tree.num_relations / (double)c.tree.num_rows : 0.0;
-    uint32_t k = 16;
-    while (k < 4.0 * mean + 16.0 && k < 1024) k <<= 1;
+    uint32_t k = kStageLabels;  // >= the LDS stage of the group kernel
+    while (k < 2.0 * mean + 8.0 && k < 1024) k <<= 1;
     return k;
 }
 
@@ -821,8 +838,8 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
         return MBRWT_ERR_CAPACITY;
     }
     {
-        const uint64_t g = std::min<uint64_t>((n + 255) / 256, 8192);
-        hipLaunchKernelGGL(k_compact, dim3((unsigned)g), dim3(256), 0, s, p.counts, d_offsets, p.temp, K, d_cols, n);
+        const uint64_t g = std::min<uint64_t>((n + kCompactTile - 1) / kCompactTile, 16384);
+        hipLaunchKernelGGL(k_compact, dim3((unsigned)g), dim3(kCompactTile), 0, s, d_offsets, p.temp, K, d_cols, n);
         MBRWT_HIP(hipGetLastError());
     }
     if (ovf) {
