@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=400_000, help="rows timed on the CPU")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host cores")
     ap.add_argument("--check-rows", type=int, default=20_000, help="GPU rows checked against the oracle")
-    ap.add_argument("--sort-rows", type=int, default=-1, help="-1 library default, 0/1 force")
+    ap.add_argument("--kernel", type=int, default=0, help="MBRWT_OPT_KERNEL variant (0 = library default)")
     return ap.parse_args()
 
 
@@ -77,8 +77,8 @@ def main():
     mat = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, device=local)
     setup_s = time.time() - t0
     log(f"device structure built in {setup_s:.1f} s ({mat.device_bytes() / 1e9:.1f} GB)")
-    if a.sort_rows >= 0:
-        mat.set_option(L.MBRWT_OPT_SORT_ROWS, a.sort_rows)
+    if a.kernel:
+        mat.set_option(L.MBRWT_OPT_KERNEL, a.kernel)
 
     rows_np = np.random.default_rng(a.seed + 1000 * rank).integers(0, a.rows, a.batch, dtype=np.uint64)
     rows_t = torch.from_numpy(rows_np.view(np.int64)).to(dev_t)

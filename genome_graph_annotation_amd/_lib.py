@@ -22,7 +22,6 @@ MBRWT_ERR_NOMEM = 6
 
 MBRWT_OPT_TIMING = 1
 MBRWT_OPT_SLOT_LABELS = 2
-MBRWT_OPT_SORT_ROWS = 3
 MBRWT_OPT_KERNEL = 4
 
 u64p = C.POINTER(C.c_uint64)

@@ -276,9 +276,6 @@ int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value) {
         if (value < 0 || value > 4096) return MBRWT_ERR_INVALID;
         c.slot_labels = (uint32_t)value;
         return MBRWT_OK;
-    case MBRWT_OPT_SORT_ROWS:
-        c.sort_rows = value != 0;
-        return MBRWT_OK;
     case MBRWT_OPT_KERNEL:
         if (value < 0 || value > 6) return MBRWT_ERR_INVALID;
         c.kernel_variant = (int)value;

@@ -125,7 +125,6 @@ struct Ctx {
     // options
     bool timing = false;
     uint32_t slot_labels = 0;           // 0 = auto
-    bool sort_rows = false;
     int kernel_variant = 0;             // MBRWT_OPT_KERNEL (0 = default = 5)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double timing_ms = 0;

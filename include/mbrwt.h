@@ -146,7 +146,6 @@ int mbrwt_count_work_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, 
 /* Options (mbrwt_set_option). */
 #define MBRWT_OPT_TIMING 1       /* 1: time the traversal kernel with HIP events */
 #define MBRWT_OPT_SLOT_LABELS 2  /* per-row label slots of the fast path (0 = auto) */
-#define MBRWT_OPT_SORT_ROWS 3    /* 1: process the batch in row order (radix sort) */
 #define MBRWT_OPT_KERNEL 4       /* traversal kernel: 0 default, 1 lane-per-row, 2/3/4 group with 1/2/4 children per lane */
 int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value);
 

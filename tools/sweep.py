@@ -20,25 +20,27 @@ ap.add_argument("--arity", type=int, default=8)
 ap.add_argument("--batch", type=int, default=8_000_000)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--variants", default="1,2,3,4")
-ap.add_argument("--sort", default="0")
+ap.add_argument("--presort", action="store_true", help="sort the batch on the host (locality experiment)")
 a = ap.parse_args()
 t0 = time.time()
 m = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, 42)
 print(f"built {m.device_bytes() / 1e9:.1f} GB in {time.time() - t0:.1f}s", flush=True)
-rows = torch.from_numpy(np.random.default_rng(42).integers(0, a.rows, a.batch, dtype=np.uint64).view(np.int64)).cuda()
+rows_np = np.random.default_rng(42).integers(0, a.rows, a.batch, dtype=np.uint64)
+if a.presort:
+    rows_np = np.sort(rows_np)
+rows = torch.from_numpy(rows_np.view(np.int64)).cuda()
 off = torch.empty(a.batch + 1, dtype=torch.int64, device="cuda")
 s = torch.cuda.current_stream().cuda_stream
 v, lab = m.count_work_device(rows, s)
 cols = torch.empty(lab + 1024, dtype=torch.int32, device="cuda")
 alg = 64 * v + 16 * a.batch + 4 * lab
 variants = [int(x) for x in a.variants.split(",")]
-sorts = [int(x) for x in a.sort.split(",")]
+sorts = [0]
 res = {}
 for rep in range(a.reps):
     for var in variants:
         for so in sorts:
             m.set_option(L.MBRWT_OPT_KERNEL, var)
-            m.set_option(L.MBRWT_OPT_SORT_ROWS, so)
             m.get_rows_device(rows, off, cols, s)
             m.take_timing()
             m.set_option(L.MBRWT_OPT_TIMING, 1)
