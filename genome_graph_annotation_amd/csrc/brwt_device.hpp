@@ -1,0 +1,150 @@
+// brwt_device.hpp -- C++ host mirror of the reference's BinaryMatrix surface
+// over the HIP engine (header-only, depends only on include/mbrwt.h).
+//
+// Reference interface restated (ratschlab/genome_graph_annotation):
+//   class BinaryMatrix           common/binary_matrix.hpp:9-29
+//   class BRWT : BinaryMatrix    annotation/hierarchical_annotation/BRWT.hpp:18-61
+// BRWTDevice keeps the reference's names, argument meaning and error
+// behaviour (out-of-range rows: the reference asserts, BRWT.cpp:27; here
+// std::out_of_range) and adds the batched get_rows() that the device path
+// is built for.  A reference build would register it where BRWTCompressed is
+// selected (main.cpp:222-225); see INTEGRATION.md.
+#pragma once
+
+#include <algorithm>
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/mbrwt.h"
+
+namespace mbrwt_host {
+
+// common/binary_matrix.hpp:9-29 (load/serialize/get_column are not part of
+// the device path; see DESIGN.md "Out of scope")
+class BinaryMatrix {
+  public:
+    typedef uint64_t Row;
+    typedef uint64_t Column;
+
+    virtual ~BinaryMatrix() {}
+
+    virtual uint64_t num_columns() const = 0;
+    virtual uint64_t num_rows() const = 0;
+
+    virtual bool get(Row row, Column column) const = 0;
+    virtual std::vector<Column> get_row(Row row) const = 0;
+
+    // Batched get_row: the default loops over get_row (every scheme of the
+    // reference); device-backed matrices override it with one launch.
+    virtual std::vector<std::vector<Column>> get_rows(const std::vector<Row> &rows) const {
+        std::vector<std::vector<Column>> out;
+        out.reserve(rows.size());
+        for (Row r : rows) out.push_back(get_row(r));
+        return out;
+    }
+
+    // number of ones in the matrix
+    virtual uint64_t num_relations() const = 0;
+};
+
+class MBRWTException : public std::runtime_error {
+  public:
+    MBRWTException(int status, const std::string &where)
+        : std::runtime_error(where + ": " + mbrwt_strerror(status) + " (" + mbrwt_last_error_message() + ")"),
+          status_(status) {}
+    int status() const { return status_; }
+
+  private:
+    int status_;
+};
+
+inline void check_status(int status, const char *where) {
+    if (status == MBRWT_OK) return;
+    if (status == MBRWT_ERR_RANGE) throw std::out_of_range(std::string(where) + ": row or column out of range");
+    throw MBRWTException(status, where);
+}
+
+// A BRWT whose queries run on an MI355X (the reference's BRWT::get_row /
+// BRWT::get, BRWT.cpp:9-53).
+class BRWTDevice : public BinaryMatrix {
+  public:
+    BRWTDevice() = default;  // the empty BRWT() (test_BRWT.cpp:15-19)
+
+    BRWTDevice(const mbrwt_tree_desc &desc, int device = 0) {
+        mbrwt_ctx *c = nullptr;
+        check_status(mbrwt_create(&desc, device, &c), "mbrwt_create");
+        ctx_.reset(c, Deleter());
+    }
+
+    static BRWTDevice synthetic(const mbrwt_synth_desc &desc, int device = 0) {
+        BRWTDevice m;
+        mbrwt_ctx *c = nullptr;
+        check_status(mbrwt_create_synthetic(&desc, device, &c), "mbrwt_create_synthetic");
+        m.ctx_.reset(c, Deleter());
+        return m;
+    }
+
+    uint64_t num_columns() const override { return ctx_ ? mbrwt_num_columns(ctx_.get()) : 0; }
+    uint64_t num_rows() const override { return ctx_ ? mbrwt_num_rows(ctx_.get()) : 0; }
+    uint64_t num_relations() const override { return ctx_ ? mbrwt_num_relations(ctx_.get()) : 0; }
+    uint64_t num_nodes() const { return ctx_ ? mbrwt_num_nodes(ctx_.get()) : 1; }
+
+    bool get(Row row, Column column) const override {
+        if (!ctx_) throw std::out_of_range("get on an empty BRWT");
+        uint8_t out = 0;
+        check_status(mbrwt_get_batch(ctx_.get(), &row, &column, 1, &out), "BRWTDevice::get");
+        return out != 0;
+    }
+
+    std::vector<Column> get_row(Row row) const override { return get_rows({row}).at(0); }
+
+    std::vector<std::vector<Column>> get_rows(const std::vector<Row> &rows) const override {
+        std::vector<uint64_t> offsets;
+        std::vector<uint32_t> cols;
+        get_rows_csr(rows, &offsets, &cols);
+        std::vector<std::vector<Column>> out(rows.size());
+        for (size_t i = 0; i < rows.size(); ++i) out[i].assign(cols.begin() + offsets[i], cols.begin() + offsets[i + 1]);
+        return out;
+    }
+
+    // CSR form: offsets[rows.size()+1], cols in the reference's per-row order
+    void get_rows_csr(const std::vector<Row> &rows, std::vector<uint64_t> *offsets,
+                      std::vector<uint32_t> *cols) const {
+        if (!ctx_) {
+            if (!rows.empty()) throw std::out_of_range("get_row on an empty BRWT");
+            offsets->assign(1, 0);
+            cols->clear();
+            return;
+        }
+        offsets->assign(rows.size() + 1, 0);
+        uint64_t cap = std::max<uint64_t>(16, 16 * rows.size()), need = 0;
+        for (;;) {
+            cols->resize(cap);
+            int st = mbrwt_get_rows(ctx_.get(), rows.data(), rows.size(), offsets->data(), cols->data(), cap, &need);
+            if (st == MBRWT_ERR_CAPACITY) {
+                cap = need;
+                continue;
+            }
+            check_status(st, "BRWTDevice::get_rows");
+            cols->resize(need);
+            return;
+        }
+    }
+
+    mbrwt_ctx *handle() const { return ctx_.get(); }
+
+  private:
+    struct Deleter {
+        void operator()(mbrwt_ctx *c) const { mbrwt_destroy(c); }
+    };
+    std::shared_ptr<mbrwt_ctx> ctx_{nullptr, Deleter()};
+
+  public:
+    BRWTDevice(const BRWTDevice &) = default;
+    BRWTDevice &operator=(const BRWTDevice &) = default;
+};
+
+}  // namespace mbrwt_host

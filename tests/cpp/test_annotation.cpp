@@ -1,0 +1,122 @@
+// Known-answer tests of tests/test_annotation_BRWT.cpp (reference) through
+// the C++ mirror StaticBinRelAnnotator, on the backend named by argv[1]:
+//   oracle  -- the CPU restatement (runs without a GPU)
+//   device  -- BRWTDevice, every query through include/mbrwt.h on the GPU
+#include <set>
+
+#include "backends.hpp"
+#include "minitest.hpp"
+
+using mbrwt_host::StaticBinRelAnnotator;
+typedef std::vector<std::string> VS;
+typedef std::vector<std::pair<std::string, size_t>> VectorCounts;
+
+static bool g_device = false;
+
+static std::set<std::string> S(const VS &v) { return std::set<std::string>(v.begin(), v.end()); }
+static std::set<std::pair<std::string, size_t>> SC(const VectorCounts &v) { return {v.begin(), v.end()}; }
+
+// convert_to_simple_BRWT (annotation_converters.cpp:76-86, grouping arity 2)
+static std::shared_ptr<StaticBinRelAnnotator<BinaryMatrix>> annotator(const LabelFixture &f) {
+    auto om = std::make_shared<OracleMatrix>(build_oracle(f.cols, f.n, 0, 2));
+    std::shared_ptr<const BinaryMatrix> m = om;
+    if (g_device) m = std::make_shared<mbrwt_host::BRWTDevice>(to_device(*om));
+    return std::make_shared<StaticBinRelAnnotator<BinaryMatrix>>(m, f.enc);
+}
+
+TEST(BRWTCompressed, GetLabelsAfterConversion) {  // test_annotation_BRWT.cpp:195-218
+    auto a = annotator(make_fixture(5, {{0, {"Label0", "Label2", "Label8"}}, {2, {"Label1", "Label2"}}, {4, {"Label8"}}}));
+    EXPECT_EQ(S({"Label0", "Label2", "Label8"}), S(a->get_labels(0)));
+    EXPECT_EQ(S({}), S(a->get_labels(1)));
+    EXPECT_EQ(S({"Label1", "Label2"}), S(a->get_labels(2)));
+    EXPECT_EQ(S({}), S(a->get_labels(3)));
+    EXPECT_EQ(S({"Label8"}), S(a->get_labels(4)));
+    EXPECT_EQ(5u, a->num_objects());
+    EXPECT_EQ(4u, a->num_labels());
+    EXPECT_EQ(6u, a->num_relations());
+}
+
+TEST(BRWTCompressed, has_labels) {  // test_annotation_BRWT.cpp:250-300
+    auto a = annotator(make_fixture(5, {{0, {"Label0", "Label2", "Label8"}}, {2, {"Label1", "Label2"}}, {4, {"Label8"}}}));
+    EXPECT_FALSE(a->has_labels(0, {"Label0", "Label1", "Label2", "Label4", "Label5", "Label8"}));
+    EXPECT_FALSE(a->has_labels(0, {"Label0", "Label2", "Label4", "Label8"}));
+    EXPECT_TRUE(a->has_labels(0, {"Label0", "Label2", "Label8"}));
+    EXPECT_TRUE(a->has_labels(0, {"Label0", "Label8"}));
+    EXPECT_TRUE(a->has_labels(0, {"Label2"}));
+    EXPECT_TRUE(a->has_labels(0, {}));
+    EXPECT_FALSE(a->has_labels(1, {"Label0", "Label1", "Label2", "Label4", "Label5", "Label8"}));
+    EXPECT_FALSE(a->has_labels(1, {"Label0", "Label2", "Label4", "Label8"}));
+    EXPECT_FALSE(a->has_labels(1, {"Label0", "Label2", "Label8"}));
+    EXPECT_FALSE(a->has_labels(1, {"Label0", "Label8"}));
+    EXPECT_FALSE(a->has_labels(1, {"Label2"}));
+    EXPECT_TRUE(a->has_labels(1, {}));
+    EXPECT_FALSE(a->has_labels(2, {"Label0", "Label1", "Label2", "Label4", "Label5", "Label8"}));
+    EXPECT_FALSE(a->has_labels(2, {"Label0", "Label2", "Label4", "Label8"}));
+    EXPECT_FALSE(a->has_labels(2, {"Label1", "Label2", "Label8"}));
+    EXPECT_FALSE(a->has_labels(2, {"Label1", "Label8"}));
+    EXPECT_TRUE(a->has_labels(2, {"Label1", "Label2"}));
+    EXPECT_TRUE(a->has_labels(2, {"Label2"}));
+    EXPECT_TRUE(a->has_labels(2, {}));
+    // has_label (annotate_static.cpp:26-33): unknown labels are false
+    EXPECT_TRUE(a->has_label(0, "Label8"));
+    EXPECT_FALSE(a->has_label(1, "Label8"));
+    EXPECT_FALSE(a->has_label(0, "NoSuchLabel"));
+}
+
+TEST(BRWTCompressed, get_top_labels) {  // test_annotation_BRWT.cpp:344-398
+    auto a = annotator(make_fixture(5, {{0, {"Label0", "Label2", "Label8"}},
+                                        {2, {"Label1", "Label2"}},
+                                        {3, {"Label1", "Label2", "Label8"}},
+                                        {4, {"Label2", "Label8"}}}));
+    EXPECT_EQ(VectorCounts({}), a->get_top_labels({0, 1, 2, 3, 4}, 0));
+    EXPECT_EQ(VectorCounts({}), a->get_top_labels({}));
+    EXPECT_EQ(VectorCounts({{"Label2", 4}, {"Label8", 3}, {"Label1", 2}, {"Label0", 1}}),
+              a->get_top_labels({0, 1, 2, 3, 4}));
+    EXPECT_EQ(SC(VectorCounts({{"Label1", 1}, {"Label2", 1}})), SC(a->get_top_labels({2})));
+    EXPECT_EQ(VectorCounts({{"Label2", 4}}), a->get_top_labels({0, 1, 2, 3, 4}, 1));
+    EXPECT_EQ(VectorCounts({{"Label2", 4}, {"Label8", 3}}), a->get_top_labels({0, 1, 2, 3, 4}, 2));
+    EXPECT_EQ(VectorCounts({{"Label2", 4}, {"Label8", 3}, {"Label1", 2}}), a->get_top_labels({0, 1, 2, 3, 4}, 3));
+    EXPECT_EQ(VectorCounts({{"Label2", 4}, {"Label8", 3}, {"Label1", 2}, {"Label0", 1}}),
+              a->get_top_labels({0, 1, 2, 3, 4}, 4));
+    EXPECT_EQ(VectorCounts({{"Label2", 4}, {"Label8", 3}, {"Label1", 2}, {"Label0", 1}}),
+              a->get_top_labels({0, 1, 2, 3, 4}, 1000));
+}
+
+TEST(BRWTCompressed, get_labels_presence_ratio) {  // test_annotation_BRWT.cpp:400-470
+    auto a = annotator(make_fixture(5, {{0, {"Label0", "Label2", "Label8"}},
+                                        {2, {"Label1", "Label2"}},
+                                        {3, {"Label1", "Label2", "Label8"}},
+                                        {4, {"Label2"}}}));
+    EXPECT_EQ(VS({}), a->get_labels(std::vector<uint64_t>{}, 1));
+    EXPECT_EQ(S({"Label1", "Label2"}), S(a->get_labels({2}, 1)));
+    EXPECT_EQ(S({"Label1", "Label2"}), S(a->get_labels({2}, 0)));
+    EXPECT_EQ(S({"Label1", "Label2"}), S(a->get_labels({2}, 0.5)));
+    EXPECT_EQ(S({"Label2"}), S(a->get_labels({2, 4}, 1)));
+    EXPECT_EQ(S({"Label1", "Label2"}), S(a->get_labels({2, 4}, 0)));
+    EXPECT_EQ(S({"Label1", "Label2"}), S(a->get_labels({2, 4}, 0.5)));
+    EXPECT_EQ(S({"Label2"}), S(a->get_labels({2, 4}, 0.501)));
+    EXPECT_EQ(S({}), S(a->get_labels({0, 1, 2, 3, 4}, 1)));
+    EXPECT_EQ(S({"Label0", "Label1", "Label2", "Label8"}), S(a->get_labels({0, 1, 2, 3, 4}, 0)));
+    EXPECT_EQ(S({"Label0", "Label1", "Label2", "Label8"}), S(a->get_labels({0, 1, 2, 3, 4}, 0.2)));
+    EXPECT_EQ(S({"Label1", "Label2", "Label8"}), S(a->get_labels({0, 1, 2, 3, 4}, 0.201)));
+    EXPECT_EQ(S({"Label1", "Label2", "Label8"}), S(a->get_labels({0, 1, 2, 3, 4}, 0.4)));
+    EXPECT_EQ(S({"Label2"}), S(a->get_labels({0, 1, 2, 3, 4}, 0.401)));
+    EXPECT_EQ(S({"Label2"}), S(a->get_labels({0, 1, 2, 3, 4}, 0.8)));
+    EXPECT_EQ(S({}), S(a->get_labels({0, 1, 2, 3, 4}, 0.801)));
+}
+
+TEST(LabelEncoder, encode_decode) {  // annotate.cpp:12-31, annotate.hpp:128
+    mbrwt_host::LabelEncoder<std::string> e;
+    EXPECT_EQ(0u, e.insert_and_encode("a"));
+    EXPECT_EQ(1u, e.insert_and_encode("b"));
+    EXPECT_EQ(0u, e.insert_and_encode("a"));
+    EXPECT_EQ(1u, e.encode("b"));
+    EXPECT_EQ(std::string("a"), e.decode(0));
+    EXPECT_THROW(e.encode("c"), std::runtime_error);
+    EXPECT_THROW(e.decode(5), std::out_of_range);
+}
+
+int main(int argc, char **argv) {
+    g_device = argc > 1 && std::string(argv[1]) == "device";
+    return minitest::run_all(argc > 2 ? argv[2] : nullptr);
+}

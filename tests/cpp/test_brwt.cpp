@@ -1,0 +1,90 @@
+// Grid tests of tests/test_BRWT.cpp:92-212 and tests/test_BRWT_optimizer.cpp
+// (reference) through the C++ mirror's BinaryMatrix interface, on the
+// backend named by argv[1] (oracle | device).
+#include <set>
+
+#include "backends.hpp"
+#include "minitest.hpp"
+
+static bool g_device = false;
+
+typedef std::vector<std::vector<bool>> Columns;
+
+static std::shared_ptr<BinaryMatrix> build(const Columns &cols, uint64_t n, uint64_t relax = 0) {
+    auto om = std::make_shared<OracleMatrix>(build_oracle(cols, n, 0, 2, relax));
+    if (!g_device) return om;
+    return std::make_shared<mbrwt_host::BRWTDevice>(to_device(*om));
+}
+
+// test_brwt (test_BRWT.cpp:92-150) minus get_column (not on the device path)
+static void test_brwt(const BinaryMatrix &m, const Columns &columns, uint64_t n) {
+    ASSERT_EQ(columns.size(), m.num_columns());
+    if (columns.empty()) {
+        ASSERT_EQ(0u, m.num_rows());
+        return;
+    }
+    ASSERT_EQ(n, m.num_rows());
+    std::vector<uint64_t> all(n);
+    for (uint64_t i = 0; i < n; ++i) all[i] = i;
+    auto rows = m.get_rows(all);
+    for (uint64_t i = 0; i < n; ++i) {
+        auto &r = rows[i];
+        std::set<uint64_t> s(r.begin(), r.end());
+        ASSERT_EQ(r.size(), s.size());  // unique
+        for (auto j : r) {
+            ASSERT_TRUE(j < m.num_columns());
+            EXPECT_TRUE(columns[j][i]);
+        }
+        for (size_t j = 0; j < columns.size(); ++j) EXPECT_EQ((bool)columns[j][i], (bool)s.count(j));
+        EXPECT_EQ(r, m.get_row(i));  // batched == single
+    }
+    for (uint64_t i = 0; i < n; ++i)
+        for (size_t j = 0; j < columns.size(); ++j) EXPECT_EQ((bool)columns[j][i], m.get(i, j));
+}
+
+static void grid(int kind, uint64_t relax) {
+    for (uint64_t n = 1; n < 20; ++n) {
+        for (size_t mcols = 1; mcols < 20; ++mcols) {
+            Columns cols(mcols, std::vector<bool>(n));
+            uint64_t ones = 0;
+            for (size_t j = 0; j < mcols; ++j)
+                for (uint64_t i = 0; i < n; ++i) {
+                    bool b = kind == 0 ? false : kind == 1 ? true : ((i + 2 * j) % 2) != 0;  // test_BRWT.cpp:200
+                    cols[j][i] = b;
+                    ones += b;
+                }
+            auto m = build(cols, n, relax);
+            EXPECT_EQ(ones, m->num_relations());
+            test_brwt(*m, cols, n);
+        }
+    }
+}
+
+TEST(BRWT, EmptyConstructor) {  // test_BRWT.cpp:15-25
+    auto m = build({}, 0);
+    EXPECT_EQ(0u, m->num_columns());
+    EXPECT_EQ(0u, m->num_rows());
+    EXPECT_THROW(m->get_row(0), std::out_of_range);
+}
+TEST(BRWT, BuildBottomUPOneColumn) {  // test_BRWT.cpp:27-35
+    auto m = build({std::vector<bool>(10, true)}, 10);
+    EXPECT_EQ(1u, m->num_columns());
+    EXPECT_EQ(10u, m->num_rows());
+    EXPECT_EQ(std::vector<uint64_t>({0}), m->get_row(3));
+}
+TEST(BRWT, OutOfRange) {  // the reference asserts (BRWT.cpp:27); the mirror throws
+    auto m = build({std::vector<bool>(10, true)}, 10);
+    EXPECT_THROW(m->get_row(10), std::out_of_range);
+    EXPECT_THROW(m->get(0, 1), std::out_of_range);
+}
+TEST(BRWT, BuildBottomUPAllZero) { grid(0, 0); }
+TEST(BRWT, BuildBottomUPAllOne) { grid(1, 0); }
+TEST(BRWT, BuildBottomUPAllMixed) { grid(2, 0); }
+TEST(BRWTOptimizer, BuildBottomUPAllZero) { grid(0, UINT64_MAX); }
+TEST(BRWTOptimizer, BuildBottomUPAllOne) { grid(1, UINT64_MAX); }
+TEST(BRWTOptimizer, BuildBottomUPAllMixed) { grid(2, UINT64_MAX); }
+
+int main(int argc, char **argv) {
+    g_device = argc > 1 && std::string(argv[1]) == "device";
+    return minitest::run_all(argc > 2 ? argv[2] : nullptr);
+}

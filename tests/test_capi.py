@@ -1,0 +1,58 @@
+"""The drop-in boundary: libmbrwt.so loads and exports every symbol that
+include/mbrwt.h declares; status strings and no-GPU error paths."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "mbrwt.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mbrwt_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from genome_graph_annotation_amd import _lib as L
+    lib = L.lib()
+    names = declared_functions()
+    assert len(names) >= 18
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in L.SIGNATURES, f"{n} missing from the ctypes binding"
+
+
+def test_status_strings_and_options():
+    from genome_graph_annotation_amd import _lib as L
+    lib = L.lib()
+    for st in range(7):
+        assert lib.mbrwt_strerror(st)
+    assert lib.mbrwt_strerror(99) == b"unknown status"
+    src = open(os.path.join(ROOT, "include", "mbrwt.h")).read()
+    for name, val in re.findall(r"#define (MBRWT_\w+) (\d+)", src):
+        assert getattr(L, name) == int(val), name
+
+
+def test_null_arguments_fail_cleanly():
+    from genome_graph_annotation_amd import _lib as L
+    lib = L.lib()
+    out = C.c_void_p()
+    assert lib.mbrwt_create(None, 0, C.byref(out)) == L.MBRWT_ERR_INVALID
+    assert lib.mbrwt_create_synthetic(None, 0, C.byref(out)) == L.MBRWT_ERR_INVALID
+    assert lib.mbrwt_get_rows(None, None, 0, None, None, 0, None) == L.MBRWT_ERR_INVALID
+    assert lib.mbrwt_set_option(None, 1, 1) == L.MBRWT_ERR_INVALID
+    assert lib.mbrwt_num_rows(None) == 0
+    lib.mbrwt_destroy(None)
+
+
+def test_no_device_is_reported_not_faked():
+    """Without a GPU the engine refuses to build a structure (there is no CPU fallback)."""
+    from conftest import gpu_available
+    if gpu_available():
+        pytest.skip("a GPU is present")
+    from genome_graph_annotation_amd import BRWTDevice, MBRWTError
+    with pytest.raises(MBRWTError):
+        BRWTDevice.synthetic(1000, 10, 0.1, 2, 1)

@@ -1,0 +1,72 @@
+"""Multi-process (world_size 2, gloo on CPU) coverage of the N>1 path:
+batch sharding + the all-gatherv reassembly of per-rank CSR slices
+(genome_graph_annotation_amd/dist.py; on GPUs the same code runs over RCCL).
+Each rank's slice is computed by the oracle here (no GPU in this container)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_batch, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle as O
+        from genome_graph_annotation_amd.dist import allgatherv_csr, shard_bounds
+        t = O.OracleTree.topdown(50_000, 300, 0.01, 8, 3)
+        rows = np.random.default_rng(9).integers(0, 50_000, n_batch, dtype=np.uint64)
+        lo, hi = shard_bounds(n_batch, world, rank)
+        off, cols = t.get_rows(rows[lo:hi])
+        g_off, g_cols = allgatherv_csr(torch.from_numpy(off.view(np.int64)),
+                                       torch.from_numpy(cols.view(np.int32)))
+        ref_off, ref_cols = t.get_rows(rows)
+        ok = np.array_equal(g_off.numpy().view(np.uint64), ref_off) and \
+            np.array_equal(g_cols.numpy().view(np.uint32), ref_cols)
+        q.put((rank, ok, int(hi - lo)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_batch", [(2, 10_001), (2, 1), (3, 7)])
+def test_allgatherv_reassembles_global_csr(world, n_batch):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_batch, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res)
+    assert sum(k for _, _, k in res) == n_batch
+
+
+def test_shard_bounds_cover_batch():
+    from genome_graph_annotation_amd.dist import shard_bounds
+    for n in (0, 1, 7, 8, 1000, 8_000_001):
+        for w in (1, 2, 3, 8):
+            spans = [shard_bounds(n, w, r) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+            assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
