@@ -180,8 +180,43 @@ int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
         }
         tree.max_arity = std::max<uint32_t>(tree.max_arity, desc.num_children[u]);
     }
-    // super-root: its single child is the root
-    {
+    // super-root: its single child is the root -- or, when the root column is
+    // at least half full, the root's children expanded to row positions
+    // (root folding, mbrwt_internal.hpp)
+    tree.folded = fold_root_enabled() && desc.num_children[0] > 0 && 2 * ones[0] >= desc.num_rows;
+    if (tree.folded) {
+        const uint32_t a = desc.num_children[0], fc = desc.first_child[0];
+        const uint64_t n = desc.num_rows, W = (n + 63) / 64;
+        std::vector<std::vector<uint64_t>> expanded(a, std::vector<uint64_t>(W, 0));
+        std::vector<const uint64_t *> cw(a);
+        std::vector<bool> leaf(a);
+        const uint64_t *root = desc.vec_words[0];
+        uint64_t jpos = 0;
+        for (uint64_t k = 0; k < W; ++k) {
+            uint64_t x = root[k];
+            if (k == W - 1 && (n & 63)) x &= (1ull << (n & 63)) - 1;
+            while (x) {
+                const uint64_t r = k * 64 + (uint64_t)__builtin_ctzll(x);
+                x &= x - 1;
+                for (uint32_t c = 0; c < a; ++c)
+                    if ((desc.vec_words[fc + c][jpos >> 6] >> (jpos & 63)) & 1) expanded[c][r >> 6] |= 1ull << (r & 63);
+                ++jpos;
+            }
+        }
+        for (uint32_t c = 0; c < a; ++c) {
+            cw[c] = expanded[c].data();
+            leaf[c] = desc.num_children[fc + c] == 0;
+        }
+        DevNode &sr = tree.nodes[0];
+        sr.first_child = fc + 1;
+        sr.label = UINT32_MAX;
+        int rc = upload_image(cw, leaf, n, sr, tree.images, tree.image_bytes);
+        if (rc) return rc;
+        DevNode &rt = tree.nodes[1];  // absorbed: never visited
+        rt.kind = KIND_FOLDED;
+        rt.arity = 0;
+        rt.first_child = 0;
+    } else {
         DevNode &sr = tree.nodes[0];
         sr.first_child = 1;
         sr.label = UINT32_MAX;
@@ -191,7 +226,7 @@ int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
     }
     for (uint32_t u = 0; u < N; ++u) {
         const uint32_t a = desc.num_children[u];
-        if (!a) continue;
+        if (!a || (u == 0 && tree.folded)) continue;
         std::vector<const uint64_t *> cw(a);
         std::vector<bool> leaf(a);
         for (uint32_t c = 0; c < a; ++c) {
@@ -224,7 +259,7 @@ int finalize_tree(Tree &tree) {
     uint32_t max_depth = 0;
     for (uint32_t v = 0; v < D; ++v) {
         const DevNode &dn = tree.nodes[v];
-        if (dn.kind == KIND_LEAF) continue;
+        if (dn.kind == KIND_LEAF || dn.kind == KIND_FOLDED) continue;
         for (uint32_t c = 0; c < dn.arity; ++c) {
             uint32_t w = dn.first_child + c;
             parent[w] = v;

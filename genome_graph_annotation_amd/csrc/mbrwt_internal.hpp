@@ -17,11 +17,17 @@
 //                    1/2/4/8 bytes wide; leaves need no rank.
 //   * Leaves have no image; their global column (RangePartition::get composed
 //     along the path, utils.cpp:689-691) is in DevNode::label.
+//   * Root folding: when the root's index column is at least half full, the
+//     super-root stores the root's CHILDREN interleaved over row positions
+//     (a child bit is 0 where the root bit is 0), so get_row starts one level
+//     lower: rank1(root, row) is never needed because rank1 of every child
+//     over the row-indexed image equals its rank over the root's positions.
 #pragma once
 
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -37,6 +43,7 @@ enum : uint8_t {
     KIND_MASK16 = 3,
     KIND_MASK32 = 4,
     KIND_MASK64 = 5,
+    KIND_FOLDED = 6,  // the BRWT root when folded into the super-root (never visited)
 };
 enum : uint8_t { FLAG_CONSEC_LABELS = 1 };
 
@@ -96,6 +103,7 @@ struct Tree {
     std::vector<uint32_t> col_leaf;         // dnode of the leaf holding each column
     uint32_t path_len = 0;                  // max_depth stride of col_path
     uint32_t stack_depth = 0;               // max KIND_PLANE dnodes on a root path (incl. super)
+    bool folded = false;                    // root folded into the super-root
     uint32_t max_arity = 0;
     uint64_t num_rows = 0, num_columns = 0, num_relations = 0, num_nodes = 0;
     uint64_t image_bytes = 0;
@@ -150,6 +158,12 @@ int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStr
 void free_tree(Tree &tree);
 // finish a Tree whose nodes/images are set: column paths, stack depth
 int finalize_tree(Tree &tree);
+
+// root folding is on unless MBRWT_FOLD_ROOT=0 (A/B measurement switch)
+inline bool fold_root_enabled() {
+    const char *e = std::getenv("MBRWT_FOLD_ROOT");
+    return !(e && e[0] == '0');
+}
 
 // queries (query.hip)
 int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,

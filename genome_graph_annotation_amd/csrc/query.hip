@@ -67,6 +67,7 @@ struct TravParams {
     unsigned long long *label_counts;  // MODE_COUNT: [num_columns]
     const CNode *cnodes;         // compact node records (group kernel)
     uint32_t n_lds;              // records [0, n_lds) are staged in LDS
+    uint32_t folded;             // root folded into the super-root (V accounting)
 };
 
 // decoded node record
@@ -254,6 +255,10 @@ __global__ __launch_bounds__(256) void k_traverse(TravParams p) {
             return;
         }
         enter<MAXD, MaskT, MODE>(p, st, sk, 0u, (uint32_t)row);
+        if constexpr (MODE == MODE_WORK) {
+            // folded root: its own probe counts once, its children's only if its bit is set
+            if (p.folded) sk.visits = sk.visits + 1 - ((st.sp == 0 && sk.cnt == 0) ? (uint64_t)gld(p.nodes).arity : 0ull);
+        }
     };
     auto end_row = [&]() {
         if constexpr (MODE == MODE_SLOTS) {
@@ -509,6 +514,10 @@ __global__ __launch_bounds__(256, WPE) void k_traverse_group(TravParams p, uint3
         }
         const NodeInfo nd = node_info(0);
         group_visit<MAXD, CPL, MaskT, MODE>(p, st, sk, nd, (uint32_t)row, c, gbase, gmask, G);
+        if constexpr (MODE == MODE_WORK) {
+            // folded root: its own probe counts once, its children's only if its bit is set
+            if (p.folded) sk.visits = sk.visits + 1 - ((st.sp == 0 && sk.cnt == 0) ? (uint64_t)nd.arity : 0ull);
+        }
     };
     auto end_row = [&]() {
         sk.flush(p, c, G);
@@ -749,6 +758,7 @@ TravParams base_params(const Ctx &c) {
     p.nodes = c.d_nodes;
     p.cnodes = c.d_cnodes;
     p.n_lds = (uint32_t)std::min<size_t>(c.tree.nodes.size(), kLdsNodes);
+    p.folded = c.tree.folded ? 1u : 0u;
     p.num_rows = c.tree.num_rows;
     p.scalars = reinterpret_cast<unsigned long long *>(c.d_scalars);
     return p;

@@ -156,6 +156,63 @@ __global__ __launch_bounds__(256) void k_gen_mask(W *img, uint64_t L, uint64_t K
     if ((threadIdx.x & 63) == 0 && local) atomicAdd(ones, (unsigned long long)local);
 }
 
+// root folding: the super-root image holds the root's children over ROW
+// positions.  The root's own column (a temporary plane, ranks scanned) gives
+// the root position j of every set row; the mask drawn at (root, j) is the
+// same draw as in the unfolded image, so the structure is identical.
+template <int A>
+__global__ __launch_bounds__(256) void k_gen_fold_plane(uint8_t *img, uint64_t n, const uint8_t *root_img,
+                                                        uint64_t K, const uint64_t *__restrict__ Tg, uint32_t nT,
+                                                        uint32_t stride) {
+    __shared__ uint64_t T[(1 << A) - 1];
+    for (uint32_t i = threadIdx.x; i < nT; i += blockDim.x) T[i] = Tg[i];
+    __syncthreads();
+    const uint64_t nb = (n + 31) / 32;
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gs) {
+        const uint2 rb = *reinterpret_cast<const uint2 *>(root_img + b * 16);
+        uint32_t bits[A];
+#pragma unroll
+        for (int c = 0; c < A; ++c) bits[c] = 0;
+        uint32_t x = rb.y;
+        while (x) {
+            const uint32_t t = __builtin_ctz(x);
+            x &= x - 1;
+            const uint64_t j = rb.x + __builtin_popcount(rb.y & ((1u << t) - 1u));
+            const uint32_t m = draw_mask(T, nT, draw(K, j));
+#pragma unroll
+            for (int c = 0; c < A; ++c) bits[c] |= ((m >> c) & 1u) << t;
+        }
+        uint8_t *blk = img + b * stride;
+#pragma unroll
+        for (int c = 0; c < A; ++c) *reinterpret_cast<uint2 *>(blk + 8 * c) = make_uint2(0u, bits[c]);
+    }
+}
+
+template <typename W, int A>
+__global__ __launch_bounds__(256) void k_gen_fold_mask(W *img, uint64_t n, const uint8_t *root_img, uint64_t K,
+                                                       const uint64_t *__restrict__ Tg, uint32_t nT,
+                                                       unsigned long long *ones) {
+    __shared__ uint64_t T[(1 << A) - 1];
+    for (uint32_t i = threadIdx.x; i < nT; i += blockDim.x) T[i] = Tg[i];
+    __syncthreads();
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t local = 0;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gs) {
+        const uint2 rb = *reinterpret_cast<const uint2 *>(root_img + (r >> 5) * 16);
+        const uint32_t t = r & 31;
+        uint32_t m = 0;
+        if ((rb.y >> t) & 1u) {
+            const uint64_t j = rb.x + __builtin_popcount(rb.y & ((1u << t) - 1u));
+            m = draw_mask(T, nT, draw(K, j));
+        }
+        img[r] = (W)m;
+        local += (uint64_t)__builtin_popcount(m);
+    }
+    for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off);
+    if ((threadIdx.x & 63) == 0 && local) atomicAdd(ones, (unsigned long long)local);
+}
+
 // ---- per-child rank scan over the blocks of a KIND_PLANE image ----------
 constexpr int kScanTile = 256;  // blocks per tile (one thread per block)
 
@@ -307,6 +364,36 @@ void launch_mask(uint8_t *img, uint64_t L, uint64_t K, const uint64_t *T, uint32
                        T, nT, ones);
 }
 
+template <int A>
+void launch_fold_plane(uint8_t *img, uint64_t n, const uint8_t *root, uint64_t K, const uint64_t *T, uint32_t nT,
+                       uint32_t stride, unsigned long long *, hipStream_t s) {
+    hipLaunchKernelGGL(k_gen_fold_plane<A>, dim3(launch_grid((n + 31) / 32)), dim3(256), 0, s, img, n, root, K, T,
+                       nT, stride);
+}
+template <typename W, int A>
+void launch_fold_mask(uint8_t *img, uint64_t n, const uint8_t *root, uint64_t K, const uint64_t *T, uint32_t nT,
+                      uint32_t, unsigned long long *ones, hipStream_t s) {
+    hipLaunchKernelGGL((k_gen_fold_mask<W, A>), dim3(launch_grid(n)), dim3(256), 0, s, reinterpret_cast<W *>(img), n,
+                       root, K, T, nT, ones);
+}
+using FoldFn = void (*)(uint8_t *, uint64_t, const uint8_t *, uint64_t, const uint64_t *, uint32_t, uint32_t,
+                        unsigned long long *, hipStream_t);
+FoldFn fold_fn(uint32_t a, bool plane) {
+    static const FoldFn tp[] = {nullptr, launch_fold_plane<1>, launch_fold_plane<2>, launch_fold_plane<3>,
+                                launch_fold_plane<4>, launch_fold_plane<5>, launch_fold_plane<6>,
+                                launch_fold_plane<7>, launch_fold_plane<8>, launch_fold_plane<9>,
+                                launch_fold_plane<10>, launch_fold_plane<11>, launch_fold_plane<12>};
+    static const FoldFn tm[] = {nullptr,
+                                launch_fold_mask<uint8_t, 1>,   launch_fold_mask<uint8_t, 2>,
+                                launch_fold_mask<uint8_t, 3>,   launch_fold_mask<uint8_t, 4>,
+                                launch_fold_mask<uint8_t, 5>,   launch_fold_mask<uint8_t, 6>,
+                                launch_fold_mask<uint8_t, 7>,   launch_fold_mask<uint8_t, 8>,
+                                launch_fold_mask<uint16_t, 9>,  launch_fold_mask<uint16_t, 10>,
+                                launch_fold_mask<uint16_t, 11>, launch_fold_mask<uint16_t, 12>};
+    if (a > kSynthMaxArity) return nullptr;
+    return plane ? tp[a] : tm[a];
+}
+
 using PlaneFn = void (*)(uint8_t *, uint64_t, uint64_t, const uint64_t *, uint32_t, uint32_t, hipStream_t);
 using MaskFn = void (*)(uint8_t *, uint64_t, uint64_t, const uint64_t *, uint32_t, unsigned long long *, hipStream_t);
 
@@ -449,13 +536,58 @@ int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStr
             if ((rc = plane_scan(img, n, 1, sr.stride, tot, s))) return fail(rc, "root scan");
             // tot[0] = popcount of the root column = length of the root's children columns
             tree.nodes[1].length = tot[0];
+            if (fold_root_enabled() && 2 * tot[0] >= n) {
+                // fold the root into the super-root (mbrwt_internal.hpp): the
+                // root plane above becomes a temporary input
+                DevNode &rt = tree.nodes[1];
+                const uint32_t a = rt.arity, nT = (1u << a) - 1;
+                const bool plane = rt.kind == KIND_PLANE;
+                void *tmp = tree.images.back();
+                const uint64_t tmp_bytes = ((n + 31) / 32) * sr.stride + kImagePad;
+                tree.images.pop_back();
+                tree.image_bytes -= tmp_bytes;
+                sr.kind = rt.kind;
+                sr.arity = rt.arity;
+                sr.stride = rt.stride;
+                sr.first_child = rt.first_child;
+                uint8_t *fimg = alloc_image(sr, plane ? ((n + 31) / 32) * sr.stride : n * mask_bytes(sr.kind));
+                if (!fimg) {
+                    (void)hipFree(tmp);
+                    return fail(MBRWT_ERR_NOMEM, "device allocation failed");
+                }
+                fold_fn(a, plane)(fimg, n, reinterpret_cast<const uint8_t *>(tmp), node_key(desc.seed, 0), node_T[0],
+                                  nT, sr.stride, d_ones, s);
+                if (hipGetLastError() != hipSuccess) {
+                    (void)hipFree(tmp);
+                    return fail(MBRWT_ERR_DEVICE, "fold kernel");
+                }
+                if (plane) {
+                    std::vector<uint64_t> ftot;
+                    if ((rc = plane_scan(fimg, n, a, sr.stride, ftot, s))) {
+                        (void)hipFree(tmp);
+                        return fail(rc, "fold scan");
+                    }
+                    for (uint32_t c = 0; c < a; ++c) {
+                        DevNode &ch = tree.nodes[shape[0].children[c] + 1];
+                        if (ch.kind == KIND_LEAF) tree.num_relations += ftot[c];
+                        else ch.length = ftot[c];
+                    }
+                }
+                MBRWT_HIP(hipStreamSynchronize(s));
+                (void)hipFree(tmp);
+                rt.kind = KIND_FOLDED;
+                rt.arity = 0;
+                rt.first_child = 0;
+                rt.base = 0;
+                tree.folded = true;
+            }
         }
     }
     // internal nodes in BFS order: parents are generated before children
     for (uint32_t u = 0; u < N; ++u) {
         const auto &sh = shape[u];
         DevNode &dn = tree.nodes[u + 1];
-        if (sh.children.empty()) continue;
+        if (sh.children.empty() || dn.kind == KIND_FOLDED) continue;
         const uint64_t L = dn.length;  // positions = popcount of u's own column
         const uint64_t K = node_key(desc.seed, u);
         const uint32_t a = dn.arity, nT = (1u << a) - 1;

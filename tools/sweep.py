@@ -21,10 +21,16 @@ ap.add_argument("--batch", type=int, default=8_000_000)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--variants", default="1,2,3,4")
 ap.add_argument("--presort", action="store_true", help="sort the batch on the host (locality experiment)")
+ap.add_argument("--fold", default="1", help="root folding settings to build, e.g. 0,1")
 a = ap.parse_args()
-t0 = time.time()
-m = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, 42)
-print(f"built {m.device_bytes() / 1e9:.1f} GB in {time.time() - t0:.1f}s", flush=True)
+ap2 = a
+mats = {}
+for fold in a.fold.split(","):
+    os.environ["MBRWT_FOLD_ROOT"] = fold
+    t0 = time.time()
+    mats[fold] = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, 42)
+    print(f"built fold={fold} {mats[fold].device_bytes() / 1e9:.1f} GB in {time.time() - t0:.1f}s", flush=True)
+m = next(iter(mats.values()))
 rows_np = np.random.default_rng(42).integers(0, a.rows, a.batch, dtype=np.uint64)
 if a.presort:
     rows_np = np.sort(rows_np)
@@ -38,8 +44,9 @@ variants = [int(x) for x in a.variants.split(",")]
 sorts = [0]
 res = {}
 for rep in range(a.reps):
+  for fold, m in mats.items():
     for var in variants:
-        for so in sorts:
+        for so in [fold]:
             m.set_option(L.MBRWT_OPT_KERNEL, var)
             m.get_rows_device(rows, off, cols, s)
             m.take_timing()
@@ -56,5 +63,5 @@ for rep in range(a.reps):
 for (var, so), xs in sorted(res.items()):
     kms = np.median([x[0] for x in xs])
     wms = np.median([x[1] for x in xs])
-    print(f"variant {var} sort {so}: kernel {kms:.3f} ms  step {wms:.3f} ms  -> {a.batch / wms * 1e3 / 1e6:.1f} M rows/s, "
+    print(f"variant {var} fold {so}: kernel {kms:.3f} ms  step {wms:.3f} ms  -> {a.batch / wms * 1e3 / 1e6:.1f} M rows/s, "
           f"alg {alg / kms / 1e6:.0f} GB/s")
