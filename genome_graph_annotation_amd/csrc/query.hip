@@ -20,6 +20,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "mbrwt_internal.hpp"
 
@@ -41,7 +42,25 @@ template <class T>
 __device__ __forceinline__ T gld_at(uint64_t addr) { return *(const AS_GLOBAL T *)addr; }
 template <class T>
 __device__ __forceinline__ void gst(T *p, T v) { *(AS_GLOBAL T *)(uintptr_t)p = v; }
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+template <class T, bool NT>
+__device__ __forceinline__ T gld_at_nt(uint64_t addr) {
+    if constexpr (!NT) {
+        return *(const AS_GLOBAL T *)addr;
+    } else if constexpr (sizeof(T) == 16) {
+        const u32x4_t v = __builtin_nontemporal_load((const AS_GLOBAL u32x4_t *)addr);
+        return T{v.x, v.y, v.z, v.w};
+    } else if constexpr (sizeof(T) == 8 && !std::is_integral<T>::value) {
+        const u32x2_t v = __builtin_nontemporal_load((const AS_GLOBAL u32x2_t *)addr);
+        return T{v.x, v.y};
+    } else {
+        return __builtin_nontemporal_load((const AS_GLOBAL T *)addr);
+    }
+}
 #else
+template <class T, bool NT>
+__device__ T gld_at_nt(uint64_t addr) { return *(const T *)addr; }
 template <class T>
 __device__ T gld(const T *p) { return *p; }
 template <class T>
@@ -392,7 +411,7 @@ __device__ __forceinline__ uint64_t spread_bits(uint64_t x, uint32_t G) {
     return r;
 }
 
-template <int MAXD, int CPL, typename MaskT, int MODE>
+template <int MAXD, int CPL, typename MaskT, int MODE, bool NT = false>
 __device__ __forceinline__ void group_visit(const TravParams &p, GroupFrames<MAXD, CPL, MaskT> &st, GroupSink<MODE> &sk,
                                             const NodeInfo &nd, uint32_t j, uint32_t c, uint32_t gbase,
                                             uint64_t gmask, uint32_t G) {
@@ -412,13 +431,13 @@ __device__ __forceinline__ void group_visit(const TravParams &p, GroupFrames<MAX
             const uint64_t blk = base + (uint64_t)(j >> 5) * nd.stride + 8u * CPL * c;
             uint32_t rk[CPL], bw[CPL];
             if constexpr (CPL == 1) {
-                const uint2 rb = gld_at<uint2>(blk);
+                const uint2 rb = gld_at_nt<uint2, NT>(blk);
                 rk[0] = rb.x;
                 bw[0] = rb.y;
             } else {
 #pragma unroll
                 for (int h = 0; h < CPL / 2; ++h) {
-                    const uint4 q4 = gld_at<uint4>(blk + 16 * h);
+                    const uint4 q4 = gld_at_nt<uint4, NT>(blk + 16 * h);
                     rk[2 * h] = q4.x;
                     bw[2 * h] = q4.y;
                     rk[2 * h + 1] = q4.z;
@@ -446,7 +465,7 @@ __device__ __forceinline__ void group_visit(const TravParams &p, GroupFrames<MAX
         return;
     }
     uint64_t m;  // all children are leaves: one mask per position (uniform load)
-    if (nd.kind == KIND_MASK8) m = gld_at<uint8_t>(base + j);
+    if (nd.kind == KIND_MASK8) m = gld_at_nt<uint8_t, NT>(base + j);
     else if (nd.kind == KIND_MASK16) m = gld_at<uint16_t>(base + 2ull * j);
     else if (nd.kind == KIND_MASK32) m = gld_at<uint32_t>(base + 4ull * j);
     else m = gld_at<uint64_t>(base + 8ull * j);
@@ -464,7 +483,7 @@ __device__ __forceinline__ void group_visit(const TravParams &p, GroupFrames<MAX
     sk.cnt += (uint32_t)__builtin_popcountll(m);
 }
 
-template <int MAXD, int CPL, typename MaskT, int MODE, int WPE>
+template <int MAXD, int CPL, typename MaskT, int MODE, int WPE, bool NT = false>
 __global__ __launch_bounds__(256, WPE) void k_traverse_group(TravParams p, uint32_t G) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c = lane & (G - 1);
@@ -513,7 +532,7 @@ __global__ __launch_bounds__(256, WPE) void k_traverse_group(TravParams p, uint3
             return;
         }
         const NodeInfo nd = node_info(0);
-        group_visit<MAXD, CPL, MaskT, MODE>(p, st, sk, nd, (uint32_t)row, c, gbase, gmask, G);
+        group_visit<MAXD, CPL, MaskT, MODE, NT>(p, st, sk, nd, (uint32_t)row, c, gbase, gmask, G);
         if constexpr (MODE == MODE_WORK) {
             // folded root: its own probe counts once, its children's only if its bit is set
             if (p.folded) sk.visits = sk.visits + 1 - ((st.sp == 0 && sk.cnt == 0) ? (uint64_t)nd.arity : 0ull);
@@ -565,7 +584,7 @@ __global__ __launch_bounds__(256, WPE) void k_traverse_group(TravParams p, uint3
                 if (c == 0) sk.put(p, 0, nd.label);
                 sk.cnt += 1;
             } else {
-                group_visit<MAXD, CPL, MaskT, MODE>(p, st, sk, nd, jw, c, gbase, gmask, G);
+                group_visit<MAXD, CPL, MaskT, MODE, NT>(p, st, sk, nd, jw, c, gbase, gmask, G);
             }
         }
     }
@@ -697,7 +716,19 @@ Trav pick_traverse(const Ctx &c) {
     // variants 5/6 request a higher occupancy (waves per SIMD) from the register allocator
     const int v = c.kernel_variant ? c.kernel_variant : 5;  // default: 2 children per lane, 8 waves/SIMD
     const int cpl = v == 2 ? 1 : (v == 4 || v == 6) ? 4 : 2;
-    const int wpe = v == 5 ? 8 : v == 6 ? 6 : 1;
+    const int wpe = (v == 5 || v == 10) ? 8 : v == 6 ? 6 : 1;
+    if (v == 10) {  // variant 5 with non-temporal block/mask reads
+        const uint32_t need = (max_arity + 1) / 2;
+        uint32_t G = 1;
+        while (G < need) G <<= 1;
+        t.G = G;
+        if (depth <= 4) t.group_fn = max_arity <= 32 ? (GroupFn)k_traverse_group<4, 2, uint32_t, MODE, 8, true>
+                                                     : (GroupFn)k_traverse_group<4, 2, uint64_t, MODE, 8, true>;
+        else if (depth <= 8) t.group_fn = max_arity <= 32 ? (GroupFn)k_traverse_group<8, 2, uint32_t, MODE, 8, true>
+                                                          : (GroupFn)k_traverse_group<8, 2, uint64_t, MODE, 8, true>;
+        t.fn = reinterpret_cast<const void *>(t.group_fn);
+        return t;
+    }
     const uint32_t need = (max_arity + cpl - 1) / cpl;
     uint32_t G = 1;
     while (G < need) G <<= 1;
