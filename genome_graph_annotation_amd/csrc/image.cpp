@@ -254,6 +254,18 @@ int finalize_tree(Tree &tree) {
             dn.label = tree.nodes[dn.first_child].label;
         }
     }
+    // shape eligible for the specialised kernel: internal nodes PLANE/MASK8 with
+    // arity <= 8, MASK8 labels consecutive, no leaf directly under a PLANE node
+    tree.fast_shape = true;
+    for (uint32_t v = 0; v < D; ++v) {
+        const DevNode &dn = tree.nodes[v];
+        if (dn.kind == KIND_LEAF || dn.kind == KIND_FOLDED) continue;
+        if (dn.arity > 8 || (dn.kind != KIND_PLANE && dn.kind != KIND_MASK8)) tree.fast_shape = false;
+        if (dn.kind == KIND_MASK8 && !(dn.flags & FLAG_CONSEC_LABELS)) tree.fast_shape = false;
+        if (dn.kind == KIND_PLANE)
+            for (uint32_t c = 0; c < dn.arity; ++c)
+                if (tree.nodes[dn.first_child + c].kind == KIND_LEAF) tree.fast_shape = false;
+    }
     // depth-first walk: stack depth (KIND_PLANE frames) and column paths
     std::vector<uint32_t> parent(D, UINT32_MAX), cidx(D, 0), depth(D, 0), planes(D, 0);
     uint32_t max_depth = 0;
@@ -271,6 +283,7 @@ int finalize_tree(Tree &tree) {
         }
     }
     tree.path_len = std::max<uint32_t>(1, max_depth);
+    if (tree.stack_depth > kFastMaxDepth) tree.fast_shape = false;
     tree.col_path.assign(tree.num_columns * tree.path_len, 0);
     tree.col_leaf.assign(tree.num_columns, 0);
     for (uint32_t v = 0; v < D; ++v) {

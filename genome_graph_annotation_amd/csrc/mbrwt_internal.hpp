@@ -69,6 +69,7 @@ struct alignas(16) CNode {
 };
 static_assert(sizeof(CNode) == 16, "CNode must be 16 bytes");
 constexpr uint32_t kLdsNodes = 512;
+constexpr uint32_t kFastMaxDepth = 4;  // PLANE levels the specialised kernel's stack holds
 
 inline CNode compact(const DevNode &d) {
     uint32_t lg = 0;
@@ -104,6 +105,7 @@ struct Tree {
     uint32_t path_len = 0;                  // max_depth stride of col_path
     uint32_t stack_depth = 0;               // max KIND_PLANE dnodes on a root path (incl. super)
     bool folded = false;                    // root folded into the super-root
+    bool fast_shape = false;                // eligible for k_traverse_fast (finalize_tree)
     uint32_t max_arity = 0;
     uint64_t num_rows = 0, num_columns = 0, num_relations = 0, num_nodes = 0;
     uint64_t image_bytes = 0;

@@ -594,6 +594,181 @@ __global__ __launch_bounds__(256, WPE) void k_traverse_group(TravParams p, uint3
     }
 }
 
+// ------------------------------------------------------------------------
+// k_traverse_fast: the group kernel specialised for the common tree shape
+// (every internal node KIND_PLANE or KIND_MASK8 with arity <= 8, leaves only
+// below MASK8 nodes with consecutive labels, <= 4 PLANE levels -- the basic
+// arity-<=8 partitioner's trees).  Same algorithm as k_traverse_group with
+// G = 4 lanes x 2 children, stripped of every branch the shape rules out:
+// the traversal is issue-bound as much as memory-bound (a cache-resident
+// 1 M-row tree runs only ~25 % faster than the 3.7 B-row one), so each
+// instruction of the per-step path matters.  Each stack level is 3 registers
+// per lane (two child positions + first child << 8 | pending mask); each
+// group preloads the ids of its next 8 rows (2 per lane).
+// ------------------------------------------------------------------------
+constexpr uint32_t kFastMaxd = 4;
+
+template <bool NT>
+__global__ __launch_bounds__(256, 8) void k_traverse_fast(TravParams p) {
+    constexpr uint32_t G = 4;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t c = lane & 3;
+    const uint32_t gbase = lane & ~3u;
+    const uint64_t gid = (uint64_t)blockIdx.x * 64 + threadIdx.x / 4;
+    const uint64_t ngroups = (uint64_t)gridDim.x * 64;
+
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_stage[];  // 64 groups x kStageLabels
+    AS_LDS uint32_t *stage = (AS_LDS uint32_t *)lds_stage + (threadIdx.x / 4) * kStageLabels;
+    AS_LDS uint64_t *lds_nodes = (AS_LDS uint64_t *)((AS_LDS uint32_t *)lds_stage + 64 * kStageLabels);
+    const uint64_t *gnodes = reinterpret_cast<const uint64_t *>(p.cnodes);
+    for (uint32_t i = threadIdx.x; i < 2 * p.n_lds; i += blockDim.x) lds_nodes[i] = gld(gnodes + i);
+    __syncthreads();
+
+    uint32_t jc0[kFastMaxd], jc1[kFastMaxd], fp[kFastMaxd];  // fp = first_child << 8 | pending mask
+#pragma unroll
+    for (int k = 0; k < (int)kFastMaxd; ++k) jc0[k] = jc1[k] = fp[k] = 0;
+    int sp = 0;
+    uint32_t cnt = 0;
+    uint64_t chunk = gid;
+    uint32_t ri = 0;
+    uint64_t slot = chunk * 8;
+
+    // visit node record (w0, w1) at position j
+    auto visit = [&](uint64_t w0, uint64_t w1, uint32_t j) {
+        const uint64_t base = w0 & ((1ull << 48) - 1);
+        const uint32_t kind = (uint32_t)(w0 >> 48) & 7u;
+        const uint32_t a = (uint32_t)(w0 >> 56);
+        if (kind == KIND_PLANE) {
+            const uint32_t stride = 1u << ((uint32_t)(w0 >> 52) & 15u);
+            const uint32_t t = j & 31, below = (1u << t) - 1u;
+            uint32_t b0 = 0, b1 = 0, j0 = 0, j1 = 0;
+            if (2 * c < a) {
+                const uint4 q = gld_at_nt<uint4, NT>(base + (uint64_t)(j >> 5) * stride + 16u * c);
+                b0 = (q.y >> t) & 1u;
+                b1 = (2 * c + 1 < a) ? (q.w >> t) & 1u : 0u;
+                j0 = q.x + (uint32_t)__builtin_popcount(q.y & below);  // rank1(j) - 1 of child 2c
+                j1 = q.z + (uint32_t)__builtin_popcount(q.w & below);  // and of child 2c+1
+            }
+            const uint32_t e = (uint32_t)(__ballot(b0) >> gbase) & 0xFu;
+            const uint32_t o = (uint32_t)(__ballot(b1) >> gbase) & 0xFu;
+            // interleave: child 2i <- e bit i, child 2i+1 <- o bit i
+            const uint32_t P = (e & 1u) | ((e & 2u) << 1) | ((e & 4u) << 2) | ((e & 8u) << 3) | ((o & 1u) << 1) |
+                               ((o & 2u) << 2) | ((o & 4u) << 3) | ((o & 8u) << 4);
+            if (P) {
+                if (sp >= (int)kFastMaxd) {
+                    if (c == 0) atomicOr(&p.scalars[2], 2ull);
+                    return;
+                }
+#pragma unroll
+                for (int k = kFastMaxd - 1; k > 0; --k) {
+                    jc0[k] = jc0[k - 1];
+                    jc1[k] = jc1[k - 1];
+                    fp[k] = fp[k - 1];
+                }
+                jc0[0] = j0;
+                jc1[0] = j1;
+                fp[0] = ((uint32_t)w1 << 8) | P;
+                ++sp;
+            }
+            return;
+        }
+        // KIND_MASK8, consecutive leaf labels
+        const uint32_t m = gld_at_nt<uint8_t, NT>(base + j);
+        const uint32_t l0 = (uint32_t)(w1 >> 32);
+#pragma unroll
+        for (uint32_t q = 0; q < 2; ++q) {
+            const uint32_t cc = 2 * c + q;
+            if ((m >> cc) & 1u) {
+                const uint32_t pos = cnt + (uint32_t)__builtin_popcount(m & ((1u << cc) - 1u));
+                if (pos < kStageLabels) stage[pos] = l0 + cc;
+                else if (pos < p.K) gst(p.temp + slot * p.K + pos, l0 + cc);  // past the LDS stage
+            }
+        }
+        cnt += (uint32_t)__builtin_popcount(m);
+    };
+
+    // rows: each group takes chunks of 8 consecutive slots, ids preloaded 2 per lane
+    uint64_t r0 = 0, r1 = 0;
+    auto load_chunk = [&]() {
+        const uint64_t sb = chunk * 8 + 2 * c;
+        r0 = sb < p.n ? gld(p.rows + sb) : 0;
+        r1 = sb + 1 < p.n ? gld(p.rows + sb + 1) : 0;
+    };
+    bool active = slot < p.n;
+    if (active) load_chunk();
+    auto begin_row = [&]() {
+        const uint64_t mine = (ri & 1) ? r1 : r0;
+        const uint32_t src = gbase + (ri >> 1);
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)mine, (int)src, 64);
+        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(mine >> 32), (int)src, 64);
+        const uint64_t row = ((uint64_t)hi << 32) | lo;
+        cnt = 0;
+        if (row >= p.num_rows) {
+            if (c == 0) atomicOr(&p.scalars[2], 1ull);
+            return;
+        }
+        visit(lds_nodes[0], lds_nodes[1], (uint32_t)row);
+    };
+    auto end_row = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t lim = cnt < kStageLabels ? cnt : kStageLabels;
+        const uint64_t sb = slot * p.K;
+        for (uint32_t pos = c; pos < lim; pos += G) gst(p.temp + sb + pos, (uint32_t)stage[pos]);
+        if (c == 0) {
+            gst(p.counts + slot, cnt);
+            if (cnt > p.K) {
+                const unsigned long long k = atomicAdd(&p.scalars[1], 1ull);
+                gst(p.ovf_list + k, (uint32_t)slot);
+            }
+        }
+    };
+
+    if (active) begin_row();
+    while (true) {
+        if (active && sp == 0) {
+            end_row();
+            if (++ri == 8) {
+                ri = 0;
+                chunk += ngroups;
+                if (chunk * 8 < p.n) load_chunk();
+            }
+            slot = chunk * 8 + ri;
+            active = slot < p.n;
+            if (active) begin_row();
+        }
+        if (!__any(active)) break;
+        if (active && sp > 0) {
+            uint32_t top = fp[0];
+            const uint32_t cs = (uint32_t)__builtin_ctz(top & 0xFFu);
+            top &= top - 1;  // clears the lowest pending bit (the mask is the low byte)
+            fp[0] = top;
+            const uint32_t w = (top >> 8) + cs;
+            const uint32_t jsel = (cs & 1) ? jc1[0] : jc0[0];
+            const uint32_t jw = (uint32_t)__shfl((int)jsel, (int)(gbase + (cs >> 1)), 64);
+            if ((top & 0xFFu) == 0) {  // no children left at this level
+#pragma unroll
+                for (int k = 0; k < (int)kFastMaxd - 1; ++k) {
+                    jc0[k] = jc0[k + 1];
+                    jc1[k] = jc1[k + 1];
+                    fp[k] = fp[k + 1];
+                }
+                --sp;
+            }
+            uint64_t w0, w1;
+            if (w < p.n_lds) {
+                w0 = lds_nodes[2 * w];
+                w1 = lds_nodes[2 * w + 1];
+            } else {
+                w0 = gld(gnodes + 2 * w);
+                w1 = gld(gnodes + 2 * w + 1);
+            }
+            visit(w0, w1, jw);
+        }
+    }
+}
+
 // CSR compaction of the label slots (rows with <= K labels).  A workgroup
 // takes 256 consecutive rows; its threads walk the tile's contiguous output
 // range [offsets[r0], offsets[r0+256]) so the stores are fully coalesced,
@@ -690,6 +865,7 @@ struct Trav {
     TravFn lane_fn = nullptr;
     GroupFn group_fn = nullptr;
     uint32_t G = 1;  // lanes per row
+    bool fast = false;
     explicit operator bool() const { return fn != nullptr; }
 };
 
@@ -697,6 +873,15 @@ template <int MODE>
 Trav pick_traverse(const Ctx &c) {
     const uint32_t depth = c.tree.stack_depth, max_arity = c.tree.max_arity;
     Trav t;
+    if (MODE == MODE_SLOTS && c.tree.fast_shape && (c.kernel_variant == 11 || c.kernel_variant == 12 ||
+                                                    c.kernel_variant == 0)) {
+        const bool nt = c.kernel_variant == 12 || (c.kernel_variant == 0 && c.tree.image_bytes > (1ull << 30));
+        t.G = 4;
+        t.fast = true;
+        t.lane_fn = nt ? (TravFn)k_traverse_fast<true> : (TravFn)k_traverse_fast<false>;
+        t.fn = reinterpret_cast<const void *>(t.lane_fn);
+        return t;
+    }
     if (c.kernel_variant == 1) {  // lane-per-row kernel (kept for A/B measurement)
         const bool wide = max_arity > 32;
 #define PICK(D)                                                                                      \
@@ -714,10 +899,11 @@ Trav pick_traverse(const Ctx &c) {
     }
     // group kernel: CPL children per lane, G = pow2ceil(ceil(max_arity / CPL)) lanes per row;
     // variants 5/6 request a higher occupancy (waves per SIMD) from the register allocator
-    const int v = c.kernel_variant ? c.kernel_variant : 5;  // default: 2 children per lane, 8 waves/SIMD
+    // default (and the fast variants on trees they do not fit): 2 children per lane, 8 waves/SIMD
+    const int v = (c.kernel_variant == 0 || c.kernel_variant >= 11) ? 5 : c.kernel_variant;
     const int cpl = v == 2 ? 1 : (v == 4 || v == 6) ? 4 : 2;
-    const int wpe = (v == 5 || v == 10) ? 8 : v == 6 ? 6 : 1;
-    if (v == 10) {  // variant 5 with non-temporal block/mask reads
+    const int wpe = (v == 5 || v == 10) ? 8 : v == 6 ? 6 : 1;  // (v == 10 past depth 8 runs as 5)
+    if (v == 10 && depth <= 8) {  // variant 5 with non-temporal block/mask reads
         const uint32_t need = (max_arity + 1) / 2;
         uint32_t G = 1;
         while (G < need) G <<= 1;
@@ -752,7 +938,7 @@ Trav pick_traverse(const Ctx &c) {
 }
 
 size_t lds_bytes(const Ctx &c, const Trav &t) {
-    if (!t.group_fn) return 0;
+    if (!t.group_fn && !t.fast) return 0;
     const size_t nl = std::min<size_t>(c.tree.nodes.size(), kLdsNodes);
     return (size_t)(256 / t.G) * kStageLabels * sizeof(uint32_t) + nl * sizeof(CNode);
 }
@@ -764,7 +950,7 @@ int grid_for(const Ctx &c, const Trav &t, uint64_t n) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, t.fn, 256, lds_bytes(c, t)) != hipSuccess || per_cu <= 0)
         per_cu = 4;
     const uint64_t resident = (uint64_t)std::max(1, dev_cus) * (uint64_t)per_cu;
-    const uint64_t rows_per_block = 256 / t.G;
+    const uint64_t rows_per_block = t.fast ? 512 : 256 / t.G;  // fast: 64 groups x 8-row chunks
     const uint64_t need = (n + rows_per_block - 1) / rows_per_block;
     return (int)std::max<uint64_t>(1, std::min(need, resident));
 }
@@ -772,7 +958,7 @@ int grid_for(const Ctx &c, const Trav &t, uint64_t n) {
 hipError_t launch(const Ctx &c, const Trav &t, uint64_t n, hipStream_t s, const TravParams &p) {
     const int grid = grid_for(c, t, n);
     if (t.group_fn) hipLaunchKernelGGL(t.group_fn, dim3(grid), dim3(256), lds_bytes(c, t), s, p, t.G);
-    else hipLaunchKernelGGL(t.lane_fn, dim3(grid), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(t.lane_fn, dim3(grid), dim3(256), lds_bytes(c, t), s, p);
     return hipGetLastError();
 }
 
