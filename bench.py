@@ -51,7 +51,26 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host cores")
     ap.add_argument("--check-rows", type=int, default=20_000, help="GPU rows checked against the oracle")
     ap.add_argument("--kernel", type=int, default=0, help="MBRWT_OPT_KERNEL variant (0 = library default)")
+    ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     return ap.parse_args()
+
+
+def committed_traffic(cfg):
+    """Per-launch HBM traffic of the traversal kernel from the committed PMC
+    summary of this exact workload (profiles/*/traffic_*.json, written by
+    tools/pmc_traffic.py from separate rocprofv3 --pmc passes of this script),
+    or None when no summary matches."""
+    import glob
+    hit = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic_*.json"))):
+        try:
+            with open(path) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if {k: str(v) for k, v in cfg.items()} == {k: str(v) for k, v in t.get("config", {}).items()}:
+            hit = (t["traffic_bytes"], os.path.relpath(path, ROOT))
+    return hit
 
 
 def log(msg):
@@ -63,10 +82,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    local = local % max(1, ndev)  # (rehearsal only: several ranks may share one GPU under gloo)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(a.dist_backend)
     else:
         torch.cuda.set_device(local)
     from genome_graph_annotation_amd import BRWTDevice, _lib as L
@@ -160,6 +184,10 @@ def main():
                          f"structure (oracle restatement of BRWT::get_row, plain rank/select; host build {gen_s:.0f} s)"}
         del ref
 
+    tcfg = {"rows": a.rows, "cols": a.cols, "density": a.density, "arity": a.arity, "batch": a.batch,
+            "kernel": a.kernel}
+    traffic = committed_traffic(tcfg)
+
     value = world * a.batch * a.steps / elapsed
     line = {
         "metric": METRIC,
@@ -180,13 +208,16 @@ def main():
             "num_rows": a.rows, "num_columns": a.cols, "density": a.density, "arity": a.arity,
             "batch_per_gpu": a.batch, "global_batch": a.batch * world,
             "parallelism": f"batch-sharded x{world}, tree replicated" + ("" if world == 1 or a.no_gather
-                                                                         else ", RCCL all-gatherv"),
+                                                                         else ", all-gatherv over " + ("RCCL" if a.dist_backend == "nccl" else a.dist_backend)),
             "structure_bytes": mat.device_bytes(), "setup_s": round(setup_s, 2),
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": "k_traverse", "kernel_ms": kern_ms,
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None if traffic is None else traffic[0],
+            "traffic_source": None if traffic is None else traffic[1] + " (rocprofv3 PMC, calibrated; per launch)",
+            "kernel": ("k_traverse_fast" if a.kernel in (0, 11, 12) and a.arity <= 8 else "k_traverse_group"),
+            "kernel_ms": kern_ms,
             "alg_bytes_per_launch": alg_bytes, "visits_per_row": visits / a.batch,
             "labels_per_row": labels / a.batch,
         },

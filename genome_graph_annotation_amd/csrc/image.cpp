@@ -254,6 +254,17 @@ int finalize_tree(Tree &tree) {
             dn.label = tree.nodes[dn.first_child].label;
         }
     }
+    // PLANE nodes whose children are all MASK8 nodes with consecutive labels
+    for (uint32_t v = 0; v < D; ++v) {
+        DevNode &dn = tree.nodes[v];
+        if (dn.kind != KIND_PLANE) continue;
+        bool all = dn.arity > 0;
+        for (uint32_t c = 0; c < dn.arity; ++c) {
+            const DevNode &ch = tree.nodes[dn.first_child + c];
+            if (ch.kind != KIND_MASK8 || !(ch.flags & FLAG_CONSEC_LABELS)) all = false;
+        }
+        if (all) dn.flags |= FLAG_MASK_CHILDREN;
+    }
     // shape eligible for the specialised kernel: internal nodes PLANE/MASK8 with
     // arity <= 8, MASK8 labels consecutive, no leaf directly under a PLANE node
     tree.fast_shape = true;

@@ -45,7 +45,11 @@ enum : uint8_t {
     KIND_MASK64 = 5,
     KIND_FOLDED = 6,  // the BRWT root when folded into the super-root (never visited)
 };
-enum : uint8_t { FLAG_CONSEC_LABELS = 1 };
+// FLAG_CONSEC_LABELS (MASK nodes): child c's label = label + c.
+// FLAG_MASK_CHILDREN (PLANE nodes): every child is a KIND_MASK8 node with
+// consecutive labels, so the fast kernel resolves the children in the
+// parent's visit (their mask reads are independent and issued together).
+enum : uint8_t { FLAG_CONSEC_LABELS = 1, FLAG_MASK_CHILDREN = 2 };
 
 struct alignas(32) DevNode {
     uint64_t base;         // device address of the children image (internal nodes)
@@ -61,7 +65,8 @@ static_assert(sizeof(DevNode) == 32, "DevNode must be 32 bytes");
 
 // Compact 16-byte node record read by the group kernel (kept in LDS for the
 // first kLdsNodes dnodes -- in BFS numbering the internal nodes come first):
-//   w0 = base[0:48) | kind[48:51) | flags[51] | log2(stride)[52:56) | arity[56:64)
+//   w0 = base[0:48) | kind[48:51) | flag[51] | log2(stride)[52:56) | arity[56:64)
+// flag = FLAG_MASK_CHILDREN for KIND_PLANE, FLAG_CONSEC_LABELS otherwise.
 struct alignas(16) CNode {
     uint64_t w0;
     uint32_t first_child;
@@ -75,7 +80,8 @@ inline CNode compact(const DevNode &d) {
     uint32_t lg = 0;
     while (d.stride && (1u << lg) < d.stride) ++lg;
     CNode c;
-    c.w0 = (d.base & ((1ull << 48) - 1)) | ((uint64_t)(d.kind & 7) << 48) | ((uint64_t)(d.flags & 1) << 51) |
+    const uint64_t flag = d.kind == KIND_PLANE ? (d.flags & FLAG_MASK_CHILDREN) ? 1 : 0 : (d.flags & FLAG_CONSEC_LABELS);
+    c.w0 = (d.base & ((1ull << 48) - 1)) | ((uint64_t)(d.kind & 7) << 48) | (flag << 51) |
            ((uint64_t)(lg & 15) << 52) | ((uint64_t)(d.arity & 0xFF) << 56);
     c.first_child = d.first_child;
     c.label = d.label;

@@ -608,7 +608,7 @@ __global__ __launch_bounds__(256, WPE) void k_traverse_group(TravParams p, uint3
 // ------------------------------------------------------------------------
 constexpr uint32_t kFastMaxd = 4;
 
-template <bool NT>
+template <bool NT, bool TERM>
 __global__ __launch_bounds__(256, 8) void k_traverse_fast(TravParams p) {
     constexpr uint32_t G = 4;
     const uint32_t lane = threadIdx.x & 63;
@@ -633,6 +633,16 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast(TravParams p) {
     uint32_t ri = 0;
     uint64_t slot = chunk * 8;
 
+    // label number `pos` of the current row: LDS stage, else straight to the slot
+    auto emit = [&](uint32_t pos, uint32_t label) {
+        if (pos < kStageLabels) stage[pos] = label;
+        else if (pos < p.K) gst(p.temp + slot * p.K + pos, label);  // past the LDS stage
+    };
+    auto node_w0 = [&](uint32_t w) -> uint64_t { return w < p.n_lds ? lds_nodes[2 * w] : gld(gnodes + 2 * w); };
+    auto node_w1 = [&](uint32_t w) -> uint64_t {
+        return w < p.n_lds ? lds_nodes[2 * w + 1] : gld(gnodes + 2 * w + 1);
+    };
+
     // visit node record (w0, w1) at position j
     auto visit = [&](uint64_t w0, uint64_t w1, uint32_t j) {
         const uint64_t base = w0 & ((1ull << 48) - 1);
@@ -648,6 +658,43 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast(TravParams p) {
                 b1 = (2 * c + 1 < a) ? (q.w >> t) & 1u : 0u;
                 j0 = q.x + (uint32_t)__builtin_popcount(q.y & below);  // rank1(j) - 1 of child 2c
                 j1 = q.z + (uint32_t)__builtin_popcount(q.w & below);  // and of child 2c+1
+            }
+            if (TERM && ((w0 >> 51) & 1u)) {
+                // FLAG_MASK_CHILDREN: every child is a MASK8 node over leaves; read
+                // the masks of the (up to 2) set children of this lane at once
+                // instead of visiting them one by one, then place their labels in
+                // child order (exclusive scan of the counts over the group).
+                const uint32_t fc = (uint32_t)w1;
+                uint32_t m0 = 0, m1 = 0, l0 = 0, l1 = 0;
+                if (b0) {
+                    const uint32_t w = fc + 2 * c;
+                    m0 = gld_at_nt<uint8_t, NT>((node_w0(w) & ((1ull << 48) - 1)) + j0);
+                    l0 = (uint32_t)(node_w1(w) >> 32);
+                }
+                if (b1) {
+                    const uint32_t w = fc + 2 * c + 1;
+                    m1 = gld_at_nt<uint8_t, NT>((node_w0(w) & ((1ull << 48) - 1)) + j1);
+                    l1 = (uint32_t)(node_w1(w) >> 32);
+                }
+                const uint32_t n0 = (uint32_t)__builtin_popcount(m0);
+                const uint32_t s0 = n0 + (uint32_t)__builtin_popcount(m1);
+                uint32_t incl = s0;
+                uint32_t y = (uint32_t)__shfl((int)incl, (int)(lane - 1), 64);
+                incl += c >= 1 ? y : 0u;
+                y = (uint32_t)__shfl((int)incl, (int)(lane - 2), 64);
+                incl += c >= 2 ? y : 0u;
+                const uint32_t total = (uint32_t)__shfl((int)incl, (int)(gbase + 3), 64);
+                uint32_t pos = cnt + incl - s0;
+                while (m0) {
+                    emit(pos++, l0 + (uint32_t)__builtin_ctz(m0));
+                    m0 &= m0 - 1;
+                }
+                while (m1) {
+                    emit(pos++, l1 + (uint32_t)__builtin_ctz(m1));
+                    m1 &= m1 - 1;
+                }
+                cnt += total;
+                return;
             }
             const uint32_t e = (uint32_t)(__ballot(b0) >> gbase) & 0xFu;
             const uint32_t o = (uint32_t)(__ballot(b1) >> gbase) & 0xFu;
@@ -678,11 +725,7 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast(TravParams p) {
 #pragma unroll
         for (uint32_t q = 0; q < 2; ++q) {
             const uint32_t cc = 2 * c + q;
-            if ((m >> cc) & 1u) {
-                const uint32_t pos = cnt + (uint32_t)__builtin_popcount(m & ((1u << cc) - 1u));
-                if (pos < kStageLabels) stage[pos] = l0 + cc;
-                else if (pos < p.K) gst(p.temp + slot * p.K + pos, l0 + cc);  // past the LDS stage
-            }
+            if ((m >> cc) & 1u) emit(cnt + (uint32_t)__builtin_popcount(m & ((1u << cc) - 1u)), l0 + cc);
         }
         cnt += (uint32_t)__builtin_popcount(m);
     };
@@ -756,15 +799,7 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast(TravParams p) {
                 }
                 --sp;
             }
-            uint64_t w0, w1;
-            if (w < p.n_lds) {
-                w0 = lds_nodes[2 * w];
-                w1 = lds_nodes[2 * w + 1];
-            } else {
-                w0 = gld(gnodes + 2 * w);
-                w1 = gld(gnodes + 2 * w + 1);
-            }
-            visit(w0, w1, jw);
+            visit(node_w0(w), node_w1(w), jw);
         }
     }
 }
@@ -873,12 +908,16 @@ template <int MODE>
 Trav pick_traverse(const Ctx &c) {
     const uint32_t depth = c.tree.stack_depth, max_arity = c.tree.max_arity;
     Trav t;
-    if (MODE == MODE_SLOTS && c.tree.fast_shape && (c.kernel_variant == 11 || c.kernel_variant == 12 ||
-                                                    c.kernel_variant == 0)) {
-        const bool nt = c.kernel_variant == 12 || (c.kernel_variant == 0 && c.tree.image_bytes > (1ull << 30));
+    const int kv = c.kernel_variant;
+    if (MODE == MODE_SLOTS && c.tree.fast_shape && (kv == 0 || (kv >= 11 && kv <= 14))) {
+        // 11/12: fast kernel without / with non-temporal reads; 13/14: the same
+        // without resolving FLAG_MASK_CHILDREN nodes' children inline (A/B)
+        const bool nt = kv == 12 || kv == 14 || (kv == 0 && c.tree.image_bytes > (1ull << 30));
+        const bool term = kv <= 12;
         t.G = 4;
         t.fast = true;
-        t.lane_fn = nt ? (TravFn)k_traverse_fast<true> : (TravFn)k_traverse_fast<false>;
+        t.lane_fn = nt ? (term ? (TravFn)k_traverse_fast<true, true> : (TravFn)k_traverse_fast<true, false>)
+                       : (term ? (TravFn)k_traverse_fast<false, true> : (TravFn)k_traverse_fast<false, false>);
         t.fn = reinterpret_cast<const void *>(t.lane_fn);
         return t;
     }

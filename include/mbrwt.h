@@ -146,7 +146,10 @@ int mbrwt_count_work_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, 
 /* Options (mbrwt_set_option). */
 #define MBRWT_OPT_TIMING 1       /* 1: time the traversal kernel with HIP events */
 #define MBRWT_OPT_SLOT_LABELS 2  /* per-row label slots of the fast path (0 = auto) */
-#define MBRWT_OPT_KERNEL 4       /* traversal kernel: 0 default, 1 lane-per-row, 2/3/4 group with 1/2/4 children per lane */
+#define MBRWT_OPT_KERNEL 4       /* traversal kernel (A/B measurement): 0 default, 1 lane-per-row,
+                                    2/3/4 group with 1/2/4 children per lane, 5/6 group at 8/6 waves per SIMD,
+                                    10 group + non-temporal reads, 11/12 fast kernel (+ non-temporal),
+                                    13/14 fast kernel without inline MASK8 children; others rejected */
 int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value);
 
 /* Traversal-kernel time accumulated while MBRWT_OPT_TIMING is on (ms, launches); resets the sums. */

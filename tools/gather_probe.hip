@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
+#include <string>
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -104,6 +105,23 @@ int main(int argc, char **argv) {
     uint4 *out = nullptr;
     hipMalloc(&out, (size_t)65536 * 256 * sizeof(uint4));
     hipDeviceSynchronize();
+    if (argc > 2 && std::string(argv[2]) == "calib") {
+        // counter calibration: ONE dispatch of k_probe_group<4> with G = 4, i.e.
+        // a known number of random 64-B segment reads (the traversal's pattern);
+        // FETCH_SIZE / TCC_EA0_RDREQ of that dispatch divided by the segment
+        // count gives the bytes each counter tallies per 64-B random read.
+        const int grid = 8192;
+        const uint32_t G = 4, iters = 64;
+        const uint64_t nlines = total / 128;
+        hipLaunchKernelGGL(k_probe_group<4>, dim3(grid), dim3(256), 0, 0, (const uint4 *)buf, nlines, G, iters,
+                           (uint64_t)11, out);
+        hipDeviceSynchronize();
+        printf("calib: buffer %.1f GiB, one k_probe_group<4> dispatch, G=%u: %llu random 64-B segments (%llu bytes)\n",
+               gib, G, (unsigned long long)grid * 256 / G * iters * 4,
+               (unsigned long long)grid * 256 / G * iters * 4 * 64);
+        hipFree(buf);
+        return 0;
+    }
     for (int grid : {2048, 8192}) {
         const uint32_t iters = 64;
         double r16 = run<1>((const uint4 *)buf, total, 128, grid, iters, out);
