@@ -295,6 +295,9 @@ int finalize_tree(Tree &tree) {
     }
     tree.path_len = std::max<uint32_t>(1, max_depth);
     if (tree.stack_depth > kFastMaxDepth) tree.fast_shape = false;
+    tree.lds_complete = true;
+    for (uint32_t v = kLdsNodes; v < D; ++v)
+        if (tree.nodes[v].kind != KIND_LEAF) tree.lds_complete = false;
     tree.col_path.assign(tree.num_columns * tree.path_len, 0);
     tree.col_leaf.assign(tree.num_columns, 0);
     for (uint32_t v = 0; v < D; ++v) {

@@ -34,6 +34,8 @@ enum { MODE_SLOTS = 0, MODE_DIRECT = 1, MODE_WORK = 2, MODE_COUNT = 3 };
 // global_* (address space 1) or ds_* (address space 3) instruction.
 #define AS_GLOBAL __attribute__((address_space(1)))
 #define AS_LDS __attribute__((address_space(3)))
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 // (the host pass of the same source only needs the declarations to parse)
 #if defined(__HIP_DEVICE_COMPILE__)
 template <class T>
@@ -42,8 +44,6 @@ template <class T>
 __device__ __forceinline__ T gld_at(uint64_t addr) { return *(const AS_GLOBAL T *)addr; }
 template <class T>
 __device__ __forceinline__ void gst(T *p, T v) { *(AS_GLOBAL T *)(uintptr_t)p = v; }
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 template <class T, bool NT>
 __device__ __forceinline__ T gld_at_nt(uint64_t addr) {
     if constexpr (!NT) {
@@ -730,21 +730,21 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast(TravParams p) {
         cnt += (uint32_t)__builtin_popcount(m);
     };
 
-    // rows: each group takes chunks of 8 consecutive slots, ids preloaded 2 per lane
-    uint64_t r0 = 0, r1 = 0;
+    // rows: each group takes chunks of 8 consecutive slots, ids preloaded 2 per
+    // lane as u32 (num_rows <= 2^32 - 1, so ids >= num_rows clamp to 0xFFFFFFFF,
+    // which is out of range too)
+    uint32_t r0 = 0, r1 = 0;
+    auto clamp_row = [&](uint64_t r) -> uint32_t { return r < p.num_rows ? (uint32_t)r : 0xFFFFFFFFu; };
     auto load_chunk = [&]() {
         const uint64_t sb = chunk * 8 + 2 * c;
-        r0 = sb < p.n ? gld(p.rows + sb) : 0;
-        r1 = sb + 1 < p.n ? gld(p.rows + sb + 1) : 0;
+        r0 = sb < p.n ? clamp_row(gld(p.rows + sb)) : 0u;
+        r1 = sb + 1 < p.n ? clamp_row(gld(p.rows + sb + 1)) : 0u;
     };
     bool active = slot < p.n;
     if (active) load_chunk();
     auto begin_row = [&]() {
-        const uint64_t mine = (ri & 1) ? r1 : r0;
-        const uint32_t src = gbase + (ri >> 1);
-        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)mine, (int)src, 64);
-        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(mine >> 32), (int)src, 64);
-        const uint64_t row = ((uint64_t)hi << 32) | lo;
+        const uint32_t mine = (ri & 1) ? r1 : r0;
+        const uint64_t row = (uint32_t)__shfl((int)mine, (int)(gbase + (ri >> 1)), 64);
         cnt = 0;
         if (row >= p.num_rows) {
             if (c == 0) atomicOr(&p.scalars[2], 1ull);
@@ -786,10 +786,10 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast(TravParams p) {
             uint32_t top = fp[0];
             const uint32_t cs = (uint32_t)__builtin_ctz(top & 0xFFu);
             top &= top - 1;  // clears the lowest pending bit (the mask is the low byte)
-            fp[0] = top;
             const uint32_t w = (top >> 8) + cs;
             const uint32_t jsel = (cs & 1) ? jc1[0] : jc0[0];
             const uint32_t jw = (uint32_t)__shfl((int)jsel, (int)(gbase + (cs >> 1)), 64);
+            fp[0] = top;
             if ((top & 0xFFu) == 0) {  // no children left at this level
 #pragma unroll
                 for (int k = 0; k < (int)kFastMaxd - 1; ++k) {
@@ -800,6 +800,209 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast(TravParams p) {
                 --sp;
             }
             visit(node_w0(w), node_w1(w), jw);
+        }
+    }
+}
+
+// Reductions over the 4 lanes of a group (lanes 4i..4i+3 = one DPP quad):
+// quad_perm DPP moves, no LDS round trip.  All 4 lanes must be active.
+__device__ __forceinline__ uint32_t quad_or(uint32_t v) {
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm(1,0,3,2)
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm(2,3,0,1)
+    return v;
+}
+// exclusive prefix sum of v over the quad (lane order); `total` = quad sum
+__device__ __forceinline__ uint32_t quad_exclusive_sum(uint32_t v, uint32_t c, uint32_t &total) {
+    uint32_t incl = v;
+    uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x90, 0xF, 0xF, false);  // quad_perm(0,0,1,2)
+    incl += c >= 1 ? y : 0u;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x40, 0xF, 0xF, false);  // quad_perm(0,0,0,1)
+    incl += c >= 2 ? y : 0u;
+    total = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0xFF, 0xF, 0xF, false);  // quad_perm(3,3,3,3)
+    return incl - v;
+}
+
+// ------------------------------------------------------------------------
+// k_traverse_fast2: k_traverse_fast restructured so that every iteration of
+// a wave runs ONE inlined visit (a group starting a row visits the root in
+// the same code as a group visiting a popped child) -- with 16 groups per
+// wave at different places of their trees, every extra code path in the loop
+// body is paid by the whole wave.  Node records come from LDS only (the tree
+// is eligible when every non-leaf dnode id is < n_lds), so the mask reads of
+// a FLAG_MASK_CHILDREN visit are not serialised behind a global-fallback
+// wait; the label stage is flushed as 16-byte vectors.
+// ------------------------------------------------------------------------
+template <bool NT, bool SMALLK>
+__global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
+    constexpr uint64_t M48 = (1ull << 48) - 1;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t c = lane & 3;
+    const uint32_t gbase = lane & ~3u;
+    const uint64_t gid = (uint64_t)blockIdx.x * 64 + threadIdx.x / 4;
+    const uint64_t ngroups = (uint64_t)gridDim.x * 64;
+
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_stage[];  // 64 groups x kStageLabels
+    AS_LDS uint32_t *stage = (AS_LDS uint32_t *)lds_stage + (threadIdx.x / 4) * kStageLabels;
+    AS_LDS uint64_t *lds_nodes = (AS_LDS uint64_t *)((AS_LDS uint32_t *)lds_stage + 64 * kStageLabels);
+    const uint64_t *gnodes = reinterpret_cast<const uint64_t *>(p.cnodes);
+    for (uint32_t i = threadIdx.x; i < 2 * p.n_lds; i += blockDim.x) lds_nodes[i] = gld(gnodes + i);
+    __syncthreads();
+
+    uint32_t jc0[kFastMaxd], jc1[kFastMaxd], fp[kFastMaxd];  // fp = first_child << 8 | pending mask
+#pragma unroll
+    for (int k = 0; k < (int)kFastMaxd; ++k) jc0[k] = jc1[k] = fp[k] = 0;
+    int sp = 0;
+    uint32_t cnt = 0;
+    uint64_t chunk = gid;
+    uint32_t ri = 0;
+    uint64_t slot = chunk * 8;
+    uint32_t *slot_ptr = p.temp + slot * p.K;
+
+    // SMALLK: K == kStageLabels, every kept label fits the stage
+    auto emit = [&](uint32_t pos, uint32_t label) {
+        if (pos < kStageLabels) stage[pos] = label;
+        else if (!SMALLK && pos < p.K) gst(slot_ptr + pos, label);  // past the LDS stage
+    };
+
+    // rows: chunks of 8 consecutive slots per group, ids preloaded 2 per lane as
+    // u32 (ids >= num_rows clamp to 0xFFFFFFFF >= num_rows)
+    uint32_t r0 = 0, r1 = 0;
+    auto clamp_row = [&](uint64_t r) -> uint32_t { return r < p.num_rows ? (uint32_t)r : 0xFFFFFFFFu; };
+    auto load_chunk = [&]() {
+        const uint64_t sb = chunk * 8 + 2 * c;
+        r0 = sb < p.n ? clamp_row(gld(p.rows + sb)) : 0u;
+        r1 = sb + 1 < p.n ? clamp_row(gld(p.rows + sb + 1)) : 0u;
+    };
+    bool active = slot < p.n, fresh = active;  // fresh: the slot's row has not been started
+    if (active) load_chunk();
+
+    while (true) {
+        if (active && !fresh && sp == 0) {  // row done: flush its stage, count, next slot
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t lim = cnt < kStageLabels ? cnt : kStageLabels;
+            for (uint32_t q = c; 4 * q < lim; q += 4)
+                gst(reinterpret_cast<u32x4_t *>(slot_ptr) + q, (u32x4_t)((AS_LDS u32x4_t *)stage)[q]);
+            if (c == 0) {
+                gst(p.counts + slot, cnt);
+                if (cnt > p.K) {
+                    const unsigned long long k = atomicAdd(&p.scalars[1], 1ull);
+                    gst(p.ovf_list + k, (uint32_t)slot);
+                }
+            }
+            if (++ri == 8) {
+                ri = 0;
+                chunk += ngroups;
+                if (chunk * 8 < p.n) load_chunk();
+            }
+            slot = chunk * 8 + ri;
+            slot_ptr = p.temp + slot * p.K;
+            active = slot < p.n;
+            fresh = active;
+        }
+        if (!__any(active)) break;
+        if (!active) continue;
+
+        // the node to visit: the root for a fresh row, else the next pending child
+        uint64_t w0, w1;
+        uint32_t j;
+        bool go = true;
+        if (fresh) {
+            fresh = false;
+            cnt = 0;
+            const uint32_t mine = (ri & 1) ? r1 : r0;
+            j = (uint32_t)__shfl((int)mine, (int)(gbase + (ri >> 1)), 64);
+            w0 = lds_nodes[0];
+            w1 = lds_nodes[1];
+            if ((uint64_t)j >= p.num_rows) {
+                if (c == 0) atomicOr(&p.scalars[2], 1ull);
+                go = false;
+            }
+        } else {
+            uint32_t top = fp[0];
+            const uint32_t cs = (uint32_t)__builtin_ctz(top & 0xFFu);
+            top &= top - 1;
+            fp[0] = top;
+            const uint32_t w = (top >> 8) + cs;
+            const uint32_t jsel = (cs & 1) ? jc1[0] : jc0[0];
+            j = (uint32_t)__shfl((int)jsel, (int)(gbase + (cs >> 1)), 64);
+            if ((top & 0xFFu) == 0) {
+#pragma unroll
+                for (int k = 0; k < (int)kFastMaxd - 1; ++k) {
+                    jc0[k] = jc0[k + 1];
+                    jc1[k] = jc1[k + 1];
+                    fp[k] = fp[k + 1];
+                }
+                --sp;
+            }
+            w0 = lds_nodes[2 * w];
+            w1 = lds_nodes[2 * w + 1];
+        }
+        if (!go) continue;
+
+        const uint64_t base = w0 & M48;
+        const uint32_t a = (uint32_t)(w0 >> 56);
+        if (((uint32_t)(w0 >> 48) & 7u) == KIND_MASK8) {  // leaves below: labels from the mask
+            const uint32_t m = gld_at_nt<uint8_t, NT>(base + j);
+            const uint32_t l0 = (uint32_t)(w1 >> 32);
+#pragma unroll
+            for (uint32_t q = 0; q < 2; ++q) {
+                const uint32_t cc = 2 * c + q;
+                if ((m >> cc) & 1u) emit(cnt + (uint32_t)__builtin_popcount(m & ((1u << cc) - 1u)), l0 + cc);
+            }
+            cnt += (uint32_t)__builtin_popcount(m);
+            continue;
+        }
+        // KIND_PLANE: one coalesced 64-byte block read, 2 children per lane
+        const uint32_t stride = 1u << ((uint32_t)(w0 >> 52) & 15u);
+        const uint32_t t = j & 31, below = (1u << t) - 1u;
+        uint32_t b0 = 0, b1 = 0, j0 = 0, j1 = 0;
+        if (2 * c < a) {
+            const uint4 q = gld_at_nt<uint4, NT>(base + (uint64_t)(j >> 5) * stride + 16u * c);
+            b0 = (q.y >> t) & 1u;
+            b1 = (2 * c + 1 < a) ? (q.w >> t) & 1u : 0u;
+            j0 = q.x + (uint32_t)__builtin_popcount(q.y & below);
+            j1 = q.z + (uint32_t)__builtin_popcount(q.w & below);
+        }
+        const uint32_t fc = (uint32_t)w1;
+        if ((w0 >> 51) & 1u) {  // FLAG_MASK_CHILDREN: resolve the children's masks now
+            uint32_t m0 = 0, m1 = 0, l0 = 0, l1 = 0;
+            if (b0) {
+                const uint32_t w = fc + 2 * c;
+                m0 = gld_at_nt<uint8_t, NT>((lds_nodes[2 * w] & M48) + j0);
+                l0 = (uint32_t)(lds_nodes[2 * w + 1] >> 32);
+            }
+            if (b1) {
+                const uint32_t w = fc + 2 * c + 1;
+                m1 = gld_at_nt<uint8_t, NT>((lds_nodes[2 * w] & M48) + j1);
+                l1 = (uint32_t)(lds_nodes[2 * w + 1] >> 32);
+            }
+            const uint32_t s0 = (uint32_t)__builtin_popcount(m0) + (uint32_t)__builtin_popcount(m1);
+            uint32_t total;
+            const uint32_t ex = quad_exclusive_sum(s0, c, total);
+            uint32_t pos = cnt + ex;
+            for (; m0; m0 &= m0 - 1) emit(pos++, l0 + (uint32_t)__builtin_ctz(m0));
+            for (; m1; m1 &= m1 - 1) emit(pos++, l1 + (uint32_t)__builtin_ctz(m1));
+            cnt += total;
+            continue;
+        }
+        const uint32_t P = quad_or((b0 | (b1 << 1)) << (2 * c));  // child k <- bit k
+        if (P) {
+            if (sp >= (int)kFastMaxd) {
+                if (c == 0) atomicOr(&p.scalars[2], 2ull);
+                continue;
+            }
+#pragma unroll
+            for (int k = kFastMaxd - 1; k > 0; --k) {
+                jc0[k] = jc0[k - 1];
+                jc1[k] = jc1[k - 1];
+                fp[k] = fp[k - 1];
+            }
+            jc0[0] = j0;
+            jc1[0] = j1;
+            fp[0] = (fc << 8) | P;
+            ++sp;
         }
     }
 }
@@ -904,20 +1107,28 @@ struct Trav {
     explicit operator bool() const { return fn != nullptr; }
 };
 
+uint32_t auto_slots(const Ctx &c);
+
 template <int MODE>
 Trav pick_traverse(const Ctx &c) {
     const uint32_t depth = c.tree.stack_depth, max_arity = c.tree.max_arity;
     Trav t;
     const int kv = c.kernel_variant;
-    if (MODE == MODE_SLOTS && c.tree.fast_shape && (kv == 0 || (kv >= 11 && kv <= 14))) {
+    if (MODE == MODE_SLOTS && c.tree.fast_shape && (kv == 0 || (kv >= 11 && kv <= 14) || kv == 17 || kv == 18)) {
         // 11/12: fast kernel without / with non-temporal reads; 13/14: the same
         // without resolving FLAG_MASK_CHILDREN nodes' children inline (A/B)
-        const bool nt = kv == 12 || kv == 14 || (kv == 0 && c.tree.image_bytes > (1ull << 30));
-        const bool term = kv <= 12;
+        const bool nt = kv == 12 || kv == 14 || kv == 18 || (kv == 0 && c.tree.image_bytes > (1ull << 30));
+        // 17/18 (and the default when every non-leaf record fits the LDS table):
+        // k_traverse_fast2 without / with non-temporal reads
+        const bool term = kv != 13 && kv != 14;
+        const bool v2 = (kv == 0 || kv >= 17) && c.tree.lds_complete;
         t.G = 4;
         t.fast = true;
-        t.lane_fn = nt ? (term ? (TravFn)k_traverse_fast<true, true> : (TravFn)k_traverse_fast<true, false>)
-                       : (term ? (TravFn)k_traverse_fast<false, true> : (TravFn)k_traverse_fast<false, false>);
+        const bool smallk = auto_slots(c) == kStageLabels;
+        if (v2 && smallk) t.lane_fn = nt ? (TravFn)k_traverse_fast2<true, true> : (TravFn)k_traverse_fast2<false, true>;
+        else if (v2) t.lane_fn = nt ? (TravFn)k_traverse_fast2<true, false> : (TravFn)k_traverse_fast2<false, false>;
+        else if (term) t.lane_fn = nt ? (TravFn)k_traverse_fast<true, true> : (TravFn)k_traverse_fast<false, true>;
+        else t.lane_fn = nt ? (TravFn)k_traverse_fast<true, false> : (TravFn)k_traverse_fast<false, false>;
         t.fn = reinterpret_cast<const void *>(t.lane_fn);
         return t;
     }

@@ -20,7 +20,7 @@ def _dev(tree):
     return BRWTDevice.from_tree(tree.export())
 
 
-def _check_rows(oracle_tree, dev, rows, variants=(0, 1, 2, 4, 5, 10, 11, 12, 13, 14)):
+def _check_rows(oracle_tree, dev, rows, variants=(0, 1, 2, 4, 5, 10, 11, 12, 13, 14, 17, 18)):
     """Every traversal kernel (1 lane-per-row; 2/3/4 group-cooperative with
     1/2/4 children per lane; 0 the default) must
     reproduce the oracle's ordered CSR exactly."""
@@ -171,6 +171,7 @@ def test_c2_kingsford_small_exact(oracle_mod):
 @pytest.mark.parametrize("n,m,dens,arity", [
     (2_000_000, 2652, 0.003, 8),   # Kingsford shape, reduced rows
     (300_000, 3173, 0.038, 8),     # RefSeq shape, reduced rows
+    (50_000, 4000, 0.003, 8),      # > kLdsNodes internal records: fast kernel, global record fallback
     (100_000, 1, 0.3, 2),          # root is a leaf
     (100_000, 2, 0.5, 2),
     (200_000, 500, 0.01, 2),
