@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--cpu-sample", type=int, default=400_000, help="rows timed on the CPU")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host cores")
-    ap.add_argument("--check-rows", type=int, default=20_000, help="GPU rows checked against the oracle")
+    ap.add_argument("--check-rows", type=int, default=0,
+                    help="GPU rows checked element-wise against the oracle (0 = the whole batch)")
     ap.add_argument("--kernel", type=int, default=0, help="MBRWT_OPT_KERNEL variant (0 = library default)")
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     return ap.parse_args()
@@ -148,6 +149,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # measured streaming-read rate of this GPU (report beside the spec peak)
+    big = torch.ones(1 << 30, dtype=torch.float32, device=dev_t)  # 4 GiB
+    big.sum()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        big.sum()
+    e1.record()
+    torch.cuda.synchronize()
+    stream_gbs = 5 * big.numel() * 4 / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del big
+
     # exact work accounting for the roofline (untimed diagnostic pass)
     visits, labels = mat.count_work_device(rows_t, sptr)
     assert labels == n_lab, (labels, n_lab)
@@ -155,8 +168,8 @@ def main():
     kern_ms = kern_ms_total / max(1, launches)
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9
 
-    # GPU result sample for the parity spot-check
-    chk = min(a.check_rows, a.batch)
+    # GPU result of the last timed step for the parity gate
+    chk = min(a.check_rows, a.batch) if a.check_rows > 0 else a.batch
     off_h = off_t[: chk + 1].cpu().numpy().view(np.uint64)
     cols_h = cols_t[: int(off_h[-1])].cpu().numpy().view(np.uint32)
 
@@ -175,6 +188,7 @@ def main():
         log(f"host structure built in {gen_s:.1f} s; checking {chk} rows and timing {a.cpu_sample} rows")
         off_o, cols_o = ref.get_rows(rows_np[:chk], threads)
         parity = bool(np.array_equal(off_o, off_h) and np.array_equal(cols_o, cols_h))
+        del off_o, cols_o
         sample = rows_np[: a.cpu_sample]
         c0 = time.perf_counter()
         ref.time_rows(sample, threads)
@@ -184,8 +198,9 @@ def main():
                          f"structure (oracle restatement of BRWT::get_row, plain rank/select; host build {gen_s:.0f} s)"}
         del ref
 
+    kname = mat.traverse_kernel()
     tcfg = {"rows": a.rows, "cols": a.cols, "density": a.density, "arity": a.arity, "batch": a.batch,
-            "kernel": a.kernel}
+            "kernel": a.kernel, "kernel_name": kname}
     traffic = committed_traffic(tcfg)
 
     value = world * a.batch * a.steps / elapsed
@@ -213,16 +228,18 @@ def main():
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
+            "frac": achieved / HBM_PEAK_GBS, "stream_read_measured": stream_gbs,
             "traffic": None if traffic is None else traffic[0],
             "traffic_source": None if traffic is None else traffic[1] + " (rocprofv3 PMC, calibrated; per launch)",
-            "kernel": ("k_traverse_fast" if a.kernel in (0, 11, 12) and a.arity <= 8 else "k_traverse_group"),
+            "kernel": kname,
             "kernel_ms": kern_ms,
             "alg_bytes_per_launch": alg_bytes, "visits_per_row": visits / a.batch,
             "labels_per_row": labels / a.batch,
         },
         "cpu_baseline": cpu,
-        "parity": None if parity is None else f"{'bit-exact' if parity else 'MISMATCH'} on {chk:,} rows vs oracle",
+        "parity": None if parity is None else f"{'bit-exact' if parity else 'MISMATCH'} on {chk:,} rows"
+                                                f"{' (the whole timed batch)' if chk == a.batch else ''}"
+                                                f" vs the oracle, element-wise CSR",
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -74,6 +74,7 @@ SIGNATURES = {
     "mbrwt_take_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), u64p]),
     "mbrwt_strerror": (C.c_char_p, [C.c_int]),
     "mbrwt_last_error_message": (C.c_char_p, []),
+    "mbrwt_traverse_kernel": (C.c_char_p, [C.c_void_p]),
 }
 
 _lib = None

@@ -160,6 +160,10 @@ class BRWTDevice:
     def set_option(self, option, value):
         L.check(L.lib().mbrwt_set_option(self._h, option, int(value)), "mbrwt_set_option")
 
+    def traverse_kernel(self) -> str:
+        """Name of the traversal kernel get_rows launches (diagnostics)."""
+        return (L.lib().mbrwt_traverse_kernel(self._h) or b"").decode()
+
     def take_timing(self):
         ms = C.c_double(0)
         k = C.c_uint64(0)

@@ -312,4 +312,11 @@ const char *mbrwt_strerror(int status) {
 
 const char *mbrwt_last_error_message(void) { return g_last_error.c_str(); }
 
+const char *mbrwt_traverse_kernel(mbrwt_ctx *ctx) {
+    if (!ctx) return "";
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    return traverse_kernel_name(c);
+}
+
 }  // extern "C"

@@ -175,6 +175,7 @@ inline bool fold_root_enabled() {
 }
 
 // queries (query.hip)
+const char *traverse_kernel_name(const Ctx &c);  // the kernel mbrwt_get_rows* launches
 int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
                  uint64_t *needed, hipStream_t s);
 int run_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n, uint8_t *d_out, hipStream_t s);

@@ -1104,6 +1104,7 @@ struct Trav {
     GroupFn group_fn = nullptr;
     uint32_t G = 1;  // lanes per row
     bool fast = false;
+    const char *name = "k_traverse_group";
     explicit operator bool() const { return fn != nullptr; }
 };
 
@@ -1125,6 +1126,7 @@ Trav pick_traverse(const Ctx &c) {
         t.G = 4;
         t.fast = true;
         const bool smallk = auto_slots(c) == kStageLabels;
+        t.name = v2 ? "k_traverse_fast2" : "k_traverse_fast";
         if (v2 && smallk) t.lane_fn = nt ? (TravFn)k_traverse_fast2<true, true> : (TravFn)k_traverse_fast2<false, true>;
         else if (v2) t.lane_fn = nt ? (TravFn)k_traverse_fast2<true, false> : (TravFn)k_traverse_fast2<false, false>;
         else if (term) t.lane_fn = nt ? (TravFn)k_traverse_fast<true, true> : (TravFn)k_traverse_fast<false, true>;
@@ -1134,6 +1136,7 @@ Trav pick_traverse(const Ctx &c) {
     }
     if (c.kernel_variant == 1) {  // lane-per-row kernel (kept for A/B measurement)
         const bool wide = max_arity > 32;
+        t.name = "k_traverse";
 #define PICK(D)                                                                                      \
     if (depth <= D) {                                                                                \
         t.lane_fn = wide ? (TravFn)k_traverse<D, uint64_t, MODE> : (TravFn)k_traverse<D, uint32_t, MODE>; \
@@ -1242,6 +1245,11 @@ int ensure(Workspace &w, size_t bytes) {
     MBRWT_HIP(hipMalloc(&w.buf, b));
     w.bytes = b;
     return MBRWT_OK;
+}
+
+const char *traverse_kernel_name(const Ctx &c) {
+    const Trav t = pick_traverse<MODE_SLOTS>(c);
+    return t ? t.name : "";
 }
 
 int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,

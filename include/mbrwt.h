@@ -159,6 +159,10 @@ int mbrwt_take_timing(mbrwt_ctx *ctx, double *kernel_ms, uint64_t *launches);
 const char *mbrwt_strerror(int status);
 const char *mbrwt_last_error_message(void); /* thread-local detail of the last failure */
 
+/* Diagnostics: name of the traversal kernel mbrwt_get_rows* launches for this
+   tree under the current MBRWT_OPT_KERNEL (static string; "" for a null ctx). */
+const char *mbrwt_traverse_kernel(mbrwt_ctx *ctx);
+
 #ifdef __cplusplus
 }
 #endif
