@@ -66,6 +66,8 @@ SIGNATURES = {
     "mbrwt_get_rows": (C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p, u32p, C.c_uint64, u64p]),
     "mbrwt_get_rows_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
                                         u64p, C.c_void_p]),
+    "mbrwt_get_column": (C.c_int, [C.c_void_p, C.c_uint64, u64p, C.c_uint64, u64p]),
+    "mbrwt_get_column_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, u64p, C.c_void_p]),
     "mbrwt_get_batch": (C.c_int, [C.c_void_p, u64p, u64p, C.c_uint64, u8p]),
     "mbrwt_get_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
     "mbrwt_count_labels_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),

@@ -126,6 +126,31 @@ class BRWTDevice:
     def get(self, row, col):
         return bool(self.get_batch([row], [col])[0])
 
+    def get_column(self, col):
+        """BRWT::get_column (BRWT.cpp:55-85): ascending rows carrying `col`."""
+        need = C.c_uint64(0)
+        st = L.lib().mbrwt_get_column(self._h, int(col), None, 0, C.byref(need))
+        if st != L.MBRWT_ERR_CAPACITY:
+            L.check(st, "mbrwt_get_column")
+            return np.zeros(0, dtype=np.uint64)
+        out = np.zeros(max(1, need.value), dtype=np.uint64)
+        L.check(L.lib().mbrwt_get_column(self._h, int(col), _p(out, C.c_uint64), len(out), C.byref(need)),
+                "mbrwt_get_column")
+        return out[: need.value]
+
+    def get_column_device(self, col, rows_t, stream=None):
+        """Device variant: rows_t = 64-bit cuda tensor of capacity >= the column's
+        size.  Returns the number of rows written; raises on capacity."""
+        need = C.c_uint64(0)
+        st = L.lib().mbrwt_get_column_device(self._h, int(col), rows_t.data_ptr(), rows_t.numel(), C.byref(need),
+                                             stream if stream is not None else None)
+        if st == L.MBRWT_ERR_CAPACITY:
+            e = L.MBRWTError(st, "mbrwt_get_column_device")
+            e.needed = int(need.value)
+            raise e
+        L.check(st, "mbrwt_get_column_device")
+        return int(need.value)
+
     # -- device-buffer queries (torch tensors as plumbing) ---------------------
     def get_rows_device(self, rows_t, offsets_t, cols_t, stream=None):
         """rows_t: uint64/int64 cuda tensor [n]; offsets_t: [n+1] 64-bit; cols_t:

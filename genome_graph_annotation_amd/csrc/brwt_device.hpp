@@ -22,8 +22,8 @@
 
 namespace mbrwt_host {
 
-// common/binary_matrix.hpp:9-29 (load/serialize/get_column are not part of
-// the device path; see DESIGN.md "Out of scope")
+// common/binary_matrix.hpp:9-29 (load/serialize are not part of the device
+// path; see DESIGN.md "Out of scope")
 class BinaryMatrix {
   public:
     typedef uint64_t Row;
@@ -36,6 +36,7 @@ class BinaryMatrix {
 
     virtual bool get(Row row, Column column) const = 0;
     virtual std::vector<Column> get_row(Row row) const = 0;
+    virtual std::vector<Row> get_column(Column column) const = 0;
 
     // Batched get_row: the default loops over get_row (every scheme of the
     // reference); device-backed matrices override it with one launch.
@@ -100,6 +101,20 @@ class BRWTDevice : public BinaryMatrix {
     }
 
     std::vector<Column> get_row(Row row) const override { return get_rows({row}).at(0); }
+
+    // BRWT::get_column (BRWT.cpp:55-85): ascending rows of the column
+    std::vector<Row> get_column(Column column) const override {
+        if (!ctx_) throw std::out_of_range("get_column on an empty BRWT");
+        uint64_t need = 0;
+        int st = mbrwt_get_column(ctx_.get(), column, nullptr, 0, &need);
+        std::vector<Row> rows;
+        if (st == MBRWT_OK) return rows;  // empty column
+        if (st != MBRWT_ERR_CAPACITY) check_status(st, "BRWTDevice::get_column");
+        rows.resize(need);
+        check_status(mbrwt_get_column(ctx_.get(), column, rows.data(), rows.size(), &need), "BRWTDevice::get_column");
+        rows.resize(need);
+        return rows;
+    }
 
     std::vector<std::vector<Column>> get_rows(const std::vector<Row> &rows) const override {
         std::vector<uint64_t> offsets;

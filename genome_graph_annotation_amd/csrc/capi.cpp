@@ -205,6 +205,51 @@ int mbrwt_get_rows(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n, uint64_t *o
     }
 }
 
+int mbrwt_get_column_device(mbrwt_ctx *ctx, uint64_t column, uint64_t *d_rows, uint64_t rows_cap,
+                            uint64_t *rows_needed, void *stream) {
+    if (!ctx) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    try {
+        MBRWT_HIP(hipSetDevice(c.device));
+        return run_get_column(c, column, d_rows, d_rows ? rows_cap : 0, rows_needed,
+                              reinterpret_cast<hipStream_t>(stream));
+    } catch (...) {
+        set_error("unexpected exception in mbrwt_get_column_device");
+        return MBRWT_ERR_INVALID;
+    }
+}
+
+int mbrwt_get_column(mbrwt_ctx *ctx, uint64_t column, uint64_t *rows, uint64_t rows_cap, uint64_t *rows_needed) {
+    if (!ctx) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    try {
+        MBRWT_HIP(hipSetDevice(c.device));
+        int rc;
+        uint64_t needed = 0;
+        // the column's size is known after the first (counting) phase
+        if ((rc = ensure(c.ws_out, std::max<uint64_t>(rows_cap, 1) * sizeof(uint64_t)))) return rc;
+        rc = run_get_column(c, column, reinterpret_cast<uint64_t *>(c.ws_out.buf), rows ? rows_cap : 0, &needed,
+                            c.stream);
+        if (rows_needed) *rows_needed = needed;
+        if (rc) return rc;
+        if (needed)
+            MBRWT_HIP(hipMemcpyAsync(rows, c.ws_out.buf, needed * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+        MBRWT_HIP(hipStreamSynchronize(c.stream));
+        return MBRWT_OK;
+    } catch (...) {
+        set_error("unexpected exception in mbrwt_get_column");
+        return MBRWT_ERR_INVALID;
+    }
+}
+
 int mbrwt_get_batch_device(mbrwt_ctx *ctx, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n,
                            uint8_t *d_out, void *stream) {
     if (!ctx || (n && (!d_rows || !d_cols || !d_out))) {

@@ -14,7 +14,6 @@ namespace {
 
 inline uint64_t popc(uint64_t x) { return (uint64_t)__builtin_popcountll(x); }
 
-inline bool bit_at(const uint64_t *w, uint64_t i) { return (w[i >> 6] >> (i & 63)) & 1; }
 
 uint64_t count_ones(const uint64_t *w, uint64_t size) {
     uint64_t c = 0, W = size / 64;

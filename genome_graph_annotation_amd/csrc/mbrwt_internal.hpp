@@ -175,6 +175,9 @@ inline bool fold_root_enabled() {
 }
 
 // queries (query.hip)
+// column query (column.hip): ascending rows of `column` into d_rows (u64)
+int run_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap, uint64_t *rows_needed,
+                   hipStream_t s);
 const char *traverse_kernel_name(const Ctx &c);  // the kernel mbrwt_get_rows* launches
 int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
                  uint64_t *needed, hipStream_t s);

@@ -10,6 +10,8 @@
  *   BinaryMatrix::get_row        common/binary_matrix.hpp:21      mbrwt_get_rows / _device (batched)
  *   BRWT::get_row                annotation/hierarchical_annotation/BRWT.cpp:26-53
  *   BRWT::get                    BRWT.cpp:9-24                     mbrwt_get_batch / _device
+ *   BRWT::get_column             BRWT.cpp:55-85 (select1,          mbrwt_get_column / _device
+ *                                bit_vector.cpp:863-869)
  *   bit_vector_rrr<63>::rank1    common/bit_vector.cpp:857-861     (inside the traversal kernel)
  *   bit_vector_rrr<63>::operator[]  common/bit_vector.cpp:884-888  (inside the traversal kernel)
  *   utils::RangePartition::get   common/utils.cpp:689-691          (leaf column table, composed)
@@ -125,6 +127,18 @@ int mbrwt_get_rows_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, ui
 int mbrwt_get_batch(mbrwt_ctx *ctx, const uint64_t *rows, const uint64_t *cols, uint64_t n, uint8_t *out);
 int mbrwt_get_batch_device(mbrwt_ctx *ctx, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n,
                            uint8_t *d_out, void *stream);
+
+/*
+ * BRWT::get_column (BRWT.cpp:55-85; BinaryMatrix::get_column,
+ * binary_matrix.hpp:21): the ascending rows carrying `column`, written to
+ * rows[0..*rows_needed).  If the column has more than rows_cap rows, returns
+ * MBRWT_ERR_CAPACITY with *rows_needed set and rows untouched (call with
+ * rows_cap = 0 to size the buffer).  column >= num_columns -> MBRWT_ERR_RANGE
+ * (an assert in the reference).  Host buffer / device buffer + stream.
+ */
+int mbrwt_get_column(mbrwt_ctx *ctx, uint64_t column, uint64_t *rows, uint64_t rows_cap, uint64_t *rows_needed);
+int mbrwt_get_column_device(mbrwt_ctx *ctx, uint64_t column, uint64_t *d_rows, uint64_t rows_cap,
+                            uint64_t *rows_needed, void *stream);
 
 /*
  * StaticBinRelAnnotator::count_labels (annotate_static.cpp:149-162) fused on

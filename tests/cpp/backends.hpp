@@ -40,6 +40,12 @@ class OracleMatrix : public BinaryMatrix {
         if (cnt == UINT64_MAX) throw std::out_of_range("oracle get_row");
         return std::vector<Column>(buf.begin(), buf.begin() + cnt);
     }
+    std::vector<Row> get_column(Column c) const override {
+        std::vector<uint64_t> buf(std::max<uint64_t>(1, num_rows()));
+        uint64_t cnt = oracle_get_column(t_.get(), c, buf.data(), buf.size());
+        if (cnt == UINT64_MAX) throw std::out_of_range("oracle get_column");
+        return std::vector<Row>(buf.begin(), buf.begin() + cnt);
+    }
     OracleTree *tree() const { return t_.get(); }
 
   private:

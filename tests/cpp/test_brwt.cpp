@@ -1,6 +1,7 @@
 // Grid tests of tests/test_BRWT.cpp:92-212 and tests/test_BRWT_optimizer.cpp
 // (reference) through the C++ mirror's BinaryMatrix interface, on the
 // backend named by argv[1] (oracle | device).
+#include <algorithm>
 #include <set>
 
 #include "backends.hpp"
@@ -16,7 +17,7 @@ static std::shared_ptr<BinaryMatrix> build(const Columns &cols, uint64_t n, uint
     return std::make_shared<mbrwt_host::BRWTDevice>(to_device(*om));
 }
 
-// test_brwt (test_BRWT.cpp:92-150) minus get_column (not on the device path)
+// test_brwt (test_BRWT.cpp:92-150)
 static void test_brwt(const BinaryMatrix &m, const Columns &columns, uint64_t n) {
     ASSERT_EQ(columns.size(), m.num_columns());
     if (columns.empty()) {
@@ -24,6 +25,19 @@ static void test_brwt(const BinaryMatrix &m, const Columns &columns, uint64_t n)
         return;
     }
     ASSERT_EQ(n, m.num_rows());
+    for (size_t j = 0; j < m.num_columns(); ++j) {  // get_column (test_BRWT.cpp:105-123)
+        auto bits = m.get_column(j);
+        std::set<uint64_t> s(bits.begin(), bits.end());
+        ASSERT_EQ(bits.size(), s.size());
+        uint64_t ones = 0;
+        for (uint64_t i = 0; i < n; ++i) ones += columns[j][i];
+        ASSERT_EQ(ones, bits.size());
+        for (auto i : bits) {
+            ASSERT_TRUE(i < m.num_rows());
+            ASSERT_TRUE(columns[j][i]);
+        }
+        EXPECT_TRUE(std::is_sorted(bits.begin(), bits.end()));
+    }
     std::vector<uint64_t> all(n);
     for (uint64_t i = 0; i < n; ++i) all[i] = i;
     auto rows = m.get_rows(all);
@@ -76,6 +90,7 @@ TEST(BRWT, OutOfRange) {  // the reference asserts (BRWT.cpp:27); the mirror thr
     auto m = build({std::vector<bool>(10, true)}, 10);
     EXPECT_THROW(m->get_row(10), std::out_of_range);
     EXPECT_THROW(m->get(0, 1), std::out_of_range);
+    EXPECT_THROW(m->get_column(1), std::out_of_range);
 }
 TEST(BRWT, BuildBottomUPAllZero) { grid(0, 0); }
 TEST(BRWT, BuildBottomUPAllOne) { grid(1, 0); }

@@ -220,3 +220,74 @@ def test_device_api_and_accounting(oracle_mod):
         d.count_labels_device(rt, cnt, s.cuda_stream)
         torch.cuda.synchronize()
         np.testing.assert_array_equal(cnt.cpu().numpy(), np.bincount(cols_o, minlength=m))
+
+
+# ---- BRWT::get_column (BRWT.cpp:55-85), §8f row 4 ------------------------------
+
+def _check_columns(oracle_tree, dev, cols):
+    for j in cols:
+        want = np.asarray(oracle_tree.get_column(int(j)), dtype=np.uint64)
+        got = dev.get_column(int(j))
+        np.testing.assert_array_equal(got, want, err_msg=f"column {j}")
+
+
+@pytest.mark.parametrize("kind", ["zero", "one", "mixed"])
+@pytest.mark.parametrize("build", [("basic", 2, 0), ("basic", 2, 2**64 - 1), ("greedy", 2, 0)])
+def test_get_column_reference_grids(oracle_mod, kind, build):
+    """test_BRWT.cpp:105-123 over the 1..19 x 1..19 grids: every column, the
+    ascending row list of the oracle (the dense matrix pins it too)."""
+    O = oracle_mod
+    part, arity, relax = build
+    for n in range(1, 20, 3):
+        for m in range(1, 20, 2):
+            dense = _grid(kind, n, m)
+            t = O.OracleTree.from_dense(dense, part, arity, relax)
+            d = _dev(t)
+            for j in range(m):
+                got = d.get_column(j)
+                np.testing.assert_array_equal(got, np.nonzero(dense[:, j])[0].astype(np.uint64))
+            _check_columns(t, d, range(m))
+
+
+@pytest.mark.parametrize("n,m,dens,part,arity", [
+    (5000, 40, 0.1, "greedy", 2),
+    (3000, 100, 0.05, "basic", 8),
+    (2000, 70, 0.3, "basic", 33),      # MASK64 leaf parents
+    (2000, 200, 0.02, "basic", 16),    # MASK16
+    (4000, 9, 0.5, "basic", 8),        # leaves directly under a PLANE node (8 + 1 columns)
+    (70_000, 5, 0.9, "basic", 2),      # long dense columns, several lift levels
+])
+def test_get_column_random(oracle_mod, n, m, dens, part, arity):
+    O = oracle_mod
+    rng = np.random.default_rng(n + m)
+    dense = rng.random((n, m)) < dens
+    t = O.OracleTree.from_dense(dense, part, arity)
+    d = _dev(t)
+    for j in range(m):
+        np.testing.assert_array_equal(d.get_column(j), np.nonzero(dense[:, j])[0].astype(np.uint64))
+
+
+def test_get_column_synthetic_and_errors(oracle_mod):
+    """Kingsford-shaped synthetic tree (root folded) and the capacity/range
+    protocol of mbrwt_get_column[_device]."""
+    import torch
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice, MBRWTError, _lib as L
+    n, m = 2_000_000, 2652
+    t = O.OracleTree.topdown(n, m, 0.003, 8, 42)
+    d = BRWTDevice.synthetic(n, m, 0.003, 8, 42)
+    cols = np.random.default_rng(4).integers(0, m, 48).tolist() + [0, m - 1]
+    _check_columns(t, d, cols)
+    with pytest.raises(MBRWTError) as ei:
+        d.get_column(m)
+    assert ei.value.status == L.MBRWT_ERR_RANGE
+    want = np.asarray(t.get_column(7), dtype=np.uint64)
+    small = torch.empty(max(0, len(want) - 1), dtype=torch.int64, device="cuda")
+    with pytest.raises(MBRWTError) as ei:
+        d.get_column_device(7, small)
+    assert ei.value.status == L.MBRWT_ERR_CAPACITY and ei.value.needed == len(want)
+    big = torch.empty(len(want) + 3, dtype=torch.int64, device="cuda")
+    got = d.get_column_device(7, big, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert got == len(want)
+    np.testing.assert_array_equal(big[:got].cpu().numpy().view(np.uint64), want)
