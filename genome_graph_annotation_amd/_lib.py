@@ -52,7 +52,25 @@ class SynthDesc(C.Structure):
     ]
 
 
-# every symbol include/mbrwt.h declares, with its signature
+class BinRelDesc(C.Structure):  # include/mbrwt_wt.h
+    _fields_ = [
+        ("num_rows", C.c_uint64),
+        ("num_columns", C.c_uint64),
+        ("offsets", u64p),
+        ("cols", u32p),
+    ]
+
+
+class BinRelSynthDesc(C.Structure):
+    _fields_ = [
+        ("num_rows", C.c_uint64),
+        ("num_columns", C.c_uint64),
+        ("density", C.c_double),
+        ("seed", C.c_uint64),
+    ]
+
+
+# every symbol include/mbrwt.h and include/mbrwt_wt.h declare, with its signature
 SIGNATURES = {
     "mbrwt_create": (C.c_int, [C.POINTER(TreeDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "mbrwt_create_synthetic": (C.c_int, [C.POINTER(SynthDesc), C.c_int, C.POINTER(C.c_void_p)]),
@@ -77,6 +95,24 @@ SIGNATURES = {
     "mbrwt_strerror": (C.c_char_p, [C.c_int]),
     "mbrwt_last_error_message": (C.c_char_p, []),
     "mbrwt_traverse_kernel": (C.c_char_p, [C.c_void_p]),
+    # include/mbrwt_wt.h (BinRel-WT)
+    "mbrwt_wt_create": (C.c_int, [C.POINTER(BinRelDesc), C.c_int, C.POINTER(C.c_void_p)]),
+    "mbrwt_wt_create_synthetic": (C.c_int, [C.POINTER(BinRelSynthDesc), C.c_int, C.POINTER(C.c_void_p)]),
+    "mbrwt_wt_destroy": (None, [C.c_void_p]),
+    "mbrwt_wt_num_rows": (C.c_uint64, [C.c_void_p]),
+    "mbrwt_wt_num_columns": (C.c_uint64, [C.c_void_p]),
+    "mbrwt_wt_num_relations": (C.c_uint64, [C.c_void_p]),
+    "mbrwt_wt_device_bytes": (C.c_uint64, [C.c_void_p]),
+    "mbrwt_wt_get_rows": (C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p, u32p, C.c_uint64, u64p]),
+    "mbrwt_wt_get_rows_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
+                                           u64p, C.c_void_p]),
+    "mbrwt_wt_get_batch": (C.c_int, [C.c_void_p, u64p, u64p, C.c_uint64, u8p]),
+    "mbrwt_wt_get_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                            C.c_void_p]),
+    "mbrwt_wt_get_column": (C.c_int, [C.c_void_p, C.c_uint64, u64p, C.c_uint64, u64p]),
+    "mbrwt_wt_get_column_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, u64p, C.c_void_p]),
+    "mbrwt_wt_set_option": (C.c_int, [C.c_void_p, C.c_int, C.c_int64]),
+    "mbrwt_wt_take_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), u64p]),
 }
 
 _lib = None

@@ -1,0 +1,103 @@
+// binrel_wt_device.hpp -- C++ host mirror of BinRelWT_sdsl over the device
+// engine (header-only, depends only on include/mbrwt_wt.h).
+//
+// Reference interface restated: class BinRelWT_sdsl : BinaryMatrix
+// (annotation/bin_rel_wt/bin_rel_wt_sdsl.hpp:9-43).  Constructed from the
+// rows generate_rows would emit (bin_rel_wt_sdsl.cpp:10-40); queries go to
+// the HIP wavelet-matrix kernels.  Out-of-range rows/columns (asserts / UB in
+// the reference) throw std::out_of_range.
+#pragma once
+
+#include <functional>
+
+#include "../../include/mbrwt_wt.h"
+#include "brwt_device.hpp"
+
+namespace mbrwt_host {
+
+class BinRelWTDevice : public BinaryMatrix {
+  public:
+    typedef std::vector<Column> RowSetBits;
+    typedef std::function<void(const RowSetBits &)> RowCallback;
+
+    BinRelWTDevice() = default;  // BinRelWT_sdsl(): no rows, no columns
+
+    // bin_rel_wt_sdsl.cpp:10-40 (num_relations is only a capacity hint here)
+    BinRelWTDevice(const std::function<void(const RowCallback &)> &generate_rows, uint64_t num_relations,
+                   uint64_t num_columns, int device = 0) {
+        std::vector<uint64_t> offsets{0};
+        std::vector<uint32_t> cols;
+        cols.reserve(num_relations);
+        generate_rows([&](const RowSetBits &row) {
+            for (auto c : row) cols.push_back((uint32_t)c);
+            offsets.push_back(cols.size());
+        });
+        mbrwt_binrel_desc d{offsets.size() - 1, num_columns, offsets.data(), cols.data()};
+        mbrwt_wt *c = nullptr;
+        check_status(mbrwt_wt_create(&d, device, &c), "mbrwt_wt_create");
+        ctx_.reset(c, Deleter());
+    }
+
+    static BinRelWTDevice synthetic(const mbrwt_binrel_synth_desc &desc, int device = 0) {
+        BinRelWTDevice m;
+        mbrwt_wt *c = nullptr;
+        check_status(mbrwt_wt_create_synthetic(&desc, device, &c), "mbrwt_wt_create_synthetic");
+        m.ctx_.reset(c, Deleter());
+        return m;
+    }
+
+    uint64_t num_columns() const override { return ctx_ ? mbrwt_wt_num_columns(ctx_.get()) : 0; }
+    uint64_t num_rows() const override { return ctx_ ? mbrwt_wt_num_rows(ctx_.get()) : 0; }
+    uint64_t num_relations() const override { return ctx_ ? mbrwt_wt_num_relations(ctx_.get()) : 0; }
+
+    bool get(Row row, Column column) const override {
+        if (!ctx_) throw std::out_of_range("get on an empty BinRelWT");
+        uint8_t out = 0;
+        check_status(mbrwt_wt_get_batch(ctx_.get(), &row, &column, 1, &out), "BinRelWTDevice::get");
+        return out != 0;
+    }
+
+    std::vector<Column> get_row(Row row) const override { return get_rows({row}).at(0); }
+
+    std::vector<std::vector<Column>> get_rows(const std::vector<Row> &rows) const override {
+        if (!ctx_) {
+            if (!rows.empty()) throw std::out_of_range("get_row on an empty BinRelWT");
+            return {};
+        }
+        std::vector<uint64_t> offsets(rows.size() + 1, 0);
+        std::vector<uint32_t> cols;
+        uint64_t need = 0;
+        int st = mbrwt_wt_get_rows(ctx_.get(), rows.data(), rows.size(), offsets.data(), nullptr, 0, &need);
+        if (st == MBRWT_ERR_CAPACITY) {
+            cols.resize(need);
+            st = mbrwt_wt_get_rows(ctx_.get(), rows.data(), rows.size(), offsets.data(), cols.data(), cols.size(),
+                                   &need);
+        }
+        check_status(st, "BinRelWTDevice::get_rows");
+        std::vector<std::vector<Column>> out(rows.size());
+        for (size_t i = 0; i < rows.size(); ++i) out[i].assign(cols.begin() + offsets[i], cols.begin() + offsets[i + 1]);
+        return out;
+    }
+
+    std::vector<Row> get_column(Column column) const override {
+        if (!ctx_) throw std::out_of_range("get_column on an empty BinRelWT");
+        uint64_t need = 0;
+        int st = mbrwt_wt_get_column(ctx_.get(), column, nullptr, 0, &need);
+        std::vector<Row> rows;
+        if (st == MBRWT_OK) return rows;
+        if (st != MBRWT_ERR_CAPACITY) check_status(st, "BinRelWTDevice::get_column");
+        rows.resize(need);
+        check_status(mbrwt_wt_get_column(ctx_.get(), column, rows.data(), rows.size(), &need),
+                     "BinRelWTDevice::get_column");
+        rows.resize(need);
+        return rows;
+    }
+
+  private:
+    struct Deleter {
+        void operator()(mbrwt_wt *c) const { mbrwt_wt_destroy(c); }
+    };
+    std::shared_ptr<mbrwt_wt> ctx_{nullptr, Deleter()};
+};
+
+}  // namespace mbrwt_host

@@ -63,6 +63,22 @@ def lib():
         "oracle_bv_get": (C.c_int, [vp, C.c_uint64]),
         "oracle_bv_num_set_bits": (C.c_uint64, [vp]),
         "oracle_synth_hash": (C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64]),
+        # BinRel-WT(sdsl) restatement (binrel_wt_oracle.h)
+        "wt_oracle_build": (vp, [u64p, u32p, C.c_uint64, C.c_uint64]),
+        "wt_oracle_empty": (vp, []),
+        "wt_oracle_free": (None, [vp]),
+        "wt_oracle_num_rows": (C.c_uint64, [vp]),
+        "wt_oracle_num_columns": (C.c_uint64, [vp]),
+        "wt_oracle_num_relations": (C.c_uint64, [vp]),
+        "wt_oracle_get_row": (C.c_uint64, [vp, C.c_uint64, u32p, C.c_uint64]),
+        "wt_oracle_get": (C.c_int, [vp, C.c_uint64, C.c_uint64]),
+        "wt_oracle_get_column": (C.c_uint64, [vp, C.c_uint64, u64p, C.c_uint64]),
+        "wt_oracle_get_rows": (C.c_int, [vp, u64p, C.c_uint64, u64p, u32p, C.c_uint64, u64p, C.c_int]),
+        "wt_oracle_time_rows": (C.c_double, [vp, u64p, C.c_uint64, C.c_int]),
+        "wt_synth_threshold": (C.c_uint64, [C.c_double]),
+        "wt_synth_row": (C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, u32p, C.c_uint64]),
+        "wt_synth_rows": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_double, C.c_uint64, u64p, u32p,
+                                    C.c_uint64, u64p, C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -266,3 +282,116 @@ def generate_columns(n, m, d, seed=42):
 
 def synth_hash(seed, key, pos):
     return lib().oracle_synth_hash(seed, key, pos)
+
+
+# ---- BinRel-WT(sdsl) (binrel_wt_oracle.h) ------------------------------------
+
+def dense_to_csr(dense: np.ndarray):
+    """rows of a dense bool matrix -> CSR (offsets u64, cols u32), ascending ids"""
+    dense = np.asarray(dense, dtype=bool)
+    counts = dense.sum(axis=1).astype(np.uint64)
+    offsets = np.zeros(dense.shape[0] + 1, dtype=np.uint64)
+    np.cumsum(counts, out=offsets[1:])
+    cols = np.nonzero(dense)[1].astype(np.uint32)
+    return offsets, cols
+
+
+def wt_synth_rows(row0, n, num_columns, density, seed=42, threads=0):
+    """CSR of synthetic BinRel rows [row0, row0+n) (DESIGN.md "BinRel-WT")."""
+    offsets = np.zeros(n + 1, dtype=np.uint64)
+    need = C.c_uint64(0)
+    dummy = np.zeros(1, dtype=np.uint32)
+    lib().wt_synth_rows(row0, n, num_columns, density, seed, _p64(offsets), _p32(dummy), 0, C.byref(need), threads)
+    cols = np.zeros(max(1, need.value), dtype=np.uint32)
+    rc = lib().wt_synth_rows(row0, n, num_columns, density, seed, _p64(offsets), _p32(cols), len(cols),
+                             C.byref(need), threads)
+    assert rc == 0
+    return offsets, cols[: need.value]
+
+
+class OracleWT:
+    """BinRelWT_sdsl restated (annotation/bin_rel_wt/bin_rel_wt_sdsl.cpp)."""
+
+    def __init__(self, handle):
+        if not handle:
+            raise ValueError("invalid BinRel-WT input")
+        self._h = handle
+
+    @classmethod
+    def from_csr(cls, offsets, cols, num_columns):
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        cols = np.ascontiguousarray(cols, dtype=np.uint32)
+        n = len(offsets) - 1
+        cptr = cols if len(cols) else np.zeros(1, dtype=np.uint32)
+        return cls(lib().wt_oracle_build(_p64(offsets), _p32(cptr), n, num_columns))
+
+    @classmethod
+    def from_dense(cls, dense):
+        dense = np.asarray(dense, dtype=bool)
+        off, cols = dense_to_csr(dense)
+        return cls.from_csr(off, cols, dense.shape[1] if dense.ndim == 2 else 0)
+
+    @classmethod
+    def empty(cls):
+        return cls(lib().wt_oracle_empty())
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().wt_oracle_free(self._h)
+            self._h = None
+
+    def num_rows(self):
+        return lib().wt_oracle_num_rows(self._h)
+
+    def num_columns(self):
+        return lib().wt_oracle_num_columns(self._h)
+
+    def num_relations(self):
+        return lib().wt_oracle_num_relations(self._h)
+
+    def get_row(self, row):
+        buf = np.zeros(max(1, self.num_columns() + 64), dtype=np.uint32)
+        cnt = lib().wt_oracle_get_row(self._h, row, _p32(buf), len(buf))
+        if cnt == 2**64 - 1:
+            raise IndexError(row)
+        if cnt > len(buf):
+            buf = np.zeros(cnt, dtype=np.uint32)
+            lib().wt_oracle_get_row(self._h, row, _p32(buf), len(buf))
+        return buf[:cnt].tolist()
+
+    def get(self, row, col):
+        v = lib().wt_oracle_get(self._h, row, col)
+        if v < 0:
+            raise IndexError((row, col))
+        return bool(v)
+
+    def get_column(self, col):
+        cap = max(1, self.num_rows())
+        out = np.zeros(cap, dtype=np.uint64)
+        cnt = lib().wt_oracle_get_column(self._h, col, _p64(out), cap)
+        if cnt == 2**64 - 1:
+            raise IndexError(col)
+        if cnt > cap:
+            out = np.zeros(cnt, dtype=np.uint64)
+            lib().wt_oracle_get_column(self._h, col, _p64(out), cnt)
+        return out[:cnt]
+
+    def get_rows(self, rows, threads=0):
+        rows = np.ascontiguousarray(rows, dtype=np.uint64)
+        n = len(rows)
+        offsets = np.zeros(n + 1, dtype=np.uint64)
+        need = C.c_uint64(0)
+        dummy = np.zeros(1, dtype=np.uint32)
+        rows_p = rows if n else np.zeros(1, dtype=np.uint64)
+        rc = lib().wt_oracle_get_rows(self._h, _p64(rows_p), n, _p64(offsets), _p32(dummy), 0, C.byref(need), threads)
+        if rc == 2:
+            raise IndexError("row out of range")
+        cols = np.zeros(max(1, need.value), dtype=np.uint32)
+        rc = lib().wt_oracle_get_rows(self._h, _p64(rows_p), n, _p64(offsets), _p32(cols), len(cols), C.byref(need),
+                                      threads)
+        assert rc == 0
+        return offsets, cols[: need.value]
+
+    def time_rows(self, rows, threads=0):
+        rows = np.ascontiguousarray(rows, dtype=np.uint64)
+        return lib().wt_oracle_time_rows(self._h, _p64(rows), len(rows), threads)

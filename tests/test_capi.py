@@ -1,5 +1,6 @@
 """The drop-in boundary: libmbrwt.so loads and exports every symbol that
-include/mbrwt.h declares; status strings and no-GPU error paths."""
+include/mbrwt.h and include/mbrwt_wt.h declare; status strings and no-GPU
+error paths."""
 import ctypes as C
 import os
 import re
@@ -10,9 +11,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_functions():
-    src = open(os.path.join(ROOT, "include", "mbrwt.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(mbrwt_[a-z_]+)\s*\(", src)))
+    names = set()
+    for h in ("mbrwt.h", "mbrwt_wt.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(mbrwt_[a-z_]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():
@@ -46,6 +50,12 @@ def test_null_arguments_fail_cleanly():
     assert lib.mbrwt_set_option(None, 1, 1) == L.MBRWT_ERR_INVALID
     assert lib.mbrwt_num_rows(None) == 0
     lib.mbrwt_destroy(None)
+    assert lib.mbrwt_wt_create(None, 0, C.byref(out)) == L.MBRWT_ERR_INVALID
+    assert lib.mbrwt_wt_create_synthetic(None, 0, C.byref(out)) == L.MBRWT_ERR_INVALID
+    assert lib.mbrwt_wt_get_rows(None, None, 0, None, None, 0, None) == L.MBRWT_ERR_INVALID
+    assert lib.mbrwt_wt_get_column(None, 0, None, 0, None) == L.MBRWT_ERR_INVALID
+    assert lib.mbrwt_wt_num_rows(None) == 0
+    lib.mbrwt_wt_destroy(None)
 
 
 def test_no_device_is_reported_not_faked():
@@ -56,3 +66,6 @@ def test_no_device_is_reported_not_faked():
     from genome_graph_annotation_amd import BRWTDevice, MBRWTError
     with pytest.raises(MBRWTError):
         BRWTDevice.synthetic(1000, 10, 0.1, 2, 1)
+    from genome_graph_annotation_amd import BinRelWTDevice
+    with pytest.raises(MBRWTError):
+        BinRelWTDevice.synthetic(1000, 10, 0.1, 1)
