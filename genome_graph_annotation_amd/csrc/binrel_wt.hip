@@ -392,11 +392,12 @@ int build_chunk(WtCtx &c, WtChunkDev &ch, uint32_t *d_sym, uint32_t *d_alt, uint
                                                (int)(nblk + 1), s));
     MBRWT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                                                 (int)std::max<uint64_t>(len, 1), 0, 1, s));
-    if ((rc = ensure(c.ws_c, (nwords + 2 * (nblk + 2)) * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c.ws_c, (nwords + 2 * (nblk + 2) + kWtMaxLevels) * sizeof(uint32_t)))) return rc;
     if ((rc = ensure(c.ws_scan, std::max(scan_bytes, sort_bytes) + 16))) return rc;
     uint32_t *d_words = reinterpret_cast<uint32_t *>(c.ws_c.buf);
     uint32_t *d_cnt = d_words + nwords;
     uint32_t *d_rank = d_cnt + nblk + 2;
+    uint32_t *d_ones = d_rank + nblk + 2;  // ones per level, read back once
     for (uint32_t l = 0; l < c.w; ++l) {
         const uint32_t sh = c.w - 1 - l;
         uint32_t *out = reinterpret_cast<uint32_t *>(ch.base + l * ch.level_bytes);
@@ -408,17 +409,18 @@ int build_chunk(WtCtx &c, WtChunkDev &ch, uint32_t *d_sym, uint32_t *d_alt, uint
         MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, d_cnt, d_rank, (int)(nblk + 1), s));
         hipLaunchKernelGGL(k_wt_blocks, dim3(grid_for(nblk + 1)), dim3(256), 0, s, d_words, nwords, d_rank, nblk, out);
         MBRWT_HIP(hipGetLastError());
-        MBRWT_HIP(hipMemcpyAsync(c.h_scalars, d_rank + nblk, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        MBRWT_HIP(hipStreamSynchronize(s));
-        uint32_t ones = 0;
-        std::memcpy(&ones, c.h_scalars, sizeof(uint32_t));
-        ch.zeros[l] = (uint32_t)(len - ones);
+        MBRWT_HIP(hipMemcpyAsync(d_ones + l, d_rank + nblk, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
         if (l + 1 < c.w && len) {  // stable partition by this bit = 1-bit radix pass
             MBRWT_HIP(hipcub::DeviceRadixSort::SortKeys(c.ws_scan.buf, sort_bytes, d_sym, d_alt, (int)len, (int)sh,
                                                         (int)sh + 1, s));
             std::swap(d_sym, d_alt);
         }
     }
+    uint32_t ones[kWtMaxLevels];
+    MBRWT_HIP(hipMemcpyAsync(c.h_scalars, d_ones, c.w * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    MBRWT_HIP(hipStreamSynchronize(s));
+    std::memcpy(ones, c.h_scalars, c.w * sizeof(uint32_t));
+    for (uint32_t l = 0; l < c.w; ++l) ch.zeros[l] = (uint32_t)(len - ones[l]);
     return MBRWT_OK;
 }
 
@@ -426,7 +428,7 @@ int init_common(WtCtx &c, int device, uint64_t num_rows, uint64_t num_columns) {
     c.device = device;
     MBRWT_HIP(hipSetDevice(device));
     MBRWT_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
-    MBRWT_HIP(hipHostMalloc(reinterpret_cast<void **>(&c.h_scalars), 8 * sizeof(uint64_t)));
+    MBRWT_HIP(hipHostMalloc(reinterpret_cast<void **>(&c.h_scalars), 32 * sizeof(uint64_t)));
     MBRWT_HIP(hipMalloc(&c.d_scalars, 8 * sizeof(uint64_t)));
     MBRWT_HIP(hipEventCreate(&c.ev0));
     MBRWT_HIP(hipEventCreate(&c.ev1));
