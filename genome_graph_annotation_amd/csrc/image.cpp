@@ -294,6 +294,18 @@ int finalize_tree(Tree &tree) {
     }
     tree.path_len = std::max<uint32_t>(1, max_depth);
     if (tree.stack_depth > kFastMaxDepth) tree.fast_shape = false;
+    // frames the fast kernels push: PLANE nodes not resolved inline (no FLAG_MASK_CHILDREN)
+    {
+        std::vector<uint32_t> fr(D, 0);
+        tree.push_frames = 0;
+        for (uint32_t v = 0; v < D; ++v) {  // BFS order: parents first
+            const DevNode &dn = tree.nodes[v];
+            const uint32_t here = (parent[v] == UINT32_MAX ? 0 : fr[parent[v]]) +
+                                  ((dn.kind == KIND_PLANE && !(dn.flags & FLAG_MASK_CHILDREN)) ? 1 : 0);
+            fr[v] = here;
+            tree.push_frames = std::max(tree.push_frames, here);
+        }
+    }
     tree.lds_complete = true;
     for (uint32_t v = kLdsNodes; v < D; ++v)
         if (tree.nodes[v].kind != KIND_LEAF) tree.lds_complete = false;

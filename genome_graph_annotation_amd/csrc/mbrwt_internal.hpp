@@ -113,6 +113,7 @@ struct Tree {
     bool folded = false;                    // root folded into the super-root
     bool fast_shape = false;                // eligible for k_traverse_fast (finalize_tree)
     bool lds_complete = false;              // every non-leaf dnode id < kLdsNodes (k_traverse_fast2)
+    uint32_t push_frames = 0;               // max stack frames of the fast kernels (non-TERM PLANE nodes on a path)
     uint32_t max_arity = 0;
     uint64_t num_rows = 0, num_columns = 0, num_relations = 0, num_nodes = 0;
     uint64_t image_bytes = 0;

@@ -792,7 +792,7 @@ __device__ __forceinline__ uint32_t quad_exclusive_sum(uint32_t v, uint32_t c, u
 // a FLAG_MASK_CHILDREN visit are not serialised behind a global-fallback
 // wait; the label stage is flushed as 16-byte vectors.
 // ------------------------------------------------------------------------
-template <bool NT, bool SMALLK>
+template <bool NT, bool SMALLK, bool DIAG = false>
 __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
     constexpr uint64_t M48 = (1ull << 48) - 1;
     const uint32_t lane = threadIdx.x & 63;
@@ -930,12 +930,13 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
             uint32_t m0 = 0, m1 = 0, l0 = 0, l1 = 0;
             if (b0) {
                 const uint32_t w = fc + 2 * c;
-                m0 = gld_at_nt<uint8_t, NT>((lds_nodes[2 * w] & M48) + j0);
+                // DIAG (variant 21, measurement only, wrong labels): no mask read
+                m0 = DIAG ? 1u << (j0 & 7) : gld_at_nt<uint8_t, NT>((lds_nodes[2 * w] & M48) + j0);
                 l0 = (uint32_t)(lds_nodes[2 * w + 1] >> 32);
             }
             if (b1) {
                 const uint32_t w = fc + 2 * c + 1;
-                m1 = gld_at_nt<uint8_t, NT>((lds_nodes[2 * w] & M48) + j1);
+                m1 = DIAG ? 1u << (j1 & 7) : gld_at_nt<uint8_t, NT>((lds_nodes[2 * w] & M48) + j1);
                 l1 = (uint32_t)(lds_nodes[2 * w + 1] >> 32);
             }
             const uint32_t s0 = (uint32_t)__builtin_popcount(m0) + (uint32_t)__builtin_popcount(m1);
@@ -963,6 +964,214 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
             jc1[0] = j1;
             fp[0] = (fc << 8) | P;
             ++sp;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
+// k_traverse_fast3: k_traverse_fast2 with TWO row contexts per group.  Each
+// iteration visits one node of each context, and the phases of the two
+// visits are interleaved (both block reads issued, then both sets of child
+// mask reads), so a group keeps two independent dependent-load chains in
+// flight -- the traversal is latency-bound with occupancy already at its
+// cap, and this doubles the memory-level parallelism per wave.  Needs
+// <= kF3Frames stack frames (two for the basic arity-8 partitioner: the
+// super-root's and the level-1 node's; FLAG_MASK_CHILDREN nodes push none).
+// ------------------------------------------------------------------------
+constexpr uint32_t kF3Frames = 2;
+
+template <bool NT, bool SMALLK>
+__global__ __launch_bounds__(256, 6) void k_traverse_fast3(TravParams p) {
+    constexpr uint64_t M48 = (1ull << 48) - 1;
+    constexpr uint32_t F = kF3Frames;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t c = lane & 3;
+    const uint32_t gbase = lane & ~3u;
+    const uint64_t gid = (uint64_t)blockIdx.x * 64 + threadIdx.x / 4;
+    const uint64_t ngroups = (uint64_t)gridDim.x * 64;
+
+    // LDS: 2 x 64 groups x kStageLabels label stages | 2 x 64 groups x 8 row ids | node records
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_stage[];
+    AS_LDS uint32_t *stage0 = (AS_LDS uint32_t *)lds_stage + (threadIdx.x / 4) * kStageLabels;
+    AS_LDS uint32_t *stage1 = stage0 + 64 * kStageLabels;
+    AS_LDS uint32_t *rowbuf = (AS_LDS uint32_t *)lds_stage + 128 * kStageLabels + (threadIdx.x / 4) * 16;
+    AS_LDS uint64_t *lds_nodes = (AS_LDS uint64_t *)((AS_LDS uint32_t *)lds_stage + 128 * kStageLabels + 64 * 16);
+    const uint64_t *gnodes = reinterpret_cast<const uint64_t *>(p.cnodes);
+    for (uint32_t i = threadIdx.x; i < 2 * p.n_lds; i += blockDim.x) lds_nodes[i] = gld(gnodes + i);
+    __syncthreads();
+
+    uint32_t jc0[2][F], jc1[2][F], fp[2][F];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int k = 0; k < (int)F; ++k) jc0[x][k] = jc1[x][k] = fp[x][k] = 0;
+    // (launch guarantees n < 2^34, so chunk indices fit u32)
+    int sp[2] = {0, 0};
+    uint32_t cnt[2] = {0, 0}, ri[2] = {0, 0};
+    uint32_t chunk[2] = {(uint32_t)(2 * gid), (uint32_t)(2 * gid + 1)};
+    const uint32_t cstride = (uint32_t)(2 * ngroups);
+    bool active[2], fresh[2];
+    auto slot_of = [&](int x) -> uint64_t { return (uint64_t)chunk[x] * 8 + ri[x]; };
+    // the 8 row ids of a context's chunk -> LDS (2 per lane; ids >= num_rows -> 0xFFFFFFFF)
+    auto load_chunk = [&](int x) {
+        const uint64_t sb = (uint64_t)chunk[x] * 8 + 2 * c;
+        const uint64_t a0 = sb < p.n ? gld(p.rows + sb) : 0, a1 = sb + 1 < p.n ? gld(p.rows + sb + 1) : 0;
+        rowbuf[8 * x + 2 * c] = a0 < p.num_rows ? (uint32_t)a0 : 0xFFFFFFFFu;
+        rowbuf[8 * x + 2 * c + 1] = a1 < p.num_rows ? (uint32_t)a1 : 0xFFFFFFFFu;
+    };
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+        active[x] = fresh[x] = slot_of(x) < p.n;
+        if (active[x]) load_chunk(x);
+    }
+    auto emit = [&](int x, uint32_t pos, uint32_t label) {
+        if (pos < kStageLabels) (x ? stage1 : stage0)[pos] = label;
+        else if (!SMALLK && pos < p.K) gst(p.temp + slot_of(x) * p.K + pos, label);
+    };
+
+    while (true) {
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            if (active[x] && !fresh[x] && sp[x] == 0) {  // row done: flush, count, next slot
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                AS_LDS uint32_t *st = x ? stage1 : stage0;
+                const uint32_t lim = cnt[x] < kStageLabels ? cnt[x] : kStageLabels;
+                const uint64_t slot = slot_of(x);
+                uint32_t *sp_out = p.temp + slot * p.K;
+                for (uint32_t q = c; 4 * q < lim; q += 4)
+                    gst(reinterpret_cast<u32x4_t *>(sp_out) + q, (u32x4_t)((AS_LDS u32x4_t *)st)[q]);
+                if (c == 0) {
+                    gst(p.counts + slot, cnt[x]);
+                    if (cnt[x] > p.K) {
+                        const unsigned long long k = atomicAdd(&p.scalars[1], 1ull);
+                        gst(p.ovf_list + k, (uint32_t)slot);
+                    }
+                }
+                if (++ri[x] == 8) {
+                    ri[x] = 0;
+                    chunk[x] += cstride;
+                    if ((uint64_t)chunk[x] * 8 < p.n) load_chunk(x);
+                }
+                active[x] = slot_of(x) < p.n;
+                fresh[x] = active[x];
+            }
+        }
+        if (!__any(active[0] || active[1])) break;
+
+        // phase 1: the node each context visits (root of a fresh row or next child)
+        uint64_t w0[2] = {0, 0}, w1[2] = {0, 0};
+        uint32_t j[2] = {0, 0};
+        bool go[2] = {false, false};
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            if (!active[x]) continue;
+            if (fresh[x]) {
+                fresh[x] = false;
+                cnt[x] = 0;
+                j[x] = rowbuf[8 * x + ri[x]];
+                w0[x] = lds_nodes[0];
+                w1[x] = lds_nodes[1];
+                go[x] = (uint64_t)j[x] < p.num_rows;
+                if (!go[x] && c == 0) atomicOr(&p.scalars[2], 1ull);
+            } else {
+                uint32_t top = fp[x][0];
+                const uint32_t cs = (uint32_t)__builtin_ctz(top & 0xFFu);
+                top &= top - 1;
+                fp[x][0] = top;
+                const uint32_t w = (top >> 8) + cs;
+                const uint32_t jsel = (cs & 1) ? jc1[x][0] : jc0[x][0];
+                j[x] = (uint32_t)__shfl((int)jsel, (int)(gbase + (cs >> 1)), 64);
+                if ((top & 0xFFu) == 0) {
+#pragma unroll
+                    for (int k = 0; k < (int)F - 1; ++k) {
+                        jc0[x][k] = jc0[x][k + 1];
+                        jc1[x][k] = jc1[x][k + 1];
+                        fp[x][k] = fp[x][k + 1];
+                    }
+                    --sp[x];
+                }
+                w0[x] = lds_nodes[2 * w];
+                w1[x] = lds_nodes[2 * w + 1];
+                go[x] = true;
+            }
+        }
+        // phase 2: both block (or root mask) reads in flight together
+        uint4 q[2];
+        uint32_t mr[2] = {0, 0};
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            q[x] = make_uint4(0, 0, 0, 0);
+            if (!go[x]) continue;
+            const uint64_t base = w0[x] & M48;
+            if (((uint32_t)(w0[x] >> 48) & 7u) == KIND_MASK8) {
+                mr[x] = gld_at_nt<uint8_t, NT>(base + j[x]);
+            } else if (2 * c < (uint32_t)(w0[x] >> 56)) {
+                const uint32_t stride = 1u << ((uint32_t)(w0[x] >> 52) & 15u);
+                q[x] = gld_at_nt<uint4, NT>(base + (uint64_t)(j[x] >> 5) * stride + 16u * c);
+            }
+        }
+        // phase 3: children bits and positions; FLAG_MASK_CHILDREN mask reads in flight together
+        uint32_t b0[2], b1[2], j0[2], j1[2], m0[2] = {0, 0}, m1[2] = {0, 0}, l0[2] = {0, 0}, l1[2] = {0, 0};
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            const uint32_t t = j[x] & 31, below = (1u << t) - 1u;
+            const uint32_t a = (uint32_t)(w0[x] >> 56);
+            b0[x] = (q[x].y >> t) & 1u;
+            b1[x] = (2 * c + 1 < a) ? (q[x].w >> t) & 1u : 0u;
+            j0[x] = q[x].x + (uint32_t)__builtin_popcount(q[x].y & below);
+            j1[x] = q[x].z + (uint32_t)__builtin_popcount(q[x].w & below);
+            if (go[x] && ((uint32_t)(w0[x] >> 48) & 15u) == (KIND_PLANE | 8u)) {
+                const uint32_t fc = (uint32_t)w1[x];
+                if (b0[x]) {
+                    const uint32_t w = fc + 2 * c;
+                    m0[x] = gld_at_nt<uint8_t, NT>((lds_nodes[2 * w] & M48) + j0[x]);
+                    l0[x] = (uint32_t)(lds_nodes[2 * w + 1] >> 32);
+                }
+                if (b1[x]) {
+                    const uint32_t w = fc + 2 * c + 1;
+                    m1[x] = gld_at_nt<uint8_t, NT>((lds_nodes[2 * w] & M48) + j1[x]);
+                    l1[x] = (uint32_t)(lds_nodes[2 * w + 1] >> 32);
+                }
+            }
+        }
+        // phase 4: labels / push
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            if (!go[x]) continue;
+            const uint32_t kind = (uint32_t)(w0[x] >> 48) & 15u;
+            if ((kind & 7u) == KIND_MASK8) {  // root with leaf children
+                const uint32_t m = mr[x], lb = (uint32_t)(w1[x] >> 32);
+#pragma unroll
+                for (uint32_t qq = 0; qq < 2; ++qq) {
+                    const uint32_t cc = 2 * c + qq;
+                    if ((m >> cc) & 1u) emit(x, cnt[x] + (uint32_t)__builtin_popcount(m & ((1u << cc) - 1u)), lb + cc);
+                }
+                cnt[x] += (uint32_t)__builtin_popcount(m);
+            } else if (kind == (KIND_PLANE | 8u)) {
+                uint32_t ma = m0[x], mb = m1[x];
+                const uint32_t s0 = (uint32_t)__builtin_popcount(ma) + (uint32_t)__builtin_popcount(mb);
+                uint32_t total;
+                uint32_t pos = cnt[x] + quad_exclusive_sum(s0, c, total);
+                for (; ma; ma &= ma - 1) emit(x, pos++, l0[x] + (uint32_t)__builtin_ctz(ma));
+                for (; mb; mb &= mb - 1) emit(x, pos++, l1[x] + (uint32_t)__builtin_ctz(mb));
+                cnt[x] += total;
+            } else {
+                const uint32_t P = quad_or((b0[x] | (b1[x] << 1)) << (2 * c));
+                if (P) {
+#pragma unroll
+                    for (int k = F - 1; k > 0; --k) {
+                        jc0[x][k] = jc0[x][k - 1];
+                        jc1[x][k] = jc1[x][k - 1];
+                        fp[x][k] = fp[x][k - 1];
+                    }
+                    jc0[x][0] = j0[x];
+                    jc1[x][0] = j1[x];
+                    fp[x][0] = ((uint32_t)w1[x] << 8) | P;
+                    ++sp[x];
+                }
+            }
         }
     }
 }
@@ -1064,6 +1273,7 @@ struct Trav {
     GroupFn group_fn = nullptr;
     uint32_t G = 1;  // lanes per row
     bool fast = false;
+    bool dual = false;  // k_traverse_fast3: two row contexts per group
     const char *name = "k_traverse_group";
     explicit operator bool() const { return fn != nullptr; }
 };
@@ -1075,7 +1285,7 @@ Trav pick_traverse(const Ctx &c) {
     const uint32_t depth = c.tree.stack_depth, max_arity = c.tree.max_arity;
     Trav t;
     const int kv = c.kernel_variant;
-    if (MODE == MODE_SLOTS && c.tree.fast_shape && (kv == 0 || (kv >= 11 && kv <= 14) || kv == 17 || kv == 18)) {
+    if (MODE == MODE_SLOTS && c.tree.fast_shape && (kv == 0 || (kv >= 11 && kv <= 14) || (kv >= 17 && kv <= 21))) {
         // 11/12: fast kernel without / with non-temporal reads; 13/14: the same
         // without resolving FLAG_MASK_CHILDREN nodes' children inline (A/B)
         const bool nt = kv == 12 || kv == 14 || kv == 18 || (kv == 0 && c.tree.image_bytes > (1ull << 30));
@@ -1087,6 +1297,22 @@ Trav pick_traverse(const Ctx &c) {
         t.fast = true;
         const bool smallk = auto_slots(c) == kStageLabels;
         t.name = v2 ? "k_traverse_fast2" : "k_traverse_fast";
+        if (kv == 21 && c.tree.lds_complete && smallk) {  // diagnostic: fast2 without the MASK8 reads
+            t.name = "k_traverse_fast2_diag";
+            t.lane_fn = (TravFn)k_traverse_fast2<true, true, true>;
+            t.fn = reinterpret_cast<const void *>(t.lane_fn);
+            return t;
+        }
+        if ((kv == 19 || kv == 20) && c.tree.lds_complete && c.tree.push_frames <= kF3Frames) {
+            // 19/20: k_traverse_fast3 without / with non-temporal reads
+            const bool nt3 = kv == 20;
+            t.dual = true;
+            t.name = "k_traverse_fast3";
+            if (smallk) t.lane_fn = nt3 ? (TravFn)k_traverse_fast3<true, true> : (TravFn)k_traverse_fast3<false, true>;
+            else t.lane_fn = nt3 ? (TravFn)k_traverse_fast3<true, false> : (TravFn)k_traverse_fast3<false, false>;
+            t.fn = reinterpret_cast<const void *>(t.lane_fn);
+            return t;
+        }
         if (v2 && smallk) t.lane_fn = nt ? (TravFn)k_traverse_fast2<true, true> : (TravFn)k_traverse_fast2<false, true>;
         else if (v2) t.lane_fn = nt ? (TravFn)k_traverse_fast2<true, false> : (TravFn)k_traverse_fast2<false, false>;
         else if (term) t.lane_fn = nt ? (TravFn)k_traverse_fast<true, true> : (TravFn)k_traverse_fast<false, true>;
@@ -1153,7 +1379,8 @@ Trav pick_traverse(const Ctx &c) {
 size_t lds_bytes(const Ctx &c, const Trav &t) {
     if (!t.group_fn && !t.fast) return 0;
     const size_t nl = std::min<size_t>(c.tree.nodes.size(), kLdsNodes);
-    return (size_t)(256 / t.G) * kStageLabels * sizeof(uint32_t) + nl * sizeof(CNode);
+    return (size_t)(256 / t.G) * kStageLabels * sizeof(uint32_t) * (t.dual ? 2 : 1) + (t.dual ? 64 * 16 * 4 : 0) +
+           nl * sizeof(CNode);
 }
 
 int grid_for(const Ctx &c, const Trav &t, uint64_t n) {
@@ -1163,7 +1390,8 @@ int grid_for(const Ctx &c, const Trav &t, uint64_t n) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, t.fn, 256, lds_bytes(c, t)) != hipSuccess || per_cu <= 0)
         per_cu = 4;
     const uint64_t resident = (uint64_t)std::max(1, dev_cus) * (uint64_t)per_cu;
-    const uint64_t rows_per_block = t.fast ? 512 : 256 / t.G;  // fast: 64 groups x 8-row chunks
+    // fast: 64 groups x 8-row chunks (x 2 contexts for fast3)
+    const uint64_t rows_per_block = t.fast ? (t.dual ? 1024 : 512) : 256 / t.G;
     const uint64_t need = (n + rows_per_block - 1) / rows_per_block;
     return (int)std::max<uint64_t>(1, std::min(need, resident));
 }

@@ -164,7 +164,8 @@ int mbrwt_count_work_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, 
                                     2/3/4 group with 1/2/4 children per lane, 5/6 group at 8/6 waves per SIMD,
                                     10 group + non-temporal reads, 11/12 fast kernel (+ non-temporal),
                                     13/14 fast kernel without inline MASK8 children,
-                                    17/18 fast2 kernel (+ non-temporal; the default where eligible); others rejected */
+                                    17/18 fast2 kernel (+ non-temporal; the default where eligible),
+                                    19/20 fast3 (two rows per group); others rejected */
 int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value);
 
 /* Traversal-kernel time accumulated while MBRWT_OPT_TIMING is on (ms, launches); resets the sums. */

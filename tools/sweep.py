@@ -38,7 +38,7 @@ rows = torch.from_numpy(rows_np.view(np.int64)).cuda()
 off = torch.empty(a.batch + 1, dtype=torch.int64, device="cuda")
 s = torch.cuda.current_stream().cuda_stream
 v, lab = m.count_work_device(rows, s)
-cols = torch.empty(lab + 1024, dtype=torch.int32, device="cuda")
+cols = torch.empty(2 * lab + 1024, dtype=torch.int32, device="cuda")  # diagnostic variants may emit more
 alg = 64 * v + 16 * a.batch + 4 * lab
 variants = [int(x) for x in a.variants.split(",")]
 sorts = [0]
