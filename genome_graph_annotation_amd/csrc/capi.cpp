@@ -322,7 +322,7 @@ int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value) {
         c.slot_labels = (uint32_t)value;
         return MBRWT_OK;
     case MBRWT_OPT_KERNEL:
-        if (value < 0 || value > 21 || (value >= 7 && value <= 9) || value == 15 || value == 16) return MBRWT_ERR_INVALID;
+        if (!(value >= 0 && value <= 6) && value != 10 && value != 17 && value != 18) return MBRWT_ERR_INVALID;
         c.kernel_variant = (int)value;
         return MBRWT_OK;
     default:

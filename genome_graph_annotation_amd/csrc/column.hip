@@ -18,6 +18,7 @@
 
 #include "device_access.hpp"
 #include "mbrwt_internal.hpp"
+#include "pack_block.hpp"
 
 namespace mbrwt {
 namespace {
@@ -25,11 +26,29 @@ namespace {
 constexpr int kColThreads = 256;  // one thread = one 32-position word
 
 // Word w (positions 32w .. 32w+31, clipped to len) of child slot c's column
-// inside the image of node nd.
-__device__ __forceinline__ uint32_t column_word(const DevNode &nd, uint32_t c, uint64_t w, uint64_t len) {
+// inside the image of node nd.  For a KIND_PACK node the word marks the
+// positions where child c is set AND its MASK8 mask has bit `leaf` (the
+// leaf's positions lifted through the image-less MASK8 child at once).
+__device__ __forceinline__ uint32_t column_word(const DevNode &nd, uint32_t c, uint64_t w, uint64_t len,
+                                                uint32_t leaf) {
     if (32 * w >= len) return 0;
     uint32_t bits = 0;
-    if (nd.kind == KIND_PLANE) {
+    if (nd.kind == KIND_PACK) {
+        for (uint32_t h = 0; h < 32 / kPackSpan; ++h) {
+            const uint64_t j0 = 32 * w + kPackSpan * h;
+            if (j0 >= len) break;
+            PackBlock pb;
+            pb.load(nd.base, (uint32_t)j0);
+            uint32_t o = 0;
+            for (uint32_t q = 0; q < c; ++q) o += (uint32_t)__builtin_popcount(pb.bits(q));
+            uint32_t bc = pb.bits(c);
+            for (uint32_t x = bc; x; x &= x - 1) {
+                const uint32_t t = (uint32_t)__builtin_ctz(x);
+                const uint32_t m = pb.mask(o + (uint32_t)__builtin_popcount(bc & ((1u << t) - 1u)));
+                if ((m >> leaf) & 1u) bits |= 1u << (kPackSpan * h + t);
+            }
+        }
+    } else if (nd.kind == KIND_PLANE) {
         bits = gld_at<uint32_t>(nd.base + w * nd.stride + 8u * c + 4u);
     } else {
         const uint32_t W = 1u << (nd.kind - KIND_MASK8);
@@ -49,22 +68,23 @@ __device__ __forceinline__ uint32_t column_word(const DevNode &nd, uint32_t c, u
     return bits;
 }
 
-__global__ __launch_bounds__(kColThreads) void k_col_count(DevNode nd, uint32_t c, uint64_t len, uint64_t nwords,
-                                                           uint64_t *block_counts) {
+__global__ __launch_bounds__(kColThreads) void k_col_count(DevNode nd, uint32_t c, uint32_t leaf, uint64_t len,
+                                                           uint64_t nwords, uint64_t *block_counts) {
     using Reduce = hipcub::BlockReduce<uint32_t, kColThreads>;
     __shared__ typename Reduce::TempStorage tmp;
     const uint64_t w = (uint64_t)blockIdx.x * kColThreads + threadIdx.x;
-    const uint32_t n = w < nwords ? (uint32_t)__builtin_popcount(column_word(nd, c, w, len)) : 0u;
+    const uint32_t n = w < nwords ? (uint32_t)__builtin_popcount(column_word(nd, c, w, len, leaf)) : 0u;
     const uint32_t total = Reduce(tmp).Sum(n);
     if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(kColThreads) void k_col_write(DevNode nd, uint32_t c, uint64_t len, uint64_t nwords,
-                                                           const uint64_t *block_offsets, uint32_t *out) {
+__global__ __launch_bounds__(kColThreads) void k_col_write(DevNode nd, uint32_t c, uint32_t leaf, uint64_t len,
+                                                           uint64_t nwords, const uint64_t *block_offsets,
+                                                           uint32_t *out) {
     using Scan = hipcub::BlockScan<uint32_t, kColThreads>;
     __shared__ typename Scan::TempStorage tmp;
     const uint64_t w = (uint64_t)blockIdx.x * kColThreads + threadIdx.x;
-    uint32_t bits = w < nwords ? column_word(nd, c, w, len) : 0u;
+    uint32_t bits = w < nwords ? column_word(nd, c, w, len, leaf) : 0u;
     uint32_t pre;
     Scan(tmp).ExclusiveSum((uint32_t)__builtin_popcount(bits), pre);
     uint64_t o = block_offsets[blockIdx.x] + pre;
@@ -128,6 +148,14 @@ int run_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap,
         set_error("inconsistent column path");
         return MBRWT_ERR_INVALID;
     }
+    // the leaf's positions come out of its parent's image -- or, when that
+    // parent is a MASK8 child of a KIND_PACK node, out of the PACK image
+    // (positions in the PACK node's space; the MASK8 level has no image)
+    uint32_t leaf_bit = 0;
+    if (path.size() >= 2 && t.nodes[path[path.size() - 2].first].kind == KIND_PACK) {
+        leaf_bit = path.back().second;
+        path.pop_back();
+    }
     const DevNode leaf_parent = t.nodes[path.back().first];
     const uint32_t leaf_slot = path.back().second;
     const uint64_t len = leaf_parent.length;
@@ -143,8 +171,8 @@ int run_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap,
     uint64_t *d_cnt = reinterpret_cast<uint64_t *>(c.ws_counts.buf);
     uint64_t *d_off = d_cnt + nblk + 1;
     if (nwords) {
-        hipLaunchKernelGGL(k_col_count, dim3((unsigned)nblk), dim3(kColThreads), 0, s, leaf_parent, leaf_slot, len,
-                           nwords, d_cnt);
+        hipLaunchKernelGGL(k_col_count, dim3((unsigned)nblk), dim3(kColThreads), 0, s, leaf_parent, leaf_slot, leaf_bit,
+                           len, nwords, d_cnt);
         MBRWT_HIP(hipGetLastError());
     } else {
         MBRWT_HIP(hipMemsetAsync(d_cnt, 0, nblk * sizeof(uint64_t), s));
@@ -163,8 +191,8 @@ int run_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap,
 
     if ((rc = ensure(c.ws_temp, total * sizeof(uint32_t)))) return rc;
     uint32_t *d_pos = reinterpret_cast<uint32_t *>(c.ws_temp.buf);
-    hipLaunchKernelGGL(k_col_write, dim3((unsigned)nblk), dim3(kColThreads), 0, s, leaf_parent, leaf_slot, len, nwords,
-                       d_off, d_pos);
+    hipLaunchKernelGGL(k_col_write, dim3((unsigned)nblk), dim3(kColThreads), 0, s, leaf_parent, leaf_slot, leaf_bit,
+                       len, nwords, d_off, d_pos);
     MBRWT_HIP(hipGetLastError());
     // lift through the ancestors: node path[k+1].first's column lives in the
     // image of path[k].first at slot path[k].second

@@ -87,6 +87,97 @@ int upload_image(const std::vector<const uint64_t *> &child_words, const std::ve
     return MBRWT_OK;
 }
 
+// KIND_PACK image of desc node u (mbrwt_internal.hpp): returns false (and
+// builds nothing) when more than 1 block in 20 would spill.
+bool build_pack_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, DevNode &dn, std::vector<void *> &images,
+                      uint64_t &image_bytes, int &rc) {
+    rc = MBRWT_OK;
+    const uint32_t a = desc.num_children[u], fc = desc.first_child[u];
+    const uint64_t blocks = (L + kPackSpan - 1) / kPackSpan;
+    std::vector<uint8_t> host(blocks * kPackBlock + kImagePad, 0);
+    std::vector<uint8_t> spill;
+    std::vector<std::pair<uint64_t, uint64_t>> spilled;  // (block, offset in spill)
+    std::vector<uint64_t> rank(a, 0);
+    for (uint64_t b = 0; b < blocks; ++b) {
+        uint8_t *blk = &host[b * kPackBlock];
+        std::vector<uint8_t> masks;
+        for (uint32_t c = 0; c < a; ++c) {
+            const uint32_t ch = fc + c;
+            const uint64_t *cw = desc.vec_words[ch];
+            uint32_t bits = 0;
+            for (uint32_t t = 0; t < kPackSpan && b * kPackSpan + t < L; ++t) {
+                const uint64_t j = b * kPackSpan + t;
+                if ((cw[j >> 6] >> (j & 63)) & 1) bits |= 1u << t;
+            }
+            const uint16_t b16 = (uint16_t)bits;
+            std::memcpy(blk + 16 * (c / 2) + 2 * (c % 2), &b16, 2);
+            const uint32_t gc = desc.num_children[ch], gfc = desc.first_child[ch];
+            for (uint32_t x = bits; x; x &= x - 1) {
+                const uint64_t jc = rank[c]++;
+                uint32_t m = 0;
+                for (uint32_t k = 0; k < gc; ++k) {
+                    const uint64_t *lw = desc.vec_words[gfc + k];
+                    if ((lw[jc >> 6] >> (jc & 63)) & 1) m |= 1u << k;
+                }
+                masks.push_back((uint8_t)m);
+            }
+        }
+        if (masks.size() <= kPackArea) {
+            for (uint32_t o = 0; o < masks.size(); ++o) blk[pack_area_byte(o)] = masks[o];
+        } else {
+            spilled.emplace_back(b, spill.size());
+            spill.insert(spill.end(), masks.begin(), masks.end());
+        }
+    }
+    if (spilled.size() * 20 > blocks) return false;
+    void *ds = nullptr;
+    if (!spill.empty()) {
+        spill.resize(spill.size() + kImagePad, 0);
+        if (hipMalloc(&ds, spill.size()) != hipSuccess || hipMemcpy(ds, spill.data(), spill.size(),
+                                                                      hipMemcpyHostToDevice) != hipSuccess) {
+            rc = hip_fail(hipErrorOutOfMemory, "pack spill upload");
+            return true;
+        }
+        images.push_back(ds);
+        image_bytes += spill.size();
+        for (const auto &sb : spilled) {  // area bytes 0..7 = spill address
+            const uint64_t addr = (uint64_t)(uintptr_t)ds + sb.second;
+            for (uint32_t k = 0; k < 8; ++k) host[sb.first * kPackBlock + pack_area_byte(k)] = (uint8_t)(addr >> (8 * k));
+        }
+    }
+    void *d = nullptr;
+    if (hipMalloc(&d, host.size()) != hipSuccess ||
+        hipMemcpy(d, host.data(), host.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        rc = hip_fail(hipErrorOutOfMemory, "pack image upload");
+        return true;
+    }
+    images.push_back(d);
+    image_bytes += host.size();
+    dn.kind = KIND_PACK;
+    dn.arity = (uint16_t)a;
+    dn.stride = kPackBlock;
+    dn.length = L;
+    dn.base = (uint64_t)(uintptr_t)d;
+    return true;
+}
+
+// desc node u may become KIND_PACK: 1..8 children, each with 1..8 leaf
+// children of consecutive columns (MASK8 nodes with FLAG_CONSEC_LABELS)
+bool pack_candidate(const mbrwt_tree_desc &desc, uint32_t u) {
+    const uint32_t a = desc.num_children[u];
+    if (a == 0 || a > 8) return false;
+    for (uint32_t c = 0; c < a; ++c) {
+        const uint32_t ch = desc.first_child[u] + c, gc = desc.num_children[ch];
+        if (gc == 0 || gc > 8) return false;
+        for (uint32_t k = 0; k < gc; ++k) {
+            const uint32_t leaf = desc.first_child[ch] + k;
+            if (desc.num_children[leaf] != 0) return false;
+            if (desc.leaf_column[leaf] != desc.leaf_column[desc.first_child[ch]] + k) return false;
+        }
+    }
+    return true;
+}
+
 }  // namespace
 
 int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
@@ -223,9 +314,26 @@ int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
                               tree.image_bytes);
         if (rc) return rc;
     }
+    std::vector<bool> in_pack(N, false);  // MASK8 children of a KIND_PACK node: no image
     for (uint32_t u = 0; u < N; ++u) {
         const uint32_t a = desc.num_children[u];
-        if (!a || (u == 0 && tree.folded)) continue;
+        if (!a || (u == 0 && tree.folded) || in_pack[u]) continue;
+        if (pack_enabled() && pack_candidate(desc, u)) {
+            int rc = MBRWT_OK;
+            if (build_pack_image(desc, u, ones[u], tree.nodes[u + 1], tree.images, tree.image_bytes, rc)) {
+                if (rc) return rc;
+                for (uint32_t c = 0; c < a; ++c) {
+                    const uint32_t ch = desc.first_child[u] + c;
+                    in_pack[ch] = true;
+                    DevNode &cn = tree.nodes[ch + 1];
+                    cn.kind = KIND_MASK8;
+                    cn.arity = (uint16_t)desc.num_children[ch];
+                    cn.length = ones[ch];
+                    cn.base = 0;
+                }
+                continue;
+            }
+        }
         std::vector<const uint64_t *> cw(a);
         std::vector<bool> leaf(a);
         for (uint32_t c = 0; c < a; ++c) {
@@ -244,7 +352,7 @@ int finalize_tree(Tree &tree) {
     // consecutive-label flag for MASK nodes
     for (uint32_t v = 0; v < D; ++v) {
         DevNode &dn = tree.nodes[v];
-        if (dn.kind < KIND_MASK8) continue;
+        if (!is_mask_kind(dn.kind)) continue;
         bool consec = true;
         for (uint32_t c = 0; c < dn.arity; ++c)
             if (tree.nodes[dn.first_child + c].label != tree.nodes[dn.first_child].label + c) consec = false;
@@ -270,7 +378,8 @@ int finalize_tree(Tree &tree) {
     for (uint32_t v = 0; v < D; ++v) {
         const DevNode &dn = tree.nodes[v];
         if (dn.kind == KIND_LEAF || dn.kind == KIND_FOLDED) continue;
-        if (dn.arity > 8 || (dn.kind != KIND_PLANE && dn.kind != KIND_MASK8)) tree.fast_shape = false;
+        if (dn.arity > 8 || (dn.kind != KIND_PLANE && dn.kind != KIND_MASK8 && dn.kind != KIND_PACK))
+            tree.fast_shape = false;
         if (dn.kind == KIND_MASK8 && !(dn.flags & FLAG_CONSEC_LABELS)) tree.fast_shape = false;
         if (dn.kind == KIND_PLANE)
             for (uint32_t c = 0; c < dn.arity; ++c)
@@ -306,9 +415,10 @@ int finalize_tree(Tree &tree) {
             tree.push_frames = std::max(tree.push_frames, here);
         }
     }
-    tree.lds_complete = true;
-    for (uint32_t v = kLdsNodes; v < D; ++v)
-        if (tree.nodes[v].kind != KIND_LEAF) tree.lds_complete = false;
+    tree.lds_records = 1;
+    for (uint32_t v = 0; v < D; ++v)
+        if (tree.nodes[v].kind != KIND_LEAF) tree.lds_records = v + 1;
+    tree.lds_complete = tree.lds_records <= kLdsNodes;
     tree.col_path.assign(tree.num_columns * tree.path_len, 0);
     tree.col_leaf.assign(tree.num_columns, 0);
     for (uint32_t v = 0; v < D; ++v) {

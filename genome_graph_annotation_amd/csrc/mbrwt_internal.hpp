@@ -44,7 +44,22 @@ enum : uint8_t {
     KIND_MASK32 = 4,
     KIND_MASK64 = 5,
     KIND_FOLDED = 6,  // the BRWT root when folded into the super-root (never visited)
+    KIND_PACK = 7,    // node whose children are all MASK8 nodes: children bits + their masks inline
 };
+inline bool is_mask_kind(uint8_t k) { return k >= KIND_MASK8 && k <= KIND_MASK64; }
+
+// KIND_PACK image: one 64-byte block per 16 positions.  Quarter q (16 bytes)
+// = {u16 bits of child 2q, u16 bits of child 2q+1, 12 bytes of the mask
+// area}; the logical 48-byte mask area (quarters' 12-byte segments in order)
+// holds the MASK8 mask of every set (child, position) pair of the block,
+// child-major, position-ascending.  A block with more than 48 pairs keeps
+// the u64 address of a spill list (same order) in area bytes 0..7.  The
+// MASK8 children keep their records (labels, arity) but have no image.
+constexpr uint32_t kPackSpan = 16;
+constexpr uint32_t kPackBlock = 64;
+constexpr uint32_t kPackArea = 48;
+// byte offset inside a block of logical mask-area byte o
+__host__ __device__ inline uint32_t pack_area_byte(uint32_t o) { return 16 * (o / 12) + 4 + o % 12; }
 // FLAG_CONSEC_LABELS (MASK nodes): child c's label = label + c.
 // FLAG_MASK_CHILDREN (PLANE nodes): every child is a KIND_MASK8 node with
 // consecutive labels, so the fast kernel resolves the children in the
@@ -66,7 +81,8 @@ static_assert(sizeof(DevNode) == 32, "DevNode must be 32 bytes");
 // Compact 16-byte node record read by the group kernel (kept in LDS for the
 // first kLdsNodes dnodes -- in BFS numbering the internal nodes come first):
 //   w0 = base[0:48) | kind[48:51) | flag[51] | log2(stride)[52:56) | arity[56:64)
-// flag = FLAG_MASK_CHILDREN for KIND_PLANE, FLAG_CONSEC_LABELS otherwise.
+// flag = FLAG_MASK_CHILDREN for KIND_PLANE, FLAG_CONSEC_LABELS otherwise
+// (unused for KIND_PACK; its log2(stride) is 6).
 struct alignas(16) CNode {
     uint64_t w0;
     uint32_t first_child;
@@ -114,6 +130,7 @@ struct Tree {
     bool fast_shape = false;                // eligible for k_traverse_fast (finalize_tree)
     bool lds_complete = false;              // every non-leaf dnode id < kLdsNodes (k_traverse_fast2)
     uint32_t push_frames = 0;               // max stack frames of the fast kernels (non-TERM PLANE nodes on a path)
+    uint32_t lds_records = 0;               // last non-leaf dnode id + 1 (node records worth staging in LDS)
     uint32_t max_arity = 0;
     uint64_t num_rows = 0, num_columns = 0, num_relations = 0, num_nodes = 0;
     uint64_t image_bytes = 0;
@@ -172,6 +189,11 @@ int finalize_tree(Tree &tree);
 // root folding is on unless MBRWT_FOLD_ROOT=0 (A/B measurement switch)
 inline bool fold_root_enabled() {
     const char *e = std::getenv("MBRWT_FOLD_ROOT");
+    return !(e && e[0] == '0');
+}
+// KIND_PACK nodes are built unless MBRWT_PACK=0 (A/B measurement switch)
+inline bool pack_enabled() {
+    const char *e = std::getenv("MBRWT_PACK");
     return !(e && e[0] == '0');
 }
 

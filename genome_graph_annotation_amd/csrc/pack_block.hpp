@@ -1,0 +1,45 @@
+// pack_block.hpp -- KIND_PACK block access for the general kernels (the
+// whole 64-byte block in 16 registers, bytes picked by selects; layout in
+// mbrwt_internal.hpp).  k_traverse_fast2 reads the same blocks its own way.
+#pragma once
+
+#include "device_access.hpp"
+#include "mbrwt_internal.hpp"
+
+namespace mbrwt {
+
+struct PackBlock {
+    uint32_t w[16];
+    uint32_t total;  // set (child, position) pairs of the block
+    __device__ __forceinline__ void load(uint64_t base, uint32_t j) {
+        const uint64_t blk = base + (uint64_t)(j / kPackSpan) * kPackBlock;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const uint4 q = gld_at<uint4>(blk + 16 * h);
+            w[4 * h] = q.x;
+            w[4 * h + 1] = q.y;
+            w[4 * h + 2] = q.z;
+            w[4 * h + 3] = q.w;
+        }
+        total = 0;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) total += __builtin_popcount(w[4 * h]);
+    }
+    __device__ __forceinline__ uint32_t bits(uint32_t k) const {  // child k's 16 position bits
+        uint32_t x = w[0];
+#pragma unroll
+        for (int h = 1; h < 4; ++h) x = (k >> 1) == (uint32_t)h ? w[4 * h] : x;
+        return (k & 1) ? x >> 16 : x & 0xFFFFu;
+    }
+    // mask-area byte o (inline, or from the spill list)
+    __device__ __forceinline__ uint32_t mask(uint32_t o) const {
+        if (total > kPackArea) return gld_at<uint8_t>(((uint64_t)w[2] << 32 | w[1]) + o);
+        const uint32_t by = pack_area_byte(o);
+        uint32_t x = w[0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) x = (by >> 2) == (uint32_t)i ? w[i] : x;
+        return (x >> (8 * (by & 3))) & 0xFFu;
+    }
+};
+
+}  // namespace mbrwt

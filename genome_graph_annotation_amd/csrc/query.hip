@@ -24,6 +24,7 @@
 
 #include "device_access.hpp"
 #include "mbrwt_internal.hpp"
+#include "pack_block.hpp"
 
 namespace mbrwt {
 
@@ -139,6 +140,26 @@ __device__ __forceinline__ void enter(const TravParams &p, Frames<MAXD, MaskT> &
     const uint32_t a = nd.arity;
     const uint64_t base = nd.base;
     if constexpr (MODE == MODE_WORK) sk.visits += a;  // operator[] on every child (BRWT.cpp:30)
+    if (kind == KIND_PACK) {  // children are MASK8 nodes: resolve them here, in child order
+        PackBlock pb;
+        pb.load(base, j);
+        const uint32_t t = j % kPackSpan;
+        uint32_t o = 0;
+        for (uint32_t k = 0; k < a; ++k) {
+            const uint32_t bk = pb.bits(k);
+            if ((bk >> t) & 1u) {
+                const DevNode ch = gld(p.nodes + nd.first_child + k);
+                if constexpr (MODE == MODE_WORK) sk.visits += ch.arity;
+                uint32_t m = pb.mask(o + (uint32_t)__builtin_popcount(bk & ((1u << t) - 1u)));
+                while (m) {
+                    sk.emit(p, ch.label + (uint32_t)__builtin_ctz(m));
+                    m &= m - 1;
+                }
+            }
+            o += (uint32_t)__builtin_popcount(bk);
+        }
+        return;
+    }
     if (kind == KIND_PLANE) {
         const uint64_t blk = base + (uint64_t)(j >> 5) * nd.stride;
         const uint32_t t = j & 31;
@@ -378,6 +399,32 @@ __device__ __forceinline__ void group_visit(const TravParams &p, GroupFrames<MAX
     const uint32_t a = nd.arity;
     const uint64_t base = nd.base;
     if constexpr (MODE == MODE_WORK) sk.visits += a;  // operator[] on every child (BRWT.cpp:30)
+    if (nd.kind == KIND_PACK) {
+        // every lane holds the whole block; each emits the labels of its own
+        // children at their rank among the node's labels (child order)
+        PackBlock pb;
+        pb.load(base, j);
+        const uint32_t t = j % kPackSpan, below = (1u << t) - 1u;
+        uint32_t o = 0, before = 0, total = 0;
+        for (uint32_t k = 0; k < a; ++k) {
+            const uint32_t bk = pb.bits(k);
+            if ((bk >> t) & 1u) {
+                const uint32_t m = pb.mask(o + (uint32_t)__builtin_popcount(bk & below));
+                const NodeInfo ch = decode(gld(reinterpret_cast<const uint64_t *>(p.cnodes) + 2 * (nd.first_child + k)),
+                                           gld(reinterpret_cast<const uint64_t *>(p.cnodes) + 2 * (nd.first_child + k) + 1));
+                if constexpr (MODE == MODE_WORK) sk.visits += ch.arity;
+                if (k / CPL == c) {
+                    uint32_t mm = m, r = before;
+                    for (; mm; mm &= mm - 1) sk.put(p, r++, ch.label + (uint32_t)__builtin_ctz(mm));
+                }
+                before += (uint32_t)__builtin_popcount(m);
+                total += (uint32_t)__builtin_popcount(m);
+            }
+            o += (uint32_t)__builtin_popcount(bk);
+        }
+        sk.cnt += total;
+        return;
+    }
     if (nd.kind == KIND_PLANE) {
         const uint32_t t = j & 31;
         const uint32_t below = (1u << t) - 1u;
@@ -554,215 +601,7 @@ __global__ __launch_bounds__(256, WPE) void k_traverse_group(TravParams p, uint3
     }
 }
 
-// ------------------------------------------------------------------------
-// k_traverse_fast: the group kernel specialised for the common tree shape
-// (every internal node KIND_PLANE or KIND_MASK8 with arity <= 8, leaves only
-// below MASK8 nodes with consecutive labels, <= 4 PLANE levels -- the basic
-// arity-<=8 partitioner's trees).  Same algorithm as k_traverse_group with
-// G = 4 lanes x 2 children, stripped of every branch the shape rules out:
-// the traversal is issue-bound as much as memory-bound (a cache-resident
-// 1 M-row tree runs only ~25 % faster than the 3.7 B-row one), so each
-// instruction of the per-step path matters.  Each stack level is 3 registers
-// per lane (two child positions + first child << 8 | pending mask); each
-// group preloads the ids of its next 8 rows (2 per lane).
-// ------------------------------------------------------------------------
-constexpr uint32_t kFastMaxd = 4;
-
-template <bool NT, bool TERM>
-__global__ __launch_bounds__(256, 8) void k_traverse_fast(TravParams p) {
-    constexpr uint32_t G = 4;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t c = lane & 3;
-    const uint32_t gbase = lane & ~3u;
-    const uint64_t gid = (uint64_t)blockIdx.x * 64 + threadIdx.x / 4;
-    const uint64_t ngroups = (uint64_t)gridDim.x * 64;
-
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds_stage[];  // 64 groups x kStageLabels
-    AS_LDS uint32_t *stage = (AS_LDS uint32_t *)lds_stage + (threadIdx.x / 4) * kStageLabels;
-    AS_LDS uint64_t *lds_nodes = (AS_LDS uint64_t *)((AS_LDS uint32_t *)lds_stage + 64 * kStageLabels);
-    const uint64_t *gnodes = reinterpret_cast<const uint64_t *>(p.cnodes);
-    for (uint32_t i = threadIdx.x; i < 2 * p.n_lds; i += blockDim.x) lds_nodes[i] = gld(gnodes + i);
-    __syncthreads();
-
-    uint32_t jc0[kFastMaxd], jc1[kFastMaxd], fp[kFastMaxd];  // fp = first_child << 8 | pending mask
-#pragma unroll
-    for (int k = 0; k < (int)kFastMaxd; ++k) jc0[k] = jc1[k] = fp[k] = 0;
-    int sp = 0;
-    uint32_t cnt = 0;
-    uint64_t chunk = gid;
-    uint32_t ri = 0;
-    uint64_t slot = chunk * 8;
-
-    // label number `pos` of the current row: LDS stage, else straight to the slot
-    auto emit = [&](uint32_t pos, uint32_t label) {
-        if (pos < kStageLabels) stage[pos] = label;
-        else if (pos < p.K) gst(p.temp + slot * p.K + pos, label);  // past the LDS stage
-    };
-    auto node_w0 = [&](uint32_t w) -> uint64_t { return w < p.n_lds ? lds_nodes[2 * w] : gld(gnodes + 2 * w); };
-    auto node_w1 = [&](uint32_t w) -> uint64_t {
-        return w < p.n_lds ? lds_nodes[2 * w + 1] : gld(gnodes + 2 * w + 1);
-    };
-
-    // visit node record (w0, w1) at position j
-    auto visit = [&](uint64_t w0, uint64_t w1, uint32_t j) {
-        const uint64_t base = w0 & ((1ull << 48) - 1);
-        const uint32_t kind = (uint32_t)(w0 >> 48) & 7u;
-        const uint32_t a = (uint32_t)(w0 >> 56);
-        if (kind == KIND_PLANE) {
-            const uint32_t stride = 1u << ((uint32_t)(w0 >> 52) & 15u);
-            const uint32_t t = j & 31, below = (1u << t) - 1u;
-            uint32_t b0 = 0, b1 = 0, j0 = 0, j1 = 0;
-            if (2 * c < a) {
-                const uint4 q = gld_at_nt<uint4, NT>(base + (uint64_t)(j >> 5) * stride + 16u * c);
-                b0 = (q.y >> t) & 1u;
-                b1 = (2 * c + 1 < a) ? (q.w >> t) & 1u : 0u;
-                j0 = q.x + (uint32_t)__builtin_popcount(q.y & below);  // rank1(j) - 1 of child 2c
-                j1 = q.z + (uint32_t)__builtin_popcount(q.w & below);  // and of child 2c+1
-            }
-            if (TERM && ((w0 >> 51) & 1u)) {
-                // FLAG_MASK_CHILDREN: every child is a MASK8 node over leaves; read
-                // the masks of the (up to 2) set children of this lane at once
-                // instead of visiting them one by one, then place their labels in
-                // child order (exclusive scan of the counts over the group).
-                const uint32_t fc = (uint32_t)w1;
-                uint32_t m0 = 0, m1 = 0, l0 = 0, l1 = 0;
-                if (b0) {
-                    const uint32_t w = fc + 2 * c;
-                    m0 = gld_at_nt<uint8_t, NT>((node_w0(w) & ((1ull << 48) - 1)) + j0);
-                    l0 = (uint32_t)(node_w1(w) >> 32);
-                }
-                if (b1) {
-                    const uint32_t w = fc + 2 * c + 1;
-                    m1 = gld_at_nt<uint8_t, NT>((node_w0(w) & ((1ull << 48) - 1)) + j1);
-                    l1 = (uint32_t)(node_w1(w) >> 32);
-                }
-                const uint32_t n0 = (uint32_t)__builtin_popcount(m0);
-                const uint32_t s0 = n0 + (uint32_t)__builtin_popcount(m1);
-                uint32_t incl = s0;
-                uint32_t y = (uint32_t)__shfl((int)incl, (int)(lane - 1), 64);
-                incl += c >= 1 ? y : 0u;
-                y = (uint32_t)__shfl((int)incl, (int)(lane - 2), 64);
-                incl += c >= 2 ? y : 0u;
-                const uint32_t total = (uint32_t)__shfl((int)incl, (int)(gbase + 3), 64);
-                uint32_t pos = cnt + incl - s0;
-                while (m0) {
-                    emit(pos++, l0 + (uint32_t)__builtin_ctz(m0));
-                    m0 &= m0 - 1;
-                }
-                while (m1) {
-                    emit(pos++, l1 + (uint32_t)__builtin_ctz(m1));
-                    m1 &= m1 - 1;
-                }
-                cnt += total;
-                return;
-            }
-            const uint32_t e = (uint32_t)(__ballot(b0) >> gbase) & 0xFu;
-            const uint32_t o = (uint32_t)(__ballot(b1) >> gbase) & 0xFu;
-            // interleave: child 2i <- e bit i, child 2i+1 <- o bit i
-            const uint32_t P = (e & 1u) | ((e & 2u) << 1) | ((e & 4u) << 2) | ((e & 8u) << 3) | ((o & 1u) << 1) |
-                               ((o & 2u) << 2) | ((o & 4u) << 3) | ((o & 8u) << 4);
-            if (P) {
-                if (sp >= (int)kFastMaxd) {
-                    if (c == 0) atomicOr(&p.scalars[2], 2ull);
-                    return;
-                }
-#pragma unroll
-                for (int k = kFastMaxd - 1; k > 0; --k) {
-                    jc0[k] = jc0[k - 1];
-                    jc1[k] = jc1[k - 1];
-                    fp[k] = fp[k - 1];
-                }
-                jc0[0] = j0;
-                jc1[0] = j1;
-                fp[0] = ((uint32_t)w1 << 8) | P;
-                ++sp;
-            }
-            return;
-        }
-        // KIND_MASK8, consecutive leaf labels
-        const uint32_t m = gld_at_nt<uint8_t, NT>(base + j);
-        const uint32_t l0 = (uint32_t)(w1 >> 32);
-#pragma unroll
-        for (uint32_t q = 0; q < 2; ++q) {
-            const uint32_t cc = 2 * c + q;
-            if ((m >> cc) & 1u) emit(cnt + (uint32_t)__builtin_popcount(m & ((1u << cc) - 1u)), l0 + cc);
-        }
-        cnt += (uint32_t)__builtin_popcount(m);
-    };
-
-    // rows: each group takes chunks of 8 consecutive slots, ids preloaded 2 per
-    // lane as u32 (num_rows <= 2^32 - 1, so ids >= num_rows clamp to 0xFFFFFFFF,
-    // which is out of range too)
-    uint32_t r0 = 0, r1 = 0;
-    auto clamp_row = [&](uint64_t r) -> uint32_t { return r < p.num_rows ? (uint32_t)r : 0xFFFFFFFFu; };
-    auto load_chunk = [&]() {
-        const uint64_t sb = chunk * 8 + 2 * c;
-        r0 = sb < p.n ? clamp_row(gld(p.rows + sb)) : 0u;
-        r1 = sb + 1 < p.n ? clamp_row(gld(p.rows + sb + 1)) : 0u;
-    };
-    bool active = slot < p.n;
-    if (active) load_chunk();
-    auto begin_row = [&]() {
-        const uint32_t mine = (ri & 1) ? r1 : r0;
-        const uint64_t row = (uint32_t)__shfl((int)mine, (int)(gbase + (ri >> 1)), 64);
-        cnt = 0;
-        if (row >= p.num_rows) {
-            if (c == 0) atomicOr(&p.scalars[2], 1ull);
-            return;
-        }
-        visit(lds_nodes[0], lds_nodes[1], (uint32_t)row);
-    };
-    auto end_row = [&]() {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t lim = cnt < kStageLabels ? cnt : kStageLabels;
-        const uint64_t sb = slot * p.K;
-        for (uint32_t pos = c; pos < lim; pos += G) gst(p.temp + sb + pos, (uint32_t)stage[pos]);
-        if (c == 0) {
-            gst(p.counts + slot, cnt);
-            if (cnt > p.K) {
-                const unsigned long long k = atomicAdd(&p.scalars[1], 1ull);
-                gst(p.ovf_list + k, (uint32_t)slot);
-            }
-        }
-    };
-
-    if (active) begin_row();
-    while (true) {
-        if (active && sp == 0) {
-            end_row();
-            if (++ri == 8) {
-                ri = 0;
-                chunk += ngroups;
-                if (chunk * 8 < p.n) load_chunk();
-            }
-            slot = chunk * 8 + ri;
-            active = slot < p.n;
-            if (active) begin_row();
-        }
-        if (!__any(active)) break;
-        if (active && sp > 0) {
-            uint32_t top = fp[0];
-            const uint32_t cs = (uint32_t)__builtin_ctz(top & 0xFFu);
-            top &= top - 1;  // clears the lowest pending bit (the mask is the low byte)
-            const uint32_t w = (top >> 8) + cs;
-            const uint32_t jsel = (cs & 1) ? jc1[0] : jc0[0];
-            const uint32_t jw = (uint32_t)__shfl((int)jsel, (int)(gbase + (cs >> 1)), 64);
-            fp[0] = top;
-            if ((top & 0xFFu) == 0) {  // no children left at this level
-#pragma unroll
-                for (int k = 0; k < (int)kFastMaxd - 1; ++k) {
-                    jc0[k] = jc0[k + 1];
-                    jc1[k] = jc1[k + 1];
-                    fp[k] = fp[k + 1];
-                }
-                --sp;
-            }
-            visit(node_w0(w), node_w1(w), jw);
-        }
-    }
-}
+constexpr uint32_t kFastMaxd = 4;  // stack frames of k_traverse_fast2 (finalize_tree: fast_shape)
 
 // Reductions over the 4 lanes of a group (lanes 4i..4i+3 = one DPP quad):
 // quad_perm DPP moves, no LDS round trip.  All 4 lanes must be active.
@@ -783,16 +622,28 @@ __device__ __forceinline__ uint32_t quad_exclusive_sum(uint32_t v, uint32_t c, u
 }
 
 // ------------------------------------------------------------------------
-// k_traverse_fast2: k_traverse_fast restructured so that every iteration of
-// a wave runs ONE inlined visit (a group starting a row visits the root in
-// the same code as a group visiting a popped child) -- with 16 groups per
-// wave at different places of their trees, every extra code path in the loop
-// body is paid by the whole wave.  Node records come from LDS only (the tree
-// is eligible when every non-leaf dnode id is < n_lds), so the mask reads of
-// a FLAG_MASK_CHILDREN visit are not serialised behind a global-fallback
-// wait; the label stage is flushed as 16-byte vectors.
+// k_traverse_fast2: the traversal kernel for the basic arity-<=8 trees
+// (every internal node PLANE, MASK8 or PACK with arity <= 8, MASK8 labels
+// consecutive, <= kFastMaxd stack frames, every non-leaf record in the LDS
+// table -- Tree::fast_shape && lds_complete).  A group of 4 lanes answers a
+// row (2 children per lane, 16 rows per wave).  Every iteration of the wave
+// runs ONE inlined visit (a group starting a row visits the root in the same
+// code as a group visiting a popped child): with 16 groups per wave at
+// different places of their trees, every extra code path in the loop body
+// is paid by the whole wave.  Visits:
+//   PLANE -- one coalesced 64-byte block read (16 B per lane = {rank, bits}
+//            of two children); child mask OR-reduced over the quad by DPP;
+//            a stack frame (3 registers per lane) is pushed;
+//   PACK  -- the same block read gives the children bits AND their MASK8
+//            masks; the block is staged in LDS and each lane picks the masks
+//            of its two children: a level costs no second dependent read;
+//   PLANE with FLAG_MASK_CHILDREN (MBRWT_PACK=0 trees) -- block read, then
+//            the (independent) mask reads of the set MASK8 children;
+//   MASK8 -- leaf labels from one byte (only as the root's child).
+// Labels are staged in LDS (32 per row) and flushed as 16-byte vectors when
+// the row ends (vmcnt counts stores on CDNA4: no stores inside the descent).
 // ------------------------------------------------------------------------
-template <bool NT, bool SMALLK, bool DIAG = false>
+template <bool NT, bool SMALLK>
 __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
     constexpr uint64_t M48 = (1ull << 48) - 1;
     const uint32_t lane = threadIdx.x & 63;
@@ -801,9 +652,11 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
     const uint64_t gid = (uint64_t)blockIdx.x * 64 + threadIdx.x / 4;
     const uint64_t ngroups = (uint64_t)gridDim.x * 64;
 
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds_stage[];  // 64 groups x kStageLabels
+    // LDS: 64 groups x kStageLabels labels | 64 groups x one 64-byte PACK block | node records
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_stage[];
     AS_LDS uint32_t *stage = (AS_LDS uint32_t *)lds_stage + (threadIdx.x / 4) * kStageLabels;
-    AS_LDS uint64_t *lds_nodes = (AS_LDS uint64_t *)((AS_LDS uint32_t *)lds_stage + 64 * kStageLabels);
+    AS_LDS uint32_t *pk = (AS_LDS uint32_t *)lds_stage + 64 * kStageLabels + (threadIdx.x / 4) * 16;
+    AS_LDS uint64_t *lds_nodes = (AS_LDS uint64_t *)((AS_LDS uint32_t *)lds_stage + 64 * kStageLabels + 64 * 16);
     const uint64_t *gnodes = reinterpret_cast<const uint64_t *>(p.cnodes);
     for (uint32_t i = threadIdx.x; i < 2 * p.n_lds; i += blockDim.x) lds_nodes[i] = gld(gnodes + i);
     __syncthreads();
@@ -903,7 +756,47 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
 
         const uint64_t base = w0 & M48;
         const uint32_t a = (uint32_t)(w0 >> 56);
-        if (((uint32_t)(w0 >> 48) & 7u) == KIND_MASK8) {  // leaves below: labels from the mask
+        const uint32_t kind = (uint32_t)(w0 >> 48) & 7u;
+        // the labels of this lane's two MASK8 children (masks m0, m1 with leaf
+        // labels l0.., l1..) at their place among the node's labels
+        auto emit_children = [&](uint32_t m0, uint32_t m1, uint32_t l0, uint32_t l1) {
+            const uint32_t s0 = (uint32_t)__builtin_popcount(m0) + (uint32_t)__builtin_popcount(m1);
+            uint32_t total;
+            uint32_t pos = cnt + quad_exclusive_sum(s0, c, total);
+            for (; m0; m0 &= m0 - 1) emit(pos++, l0 + (uint32_t)__builtin_ctz(m0));
+            for (; m1; m1 &= m1 - 1) emit(pos++, l1 + (uint32_t)__builtin_ctz(m1));
+            cnt += total;
+        };
+        if (kind == KIND_PACK) {
+            const uint32_t t = j % kPackSpan, below = (1u << t) - 1u;
+            const uint4 q = gld_at_nt<uint4, NT>(base + (uint64_t)(j / kPackSpan) * kPackBlock + 16u * c);
+            const uint32_t lo = q.x & 0xFFFFu, hi = q.x >> 16;  // bits of children 2c, 2c+1
+            const uint32_t b0 = (lo >> t) & 1u, b1 = (hi >> t) & 1u;
+            uint32_t pairs;
+            const uint32_t pre = quad_exclusive_sum((uint32_t)__builtin_popcount(q.x), c, pairs);
+            ((AS_LDS u32x4_t *)pk)[c] = u32x4_t{q.x, q.y, q.z, q.w};
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t o0 = pre + (uint32_t)__builtin_popcount(lo & below);
+            const uint32_t o1 = pre + (uint32_t)__builtin_popcount(lo) + (uint32_t)__builtin_popcount(hi & below);
+            uint32_t m0 = 0, m1 = 0, l0 = 0, l1 = 0;
+            const uint32_t fc = (uint32_t)w1;
+            if (pairs <= kPackArea) {
+                const AS_LDS uint8_t *pb = (const AS_LDS uint8_t *)pk;
+                if (b0) m0 = pb[pack_area_byte(o0)];
+                if (b1) m1 = pb[pack_area_byte(o1)];
+            } else {  // spilled block: area bytes 0..7 hold the list's address
+                const uint64_t sa = ((uint64_t)pk[2] << 32) | pk[1];
+                if (b0) m0 = gld_at_nt<uint8_t, NT>(sa + o0);
+                if (b1) m1 = gld_at_nt<uint8_t, NT>(sa + o1);
+            }
+            if (b0) l0 = (uint32_t)(lds_nodes[2 * (fc + 2 * c) + 1] >> 32);
+            if (b1) l1 = (uint32_t)(lds_nodes[2 * (fc + 2 * c + 1) + 1] >> 32);
+            emit_children(m0, m1, l0, l1);
+            continue;
+        }
+        if (kind == KIND_MASK8) {  // leaves below: labels from the mask
             const uint32_t m = gld_at_nt<uint8_t, NT>(base + j);
             const uint32_t l0 = (uint32_t)(w1 >> 32);
 #pragma unroll
@@ -926,26 +819,19 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
             j1 = q.z + (uint32_t)__builtin_popcount(q.w & below);
         }
         const uint32_t fc = (uint32_t)w1;
-        if ((w0 >> 51) & 1u) {  // FLAG_MASK_CHILDREN: resolve the children's masks now
+        if ((w0 >> 51) & 1u) {  // FLAG_MASK_CHILDREN: the set children's mask reads, together
             uint32_t m0 = 0, m1 = 0, l0 = 0, l1 = 0;
             if (b0) {
                 const uint32_t w = fc + 2 * c;
-                // DIAG (variant 21, measurement only, wrong labels): no mask read
-                m0 = DIAG ? 1u << (j0 & 7) : gld_at_nt<uint8_t, NT>((lds_nodes[2 * w] & M48) + j0);
+                m0 = gld_at_nt<uint8_t, NT>((lds_nodes[2 * w] & M48) + j0);
                 l0 = (uint32_t)(lds_nodes[2 * w + 1] >> 32);
             }
             if (b1) {
                 const uint32_t w = fc + 2 * c + 1;
-                m1 = DIAG ? 1u << (j1 & 7) : gld_at_nt<uint8_t, NT>((lds_nodes[2 * w] & M48) + j1);
+                m1 = gld_at_nt<uint8_t, NT>((lds_nodes[2 * w] & M48) + j1);
                 l1 = (uint32_t)(lds_nodes[2 * w + 1] >> 32);
             }
-            const uint32_t s0 = (uint32_t)__builtin_popcount(m0) + (uint32_t)__builtin_popcount(m1);
-            uint32_t total;
-            const uint32_t ex = quad_exclusive_sum(s0, c, total);
-            uint32_t pos = cnt + ex;
-            for (; m0; m0 &= m0 - 1) emit(pos++, l0 + (uint32_t)__builtin_ctz(m0));
-            for (; m1; m1 &= m1 - 1) emit(pos++, l1 + (uint32_t)__builtin_ctz(m1));
-            cnt += total;
+            emit_children(m0, m1, l0, l1);
             continue;
         }
         const uint32_t P = quad_or((b0 | (b1 << 1)) << (2 * c));  // child k <- bit k
@@ -964,214 +850,6 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
             jc1[0] = j1;
             fp[0] = (fc << 8) | P;
             ++sp;
-        }
-    }
-}
-
-// ------------------------------------------------------------------------
-// k_traverse_fast3: k_traverse_fast2 with TWO row contexts per group.  Each
-// iteration visits one node of each context, and the phases of the two
-// visits are interleaved (both block reads issued, then both sets of child
-// mask reads), so a group keeps two independent dependent-load chains in
-// flight -- the traversal is latency-bound with occupancy already at its
-// cap, and this doubles the memory-level parallelism per wave.  Needs
-// <= kF3Frames stack frames (two for the basic arity-8 partitioner: the
-// super-root's and the level-1 node's; FLAG_MASK_CHILDREN nodes push none).
-// ------------------------------------------------------------------------
-constexpr uint32_t kF3Frames = 2;
-
-template <bool NT, bool SMALLK>
-__global__ __launch_bounds__(256, 6) void k_traverse_fast3(TravParams p) {
-    constexpr uint64_t M48 = (1ull << 48) - 1;
-    constexpr uint32_t F = kF3Frames;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t c = lane & 3;
-    const uint32_t gbase = lane & ~3u;
-    const uint64_t gid = (uint64_t)blockIdx.x * 64 + threadIdx.x / 4;
-    const uint64_t ngroups = (uint64_t)gridDim.x * 64;
-
-    // LDS: 2 x 64 groups x kStageLabels label stages | 2 x 64 groups x 8 row ids | node records
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds_stage[];
-    AS_LDS uint32_t *stage0 = (AS_LDS uint32_t *)lds_stage + (threadIdx.x / 4) * kStageLabels;
-    AS_LDS uint32_t *stage1 = stage0 + 64 * kStageLabels;
-    AS_LDS uint32_t *rowbuf = (AS_LDS uint32_t *)lds_stage + 128 * kStageLabels + (threadIdx.x / 4) * 16;
-    AS_LDS uint64_t *lds_nodes = (AS_LDS uint64_t *)((AS_LDS uint32_t *)lds_stage + 128 * kStageLabels + 64 * 16);
-    const uint64_t *gnodes = reinterpret_cast<const uint64_t *>(p.cnodes);
-    for (uint32_t i = threadIdx.x; i < 2 * p.n_lds; i += blockDim.x) lds_nodes[i] = gld(gnodes + i);
-    __syncthreads();
-
-    uint32_t jc0[2][F], jc1[2][F], fp[2][F];
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int k = 0; k < (int)F; ++k) jc0[x][k] = jc1[x][k] = fp[x][k] = 0;
-    // (launch guarantees n < 2^34, so chunk indices fit u32)
-    int sp[2] = {0, 0};
-    uint32_t cnt[2] = {0, 0}, ri[2] = {0, 0};
-    uint32_t chunk[2] = {(uint32_t)(2 * gid), (uint32_t)(2 * gid + 1)};
-    const uint32_t cstride = (uint32_t)(2 * ngroups);
-    bool active[2], fresh[2];
-    auto slot_of = [&](int x) -> uint64_t { return (uint64_t)chunk[x] * 8 + ri[x]; };
-    // the 8 row ids of a context's chunk -> LDS (2 per lane; ids >= num_rows -> 0xFFFFFFFF)
-    auto load_chunk = [&](int x) {
-        const uint64_t sb = (uint64_t)chunk[x] * 8 + 2 * c;
-        const uint64_t a0 = sb < p.n ? gld(p.rows + sb) : 0, a1 = sb + 1 < p.n ? gld(p.rows + sb + 1) : 0;
-        rowbuf[8 * x + 2 * c] = a0 < p.num_rows ? (uint32_t)a0 : 0xFFFFFFFFu;
-        rowbuf[8 * x + 2 * c + 1] = a1 < p.num_rows ? (uint32_t)a1 : 0xFFFFFFFFu;
-    };
-#pragma unroll
-    for (int x = 0; x < 2; ++x) {
-        active[x] = fresh[x] = slot_of(x) < p.n;
-        if (active[x]) load_chunk(x);
-    }
-    auto emit = [&](int x, uint32_t pos, uint32_t label) {
-        if (pos < kStageLabels) (x ? stage1 : stage0)[pos] = label;
-        else if (!SMALLK && pos < p.K) gst(p.temp + slot_of(x) * p.K + pos, label);
-    };
-
-    while (true) {
-#pragma unroll
-        for (int x = 0; x < 2; ++x) {
-            if (active[x] && !fresh[x] && sp[x] == 0) {  // row done: flush, count, next slot
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                AS_LDS uint32_t *st = x ? stage1 : stage0;
-                const uint32_t lim = cnt[x] < kStageLabels ? cnt[x] : kStageLabels;
-                const uint64_t slot = slot_of(x);
-                uint32_t *sp_out = p.temp + slot * p.K;
-                for (uint32_t q = c; 4 * q < lim; q += 4)
-                    gst(reinterpret_cast<u32x4_t *>(sp_out) + q, (u32x4_t)((AS_LDS u32x4_t *)st)[q]);
-                if (c == 0) {
-                    gst(p.counts + slot, cnt[x]);
-                    if (cnt[x] > p.K) {
-                        const unsigned long long k = atomicAdd(&p.scalars[1], 1ull);
-                        gst(p.ovf_list + k, (uint32_t)slot);
-                    }
-                }
-                if (++ri[x] == 8) {
-                    ri[x] = 0;
-                    chunk[x] += cstride;
-                    if ((uint64_t)chunk[x] * 8 < p.n) load_chunk(x);
-                }
-                active[x] = slot_of(x) < p.n;
-                fresh[x] = active[x];
-            }
-        }
-        if (!__any(active[0] || active[1])) break;
-
-        // phase 1: the node each context visits (root of a fresh row or next child)
-        uint64_t w0[2] = {0, 0}, w1[2] = {0, 0};
-        uint32_t j[2] = {0, 0};
-        bool go[2] = {false, false};
-#pragma unroll
-        for (int x = 0; x < 2; ++x) {
-            if (!active[x]) continue;
-            if (fresh[x]) {
-                fresh[x] = false;
-                cnt[x] = 0;
-                j[x] = rowbuf[8 * x + ri[x]];
-                w0[x] = lds_nodes[0];
-                w1[x] = lds_nodes[1];
-                go[x] = (uint64_t)j[x] < p.num_rows;
-                if (!go[x] && c == 0) atomicOr(&p.scalars[2], 1ull);
-            } else {
-                uint32_t top = fp[x][0];
-                const uint32_t cs = (uint32_t)__builtin_ctz(top & 0xFFu);
-                top &= top - 1;
-                fp[x][0] = top;
-                const uint32_t w = (top >> 8) + cs;
-                const uint32_t jsel = (cs & 1) ? jc1[x][0] : jc0[x][0];
-                j[x] = (uint32_t)__shfl((int)jsel, (int)(gbase + (cs >> 1)), 64);
-                if ((top & 0xFFu) == 0) {
-#pragma unroll
-                    for (int k = 0; k < (int)F - 1; ++k) {
-                        jc0[x][k] = jc0[x][k + 1];
-                        jc1[x][k] = jc1[x][k + 1];
-                        fp[x][k] = fp[x][k + 1];
-                    }
-                    --sp[x];
-                }
-                w0[x] = lds_nodes[2 * w];
-                w1[x] = lds_nodes[2 * w + 1];
-                go[x] = true;
-            }
-        }
-        // phase 2: both block (or root mask) reads in flight together
-        uint4 q[2];
-        uint32_t mr[2] = {0, 0};
-#pragma unroll
-        for (int x = 0; x < 2; ++x) {
-            q[x] = make_uint4(0, 0, 0, 0);
-            if (!go[x]) continue;
-            const uint64_t base = w0[x] & M48;
-            if (((uint32_t)(w0[x] >> 48) & 7u) == KIND_MASK8) {
-                mr[x] = gld_at_nt<uint8_t, NT>(base + j[x]);
-            } else if (2 * c < (uint32_t)(w0[x] >> 56)) {
-                const uint32_t stride = 1u << ((uint32_t)(w0[x] >> 52) & 15u);
-                q[x] = gld_at_nt<uint4, NT>(base + (uint64_t)(j[x] >> 5) * stride + 16u * c);
-            }
-        }
-        // phase 3: children bits and positions; FLAG_MASK_CHILDREN mask reads in flight together
-        uint32_t b0[2], b1[2], j0[2], j1[2], m0[2] = {0, 0}, m1[2] = {0, 0}, l0[2] = {0, 0}, l1[2] = {0, 0};
-#pragma unroll
-        for (int x = 0; x < 2; ++x) {
-            const uint32_t t = j[x] & 31, below = (1u << t) - 1u;
-            const uint32_t a = (uint32_t)(w0[x] >> 56);
-            b0[x] = (q[x].y >> t) & 1u;
-            b1[x] = (2 * c + 1 < a) ? (q[x].w >> t) & 1u : 0u;
-            j0[x] = q[x].x + (uint32_t)__builtin_popcount(q[x].y & below);
-            j1[x] = q[x].z + (uint32_t)__builtin_popcount(q[x].w & below);
-            if (go[x] && ((uint32_t)(w0[x] >> 48) & 15u) == (KIND_PLANE | 8u)) {
-                const uint32_t fc = (uint32_t)w1[x];
-                if (b0[x]) {
-                    const uint32_t w = fc + 2 * c;
-                    m0[x] = gld_at_nt<uint8_t, NT>((lds_nodes[2 * w] & M48) + j0[x]);
-                    l0[x] = (uint32_t)(lds_nodes[2 * w + 1] >> 32);
-                }
-                if (b1[x]) {
-                    const uint32_t w = fc + 2 * c + 1;
-                    m1[x] = gld_at_nt<uint8_t, NT>((lds_nodes[2 * w] & M48) + j1[x]);
-                    l1[x] = (uint32_t)(lds_nodes[2 * w + 1] >> 32);
-                }
-            }
-        }
-        // phase 4: labels / push
-#pragma unroll
-        for (int x = 0; x < 2; ++x) {
-            if (!go[x]) continue;
-            const uint32_t kind = (uint32_t)(w0[x] >> 48) & 15u;
-            if ((kind & 7u) == KIND_MASK8) {  // root with leaf children
-                const uint32_t m = mr[x], lb = (uint32_t)(w1[x] >> 32);
-#pragma unroll
-                for (uint32_t qq = 0; qq < 2; ++qq) {
-                    const uint32_t cc = 2 * c + qq;
-                    if ((m >> cc) & 1u) emit(x, cnt[x] + (uint32_t)__builtin_popcount(m & ((1u << cc) - 1u)), lb + cc);
-                }
-                cnt[x] += (uint32_t)__builtin_popcount(m);
-            } else if (kind == (KIND_PLANE | 8u)) {
-                uint32_t ma = m0[x], mb = m1[x];
-                const uint32_t s0 = (uint32_t)__builtin_popcount(ma) + (uint32_t)__builtin_popcount(mb);
-                uint32_t total;
-                uint32_t pos = cnt[x] + quad_exclusive_sum(s0, c, total);
-                for (; ma; ma &= ma - 1) emit(x, pos++, l0[x] + (uint32_t)__builtin_ctz(ma));
-                for (; mb; mb &= mb - 1) emit(x, pos++, l1[x] + (uint32_t)__builtin_ctz(mb));
-                cnt[x] += total;
-            } else {
-                const uint32_t P = quad_or((b0[x] | (b1[x] << 1)) << (2 * c));
-                if (P) {
-#pragma unroll
-                    for (int k = F - 1; k > 0; --k) {
-                        jc0[x][k] = jc0[x][k - 1];
-                        jc1[x][k] = jc1[x][k - 1];
-                        fp[x][k] = fp[x][k - 1];
-                    }
-                    jc0[x][0] = j0[x];
-                    jc1[x][0] = j1[x];
-                    fp[x][0] = ((uint32_t)w1[x] << 8) | P;
-                    ++sp[x];
-                }
-            }
         }
     }
 }
@@ -1233,6 +911,19 @@ __global__ __launch_bounds__(256) void k_get(const DevNode *__restrict__ nodes, 
             const DevNode *nd = &ndv;
             const uint32_t c = col_path[col * path_len + k];
             const uint64_t base = nd->base;
+            if (nd->kind == KIND_PACK) {  // child c is a MASK8 node: its bit, then its mask
+                PackBlock pb;
+                pb.load(base, j);
+                const uint32_t t = j % kPackSpan;
+                uint32_t o = 0;
+                for (uint32_t q = 0; q < c; ++q) o += (uint32_t)__builtin_popcount(pb.bits(q));
+                const uint32_t bc = pb.bits(c);
+                if ((bc >> t) & 1u) {
+                    const uint32_t m = pb.mask(o + (uint32_t)__builtin_popcount(bc & ((1u << t) - 1u)));
+                    bit = (uint8_t)((m >> col_path[col * path_len + k + 1]) & 1u);
+                }
+                break;
+            }
             if (nd->kind == KIND_PLANE) {
                 const uint2 rb = gld_at<uint2>(base + (uint64_t)(j >> 5) * nd->stride + 8u * c);
                 const uint32_t t = j & 31;
@@ -1273,7 +964,6 @@ struct Trav {
     GroupFn group_fn = nullptr;
     uint32_t G = 1;  // lanes per row
     bool fast = false;
-    bool dual = false;  // k_traverse_fast3: two row contexts per group
     const char *name = "k_traverse_group";
     explicit operator bool() const { return fn != nullptr; }
 };
@@ -1285,38 +975,16 @@ Trav pick_traverse(const Ctx &c) {
     const uint32_t depth = c.tree.stack_depth, max_arity = c.tree.max_arity;
     Trav t;
     const int kv = c.kernel_variant;
-    if (MODE == MODE_SLOTS && c.tree.fast_shape && (kv == 0 || (kv >= 11 && kv <= 14) || (kv >= 17 && kv <= 21))) {
-        // 11/12: fast kernel without / with non-temporal reads; 13/14: the same
-        // without resolving FLAG_MASK_CHILDREN nodes' children inline (A/B)
-        const bool nt = kv == 12 || kv == 14 || kv == 18 || (kv == 0 && c.tree.image_bytes > (1ull << 30));
-        // 17/18 (and the default when every non-leaf record fits the LDS table):
-        // k_traverse_fast2 without / with non-temporal reads
-        const bool term = kv != 13 && kv != 14;
-        const bool v2 = (kv == 0 || kv >= 17) && c.tree.lds_complete;
+    if (MODE == MODE_SLOTS && c.tree.fast_shape && c.tree.lds_complete && (kv == 0 || kv == 17 || kv == 18)) {
+        // k_traverse_fast2; 17/18 force plain / non-temporal block reads, the
+        // default uses non-temporal reads on images larger than 1 GiB (+2.6 %)
+        const bool nt = kv == 18 || (kv == 0 && c.tree.image_bytes > (1ull << 30));
+        const bool smallk = auto_slots(c) == kStageLabels;
         t.G = 4;
         t.fast = true;
-        const bool smallk = auto_slots(c) == kStageLabels;
-        t.name = v2 ? "k_traverse_fast2" : "k_traverse_fast";
-        if (kv == 21 && c.tree.lds_complete && smallk) {  // diagnostic: fast2 without the MASK8 reads
-            t.name = "k_traverse_fast2_diag";
-            t.lane_fn = (TravFn)k_traverse_fast2<true, true, true>;
-            t.fn = reinterpret_cast<const void *>(t.lane_fn);
-            return t;
-        }
-        if ((kv == 19 || kv == 20) && c.tree.lds_complete && c.tree.push_frames <= kF3Frames) {
-            // 19/20: k_traverse_fast3 without / with non-temporal reads
-            const bool nt3 = kv == 20;
-            t.dual = true;
-            t.name = "k_traverse_fast3";
-            if (smallk) t.lane_fn = nt3 ? (TravFn)k_traverse_fast3<true, true> : (TravFn)k_traverse_fast3<false, true>;
-            else t.lane_fn = nt3 ? (TravFn)k_traverse_fast3<true, false> : (TravFn)k_traverse_fast3<false, false>;
-            t.fn = reinterpret_cast<const void *>(t.lane_fn);
-            return t;
-        }
-        if (v2 && smallk) t.lane_fn = nt ? (TravFn)k_traverse_fast2<true, true> : (TravFn)k_traverse_fast2<false, true>;
-        else if (v2) t.lane_fn = nt ? (TravFn)k_traverse_fast2<true, false> : (TravFn)k_traverse_fast2<false, false>;
-        else if (term) t.lane_fn = nt ? (TravFn)k_traverse_fast<true, true> : (TravFn)k_traverse_fast<false, true>;
-        else t.lane_fn = nt ? (TravFn)k_traverse_fast<true, false> : (TravFn)k_traverse_fast<false, false>;
+        t.name = "k_traverse_fast2";
+        if (smallk) t.lane_fn = nt ? (TravFn)k_traverse_fast2<true, true> : (TravFn)k_traverse_fast2<false, true>;
+        else t.lane_fn = nt ? (TravFn)k_traverse_fast2<true, false> : (TravFn)k_traverse_fast2<false, false>;
         t.fn = reinterpret_cast<const void *>(t.lane_fn);
         return t;
     }
@@ -1339,7 +1007,7 @@ Trav pick_traverse(const Ctx &c) {
     // group kernel: CPL children per lane, G = pow2ceil(ceil(max_arity / CPL)) lanes per row;
     // variants 5/6 request a higher occupancy (waves per SIMD) from the register allocator
     // default (and the fast variants on trees they do not fit): 2 children per lane, 8 waves/SIMD
-    const int v = (c.kernel_variant == 0 || c.kernel_variant >= 11) ? 5 : c.kernel_variant;
+    const int v = (c.kernel_variant == 0 || c.kernel_variant >= 11) ? 5 : c.kernel_variant;  // 17/18: fast2 only
     const int cpl = v == 2 ? 1 : (v == 4 || v == 6) ? 4 : 2;
     const int wpe = (v == 5 || v == 10) ? 8 : v == 6 ? 6 : 1;  // (v == 10 past depth 8 runs as 5)
     if (v == 10 && depth <= 8) {  // variant 5 with non-temporal block/mask reads
@@ -1376,11 +1044,16 @@ Trav pick_traverse(const Ctx &c) {
     return t;
 }
 
+// node records staged in LDS: the first min(kLdsNodes, last non-leaf + 1)
+uint32_t lds_node_count(const Ctx &c) {
+    return (uint32_t)std::min<size_t>({c.tree.nodes.size(), (size_t)kLdsNodes, (size_t)c.tree.lds_records});
+}
+
 size_t lds_bytes(const Ctx &c, const Trav &t) {
     if (!t.group_fn && !t.fast) return 0;
-    const size_t nl = std::min<size_t>(c.tree.nodes.size(), kLdsNodes);
-    return (size_t)(256 / t.G) * kStageLabels * sizeof(uint32_t) * (t.dual ? 2 : 1) + (t.dual ? 64 * 16 * 4 : 0) +
-           nl * sizeof(CNode);
+    // label stages (+ one 64-byte PACK block per group for fast2) + node records
+    return (size_t)(256 / t.G) * kStageLabels * sizeof(uint32_t) + (t.fast ? 64 * kPackBlock : 0) +
+           (size_t)lds_node_count(c) * sizeof(CNode);
 }
 
 int grid_for(const Ctx &c, const Trav &t, uint64_t n) {
@@ -1391,7 +1064,7 @@ int grid_for(const Ctx &c, const Trav &t, uint64_t n) {
         per_cu = 4;
     const uint64_t resident = (uint64_t)std::max(1, dev_cus) * (uint64_t)per_cu;
     // fast: 64 groups x 8-row chunks (x 2 contexts for fast3)
-    const uint64_t rows_per_block = t.fast ? (t.dual ? 1024 : 512) : 256 / t.G;
+    const uint64_t rows_per_block = t.fast ? 512 : 256 / t.G;
     const uint64_t need = (n + rows_per_block - 1) / rows_per_block;
     return (int)std::max<uint64_t>(1, std::min(need, resident));
 }
@@ -1415,7 +1088,7 @@ TravParams base_params(const Ctx &c) {
     TravParams p{};
     p.nodes = c.d_nodes;
     p.cnodes = c.d_cnodes;
-    p.n_lds = (uint32_t)std::min<size_t>(c.tree.nodes.size(), kLdsNodes);
+    p.n_lds = lds_node_count(c);
     p.folded = c.tree.folded ? 1u : 0u;
     p.num_rows = c.tree.num_rows;
     p.scalars = reinterpret_cast<unsigned long long *>(c.d_scalars);

@@ -213,6 +213,86 @@ __global__ __launch_bounds__(256) void k_gen_fold_mask(W *img, uint64_t n, const
     if ((threadIdx.x & 63) == 0 && local) atomicAdd(ones, (unsigned long long)local);
 }
 
+// KIND_PACK image (mbrwt_internal.hpp) of a node whose children are MASK8
+// nodes, from its temporary KIND_PLANE image (children bits + ranks): the
+// mask of child c at child position jc is the same draw (child key, jc) as
+// the child's own MASK8 image would hold.  Pass 0 counts the blocks that
+// spill; pass 1 writes (spill lists in 128-byte slots taken atomically).
+struct PackArgs {
+    const uint64_t *T[8];
+    uint32_t nT[8];
+    uint64_t K[8];
+};
+
+template <int A>
+__global__ __launch_bounds__(256) void k_gen_pack(uint8_t *img, uint64_t L, const uint8_t *plane, uint32_t pstride,
+                                                  PackArgs args, uint8_t *spill, unsigned long long *spill_ctr,
+                                                  unsigned long long *ones, int pass) {
+    __shared__ uint64_t T[A][255];
+    for (int c = 0; c < A; ++c)
+        for (uint32_t i = threadIdx.x; i < args.nT[c]; i += blockDim.x) T[c][i] = args.T[c][i];
+    __syncthreads();
+    const uint64_t nb = (L + kPackSpan - 1) / kPackSpan;
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t local = 0;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gs) {
+        const uint8_t *pb = plane + (b >> 1) * pstride;
+        const uint32_t half = (uint32_t)(b & 1) * 16;
+        uint32_t total = 0;
+        uint32_t bits[A];
+#pragma unroll
+        for (int c = 0; c < A; ++c) {
+            bits[c] = (reinterpret_cast<const uint2 *>(pb + 8 * c)->y >> half) & 0xFFFFu;
+            total += __builtin_popcount(bits[c]);
+        }
+        if (pass == 0) {
+            if (total > kPackArea) atomicAdd(spill_ctr, 1ull);
+            continue;
+        }
+        uint8_t *blk = img + b * kPackBlock;
+        uint8_t *out = nullptr;
+        if (total > kPackArea) {
+            out = spill + atomicAdd(spill_ctr, 1ull) * 128;
+            const uint64_t addr = (uint64_t)(uintptr_t)out;
+            for (uint32_t k = 0; k < 8; ++k) blk[pack_area_byte(k)] = (uint8_t)(addr >> (8 * k));
+        }
+        uint32_t o = 0;
+#pragma unroll
+        for (int c = 0; c < A; ++c) {
+            const uint2 rb = *reinterpret_cast<const uint2 *>(pb + 8 * c);
+            *reinterpret_cast<uint16_t *>(blk + 16 * (c / 2) + 2 * (c % 2)) = (uint16_t)bits[c];
+            for (uint32_t x = bits[c]; x; x &= x - 1) {
+                const uint32_t t = half + __builtin_ctz(x);
+                const uint64_t jc = rb.x + __builtin_popcount(rb.y & ((1u << t) - 1u));
+                const uint32_t m = draw_mask(T[c], args.nT[c], draw(args.K[c], jc));
+                local += __builtin_popcount(m);
+                if (out) out[o] = (uint8_t)m;
+                else blk[pack_area_byte(o)] = (uint8_t)m;
+                ++o;
+            }
+        }
+    }
+    if (pass == 1) {
+        for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off);
+        if ((threadIdx.x & 63) == 0 && local) atomicAdd(ones, (unsigned long long)local);
+    }
+}
+
+template <int A>
+void launch_pack(uint8_t *img, uint64_t L, const uint8_t *plane, uint32_t pstride, const PackArgs &args,
+                 uint8_t *spill, unsigned long long *ctr, unsigned long long *ones, int pass, hipStream_t s) {
+    const uint64_t nb = (L + kPackSpan - 1) / kPackSpan;
+    hipLaunchKernelGGL(k_gen_pack<A>, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nb + 255) / 256, 65536))),
+                       dim3(256), 0, s, img, L, plane, pstride, args, spill, ctr, ones, pass);
+}
+using PackFn = void (*)(uint8_t *, uint64_t, const uint8_t *, uint32_t, const PackArgs &, uint8_t *,
+                        unsigned long long *, unsigned long long *, int, hipStream_t);
+PackFn pack_fn(uint32_t a) {
+    static const PackFn t[] = {nullptr, launch_pack<1>, launch_pack<2>, launch_pack<3>, launch_pack<4>,
+                               launch_pack<5>, launch_pack<6>, launch_pack<7>, launch_pack<8>};
+    return a >= 1 && a <= 8 ? t[a] : nullptr;
+}
+
 // ---- per-child rank scan over the blocks of a KIND_PLANE image ----------
 constexpr int kScanTile = 256;  // blocks per tile (one thread per block)
 
@@ -584,13 +664,88 @@ int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStr
         }
     }
     // internal nodes in BFS order: parents are generated before children
+    std::vector<bool> in_pack(N, false);  // MASK8 children of a KIND_PACK node: no image
+    unsigned long long *d_ctr = nullptr;
+    if (hipMalloc(&d_ctr, sizeof(unsigned long long)) != hipSuccess) return fail(MBRWT_ERR_NOMEM, "hipMalloc");
     for (uint32_t u = 0; u < N; ++u) {
         const auto &sh = shape[u];
         DevNode &dn = tree.nodes[u + 1];
-        if (sh.children.empty() || dn.kind == KIND_FOLDED) continue;
+        if (sh.children.empty() || dn.kind == KIND_FOLDED || in_pack[u]) continue;
         const uint64_t L = dn.length;  // positions = popcount of u's own column
         const uint64_t K = node_key(desc.seed, u);
         const uint32_t a = dn.arity, nT = (1u << a) - 1;
+        // KIND_PACK when every child is a MASK8 node with <= 8 leaves and a
+        // block of 16 positions is expected to hold <= 30 masks (rare spills)
+        bool pack = pack_enabled() && dn.kind == KIND_PLANE && a <= 8;
+        double expect = 0.0;
+        for (uint32_t c = 0; pack && c < a; ++c) {
+            const DevNode &ch = tree.nodes[sh.children[c] + 1];
+            pack = ch.kind == KIND_MASK8 && ch.arity <= 8;
+            expect += q[sh.children[c]];
+        }
+        if (pack && q[u] > 0.0 && kPackSpan * expect / q[u] > 30.0) pack = false;
+        if (pack) {
+            void *tmp = nullptr;
+            const uint64_t pbytes = ((L + 31) / 32) * dn.stride + kImagePad;
+            if (hipMalloc(&tmp, pbytes) != hipSuccess) {
+                (void)hipFree(d_ctr);
+                return fail(MBRWT_ERR_NOMEM, "device allocation failed");
+            }
+            (void)hipMemsetAsync(tmp, 0, pbytes, s);
+            uint8_t *pl = reinterpret_cast<uint8_t *>(tmp);
+            plane_fn(a)(pl, L, K, node_T[u], nT, dn.stride, s);
+            std::vector<uint64_t> tot;
+            if ((rc = plane_scan(pl, L, a, dn.stride, tot, s))) {
+                (void)hipFree(tmp);
+                (void)hipFree(d_ctr);
+                return fail(rc, "plane scan");
+            }
+            PackArgs args{};
+            for (uint32_t c = 0; c < a; ++c) {
+                const uint32_t cu = sh.children[c];
+                DevNode &ch = tree.nodes[cu + 1];
+                ch.length = tot[c];
+                ch.base = 0;
+                in_pack[cu] = true;
+                args.T[c] = node_T[cu];
+                args.nT[c] = (1u << ch.arity) - 1;
+                args.K[c] = node_key(desc.seed, cu);
+            }
+            const uint32_t pstride = dn.stride;
+            (void)hipMemsetAsync(d_ctr, 0, sizeof(unsigned long long), s);
+            pack_fn(a)(nullptr, L, pl, pstride, args, nullptr, d_ctr, d_ones, 0, s);
+            unsigned long long nspill = 0;
+            MBRWT_HIP(hipMemcpyAsync(&nspill, d_ctr, sizeof(nspill), hipMemcpyDeviceToHost, s));
+            MBRWT_HIP(hipStreamSynchronize(s));
+            uint8_t *spill = nullptr;
+            if (nspill) {
+                DevNode dummy;
+                spill = alloc_image(dummy, nspill * 128);
+                if (!spill) {
+                    (void)hipFree(tmp);
+                    (void)hipFree(d_ctr);
+                    return fail(MBRWT_ERR_NOMEM, "device allocation failed");
+                }
+            }
+            dn.kind = KIND_PACK;
+            dn.stride = kPackBlock;
+            uint8_t *img = alloc_image(dn, ((L + kPackSpan - 1) / kPackSpan) * kPackBlock);
+            if (!img) {
+                (void)hipFree(tmp);
+                (void)hipFree(d_ctr);
+                return fail(MBRWT_ERR_NOMEM, "device allocation failed");
+            }
+            (void)hipMemsetAsync(d_ctr, 0, sizeof(unsigned long long), s);
+            pack_fn(a)(img, L, pl, pstride, args, spill, d_ctr, d_ones, 1, s);
+            if (hipGetLastError() != hipSuccess) {
+                (void)hipFree(tmp);
+                (void)hipFree(d_ctr);
+                return fail(MBRWT_ERR_DEVICE, "pack kernel");
+            }
+            MBRWT_HIP(hipStreamSynchronize(s));
+            (void)hipFree(tmp);
+            continue;
+        }
         if (dn.kind == KIND_PLANE) {
             uint8_t *img = alloc_image(dn, ((L + 31) / 32) * dn.stride);
             if (!img) return fail(MBRWT_ERR_NOMEM, "device allocation failed");
@@ -610,6 +765,7 @@ int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStr
             if (hipGetLastError() != hipSuccess) return fail(MBRWT_ERR_DEVICE, "mask kernel");
         }
     }
+    (void)hipFree(d_ctr);
     unsigned long long ones = 0;
     if (hipMemcpyAsync(&ones, d_ones, sizeof(ones), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)

@@ -160,12 +160,11 @@ int mbrwt_count_work_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, 
 /* Options (mbrwt_set_option). */
 #define MBRWT_OPT_TIMING 1       /* 1: time the traversal kernel with HIP events */
 #define MBRWT_OPT_SLOT_LABELS 2  /* per-row label slots of the fast path (0 = auto) */
-#define MBRWT_OPT_KERNEL 4       /* traversal kernel (A/B measurement): 0 default, 1 lane-per-row,
-                                    2/3/4 group with 1/2/4 children per lane, 5/6 group at 8/6 waves per SIMD,
-                                    10 group + non-temporal reads, 11/12 fast kernel (+ non-temporal),
-                                    13/14 fast kernel without inline MASK8 children,
-                                    17/18 fast2 kernel (+ non-temporal; the default where eligible),
-                                    19/20 fast3 (two rows per group); others rejected */
+#define MBRWT_OPT_KERNEL 4       /* traversal kernel (A/B measurement): 0 default (k_traverse_fast2 where
+                                    eligible, else the group kernel), 1 lane-per-row, 2/3/4 group with
+                                    1/2/4 children per lane, 5/6 group at 8/6 waves per SIMD, 10 group +
+                                    non-temporal reads, 17/18 k_traverse_fast2 plain / non-temporal;
+                                    others rejected */
 int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value);
 
 /* Traversal-kernel time accumulated while MBRWT_OPT_TIMING is on (ms, launches); resets the sums. */
