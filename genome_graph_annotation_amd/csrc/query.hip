@@ -40,6 +40,7 @@ struct TravParams {
     uint32_t K;
     uint32_t *temp;              // MODE_SLOTS: [n_batch][K]
     uint32_t *counts;            // MODE_SLOTS: [n_batch]
+    uint32_t *chunk_counts;      // k_traverse_fast2: labels per 8-row chunk [n_batch / 8]
     uint32_t *ovf_list;          // MODE_SLOTS
     unsigned long long *scalars; // [0] total, [1] overflow count, [2] error flags, [3] visits, [4] labels
     const uint64_t *offsets;     // MODE_DIRECT
@@ -669,7 +670,11 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
     uint64_t chunk = gid;
     uint32_t ri = 0;
     uint64_t slot = chunk * 8;
-    uint32_t *slot_ptr = p.temp + slot * p.K;
+    // output: the labels of a chunk's rows are packed back to back in the
+    // chunk's 8*K-label region (rows with > K labels are left out for the
+    // overflow pass), so the compaction is a contiguous copy per chunk
+    uint32_t running = 0, chunk_total = 0;
+    uint32_t *slot_ptr = p.temp + chunk * 8 * p.K;
 
     // SMALLK: K == kStageLabels, every kept label fits the stage
     auto emit = [&](uint32_t pos, uint32_t label) {
@@ -695,8 +700,7 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const uint32_t lim = cnt < kStageLabels ? cnt : kStageLabels;
-            for (uint32_t q = c; 4 * q < lim; q += 4)
-                gst(reinterpret_cast<u32x4_t *>(slot_ptr) + q, (u32x4_t)((AS_LDS u32x4_t *)stage)[q]);
+            for (uint32_t q = c; q < lim; q += 4) gst(slot_ptr + q, (uint32_t)stage[q]);
             if (c == 0) {
                 gst(p.counts + slot, cnt);
                 if (cnt > p.K) {
@@ -704,13 +708,18 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
                     gst(p.ovf_list + k, (uint32_t)slot);
                 }
             }
+            if (cnt <= p.K) running += cnt;
+            chunk_total += cnt;
+            if ((ri == 7 || slot + 1 == p.n) && c == 0) gst(p.chunk_counts + chunk, chunk_total);
             if (++ri == 8) {
                 ri = 0;
+                running = 0;
+                chunk_total = 0;
                 chunk += ngroups;
                 if (chunk * 8 < p.n) load_chunk();
             }
             slot = chunk * 8 + ri;
-            slot_ptr = p.temp + slot * p.K;
+            slot_ptr = p.temp + chunk * 8 * p.K + running;
             active = slot < p.n;
             fresh = active;
         }
@@ -860,6 +869,65 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
 // find each position's row by a binary search over the tile's offsets in
 // LDS, and read the slot labels (a row's labels are adjacent in its slot).
 constexpr int kCompactTile = 256;
+
+// k_compact_chunks: output of k_traverse_fast2 -> CSR.  The traversal packs
+// the labels of the 8 rows of chunk ch back to back at temp + ch*8*K (rows
+// with more than K labels left out for the overflow pass) and counts labels
+// per row and per chunk; the scan runs over the chunk counts only.  Here 8
+// lanes per chunk (8 chunks per wave) write the chunk's 8 row offsets (chunk
+// offset + in-chunk prefix) and copy the packed labels; each lane issues its
+// (up to 8) label reads before any store.  Contiguous reads and writes.
+__global__ __launch_bounds__(256) void k_compact_chunks(const uint32_t *__restrict__ counts,
+                                                        const uint64_t *__restrict__ chunk_offsets,
+                                                        const uint32_t *__restrict__ temp, uint32_t K,
+                                                        uint64_t *__restrict__ offsets, uint32_t *__restrict__ cols,
+                                                        uint64_t n) {
+    const uint32_t lane = threadIdx.x & 63, sub = lane & 7, gb = lane & ~7u;
+    const uint64_t nch = (n + 7) / 8;
+    const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) >> 3;
+    for (uint64_t ch = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3; ch < nch; ch += stride) {
+        const uint64_t r0 = ch * 8;
+        const uint32_t nr = (uint32_t)(n - r0 < 8 ? n - r0 : 8);
+        const uint64_t base = gld(chunk_offsets + ch);
+        const uint32_t mine = sub < nr ? gld(counts + r0 + sub) : 0u;
+        uint32_t cr[8];
+#pragma unroll
+        for (uint32_t r = 0; r < 8; ++r) cr[r] = (uint32_t)__shfl((int)mine, (int)(gb + r), 64);
+        uint32_t pre[9], buf[9];
+        pre[0] = buf[0] = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < 8; ++r) {
+            pre[r + 1] = pre[r] + cr[r];
+            buf[r + 1] = buf[r] + (cr[r] <= K ? cr[r] : 0u);  // overflow rows hold no labels here
+        }
+        if (sub < nr) gst(offsets + r0 + sub, base + pre[sub]);
+        if (sub == 0 && r0 + nr == n) gst(offsets + n, base + pre[nr]);
+        const uint32_t stored = buf[nr];
+        const uint32_t *src = temp + ch * 8 * K;
+        for (uint32_t i0 = 0; i0 < stored; i0 += 64) {
+            uint32_t v[8];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint32_t i = i0 + sub + 8 * k;
+                v[k] = i < stored ? gld(src + i) : 0u;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint32_t i = i0 + sub + 8 * k;
+                if (i >= stored) continue;
+                // the row owning packed label i (empty rows before it share its buf value)
+                uint32_t prow = pre[0], brow = buf[0];
+#pragma unroll
+                for (uint32_t r = 1; r < 8; ++r)
+                    if (r < nr && buf[r] <= i) {
+                        prow = pre[r];
+                        brow = buf[r];
+                    }
+                gst(cols + base + prow + (i - brow), v[k]);
+            }
+        }
+    }
+}
 
 __global__ __launch_bounds__(kCompactTile) void k_compact(const uint64_t *__restrict__ offsets,
                                                           const uint32_t *__restrict__ temp, uint32_t K,
@@ -1137,13 +1205,22 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
         return MBRWT_ERR_UNSUPPORTED;
     }
     int rc;
+    const uint64_t nch = (n + 7) / 8;
+    // counts: n+1 row counts | nch+1 chunk counts | (8-byte aligned) nch+1 chunk offsets
+    const uint64_t cc_off = n + 1, co_off = ((cc_off + nch + 1) * sizeof(uint32_t) + 7) / 8 * 8;
     if ((rc = ensure(c.ws_temp, n * K * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c.ws_counts, (n + 1) * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c.ws_counts, co_off + (nch + 1) * sizeof(uint64_t)))) return rc;
     if ((rc = ensure(c.ws_ovf, n * sizeof(uint32_t)))) return rc;
+    uint32_t *d_counts = reinterpret_cast<uint32_t *>(c.ws_counts.buf);
+    uint32_t *d_chunk_counts = d_counts + cc_off;
+    uint64_t *d_chunk_offsets = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + co_off);
+    // scan input: the row counts (general kernels) or the chunk counts (fast2)
+    hipcub::TransformInputIterator<uint64_t, U32ToU64, const uint32_t *> it(fn.fast ? d_chunk_counts : d_counts,
+                                                                            U32ToU64());
+    uint64_t *scan_out = fn.fast ? d_chunk_offsets : d_offsets;
+    const uint64_t scan_n = (fn.fast ? nch : n) + 1;
     size_t scan_bytes = 0;
-    hipcub::TransformInputIterator<uint64_t, U32ToU64, const uint32_t *> it(
-        reinterpret_cast<const uint32_t *>(c.ws_counts.buf), U32ToU64());
-    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, it, d_offsets, n + 1, s));
+    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, it, scan_out, scan_n, s));
     if ((rc = ensure(c.ws_scan, scan_bytes))) return rc;
 
     TravParams p = base_params(c);
@@ -1151,16 +1228,17 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
     p.n = n;
     p.K = K;
     p.temp = reinterpret_cast<uint32_t *>(c.ws_temp.buf);
-    p.counts = reinterpret_cast<uint32_t *>(c.ws_counts.buf);
+    p.counts = d_counts;
+    p.chunk_counts = d_chunk_counts;
     p.ovf_list = reinterpret_cast<uint32_t *>(c.ws_ovf.buf);
 
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
-    MBRWT_HIP(hipMemsetAsync(p.counts + n, 0, sizeof(uint32_t), s));
+    MBRWT_HIP(hipMemsetAsync(fn.fast ? d_chunk_counts + nch : d_counts + n, 0, sizeof(uint32_t), s));
     if (c.timing) MBRWT_HIP(hipEventRecord(c.ev0, s));
     MBRWT_HIP(launch(c, fn, n, s, p));
     if (c.timing) MBRWT_HIP(hipEventRecord(c.ev1, s));
-    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_offsets, n + 1, s));
-    MBRWT_HIP(hipMemcpyAsync(c.d_scalars, d_offsets + n, sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, scan_out, scan_n, s));
+    MBRWT_HIP(hipMemcpyAsync(c.d_scalars, scan_out + scan_n - 1, sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
     MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     MBRWT_HIP(hipStreamSynchronize(s));
     if (c.timing) {
@@ -1184,8 +1262,15 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
         return MBRWT_ERR_CAPACITY;
     }
     {
-        const uint64_t g = std::min<uint64_t>((n + kCompactTile - 1) / kCompactTile, 16384);
-        hipLaunchKernelGGL(k_compact, dim3((unsigned)g), dim3(kCompactTile), 0, s, d_offsets, p.temp, K, d_cols, n);
+        if (fn.fast) {  // chunk-packed output (k_traverse_fast2)
+            const uint64_t g = std::min<uint64_t>(((n + 7) / 8 + 31) / 32, 8192);
+            hipLaunchKernelGGL(k_compact_chunks, dim3((unsigned)g), dim3(256), 0, s, d_counts, d_chunk_offsets, p.temp,
+                               K, d_offsets, d_cols, n);
+        } else {
+            const uint64_t g = std::min<uint64_t>((n + kCompactTile - 1) / kCompactTile, 16384);
+            hipLaunchKernelGGL(k_compact, dim3((unsigned)g), dim3(kCompactTile), 0, s, d_offsets, p.temp, K, d_cols,
+                               n);
+        }
         MBRWT_HIP(hipGetLastError());
     }
     if (ovf) {
