@@ -675,7 +675,7 @@ int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStr
         const uint64_t K = node_key(desc.seed, u);
         const uint32_t a = dn.arity, nT = (1u << a) - 1;
         // KIND_PACK when every child is a MASK8 node with <= 8 leaves and a
-        // block of 16 positions is expected to hold <= 30 masks (rare spills)
+        // block of 16 positions is expected to hold <= 40 masks (spills: ~1 % of the blocks)
         bool pack = pack_enabled() && dn.kind == KIND_PLANE && a <= 8;
         double expect = 0.0;
         for (uint32_t c = 0; pack && c < a; ++c) {
@@ -683,7 +683,7 @@ int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStr
             pack = ch.kind == KIND_MASK8 && ch.arity <= 8;
             expect += q[sh.children[c]];
         }
-        if (pack && q[u] > 0.0 && kPackSpan * expect / q[u] > 30.0) pack = false;
+        if (pack && q[u] > 0.0 && kPackSpan * expect / q[u] > 40.0) pack = false;
         if (pack) {
             void *tmp = nullptr;
             const uint64_t pbytes = ((L + 31) / 32) * dn.stride + kImagePad;
