@@ -28,12 +28,34 @@ constexpr int kColThreads = 256;  // one thread = one 32-position word
 // Word w (positions 32w .. 32w+31, clipped to len) of child slot c's column
 // inside the image of node nd.  For a KIND_PACK node the word marks the
 // positions where child c is set AND its MASK8 mask has bit `leaf` (the
-// leaf's positions lifted through the image-less MASK8 child at once).
+// leaf's positions lifted through the image-less MASK8 child at once); for a
+// KIND_PACK2 node, where child c, its child leaf >> 8 and that child's leaf
+// (leaf & 0xFF) are all set (two image-less levels lifted at once).
 __device__ __forceinline__ uint32_t column_word(const DevNode &nd, uint32_t c, uint64_t w, uint64_t len,
                                                 uint32_t leaf) {
     if (32 * w >= len) return 0;
     uint32_t bits = 0;
-    if (nd.kind == KIND_PACK) {
+    if (nd.kind == KIND_PACK2) {  // leaf = (B << 8) | leaf slot of the MASK8 grandchild B below child c
+        const uint32_t B = leaf >> 8, lf = leaf & 0xFFu;
+        for (uint32_t h = 0; h < 32 / kPack2Span; ++h) {
+            const uint64_t j0 = 32 * w + kPack2Span * h;
+            if (j0 >= len) break;
+            Pack2Block pb;
+            pb.load(nd.base, (uint32_t)j0);
+            for (uint32_t t = 0; t < kPack2Span && j0 + t < len; ++t) {
+                const uint32_t s = pb.start(t);
+                const uint32_t m2 = pb.byte(s);
+                if (!((m2 >> c) & 1u)) continue;
+                const uint32_t i = (uint32_t)__builtin_popcount(m2 & ((1u << c) - 1u));
+                const uint32_t m1 = pb.byte(s + 1 + i);
+                if (!((m1 >> B) & 1u)) continue;
+                uint32_t o = s + 1 + (uint32_t)__builtin_popcount(m2);
+                for (uint32_t q = 0; q < i; ++q) o += (uint32_t)__builtin_popcount(pb.byte(s + 1 + q));
+                o += (uint32_t)__builtin_popcount(m1 & ((1u << B) - 1u));
+                if ((pb.byte(o) >> lf) & 1u) bits |= 1u << (kPack2Span * h + t);
+            }
+        }
+    } else if (nd.kind == KIND_PACK) {
         for (uint32_t h = 0; h < 32 / kPackSpan; ++h) {
             const uint64_t j0 = 32 * w + kPackSpan * h;
             if (j0 >= len) break;
@@ -152,7 +174,13 @@ int run_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap,
     // parent is a MASK8 child of a KIND_PACK node, out of the PACK image
     // (positions in the PACK node's space; the MASK8 level has no image)
     uint32_t leaf_bit = 0;
-    if (path.size() >= 2 && t.nodes[path[path.size() - 2].first].kind == KIND_PACK) {
+    if (path.size() >= 3 && t.nodes[path[path.size() - 3].first].kind == KIND_PACK2) {
+        // two image-less levels: positions come out of the PACK2 node's records
+        leaf_bit = path.back().second;
+        path.pop_back();
+        leaf_bit |= path.back().second << 8;
+        path.pop_back();
+    } else if (path.size() >= 2 && t.nodes[path[path.size() - 2].first].kind == KIND_PACK) {
         leaf_bit = path.back().second;
         path.pop_back();
     }

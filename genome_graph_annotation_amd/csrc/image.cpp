@@ -178,6 +178,108 @@ bool pack_candidate(const mbrwt_tree_desc &desc, uint32_t u) {
     return true;
 }
 
+// desc node u may become KIND_PACK2: 1..8 children, each a KIND_PACK candidate
+bool pack2_candidate(const mbrwt_tree_desc &desc, uint32_t u) {
+    const uint32_t a = desc.num_children[u];
+    if (a == 0 || a > 8) return false;
+    for (uint32_t c = 0; c < a; ++c)
+        if (!pack_candidate(desc, desc.first_child[u] + c)) return false;
+    return true;
+}
+
+inline uint32_t desc_bit(const mbrwt_tree_desc &desc, uint32_t node, uint64_t j) {
+    return (uint32_t)((desc.vec_words[node][j >> 6] >> (j & 63)) & 1);
+}
+
+// KIND_PACK2 image of desc node u (mbrwt_internal.hpp): returns false (and
+// builds nothing) when more than 1 block in 20 would spill.
+bool build_pack2_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, DevNode &dn, std::vector<void *> &images,
+                       uint64_t &image_bytes, int &rc) {
+    rc = MBRWT_OK;
+    const uint32_t a = desc.num_children[u], fc = desc.first_child[u];
+    const uint64_t blocks = (L + kPack2Span - 1) / kPack2Span;
+    std::vector<uint8_t> host(blocks * kPack2Block + kImagePad, 0);
+    std::vector<uint8_t> spill;
+    std::vector<std::pair<uint64_t, uint64_t>> spilled;  // (block, offset in spill)
+    std::vector<uint64_t> rA(a, 0), rB(8 * a, 0);         // running ranks of the A and B columns
+    std::vector<uint8_t> rec;
+    for (uint64_t b = 0; b < blocks; ++b) {
+        rec.clear();
+        uint32_t start[kPack2Span];
+        for (uint32_t t = 0; t < kPack2Span; ++t) {
+            const uint64_t j = b * kPack2Span + t;
+            start[t] = (uint32_t)rec.size();
+            if (j >= L) continue;
+            uint32_t m2 = 0;
+            for (uint32_t A = 0; A < a; ++A) m2 |= desc_bit(desc, fc + A, j) << A;
+            rec.push_back((uint8_t)m2);
+            uint32_t m1s[8] = {0};
+            for (uint32_t A = 0; A < a; ++A) {
+                if (!((m2 >> A) & 1)) continue;
+                const uint32_t na = fc + A, ga = desc.num_children[na], gfa = desc.first_child[na];
+                const uint64_t jA = rA[A]++;
+                for (uint32_t B = 0; B < ga; ++B) m1s[A] |= desc_bit(desc, gfa + B, jA) << B;
+                rec.push_back((uint8_t)m1s[A]);
+            }
+            for (uint32_t A = 0; A < a; ++A) {
+                const uint32_t gfa = desc.first_child[fc + A];
+                for (uint32_t x = m1s[A]; x; x &= x - 1) {
+                    const uint32_t B = (uint32_t)__builtin_ctz(x), nb = gfa + B;
+                    const uint64_t jB = rB[8 * A + B]++;
+                    uint32_t lm = 0;
+                    for (uint32_t k = 0; k < desc.num_children[nb]; ++k)
+                        lm |= desc_bit(desc, desc.first_child[nb] + k, jB) << k;
+                    rec.push_back((uint8_t)lm);
+                }
+            }
+        }
+        uint8_t *blk = &host[b * kPack2Block];
+        if (rec.size() <= kPack2Inline) {
+            for (uint32_t t = 0; t < kPack2Span; ++t) blk[t] = (uint8_t)(8 + start[t]);
+            std::memcpy(blk + 8, rec.data(), rec.size());
+        } else {  // start[0] = 0 marks the block; list = u16 starts, then the records
+            spilled.emplace_back(b, spill.size());
+            for (uint32_t t = 0; t < kPack2Span; ++t) {
+                const uint16_t st = (uint16_t)(2 * kPack2Span + start[t]);
+                spill.push_back((uint8_t)st);
+                spill.push_back((uint8_t)(st >> 8));
+            }
+            spill.insert(spill.end(), rec.begin(), rec.end());
+            if (spill.size() & 1) spill.push_back(0);  // keep the u16 starts aligned
+        }
+    }
+    if (spilled.size() * 20 > blocks) return false;
+    if (!spill.empty()) {
+        void *ds = nullptr;
+        spill.resize(spill.size() + kImagePad, 0);
+        if (hipMalloc(&ds, spill.size()) != hipSuccess || hipMemcpy(ds, spill.data(), spill.size(),
+                                                                      hipMemcpyHostToDevice) != hipSuccess) {
+            rc = hip_fail(hipErrorOutOfMemory, "pack2 spill upload");
+            return true;
+        }
+        images.push_back(ds);
+        image_bytes += spill.size();
+        for (const auto &sb : spilled) {
+            const uint64_t addr = (uint64_t)(uintptr_t)ds + sb.second;
+            std::memcpy(&host[sb.first * kPack2Block + 8], &addr, 8);
+        }
+    }
+    void *d = nullptr;
+    if (hipMalloc(&d, host.size()) != hipSuccess ||
+        hipMemcpy(d, host.data(), host.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        rc = hip_fail(hipErrorOutOfMemory, "pack2 image upload");
+        return true;
+    }
+    images.push_back(d);
+    image_bytes += host.size();
+    dn.kind = KIND_PACK2;
+    dn.arity = (uint16_t)a;
+    dn.stride = kPack2Block;
+    dn.length = L;
+    dn.base = (uint64_t)(uintptr_t)d;
+    return true;
+}
+
 }  // namespace
 
 int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
@@ -318,6 +420,32 @@ int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
     for (uint32_t u = 0; u < N; ++u) {
         const uint32_t a = desc.num_children[u];
         if (!a || (u == 0 && tree.folded) || in_pack[u]) continue;
+        if (pack2_enabled() && pack2_candidate(desc, u)) {
+            int rc = MBRWT_OK;
+            if (build_pack2_image(desc, u, ones[u], tree.nodes[u + 1], tree.images, tree.image_bytes, rc)) {
+                if (rc) return rc;
+                for (uint32_t c = 0; c < a; ++c) {  // children: PACK-shaped records, grandchildren: MASK8 records
+                    const uint32_t ch = desc.first_child[u] + c;
+                    in_pack[ch] = true;
+                    DevNode &cn = tree.nodes[ch + 1];
+                    cn.kind = KIND_PACK;
+                    cn.arity = (uint16_t)desc.num_children[ch];
+                    cn.stride = kPackBlock;
+                    cn.length = ones[ch];
+                    cn.base = 0;
+                    for (uint32_t g = 0; g < desc.num_children[ch]; ++g) {
+                        const uint32_t gc = desc.first_child[ch] + g;
+                        in_pack[gc] = true;
+                        DevNode &gn = tree.nodes[gc + 1];
+                        gn.kind = KIND_MASK8;
+                        gn.arity = (uint16_t)desc.num_children[gc];
+                        gn.length = ones[gc];
+                        gn.base = 0;
+                    }
+                }
+                continue;
+            }
+        }
         if (pack_enabled() && pack_candidate(desc, u)) {
             int rc = MBRWT_OK;
             if (build_pack_image(desc, u, ones[u], tree.nodes[u + 1], tree.images, tree.image_bytes, rc)) {
@@ -372,13 +500,19 @@ int finalize_tree(Tree &tree) {
         }
         if (all) dn.flags |= FLAG_MASK_CHILDREN;
     }
+    tree.has_pack2 = tree.has_mask_children = false;
+    for (uint32_t v = 0; v < D; ++v) {
+        tree.has_pack2 |= tree.nodes[v].kind == KIND_PACK2;
+        tree.has_mask_children |= tree.nodes[v].kind == KIND_PLANE && (tree.nodes[v].flags & FLAG_MASK_CHILDREN);
+    }
     // shape eligible for the specialised kernel: internal nodes PLANE/MASK8 with
     // arity <= 8, MASK8 labels consecutive, no leaf directly under a PLANE node
     tree.fast_shape = true;
     for (uint32_t v = 0; v < D; ++v) {
         const DevNode &dn = tree.nodes[v];
         if (dn.kind == KIND_LEAF || dn.kind == KIND_FOLDED) continue;
-        if (dn.arity > 8 || (dn.kind != KIND_PLANE && dn.kind != KIND_MASK8 && dn.kind != KIND_PACK))
+        if (dn.arity > 8 ||
+            (dn.kind != KIND_PLANE && dn.kind != KIND_MASK8 && dn.kind != KIND_PACK && dn.kind != KIND_PACK2))
             tree.fast_shape = false;
         if (dn.kind == KIND_MASK8 && !(dn.flags & FLAG_CONSEC_LABELS)) tree.fast_shape = false;
         if (dn.kind == KIND_PLANE)

@@ -45,6 +45,7 @@ enum : uint8_t {
     KIND_MASK64 = 5,
     KIND_FOLDED = 6,  // the BRWT root when folded into the super-root (never visited)
     KIND_PACK = 7,    // node whose children are all MASK8 nodes: children bits + their masks inline
+    KIND_PACK2 = 8,   // node whose children are all PACK-shaped: the whole 3-level subtree inline
 };
 inline bool is_mask_kind(uint8_t k) { return k >= KIND_MASK8 && k <= KIND_MASK64; }
 
@@ -60,6 +61,23 @@ constexpr uint32_t kPackBlock = 64;
 constexpr uint32_t kPackArea = 48;
 // byte offset inside a block of logical mask-area byte o
 __host__ __device__ inline uint32_t pack_area_byte(uint32_t o) { return 16 * (o / 12) + 4 + o % 12; }
+
+// KIND_PACK2 image (node u whose children A are all PACK-shaped: each A has
+// 1..8 MASK8 children B with consecutive leaf columns): one 64-byte block per
+// 8 positions of u.  Bytes 0..7 = start[t], the byte offset of position t's
+// record (start[0] = 8); records back to back.  Record of position j =
+//   m2                      u's children bits at j (never 0: u's bit is set),
+//   m1(A) per set A         A's children bits at A's position (rank1(A, j) - 1),
+//   leaf(A,B) per set A, per set B of m1(A), both in child order
+//                           B's leaf mask at B's position,
+// i.e. the index bits of the whole subtree below u at j, in the reference's
+// pre-order (BRWT.cpp:45-51).  A block whose records exceed 56 bytes holds
+// start[0] = 0 and, in bytes 8..15, the address of a spill list: u16 start[8]
+// (relative to the list) followed by the records.  The A and B nodes keep
+// their records (arity, first child, labels) but have no image.
+constexpr uint32_t kPack2Span = 8;
+constexpr uint32_t kPack2Block = 64;
+constexpr uint32_t kPack2Inline = 56;  // record bytes that fit after the header
 // FLAG_CONSEC_LABELS (MASK nodes): child c's label = label + c.
 // FLAG_MASK_CHILDREN (PLANE nodes): every child is a KIND_MASK8 node with
 // consecutive labels, so the fast kernel resolves the children in the
@@ -81,8 +99,9 @@ static_assert(sizeof(DevNode) == 32, "DevNode must be 32 bytes");
 // Compact 16-byte node record read by the group kernel (kept in LDS for the
 // first kLdsNodes dnodes -- in BFS numbering the internal nodes come first):
 //   w0 = base[0:48) | kind[48:51) | flag[51] | log2(stride)[52:56) | arity[56:64)
-// flag = FLAG_MASK_CHILDREN for KIND_PLANE, FLAG_CONSEC_LABELS otherwise
-// (unused for KIND_PACK; its log2(stride) is 6).
+// flag = FLAG_MASK_CHILDREN for KIND_PLANE, FLAG_CONSEC_LABELS for MASK kinds;
+// KIND_PACK2 is stored as kind KIND_PACK with flag 1 (kind bits 48..51 = 0xF).
+// For KIND_PACK / KIND_PACK2 log2(stride) is 6.
 struct alignas(16) CNode {
     uint64_t w0;
     uint32_t first_child;
@@ -96,8 +115,12 @@ inline CNode compact(const DevNode &d) {
     uint32_t lg = 0;
     while (d.stride && (1u << lg) < d.stride) ++lg;
     CNode c;
-    const uint64_t flag = d.kind == KIND_PLANE ? (d.flags & FLAG_MASK_CHILDREN) ? 1 : 0 : (d.flags & FLAG_CONSEC_LABELS);
-    c.w0 = (d.base & ((1ull << 48) - 1)) | ((uint64_t)(d.kind & 7) << 48) | (flag << 51) |
+    const uint64_t flag = d.kind == KIND_PLANE   ? ((d.flags & FLAG_MASK_CHILDREN) ? 1 : 0)
+                          : d.kind == KIND_PACK2 ? 1
+                          : d.kind == KIND_PACK  ? 0
+                                                 : (d.flags & FLAG_CONSEC_LABELS);
+    const uint64_t kind = d.kind == KIND_PACK2 ? KIND_PACK : d.kind;
+    c.w0 = (d.base & ((1ull << 48) - 1)) | ((kind & 7) << 48) | (flag << 51) |
            ((uint64_t)(lg & 15) << 52) | ((uint64_t)(d.arity & 0xFF) << 56);
     c.first_child = d.first_child;
     c.label = d.label;
@@ -129,6 +152,8 @@ struct Tree {
     bool folded = false;                    // root folded into the super-root
     bool fast_shape = false;                // eligible for k_traverse_fast (finalize_tree)
     bool lds_complete = false;              // every non-leaf dnode id < kLdsNodes (k_traverse_fast2)
+    bool has_pack2 = false;                 // some node is KIND_PACK2
+    bool has_mask_children = false;         // some PLANE node has FLAG_MASK_CHILDREN
     uint32_t push_frames = 0;               // max stack frames of the fast kernels (non-TERM PLANE nodes on a path)
     uint32_t lds_records = 0;               // last non-leaf dnode id + 1 (node records worth staging in LDS)
     uint32_t max_arity = 0;
@@ -195,6 +220,11 @@ inline bool fold_root_enabled() {
 inline bool pack_enabled() {
     const char *e = std::getenv("MBRWT_PACK");
     return !(e && e[0] == '0');
+}
+// KIND_PACK2 nodes are built unless MBRWT_PACK2=0 or MBRWT_PACK=0
+inline bool pack2_enabled() {
+    const char *e = std::getenv("MBRWT_PACK2");
+    return pack_enabled() && !(e && e[0] == '0');
 }
 
 // queries (query.hip)

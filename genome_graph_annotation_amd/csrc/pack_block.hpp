@@ -43,3 +43,41 @@ struct PackBlock {
 };
 
 }  // namespace mbrwt
+
+namespace mbrwt {
+
+// KIND_PACK2 block access for the general kernels (layout in
+// mbrwt_internal.hpp): the 64-byte block in 16 registers, record bytes
+// picked by selects, or read from the spill list.
+struct Pack2Block {
+    uint32_t w[16];
+    bool spilled;
+    uint64_t sa;  // spill list address
+    __device__ __forceinline__ void load(uint64_t base, uint32_t j) {
+        const uint64_t blk = base + (uint64_t)(j / kPack2Span) * kPack2Block;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const uint4 q = gld_at<uint4>(blk + 16 * h);
+            w[4 * h] = q.x;
+            w[4 * h + 1] = q.y;
+            w[4 * h + 2] = q.z;
+            w[4 * h + 3] = q.w;
+        }
+        spilled = (w[0] & 0xFFu) == 0;
+        sa = ((uint64_t)w[3] << 32) | w[2];
+    }
+    __device__ __forceinline__ uint32_t byte(uint32_t o) const {
+        if (spilled) return gld_at<uint8_t>(sa + o);
+        uint32_t x = w[0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) x = (o >> 2) == (uint32_t)i ? w[i] : x;
+        return (x >> (8 * (o & 3))) & 0xFFu;
+    }
+    // byte offset of the record of position t (t = j % kPack2Span)
+    __device__ __forceinline__ uint32_t start(uint32_t t) const {
+        if (spilled) return gld_at<uint16_t>(sa + 2ull * t);
+        return byte(t);
+    }
+};
+
+}  // namespace mbrwt

@@ -66,6 +66,7 @@ __device__ __forceinline__ NodeInfo decode(uint64_t w0, uint64_t w1) {
     n.base = w0 & ((1ull << 48) - 1);
     n.kind = (uint32_t)(w0 >> 48) & 7u;
     n.flags = (uint32_t)(w0 >> 51) & 1u;
+    if (n.kind == KIND_PACK && n.flags) n.kind = KIND_PACK2;  // CNode encoding (mbrwt_internal.hpp)
     n.stride = 1u << ((uint32_t)(w0 >> 52) & 15u);
     n.arity = (uint32_t)(w0 >> 56);
     n.first_child = (uint32_t)w1;
@@ -141,6 +142,24 @@ __device__ __forceinline__ void enter(const TravParams &p, Frames<MAXD, MaskT> &
     const uint32_t a = nd.arity;
     const uint64_t base = nd.base;
     if constexpr (MODE == MODE_WORK) sk.visits += a;  // operator[] on every child (BRWT.cpp:30)
+    if (kind == KIND_PACK2) {  // the whole subtree below v at j, in pre-order
+        Pack2Block pb;
+        pb.load(base, j);
+        const uint32_t s = pb.start(j % kPack2Span);
+        const uint32_t m2 = pb.byte(s);
+        uint32_t o1 = s + 1, o2 = s + 1 + (uint32_t)__builtin_popcount(m2);
+        for (uint32_t A = 0; A < a; ++A) {
+            if (!((m2 >> A) & 1u)) continue;
+            const DevNode na = gld(p.nodes + nd.first_child + A);
+            if constexpr (MODE == MODE_WORK) sk.visits += na.arity;
+            for (uint32_t x = pb.byte(o1++); x; x &= x - 1) {
+                const DevNode nb = gld(p.nodes + na.first_child + (uint32_t)__builtin_ctz(x));
+                if constexpr (MODE == MODE_WORK) sk.visits += nb.arity;
+                for (uint32_t m = pb.byte(o2++); m; m &= m - 1) sk.emit(p, nb.label + (uint32_t)__builtin_ctz(m));
+            }
+        }
+        return;
+    }
     if (kind == KIND_PACK) {  // children are MASK8 nodes: resolve them here, in child order
         PackBlock pb;
         pb.load(base, j);
@@ -400,6 +419,35 @@ __device__ __forceinline__ void group_visit(const TravParams &p, GroupFrames<MAX
     const uint32_t a = nd.arity;
     const uint64_t base = nd.base;
     if constexpr (MODE == MODE_WORK) sk.visits += a;  // operator[] on every child (BRWT.cpp:30)
+    if (nd.kind == KIND_PACK2) {
+        // every lane walks the whole record; each emits the labels below its
+        // own children at their rank among the node's labels (pre-order)
+        Pack2Block pb;
+        pb.load(base, j);
+        const uint32_t s = pb.start(j % kPack2Span);
+        const uint32_t m2 = pb.byte(s);
+        uint32_t o1 = s + 1, o2 = s + 1 + (uint32_t)__builtin_popcount(m2), total = 0;
+        const uint64_t *cn = reinterpret_cast<const uint64_t *>(p.cnodes);
+        for (uint32_t A = 0; A < a; ++A) {
+            if (!((m2 >> A) & 1u)) continue;
+            const uint32_t wa = nd.first_child + A;
+            const NodeInfo na = decode(gld(cn + 2 * wa), gld(cn + 2 * wa + 1));
+            if constexpr (MODE == MODE_WORK) sk.visits += na.arity;
+            for (uint32_t x = pb.byte(o1++); x; x &= x - 1) {
+                const uint32_t wb = na.first_child + (uint32_t)__builtin_ctz(x);
+                const NodeInfo nb = decode(gld(cn + 2 * wb), gld(cn + 2 * wb + 1));
+                if constexpr (MODE == MODE_WORK) sk.visits += nb.arity;
+                const uint32_t lm = pb.byte(o2++);
+                if (A / CPL == c) {
+                    uint32_t r = total;
+                    for (uint32_t mm = lm; mm; mm &= mm - 1) sk.put(p, r++, nb.label + (uint32_t)__builtin_ctz(mm));
+                }
+                total += (uint32_t)__builtin_popcount(lm);
+            }
+        }
+        sk.cnt += total;
+        return;
+    }
     if (nd.kind == KIND_PACK) {
         // every lane holds the whole block; each emits the labels of its own
         // children at their rank among the node's labels (child order)
@@ -644,8 +692,11 @@ __device__ __forceinline__ uint32_t quad_exclusive_sum(uint32_t v, uint32_t c, u
 // Labels are staged in LDS (32 per row) and flushed as 16-byte vectors when
 // the row ends (vmcnt counts stores on CDNA4: no stores inside the descent).
 // ------------------------------------------------------------------------
-template <bool NT, bool SMALLK>
+template <bool NT, bool SMALLK, bool P2>
 __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
+    // P2: trees with KIND_PACK2 nodes (one stack frame, no FLAG_MASK_CHILDREN
+    // nodes): the PACK2 visit replaces the MASK_CHILDREN one, a shorter stack
+    constexpr int kFastMaxd = P2 ? 1 : (int)mbrwt::kFastMaxd;
     constexpr uint64_t M48 = (1ull << 48) - 1;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c = lane & 3;
@@ -776,6 +827,55 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
             for (; m1; m1 &= m1 - 1) emit(pos++, l1 + (uint32_t)__builtin_ctz(m1));
             cnt += total;
         };
+        if (P2 && ((w0 >> 48) & 15u) == 15u) {  // KIND_PACK2 (kind PACK + flag): the subtree below at j
+            // one coalesced 64-byte block read; staged in LDS, each lane takes
+            // children 2c, 2c+1 of the node: their m1 bytes, then the leaf
+            // masks of their set children (offsets by quad scans)
+            const uint32_t t = j % kPack2Span;
+            const uint4 q = gld_at_nt<uint4, NT>(base + (uint64_t)(j / kPack2Span) * kPack2Block + 16u * c);
+            ((AS_LDS u32x4_t *)pk)[c] = u32x4_t{q.x, q.y, q.z, q.w};
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const AS_LDS uint8_t *pb = (const AS_LDS uint8_t *)pk;
+            const bool spilled = pb[0] == 0;
+            uint64_t sa = 0;
+            uint32_t s = pb[t];
+            if (spilled) {  // rare: records in a spill list (bytes 8..15 = its address)
+                sa = ((uint64_t)pk[3] << 32) | pk[2];
+                s = gld_at<uint16_t>(sa + 2ull * t);
+            }
+            auto rd = [&](uint32_t o) -> uint32_t {
+                return spilled ? (uint32_t)gld_at<uint8_t>(sa + o) : (uint32_t)pb[o];
+            };
+            const uint32_t m2 = rd(s);
+            const uint32_t A0 = 2 * c;
+            const uint32_t bA0 = (m2 >> A0) & 1u, bA1 = (m2 >> (A0 + 1)) & 1u;
+            const uint32_t i0 = s + 1 + (uint32_t)__builtin_popcount(m2 & ((1u << A0) - 1u));
+            const uint32_t m10 = bA0 ? rd(i0) : 0u;
+            const uint32_t m11 = bA1 ? rd(i0 + bA0) : 0u;
+            const uint32_t n1 = (uint32_t)__builtin_popcount(m10) + (uint32_t)__builtin_popcount(m11);
+            uint32_t n1_tot;
+            const uint32_t o2 = s + 1 + (uint32_t)__builtin_popcount(m2) + quad_exclusive_sum(n1, c, n1_tot);
+            uint32_t nl = 0;
+            for (uint32_t k = 0; k < n1; ++k) nl += (uint32_t)__builtin_popcount(rd(o2 + k));
+            uint32_t ltot;
+            uint32_t pos = cnt + quad_exclusive_sum(nl, c, ltot);
+            const uint32_t fc = (uint32_t)w1;
+            uint32_t o = o2;
+#pragma unroll
+            for (uint32_t h = 0; h < 2; ++h) {
+                uint32_t x = h ? m11 : m10;
+                if (!x) continue;
+                const uint32_t fa = (uint32_t)lds_nodes[2 * (fc + A0 + h) + 1];  // first MASK8 child of A
+                for (; x; x &= x - 1) {
+                    const uint32_t l = (uint32_t)(lds_nodes[2 * (fa + (uint32_t)__builtin_ctz(x)) + 1] >> 32);
+                    for (uint32_t lm = rd(o++); lm; lm &= lm - 1) emit(pos++, l + (uint32_t)__builtin_ctz(lm));
+                }
+            }
+            cnt += ltot;
+            continue;
+        }
         if (kind == KIND_PACK) {
             const uint32_t t = j % kPackSpan, below = (1u << t) - 1u;
             const uint4 q = gld_at_nt<uint4, NT>(base + (uint64_t)(j / kPackSpan) * kPackBlock + 16u * c);
@@ -828,7 +928,7 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
             j1 = q.z + (uint32_t)__builtin_popcount(q.w & below);
         }
         const uint32_t fc = (uint32_t)w1;
-        if ((w0 >> 51) & 1u) {  // FLAG_MASK_CHILDREN: the set children's mask reads, together
+        if (!P2 && ((w0 >> 51) & 1u)) {  // FLAG_MASK_CHILDREN: the set children's mask reads, together
             uint32_t m0 = 0, m1 = 0, l0 = 0, l1 = 0;
             if (b0) {
                 const uint32_t w = fc + 2 * c;
@@ -979,6 +1079,24 @@ __global__ __launch_bounds__(256) void k_get(const DevNode *__restrict__ nodes, 
             const DevNode *nd = &ndv;
             const uint32_t c = col_path[col * path_len + k];
             const uint64_t base = nd->base;
+            if (nd->kind == KIND_PACK2) {  // child c, its child c2, leaf c3: one record walk
+                Pack2Block pb;
+                pb.load(base, j);
+                const uint32_t s = pb.start(j % kPack2Span);
+                const uint32_t m2 = pb.byte(s);
+                if ((m2 >> c) & 1u) {
+                    const uint32_t c2 = col_path[col * path_len + k + 1], c3 = col_path[col * path_len + k + 2];
+                    const uint32_t i = (uint32_t)__builtin_popcount(m2 & ((1u << c) - 1u));
+                    const uint32_t m1 = pb.byte(s + 1 + i);
+                    if ((m1 >> c2) & 1u) {
+                        uint32_t o = s + 1 + (uint32_t)__builtin_popcount(m2);  // leaf masks of earlier children
+                        for (uint32_t q = 0; q < i; ++q) o += (uint32_t)__builtin_popcount(pb.byte(s + 1 + q));
+                        o += (uint32_t)__builtin_popcount(m1 & ((1u << c2) - 1u));
+                        bit = (uint8_t)((pb.byte(o) >> c3) & 1u);
+                    }
+                }
+                break;
+            }
             if (nd->kind == KIND_PACK) {  // child c is a MASK8 node: its bit, then its mask
                 PackBlock pb;
                 pb.load(base, j);
@@ -1043,16 +1161,25 @@ Trav pick_traverse(const Ctx &c) {
     const uint32_t depth = c.tree.stack_depth, max_arity = c.tree.max_arity;
     Trav t;
     const int kv = c.kernel_variant;
-    if (MODE == MODE_SLOTS && c.tree.fast_shape && c.tree.lds_complete && (kv == 0 || kv == 17 || kv == 18)) {
+    const bool p2 = c.tree.has_pack2;
+    if (MODE == MODE_SLOTS && c.tree.fast_shape && c.tree.lds_complete && (kv == 0 || kv == 17 || kv == 18) &&
+        (!p2 || (c.tree.push_frames <= 1 && !c.tree.has_mask_children))) {
         // k_traverse_fast2; 17/18 force plain / non-temporal block reads, the
         // default uses non-temporal reads on images larger than 1 GiB (+2.6 %)
         const bool nt = kv == 18 || (kv == 0 && c.tree.image_bytes > (1ull << 30));
         const bool smallk = auto_slots(c) == kStageLabels;
         t.G = 4;
         t.fast = true;
-        t.name = "k_traverse_fast2";
-        if (smallk) t.lane_fn = nt ? (TravFn)k_traverse_fast2<true, true> : (TravFn)k_traverse_fast2<false, true>;
-        else t.lane_fn = nt ? (TravFn)k_traverse_fast2<true, false> : (TravFn)k_traverse_fast2<false, false>;
+        t.name = p2 ? "k_traverse_fast2/pack2" : "k_traverse_fast2";
+#define FAST2(P)                                                                                          \
+    if (smallk) t.lane_fn = nt ? (TravFn)k_traverse_fast2<true, true, P> : (TravFn)k_traverse_fast2<false, true, P>; \
+    else t.lane_fn = nt ? (TravFn)k_traverse_fast2<true, false, P> : (TravFn)k_traverse_fast2<false, false, P>;
+        if (p2) {
+            FAST2(true)
+        } else {
+            FAST2(false)
+        }
+#undef FAST2
         t.fn = reinterpret_cast<const void *>(t.lane_fn);
         return t;
     }

@@ -293,6 +293,117 @@ PackFn pack_fn(uint32_t a) {
     return a >= 1 && a <= 8 ? t[a] : nullptr;
 }
 
+// KIND_PACK2 image (mbrwt_internal.hpp) of node u from temporary KIND_PLANE
+// images of u (its children A's bits + ranks over u's positions) and of
+// every A (A's MASK8 children B's bits + ranks over A's positions); the leaf
+// mask of B at B's position jB is the same draw (B's key, jB) as B's own
+// MASK8 image would hold.  One thread per block of 8 positions.  Pass 0 sums
+// the bytes of the spill lists; pass 1 writes (lists placed atomically).
+struct Pack2Args {
+    const uint8_t *uplane;
+    uint32_t ustride;
+    uint32_t a;                  // u's arity
+    const uint8_t *aplane[8];    // A's temporary planes
+    uint32_t astride[8];
+    uint32_t aarity[8];
+    uint64_t KB[64];             // key of B = child b of A: [8 * A + b]
+    uint8_t tB[64];              // table slot of B
+    const uint64_t *T[4];        // distinct tables of the B nodes (<= 4)
+    uint32_t nT[4];
+};
+
+__device__ __forceinline__ uint32_t plane_bit_rank(const uint8_t *plane, uint32_t stride, uint32_t c, uint64_t j,
+                                                   uint32_t &rank) {
+    const uint2 e = *reinterpret_cast<const uint2 *>(plane + (j >> 5) * stride + 8 * c);
+    const uint32_t t = (uint32_t)(j & 31);
+    rank = e.x + (uint32_t)__builtin_popcount(e.y & ((1u << t) - 1u));
+    return (e.y >> t) & 1u;
+}
+
+__global__ __launch_bounds__(256) void k_gen_pack2(uint8_t *img, uint64_t L, Pack2Args args, uint8_t *spill,
+                                                   unsigned long long *spill_ctr, unsigned long long *ones, int pass) {
+    __shared__ uint64_t T[4][255];
+    for (int k = 0; k < 4; ++k)
+        for (uint32_t i = threadIdx.x; i < args.nT[k]; i += blockDim.x) T[k][i] = args.T[k][i];
+    __syncthreads();
+    const uint64_t nb = (L + kPack2Span - 1) / kPack2Span;
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t local = 0;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gs) {
+        // record bytes of the block
+        uint32_t size = 0;
+        for (uint32_t t = 0; t < kPack2Span; ++t) {
+            const uint64_t j = b * kPack2Span + t;
+            if (j >= L) break;
+            size += 1;
+            for (uint32_t A = 0; A < args.a; ++A) {
+                uint32_t jA;
+                if (!plane_bit_rank(args.uplane, args.ustride, A, j, jA)) continue;
+                size += 1;
+                for (uint32_t B = 0; B < args.aarity[A]; ++B) {
+                    uint32_t jB;
+                    size += plane_bit_rank(args.aplane[A], args.astride[A], B, jA, jB);
+                }
+            }
+        }
+        const bool spills = size > kPack2Inline;
+        const uint32_t list_bytes = (2 * kPack2Span + size + 15) & ~15u;
+        if (pass == 0) {
+            if (spills) atomicAdd(spill_ctr, (unsigned long long)list_bytes);
+            continue;
+        }
+        uint8_t *blk = img + b * kPack2Block;
+        uint8_t *dst;
+        uint32_t hdr;  // start[t] = hdr + offset in the record bytes
+        if (spills) {
+            uint8_t *list = spill + atomicAdd(spill_ctr, (unsigned long long)list_bytes);
+            const uint64_t addr = (uint64_t)(uintptr_t)list;
+            for (uint32_t k = 0; k < 8; ++k) {
+                blk[k] = 0;
+                blk[8 + k] = (uint8_t)(addr >> (8 * k));
+            }
+            dst = list + 2 * kPack2Span;
+            hdr = 2 * kPack2Span;
+        } else {
+            dst = blk + 8;
+            hdr = 8;
+        }
+        uint32_t o = 0;
+        for (uint32_t t = 0; t < kPack2Span; ++t) {
+            const uint64_t j = b * kPack2Span + t;
+            if (spills) *reinterpret_cast<uint16_t *>(dst - 2 * kPack2Span + 2 * t) = (uint16_t)(hdr + o);
+            else blk[t] = (uint8_t)(hdr + o);
+            if (j >= L) continue;
+            uint32_t m2 = 0, jA[8], m1[8];
+            for (uint32_t A = 0; A < args.a; ++A) m2 |= plane_bit_rank(args.uplane, args.ustride, A, j, jA[A]) << A;
+            dst[o++] = (uint8_t)m2;
+            for (uint32_t A = 0; A < args.a; ++A) {
+                m1[A] = 0;
+                if (!((m2 >> A) & 1u)) continue;
+                uint32_t r;
+                for (uint32_t B = 0; B < args.aarity[A]; ++B)
+                    m1[A] |= plane_bit_rank(args.aplane[A], args.astride[A], B, jA[A], r) << B;
+                dst[o++] = (uint8_t)m1[A];
+            }
+            for (uint32_t A = 0; A < args.a; ++A) {
+                for (uint32_t x = m1[A]; x; x &= x - 1) {
+                    const uint32_t B = (uint32_t)__builtin_ctz(x);
+                    uint32_t jB;
+                    (void)plane_bit_rank(args.aplane[A], args.astride[A], B, jA[A], jB);
+                    const uint32_t ti = args.tB[8 * A + B];
+                    const uint32_t lm = draw_mask(T[ti], args.nT[ti], draw(args.KB[8 * A + B], jB));
+                    local += (uint64_t)__builtin_popcount(lm);
+                    dst[o++] = (uint8_t)lm;
+                }
+            }
+        }
+    }
+    if (pass == 1) {
+        for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off);
+        if ((threadIdx.x & 63) == 0 && local) atomicAdd(ones, (unsigned long long)local);
+    }
+}
+
 // ---- per-child rank scan over the blocks of a KIND_PLANE image ----------
 constexpr int kScanTile = 256;  // blocks per tile (one thread per block)
 
@@ -674,6 +785,132 @@ int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStr
         const uint64_t L = dn.length;  // positions = popcount of u's own column
         const uint64_t K = node_key(desc.seed, u);
         const uint32_t a = dn.arity, nT = (1u << a) - 1;
+        // KIND_PACK2 when every child A is a PLANE node of <= 8 MASK8 children
+        // with <= 8 leaves and a block of 8 positions is expected to hold <= 40
+        // record bytes (+ 8 header bytes; spills: ~0.1 % of the blocks)
+        bool pack2 = pack2_enabled() && dn.kind == KIND_PLANE && a <= 8 && q[u] > 0.0;
+        double rec = 1.0;
+        std::vector<uint64_t *> utab;
+        for (uint32_t c = 0; pack2 && c < a; ++c) {
+            const uint32_t cu = sh.children[c];
+            const DevNode &ch = tree.nodes[cu + 1];
+            pack2 = ch.kind == KIND_PLANE && ch.arity <= 8;
+            rec += q[cu] / q[u];
+            for (uint32_t g = 0; pack2 && g < ch.arity; ++g) {
+                const uint32_t gu = shape[cu].children[g];
+                const DevNode &gn = tree.nodes[gu + 1];
+                pack2 = gn.kind == KIND_MASK8 && gn.arity <= 8;
+                rec += q[gu] / q[u];
+                if (std::find(utab.begin(), utab.end(), node_T[gu]) == utab.end()) utab.push_back(node_T[gu]);
+            }
+        }
+        if (pack2 && (kPack2Span * rec > 40.0 || utab.size() > 4)) pack2 = false;
+        if (pack2) {
+            std::vector<void *> tmps;
+            auto free_tmps = [&]() {
+                for (void *t : tmps) (void)hipFree(t);
+            };
+            auto tmp_plane = [&](uint64_t len, uint32_t stride) -> uint8_t * {
+                void *t = nullptr;
+                const uint64_t bytes = ((len + 31) / 32) * stride + kImagePad;
+                if (hipMalloc(&t, bytes) != hipSuccess) return nullptr;
+                (void)hipMemsetAsync(t, 0, bytes, s);
+                tmps.push_back(t);
+                return reinterpret_cast<uint8_t *>(t);
+            };
+            Pack2Args args{};
+            args.a = a;
+            args.ustride = dn.stride;
+            uint8_t *up = tmp_plane(L, dn.stride);
+            std::vector<uint64_t> tot;
+            if (!up) {
+                (void)hipFree(d_ctr);
+                return fail(MBRWT_ERR_NOMEM, "device allocation failed");
+            }
+            plane_fn(a)(up, L, K, node_T[u], nT, dn.stride, s);
+            if ((rc = plane_scan(up, L, a, dn.stride, tot, s))) {
+                free_tmps();
+                (void)hipFree(d_ctr);
+                return fail(rc, "plane scan");
+            }
+            args.uplane = up;
+            for (uint32_t k = 0; k < utab.size(); ++k) {
+                args.T[k] = utab[k];
+                args.nT[k] = 255;
+            }
+            for (uint32_t c = 0; c < a; ++c) {
+                const uint32_t cu = sh.children[c];
+                DevNode &ch = tree.nodes[cu + 1];
+                const uint32_t ca = ch.arity;
+                ch.length = tot[c];
+                uint8_t *ap = tmp_plane(tot[c], ch.stride);
+                std::vector<uint64_t> gtot;
+                if (!ap) {
+                    free_tmps();
+                    (void)hipFree(d_ctr);
+                    return fail(MBRWT_ERR_NOMEM, "device allocation failed");
+                }
+                plane_fn(ca)(ap, tot[c], node_key(desc.seed, cu), node_T[cu], (1u << ca) - 1, ch.stride, s);
+                if ((rc = plane_scan(ap, tot[c], ca, ch.stride, gtot, s))) {
+                    free_tmps();
+                    (void)hipFree(d_ctr);
+                    return fail(rc, "plane scan");
+                }
+                args.aplane[c] = ap;
+                args.astride[c] = ch.stride;
+                args.aarity[c] = ca;
+                in_pack[cu] = true;
+                ch.kind = KIND_PACK;  // record only (no image)
+                ch.stride = kPackBlock;
+                for (uint32_t g = 0; g < ca; ++g) {
+                    const uint32_t gu = shape[cu].children[g];
+                    DevNode &gn = tree.nodes[gu + 1];
+                    gn.length = gtot[g];
+                    gn.base = 0;
+                    in_pack[gu] = true;
+                    args.KB[8 * c + g] = node_key(desc.seed, gu);
+                    const uint32_t ti = (uint32_t)(std::find(utab.begin(), utab.end(), node_T[gu]) - utab.begin());
+                    args.tB[8 * c + g] = (uint8_t)ti;
+                    args.nT[ti] = (1u << gn.arity) - 1;
+                }
+            }
+            const uint64_t nb2 = (L + kPack2Span - 1) / kPack2Span;
+            (void)hipMemsetAsync(d_ctr, 0, sizeof(unsigned long long), s);
+            hipLaunchKernelGGL(k_gen_pack2, dim3(launch_grid(nb2)), dim3(256), 0, s, nullptr, L, args, nullptr, d_ctr,
+                               d_ones, 0);
+            unsigned long long spill_bytes = 0;
+            MBRWT_HIP(hipMemcpyAsync(&spill_bytes, d_ctr, sizeof(spill_bytes), hipMemcpyDeviceToHost, s));
+            MBRWT_HIP(hipStreamSynchronize(s));
+            uint8_t *spill = nullptr;
+            if (spill_bytes) {
+                DevNode dummy;
+                spill = alloc_image(dummy, spill_bytes);
+                if (!spill) {
+                    free_tmps();
+                    (void)hipFree(d_ctr);
+                    return fail(MBRWT_ERR_NOMEM, "device allocation failed");
+                }
+            }
+            dn.kind = KIND_PACK2;
+            dn.stride = kPack2Block;
+            uint8_t *img = alloc_image(dn, nb2 * kPack2Block);
+            if (!img) {
+                free_tmps();
+                (void)hipFree(d_ctr);
+                return fail(MBRWT_ERR_NOMEM, "device allocation failed");
+            }
+            (void)hipMemsetAsync(d_ctr, 0, sizeof(unsigned long long), s);
+            hipLaunchKernelGGL(k_gen_pack2, dim3(launch_grid(nb2)), dim3(256), 0, s, img, L, args, spill, d_ctr, d_ones,
+                               1);
+            if (hipGetLastError() != hipSuccess) {
+                free_tmps();
+                (void)hipFree(d_ctr);
+                return fail(MBRWT_ERR_DEVICE, "pack2 kernel");
+            }
+            MBRWT_HIP(hipStreamSynchronize(s));
+            free_tmps();
+            continue;
+        }
         // KIND_PACK when every child is a MASK8 node with <= 8 leaves and a
         // block of 16 positions is expected to hold <= 40 masks (spills: ~1 % of the blocks)
         bool pack = pack_enabled() && dn.kind == KIND_PLANE && a <= 8;

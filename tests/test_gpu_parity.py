@@ -357,3 +357,63 @@ def test_pack_layout_synthetic(oracle_mod, fold):
     assert packed.device_bytes() != plain.device_bytes()
     rows = np.random.default_rng(9).integers(0, n, 100_000).astype(np.uint64)
     _agree(t, [packed, plain], rows, np.random.default_rng(2).integers(0, m, 16), m)
+
+
+# ---- KIND_PACK2 layout: a node's whole 3-level subtree inline per position ----
+
+def test_pack2_layout_with_spills(oracle_mod):
+    """Arity-4 tree (256 -> 64 -> 16 -> 4 -> root, folded): the 4 nodes under
+    the root become KIND_PACK2; a run of dense rows makes a few of their
+    blocks spill.  PACK2, PACK-only and plain images answer like the oracle
+    (rows under every kernel, columns, get, V/L accounting)."""
+    O = oracle_mod
+    rng = np.random.default_rng(12)
+    n, m = 4000, 256
+    dense = rng.random((n, m)) < 0.004
+    dense[2000:2024] = True
+    t = O.OracleTree.from_dense(dense, "basic", 4)
+    p2 = _dev(t)
+    p1 = _with_env("MBRWT_PACK2", "0", lambda: _dev(t))
+    plain = _with_env("MBRWT_PACK", "0", lambda: _dev(t))
+    assert p2.traverse_kernel() == "k_traverse_fast2/pack2"
+    assert p1.traverse_kernel() == plain.traverse_kernel() == "k_traverse_fast2"
+    # (the dense run makes PACK decline here: > 1 block in 20 would spill)
+    assert p2.device_bytes() not in (p1.device_bytes(), plain.device_bytes())
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 20000)]).astype(np.uint64)
+    _agree(t, [p2, p1, plain], rows, range(m), m)
+
+
+def test_pack2_records_longer_than_a_block(oracle_mod):
+    """Arity 8, 2048 columns (2048 -> 256 -> 32 -> 4 -> root): a fully set row
+    gives a 73-byte record (1 + 8 + 64 masks), longer than a block -- served
+    from the spill list."""
+    O = oracle_mod
+    rng = np.random.default_rng(13)
+    n, m = 3000, 2048
+    dense = rng.random((n, m)) < 0.0005
+    dense[[5, 1500, 1501]] = True
+    t = O.OracleTree.from_dense(dense, "basic", 8)
+    p2 = _dev(t)
+    assert p2.traverse_kernel() == "k_traverse_fast2/pack2"
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 5000)]).astype(np.uint64)
+    _agree(t, [p2], rows, [0, 7, 8, 511, 512, 2047], m)
+
+
+@pytest.mark.parametrize("fold", ["1", "0"])
+def test_pack2_layout_synthetic(oracle_mod, fold):
+    """Synthetic Kingsford-shaped trees: the generator's PACK2 images (default)
+    agree with the oracle, as do PACK-only images."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    n, m = 400_000, 2652
+    t = O.OracleTree.topdown(n, m, 0.003, 8, 6)
+
+    def mk():
+        return BRWTDevice.synthetic(n, m, 0.003, 8, 6)
+    p2 = _with_env("MBRWT_FOLD_ROOT", fold, mk)
+    p1 = _with_env("MBRWT_FOLD_ROOT", fold, lambda: _with_env("MBRWT_PACK2", "0", mk))
+    assert p2.device_bytes() != p1.device_bytes()
+    if fold == "1":
+        assert p2.traverse_kernel() == "k_traverse_fast2/pack2"
+    rows = np.random.default_rng(10).integers(0, n, 100_000).astype(np.uint64)
+    _agree(t, [p2, p1], rows, np.random.default_rng(4).integers(0, m, 16), m)
