@@ -123,7 +123,7 @@ def main():
     def step():
         n_lab = mat.get_rows_device(rows_t, off_t, cols_t, sptr)
         if world > 1 and not a.no_gather:
-            allgatherv_csr(off_t, cols_t[:n_lab])
+            allgatherv_csr(off_t, cols_t, n_labels=n_lab, num_columns=a.cols)
         return n_lab
 
     for _ in range(a.warmup):
@@ -148,6 +148,22 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # N > 1: the reassembled global CSR must hold this rank's slice verbatim
+    # (every rank checks its own slice; the verdicts are all-reduced)
+    reassembly = None
+    if world > 1 and not a.no_gather:
+        g_off, g_cols = allgatherv_csr(off_t, cols_t, n_labels=n_lab, num_columns=a.cols)
+        lo, hi = rank * a.batch, (rank + 1) * a.batch
+        b0 = int(g_off[lo].item())
+        ok = bool(torch.equal(g_off[lo:hi + 1] - b0, off_t) and
+                  torch.equal(g_cols[b0:b0 + n_lab], cols_t[:n_lab]) and
+                  g_off.numel() == world * a.batch + 1)
+        flag = torch.tensor([0 if ok else 1], dtype=torch.int64, device=dev_t)
+        dist.all_reduce(flag, op=dist.ReduceOp.SUM)
+        reassembly = (f"all-gatherv CSR ({g_off.numel() - 1:,} rows, {g_cols.numel():,} labels) holds every "
+                      f"rank's slice verbatim" if int(flag.item()) == 0 else f"MISMATCH on {int(flag.item())} ranks")
+        del g_off, g_cols
 
     # measured streaming-read rate of this GPU (report beside the spec peak)
     big = torch.ones(1 << 30, dtype=torch.float32, device=dev_t)  # 4 GiB
@@ -237,6 +253,7 @@ def main():
             "labels_per_row": labels / a.batch,
         },
         "cpu_baseline": cpu,
+        "reassembly": reassembly,
         "parity": None if parity is None else f"{'bit-exact' if parity else 'MISMATCH'} on {chk:,} rows"
                                                 f"{' (the whole timed batch)' if chk == a.batch else ''}"
                                                 f" vs the oracle, element-wise CSR",

@@ -4,9 +4,20 @@ The BRWT image is replicated on every GPU (each rank builds or loads its own
 copy; nothing of the structure crosses xGMI).  A batch of query rows is cut
 into contiguous per-rank slices; every rank runs the HIP traversal on its
 slice and the per-row label sets are reassembled into one global CSR by an
-all-gatherv over RCCL (backend "nccl" on ROCm).  RCCL has no all-gatherv, so
-the label arrays are padded to the largest rank's count and gathered with one
-all_gather_into_tensor; the padding is <1% for equal-sized random slices.
+all-gatherv over RCCL (backend "nccl" on ROCm).
+
+RCCL has no all-gatherv, so the exchange is:
+  1. one tiny all-gather of every rank's (rows, labels) sizes (the only host
+     synchronisation);
+  2. ONE all_gather_into_tensor of a packed byte buffer per rank, padded to
+     the largest rank: [per-row label counts | labels].  The wire types are
+     u16 when the matrix has < 2^16 columns (a count is <= num_columns, a
+     label < num_columns) and u32 otherwise -- the Kingsford shape (2,652
+     columns) ships 2 bytes per label and per row instead of 4 + 8, i.e.
+     ~2.2x fewer bytes over xGMI than u32 labels + u64 offsets;
+  3. unpacking with contiguous slice copies: one scan of the gathered counts
+     gives the global offsets, each rank's label slice is widened into its
+     place of the global label array.
 The same code runs on gloo (CPU tensors) for the multi-process CPU tests.
 """
 from __future__ import annotations
@@ -31,34 +42,68 @@ def _all_gather(out: torch.Tensor, inp: torch.Tensor, group=None):
         dist.all_gather(parts, inp, group=group)
 
 
-def allgatherv_csr(offsets: torch.Tensor, cols: torch.Tensor, group=None):
+def _round16(x: int) -> int:
+    return (x + 15) // 16 * 16
+
+
+def wire_is_narrow(num_columns) -> bool:
+    """u16 wire types are exact when every count (<= num_columns) and every
+    label (< num_columns) fits 16 bits."""
+    return num_columns is not None and num_columns < (1 << 16)
+
+
+def allgatherv_csr(offsets: torch.Tensor, cols: torch.Tensor, n_labels=None, num_columns=None, group=None):
     """Reassemble per-rank CSR slices (offsets: int64 [n_r + 1] starting at 0;
     cols: int32 [>= offsets[-1]]) into the global CSR of the concatenated
-    batch, on every rank.  Returns (offsets [N + 1] int64, cols [L] int32)."""
+    batch, on every rank.  `n_labels` (= offsets[-1], if the caller already
+    has it on the host) saves a device read; `num_columns` (the same on every
+    rank) enables the u16 wire format.  Returns (offsets [N + 1] int64,
+    cols [L] int32)."""
     world = dist.get_world_size(group)
     dev = offsets.device
     n_r = offsets.numel() - 1
-    l_r = int(offsets[-1].item())
+    l_r = int(offsets[-1].item()) if n_labels is None else int(n_labels)
     sizes = torch.tensor([n_r, l_r], dtype=torch.int64, device=dev)
     all_sizes = torch.empty(world * 2, dtype=torch.int64, device=dev)
     _all_gather(all_sizes, sizes, group)
-    all_sizes = all_sizes.view(world, 2).cpu()
-    max_n = int(all_sizes[:, 0].max())
-    max_l = int(all_sizes[:, 1].max())
-    # rows: gather per-row counts (offsets deltas), padded
-    cnt = torch.zeros(max_n, dtype=torch.int64, device=dev)
-    cnt[:n_r] = offsets[1:] - offsets[:-1]
-    all_cnt = torch.empty(world * max_n, dtype=torch.int64, device=dev)
-    _all_gather(all_cnt, cnt, group)
-    # labels, padded to the largest slice
-    lab = torch.zeros(max(1, max_l), dtype=torch.int32, device=dev)
-    lab[:l_r] = cols[:l_r]
-    all_lab = torch.empty(world * max(1, max_l), dtype=torch.int32, device=dev)
-    _all_gather(all_lab, lab, group)
-    # compact: drop the padding of every slice
-    keep_rows = torch.cat([torch.arange(int(all_sizes[r, 0]), device=dev) + r * max_n for r in range(world)])
-    keep_lab = torch.cat([torch.arange(int(all_sizes[r, 1]), device=dev) + r * max(1, max_l) for r in range(world)])
-    g_cnt = all_cnt[keep_rows]
-    g_off = torch.zeros(g_cnt.numel() + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(g_cnt, 0, out=g_off[1:])
-    return g_off, all_lab[keep_lab]
+    table = all_sizes.view(world, 2).cpu().tolist()
+    ns, ls = [t[0] for t in table], [t[1] for t in table]
+    max_n, max_l = max(ns), max(ls)
+
+    narrow = wire_is_narrow(num_columns)
+    wdt = torch.int16 if narrow else torch.int32
+    wb = 2 if narrow else 4
+    cnt_bytes = _round16(max(1, max_n) * wb)
+    per = cnt_bytes + _round16(max(1, max_l) * wb)
+
+    # pack: counts (offsets deltas) then labels, in the wire type (int64 ->
+    # int16 keeps the low 16 bits: exact for values < 2^16, read back & 0xFFFF)
+    send = torch.empty(per, dtype=torch.uint8, device=dev)
+    if n_r:
+        send[:cnt_bytes].view(wdt)[:n_r].copy_(offsets[1:] - offsets[:-1])
+    if l_r:
+        send[cnt_bytes:].view(wdt)[:l_r].copy_(cols[:l_r])
+    recv = torch.empty(world * per, dtype=torch.uint8, device=dev)
+    _all_gather(recv, send, group)
+    R = recv.view(world, per)
+
+    # unpack: global offsets by one scan over the ranks' counts in rank order
+    N, L = sum(ns), sum(ls)
+    g_cnt = torch.empty(N, dtype=torch.int64, device=dev)
+    g_cols = torch.empty(L, dtype=torch.int32, device=dev)
+    rb = lb = 0
+    for r in range(world):
+        if ns[r]:
+            g_cnt[rb:rb + ns[r]].copy_(R[r, :cnt_bytes].view(wdt)[:ns[r]])
+        if ls[r]:
+            g_cols[lb:lb + ls[r]].copy_(R[r, cnt_bytes:].view(wdt)[:ls[r]])
+        rb += ns[r]
+        lb += ls[r]
+    if narrow:  # int16 sign-extended on the way back: restore the u16 values
+        g_cnt.bitwise_and_(0xFFFF)
+        if num_columns > (1 << 15):
+            g_cols.bitwise_and_(0xFFFF)
+    g_off = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+    if N:
+        torch.cumsum(g_cnt, 0, out=g_off[1:])
+    return g_off, g_cols

@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_batch, q):
+def _worker(rank, world, port, n_batch, q, num_columns=None, m=300):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -32,12 +32,13 @@ def _worker(rank, world, port, n_batch, q):
     try:
         import oracle as O
         from genome_graph_annotation_amd.dist import allgatherv_csr, shard_bounds
-        t = O.OracleTree.topdown(50_000, 300, 0.01, 8, 3)
+        t = O.OracleTree.topdown(50_000, m, 0.01 if m < 1000 else 0.002, 8, 3)
         rows = np.random.default_rng(9).integers(0, 50_000, n_batch, dtype=np.uint64)
         lo, hi = shard_bounds(n_batch, world, rank)
         off, cols = t.get_rows(rows[lo:hi])
         g_off, g_cols = allgatherv_csr(torch.from_numpy(off.view(np.int64)),
-                                       torch.from_numpy(cols.view(np.int32)))
+                                       torch.from_numpy(cols.view(np.int32)),
+                                       n_labels=None if rank else int(off[-1]), num_columns=num_columns)
         ref_off, ref_cols = t.get_rows(rows)
         ok = np.array_equal(g_off.numpy().view(np.uint64), ref_off) and \
             np.array_equal(g_cols.numpy().view(np.uint32), ref_cols)
@@ -46,12 +47,19 @@ def _worker(rank, world, port, n_batch, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_batch", [(2, 10_001), (2, 1), (3, 7)])
-def test_allgatherv_reassembles_global_csr(world, n_batch):
+@pytest.mark.parametrize("world,n_batch,num_columns,m", [
+    (2, 10_001, None, 300),      # u32 wire
+    (2, 10_001, 300, 300),       # u16 wire
+    (3, 4_001, 40_000, 40_000),  # u16 wire, labels >= 2^15 (sign bit on the wire)
+    (2, 1, 300, 300),
+    (3, 7, None, 300),
+    (3, 2, 300, 300),            # a rank with an empty slice
+])
+def test_allgatherv_reassembles_global_csr(world, n_batch, num_columns, m):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_batch, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_batch, q, num_columns, m)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]
