@@ -37,12 +37,13 @@ __device__ __forceinline__ uint32_t column_word(const DevNode &nd, uint32_t c, u
     uint32_t bits = 0;
     if (nd.kind == KIND_PACK2) {  // leaf = (B << 8) | leaf slot of the MASK8 grandchild B below child c
         const uint32_t B = leaf >> 8, lf = leaf & 0xFFu;
-        for (uint32_t h = 0; h < 32 / kPack2Span; ++h) {
-            const uint64_t j0 = 32 * w + kPack2Span * h;
+        const uint32_t S = nd.stride;  // positions per block
+        for (uint32_t h = 0; h < 32; h += S) {
+            const uint64_t j0 = 32 * w + h;
             if (j0 >= len) break;
             Pack2Block pb;
-            pb.load(nd.base, (uint32_t)j0);
-            for (uint32_t t = 0; t < kPack2Span && j0 + t < len; ++t) {
+            pb.load(nd.base, (uint32_t)j0, S);
+            for (uint32_t t = 0; t < S && j0 + t < len; ++t) {
                 const uint32_t s = pb.start(t);
                 const uint32_t m2 = pb.byte(s);
                 if (!((m2 >> c) & 1u)) continue;
@@ -52,7 +53,7 @@ __device__ __forceinline__ uint32_t column_word(const DevNode &nd, uint32_t c, u
                 uint32_t o = s + 1 + (uint32_t)__builtin_popcount(m2);
                 for (uint32_t q = 0; q < i; ++q) o += (uint32_t)__builtin_popcount(pb.byte(s + 1 + q));
                 o += (uint32_t)__builtin_popcount(m1 & ((1u << B) - 1u));
-                if ((pb.byte(o) >> lf) & 1u) bits |= 1u << (kPack2Span * h + t);
+                if ((pb.byte(o) >> lf) & 1u) bits |= 1u << (h + t);
             }
         }
     } else if (nd.kind == KIND_PACK) {

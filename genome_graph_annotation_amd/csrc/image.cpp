@@ -191,64 +191,78 @@ inline uint32_t desc_bit(const mbrwt_tree_desc &desc, uint32_t node, uint64_t j)
     return (uint32_t)((desc.vec_words[node][j >> 6] >> (j & 63)) & 1);
 }
 
-// KIND_PACK2 image of desc node u (mbrwt_internal.hpp): returns false (and
-// builds nothing) when more than 1 block in 20 would spill.
+// KIND_PACK2 image of desc node u (mbrwt_internal.hpp) with the largest span
+// (8, 4, 2, 1 positions per block) at which at most 1 block in 20 spills;
+// returns false (and builds nothing) when no span qualifies.
 bool build_pack2_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, DevNode &dn, std::vector<void *> &images,
                        uint64_t &image_bytes, int &rc) {
     rc = MBRWT_OK;
     const uint32_t a = desc.num_children[u], fc = desc.first_child[u];
-    const uint64_t blocks = (L + kPack2Span - 1) / kPack2Span;
+    // the record of every position (flat, with offsets)
+    std::vector<uint8_t> recs;
+    std::vector<uint64_t> roff(L + 1, 0);
+    std::vector<uint64_t> rA(a, 0), rB(8 * a, 0);  // running ranks of the A and B columns
+    for (uint64_t j = 0; j < L; ++j) {
+        uint32_t m2 = 0;
+        for (uint32_t A = 0; A < a; ++A) m2 |= desc_bit(desc, fc + A, j) << A;
+        recs.push_back((uint8_t)m2);
+        uint32_t m1s[8] = {0};
+        for (uint32_t A = 0; A < a; ++A) {
+            if (!((m2 >> A) & 1)) continue;
+            const uint32_t na = fc + A, ga = desc.num_children[na], gfa = desc.first_child[na];
+            const uint64_t jA = rA[A]++;
+            for (uint32_t B = 0; B < ga; ++B) m1s[A] |= desc_bit(desc, gfa + B, jA) << B;
+            recs.push_back((uint8_t)m1s[A]);
+        }
+        for (uint32_t A = 0; A < a; ++A) {
+            const uint32_t gfa = desc.first_child[fc + A];
+            for (uint32_t x = m1s[A]; x; x &= x - 1) {
+                const uint32_t B = (uint32_t)__builtin_ctz(x), nb = gfa + B;
+                const uint64_t jB = rB[8 * A + B]++;
+                uint32_t lm = 0;
+                for (uint32_t k = 0; k < desc.num_children[nb]; ++k)
+                    lm |= desc_bit(desc, desc.first_child[nb] + k, jB) << k;
+                recs.push_back((uint8_t)lm);
+            }
+        }
+        roff[j + 1] = recs.size();
+    }
+    auto block_bytes = [&](uint64_t b, uint32_t S) {
+        return roff[std::min<uint64_t>(L, (b + 1) * S)] - roff[std::min<uint64_t>(L, b * S)];
+    };
+    uint32_t S = 0;
+    uint64_t blocks = 0;
+    for (uint32_t span = kPack2MaxSpan; span >= 1 && !S; span /= 2) {
+        const uint64_t nb = (L + span - 1) / span;
+        uint64_t spills = 0;
+        for (uint64_t b = 0; b < nb; ++b) spills += block_bytes(b, span) > pack2_inline(span);
+        if (spills * 20 <= nb) {
+            S = span;
+            blocks = nb;
+        }
+    }
+    if (!S) return false;
     std::vector<uint8_t> host(blocks * kPack2Block + kImagePad, 0);
     std::vector<uint8_t> spill;
     std::vector<std::pair<uint64_t, uint64_t>> spilled;  // (block, offset in spill)
-    std::vector<uint64_t> rA(a, 0), rB(8 * a, 0);         // running ranks of the A and B columns
-    std::vector<uint8_t> rec;
     for (uint64_t b = 0; b < blocks; ++b) {
-        rec.clear();
-        uint32_t start[kPack2Span];
-        for (uint32_t t = 0; t < kPack2Span; ++t) {
-            const uint64_t j = b * kPack2Span + t;
-            start[t] = (uint32_t)rec.size();
-            if (j >= L) continue;
-            uint32_t m2 = 0;
-            for (uint32_t A = 0; A < a; ++A) m2 |= desc_bit(desc, fc + A, j) << A;
-            rec.push_back((uint8_t)m2);
-            uint32_t m1s[8] = {0};
-            for (uint32_t A = 0; A < a; ++A) {
-                if (!((m2 >> A) & 1)) continue;
-                const uint32_t na = fc + A, ga = desc.num_children[na], gfa = desc.first_child[na];
-                const uint64_t jA = rA[A]++;
-                for (uint32_t B = 0; B < ga; ++B) m1s[A] |= desc_bit(desc, gfa + B, jA) << B;
-                rec.push_back((uint8_t)m1s[A]);
-            }
-            for (uint32_t A = 0; A < a; ++A) {
-                const uint32_t gfa = desc.first_child[fc + A];
-                for (uint32_t x = m1s[A]; x; x &= x - 1) {
-                    const uint32_t B = (uint32_t)__builtin_ctz(x), nb = gfa + B;
-                    const uint64_t jB = rB[8 * A + B]++;
-                    uint32_t lm = 0;
-                    for (uint32_t k = 0; k < desc.num_children[nb]; ++k)
-                        lm |= desc_bit(desc, desc.first_child[nb] + k, jB) << k;
-                    rec.push_back((uint8_t)lm);
-                }
-            }
-        }
+        const uint64_t j0 = b * S, r0 = roff[std::min<uint64_t>(L, j0)];
+        const uint64_t bytes = block_bytes(b, S);
         uint8_t *blk = &host[b * kPack2Block];
-        if (rec.size() <= kPack2Inline) {
-            for (uint32_t t = 0; t < kPack2Span; ++t) blk[t] = (uint8_t)(8 + start[t]);
-            std::memcpy(blk + 8, rec.data(), rec.size());
+        if (bytes <= pack2_inline(S)) {
+            for (uint32_t t = 0; t < S; ++t) blk[t] = (uint8_t)(S + roff[std::min<uint64_t>(L, j0 + t)] - r0);
+            std::memcpy(blk + S, recs.data() + r0, bytes);
         } else {  // start[0] = 0 marks the block; list = u16 starts, then the records
             spilled.emplace_back(b, spill.size());
-            for (uint32_t t = 0; t < kPack2Span; ++t) {
-                const uint16_t st = (uint16_t)(2 * kPack2Span + start[t]);
+            for (uint32_t t = 0; t < S; ++t) {
+                const uint16_t st = (uint16_t)(2 * S + roff[std::min<uint64_t>(L, j0 + t)] - r0);
                 spill.push_back((uint8_t)st);
                 spill.push_back((uint8_t)(st >> 8));
             }
-            spill.insert(spill.end(), rec.begin(), rec.end());
+            spill.insert(spill.end(), recs.begin() + r0, recs.begin() + r0 + bytes);
             if (spill.size() & 1) spill.push_back(0);  // keep the u16 starts aligned
         }
     }
-    if (spilled.size() * 20 > blocks) return false;
     if (!spill.empty()) {
         void *ds = nullptr;
         spill.resize(spill.size() + kImagePad, 0);
@@ -274,7 +288,7 @@ bool build_pack2_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, DevN
     image_bytes += host.size();
     dn.kind = KIND_PACK2;
     dn.arity = (uint16_t)a;
-    dn.stride = kPack2Block;
+    dn.stride = S;  // positions per block
     dn.length = L;
     dn.base = (uint64_t)(uintptr_t)d;
     return true;

@@ -64,20 +64,24 @@ __host__ __device__ inline uint32_t pack_area_byte(uint32_t o) { return 16 * (o 
 
 // KIND_PACK2 image (node u whose children A are all PACK-shaped: each A has
 // 1..8 MASK8 children B with consecutive leaf columns): one 64-byte block per
-// 8 positions of u.  Bytes 0..7 = start[t], the byte offset of position t's
-// record (start[0] = 8); records back to back.  Record of position j =
+// S positions of u, S = the node's span (1, 2, 4 or 8, kept in
+// DevNode::stride and as log2 in the CNode's log2(stride) bits).  Bytes
+// 0..S-1 = start[t], the byte offset of position t's record (start[0] = S);
+// records back to back.  Record of position j =
 //   m2                      u's children bits at j (never 0: u's bit is set),
 //   m1(A) per set A         A's children bits at A's position (rank1(A, j) - 1),
 //   leaf(A,B) per set A, per set B of m1(A), both in child order
 //                           B's leaf mask at B's position,
 // i.e. the index bits of the whole subtree below u at j, in the reference's
-// pre-order (BRWT.cpp:45-51).  A block whose records exceed 56 bytes holds
-// start[0] = 0 and, in bytes 8..15, the address of a spill list: u16 start[8]
-// (relative to the list) followed by the records.  The A and B nodes keep
-// their records (arity, first child, labels) but have no image.
-constexpr uint32_t kPack2Span = 8;
+// pre-order (BRWT.cpp:45-51).  A block whose records exceed 64 - S bytes
+// holds start[0] = 0 and, in bytes 8..15, the address of a spill list:
+// u16 start[S] (relative to the list) followed by the records.  The A and B
+// nodes keep their records (arity, first child, labels) but have no image.
+// Sparse subtrees take S = 8 (Kingsford shape: ~4.5 record bytes per
+// position), dense ones a smaller span (RefSeq shape: ~23 bytes, S = 2).
+constexpr uint32_t kPack2MaxSpan = 8;
 constexpr uint32_t kPack2Block = 64;
-constexpr uint32_t kPack2Inline = 56;  // record bytes that fit after the header
+__host__ __device__ inline uint32_t pack2_inline(uint32_t span) { return kPack2Block - span; }
 // FLAG_CONSEC_LABELS (MASK nodes): child c's label = label + c.
 // FLAG_MASK_CHILDREN (PLANE nodes): every child is a KIND_MASK8 node with
 // consecutive labels, so the fast kernel resolves the children in the
@@ -101,7 +105,7 @@ static_assert(sizeof(DevNode) == 32, "DevNode must be 32 bytes");
 //   w0 = base[0:48) | kind[48:51) | flag[51] | log2(stride)[52:56) | arity[56:64)
 // flag = FLAG_MASK_CHILDREN for KIND_PLANE, FLAG_CONSEC_LABELS for MASK kinds;
 // KIND_PACK2 is stored as kind KIND_PACK with flag 1 (kind bits 48..51 = 0xF).
-// For KIND_PACK / KIND_PACK2 log2(stride) is 6.
+// For KIND_PACK log2(stride) is 6, for KIND_PACK2 it is log2(span).
 struct alignas(16) CNode {
     uint64_t w0;
     uint32_t first_child;

@@ -53,8 +53,9 @@ struct Pack2Block {
     uint32_t w[16];
     bool spilled;
     uint64_t sa;  // spill list address
-    __device__ __forceinline__ void load(uint64_t base, uint32_t j) {
-        const uint64_t blk = base + (uint64_t)(j / kPack2Span) * kPack2Block;
+    // j: position of the node; span: positions per block (DevNode::stride)
+    __device__ __forceinline__ void load(uint64_t base, uint32_t j, uint32_t span) {
+        const uint64_t blk = base + (uint64_t)(j / span) * kPack2Block;
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
             const uint4 q = gld_at<uint4>(blk + 16 * h);
@@ -73,7 +74,7 @@ struct Pack2Block {
         for (int i = 1; i < 16; ++i) x = (o >> 2) == (uint32_t)i ? w[i] : x;
         return (x >> (8 * (o & 3))) & 0xFFu;
     }
-    // byte offset of the record of position t (t = j % kPack2Span)
+    // byte offset of the record of position t (t = j % span)
     __device__ __forceinline__ uint32_t start(uint32_t t) const {
         if (spilled) return gld_at<uint16_t>(sa + 2ull * t);
         return byte(t);

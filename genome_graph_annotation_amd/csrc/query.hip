@@ -144,8 +144,8 @@ __device__ __forceinline__ void enter(const TravParams &p, Frames<MAXD, MaskT> &
     if constexpr (MODE == MODE_WORK) sk.visits += a;  // operator[] on every child (BRWT.cpp:30)
     if (kind == KIND_PACK2) {  // the whole subtree below v at j, in pre-order
         Pack2Block pb;
-        pb.load(base, j);
-        const uint32_t s = pb.start(j % kPack2Span);
+        pb.load(base, j, nd.stride);
+        const uint32_t s = pb.start(j % nd.stride);
         const uint32_t m2 = pb.byte(s);
         uint32_t o1 = s + 1, o2 = s + 1 + (uint32_t)__builtin_popcount(m2);
         for (uint32_t A = 0; A < a; ++A) {
@@ -423,8 +423,8 @@ __device__ __forceinline__ void group_visit(const TravParams &p, GroupFrames<MAX
         // every lane walks the whole record; each emits the labels below its
         // own children at their rank among the node's labels (pre-order)
         Pack2Block pb;
-        pb.load(base, j);
-        const uint32_t s = pb.start(j % kPack2Span);
+        pb.load(base, j, nd.stride);
+        const uint32_t s = pb.start(j % nd.stride);
         const uint32_t m2 = pb.byte(s);
         uint32_t o1 = s + 1, o2 = s + 1 + (uint32_t)__builtin_popcount(m2), total = 0;
         const uint64_t *cn = reinterpret_cast<const uint64_t *>(p.cnodes);
@@ -831,8 +831,9 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
             // one coalesced 64-byte block read; staged in LDS, each lane takes
             // children 2c, 2c+1 of the node: their m1 bytes, then the leaf
             // masks of their set children (offsets by quad scans)
-            const uint32_t t = j % kPack2Span;
-            const uint4 q = gld_at_nt<uint4, NT>(base + (uint64_t)(j / kPack2Span) * kPack2Block + 16u * c);
+            const uint32_t lgs = (uint32_t)(w0 >> 52) & 15u;  // log2(span)
+            const uint32_t t = j & ((1u << lgs) - 1u);
+            const uint4 q = gld_at_nt<uint4, NT>(base + (uint64_t)(j >> lgs) * kPack2Block + 16u * c);
             ((AS_LDS u32x4_t *)pk)[c] = u32x4_t{q.x, q.y, q.z, q.w};
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -1081,8 +1082,8 @@ __global__ __launch_bounds__(256) void k_get(const DevNode *__restrict__ nodes, 
             const uint64_t base = nd->base;
             if (nd->kind == KIND_PACK2) {  // child c, its child c2, leaf c3: one record walk
                 Pack2Block pb;
-                pb.load(base, j);
-                const uint32_t s = pb.start(j % kPack2Span);
+                pb.load(base, j, nd->stride);
+                const uint32_t s = pb.start(j % nd->stride);
                 const uint32_t m2 = pb.byte(s);
                 if ((m2 >> c) & 1u) {
                     const uint32_t c2 = col_path[col * path_len + k + 1], c3 = col_path[col * path_len + k + 2];

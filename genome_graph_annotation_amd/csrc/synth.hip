@@ -297,8 +297,9 @@ PackFn pack_fn(uint32_t a) {
 // images of u (its children A's bits + ranks over u's positions) and of
 // every A (A's MASK8 children B's bits + ranks over A's positions); the leaf
 // mask of B at B's position jB is the same draw (B's key, jB) as B's own
-// MASK8 image would hold.  One thread per block of 8 positions.  Pass 0 sums
-// the bytes of the spill lists; pass 1 writes (lists placed atomically).
+// MASK8 image would hold.  One thread per block of S positions (the node's
+// span).  Pass 0 sums the bytes of the spill lists; pass 1 writes (lists
+// placed atomically).
 struct Pack2Args {
     const uint8_t *uplane;
     uint32_t ustride;
@@ -320,20 +321,21 @@ __device__ __forceinline__ uint32_t plane_bit_rank(const uint8_t *plane, uint32_
     return (e.y >> t) & 1u;
 }
 
-__global__ __launch_bounds__(256) void k_gen_pack2(uint8_t *img, uint64_t L, Pack2Args args, uint8_t *spill,
-                                                   unsigned long long *spill_ctr, unsigned long long *ones, int pass) {
+__global__ __launch_bounds__(256) void k_gen_pack2(uint8_t *img, uint64_t L, uint32_t S, Pack2Args args,
+                                                   uint8_t *spill, unsigned long long *spill_ctr,
+                                                   unsigned long long *ones, int pass) {
     __shared__ uint64_t T[4][255];
     for (int k = 0; k < 4; ++k)
         for (uint32_t i = threadIdx.x; i < args.nT[k]; i += blockDim.x) T[k][i] = args.T[k][i];
     __syncthreads();
-    const uint64_t nb = (L + kPack2Span - 1) / kPack2Span;
+    const uint64_t nb = (L + S - 1) / S;
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     uint64_t local = 0;
     for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gs) {
         // record bytes of the block
         uint32_t size = 0;
-        for (uint32_t t = 0; t < kPack2Span; ++t) {
-            const uint64_t j = b * kPack2Span + t;
+        for (uint32_t t = 0; t < S; ++t) {
+            const uint64_t j = b * S + t;
             if (j >= L) break;
             size += 1;
             for (uint32_t A = 0; A < args.a; ++A) {
@@ -346,8 +348,8 @@ __global__ __launch_bounds__(256) void k_gen_pack2(uint8_t *img, uint64_t L, Pac
                 }
             }
         }
-        const bool spills = size > kPack2Inline;
-        const uint32_t list_bytes = (2 * kPack2Span + size + 15) & ~15u;
+        const bool spills = size > pack2_inline(S);
+        const uint32_t list_bytes = (2 * S + size + 15) & ~15u;
         if (pass == 0) {
             if (spills) atomicAdd(spill_ctr, (unsigned long long)list_bytes);
             continue;
@@ -362,16 +364,16 @@ __global__ __launch_bounds__(256) void k_gen_pack2(uint8_t *img, uint64_t L, Pac
                 blk[k] = 0;
                 blk[8 + k] = (uint8_t)(addr >> (8 * k));
             }
-            dst = list + 2 * kPack2Span;
-            hdr = 2 * kPack2Span;
+            dst = list + 2 * S;
+            hdr = 2 * S;
         } else {
-            dst = blk + 8;
-            hdr = 8;
+            dst = blk + S;
+            hdr = S;
         }
         uint32_t o = 0;
-        for (uint32_t t = 0; t < kPack2Span; ++t) {
-            const uint64_t j = b * kPack2Span + t;
-            if (spills) *reinterpret_cast<uint16_t *>(dst - 2 * kPack2Span + 2 * t) = (uint16_t)(hdr + o);
+        for (uint32_t t = 0; t < S; ++t) {
+            const uint64_t j = b * S + t;
+            if (spills) *reinterpret_cast<uint16_t *>(dst - 2 * S + 2 * t) = (uint16_t)(hdr + o);
             else blk[t] = (uint8_t)(hdr + o);
             if (j >= L) continue;
             uint32_t m2 = 0, jA[8], m1[8];
@@ -786,8 +788,10 @@ int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStr
         const uint64_t K = node_key(desc.seed, u);
         const uint32_t a = dn.arity, nT = (1u << a) - 1;
         // KIND_PACK2 when every child A is a PLANE node of <= 8 MASK8 children
-        // with <= 8 leaves and a block of 8 positions is expected to hold <= 40
-        // record bytes (+ 8 header bytes; spills: ~0.1 % of the blocks)
+        // with <= 8 leaves; span S = the largest of 8, 4, 2 at which a block
+        // is expected to hold <= 56 bytes (S header bytes + S records; spills:
+        // ~0.1 % of the blocks at the Kingsford shape, S = 8, mean 45.7 bytes;
+        // a few % at the RefSeq shape, S = 2, mean 52.6 bytes)
         bool pack2 = pack2_enabled() && dn.kind == KIND_PLANE && a <= 8 && q[u] > 0.0;
         double rec = 1.0;
         std::vector<uint64_t *> utab;
@@ -804,7 +808,10 @@ int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStr
                 if (std::find(utab.begin(), utab.end(), node_T[gu]) == utab.end()) utab.push_back(node_T[gu]);
             }
         }
-        if (pack2 && (kPack2Span * rec > 40.0 || utab.size() > 4)) pack2 = false;
+        uint32_t span = 0;
+        for (uint32_t S = kPack2MaxSpan; pack2 && S >= 2 && !span; S /= 2)
+            if (S * (rec + 1.0) <= 56.0) span = S;
+        if (pack2 && (!span || utab.size() > 4)) pack2 = false;
         if (pack2) {
             std::vector<void *> tmps;
             auto free_tmps = [&]() {
@@ -874,10 +881,10 @@ int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStr
                     args.nT[ti] = (1u << gn.arity) - 1;
                 }
             }
-            const uint64_t nb2 = (L + kPack2Span - 1) / kPack2Span;
+            const uint64_t nb2 = (L + span - 1) / span;
             (void)hipMemsetAsync(d_ctr, 0, sizeof(unsigned long long), s);
-            hipLaunchKernelGGL(k_gen_pack2, dim3(launch_grid(nb2)), dim3(256), 0, s, nullptr, L, args, nullptr, d_ctr,
-                               d_ones, 0);
+            hipLaunchKernelGGL(k_gen_pack2, dim3(launch_grid(nb2)), dim3(256), 0, s, nullptr, L, span, args, nullptr,
+                               d_ctr, d_ones, 0);
             unsigned long long spill_bytes = 0;
             MBRWT_HIP(hipMemcpyAsync(&spill_bytes, d_ctr, sizeof(spill_bytes), hipMemcpyDeviceToHost, s));
             MBRWT_HIP(hipStreamSynchronize(s));
@@ -892,7 +899,7 @@ int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStr
                 }
             }
             dn.kind = KIND_PACK2;
-            dn.stride = kPack2Block;
+            dn.stride = span;  // positions per block
             uint8_t *img = alloc_image(dn, nb2 * kPack2Block);
             if (!img) {
                 free_tmps();
@@ -900,8 +907,8 @@ int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStr
                 return fail(MBRWT_ERR_NOMEM, "device allocation failed");
             }
             (void)hipMemsetAsync(d_ctr, 0, sizeof(unsigned long long), s);
-            hipLaunchKernelGGL(k_gen_pack2, dim3(launch_grid(nb2)), dim3(256), 0, s, img, L, args, spill, d_ctr, d_ones,
-                               1);
+            hipLaunchKernelGGL(k_gen_pack2, dim3(launch_grid(nb2)), dim3(256), 0, s, img, L, span, args, spill, d_ctr,
+                               d_ones, 1);
             if (hipGetLastError() != hipSuccess) {
                 free_tmps();
                 (void)hipFree(d_ctr);

@@ -417,3 +417,35 @@ def test_pack2_layout_synthetic(oracle_mod, fold):
         assert p2.traverse_kernel() == "k_traverse_fast2/pack2"
     rows = np.random.default_rng(10).integers(0, n, 100_000).astype(np.uint64)
     _agree(t, [p2, p1], rows, np.random.default_rng(4).integers(0, m, 16), m)
+
+
+def test_pack2_dense_subtrees_take_a_short_span(oracle_mod):
+    """d = 4 %: ~26 record bytes per position, so the host builder picks a
+    span of 2 or 1 positions per block (mbrwt_internal.hpp); results as the
+    oracle's under every kernel."""
+    O = oracle_mod
+    rng = np.random.default_rng(14)
+    n, m = 3000, 2048
+    dense = rng.random((n, m)) < 0.04
+    t = O.OracleTree.from_dense(dense, "basic", 8)
+    p2 = _dev(t)
+    p1 = _with_env("MBRWT_PACK2", "0", lambda: _dev(t))
+    assert p2.traverse_kernel() == "k_traverse_fast2/pack2"
+    assert p2.device_bytes() != p1.device_bytes()
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 5000)]).astype(np.uint64)
+    _agree(t, [p2, p1], rows, [0, 9, 100, 1023, 2047], m)
+
+
+def test_pack2_refseq_shape_synthetic(oracle_mod):
+    """RefSeq shape (3,173 columns, d = 3.8 %): the generator's span-2 PACK2
+    images agree with the oracle's independent implementation of the spec."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    n, m = 200_000, 3173
+    t = O.OracleTree.topdown(n, m, 0.038, 8, 8)
+    p2 = BRWTDevice.synthetic(n, m, 0.038, 8, 8)
+    p1 = _with_env("MBRWT_PACK2", "0", lambda: BRWTDevice.synthetic(n, m, 0.038, 8, 8))
+    assert p2.traverse_kernel() == "k_traverse_fast2/pack2"
+    assert p2.device_bytes() != p1.device_bytes()
+    rows = np.random.default_rng(11).integers(0, n, 20_000).astype(np.uint64)
+    _agree(t, [p2, p1], rows, np.random.default_rng(5).integers(0, m, 6), m)
