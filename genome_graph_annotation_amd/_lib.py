@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmbrwt.so")
+# MBRWT_LIB: another build of the same library (same-box A/B of kernel changes, tools/ab.sh)
+LIB_PATH = os.environ.get("MBRWT_LIB") or os.path.join(_HERE, "libmbrwt.so")
 
 MBRWT_OK = 0
 MBRWT_ERR_INVALID = 1
