@@ -6,20 +6,23 @@
 // * The row delimiters become the CSR offsets they encode:
 //   select1(row + 1) - row == offsets[row] (bin_rel_wt_sdsl.cpp:58-62), kept
 //   as a u64 array in HBM (one 16-byte read per row instead of two selects).
-// * The string of column ids is held in a WAVELET MATRIX (not the levelwise
-//   wavelet tree of wt_int): level l stores bit (w-1-l) of every symbol, the
-//   symbols of level l+1 being level l's stably partitioned by that bit; a
-//   position maps down with ONE rank per level (bit 0: rank0(p); bit 1:
-//   Z_l + rank1(p)), so decoding needs no node boundaries.
+// * The string of column ids is held in a 4-ARY WAVELET MATRIX (not the
+//   binary levelwise wavelet tree of wt_int): level l stores the 2-bit digit
+//   l (from the top) of every symbol, the symbols of level l+1 being level
+//   l's stably partitioned by that digit into 4 buckets; a position maps
+//   down with ONE rank per level (digit d: Z_l[d] + rank_d(p)), so decoding
+//   needs no node boundaries and ceil(w/2) levels instead of w (6 instead of
+//   12 at 3,173 columns): half the dependent random block reads per label.
 // * Rows are stored with their ids ascending.  That changes no query result
 //   (get_row returns the ascending distinct ids, get is membership,
 //   get_column lists rows in row order) and makes a row's decoded positions
 //   come out in output order: get_row is "access" of the row's contiguous
 //   string range, one thread per output label, with adjacent threads walking
 //   adjacent positions (their level reads coalesce).
-// * Every level is a sequence of 32-byte rank blocks {u32 ones before the
-//   block, 7 u32 data words} = 224 positions; a rank is one 16-byte read (two
-//   when the position is in the block's last 128 bits).
+// * Every level is a sequence of 64-byte rank blocks {u32 occurrences of
+//   digits 0, 1, 2 before the block, 13 u32 words of 16 digits} = 208
+//   positions; a rank is one 64-byte segment (the 16-byte quarters up to the
+//   position's word) plus popcounts of digit-match masks.
 // * Rows are cut into chunks of 2^k rows with < 2^31 symbols each (u32
 //   positions and ranks), each chunk an independent wavelet matrix.
 #include <hipcub/hipcub.hpp>
@@ -37,8 +40,9 @@
 namespace mbrwt {
 namespace {
 
-constexpr uint32_t kWtBlockPos = 224;  // positions per 32-byte rank block
-constexpr uint32_t kWtMaxLevels = 32;
+constexpr uint32_t kWtBlockPos = 208;    // 2-bit digits per 64-byte rank block
+constexpr uint32_t kWtBlockBytes = 64;
+constexpr uint32_t kWtMaxLevels = 16;    // digit levels (symbols of <= 32 bits)
 
 struct WtChunkDev {
     uint64_t base;       // level 0 block array; level l at base + l * level_bytes
@@ -46,7 +50,7 @@ struct WtChunkDev {
     uint64_t level_bytes;
     uint32_t len;        // symbols in the chunk
     uint32_t pad;
-    uint32_t zeros[kWtMaxLevels];
+    uint32_t z[kWtMaxLevels][4];  // level l: start of digit v's bucket in level l + 1
 };
 
 __device__ __forceinline__ uint64_t mix64_d(uint64_t z) {
@@ -55,50 +59,96 @@ __device__ __forceinline__ uint64_t mix64_d(uint64_t z) {
     return z ^ (z >> 31);
 }
 
-// ones in [0, p) of the level whose blocks start at `lvl`, and bit p
-__device__ __forceinline__ uint32_t wt_rank(uint64_t lvl, uint32_t p, uint32_t &bit) {
-    const uint32_t blk = p / kWtBlockPos, o = p - blk * kWtBlockPos;
-    const uint64_t a = lvl + (uint64_t)blk * 32;
-    const uint4 q0 = gld_at<uint4>(a);
-    uint32_t r = q0.x, word;
-    const uint32_t k = o >> 5, b = o & 31;
-    if (k < 3) {
-        word = k == 0 ? q0.y : k == 1 ? q0.z : q0.w;
-        if (k >= 1) r += __builtin_popcount(q0.y);
-        if (k >= 2) r += __builtin_popcount(q0.z);
-    } else {
-        const uint4 q1 = gld_at<uint4>(a + 16);
-        r += __builtin_popcount(q0.y) + __builtin_popcount(q0.z) + __builtin_popcount(q0.w);
-        word = k == 3 ? q1.x : k == 4 ? q1.y : k == 5 ? q1.z : q1.w;
-        if (k >= 4) r += __builtin_popcount(q1.x);
-        if (k >= 5) r += __builtin_popcount(q1.y);
-        if (k >= 6) r += __builtin_popcount(q1.z);
-    }
-    bit = (word >> b) & 1u;
-    return r + __builtin_popcount(word & ((1u << b) - 1u));
+// bit 2i of the result is set iff digit i of x equals the digit in pat
+// (pat = digit * 0x55555555)
+__device__ __forceinline__ uint32_t digit_matches(uint32_t x, uint32_t pat) {
+    const uint32_t y = x ^ pat;
+    return ~(y | (y >> 1)) & 0x55555555u;
 }
 
-// position of the j-th one (ONE = true) or zero of a level (1-based j)
-template <bool ONE>
-__device__ uint32_t wt_select(uint64_t lvl, uint32_t nblk1, uint32_t j) {
-    uint32_t lo = 0, hi = nblk1;  // last block with (ones|zeros) before it < j
+// A level's block at `a`: dwords 0..2 = digits 0, 1, 2 before the block;
+// dwords 3..15 = 13 words of 16 digits (digit i of word k = position 16k + i).
+// The words up to word k are read (1..4 16-byte loads of one 64-byte segment).
+struct WtBlock {
+    uint32_t c0, c1, c2;
+    uint32_t w[13];
+    __device__ __forceinline__ void load(uint64_t a, uint32_t k) {
+        const uint4 q0 = gld_at<uint4>(a);
+        c0 = q0.x;
+        c1 = q0.y;
+        c2 = q0.z;
+        w[0] = q0.w;
+#pragma unroll
+        for (uint32_t h = 1; h < 4; ++h) {
+            if (k >= 4 * h - 3) {
+                const uint4 q = gld_at<uint4>(a + 16 * h);
+                w[4 * h - 3] = q.x;
+                w[4 * h - 2] = q.y;
+                w[4 * h - 1] = q.z;
+                w[4 * h] = q.w;
+            } else {
+                w[4 * h - 3] = w[4 * h - 2] = w[4 * h - 1] = w[4 * h] = 0;
+            }
+        }
+    }
+    __device__ __forceinline__ uint32_t before(uint32_t blk, uint32_t v) const {
+        return v == 0 ? c0 : v == 1 ? c1 : v == 2 ? c2 : blk * kWtBlockPos - c0 - c1 - c2;
+    }
+    // occurrences of digit v in positions [0, 16k + b) of the block
+    __device__ __forceinline__ uint32_t count(uint32_t v, uint32_t k, uint32_t b) const {
+        const uint32_t pat = v * 0x55555555u;
+        uint32_t r = 0, x = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 13; ++i) {
+            const uint32_t m = digit_matches(w[i], pat);
+            if (i < k) r += __builtin_popcount(m);
+            x = i == k ? m : x;
+        }
+        return r + __builtin_popcount(x & ((1u << (2 * b)) - 1u));
+    }
+};
+
+// rank of digit v at position p of a level: occurrences in [0, p)
+__device__ __forceinline__ uint32_t wt_rank(uint64_t lvl, uint32_t p, uint32_t v) {
+    const uint32_t blk = p / kWtBlockPos, o = p - blk * kWtBlockPos;
+    WtBlock B;
+    B.load(lvl + (uint64_t)blk * kWtBlockBytes, o >> 4);
+    return B.before(blk, v) + B.count(v, o >> 4, o & 15);
+}
+
+// access + rank: digit d at position p, returns occurrences of d in [0, p)
+__device__ __forceinline__ uint32_t wt_access_rank(uint64_t lvl, uint32_t p, uint32_t &d) {
+    const uint32_t blk = p / kWtBlockPos, o = p - blk * kWtBlockPos, k = o >> 4, b = o & 15;
+    WtBlock B;
+    B.load(lvl + (uint64_t)blk * kWtBlockBytes, k);
+    uint32_t wk = B.w[0];
+#pragma unroll
+    for (uint32_t i = 1; i < 13; ++i) wk = i == k ? B.w[i] : wk;
+    d = (wk >> (2 * b)) & 3u;
+    return B.before(blk, d) + B.count(d, k, b);
+}
+
+// position of the j-th (1-based) occurrence of digit v in a level of nblk1
+// blocks (the last one the sentinel)
+__device__ uint32_t wt_select(uint64_t lvl, uint32_t nblk1, uint32_t v, uint32_t j) {
+    uint32_t lo = 0, hi = nblk1;  // last block with occurrences before it < j
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
-        const uint32_t r = gld_at<uint32_t>(lvl + (uint64_t)mid * 32);
-        const uint32_t before = ONE ? r : mid * kWtBlockPos - r;
+        const uint4 q = gld_at<uint4>(lvl + (uint64_t)mid * kWtBlockBytes);
+        const uint32_t before = v == 0 ? q.x : v == 1 ? q.y : v == 2 ? q.z : mid * kWtBlockPos - q.x - q.y - q.z;
         if (before < j) lo = mid;
         else hi = mid;
     }
-    const uint64_t a = lvl + (uint64_t)lo * 32;
-    const uint32_t r = gld_at<uint32_t>(a);
-    uint32_t need = j - (ONE ? r : lo * kWtBlockPos - r);
-    for (uint32_t k = 0; k < 7; ++k) {
-        uint32_t w = gld_at<uint32_t>(a + 4 + 4 * k);
-        if (!ONE) w = ~w;
-        const uint32_t c = __builtin_popcount(w);
+    WtBlock B;
+    B.load(lvl + (uint64_t)lo * kWtBlockBytes, 12);
+    uint32_t need = j - B.before(lo, v);
+    const uint32_t pat = v * 0x55555555u;
+    for (uint32_t k = 0; k < 13; ++k) {
+        uint32_t m = digit_matches(B.w[k], pat);
+        const uint32_t c = __builtin_popcount(m);
         if (need <= c) {
-            while (--need) w &= w - 1;
-            return lo * kWtBlockPos + 32 * k + __builtin_ctz(w);
+            while (--need) m &= m - 1;
+            return lo * kWtBlockPos + 16 * k + (__builtin_ctz(m) >> 1);
         }
         need -= c;
     }
@@ -107,37 +157,44 @@ __device__ uint32_t wt_select(uint64_t lvl, uint32_t nblk1, uint32_t j) {
 
 // ---- construction ----------------------------------------------------------
 
-// one 32-position word of bit `sh` of the symbols
-__global__ void k_wt_bits(const uint32_t *__restrict__ sym, uint64_t len, uint32_t sh, uint32_t *__restrict__ words,
-                          uint64_t nwords) {
+// one word of 16 digits (bits sh, sh+1 of the symbols)
+__global__ void k_wt_words(const uint32_t *__restrict__ sym, uint64_t len, uint32_t sh, uint32_t *__restrict__ words,
+                           uint64_t nwords) {
     const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += gstride) {
         uint32_t x = 0;
-        const uint64_t p0 = 32 * w;
-        for (uint32_t k = 0; k < 32 && p0 + k < len; ++k) x |= ((sym[p0 + k] >> sh) & 1u) << k;
+        const uint64_t p0 = 16 * w;
+        for (uint32_t k = 0; k < 16 && p0 + k < len; ++k) x |= ((sym[p0 + k] >> sh) & 3u) << (2 * k);
         words[w] = x;
     }
 }
 
-__global__ void k_wt_block_counts(const uint32_t *__restrict__ words, uint64_t nwords, uint32_t *__restrict__ cnt,
-                                  uint64_t nblk) {
+// digits 0, 1, 2 per block (positions >= len, padded with digit 0, excluded):
+// cnt[v * stride + b]
+__global__ void k_wt_block_counts(const uint32_t *__restrict__ words, uint64_t nwords, uint64_t len,
+                                  uint32_t *__restrict__ cnt, uint64_t stride, uint64_t nblk) {
     const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nblk; b += gstride) {
-        uint32_t c = 0;
-        for (uint32_t k = 0; k < 7; ++k)
-            if (7 * b + k < nwords) c += __builtin_popcount(words[7 * b + k]);
-        cnt[b] = c;
+        uint32_t c[3] = {0, 0, 0};
+        for (uint32_t k = 0; k < 13; ++k) {
+            const uint64_t wi = 13 * b + k;
+            if (wi >= nwords) break;
+            const uint64_t valid = len - 16 * wi;  // > 0
+            const uint32_t keep = valid >= 16 ? 0x55555555u : 0x55555555u & ((1u << (2 * valid)) - 1u);
+            for (uint32_t v = 0; v < 3; ++v) c[v] += __builtin_popcount(digit_matches(words[wi], v * 0x55555555u) & keep);
+        }
+        for (uint32_t v = 0; v < 3; ++v) cnt[v * stride + b] = c[v];
     }
 }
 
-// blocks [0, nblk) + the sentinel block nblk (rank = total ones, zero words)
+// blocks [0, nblk) + the sentinel block nblk (counts = totals, zero words)
 __global__ void k_wt_blocks(const uint32_t *__restrict__ words, uint64_t nwords, const uint32_t *__restrict__ ranks,
-                            uint64_t nblk, uint32_t *__restrict__ out) {
+                            uint64_t stride, uint64_t nblk, uint32_t *__restrict__ out) {
     const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b <= nblk; b += gstride) {
-        uint32_t *o = out + 8 * b;
-        o[0] = ranks[b];
-        for (uint32_t k = 0; k < 7; ++k) o[1 + k] = (b < nblk && 7 * b + k < nwords) ? words[7 * b + k] : 0u;
+        uint32_t *o = out + 16 * b;
+        for (uint32_t v = 0; v < 3; ++v) o[v] = ranks[v * stride + b];
+        for (uint32_t k = 0; k < 13; ++k) o[3 + k] = (b < nblk && 13 * b + k < nwords) ? words[13 * b + k] : 0u;
     }
 }
 
@@ -174,6 +231,7 @@ struct WtParams {
     const uint64_t *offsets;  // [num_rows + 1] global string offsets
     uint64_t num_rows, num_columns;
     uint32_t w, log2_rows;  // symbol bits; rows per chunk = 2^log2_rows
+    uint32_t levels;        // 2-bit digit levels = ceil(w / 2)
     unsigned long long *scalars;  // [2] error flags
 };
 
@@ -217,11 +275,11 @@ __global__ __launch_bounds__(kWtTile) void k_wt_decode(WtParams P, const uint64_
             const uint64_t base = ch->base, lb = ch->level_bytes;
             uint32_t p = (uint32_t)(P.offsets[row] + (e - s_csr[lo]) - ch->str0);
             uint32_t sym = 0;
-            for (uint32_t l = 0; l < P.w; ++l) {
-                uint32_t bit;
-                const uint32_t r1 = wt_rank(base + l * lb, p, bit);
-                sym = (sym << 1) | bit;
-                p = bit ? ch->zeros[l] + r1 : p - r1;
+            for (uint32_t l = 0; l < P.levels; ++l) {
+                uint32_t d;
+                const uint32_t r = wt_access_rank(base + l * lb, p, d);
+                sym = (sym << 2) | d;
+                p = ch->z[l][d] + r;
             }
             cols[e] = sym;
         }
@@ -242,17 +300,11 @@ __global__ void k_wt_get(WtParams P, const uint64_t *__restrict__ rows, const ui
         }
         const WtChunkDev *ch = P.chunks + (row >> P.log2_rows);
         uint32_t s = (uint32_t)(P.offsets[row] - ch->str0), e = (uint32_t)(P.offsets[row + 1] - ch->str0);
-        for (uint32_t l = 0; l < P.w && s < e; ++l) {
+        for (uint32_t l = 0; l < P.levels && s < e; ++l) {
             const uint64_t lvl = ch->base + l * ch->level_bytes;
-            uint32_t bs, be;
-            const uint32_t rs = wt_rank(lvl, s, bs), re = wt_rank(lvl, e, be);
-            if ((col >> (P.w - 1 - l)) & 1) {
-                s = ch->zeros[l] + rs;
-                e = ch->zeros[l] + re;
-            } else {
-                s -= rs;
-                e -= re;
-            }
+            const uint32_t d = (uint32_t)(col >> (2 * (P.levels - 1 - l))) & 3u;
+            s = ch->z[l][d] + wt_rank(lvl, s, d);
+            e = ch->z[l][d] + wt_rank(lvl, e, d);
         }
         out[i] = e > s ? 1 : 0;
     }
@@ -265,17 +317,11 @@ __global__ void k_wt_col_range(WtParams P, uint64_t nchunks, uint32_t col, uint3
     for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += gstride) {
         const WtChunkDev *ch = P.chunks + c;
         uint32_t s = 0, e = ch->len;
-        for (uint32_t l = 0; l < P.w && s < e; ++l) {
+        for (uint32_t l = 0; l < P.levels && s < e; ++l) {
             const uint64_t lvl = ch->base + l * ch->level_bytes;
-            uint32_t bs, be;
-            const uint32_t rs = wt_rank(lvl, s, bs), re = wt_rank(lvl, e, be);
-            if ((col >> (P.w - 1 - l)) & 1) {
-                s = ch->zeros[l] + rs;
-                e = ch->zeros[l] + re;
-            } else {
-                s -= rs;
-                e -= re;
-            }
+            const uint32_t d = (col >> (2 * (P.levels - 1 - l))) & 3u;
+            s = ch->z[l][d] + wt_rank(lvl, s, d);
+            e = ch->z[l][d] + wt_rank(lvl, e, d);
         }
         start[c] = s;
         count[c] = e > s ? e - s : 0;
@@ -295,12 +341,12 @@ __global__ void k_wt_col_lift(WtParams P, uint64_t nchunks, uint32_t col, const 
             else hi = mid;
         }
         const WtChunkDev *ch = P.chunks + lo;
-        const uint32_t nblk1 = (uint32_t)(ch->level_bytes / 32);
+        const uint32_t nblk1 = (uint32_t)(ch->level_bytes / kWtBlockBytes);
         uint32_t q = start[lo] + (uint32_t)(i - coff[lo]);
-        for (uint32_t l = P.w; l-- > 0;) {
+        for (uint32_t l = P.levels; l-- > 0;) {
             const uint64_t lvl = ch->base + l * ch->level_bytes;
-            if ((col >> (P.w - 1 - l)) & 1) q = wt_select<true>(lvl, nblk1, q - ch->zeros[l] + 1);
-            else q = wt_select<false>(lvl, nblk1, q + 1);
+            const uint32_t d = (col >> (2 * (P.levels - 1 - l))) & 3u;
+            q = wt_select(lvl, nblk1, d, q - ch->z[l][d] + 1);
         }
         // row = last row of the chunk whose start offset <= str0 + q
         const uint64_t g = ch->str0 + q;
@@ -348,6 +394,7 @@ struct WtCtx {
         p.num_rows = num_rows;
         p.num_columns = num_columns;
         p.w = w;
+        p.levels = (w + 1) / 2;
         p.log2_rows = log2_rows;
         p.scalars = reinterpret_cast<unsigned long long *>(d_scalars);
         return p;
@@ -377,50 +424,63 @@ uint32_t symbol_bits(uint64_t num_columns) {  // ids < num_columns
 // Build the wavelet matrix of one chunk from its symbols (d_sym, len, in
 // string order); d_sym and d_alt are consumed (sorted level by level).
 int build_chunk(WtCtx &c, WtChunkDev &ch, uint32_t *d_sym, uint32_t *d_alt, uint64_t len, hipStream_t s) {
-    const uint64_t nwords = (len + 31) / 32, nblk = (len + kWtBlockPos - 1) / kWtBlockPos;
+    const uint32_t levels = (c.w + 1) / 2;
+    const uint64_t nwords = (len + 15) / 16, nblk = (len + kWtBlockPos - 1) / kWtBlockPos;
+    const uint64_t stride = nblk + 2;  // per-digit count / rank arrays
     ch.len = (uint32_t)len;
-    ch.level_bytes = (nblk + 1) * 32;
+    ch.level_bytes = (nblk + 1) * kWtBlockBytes;
     void *lv = nullptr;
-    MBRWT_HIP(hipMalloc(&lv, ch.level_bytes * c.w));
+    MBRWT_HIP(hipMalloc(&lv, ch.level_bytes * levels));
     c.allocs.push_back(lv);
-    c.device_bytes += ch.level_bytes * c.w;
+    c.device_bytes += ch.level_bytes * levels;
     ch.base = reinterpret_cast<uint64_t>(lv);
     int rc;
-    // workspace: words | block counts | ranks | scan/sort temp
+    // workspace: words | 3 x block counts | 3 x ranks | totals | scan/sort temp
     size_t scan_bytes = 0, sort_bytes = 0;
     MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                                (int)(nblk + 1), s));
     MBRWT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                                (int)std::max<uint64_t>(len, 1), 0, 1, s));
-    if ((rc = ensure(c.ws_c, (nwords + 2 * (nblk + 2) + kWtMaxLevels) * sizeof(uint32_t)))) return rc;
+                                                (int)std::max<uint64_t>(len, 1), 0, 2, s));
+    if ((rc = ensure(c.ws_c, (nwords + 6 * stride + 4 * kWtMaxLevels) * sizeof(uint32_t)))) return rc;
     if ((rc = ensure(c.ws_scan, std::max(scan_bytes, sort_bytes) + 16))) return rc;
     uint32_t *d_words = reinterpret_cast<uint32_t *>(c.ws_c.buf);
     uint32_t *d_cnt = d_words + nwords;
-    uint32_t *d_rank = d_cnt + nblk + 2;
-    uint32_t *d_ones = d_rank + nblk + 2;  // ones per level, read back once
-    for (uint32_t l = 0; l < c.w; ++l) {
-        const uint32_t sh = c.w - 1 - l;
+    uint32_t *d_rank = d_cnt + 3 * stride;
+    uint32_t *d_tot = d_rank + 3 * stride;  // digits 0..2 per level, read back once
+    for (uint32_t l = 0; l < levels; ++l) {
+        const uint32_t sh = 2 * (levels - 1 - l);
         uint32_t *out = reinterpret_cast<uint32_t *>(ch.base + l * ch.level_bytes);
         if (nwords) {
-            hipLaunchKernelGGL(k_wt_bits, dim3(grid_for(nwords)), dim3(256), 0, s, d_sym, len, sh, d_words, nwords);
-            hipLaunchKernelGGL(k_wt_block_counts, dim3(grid_for(nblk)), dim3(256), 0, s, d_words, nwords, d_cnt, nblk);
+            hipLaunchKernelGGL(k_wt_words, dim3(grid_for(nwords)), dim3(256), 0, s, d_sym, len, sh, d_words, nwords);
+            hipLaunchKernelGGL(k_wt_block_counts, dim3(grid_for(nblk)), dim3(256), 0, s, d_words, nwords, len, d_cnt,
+                               stride, nblk);
         }
-        MBRWT_HIP(hipMemsetAsync(d_cnt + nblk, 0, sizeof(uint32_t), s));
-        MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, d_cnt, d_rank, (int)(nblk + 1), s));
-        hipLaunchKernelGGL(k_wt_blocks, dim3(grid_for(nblk + 1)), dim3(256), 0, s, d_words, nwords, d_rank, nblk, out);
+        for (uint32_t v = 0; v < 3; ++v) {
+            MBRWT_HIP(hipMemsetAsync(d_cnt + v * stride + nblk, 0, sizeof(uint32_t), s));
+            MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, d_cnt + v * stride,
+                                                       d_rank + v * stride, (int)(nblk + 1), s));
+            MBRWT_HIP(hipMemcpyAsync(d_tot + 3 * l + v, d_rank + v * stride + nblk, sizeof(uint32_t),
+                                     hipMemcpyDeviceToDevice, s));
+        }
+        hipLaunchKernelGGL(k_wt_blocks, dim3(grid_for(nblk + 1)), dim3(256), 0, s, d_words, nwords, d_rank, stride,
+                           nblk, out);
         MBRWT_HIP(hipGetLastError());
-        MBRWT_HIP(hipMemcpyAsync(d_ones + l, d_rank + nblk, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-        if (l + 1 < c.w && len) {  // stable partition by this bit = 1-bit radix pass
+        if (l + 1 < levels && len) {  // stable partition by this digit = one 2-bit radix pass
             MBRWT_HIP(hipcub::DeviceRadixSort::SortKeys(c.ws_scan.buf, sort_bytes, d_sym, d_alt, (int)len, (int)sh,
-                                                        (int)sh + 1, s));
+                                                        (int)sh + 2, s));
             std::swap(d_sym, d_alt);
         }
     }
-    uint32_t ones[kWtMaxLevels];
-    MBRWT_HIP(hipMemcpyAsync(c.h_scalars, d_ones, c.w * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    uint32_t tot[3 * kWtMaxLevels];
+    MBRWT_HIP(hipMemcpyAsync(c.h_scalars, d_tot, 3 * levels * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     MBRWT_HIP(hipStreamSynchronize(s));
-    std::memcpy(ones, c.h_scalars, c.w * sizeof(uint32_t));
-    for (uint32_t l = 0; l < c.w; ++l) ch.zeros[l] = (uint32_t)(len - ones[l]);
+    std::memcpy(tot, c.h_scalars, 3 * levels * sizeof(uint32_t));
+    for (uint32_t l = 0; l < levels; ++l) {
+        ch.z[l][0] = 0;
+        ch.z[l][1] = tot[3 * l];
+        ch.z[l][2] = tot[3 * l] + tot[3 * l + 1];
+        ch.z[l][3] = tot[3 * l] + tot[3 * l + 1] + tot[3 * l + 2];
+    }
     return MBRWT_OK;
 }
 

@@ -6,7 +6,8 @@ One step = one batched get_row over 10 M uniform random rows (device-resident
 ids -> device-resident CSR).  roofline: algorithmic bytes of the decode
 kernel per launch = sum over rows of (16 + 4 L + 64 B x w x L) -- one 64-byte
 line per symbol per wavelet level, w = 12 bits for 3,173 columns
-(DESIGN.md "BinRel-WT") -- over its HIP-event time.  cpu_baseline: the
+(DESIGN.md "BinRel-WT"; the reference's levelwise tree, not this build's
+4-ary wavelet matrix of ceil(w/2) levels) -- over its HIP-event time.  cpu_baseline: the
 oracle's restatement of BinRelWT_sdsl::get_row (sdsl-style levelwise wavelet
 tree, interval_symbols) over the first --cpu-rows rows of the SAME matrix,
 timed on random rows of that prefix on the host cores.  Parity: the device
@@ -139,7 +140,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_wt_decode",
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
-                     "labels_per_row": n_lab / a.batch, "levels": w},
+                     "labels_per_row": n_lab / a.batch, "levels": w, "digit_levels": (w + 1) // 2},
         "cpu_baseline": cpu,
         "parity": parity,
     }
