@@ -53,6 +53,15 @@ class SynthDesc(C.Structure):
     ]
 
 
+class ColumnsDesc(C.Structure):
+    _fields_ = [
+        ("num_rows", C.c_uint64),
+        ("num_columns", C.c_uint64),
+        ("columns", C.POINTER(u64p)),
+        ("arity", C.c_uint32),
+    ]
+
+
 class BinRelDesc(C.Structure):  # include/mbrwt_wt.h
     _fields_ = [
         ("num_rows", C.c_uint64),
@@ -75,6 +84,7 @@ class BinRelSynthDesc(C.Structure):
 SIGNATURES = {
     "mbrwt_create": (C.c_int, [C.POINTER(TreeDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "mbrwt_create_synthetic": (C.c_int, [C.POINTER(SynthDesc), C.c_int, C.POINTER(C.c_void_p)]),
+    "mbrwt_create_from_columns": (C.c_int, [C.POINTER(ColumnsDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "mbrwt_destroy": (None, [C.c_void_p]),
     "mbrwt_num_rows": (C.c_uint64, [C.c_void_p]),
     "mbrwt_num_columns": (C.c_uint64, [C.c_void_p]),

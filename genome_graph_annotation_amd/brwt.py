@@ -64,6 +64,25 @@ class BRWTDevice:
         L.check(lib.mbrwt_create_synthetic(C.byref(d), device, C.byref(h)), "mbrwt_create_synthetic")
         return cls(h)
 
+    @classmethod
+    def from_columns(cls, columns, num_rows, arity=2, device=0):
+        """BRWTBottomUpBuilder::build with the basic partitioner on the device
+        (include/mbrwt.h mbrwt_create_from_columns).  `columns`: a sequence of
+        uint64 arrays (ceil(num_rows/64) LSB-first words each), or a 2-D
+        uint64 array [num_columns, words]."""
+        lib = L.lib()
+        cols = [np.ascontiguousarray(c, dtype=np.uint64) for c in columns]
+        W = (num_rows + 63) // 64
+        if any(len(c) < W for c in cols):
+            raise ValueError("a column has fewer than ceil(num_rows/64) words")
+        ptrs = (L.u64p * max(1, len(cols)))()
+        for j, c in enumerate(cols):
+            ptrs[j] = c.ctypes.data_as(L.u64p)
+        d = L.ColumnsDesc(num_rows, len(cols), ptrs, arity)
+        h = C.c_void_p()
+        L.check(lib.mbrwt_create_from_columns(C.byref(d), device, C.byref(h)), "mbrwt_create_from_columns")
+        return cls(h)
+
     def close(self):
         if getattr(self, "_h", None):
             L.lib().mbrwt_destroy(self._h)

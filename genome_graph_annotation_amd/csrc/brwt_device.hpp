@@ -88,6 +88,21 @@ class BRWTDevice : public BinaryMatrix {
         return m;
     }
 
+    // BRWTBottomUpBuilder::build(columns, get_basic_partitioner(arity))
+    // (BRWT_builders.cpp:20-31, :119-163), run on the device; columns[j] =
+    // ceil(num_rows/64) LSB-first words
+    static BRWTDevice build_bottom_up(const std::vector<std::vector<uint64_t>> &columns, uint64_t num_rows,
+                                      uint32_t arity, int device = 0) {
+        std::vector<const uint64_t *> ptrs(columns.size());
+        for (size_t j = 0; j < columns.size(); ++j) ptrs[j] = columns[j].data();
+        mbrwt_columns_desc d{num_rows, columns.size(), ptrs.data(), arity};
+        BRWTDevice m;
+        mbrwt_ctx *c = nullptr;
+        check_status(mbrwt_create_from_columns(&d, device, &c), "mbrwt_create_from_columns");
+        m.ctx_.reset(c, Deleter());
+        return m;
+    }
+
     uint64_t num_columns() const override { return ctx_ ? mbrwt_num_columns(ctx_.get()) : 0; }
     uint64_t num_rows() const override { return ctx_ ? mbrwt_num_rows(ctx_.get()) : 0; }
     uint64_t num_relations() const override { return ctx_ ? mbrwt_num_relations(ctx_.get()) : 0; }

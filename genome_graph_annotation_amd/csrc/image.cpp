@@ -2,6 +2,9 @@
 // (include/mbrwt.h mbrwt_tree_desc), replacing BRWT::load (BRWT.cpp:87-111)
 // as the way structure enters the engine.  Layout: mbrwt_internal.hpp.
 #include <algorithm>
+#include <chrono>
+#include <thread>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -14,12 +17,47 @@ namespace {
 
 inline uint64_t popc(uint64_t x) { return (uint64_t)__builtin_popcountll(x); }
 
+// MBRWT_BUILD_TIMING=1: phase times of the image build on stderr
+struct PhaseTimer {
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    PhaseTimer() : t(std::chrono::steady_clock::now()) {
+        const char *e = std::getenv("MBRWT_BUILD_TIMING");
+        on = e && e[0] == '1';
+    }
+    void lap(const char *what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[mbrwt image] %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
+
+
 
 uint64_t count_ones(const uint64_t *w, uint64_t size) {
     uint64_t c = 0, W = size / 64;
     for (uint64_t k = 0; k < W; ++k) c += popc(w[k]);
     if (size & 63) c += popc(w[W] & ((1ull << (size & 63)) - 1));
     return c;
+}
+
+// hipMalloc + copy of a host image; large images are page-locked for the
+// copy (pageable copies of freshly built images measured ~0.3 GB/s)
+hipError_t upload_bytes(const void *src, size_t bytes, void **out) {
+    void *d = nullptr;
+    hipError_t e = hipMalloc(&d, bytes);
+    if (e != hipSuccess) return e;
+    void *h = const_cast<void *>(src);
+    const bool reg = bytes >= (1u << 20) && hipHostRegister(h, bytes, hipHostRegisterDefault) == hipSuccess;
+    e = hipMemcpy(d, src, bytes, hipMemcpyHostToDevice);
+    if (reg) (void)hipHostUnregister(h);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        return e;
+    }
+    *out = d;
+    return hipSuccess;
 }
 
 // 32-bit chunk b of a bit vector, tail bits past `size` cleared
@@ -79,13 +117,15 @@ int upload_image(const std::vector<const uint64_t *> &child_words, const std::ve
     dn.arity = (uint16_t)a;
     dn.length = L;
     void *d = nullptr;
-    MBRWT_HIP(hipMalloc(&d, host.size()));
+    MBRWT_HIP(upload_bytes(host.data(), host.size(), &d));
     images.push_back(d);
-    MBRWT_HIP(hipMemcpy(d, host.data(), host.size(), hipMemcpyHostToDevice));
     dn.base = (uint64_t)(uintptr_t)d;
     image_bytes += host.size();
     return MBRWT_OK;
 }
+
+std::vector<uint8_t> child_masks(const mbrwt_tree_desc &desc, uint32_t v, uint64_t len);
+
 
 // KIND_PACK image of desc node u (mbrwt_internal.hpp): returns false (and
 // builds nothing) when more than 1 block in 20 would spill.
@@ -98,29 +138,22 @@ bool build_pack_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, DevNo
     std::vector<uint8_t> spill;
     std::vector<std::pair<uint64_t, uint64_t>> spilled;  // (block, offset in spill)
     std::vector<uint64_t> rank(a, 0);
+    std::vector<std::vector<uint8_t>> cm(a);  // each MASK8 child's masks over its positions
+    for (uint32_t c = 0; c < a; ++c) cm[c] = child_masks(desc, fc + c, desc.vec_size[desc.first_child[fc + c]]);
+    std::vector<uint8_t> masks;
     for (uint64_t b = 0; b < blocks; ++b) {
         uint8_t *blk = &host[b * kPackBlock];
-        std::vector<uint8_t> masks;
+        masks.clear();
         for (uint32_t c = 0; c < a; ++c) {
             const uint32_t ch = fc + c;
             const uint64_t *cw = desc.vec_words[ch];
-            uint32_t bits = 0;
-            for (uint32_t t = 0; t < kPackSpan && b * kPackSpan + t < L; ++t) {
-                const uint64_t j = b * kPackSpan + t;
-                if ((cw[j >> 6] >> (j & 63)) & 1) bits |= 1u << t;
-            }
+            // bits b*16 .. b*16+15 of the child's column (tail past L cleared)
+            const uint64_t j0 = b * kPackSpan;
+            uint32_t bits = (uint32_t)(cw[j0 >> 6] >> (j0 & 63)) & 0xFFFFu;
+            if (L - j0 < kPackSpan) bits &= (1u << (L - j0)) - 1u;
             const uint16_t b16 = (uint16_t)bits;
             std::memcpy(blk + 16 * (c / 2) + 2 * (c % 2), &b16, 2);
-            const uint32_t gc = desc.num_children[ch], gfc = desc.first_child[ch];
-            for (uint32_t x = bits; x; x &= x - 1) {
-                const uint64_t jc = rank[c]++;
-                uint32_t m = 0;
-                for (uint32_t k = 0; k < gc; ++k) {
-                    const uint64_t *lw = desc.vec_words[gfc + k];
-                    if ((lw[jc >> 6] >> (jc & 63)) & 1) m |= 1u << k;
-                }
-                masks.push_back((uint8_t)m);
-            }
+            for (uint32_t x = bits; x; x &= x - 1) masks.push_back(cm[c][rank[c]++]);
         }
         if (masks.size() <= kPackArea) {
             for (uint32_t o = 0; o < masks.size(); ++o) blk[pack_area_byte(o)] = masks[o];
@@ -146,8 +179,7 @@ bool build_pack_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, DevNo
         }
     }
     void *d = nullptr;
-    if (hipMalloc(&d, host.size()) != hipSuccess ||
-        hipMemcpy(d, host.data(), host.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    if (upload_bytes(host.data(), host.size(), &d) != hipSuccess) {
         rc = hip_fail(hipErrorOutOfMemory, "pack image upload");
         return true;
     }
@@ -187,8 +219,20 @@ bool pack2_candidate(const mbrwt_tree_desc &desc, uint32_t u) {
     return true;
 }
 
-inline uint32_t desc_bit(const mbrwt_tree_desc &desc, uint32_t node, uint64_t j) {
-    return (uint32_t)((desc.vec_words[node][j >> 6] >> (j & 63)) & 1);
+// children bits of desc node v (<= 8 children) at each of its len positions,
+// by walking the set bits of every child's index column
+std::vector<uint8_t> child_masks(const mbrwt_tree_desc &desc, uint32_t v, uint64_t len) {
+    std::vector<uint8_t> mk(len, 0);
+    const uint64_t W = (len + 63) / 64;
+    for (uint32_t k = 0; k < desc.num_children[v]; ++k) {
+        const uint64_t *cw = desc.vec_words[desc.first_child[v] + k];
+        for (uint64_t w = 0; w < W; ++w) {
+            uint64_t x = cw[w];
+            if (w == W - 1 && (len & 63)) x &= (1ull << (len & 63)) - 1;
+            for (; x; x &= x - 1) mk[w * 64 + (uint64_t)__builtin_ctzll(x)] |= (uint8_t)(1u << k);
+        }
+    }
+    return mk;
 }
 
 // KIND_PACK2 image of desc node u (mbrwt_internal.hpp) with the largest span
@@ -198,35 +242,47 @@ bool build_pack2_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, DevN
                        uint64_t &image_bytes, int &rc) {
     rc = MBRWT_OK;
     const uint32_t a = desc.num_children[u], fc = desc.first_child[u];
-    // the record of every position (flat, with offsets)
+    // the record of every position (flat, with offsets), from the children
+    // masks of u, of every child A and of every grandchild B (set-bit walks)
+    PhaseTimer timer;
+    const std::vector<uint8_t> m2s = child_masks(desc, u, L);
+    std::vector<std::vector<uint8_t>> m1s(a);
+    std::vector<std::vector<std::vector<uint8_t>>> lms(a);
+    std::vector<uint64_t> lenA(a, 0);
+    for (uint32_t A = 0; A < a; ++A) {
+        const uint32_t na = fc + A;
+        lenA[A] = desc.vec_size[desc.first_child[na]];  // = ones of A's column
+        m1s[A] = child_masks(desc, na, lenA[A]);
+        lms[A].resize(desc.num_children[na]);
+        for (uint32_t B = 0; B < desc.num_children[na]; ++B) {
+            const uint32_t nb = desc.first_child[na] + B;
+            lms[A][B] = child_masks(desc, nb, desc.vec_size[desc.first_child[nb]]);
+        }
+    }
     std::vector<uint8_t> recs;
+    recs.reserve(L * 4);
     std::vector<uint64_t> roff(L + 1, 0);
     std::vector<uint64_t> rA(a, 0), rB(8 * a, 0);  // running ranks of the A and B columns
     for (uint64_t j = 0; j < L; ++j) {
-        uint32_t m2 = 0;
-        for (uint32_t A = 0; A < a; ++A) m2 |= desc_bit(desc, fc + A, j) << A;
+        const uint32_t m2 = m2s[j];
         recs.push_back((uint8_t)m2);
-        uint32_t m1s[8] = {0};
-        for (uint32_t A = 0; A < a; ++A) {
-            if (!((m2 >> A) & 1)) continue;
-            const uint32_t na = fc + A, ga = desc.num_children[na], gfa = desc.first_child[na];
-            const uint64_t jA = rA[A]++;
-            for (uint32_t B = 0; B < ga; ++B) m1s[A] |= desc_bit(desc, gfa + B, jA) << B;
-            recs.push_back((uint8_t)m1s[A]);
+        uint32_t m1[8] = {0}, jA[8] = {0};
+        for (uint32_t x = m2; x; x &= x - 1) {
+            const uint32_t A = (uint32_t)__builtin_ctz(x);
+            jA[A] = (uint32_t)rA[A]++;
+            m1[A] = m1s[A][jA[A]];
+            recs.push_back((uint8_t)m1[A]);
         }
-        for (uint32_t A = 0; A < a; ++A) {
-            const uint32_t gfa = desc.first_child[fc + A];
-            for (uint32_t x = m1s[A]; x; x &= x - 1) {
-                const uint32_t B = (uint32_t)__builtin_ctz(x), nb = gfa + B;
-                const uint64_t jB = rB[8 * A + B]++;
-                uint32_t lm = 0;
-                for (uint32_t k = 0; k < desc.num_children[nb]; ++k)
-                    lm |= desc_bit(desc, desc.first_child[nb] + k, jB) << k;
-                recs.push_back((uint8_t)lm);
+        for (uint32_t x = m2; x; x &= x - 1) {
+            const uint32_t A = (uint32_t)__builtin_ctz(x);
+            for (uint32_t y = m1[A]; y; y &= y - 1) {
+                const uint32_t B = (uint32_t)__builtin_ctz(y);
+                recs.push_back(lms[A][B][rB[8 * A + B]++]);
             }
         }
         roff[j + 1] = recs.size();
     }
+    timer.lap("pack2: masks + records");
     auto block_bytes = [&](uint64_t b, uint32_t S) {
         return roff[std::min<uint64_t>(L, (b + 1) * S)] - roff[std::min<uint64_t>(L, b * S)];
     };
@@ -242,6 +298,7 @@ bool build_pack2_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, DevN
         }
     }
     if (!S) return false;
+    timer.lap("pack2: span");
     std::vector<uint8_t> host(blocks * kPack2Block + kImagePad, 0);
     std::vector<uint8_t> spill;
     std::vector<std::pair<uint64_t, uint64_t>> spilled;  // (block, offset in spill)
@@ -263,6 +320,7 @@ bool build_pack2_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, DevN
             if (spill.size() & 1) spill.push_back(0);  // keep the u16 starts aligned
         }
     }
+    timer.lap("pack2: blocks");
     if (!spill.empty()) {
         void *ds = nullptr;
         spill.resize(spill.size() + kImagePad, 0);
@@ -279,11 +337,11 @@ bool build_pack2_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, DevN
         }
     }
     void *d = nullptr;
-    if (hipMalloc(&d, host.size()) != hipSuccess ||
-        hipMemcpy(d, host.data(), host.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    if (upload_bytes(host.data(), host.size(), &d) != hipSuccess) {
         rc = hip_fail(hipErrorOutOfMemory, "pack2 image upload");
         return true;
     }
+    timer.lap("pack2: upload");
     images.push_back(d);
     image_bytes += host.size();
     dn.kind = KIND_PACK2;
@@ -296,7 +354,9 @@ bool build_pack2_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, DevN
 
 }  // namespace
 
+
 int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
+    PhaseTimer timer;
     MBRWT_HIP(hipSetDevice(device));
     tree = Tree();
     tree.num_rows = desc.num_rows;
@@ -389,6 +449,7 @@ int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
     // super-root: its single child is the root -- or, when the root column is
     // at least half full, the root's children expanded to row positions
     // (root folding, mbrwt_internal.hpp)
+    timer.lap("validate");
     tree.folded = fold_root_enabled() && desc.num_children[0] > 0 && 2 * ones[0] >= desc.num_rows;
     if (tree.folded) {
         const uint32_t a = desc.num_children[0], fc = desc.first_child[0];
@@ -430,14 +491,63 @@ int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
                               tree.image_bytes);
         if (rc) return rc;
     }
+    timer.lap("super-root");
+    // PACK2 candidates are disjoint subtrees (a candidate's descendants are
+    // PACK/MASK8-shaped): their images are built concurrently, one host thread
+    // per candidate (at most 16 at a time)
+    struct P2 {
+        uint32_t u;
+        bool built = false;
+        int rc = MBRWT_OK;
+        DevNode dn{};
+        std::vector<void *> images;
+        uint64_t bytes = 0;
+    };
+    std::vector<P2> p2;
+    if (pack2_enabled())
+        for (uint32_t u = 0; u < N; ++u)
+            if (desc.num_children[u] && !(u == 0 && tree.folded) && pack2_candidate(desc, u)) {
+                p2.emplace_back();
+                p2.back().u = u;
+            }
+    for (size_t i0 = 0; i0 < p2.size(); i0 += 16) {
+        std::vector<std::thread> pool;
+        for (size_t i = i0; i < std::min(p2.size(), i0 + 16); ++i)
+            pool.emplace_back([&, i]() {
+                P2 &r = p2[i];
+                if (hipSetDevice(device) != hipSuccess) {
+                    r.rc = MBRWT_ERR_DEVICE;
+                    return;
+                }
+                try {
+                    r.built = build_pack2_image(desc, r.u, ones[r.u], r.dn, r.images, r.bytes, r.rc);
+                } catch (...) {
+                    r.rc = MBRWT_ERR_NOMEM;
+                }
+            });
+        for (auto &t : pool) t.join();
+    }
+    std::vector<int> p2_of(N, -1);
+    for (size_t i = 0; i < p2.size(); ++i) {  // every allocation joins the tree (freed with it)
+        tree.images.insert(tree.images.end(), p2[i].images.begin(), p2[i].images.end());
+        tree.image_bytes += p2[i].bytes;
+        if (p2[i].rc) return p2[i].rc;
+        p2_of[p2[i].u] = (int)i;
+    }
+    timer.lap("pack2 images");
     std::vector<bool> in_pack(N, false);  // MASK8 children of a KIND_PACK node: no image
     for (uint32_t u = 0; u < N; ++u) {
         const uint32_t a = desc.num_children[u];
         if (!a || (u == 0 && tree.folded) || in_pack[u]) continue;
-        if (pack2_enabled() && pack2_candidate(desc, u)) {
-            int rc = MBRWT_OK;
-            if (build_pack2_image(desc, u, ones[u], tree.nodes[u + 1], tree.images, tree.image_bytes, rc)) {
-                if (rc) return rc;
+        if (p2_of[u] >= 0) {
+            const P2 &r = p2[p2_of[u]];
+            if (r.built) {
+                DevNode &dn = tree.nodes[u + 1];
+                dn.kind = r.dn.kind;
+                dn.arity = r.dn.arity;
+                dn.stride = r.dn.stride;
+                dn.length = r.dn.length;
+                dn.base = r.dn.base;
                 for (uint32_t c = 0; c < a; ++c) {  // children: PACK-shaped records, grandchildren: MASK8 records
                     const uint32_t ch = desc.first_child[u] + c;
                     in_pack[ch] = true;
@@ -485,7 +595,10 @@ int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
         int rc = upload_image(cw, leaf, ones[u], tree.nodes[u + 1], tree.images, tree.image_bytes);
         if (rc) return rc;
     }
-    return finalize_tree(tree);
+    timer.lap("node images");
+    const int rc = finalize_tree(tree);
+    timer.lap("finalize");
+    return rc;
 }
 
 int finalize_tree(Tree &tree) {

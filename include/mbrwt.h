@@ -93,6 +93,24 @@ typedef struct mbrwt_synth_desc {
 } mbrwt_synth_desc;
 int mbrwt_create_synthetic(const mbrwt_synth_desc *desc, int device, mbrwt_ctx **out);
 
+/*
+ * Build a BRWT from its columns on the device: BRWTBottomUpBuilder::build
+ * (BRWT_builders.cpp:119-163) with the basic partitioner of the given arity
+ * (get_basic_partitioner, BRWT_builders.cpp:20-31; groups of one pass
+ * through).  compute_or and generate_subindex run as HIP kernels; the result
+ * is the image mbrwt_create would build from the same tree.  columns[j] is
+ * column j over the rows as ceil(num_rows/64) LSB-first uint64 words in host
+ * memory (bits past num_rows are ignored).  arity in [2, 64]; num_columns == 0
+ * gives the empty BRWT().
+ */
+typedef struct mbrwt_columns_desc {
+    uint64_t num_rows;
+    uint64_t num_columns;
+    const uint64_t *const *columns;
+    uint32_t arity;
+} mbrwt_columns_desc;
+int mbrwt_create_from_columns(const mbrwt_columns_desc *desc, int device, mbrwt_ctx **out);
+
 void mbrwt_destroy(mbrwt_ctx *ctx);
 
 /* ---- properties (BRWT.hpp:33-51) -------------------------------------- */

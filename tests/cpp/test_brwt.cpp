@@ -92,6 +92,33 @@ TEST(BRWT, OutOfRange) {  // the reference asserts (BRWT.cpp:27); the mirror thr
     EXPECT_THROW(m->get(0, 1), std::out_of_range);
     EXPECT_THROW(m->get_column(1), std::out_of_range);
 }
+// the same grids built from their columns by the device builder
+// (mbrwt_create_from_columns); device backend only
+static void grid_device_built(int kind) {
+    if (!g_device) return;
+    for (uint64_t n = 1; n < 20; ++n) {
+        for (size_t mcols = 1; mcols < 20; ++mcols) {
+            Columns cols(mcols, std::vector<bool>(n));
+            std::vector<std::vector<uint64_t>> words(mcols, std::vector<uint64_t>((n + 63) / 64, 0));
+            uint64_t ones = 0;
+            for (size_t j = 0; j < mcols; ++j)
+                for (uint64_t i = 0; i < n; ++i) {
+                    bool b = kind == 0 ? false : kind == 1 ? true : ((i + 2 * j) % 2) != 0;
+                    cols[j][i] = b;
+                    ones += b;
+                    if (b) words[j][i / 64] |= 1ull << (i % 64);
+                }
+            auto m = mbrwt_host::BRWTDevice::build_bottom_up(words, n, 2);
+            EXPECT_EQ(ones, m.num_relations());
+            // same shape as the reference builder's tree (the oracle's restatement)
+            EXPECT_EQ(OracleMatrix(build_oracle(cols, n, 0, 2, 0)).num_relations(), m.num_relations());
+            test_brwt(m, cols, n);
+        }
+    }
+}
+TEST(BRWT, DeviceBuilderAllZero) { grid_device_built(0); }
+TEST(BRWT, DeviceBuilderAllOne) { grid_device_built(1); }
+TEST(BRWT, DeviceBuilderAllMixed) { grid_device_built(2); }
 TEST(BRWT, BuildBottomUPAllZero) { grid(0, 0); }
 TEST(BRWT, BuildBottomUPAllOne) { grid(1, 0); }
 TEST(BRWT, BuildBottomUPAllMixed) { grid(2, 0); }

@@ -449,3 +449,57 @@ def test_pack2_refseq_shape_synthetic(oracle_mod):
     assert p2.device_bytes() != p1.device_bytes()
     rows = np.random.default_rng(11).integers(0, n, 20_000).astype(np.uint64)
     _agree(t, [p2, p1], rows, np.random.default_rng(5).integers(0, m, 6), m)
+
+
+# ---- device builder (mbrwt_create_from_columns): BRWTBottomUpBuilder::build ----
+
+def _oracle_from_words(O, words, n, m, arity):
+    return O.OracleTree(O.lib().oracle_build_from_columns(O._p64(words), n, m, 0, arity, 0))
+
+
+@pytest.mark.parametrize("n,m,d,arity", [(1, 1, 0.5, 2), (64, 3, 0.5, 2), (1000, 37, 0.05, 2), (5000, 300, 0.01, 8),
+                                         (3001, 100, 0.2, 3), (777, 130, 0.03, 64), (4096, 513, 0.004, 8)])
+def test_device_builder_matches_reference_builder(oracle_mod, n, m, d, arity):
+    """The device-built BRWT is the reference builder's tree: the same image
+    as the oracle's tree exported through mbrwt_create (byte count) and the
+    same answers to every query."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    words = O.generate_columns(n, m, d, seed=n + m)
+    W = (n + 63) // 64
+    t = _oracle_from_words(O, words, n, m, arity)
+    built = BRWTDevice.from_columns(words[: m * W].reshape(m, W), n, arity)
+    ref = BRWTDevice.from_tree(t.export())
+    assert built.device_bytes() == ref.device_bytes()
+    assert built.num_relations() == t.num_relations() and built.num_nodes() == ref.num_nodes()
+    rows = np.concatenate([np.arange(n), np.random.default_rng(1).integers(0, n, 3000)]).astype(np.uint64)
+    _agree(t, [built], rows, np.unique(np.linspace(0, m - 1, 12).astype(int)), m)
+
+
+def test_device_builder_edge_cases(oracle_mod):
+    from genome_graph_annotation_amd import BRWTDevice, _lib as L
+    empty = BRWTDevice.from_columns([], 10, 2)  # no columns: BRWT() (BRWT_builders.cpp:122-123)
+    assert empty.num_columns() == 0 and empty.num_rows() == 0
+    # garbage past num_rows is ignored
+    col = np.array([0xFFFFFFFFFFFFFFFF], dtype=np.uint64)
+    one = BRWTDevice.from_columns([col], 10, 2)
+    assert one.num_relations() == 10
+    off, cols = one.get_rows(np.arange(10, dtype=np.uint64))
+    assert list(off) == list(range(11)) and set(cols.tolist()) == {0}
+    with pytest.raises(L.MBRWTError):
+        BRWTDevice.from_columns([col], 10, 1)  # arity < 2
+
+
+def test_device_builder_c2_shape(oracle_mod):
+    """BASELINE configs[1] shape from the reference's own column generator
+    (mt19937, data_generation.cpp:20-29): 1 M x 2,652, d = 0.3 %, arity 8."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    n, m = 1_000_000, 2652
+    words = O.generate_columns(n, m, 0.003, seed=42)
+    W = (n + 63) // 64
+    t = _oracle_from_words(O, words, n, m, 8)
+    built = BRWTDevice.from_columns(words.reshape(m, W), n, 8)
+    assert built.device_bytes() == BRWTDevice.from_tree(t.export()).device_bytes()
+    rows = np.random.default_rng(2).integers(0, n, 200_000).astype(np.uint64)
+    _check_rows(t, built, rows, variants=(0,))
