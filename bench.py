@@ -95,7 +95,7 @@ def main():
     else:
         torch.cuda.set_device(local)
     from genome_graph_annotation_amd import BRWTDevice, _lib as L
-    from genome_graph_annotation_amd.dist import allgatherv_csr
+    from genome_graph_annotation_amd.dist import AllGatherV, allgatherv_csr
 
     dev_t = torch.device("cuda", local)
     t0 = time.time()
@@ -120,14 +120,33 @@ def main():
         need = e.needed
     cols_t = torch.empty(int(need * 1.02) + 1024, dtype=torch.int32, device=dev_t)
 
+    # N > 1: steps are pipelined -- batch k's all-gatherv (RCCL stream) runs
+    # while batch k+1 is traversed, so the outputs are double-buffered; drain()
+    # completes the last exchange inside the timed region
+    gather = world > 1 and not a.no_gather
+    bufs = [(off_t, cols_t)]
+    if gather:
+        bufs.append((torch.empty_like(off_t), torch.empty_like(cols_t)))
+    state = {"i": 0, "pending": None}
+
     def step():
-        n_lab = mat.get_rows_device(rows_t, off_t, cols_t, sptr)
-        if world > 1 and not a.no_gather:
-            allgatherv_csr(off_t, cols_t, n_labels=n_lab, num_columns=a.cols)
+        o, cb = bufs[state["i"] % len(bufs)]
+        state["i"] += 1
+        n_lab = mat.get_rows_device(rows_t, o, cb, sptr)
+        if gather:
+            if state["pending"] is not None:
+                state["pending"].finish()
+            state["pending"] = AllGatherV(o, cb, n_labels=n_lab, num_columns=a.cols)
         return n_lab
+
+    def drain():
+        if state["pending"] is not None:
+            state["pending"].finish()
+            state["pending"] = None
 
     for _ in range(a.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     mat.take_timing()
     mat.set_option(L.MBRWT_OPT_TIMING, 1)
@@ -137,6 +156,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         n_lab = step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -152,12 +172,13 @@ def main():
     # N > 1: the reassembled global CSR must hold this rank's slice verbatim
     # (every rank checks its own slice; the verdicts are all-reduced)
     reassembly = None
-    if world > 1 and not a.no_gather:
-        g_off, g_cols = allgatherv_csr(off_t, cols_t, n_labels=n_lab, num_columns=a.cols)
+    last_off, last_cols = bufs[(state["i"] - 1) % len(bufs)]
+    if gather:
+        g_off, g_cols = allgatherv_csr(last_off, last_cols, n_labels=n_lab, num_columns=a.cols)
         lo, hi = rank * a.batch, (rank + 1) * a.batch
         b0 = int(g_off[lo].item())
-        ok = bool(torch.equal(g_off[lo:hi + 1] - b0, off_t) and
-                  torch.equal(g_cols[b0:b0 + n_lab], cols_t[:n_lab]) and
+        ok = bool(torch.equal(g_off[lo:hi + 1] - b0, last_off) and
+                  torch.equal(g_cols[b0:b0 + n_lab], last_cols[:n_lab]) and
                   g_off.numel() == world * a.batch + 1)
         flag = torch.tensor([0 if ok else 1], dtype=torch.int64, device=dev_t)
         dist.all_reduce(flag, op=dist.ReduceOp.SUM)
@@ -186,8 +207,8 @@ def main():
 
     # GPU result of the last timed step for the parity gate
     chk = min(a.check_rows, a.batch) if a.check_rows > 0 else a.batch
-    off_h = off_t[: chk + 1].cpu().numpy().view(np.uint64)
-    cols_h = cols_t[: int(off_h[-1])].cpu().numpy().view(np.uint32)
+    off_h = last_off[: chk + 1].cpu().numpy().view(np.uint64)
+    cols_h = last_cols[: int(off_h[-1])].cpu().numpy().view(np.uint32)
 
     cpu = None
     parity = None
