@@ -188,6 +188,18 @@ int build_from_columns(const mbrwt_columns_desc &cd, int device, Tree &tree, hip
         for (size_t g0 = 0; g0 < level.size(); g0 += cd.arity) {
             const size_t g1 = std::min<size_t>(level.size(), g0 + cd.arity);
             if (g1 - g0 == 1) {
+                // a passed-through internal node keeps its row column: move it
+                // out of the previous level's parent arena, freed below
+                BNode &single = nodes[level[g0]];
+                if (!single.children.empty() && W) {
+                    uint64_t *own = reinterpret_cast<uint64_t *>(dalloc(W * sizeof(uint64_t)));
+                    if (!own) {
+                        cleanup();
+                        return hip_fail(hipErrorOutOfMemory, "builder allocation");
+                    }
+                    MBRWT_HIP(hipMemcpyAsync(own, single.rowcol, W * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+                    single.rowcol = own;
+                }
                 next.push_back(level[g0]);
                 continue;
             }

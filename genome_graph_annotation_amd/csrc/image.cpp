@@ -283,6 +283,8 @@ bool build_pack2_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, DevN
         roff[j + 1] = recs.size();
     }
     timer.lap("pack2: masks + records");
+    for (uint64_t j = 0; j < L; ++j)
+        if (roff[j + 1] - roff[j] > kPack2Block) return false;  // a record must fit a block (mbrwt_internal.hpp)
     auto block_bytes = [&](uint64_t b, uint32_t S) {
         return roff[std::min<uint64_t>(L, (b + 1) * S)] - roff[std::min<uint64_t>(L, b * S)];
     };
@@ -309,10 +311,10 @@ bool build_pack2_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, DevN
         if (bytes <= pack2_inline(S)) {
             for (uint32_t t = 0; t < S; ++t) blk[t] = (uint8_t)(S + roff[std::min<uint64_t>(L, j0 + t)] - r0);
             std::memcpy(blk + S, recs.data() + r0, bytes);
-        } else {  // start[0] = 0 marks the block; list = u16 starts, then the records
+        } else {  // start[0] = 0 marks the block; list = u16 start[S+1], then the records
             spilled.emplace_back(b, spill.size());
-            for (uint32_t t = 0; t < S; ++t) {
-                const uint16_t st = (uint16_t)(2 * S + roff[std::min<uint64_t>(L, j0 + t)] - r0);
+            for (uint32_t t = 0; t <= S; ++t) {
+                const uint16_t st = (uint16_t)(2 * (S + 1) + roff[std::min<uint64_t>(L, j0 + t)] - r0);
                 spill.push_back((uint8_t)st);
                 spill.push_back((uint8_t)(st >> 8));
             }

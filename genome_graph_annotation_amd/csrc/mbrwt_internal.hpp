@@ -75,7 +75,11 @@ __host__ __device__ inline uint32_t pack_area_byte(uint32_t o) { return 16 * (o 
 // i.e. the index bits of the whole subtree below u at j, in the reference's
 // pre-order (BRWT.cpp:45-51).  A block whose records exceed 64 - S bytes
 // holds start[0] = 0 and, in bytes 8..15, the address of a spill list:
-// u16 start[S] (relative to the list) followed by the records.  The A and B
+// u16 start[S+1] (relative to the list; start[S] = the end) followed by the
+// records.  No record is longer than 64 bytes (the fast kernel stages a
+// spilled record in a 64-byte LDS slot): the host builder declines PACK2 for
+// a node with a longer record, the generator fails loudly (it needs >= 55 of
+// a node's <= 64 grandchildren set at one position).  The A and B
 // nodes keep their records (arity, first child, labels) but have no image.
 // Sparse subtrees take S = 8 (Kingsford shape: ~4.5 record bytes per
 // position), dense ones a smaller span (RefSeq shape: ~23 bytes, S = 2).

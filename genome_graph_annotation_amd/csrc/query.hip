@@ -718,19 +718,21 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
     for (int k = 0; k < (int)kFastMaxd; ++k) jc0[k] = jc1[k] = fp[k] = 0;
     int sp = 0;
     uint32_t cnt = 0;
-    uint64_t chunk = gid;
+    // u32 chunk / slot indices: run_get_rows keeps batches below 2^31 rows
+    uint32_t chunk = (uint32_t)gid;
     uint32_t ri = 0;
-    uint64_t slot = chunk * 8;
+    uint32_t slot = chunk * 8;
     // output: the labels of a chunk's rows are packed back to back in the
     // chunk's 8*K-label region (rows with > K labels are left out for the
     // overflow pass), so the compaction is a contiguous copy per chunk
     uint32_t running = 0, chunk_total = 0;
-    uint32_t *slot_ptr = p.temp + chunk * 8 * p.K;
+    // the current row's first label in its chunk's region (recomputed, not held)
+    auto slot_ptr = [&]() -> uint32_t * { return p.temp + (uint64_t)chunk * 8 * p.K + running; };
 
     // SMALLK: K == kStageLabels, every kept label fits the stage
     auto emit = [&](uint32_t pos, uint32_t label) {
         if (pos < kStageLabels) stage[pos] = label;
-        else if (!SMALLK && pos < p.K) gst(slot_ptr + pos, label);  // past the LDS stage
+        else if (!SMALLK && pos < p.K) gst(slot_ptr() + pos, label);  // past the LDS stage
     };
 
     // rows: chunks of 8 consecutive slots per group, ids preloaded 2 per lane as
@@ -738,11 +740,11 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
     uint32_t r0 = 0, r1 = 0;
     auto clamp_row = [&](uint64_t r) -> uint32_t { return r < p.num_rows ? (uint32_t)r : 0xFFFFFFFFu; };
     auto load_chunk = [&]() {
-        const uint64_t sb = chunk * 8 + 2 * c;
+        const uint64_t sb = (uint64_t)chunk * 8 + 2 * c;
         r0 = sb < p.n ? clamp_row(gld(p.rows + sb)) : 0u;
         r1 = sb + 1 < p.n ? clamp_row(gld(p.rows + sb + 1)) : 0u;
     };
-    bool active = slot < p.n, fresh = active;  // fresh: the slot's row has not been started
+    bool active = (uint64_t)slot < p.n, fresh = active;  // fresh: the slot's row has not been started
     if (active) load_chunk();
 
     while (true) {
@@ -751,12 +753,13 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const uint32_t lim = cnt < kStageLabels ? cnt : kStageLabels;
-            for (uint32_t q = c; q < lim; q += 4) gst(slot_ptr + q, (uint32_t)stage[q]);
+            uint32_t *const dst = slot_ptr();
+            for (uint32_t q = c; q < lim; q += 4) gst(dst + q, (uint32_t)stage[q]);
             if (c == 0) {
                 gst(p.counts + slot, cnt);
                 if (cnt > p.K) {
                     const unsigned long long k = atomicAdd(&p.scalars[1], 1ull);
-                    gst(p.ovf_list + k, (uint32_t)slot);
+                    gst(p.ovf_list + k, slot);
                 }
             }
             if (cnt <= p.K) running += cnt;
@@ -766,12 +769,11 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
                 ri = 0;
                 running = 0;
                 chunk_total = 0;
-                chunk += ngroups;
-                if (chunk * 8 < p.n) load_chunk();
+                chunk += (uint32_t)ngroups;
+                if ((uint64_t)chunk * 8 < p.n) load_chunk();
             }
             slot = chunk * 8 + ri;
-            slot_ptr = p.temp + chunk * 8 * p.K + running;
-            active = slot < p.n;
+            active = (uint64_t)chunk * 8 + ri < p.n;
             fresh = active;
         }
         if (!__any(active)) break;
@@ -839,41 +841,54 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const AS_LDS uint8_t *pb = (const AS_LDS uint8_t *)pk;
-            const bool spilled = pb[0] == 0;
-            uint64_t sa = 0;
             uint32_t s = pb[t];
-            if (spilled) {  // rare: records in a spill list (bytes 8..15 = its address)
-                sa = ((uint64_t)pk[3] << 32) | pk[2];
-                s = gld_at<uint16_t>(sa + 2ull * t);
+            if (pb[0] == 0) {
+                // rare (spilled block): the position's record is copied into the
+                // group's LDS slot -- list = u16 start[S+1], then the records;
+                // builders keep every record <= 64 bytes (mbrwt_internal.hpp)
+                const uint64_t la = ((uint64_t)pk[3] << 32) | pk[2];
+                const uint32_t s0 = gld_at<uint16_t>(la + 2ull * t), len = gld_at<uint16_t>(la + 2ull * t + 2) - s0;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();  // every lane has read the list address
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                AS_LDS uint8_t *pw = (AS_LDS uint8_t *)pk;
+                for (uint32_t o = c; o < len; o += 4) pw[o] = gld_at<uint8_t>(la + s0 + o);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                s = 0;
             }
-            auto rd = [&](uint32_t o) -> uint32_t {
-                return spilled ? (uint32_t)gld_at<uint8_t>(sa + o) : (uint32_t)pb[o];
-            };
-            const uint32_t m2 = rd(s);
-            const uint32_t A0 = 2 * c;
-            const uint32_t bA0 = (m2 >> A0) & 1u, bA1 = (m2 >> (A0 + 1)) & 1u;
-            const uint32_t i0 = s + 1 + (uint32_t)__builtin_popcount(m2 & ((1u << A0) - 1u));
-            const uint32_t m10 = bA0 ? rd(i0) : 0u;
-            const uint32_t m11 = bA1 ? rd(i0 + bA0) : 0u;
-            const uint32_t n1 = (uint32_t)__builtin_popcount(m10) + (uint32_t)__builtin_popcount(m11);
-            uint32_t n1_tot;
-            const uint32_t o2 = s + 1 + (uint32_t)__builtin_popcount(m2) + quad_exclusive_sum(n1, c, n1_tot);
-            uint32_t nl = 0;
-            for (uint32_t k = 0; k < n1; ++k) nl += (uint32_t)__builtin_popcount(rd(o2 + k));
-            uint32_t ltot;
-            uint32_t pos = cnt + quad_exclusive_sum(nl, c, ltot);
             const uint32_t fc = (uint32_t)w1;
-            uint32_t o = o2;
+            // the record walk: lane c takes children 2c, 2c+1 of the node
+            auto walk = [&](auto rd) {
+                const uint32_t m2 = rd(s);
+                const uint32_t A0 = 2 * c;
+                const uint32_t bA0 = (m2 >> A0) & 1u, bA1 = (m2 >> (A0 + 1)) & 1u;
+                const uint32_t i0 = s + 1 + (uint32_t)__builtin_popcount(m2 & ((1u << A0) - 1u));
+                const uint32_t m10 = bA0 ? rd(i0) : 0u;
+                const uint32_t m11 = bA1 ? rd(i0 + bA0) : 0u;
+                const uint32_t n1 = (uint32_t)__builtin_popcount(m10) + (uint32_t)__builtin_popcount(m11);
+                uint32_t n1_tot;
+                const uint32_t o2 = s + 1 + (uint32_t)__builtin_popcount(m2) + quad_exclusive_sum(n1, c, n1_tot);
+                uint32_t nl = 0;
+#pragma nounroll
+                for (uint32_t k = 0; k < n1; ++k) nl += (uint32_t)__builtin_popcount(rd(o2 + k));
+                uint32_t ltot;
+                uint32_t pos = cnt + quad_exclusive_sum(nl, c, ltot);
+                uint32_t o = o2;
 #pragma unroll
-            for (uint32_t h = 0; h < 2; ++h) {
-                uint32_t x = h ? m11 : m10;
-                if (!x) continue;
-                const uint32_t fa = (uint32_t)lds_nodes[2 * (fc + A0 + h) + 1];  // first MASK8 child of A
-                for (; x; x &= x - 1) {
-                    const uint32_t l = (uint32_t)(lds_nodes[2 * (fa + (uint32_t)__builtin_ctz(x)) + 1] >> 32);
-                    for (uint32_t lm = rd(o++); lm; lm &= lm - 1) emit(pos++, l + (uint32_t)__builtin_ctz(lm));
+                for (uint32_t h = 0; h < 2; ++h) {
+                    uint32_t x = h ? m11 : m10;
+                    if (!x) continue;
+                    const uint32_t fa = (uint32_t)lds_nodes[2 * (fc + A0 + h) + 1];  // first MASK8 child of A
+                    for (; x; x &= x - 1) {
+                        const uint32_t l = (uint32_t)(lds_nodes[2 * (fa + (uint32_t)__builtin_ctz(x)) + 1] >> 32);
+                        for (uint32_t lm = rd(o++); lm; lm &= lm - 1) emit(pos++, l + (uint32_t)__builtin_ctz(lm));
+                    }
                 }
-            }
+                return ltot;
+            };
+            const uint32_t ltot = walk([&](uint32_t o) -> uint32_t { return pb[o]; });
             cnt += ltot;
             continue;
         }
@@ -1321,8 +1336,8 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
         set_error("query on an empty BRWT");
         return MBRWT_ERR_RANGE;
     }
-    if (n > 0xFFFFFFFFull) {
-        set_error("batch larger than 2^32 rows");
+    if (n > 0x7FFFFFF0ull) {  // u32 slot arithmetic in the kernels
+        set_error("batch larger than 2^31 rows");
         return MBRWT_ERR_UNSUPPORTED;
     }
     const uint32_t K = auto_slots(c);

@@ -349,9 +349,26 @@ __global__ __launch_bounds__(256) void k_gen_pack2(uint8_t *img, uint64_t L, uin
             }
         }
         const bool spills = size > pack2_inline(S);
-        const uint32_t list_bytes = (2 * S + size + 15) & ~15u;
+        const uint32_t list_bytes = (2 * (S + 1) + size + 15) & ~15u;
         if (pass == 0) {
             if (spills) atomicAdd(spill_ctr, (unsigned long long)list_bytes);
+            if (spills && size > kPack2Block) {  // some record may exceed 64 bytes: check each
+                for (uint32_t t = 0; t < S; ++t) {
+                    const uint64_t j = b * S + t;
+                    if (j >= L) break;
+                    uint32_t rs = 1;
+                    for (uint32_t A = 0; A < args.a; ++A) {
+                        uint32_t jA;
+                        if (!plane_bit_rank(args.uplane, args.ustride, A, j, jA)) continue;
+                        rs += 1;
+                        for (uint32_t B = 0; B < args.aarity[A]; ++B) {
+                            uint32_t jB;
+                            rs += plane_bit_rank(args.aplane[A], args.astride[A], B, jA, jB);
+                        }
+                    }
+                    if (rs > kPack2Block) atomicAdd(spill_ctr + 1, 1ull);
+                }
+            }
             continue;
         }
         uint8_t *blk = img + b * kPack2Block;
@@ -364,8 +381,8 @@ __global__ __launch_bounds__(256) void k_gen_pack2(uint8_t *img, uint64_t L, uin
                 blk[k] = 0;
                 blk[8 + k] = (uint8_t)(addr >> (8 * k));
             }
-            dst = list + 2 * S;
-            hdr = 2 * S;
+            dst = list + 2 * (S + 1);  // u16 start[S+1], then the records
+            hdr = 2 * (S + 1);
         } else {
             dst = blk + S;
             hdr = S;
@@ -373,7 +390,7 @@ __global__ __launch_bounds__(256) void k_gen_pack2(uint8_t *img, uint64_t L, uin
         uint32_t o = 0;
         for (uint32_t t = 0; t < S; ++t) {
             const uint64_t j = b * S + t;
-            if (spills) *reinterpret_cast<uint16_t *>(dst - 2 * S + 2 * t) = (uint16_t)(hdr + o);
+            if (spills) *reinterpret_cast<uint16_t *>(dst - 2 * (S + 1) + 2 * t) = (uint16_t)(hdr + o);
             else blk[t] = (uint8_t)(hdr + o);
             if (j >= L) continue;
             uint32_t m2 = 0, jA[8], m1[8];
@@ -399,6 +416,7 @@ __global__ __launch_bounds__(256) void k_gen_pack2(uint8_t *img, uint64_t L, uin
                 }
             }
         }
+        if (spills) *reinterpret_cast<uint16_t *>(dst - 2 * (S + 1) + 2 * S) = (uint16_t)(hdr + o);  // end
     }
     if (pass == 1) {
         for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off);
@@ -779,7 +797,7 @@ int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStr
     // internal nodes in BFS order: parents are generated before children
     std::vector<bool> in_pack(N, false);  // MASK8 children of a KIND_PACK node: no image
     unsigned long long *d_ctr = nullptr;
-    if (hipMalloc(&d_ctr, sizeof(unsigned long long)) != hipSuccess) return fail(MBRWT_ERR_NOMEM, "hipMalloc");
+    if (hipMalloc(&d_ctr, 2 * sizeof(unsigned long long)) != hipSuccess) return fail(MBRWT_ERR_NOMEM, "hipMalloc");
     for (uint32_t u = 0; u < N; ++u) {
         const auto &sh = shape[u];
         DevNode &dn = tree.nodes[u + 1];
@@ -882,12 +900,18 @@ int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStr
                 }
             }
             const uint64_t nb2 = (L + span - 1) / span;
-            (void)hipMemsetAsync(d_ctr, 0, sizeof(unsigned long long), s);
+            (void)hipMemsetAsync(d_ctr, 0, 2 * sizeof(unsigned long long), s);
             hipLaunchKernelGGL(k_gen_pack2, dim3(launch_grid(nb2)), dim3(256), 0, s, nullptr, L, span, args, nullptr,
                                d_ctr, d_ones, 0);
-            unsigned long long spill_bytes = 0;
-            MBRWT_HIP(hipMemcpyAsync(&spill_bytes, d_ctr, sizeof(spill_bytes), hipMemcpyDeviceToHost, s));
+            unsigned long long ctr2[2] = {0, 0};
+            MBRWT_HIP(hipMemcpyAsync(ctr2, d_ctr, sizeof(ctr2), hipMemcpyDeviceToHost, s));
             MBRWT_HIP(hipStreamSynchronize(s));
+            const unsigned long long spill_bytes = ctr2[0];
+            if (ctr2[1]) {
+                free_tmps();
+                (void)hipFree(d_ctr);
+                return fail(MBRWT_ERR_UNSUPPORTED, "synthetic: a PACK2 record longer than 64 bytes (density too high)");
+            }
             uint8_t *spill = nullptr;
             if (spill_bytes) {
                 DevNode dummy;

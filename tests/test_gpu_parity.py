@@ -385,8 +385,9 @@ def test_pack2_layout_with_spills(oracle_mod):
 
 def test_pack2_records_longer_than_a_block(oracle_mod):
     """Arity 8, 2048 columns (2048 -> 256 -> 32 -> 4 -> root): a fully set row
-    gives a 73-byte record (1 + 8 + 64 masks), longer than a block -- served
-    from the spill list."""
+    gives a 73-byte record (1 + 8 + 64 masks), longer than a block: the host
+    builder declines PACK2 for those nodes (mbrwt_internal.hpp) and the
+    results stay the oracle's."""
     O = oracle_mod
     rng = np.random.default_rng(13)
     n, m = 3000, 2048
@@ -394,7 +395,7 @@ def test_pack2_records_longer_than_a_block(oracle_mod):
     dense[[5, 1500, 1501]] = True
     t = O.OracleTree.from_dense(dense, "basic", 8)
     p2 = _dev(t)
-    assert p2.traverse_kernel() == "k_traverse_fast2/pack2"
+    assert p2.traverse_kernel() == "k_traverse_fast2"
     rows = np.concatenate([np.arange(n), rng.integers(0, n, 5000)]).astype(np.uint64)
     _agree(t, [p2], rows, [0, 7, 8, 511, 512, 2047], m)
 
@@ -503,3 +504,18 @@ def test_device_builder_c2_shape(oracle_mod):
     assert built.device_bytes() == BRWTDevice.from_tree(t.export()).device_bytes()
     rows = np.random.default_rng(2).integers(0, n, 200_000).astype(np.uint64)
     _check_rows(t, built, rows, variants=(0,))
+
+
+@pytest.mark.parametrize("m", [9, 17, 65, 129])
+def test_device_builder_pass_through_nodes(oracle_mod, m):
+    """Column counts that leave a single node in a group on several levels
+    (pass-through of internal nodes, BRWT_builders.cpp:75-77), arity 2."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    n = 3000
+    words = O.generate_columns(n, m, 0.05, seed=m)
+    W = (n + 63) // 64
+    t = _oracle_from_words(O, words, n, m, 2)
+    built = BRWTDevice.from_columns(words[: m * W].reshape(m, W), n, 2)
+    assert built.device_bytes() == BRWTDevice.from_tree(t.export()).device_bytes()
+    _check_rows(t, built, np.arange(n, dtype=np.uint64), variants=(0,))
