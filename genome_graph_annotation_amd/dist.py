@@ -19,7 +19,8 @@ RCCL has no all-gatherv, so the exchange is:
      gives the global offsets, each rank's label slice is widened into its
      place of the global label array.
 AllGatherV splits 1-2 from 3 so that a batch's exchange overlaps the next
-batch's traversal (bench.py pipelines its steps this way).
+batch's traversal (bench.py pipelines its steps this way); on GPUs the
+unpacking is queued behind the all-gather on a side stream and overlaps too.
 The same code runs on gloo (CPU tensors) for the multi-process CPU tests.
 """
 from __future__ import annotations
@@ -93,11 +94,36 @@ class AllGatherV:
             self.work = dist.all_gather_into_tensor(self.recv, send, group=group, async_op=True)
         else:
             self.work = dist.all_gather(list(self.recv.chunk(world)), send, group=group, async_op=True)
+        self.result = None
+        self.done = None
+        if dev.type == "cuda":
+            # the unpacking is queued right behind the all-gather on a side
+            # stream, so it too overlaps whatever the caller runs next
+            side = _side_stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                self.work.wait()
+                self.result = self._unpack()
+                self.done = torch.cuda.Event()
+                self.done.record(side)
+            for t in (self.send, self.recv):
+                t.record_stream(side)
 
     def finish(self):
         """Wait for the exchange and return the global CSR (offsets [N + 1]
         int64, cols [L] int32)."""
-        self.work.wait()
+        if self.done is not None:
+            torch.cuda.current_stream(self.recv.device).wait_event(self.done)
+            g_off, g_cols = self.result
+            for t in (g_off, g_cols):
+                t.record_stream(torch.cuda.current_stream(self.recv.device))
+        else:
+            self.work.wait()
+            g_off, g_cols = self._unpack()
+        self.send = self.recv = self.result = None
+        return g_off, g_cols
+
+    def _unpack(self):
         world = len(self.ns)
         dev = self.recv.device
         R = self.recv.view(world, self.per)
@@ -120,8 +146,16 @@ class AllGatherV:
         g_off = torch.zeros(N + 1, dtype=torch.int64, device=dev)
         if N:
             torch.cumsum(g_cnt, 0, out=g_off[1:])
-        self.send = self.recv = None
         return g_off, g_cols
+
+
+_SIDE = {}
+
+
+def _side_stream(dev):
+    if dev not in _SIDE:
+        _SIDE[dev] = torch.cuda.Stream(dev)
+    return _SIDE[dev]
 
 
 def allgatherv_csr(offsets: torch.Tensor, cols: torch.Tensor, n_labels=None, num_columns=None, group=None):
