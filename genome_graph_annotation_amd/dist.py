@@ -10,11 +10,10 @@ RCCL has no all-gatherv, so the exchange is:
   1. one tiny all-gather of every rank's (rows, labels) sizes (the only host
      synchronisation);
   2. ONE all_gather_into_tensor of a packed byte buffer per rank, padded to
-     the largest rank: [per-row label counts | labels].  The wire types are
-     u16 when the matrix has < 2^16 columns (a count is <= num_columns, a
-     label < num_columns) and u32 otherwise -- the Kingsford shape (2,652
-     columns) ships 2 bytes per label and per row instead of 4 + 8, i.e.
-     ~2.2x fewer bytes over xGMI than u32 labels + u64 offsets;
+     the largest rank: [per-row label counts | labels], both bit-packed at
+     ceil(log2(num_columns)) bits (mbrwt_pack_ids_device) -- the Kingsford
+     shape (2,652 columns) ships 12 bits per label and per row instead of
+     32 + 64, i.e. ~2.9x fewer bytes over xGMI than u32 labels + u64 offsets;
   3. unpacking with contiguous slice copies: one scan of the gathered counts
      gives the global offsets, each rank's label slice is widened into its
      place of the global label array.
@@ -49,10 +48,52 @@ def _round16(x: int) -> int:
     return (x + 15) // 16 * 16
 
 
-def wire_is_narrow(num_columns) -> bool:
-    """u16 wire types are exact when every count (<= num_columns) and every
-    label (< num_columns) fits 16 bits."""
-    return num_columns is not None and num_columns < (1 << 16)
+def wire_bits(num_columns):
+    """Bits per label and per row count on the wire: labels < num_columns,
+    counts <= num_columns; 32 each when num_columns is unknown."""
+    if num_columns is None:
+        return 32, 32
+    return max(1, int(num_columns - 1).bit_length()), max(1, int(num_columns).bit_length())
+
+
+def _words(n: int, bits: int) -> int:
+    return (n * bits + 31) // 32
+
+
+def _pack(values: torch.Tensor, n: int, bits: int, out_words: torch.Tensor):
+    """values (int32, >= n entries) -> out_words (int32 view of the wire):
+    value i at bits [i*bits, (i+1)*bits), LSB-first (include/mbrwt.h
+    mbrwt_pack_ids_device; numpy on CPU tensors)."""
+    if not n:
+        return
+    if values.is_cuda:
+        from . import _lib as L
+        s = torch.cuda.current_stream(values.device).cuda_stream
+        L.check(L.lib().mbrwt_pack_ids_device(values.data_ptr(), n, bits, out_words.data_ptr(), s),
+                "mbrwt_pack_ids_device")
+        return
+    import numpy as np
+    v = values[:n].numpy().view(np.uint32).astype(np.uint64)
+    bitm = ((v[:, None] >> np.arange(bits, dtype=np.uint64)) & 1).astype(np.uint8).ravel()
+    nw = _words(n, bits)
+    bitm = np.concatenate([bitm, np.zeros(nw * 32 - len(bitm), dtype=np.uint8)])
+    out_words[:nw].copy_(torch.from_numpy(np.packbits(bitm, bitorder="little").view(np.int32).copy()))
+
+
+def _unpack(words: torch.Tensor, n: int, bits: int, out_values: torch.Tensor):
+    """Inverse of _pack into out_values (int32, n entries)."""
+    if not n:
+        return
+    if words.is_cuda:
+        from . import _lib as L
+        s = torch.cuda.current_stream(words.device).cuda_stream
+        L.check(L.lib().mbrwt_unpack_ids_device(words.data_ptr(), n, bits, out_values.data_ptr(), s),
+                "mbrwt_unpack_ids_device")
+        return
+    import numpy as np
+    b = np.unpackbits(words.contiguous().numpy().view(np.uint8), bitorder="little")[: n * bits].reshape(n, bits)
+    v = (b.astype(np.uint64) << np.arange(bits, dtype=np.uint64)).sum(axis=1).astype(np.uint32)
+    out_values[:n].copy_(torch.from_numpy(v.view(np.int32)))
 
 
 class AllGatherV:
@@ -75,19 +116,16 @@ class AllGatherV:
         table = all_sizes.view(world, 2).cpu().tolist()
         self.ns, self.ls = [t[0] for t in table], [t[1] for t in table]
         max_n, max_l = max(self.ns), max(self.ls)
-        self.num_columns = num_columns
-        self.narrow = wire_is_narrow(num_columns)
-        self.wdt = torch.int16 if self.narrow else torch.int32
-        wb = 2 if self.narrow else 4
-        self.cnt_bytes = _round16(max(1, max_n) * wb)
-        self.per = self.cnt_bytes + _round16(max(1, max_l) * wb)
-        # pack: counts (offsets deltas) then labels, in the wire type (int64 ->
-        # int16 keeps the low 16 bits: exact for values < 2^16, read back & 0xFFFF)
+        self.bits_l, self.bits_c = wire_bits(num_columns)
+        self.cnt_bytes = _round16(max(1, _words(max_n, self.bits_c)) * 4)
+        self.per = self.cnt_bytes + _round16(max(1, _words(max_l, self.bits_l)) * 4)
+        # pack: row counts (offsets deltas), then labels, bit-packed
         send = torch.empty(self.per, dtype=torch.uint8, device=dev)
         if n_r:
-            send[:self.cnt_bytes].view(self.wdt)[:n_r].copy_(offsets[1:] - offsets[:-1])
+            cnt = (offsets[1:] - offsets[:-1]).to(torch.int32)
+            _pack(cnt, n_r, self.bits_c, send[:self.cnt_bytes].view(torch.int32))
         if l_r:
-            send[self.cnt_bytes:].view(self.wdt)[:l_r].copy_(cols[:l_r])
+            _pack(cols, l_r, self.bits_l, send[self.cnt_bytes:].view(torch.int32))
         self.recv = torch.empty(world * self.per, dtype=torch.uint8, device=dev)
         self.send = send  # kept alive until the exchange is done
         if dist.get_backend(group) == "nccl":
@@ -129,23 +167,17 @@ class AllGatherV:
         R = self.recv.view(world, self.per)
         # unpack: global offsets by one scan over the ranks' counts in rank order
         N, L = sum(self.ns), sum(self.ls)
-        g_cnt = torch.empty(N, dtype=torch.int64, device=dev)
+        g_cnt = torch.empty(max(1, N), dtype=torch.int32, device=dev)
         g_cols = torch.empty(L, dtype=torch.int32, device=dev)
         rb = lb = 0
         for r in range(world):
-            if self.ns[r]:
-                g_cnt[rb:rb + self.ns[r]].copy_(R[r, :self.cnt_bytes].view(self.wdt)[:self.ns[r]])
-            if self.ls[r]:
-                g_cols[lb:lb + self.ls[r]].copy_(R[r, self.cnt_bytes:].view(self.wdt)[:self.ls[r]])
+            _unpack(R[r, :self.cnt_bytes].view(torch.int32), self.ns[r], self.bits_c, g_cnt[rb:])
+            _unpack(R[r, self.cnt_bytes:].view(torch.int32), self.ls[r], self.bits_l, g_cols[lb:])
             rb += self.ns[r]
             lb += self.ls[r]
-        if self.narrow:  # int16 sign-extended on the way back: restore the u16 values
-            g_cnt.bitwise_and_(0xFFFF)
-            if self.num_columns > (1 << 15):
-                g_cols.bitwise_and_(0xFFFF)
         g_off = torch.zeros(N + 1, dtype=torch.int64, device=dev)
         if N:
-            torch.cumsum(g_cnt, 0, out=g_off[1:])
+            torch.cumsum(g_cnt[:N], 0, dtype=torch.int64, out=g_off[1:])
         return g_off, g_cols
 
 
@@ -163,6 +195,6 @@ def allgatherv_csr(offsets: torch.Tensor, cols: torch.Tensor, n_labels=None, num
     cols: int32 [>= offsets[-1]]) into the global CSR of the concatenated
     batch, on every rank.  `n_labels` (= offsets[-1], if the caller already
     has it on the host) saves a device read; `num_columns` (the same on every
-    rank) enables the u16 wire format.  Returns (offsets [N + 1] int64,
+    rank) sets the wire's bit width.  Returns (offsets [N + 1] int64,
     cols [L] int32)."""
     return AllGatherV(offsets, cols, n_labels, num_columns, group).finish()

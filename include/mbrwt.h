@@ -176,6 +176,18 @@ int mbrwt_count_work_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, 
                             uint64_t *sum_labels, void *stream);
 
 /* Options (mbrwt_set_option). */
+/* ---- multi-GPU exchange helpers --------------------------------------- */
+/*
+ * Bit-packing of n values < 2^bits (bits in 1..32) into ceil(n*bits/32) u32
+ * words (value i at bits [i*bits, (i+1)*bits), LSB-first), and back; device
+ * buffers, launched on `stream`.  The all-gatherv that reassembles a sharded
+ * batch's CSR (genome_graph_annotation_amd/dist.py) ships labels and row
+ * counts at ceil(log2(num_columns)) bits with these.  No reference
+ * counterpart (the reference has no multi-GPU path).
+ */
+int mbrwt_pack_ids_device(const uint32_t *d_values, uint64_t n, uint32_t bits, uint32_t *d_words, void *stream);
+int mbrwt_unpack_ids_device(const uint32_t *d_words, uint64_t n, uint32_t bits, uint32_t *d_values, void *stream);
+
 #define MBRWT_OPT_TIMING 1       /* 1: time the traversal kernel with HIP events */
 #define MBRWT_OPT_SLOT_LABELS 2  /* per-row label slots of the fast path (0 = auto) */
 #define MBRWT_OPT_KERNEL 4       /* traversal kernel (A/B measurement): 0 default (k_traverse_fast2 where

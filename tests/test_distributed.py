@@ -48,9 +48,9 @@ def _worker(rank, world, port, n_batch, q, num_columns=None, m=300):
 
 
 @pytest.mark.parametrize("world,n_batch,num_columns,m", [
-    (2, 10_001, None, 300),      # u32 wire
-    (2, 10_001, 300, 300),       # u16 wire
-    (3, 4_001, 40_000, 40_000),  # u16 wire, labels >= 2^15 (sign bit on the wire)
+    (2, 10_001, None, 300),      # 32-bit wire
+    (2, 10_001, 300, 300),       # 9-bit wire (labels < 300, counts <= 300)
+    (3, 4_001, 40_000, 40_000),  # 16-bit wire
     (2, 1, 300, 300),
     (3, 7, None, 300),
     (3, 2, 300, 300),            # a rank with an empty slice
@@ -78,3 +78,18 @@ def test_shard_bounds_cover_batch():
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def test_wire_bit_packing_roundtrip():
+    """dist.py's CPU bit-packing (the format of mbrwt_pack_ids_device) round-trips
+    at every width, values spanning word boundaries."""
+    from genome_graph_annotation_amd.dist import _pack, _unpack, _words
+    rng = np.random.default_rng(5)
+    for bits in (1, 3, 7, 12, 16, 17, 31, 32):
+        n = 1000
+        v = rng.integers(0, 1 << bits, n, dtype=np.uint64).astype(np.uint32)
+        words = torch.zeros(_words(n, bits) + 1, dtype=torch.int32)
+        _pack(torch.from_numpy(v.view(np.int32)), n, bits, words)
+        out = torch.empty(n, dtype=torch.int32)
+        _unpack(words, n, bits, out)
+        assert np.array_equal(out.numpy().view(np.uint32), v)

@@ -519,3 +519,25 @@ def test_device_builder_pass_through_nodes(oracle_mod, m):
     built = BRWTDevice.from_columns(words[: m * W].reshape(m, W), n, 2)
     assert built.device_bytes() == BRWTDevice.from_tree(t.export()).device_bytes()
     _check_rows(t, built, np.arange(n, dtype=np.uint64), variants=(0,))
+
+
+def test_pack_ids_kernels_match_the_wire_format():
+    """mbrwt_pack_ids_device / mbrwt_unpack_ids_device (the all-gatherv's wire
+    format) against dist.py's CPU reference implementation."""
+    import torch
+    from genome_graph_annotation_amd.dist import _pack, _unpack, _words
+    rng = np.random.default_rng(6)
+    for bits in (1, 5, 12, 16, 23, 32):
+        for n in (1, 31, 32, 33, 100_003):
+            v = rng.integers(0, 1 << bits, n, dtype=np.uint64).astype(np.uint32)
+            cpu_words = torch.zeros(_words(n, bits), dtype=torch.int32)
+            _pack(torch.from_numpy(v.view(np.int32)), n, bits, cpu_words)
+            g = torch.from_numpy(v.view(np.int32)).cuda()
+            gw = torch.zeros(_words(n, bits) + 1, dtype=torch.int32, device="cuda")
+            _pack(g, n, bits, gw)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(gw[: _words(n, bits)].cpu().numpy(), cpu_words.numpy())
+            out = torch.empty(n, dtype=torch.int32, device="cuda")
+            _unpack(gw, n, bits, out)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), v)
