@@ -32,6 +32,23 @@ METRIC = "get_rows()/s on BinRel-WT(sdsl), 1B×3,173 d=3.8% (BASELINE configs[4]
 HBM_PEAK_GBS = 8000.0
 
 
+def committed_traffic(cfg):
+    """Per-launch HBM traffic of k_wt_decode from the committed PMC summary of
+    this workload (profiles/*/traffic_k_wt_decode*.json, tools/pmc_traffic.py),
+    or None."""
+    import glob
+    hit = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic_k_wt_decode*.json"))):
+        try:
+            with open(path) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if {k: str(v) for k, v in cfg.items()} == {k: str(v) for k, v in t.get("config", {}).items()}:
+            hit = (t["traffic_bytes"], os.path.relpath(path, ROOT))
+    return hit
+
+
 def log(msg):
     print(f"[bench_wt] {msg}", file=sys.stderr, flush=True)
 
@@ -128,6 +145,8 @@ def main():
                          f"host build {gen_s:.0f} s)"}
         del ref
 
+    traffic = committed_traffic({"rows": a.rows, "cols": a.cols, "density": a.density, "batch": a.batch,
+                                 "kernel_name": "k_wt_decode"})
     line = {
         "metric": METRIC, "value": a.batch * a.steps / elapsed, "unit": "rows/s", "n_gpus": 1,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
@@ -138,7 +157,9 @@ def main():
                    "structure_bytes": mat.device_bytes(), "relations": mat.num_relations(),
                    "setup_s": round(setup_s, 1)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_wt_decode",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None if traffic is None else traffic[0],
+                     "traffic_source": None if traffic is None else traffic[1] + " (rocprofv3 PMC; per launch)",
+                     "kernel": "k_wt_decode",
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
                      "labels_per_row": n_lab / a.batch, "levels": w, "digit_levels": (w + 1) // 2},
         "cpu_baseline": cpu,
