@@ -193,6 +193,42 @@ class BRWTDevice:
         L.check(L.lib().mbrwt_count_labels_device(self._h, rows_t.data_ptr(), rows_t.numel(), counts_t.data_ptr(),
                                                   stream), "mbrwt_count_labels_device")
 
+    def get_labels_batch_device(self, rows_t, read_off_t, presence_ratio, lab_off_t, labels_t, stream=None):
+        """get_labels(indices, presence_ratio) for many reads (include/mbrwt.h
+        mbrwt_get_labels_batch_device); torch device tensors; returns the
+        label count (raises MBRWTError with .needed on MBRWT_ERR_CAPACITY)."""
+        need = C.c_uint64(0)
+        st = L.lib().mbrwt_get_labels_batch_device(
+            self._h, rows_t.data_ptr(), rows_t.numel(), read_off_t.data_ptr(), read_off_t.numel() - 1,
+            float(presence_ratio), lab_off_t.data_ptr(), labels_t.data_ptr() if labels_t is not None else None,
+            labels_t.numel() if labels_t is not None else 0, C.byref(need), stream)
+        if st == L.MBRWT_ERR_CAPACITY:
+            e = L.MBRWTError(st, "mbrwt_get_labels_batch_device")
+            e.needed = int(need.value)
+            raise e
+        L.check(st, "mbrwt_get_labels_batch_device")
+        return int(need.value)
+
+    def get_labels_batch(self, rows, read_offsets, presence_ratio):
+        """Host convenience over get_labels_batch_device: numpy in, (label
+        offsets u64, labels u32) out."""
+        import torch
+        dev = torch.device("cuda", L.lib().mbrwt_device(self._h))
+        rt = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.uint64).view(np.int64)).to(dev)
+        ot = torch.from_numpy(np.ascontiguousarray(read_offsets, dtype=np.uint64).view(np.int64)).to(dev)
+        lo = torch.empty(len(read_offsets), dtype=torch.int64, device=dev)
+        s = torch.cuda.current_stream(dev).cuda_stream
+        try:
+            n = self.get_labels_batch_device(rt, ot, presence_ratio, lo, None, s)
+        except L.MBRWTError as e:
+            if e.status != L.MBRWT_ERR_CAPACITY:
+                raise
+            n = e.needed
+        lt = torch.empty(max(1, n), dtype=torch.int32, device=dev)
+        self.get_labels_batch_device(rt, ot, presence_ratio, lo, lt, s)
+        torch.cuda.synchronize(dev)
+        return lo.cpu().numpy().view(np.uint64), lt[:n].cpu().numpy().view(np.uint32)
+
     def count_work_device(self, rows_t, stream=None):
         v = C.c_uint64(0)
         lab = C.c_uint64(0)

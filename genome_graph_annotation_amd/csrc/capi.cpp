@@ -55,7 +55,8 @@ static void release(Ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     free_tree(c->tree);
-    for (Workspace *w : {&c->ws_temp, &c->ws_counts, &c->ws_ovf, &c->ws_scan, &c->ws_rows, &c->ws_out, &c->ws_sort})
+    for (Workspace *w : {&c->ws_temp, &c->ws_counts, &c->ws_ovf, &c->ws_scan, &c->ws_rows, &c->ws_out, &c->ws_sort,
+                         &c->ws_cls_off, &c->ws_cls_cols})
         if (w->buf) (void)hipFree(w->buf);
     if (c->d_nodes) (void)hipFree(c->d_nodes);
     if (c->d_cnodes) (void)hipFree(c->d_cnodes);
@@ -312,6 +313,27 @@ int mbrwt_count_labels_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n
     std::lock_guard<std::mutex> lk(c.mu);
     MBRWT_HIP(hipSetDevice(c.device));
     return run_count_labels(c, d_rows, n, d_counts, reinterpret_cast<hipStream_t>(stream));
+}
+
+int mbrwt_get_labels_batch_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n_rows,
+                                  const uint64_t *d_read_offsets, uint64_t n_reads, double presence_ratio,
+                                  uint64_t *d_label_offsets, uint32_t *d_labels, uint64_t labels_cap,
+                                  uint64_t *labels_needed, void *stream) {
+    if (!ctx || (n_rows && !d_rows) || !d_read_offsets || !d_label_offsets) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    try {
+        MBRWT_HIP(hipSetDevice(c.device));
+        return run_get_labels_batch(c, d_rows, n_rows, d_read_offsets, n_reads, presence_ratio, d_label_offsets,
+                                    d_labels, d_labels ? labels_cap : 0, labels_needed,
+                                    reinterpret_cast<hipStream_t>(stream));
+    } catch (...) {
+        set_error("unexpected exception in mbrwt_get_labels_batch_device");
+        return MBRWT_ERR_INVALID;
+    }
 }
 
 int mbrwt_count_work_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, uint64_t *sum_visits,

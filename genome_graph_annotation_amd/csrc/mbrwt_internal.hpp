@@ -187,6 +187,7 @@ struct Ctx {
     // reusable device workspace (grown on demand, never inside a timed call
     // once warmed up)
     Workspace ws_temp, ws_counts, ws_ovf, ws_scan, ws_rows, ws_out, ws_sort;
+    Workspace ws_cls_off, ws_cls_cols;  // get_labels batch: the rows' CSR
     uint64_t *h_scalars = nullptr;      // pinned: [0] total, [1] overflow count, [2] error
     uint64_t *d_scalars = nullptr;      // device twin
 
@@ -245,6 +246,10 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
                  uint64_t *needed, hipStream_t s);
 int run_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n, uint8_t *d_out, hipStream_t s);
 int run_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts, hipStream_t s);
+// batched get_labels(indices, presence_ratio) (classify.hip)
+int run_get_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const uint64_t *d_read_off, uint64_t n_reads,
+                         double ratio, uint64_t *d_lab_off, uint32_t *d_labels, uint64_t cap, uint64_t *needed,
+                         hipStream_t s);
 int run_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s);
 
 }  // namespace mbrwt

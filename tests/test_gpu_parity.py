@@ -541,3 +541,51 @@ def test_pack_ids_kernels_match_the_wire_format():
             _unpack(gw, n, bits, out)
             torch.cuda.synchronize()
             np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), v)
+
+
+# ---- batched get_labels(indices, presence_ratio): the classify consumer (§8f row 2) ----
+
+def _ref_get_labels(off_o, cols_o, read_offsets, m, ratio):
+    """annotate_static.cpp:71-94 over the oracle's rows (std::ceil in double)."""
+    import math
+    out_off, out = [0], []
+    for r in range(len(read_offsets) - 1):
+        a, b = int(read_offsets[r]), int(read_offsets[r + 1])
+        cnt = np.bincount(cols_o[off_o[a]:off_o[b]], minlength=m)
+        thr = 1 if ratio == 0 else math.ceil((b - a) * ratio)
+        labs = np.nonzero((cnt > 0) & (cnt >= thr))[0]
+        out.extend(labs.tolist())
+        out_off.append(len(out))
+    return np.array(out_off, dtype=np.uint64), np.array(out, dtype=np.uint32)
+
+
+@pytest.mark.parametrize("ratio", [0.0, 0.1, 0.5, 1.0])
+def test_get_labels_batch_matches_reference_semantics(oracle_mod, ratio):
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    n, m = 200_000, 2652
+    t = O.OracleTree.topdown(n, m, 0.003, 8, 21)
+    d = BRWTDevice.synthetic(n, m, 0.003, 8, 21)
+    rng = np.random.default_rng(7)
+    lens = rng.integers(0, 60, 3000)  # reads of 0..59 k-mer rows, some empty
+    read_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    # a read's k-mers hit neighbouring rows often: draw around a per-read anchor
+    anchors = rng.integers(0, n - 100, len(lens))
+    rows = np.concatenate([a + rng.integers(0, 100, k) for a, k in zip(anchors, lens)]).astype(np.uint64)
+    off_o, cols_o = t.get_rows(rows)
+    want_off, want = _ref_get_labels(off_o, cols_o, read_off, m, ratio)
+    got_off, got = d.get_labels_batch(rows, read_off, ratio)
+    np.testing.assert_array_equal(got_off, want_off)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_get_labels_batch_errors(oracle_mod):
+    from genome_graph_annotation_amd import BRWTDevice, _lib as L
+    d = BRWTDevice.synthetic(1000, 100, 0.05, 8, 3)
+    rows = np.arange(10, dtype=np.uint64)
+    with pytest.raises(L.MBRWTError):
+        d.get_labels_batch(rows, np.array([0, 10], dtype=np.uint64), 1.5)  # an assert in the reference
+    with pytest.raises(L.MBRWTError):
+        d.get_labels_batch(np.array([5000], dtype=np.uint64), np.array([0, 1], dtype=np.uint64), 0.0)  # row range
+    off, labs = d.get_labels_batch(rows, np.array([0, 0, 10], dtype=np.uint64), 0.0)  # an empty read
+    assert off[0] == 0 and off[1] == 0 and off[2] == len(labs)
