@@ -210,24 +210,26 @@ class BRWTDevice:
         return int(need.value)
 
     def get_labels_batch(self, rows, read_offsets, presence_ratio):
-        """Host convenience over get_labels_batch_device: numpy in, (label
-        offsets u64, labels u32) out."""
-        import torch
-        dev = torch.device("cuda", L.lib().mbrwt_device(self._h))
-        rt = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.uint64).view(np.int64)).to(dev)
-        ot = torch.from_numpy(np.ascontiguousarray(read_offsets, dtype=np.uint64).view(np.int64)).to(dev)
-        lo = torch.empty(len(read_offsets), dtype=torch.int64, device=dev)
-        s = torch.cuda.current_stream(dev).cuda_stream
-        try:
-            n = self.get_labels_batch_device(rt, ot, presence_ratio, lo, None, s)
-        except L.MBRWTError as e:
-            if e.status != L.MBRWT_ERR_CAPACITY:
-                raise
-            n = e.needed
-        lt = torch.empty(max(1, n), dtype=torch.int32, device=dev)
-        self.get_labels_batch_device(rt, ot, presence_ratio, lo, lt, s)
-        torch.cuda.synchronize(dev)
-        return lo.cpu().numpy().view(np.uint64), lt[:n].cpu().numpy().view(np.uint32)
+        """Host-buffer form (include/mbrwt.h mbrwt_get_labels_batch): numpy in,
+        (label offsets u64 [n_reads+1], labels u32) out."""
+        lib = L.lib()
+        rows = np.ascontiguousarray(rows, dtype=np.uint64)
+        ro = np.ascontiguousarray(read_offsets, dtype=np.uint64)
+        if ro.size == 0:
+            raise ValueError("read_offsets needs n_reads + 1 entries")
+        lo = np.zeros(ro.size, dtype=np.uint64)
+        need = C.c_uint64(0)
+        cap = max(16, 4 * rows.size)
+        while True:
+            labs = np.zeros(cap, dtype=np.uint32)
+            st = lib.mbrwt_get_labels_batch(self._h, _p(rows, C.c_uint64), rows.size, _p(ro, C.c_uint64),
+                                            ro.size - 1, float(presence_ratio), _p(lo, C.c_uint64),
+                                            _p(labs, C.c_uint32), cap, C.byref(need))
+            if st == L.MBRWT_ERR_CAPACITY:
+                cap = int(need.value)
+                continue
+            L.check(st, "mbrwt_get_labels_batch")
+            return lo, labs[: need.value]
 
     def count_work_device(self, rows_t, stream=None):
         v = C.c_uint64(0)

@@ -113,6 +113,31 @@ class StaticBinRelAnnotator {
         return filtered;
     }
 
+    // get_labels(indices, presence_ratio) for a batch of reads (the classify
+    // loop over reads, annotated_dbg.cpp:88-110): one device call for all
+    // reads when the matrix is a BRWTDevice, else one get_labels per read
+    std::vector<VLabels> get_labels_batch(const std::vector<std::vector<Index>> &reads,
+                                          double presence_ratio) const {
+        std::vector<VLabels> out(reads.size());
+        const auto *dev = dynamic_cast<const BRWTDevice *>(matrix_.get());
+        if (!dev) {
+            for (size_t r = 0; r < reads.size(); ++r) out[r] = get_labels(reads[r], presence_ratio);
+            return out;
+        }
+        assert(presence_ratio >= 0 && presence_ratio <= 1);
+        std::vector<Index> rows;
+        std::vector<uint64_t> read_off{0}, lab_off;
+        for (const auto &read : reads) {
+            rows.insert(rows.end(), read.begin(), read.end());
+            read_off.push_back(rows.size());
+        }
+        std::vector<uint32_t> codes;
+        dev->get_labels_batch_csr(rows, read_off, presence_ratio, &lab_off, &codes);
+        for (size_t r = 0; r < reads.size(); ++r)
+            for (uint64_t i = lab_off[r]; i < lab_off[r + 1]; ++i) out[r].push_back(label_encoder_.decode(codes[i]));
+        return out;
+    }
+
     // annotate.cpp:57-83 (std::sort: ties in unspecified order, as in the reference)
     std::vector<std::pair<Label, size_t>> get_top_labels(const std::vector<Index> &indices,
                                                          size_t num_top = static_cast<size_t>(-1)) const {

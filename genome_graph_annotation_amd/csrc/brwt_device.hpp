@@ -140,6 +140,36 @@ class BRWTDevice : public BinaryMatrix {
         return out;
     }
 
+    // StaticBinRelAnnotator::get_labels(indices, presence_ratio)
+    // (annotate_static.cpp:71-94) for many reads in one call: read r =
+    // rows[read_offsets[r] .. read_offsets[r+1]); label_offsets[reads+1] and
+    // the ascending label codes of each read (mbrwt_get_labels_batch)
+    void get_labels_batch_csr(const std::vector<Row> &rows, const std::vector<uint64_t> &read_offsets,
+                              double presence_ratio, std::vector<uint64_t> *label_offsets,
+                              std::vector<uint32_t> *labels) const {
+        if (read_offsets.empty()) throw std::invalid_argument("read_offsets needs n_reads + 1 entries");
+        const uint64_t n_reads = read_offsets.size() - 1;
+        label_offsets->assign(read_offsets.size(), 0);
+        labels->clear();
+        if (!ctx_) {
+            if (!rows.empty()) throw std::out_of_range("get_labels on an empty BRWT");
+            return;
+        }
+        uint64_t cap = std::max<uint64_t>(16, 4 * rows.size()), need = 0;
+        for (;;) {
+            labels->resize(cap);
+            int st = mbrwt_get_labels_batch(ctx_.get(), rows.data(), rows.size(), read_offsets.data(), n_reads,
+                                            presence_ratio, label_offsets->data(), labels->data(), cap, &need);
+            if (st == MBRWT_ERR_CAPACITY) {
+                cap = need;
+                continue;
+            }
+            check_status(st, "BRWTDevice::get_labels_batch");
+            labels->resize(need);
+            return;
+        }
+    }
+
     // CSR form: offsets[rows.size()+1], cols in the reference's per-row order
     void get_rows_csr(const std::vector<Row> &rows, std::vector<uint64_t> *offsets,
                       std::vector<uint32_t> *cols) const {

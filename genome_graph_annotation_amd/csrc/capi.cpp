@@ -336,6 +336,45 @@ int mbrwt_get_labels_batch_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64
     }
 }
 
+int mbrwt_get_labels_batch(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n_rows, const uint64_t *read_offsets,
+                           uint64_t n_reads, double presence_ratio, uint64_t *label_offsets, uint32_t *labels,
+                           uint64_t labels_cap, uint64_t *labels_needed) {
+    if (!ctx || (n_rows && !rows) || !read_offsets || !label_offsets) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    try {
+        MBRWT_HIP(hipSetDevice(c.device));
+        int rc;
+        // rows | read offsets | label offsets, one host-path workspace
+        if ((rc = ensure(c.ws_rows, (n_rows + 2 * (n_reads + 1)) * sizeof(uint64_t)))) return rc;
+        uint64_t *d_rows = reinterpret_cast<uint64_t *>(c.ws_rows.buf);
+        uint64_t *d_roff = d_rows + n_rows;
+        uint64_t *d_loff = d_roff + n_reads + 1;
+        if (n_rows) MBRWT_HIP(hipMemcpyAsync(d_rows, rows, n_rows * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+        MBRWT_HIP(hipMemcpyAsync(d_roff, read_offsets, (n_reads + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                                 c.stream));
+        if ((rc = ensure(c.ws_out, std::max<uint64_t>(labels_cap, 1) * sizeof(uint32_t)))) return rc;
+        uint64_t needed = 0;
+        rc = run_get_labels_batch(c, d_rows, n_rows, d_roff, n_reads, presence_ratio, d_loff,
+                                  reinterpret_cast<uint32_t *>(c.ws_out.buf), labels ? labels_cap : 0, &needed,
+                                  c.stream);
+        if (labels_needed) *labels_needed = needed;
+        if (rc) return rc;
+        MBRWT_HIP(hipMemcpyAsync(label_offsets, d_loff, (n_reads + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                 c.stream));
+        if (needed)
+            MBRWT_HIP(hipMemcpyAsync(labels, c.ws_out.buf, needed * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+        MBRWT_HIP(hipStreamSynchronize(c.stream));
+        return MBRWT_OK;
+    } catch (...) {
+        set_error("unexpected exception in mbrwt_get_labels_batch");
+        return MBRWT_ERR_INVALID;
+    }
+}
+
 int mbrwt_count_work_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, uint64_t *sum_visits,
                             uint64_t *sum_labels, void *stream) {
     if (!ctx || (n && !d_rows)) {

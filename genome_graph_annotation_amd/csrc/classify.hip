@@ -23,7 +23,7 @@ constexpr uint32_t kClsThreads = 256;
 constexpr uint32_t kClsMaxColumns = 15360;  // LDS histogram of u32 counters (60 KB)
 
 __global__ __launch_bounds__(kClsThreads) void k_read_labels(const uint64_t *__restrict__ read_off, uint64_t n_reads,
-                                                             const uint64_t *__restrict__ row_csr,
+                                                             uint64_t n_rows, const uint64_t *__restrict__ row_csr,
                                                              const uint32_t *__restrict__ cols, uint32_t m,
                                                              double ratio, uint64_t *__restrict__ counts_or_offsets,
                                                              uint32_t *__restrict__ out, int pass) {
@@ -36,6 +36,15 @@ __global__ __launch_bounds__(kClsThreads) void k_read_labels(const uint64_t *__r
         for (uint32_t i = t; i < m; i += kClsThreads) hist[i] = 0;
         __syncthreads();
         const uint64_t rs = gld(read_off + r), re = gld(read_off + r + 1);
+        if (rs > re || re > n_rows || (r == 0 && rs != 0) || (r + 1 == n_reads && re != n_rows)) {
+            // malformed read offsets: flag (pass 0 only runs over them) and skip
+            if (t == 0) {
+                gst(counts_or_offsets + r, (uint64_t)0);
+                gst(counts_or_offsets + n_reads, (uint64_t)1);
+            }
+            __syncthreads();
+            continue;
+        }
         const uint64_t l0 = gld(row_csr + rs), l1 = gld(row_csr + re);
         for (uint64_t i = l0 + t; i < l1; i += kClsThreads) atomicAdd(&hist[gld(cols + i)], 1u);
         __syncthreads();
@@ -78,6 +87,10 @@ int run_get_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const 
         set_error("get_labels batch: more than 15360 columns is not supported by this build");
         return MBRWT_ERR_UNSUPPORTED;
     }
+    if (!n_reads && n_rows) {  // the one offset would have to be both 0 and n_rows
+        set_error("read offsets must ascend from 0 to n_rows");
+        return MBRWT_ERR_INVALID;
+    }
     int rc;
     // 1. the labels of every row of every read
     if ((rc = ensure(c.ws_cls_off, (n_rows + 1) * sizeof(uint64_t)))) return rc;
@@ -100,19 +113,26 @@ int run_get_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const 
     const uint32_t *d_cols = reinterpret_cast<const uint32_t *>(c.ws_cls_cols.buf);
     const size_t lds = std::max<uint64_t>(m, 1) * sizeof(uint32_t);
     // 2. per-read counts, inclusive scan -> d_lab_off[1..n_reads]
-    if ((rc = ensure(c.ws_sort, n_reads * sizeof(uint64_t)))) return rc;
+    //    (d_cnt[n_reads] = the malformed-offsets flag)
+    if ((rc = ensure(c.ws_sort, (n_reads + 1) * sizeof(uint64_t)))) return rc;
     uint64_t *d_cnt = reinterpret_cast<uint64_t *>(c.ws_sort.buf);
-    hipLaunchKernelGGL(k_read_labels, dim3(grid_of(n_reads)), dim3(kClsThreads), lds, s, d_read_off, n_reads, d_off,
-                       d_cols, (uint32_t)m, ratio, d_cnt, nullptr, 0);
+    MBRWT_HIP(hipMemsetAsync(d_cnt + n_reads, 0, sizeof(uint64_t), s));
+    hipLaunchKernelGGL(k_read_labels, dim3(grid_of(n_reads)), dim3(kClsThreads), lds, s, d_read_off, n_reads, n_rows,
+                       d_off, d_cols, (uint32_t)m, ratio, d_cnt, nullptr, 0);
     MBRWT_HIP(hipGetLastError());
     MBRWT_HIP(hipMemsetAsync(d_lab_off, 0, sizeof(uint64_t), s));
     size_t scan_bytes = 0;
     MBRWT_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, d_cnt, d_lab_off + 1, (int)n_reads, s));
     if ((rc = ensure(c.ws_scan, scan_bytes + 16))) return rc;
     MBRWT_HIP(hipcub::DeviceScan::InclusiveSum(c.ws_scan.buf, scan_bytes, d_cnt, d_lab_off + 1, (int)n_reads, s));
-    uint64_t total = 0;
+    uint64_t total = 0, bad = 0;
     MBRWT_HIP(hipMemcpyAsync(&total, d_lab_off + n_reads, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    MBRWT_HIP(hipMemcpyAsync(&bad, d_cnt + n_reads, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     MBRWT_HIP(hipStreamSynchronize(s));
+    if (bad) {
+        set_error("read offsets must ascend from 0 to n_rows");
+        return MBRWT_ERR_INVALID;
+    }
     if (needed) *needed = total;
     if (total > cap || (total && !d_labels)) {
         set_error("label buffer too small (see labels_needed)");
@@ -121,7 +141,7 @@ int run_get_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const 
     // 3. the labels, ascending per read
     if (total) {
         hipLaunchKernelGGL(k_read_labels, dim3(grid_of(n_reads)), dim3(kClsThreads), lds, s, d_read_off, n_reads,
-                           d_off, d_cols, (uint32_t)m, ratio, d_lab_off, d_labels, 1);
+                           n_rows, d_off, d_cols, (uint32_t)m, ratio, d_lab_off, d_labels, 1);
         MBRWT_HIP(hipGetLastError());
     }
     return MBRWT_OK;

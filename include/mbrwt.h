@@ -163,6 +163,9 @@ int mbrwt_get_column_device(mbrwt_ctx *ctx, uint64_t column, uint64_t *d_rows, u
  * the device: counts[c] (num_columns uint64, zeroed by the call) = number of
  * rows among d_rows[0..n) that carry column c.  Device buffers.
  */
+int mbrwt_count_labels_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts,
+                              void *stream);
+
 /*
  * StaticBinRelAnnotator::get_labels(indices, presence_ratio)
  * (annotate_static.cpp:71-94) for many reads at once -- the `classify`
@@ -174,15 +177,16 @@ int mbrwt_get_column_device(mbrwt_ctx *ctx, uint64_t column, uint64_t *d_rows, u
  * (capacity protocol as mbrwt_get_rows: MBRWT_ERR_CAPACITY + labels_needed).
  * presence_ratio outside [0, 1] (an assert in the reference) ->
  * MBRWT_ERR_INVALID; more than 15,360 columns -> MBRWT_ERR_UNSUPPORTED.
- * Device buffers + stream.
+ * Device buffers + stream; mbrwt_get_labels_batch is the host-buffer form
+ * (read_offsets validated as on the device: ascending, last = n_rows).
  */
+int mbrwt_get_labels_batch(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n_rows, const uint64_t *read_offsets,
+                           uint64_t n_reads, double presence_ratio, uint64_t *label_offsets, uint32_t *labels,
+                           uint64_t labels_cap, uint64_t *labels_needed);
 int mbrwt_get_labels_batch_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n_rows,
                                   const uint64_t *d_read_offsets, uint64_t n_reads, double presence_ratio,
                                   uint64_t *d_label_offsets, uint32_t *d_labels, uint64_t labels_cap,
                                   uint64_t *labels_needed, void *stream);
-
-int mbrwt_count_labels_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts,
-                              void *stream);
 
 /* ---- measurement ------------------------------------------------------- */
 /*

@@ -105,6 +105,33 @@ TEST(BRWTCompressed, get_labels_presence_ratio) {  // test_annotation_BRWT.cpp:4
     EXPECT_EQ(S({}), S(a->get_labels({0, 1, 2, 3, 4}, 0.801)));
 }
 
+TEST(BRWTCompressed, get_labels_batch_presence_ratio) {  // the vectors above, all reads in one batch
+    auto a = annotator(make_fixture(5, {{0, {"Label0", "Label2", "Label8"}},
+                                        {2, {"Label1", "Label2"}},
+                                        {3, {"Label1", "Label2", "Label8"}},
+                                        {4, {"Label2"}}}));
+    const std::vector<std::vector<uint64_t>> reads{{}, {2}, {2, 4}, {0, 1, 2, 3, 4}, {4, 4, 2}};
+    const std::vector<std::pair<double, std::vector<VS>>> want{
+        {0, {{}, {"Label1", "Label2"}, {"Label1", "Label2"}, {"Label0", "Label1", "Label2", "Label8"},
+             {"Label1", "Label2"}}},
+        {0.2, {{}, {"Label1", "Label2"}, {"Label1", "Label2"}, {"Label0", "Label1", "Label2", "Label8"},
+               {"Label1", "Label2"}}},
+        {0.201, {{}, {"Label1", "Label2"}, {"Label1", "Label2"}, {"Label1", "Label2", "Label8"}, {"Label1", "Label2"}}},
+        {0.401, {{}, {"Label1", "Label2"}, {"Label1", "Label2"}, {"Label2"}, {"Label2"}}},
+        {0.8, {{}, {"Label1", "Label2"}, {"Label2"}, {"Label2"}, {"Label2"}}},
+        {1, {{}, {"Label1", "Label2"}, {"Label2"}, {}, {"Label2"}}},
+    };
+    for (const auto &w : want) {
+        auto got = a->get_labels_batch(reads, w.first);
+        EXPECT_EQ(reads.size(), got.size());
+        for (size_t r = 0; r < reads.size(); ++r) {
+            EXPECT_EQ(S(w.second[r]), S(got[r]));
+            EXPECT_EQ(S(a->get_labels(reads[r], w.first)), S(got[r]));
+        }
+    }
+    EXPECT_EQ(0u, a->get_labels_batch({}, 0.5).size());
+}
+
 TEST(LabelEncoder, encode_decode) {  // annotate.cpp:12-31, annotate.hpp:128
     mbrwt_host::LabelEncoder<std::string> e;
     EXPECT_EQ(0u, e.insert_and_encode("a"));

@@ -589,3 +589,37 @@ def test_get_labels_batch_errors(oracle_mod):
         d.get_labels_batch(np.array([5000], dtype=np.uint64), np.array([0, 1], dtype=np.uint64), 0.0)  # row range
     off, labs = d.get_labels_batch(rows, np.array([0, 0, 10], dtype=np.uint64), 0.0)  # an empty read
     assert off[0] == 0 and off[1] == 0 and off[2] == len(labs)
+    for bad in ([0, 11], [1, 10], [0, 6, 4, 10], [0, 5, 9]):  # past n_rows, not from 0, descending, short
+        with pytest.raises(L.MBRWTError) as e:
+            d.get_labels_batch(rows, np.array(bad, dtype=np.uint64), 0.0)
+        assert e.value.status == L.MBRWT_ERR_INVALID
+    off, labs = d.get_labels_batch(np.zeros(0, dtype=np.uint64), np.array([0], dtype=np.uint64), 0.5)  # no reads
+    assert off.tolist() == [0] and labs.size == 0
+
+
+def test_get_labels_batch_device_matches_host(oracle_mod):
+    """The device-buffer form (torch tensors as plumbing, capacity protocol)
+    returns what the host-buffer form returns."""
+    import torch
+    from genome_graph_annotation_amd import BRWTDevice, _lib as L
+    n, m = 100_000, 700
+    d = BRWTDevice.synthetic(n, m, 0.01, 8, 5)
+    rng = np.random.default_rng(9)
+    lens = rng.integers(1, 40, 2000)
+    read_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    rows = rng.integers(0, n, int(read_off[-1])).astype(np.uint64)
+    want_off, want = d.get_labels_batch(rows, read_off, 0.25)
+    rt = torch.from_numpy(rows.view(np.int64)).cuda()
+    ot = torch.from_numpy(read_off.view(np.int64)).cuda()
+    lo = torch.empty(len(read_off), dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    small = torch.empty(1, dtype=torch.int32, device="cuda")
+    with pytest.raises(L.MBRWTError) as e:
+        d.get_labels_batch_device(rt, ot, 0.25, lo, small, s)
+    assert e.value.needed == len(want)
+    lt = torch.empty(e.value.needed, dtype=torch.int32, device="cuda")
+    got = d.get_labels_batch_device(rt, ot, 0.25, lo, lt, s)
+    torch.cuda.synchronize()
+    assert got == len(want)
+    np.testing.assert_array_equal(lo.cpu().numpy().view(np.uint64), want_off)
+    np.testing.assert_array_equal(lt.cpu().numpy().view(np.uint32), want)
