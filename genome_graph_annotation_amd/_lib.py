@@ -87,6 +87,11 @@ SIGNATURES = {
     "mbrwt_create_from_columns": (C.c_int, [C.POINTER(ColumnsDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "mbrwt_get_labels_batch": (C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p, C.c_uint64, C.c_double, u64p, u32p,
                                          C.c_uint64, u64p]),
+    "mbrwt_get_top_labels_batch": (C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p, C.c_uint64, C.c_uint64, u64p,
+                                             u32p, u64p, C.c_uint64, u64p]),
+    "mbrwt_get_top_labels_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                                    C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                                    u64p, C.c_void_p]),
     "mbrwt_get_labels_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                                                 C.c_double, C.c_void_p, C.c_void_p, C.c_uint64, u64p, C.c_void_p]),
     "mbrwt_pack_ids_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]),

@@ -231,6 +231,47 @@ class BRWTDevice:
             L.check(st, "mbrwt_get_labels_batch")
             return lo, labs[: need.value]
 
+    def get_top_labels_batch(self, rows, read_offsets, num_top=2**64 - 1):
+        """MultiLabelEncoded::get_top_labels(indices, num_top) for many reads
+        (include/mbrwt.h mbrwt_get_top_labels_batch): -> (label offsets u64
+        [n_reads+1], labels u32, counts u64), each read by count descending,
+        equal counts by label ascending."""
+        lib = L.lib()
+        rows = np.ascontiguousarray(rows, dtype=np.uint64)
+        ro = np.ascontiguousarray(read_offsets, dtype=np.uint64)
+        if ro.size == 0:
+            raise ValueError("read_offsets needs n_reads + 1 entries")
+        lo = np.zeros(ro.size, dtype=np.uint64)
+        need = C.c_uint64(0)
+        cap = max(16, 4 * rows.size)
+        while True:
+            labs = np.zeros(cap, dtype=np.uint32)
+            cnts = np.zeros(cap, dtype=np.uint64)
+            st = lib.mbrwt_get_top_labels_batch(self._h, _p(rows, C.c_uint64), rows.size, _p(ro, C.c_uint64),
+                                                ro.size - 1, int(num_top), _p(lo, C.c_uint64), _p(labs, C.c_uint32),
+                                                _p(cnts, C.c_uint64), cap, C.byref(need))
+            if st == L.MBRWT_ERR_CAPACITY:
+                cap = int(need.value)
+                continue
+            L.check(st, "mbrwt_get_top_labels_batch")
+            return lo, labs[: need.value], cnts[: need.value]
+
+    def get_top_labels_batch_device(self, rows_t, read_off_t, num_top, lab_off_t, labels_t, counts_t, stream=None):
+        """Device-buffer form on torch tensors (labels int32, counts int64);
+        returns the label count (raises MBRWTError with .needed on capacity)."""
+        need = C.c_uint64(0)
+        out = labels_t is not None and counts_t is not None
+        st = L.lib().mbrwt_get_top_labels_batch_device(
+            self._h, rows_t.data_ptr(), rows_t.numel(), read_off_t.data_ptr(), read_off_t.numel() - 1, int(num_top),
+            lab_off_t.data_ptr(), labels_t.data_ptr() if out else None, counts_t.data_ptr() if out else None,
+            min(labels_t.numel(), counts_t.numel()) if out else 0, C.byref(need), stream)
+        if st == L.MBRWT_ERR_CAPACITY:
+            e = L.MBRWTError(st, "mbrwt_get_top_labels_batch_device")
+            e.needed = int(need.value)
+            raise e
+        L.check(st, "mbrwt_get_top_labels_batch_device")
+        return int(need.value)
+
     def count_work_device(self, rows_t, stream=None):
         v = C.c_uint64(0)
         lab = C.c_uint64(0)

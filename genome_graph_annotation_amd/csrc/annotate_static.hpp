@@ -153,6 +153,31 @@ class StaticBinRelAnnotator {
         return top;
     }
 
+    // get_top_labels for a batch of reads (classify --count-labels,
+    // main.cpp:177): one device call when the matrix is a BRWTDevice, else
+    // one get_top_labels per read
+    std::vector<std::vector<std::pair<Label, size_t>>> get_top_labels_batch(
+        const std::vector<std::vector<Index>> &reads, size_t num_top = static_cast<size_t>(-1)) const {
+        std::vector<std::vector<std::pair<Label, size_t>>> out(reads.size());
+        const auto *dev = dynamic_cast<const BRWTDevice *>(matrix_.get());
+        if (!dev) {
+            for (size_t r = 0; r < reads.size(); ++r) out[r] = get_top_labels(reads[r], num_top);
+            return out;
+        }
+        std::vector<Index> rows;
+        std::vector<uint64_t> read_off{0}, lab_off, counts;
+        for (const auto &read : reads) {
+            rows.insert(rows.end(), read.begin(), read.end());
+            read_off.push_back(rows.size());
+        }
+        std::vector<uint32_t> codes;
+        dev->get_top_labels_batch_csr(rows, read_off, num_top, &lab_off, &codes, &counts);
+        for (size_t r = 0; r < reads.size(); ++r)
+            for (uint64_t i = lab_off[r]; i < lab_off[r + 1]; ++i)
+                out[r].emplace_back(label_encoder_.decode(codes[i]), counts[i]);
+        return out;
+    }
+
     uint64_t num_objects() const { return matrix_->num_rows(); }
     size_t num_labels() const { return label_encoder_.size(); }
     uint64_t num_relations() const { return matrix_->num_relations(); }

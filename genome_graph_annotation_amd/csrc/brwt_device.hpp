@@ -170,6 +170,39 @@ class BRWTDevice : public BinaryMatrix {
         }
     }
 
+    // MultiLabelEncoded::get_top_labels(indices, num_top) (annotate.cpp:57-83)
+    // for many reads in one call (mbrwt_get_top_labels_batch): per read, the
+    // label codes and their counts by count descending (ties: code ascending)
+    void get_top_labels_batch_csr(const std::vector<Row> &rows, const std::vector<uint64_t> &read_offsets,
+                                  uint64_t num_top, std::vector<uint64_t> *label_offsets,
+                                  std::vector<uint32_t> *labels, std::vector<uint64_t> *counts) const {
+        if (read_offsets.empty()) throw std::invalid_argument("read_offsets needs n_reads + 1 entries");
+        const uint64_t n_reads = read_offsets.size() - 1;
+        label_offsets->assign(read_offsets.size(), 0);
+        labels->clear();
+        counts->clear();
+        if (!ctx_) {
+            if (!rows.empty()) throw std::out_of_range("get_top_labels on an empty BRWT");
+            return;
+        }
+        uint64_t cap = std::max<uint64_t>(16, 4 * rows.size()), need = 0;
+        for (;;) {
+            labels->resize(cap);
+            counts->resize(cap);
+            int st = mbrwt_get_top_labels_batch(ctx_.get(), rows.data(), rows.size(), read_offsets.data(), n_reads,
+                                                num_top, label_offsets->data(), labels->data(), counts->data(), cap,
+                                                &need);
+            if (st == MBRWT_ERR_CAPACITY) {
+                cap = need;
+                continue;
+            }
+            check_status(st, "BRWTDevice::get_top_labels_batch");
+            labels->resize(need);
+            counts->resize(need);
+            return;
+        }
+    }
+
     // CSR form: offsets[rows.size()+1], cols in the reference's per-row order
     void get_rows_csr(const std::vector<Row> &rows, std::vector<uint64_t> *offsets,
                       std::vector<uint32_t> *cols) const {

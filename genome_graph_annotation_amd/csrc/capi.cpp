@@ -375,6 +375,72 @@ int mbrwt_get_labels_batch(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n_rows
     }
 }
 
+int mbrwt_get_top_labels_batch_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n_rows,
+                                      const uint64_t *d_read_offsets, uint64_t n_reads, uint64_t num_top,
+                                      uint64_t *d_label_offsets, uint32_t *d_labels, uint64_t *d_counts,
+                                      uint64_t labels_cap, uint64_t *labels_needed, void *stream) {
+    if (!ctx || (n_rows && !d_rows) || !d_read_offsets || !d_label_offsets) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    try {
+        MBRWT_HIP(hipSetDevice(c.device));
+        const bool out = d_labels && d_counts;
+        return run_get_top_labels_batch(c, d_rows, n_rows, d_read_offsets, n_reads, num_top, d_label_offsets,
+                                        d_labels, d_counts, out ? labels_cap : 0, labels_needed,
+                                        reinterpret_cast<hipStream_t>(stream));
+    } catch (...) {
+        set_error("unexpected exception in mbrwt_get_top_labels_batch_device");
+        return MBRWT_ERR_INVALID;
+    }
+}
+
+int mbrwt_get_top_labels_batch(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n_rows, const uint64_t *read_offsets,
+                               uint64_t n_reads, uint64_t num_top, uint64_t *label_offsets, uint32_t *labels,
+                               uint64_t *counts, uint64_t labels_cap, uint64_t *labels_needed) {
+    if (!ctx || (n_rows && !rows) || !read_offsets || !label_offsets) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    try {
+        MBRWT_HIP(hipSetDevice(c.device));
+        int rc;
+        if ((rc = ensure(c.ws_rows, (n_rows + 2 * (n_reads + 1)) * sizeof(uint64_t)))) return rc;
+        uint64_t *d_rows = reinterpret_cast<uint64_t *>(c.ws_rows.buf);
+        uint64_t *d_roff = d_rows + n_rows;
+        uint64_t *d_loff = d_roff + n_reads + 1;
+        if (n_rows) MBRWT_HIP(hipMemcpyAsync(d_rows, rows, n_rows * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+        MBRWT_HIP(hipMemcpyAsync(d_roff, read_offsets, (n_reads + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                                 c.stream));
+        // labels (u32) then counts (u64, 8-byte aligned) in the host-path output workspace
+        const uint64_t lab_words = (std::max<uint64_t>(labels_cap, 1) + 1) & ~1ull;
+        if ((rc = ensure(c.ws_out, lab_words * sizeof(uint32_t) + std::max<uint64_t>(labels_cap, 1) * 8))) return rc;
+        uint32_t *d_lab = reinterpret_cast<uint32_t *>(c.ws_out.buf);
+        uint64_t *d_cnt = reinterpret_cast<uint64_t *>(d_lab + lab_words);
+        uint64_t needed = 0;
+        const bool out = labels && counts;
+        rc = run_get_top_labels_batch(c, d_rows, n_rows, d_roff, n_reads, num_top, d_loff, d_lab, d_cnt,
+                                      out ? labels_cap : 0, &needed, c.stream);
+        if (labels_needed) *labels_needed = needed;
+        if (rc) return rc;
+        MBRWT_HIP(hipMemcpyAsync(label_offsets, d_loff, (n_reads + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                 c.stream));
+        if (needed) {
+            MBRWT_HIP(hipMemcpyAsync(labels, d_lab, needed * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+            MBRWT_HIP(hipMemcpyAsync(counts, d_cnt, needed * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+        }
+        MBRWT_HIP(hipStreamSynchronize(c.stream));
+        return MBRWT_OK;
+    } catch (...) {
+        set_error("unexpected exception in mbrwt_get_top_labels_batch");
+        return MBRWT_ERR_INVALID;
+    }
+}
+
 int mbrwt_count_work_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, uint64_t *sum_visits,
                             uint64_t *sum_labels, void *stream) {
     if (!ctx || (n && !d_rows)) {

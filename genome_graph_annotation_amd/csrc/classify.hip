@@ -9,6 +9,8 @@
 // least ceil(|indices| * presence_ratio) rows (>= 1 row when the ratio is 0,
 // :78-83) are written in ascending code order (:87-91).  Pass 0 counts them,
 // a scan gives every read's output offset, pass 1 writes.
+// get_top_labels(indices, num_top) (annotate.cpp:57-83; classify
+// --count-labels, main.cpp:177) runs the same driver with a sorting kernel.
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
@@ -71,22 +73,121 @@ __global__ __launch_bounds__(kClsThreads) void k_read_labels(const uint64_t *__r
     }
 }
 
+// MultiLabelEncoded::get_top_labels (annotate.cpp:57-83) per read: the
+// read's histogram in LDS as u64, turned into sort keys (count << 14 |
+// 16383 - label) that are gathered, in any order, into a compact buffer of
+// kTopCompact entries; a bitonic sort of pow2 >= nonzero keys in descending
+// order then gives labels by count descending and equal counts by label
+// ascending (one of the orders the reference's unstable std::sort may
+// produce).  A read with more nonzero labels than the buffer holds sorts
+// the whole histogram (P = pow2 >= m keys, zeros last) in place.  Pass 0
+// only writes min(nonzero, num_top).
+constexpr uint32_t kTopLabelBits = 14;
+constexpr uint32_t kTopLabelMask = (1u << kTopLabelBits) - 1;
+constexpr uint32_t kTopMaxColumns = 8192;  // P * 8 bytes of LDS <= 64 KB
+constexpr uint32_t kTopCompact = 1024;     // + 8 KB
+
+// descending bitonic sort of key[0..Q), Q a power of two, one block
+__device__ inline void bitonic_desc(unsigned long long *key, uint32_t Q) {
+    const uint32_t t = threadIdx.x;
+    for (uint32_t k = 2; k <= Q; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t p = t; p < Q / 2; p += kClsThreads) {
+                const uint32_t i = 2 * j * (p / j) + (p % j), l = i + j;
+                const unsigned long long a = key[i], b = key[l];
+                // runs with (i & k) == 0 descend, so the whole array ends descending
+                if (((i & k) == 0) ? (a < b) : (a > b)) {
+                    key[i] = b;
+                    key[l] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ __launch_bounds__(kClsThreads) void k_read_top_labels(const uint64_t *__restrict__ read_off,
+                                                                 uint64_t n_reads, uint64_t n_rows,
+                                                                 const uint64_t *__restrict__ row_csr,
+                                                                 const uint32_t *__restrict__ cols, uint32_t m,
+                                                                 uint32_t P, uint64_t num_top,
+                                                                 uint64_t *__restrict__ counts_or_offsets,
+                                                                 uint32_t *__restrict__ out_labels,
+                                                                 uint64_t *__restrict__ out_counts, int pass) {
+    extern __shared__ unsigned long long key[];  // [P] histogram / keys, then [kTopCompact]
+    unsigned long long *compact = key + P;
+    __shared__ uint32_t nz_all;
+    const uint32_t t = threadIdx.x;
+    for (uint64_t r = blockIdx.x; r < n_reads; r += gridDim.x) {
+        for (uint32_t i = t; i < P; i += kClsThreads) key[i] = 0;
+        if (t == 0) nz_all = 0;
+        __syncthreads();
+        const uint64_t rs = gld(read_off + r), re = gld(read_off + r + 1);
+        if (rs > re || re > n_rows || (r == 0 && rs != 0) || (r + 1 == n_reads && re != n_rows)) {
+            if (t == 0) {
+                gst(counts_or_offsets + r, (uint64_t)0);
+                gst(counts_or_offsets + n_reads, (uint64_t)1);
+            }
+            __syncthreads();
+            continue;
+        }
+        const uint64_t l0 = gld(row_csr + rs), l1 = gld(row_csr + re);
+        for (uint64_t i = l0 + t; i < l1; i += kClsThreads) atomicAdd(&key[gld(cols + i)], 1ull);
+        __syncthreads();
+        for (uint32_t c = t; c < m; c += kClsThreads) {
+            const unsigned long long k = key[c];
+            if (k) {
+                const unsigned long long kk = (k << kTopLabelBits) | (kTopLabelMask - c);
+                key[c] = kk;
+                if (pass) {
+                    const uint32_t at = atomicAdd(&nz_all, 1u);
+                    if (at < kTopCompact) compact[at] = kk;
+                } else {
+                    atomicAdd(&nz_all, 1u);
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t nz = nz_all;
+        const uint64_t n_out = std::min<uint64_t>(nz, num_top);
+        if (pass == 0) {
+            if (t == 0) gst(counts_or_offsets + r, n_out);
+            __syncthreads();
+            continue;
+        }
+        if (n_out) {
+            unsigned long long *sorted = key;
+            if (nz <= kTopCompact) {
+                uint32_t Q = 1;
+                while (Q < nz) Q <<= 1;
+                for (uint32_t i = nz + t; i < Q; i += kClsThreads) compact[i] = 0;
+                __syncthreads();
+                bitonic_desc(compact, Q);
+                sorted = compact;
+            } else {
+                bitonic_desc(key, P);
+            }
+            const uint64_t o = gld(counts_or_offsets + r);
+            for (uint32_t i = t; i < n_out; i += kClsThreads) {
+                const unsigned long long k = sorted[i];
+                gst(out_labels + o + i, kTopLabelMask - (uint32_t)(k & kTopLabelMask));
+                gst(out_counts + o + i, (uint64_t)(k >> kTopLabelBits));
+            }
+        }
+        __syncthreads();
+    }
+}
+
 unsigned grid_of(uint64_t n) { return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(n, 65536)); }
 
 }  // namespace
 
-int run_get_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const uint64_t *d_read_off, uint64_t n_reads,
-                         double ratio, uint64_t *d_lab_off, uint32_t *d_labels, uint64_t cap, uint64_t *needed,
-                         hipStream_t s) {
-    const uint64_t m = c.tree.num_columns;
-    if (!(ratio >= 0.0 && ratio <= 1.0)) {  // an assert in the reference (annotate_static.cpp:76)
-        set_error("presence_ratio outside [0, 1]");
-        return MBRWT_ERR_INVALID;
-    }
-    if (m > kClsMaxColumns) {
-        set_error("get_labels batch: more than 15360 columns is not supported by this build");
-        return MBRWT_ERR_UNSUPPORTED;
-    }
+// The rows of all reads through run_get_rows (CSR in ws_cls_*), then
+// launch(pass 0, counts) per read, a scan into d_lab_off, the capacity check
+// and launch(pass 1, d_lab_off).  Shared by get_labels and get_top_labels.
+template <class Launch>
+int classify_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, uint64_t n_reads, uint64_t *d_lab_off,
+                   bool have_out, uint64_t cap, uint64_t *needed, hipStream_t s, Launch launch) {
     if (!n_reads && n_rows) {  // the one offset would have to be both 0 and n_rows
         set_error("read offsets must ascend from 0 to n_rows");
         return MBRWT_ERR_INVALID;
@@ -111,14 +212,12 @@ int run_get_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const 
         return MBRWT_OK;
     }
     const uint32_t *d_cols = reinterpret_cast<const uint32_t *>(c.ws_cls_cols.buf);
-    const size_t lds = std::max<uint64_t>(m, 1) * sizeof(uint32_t);
     // 2. per-read counts, inclusive scan -> d_lab_off[1..n_reads]
     //    (d_cnt[n_reads] = the malformed-offsets flag)
     if ((rc = ensure(c.ws_sort, (n_reads + 1) * sizeof(uint64_t)))) return rc;
     uint64_t *d_cnt = reinterpret_cast<uint64_t *>(c.ws_sort.buf);
     MBRWT_HIP(hipMemsetAsync(d_cnt + n_reads, 0, sizeof(uint64_t), s));
-    hipLaunchKernelGGL(k_read_labels, dim3(grid_of(n_reads)), dim3(kClsThreads), lds, s, d_read_off, n_reads, n_rows,
-                       d_off, d_cols, (uint32_t)m, ratio, d_cnt, nullptr, 0);
+    launch(0, d_off, d_cols, d_cnt);
     MBRWT_HIP(hipGetLastError());
     MBRWT_HIP(hipMemsetAsync(d_lab_off, 0, sizeof(uint64_t), s));
     size_t scan_bytes = 0;
@@ -134,17 +233,57 @@ int run_get_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const 
         return MBRWT_ERR_INVALID;
     }
     if (needed) *needed = total;
-    if (total > cap || (total && !d_labels)) {
+    if (total > cap || (total && !have_out)) {
         set_error("label buffer too small (see labels_needed)");
         return MBRWT_ERR_CAPACITY;
     }
-    // 3. the labels, ascending per read
+    // 3. the output
     if (total) {
-        hipLaunchKernelGGL(k_read_labels, dim3(grid_of(n_reads)), dim3(kClsThreads), lds, s, d_read_off, n_reads,
-                           n_rows, d_off, d_cols, (uint32_t)m, ratio, d_lab_off, d_labels, 1);
+        launch(1, d_off, d_cols, d_lab_off);
         MBRWT_HIP(hipGetLastError());
     }
     return MBRWT_OK;
+}
+
+int run_get_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const uint64_t *d_read_off, uint64_t n_reads,
+                         double ratio, uint64_t *d_lab_off, uint32_t *d_labels, uint64_t cap, uint64_t *needed,
+                         hipStream_t s) {
+    const uint64_t m = c.tree.num_columns;
+    if (!(ratio >= 0.0 && ratio <= 1.0)) {  // an assert in the reference (annotate_static.cpp:76)
+        set_error("presence_ratio outside [0, 1]");
+        return MBRWT_ERR_INVALID;
+    }
+    if (m > kClsMaxColumns) {
+        set_error("get_labels batch: more than 15360 columns is not supported by this build");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
+    const size_t lds = std::max<uint64_t>(m, 1) * sizeof(uint32_t);
+    return classify_batch(c, d_rows, n_rows, n_reads, d_lab_off, d_labels != nullptr, cap, needed, s,
+                          [&](int pass, const uint64_t *d_off, const uint32_t *d_cols, uint64_t *cnt_or_off) {
+                              hipLaunchKernelGGL(k_read_labels, dim3(grid_of(n_reads)), dim3(kClsThreads), lds, s,
+                                                 d_read_off, n_reads, n_rows, d_off, d_cols, (uint32_t)m, ratio,
+                                                 cnt_or_off, pass ? d_labels : nullptr, pass);
+                          });
+}
+
+int run_get_top_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const uint64_t *d_read_off,
+                             uint64_t n_reads, uint64_t num_top, uint64_t *d_lab_off, uint32_t *d_labels,
+                             uint64_t *d_counts, uint64_t cap, uint64_t *needed, hipStream_t s) {
+    const uint64_t m = c.tree.num_columns;
+    if (m > kTopMaxColumns) {
+        set_error("get_top_labels batch: more than 8192 columns is not supported by this build");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
+    uint32_t P = 2;
+    while (P < m) P <<= 1;
+    const size_t lds = (size_t)(P + kTopCompact) * sizeof(unsigned long long);
+    return classify_batch(c, d_rows, n_rows, n_reads, d_lab_off, d_labels && d_counts, cap, needed, s,
+                          [&](int pass, const uint64_t *d_off, const uint32_t *d_cols, uint64_t *cnt_or_off) {
+                              hipLaunchKernelGGL(k_read_top_labels, dim3(grid_of(n_reads)), dim3(kClsThreads), lds,
+                                                 s, d_read_off, n_reads, n_rows, d_off, d_cols, (uint32_t)m, P,
+                                                 num_top, cnt_or_off, pass ? d_labels : nullptr,
+                                                 pass ? d_counts : nullptr, pass);
+                          });
 }
 
 }  // namespace mbrwt

@@ -250,6 +250,9 @@ int run_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_cou
 int run_get_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const uint64_t *d_read_off, uint64_t n_reads,
                          double ratio, uint64_t *d_lab_off, uint32_t *d_labels, uint64_t cap, uint64_t *needed,
                          hipStream_t s);
+int run_get_top_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const uint64_t *d_read_off,
+                             uint64_t n_reads, uint64_t num_top, uint64_t *d_lab_off, uint32_t *d_labels,
+                             uint64_t *d_counts, uint64_t cap, uint64_t *needed, hipStream_t s);
 int run_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s);
 
 }  // namespace mbrwt

@@ -188,6 +188,24 @@ int mbrwt_get_labels_batch_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64
                                   uint64_t *d_label_offsets, uint32_t *d_labels, uint64_t labels_cap,
                                   uint64_t *labels_needed, void *stream);
 
+/*
+ * MultiLabelEncoded::get_top_labels(indices, num_top) (annotate.cpp:57-83;
+ * `classify --count-labels`, main.cpp:177) for many reads at once: read r's
+ * labels present in >= 1 of its rows with their row counts, by count
+ * descending, at most num_top of them.  Equal counts come in ascending label
+ * order (the reference's std::sort leaves their order unspecified).  Reads as
+ * mbrwt_get_labels_batch; output d_label_offsets[n_reads + 1], d_labels (u32)
+ * and d_counts (u64) side by side, labels_cap entries each (capacity protocol
+ * as mbrwt_get_rows).  More than 8,192 columns -> MBRWT_ERR_UNSUPPORTED.
+ */
+int mbrwt_get_top_labels_batch(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n_rows, const uint64_t *read_offsets,
+                               uint64_t n_reads, uint64_t num_top, uint64_t *label_offsets, uint32_t *labels,
+                               uint64_t *counts, uint64_t labels_cap, uint64_t *labels_needed);
+int mbrwt_get_top_labels_batch_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n_rows,
+                                      const uint64_t *d_read_offsets, uint64_t n_reads, uint64_t num_top,
+                                      uint64_t *d_label_offsets, uint32_t *d_labels, uint64_t *d_counts,
+                                      uint64_t labels_cap, uint64_t *labels_needed, void *stream);
+
 /* ---- measurement ------------------------------------------------------- */
 /*
  * Roofline accounting (DESIGN.md "Measurement"): over rows[0..n) (device

@@ -132,6 +132,28 @@ TEST(BRWTCompressed, get_labels_batch_presence_ratio) {  // the vectors above, a
     EXPECT_EQ(0u, a->get_labels_batch({}, 0.5).size());
 }
 
+TEST(BRWTCompressed, get_top_labels_batch) {  // test_annotation_BRWT.cpp:344-398, all reads in one batch
+    auto a = annotator(make_fixture(5, {{0, {"Label0", "Label2", "Label8"}},
+                                        {2, {"Label1", "Label2"}},
+                                        {3, {"Label1", "Label2", "Label8"}},
+                                        {4, {"Label2", "Label8"}}}));
+    const std::vector<std::vector<uint64_t>> reads{{0, 1, 2, 3, 4}, {}, {2}, {1}, {0, 1, 2, 3, 4}};
+    const VectorCounts all{{"Label2", 4}, {"Label8", 3}, {"Label1", 2}, {"Label0", 1}};
+    for (size_t k : {0ul, 1ul, 2ul, 3ul, 4ul, 1000ul}) {
+        auto got = a->get_top_labels_batch(reads, k);
+        EXPECT_EQ(reads.size(), got.size());
+        VectorCounts top(all.begin(), all.begin() + std::min(k, all.size()));
+        EXPECT_EQ(top, got[0]);
+        EXPECT_EQ(top, got[4]);
+        EXPECT_EQ(VectorCounts({}), got[1]);
+        EXPECT_EQ(VectorCounts({}), got[3]);
+        if (k >= 2) EXPECT_EQ(SC(VectorCounts({{"Label1", 1}, {"Label2", 1}})), SC(got[2]));
+        if (k == 1) EXPECT_EQ(1u, got[2].size());
+    }
+    auto got = a->get_top_labels_batch(reads);  // default: all labels
+    EXPECT_EQ(all, got[0]);
+}
+
 TEST(LabelEncoder, encode_decode) {  // annotate.cpp:12-31, annotate.hpp:128
     mbrwt_host::LabelEncoder<std::string> e;
     EXPECT_EQ(0u, e.insert_and_encode("a"));

@@ -623,3 +623,79 @@ def test_get_labels_batch_device_matches_host(oracle_mod):
     assert got == len(want)
     np.testing.assert_array_equal(lo.cpu().numpy().view(np.uint64), want_off)
     np.testing.assert_array_equal(lt.cpu().numpy().view(np.uint32), want)
+
+
+# ---- batched get_top_labels(indices, num_top): classify --count-labels (§8f row 2) ----
+
+def _ref_top_labels(off_o, cols_o, read_offsets, m, num_top):
+    """annotate.cpp:57-83 over the oracle's rows; equal counts put in ascending
+    label order (the reference's std::sort leaves them unspecified)."""
+    out_off, labs, cnts = [0], [], []
+    for r in range(len(read_offsets) - 1):
+        a, b = int(read_offsets[r]), int(read_offsets[r + 1])
+        cnt = np.bincount(cols_o[off_o[a]:off_o[b]], minlength=m)
+        nz = np.nonzero(cnt)[0]
+        order = nz[np.lexsort((nz, -cnt[nz].astype(np.int64)))][:num_top]
+        labs.extend(order.tolist())
+        cnts.extend(cnt[order].tolist())
+        out_off.append(len(labs))
+    return (np.array(out_off, dtype=np.uint64), np.array(labs, dtype=np.uint32), np.array(cnts, dtype=np.uint64))
+
+
+# density 0.2 at m = 2652: most reads hold > 1024 distinct labels (the in-place
+# whole-histogram sort); the others fit the compact buffer
+@pytest.mark.parametrize("m,num_top,dens", [(2652, 2**64 - 1, 0.003), (2652, 5, 0.003), (2652, 1, 0.003),
+                                            (2652, 0, 0.003), (8192, 20, 0.003), (3, 2, 0.3),
+                                            (2652, 2**64 - 1, 0.2), (2652, 50, 0.2)])
+def test_get_top_labels_batch_matches_reference_semantics(oracle_mod, m, num_top, dens):
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    n = 100_000 if dens < 0.1 else 5_000
+    t = O.OracleTree.topdown(n, m, dens, 8, 31)
+    d = BRWTDevice.synthetic(n, m, dens, 8, 31)
+    rng = np.random.default_rng(11)
+    lens = rng.integers(0, 80, 1500 if dens < 0.1 else 200)
+    read_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    anchors = rng.integers(0, n - 50, len(lens))
+    rows = np.concatenate([a + rng.integers(0, 50, k) for a, k in zip(anchors, lens)]).astype(np.uint64)
+    off_o, cols_o = t.get_rows(rows)
+    want_off, want_l, want_c = _ref_top_labels(off_o, cols_o, read_off, m, min(num_top, m + 1))
+    got_off, got_l, got_c = d.get_top_labels_batch(rows, read_off, num_top)
+    np.testing.assert_array_equal(got_off, want_off)
+    np.testing.assert_array_equal(got_l, want_l)
+    np.testing.assert_array_equal(got_c, want_c)
+
+
+def test_get_top_labels_batch_errors_and_device_form(oracle_mod):
+    import torch
+    from genome_graph_annotation_amd import BRWTDevice, _lib as L
+    big = BRWTDevice.synthetic(1000, 8193, 0.001, 8, 3)
+    with pytest.raises(L.MBRWTError) as e:
+        big.get_top_labels_batch(np.arange(4, dtype=np.uint64), np.array([0, 4], dtype=np.uint64), 3)
+    assert e.value.status == L.MBRWT_ERR_UNSUPPORTED
+    d = BRWTDevice.synthetic(50_000, 700, 0.01, 8, 5)
+    rows = np.arange(10, dtype=np.uint64)
+    for bad in ([0, 11], [1, 10], [0, 6, 4, 10]):
+        with pytest.raises(L.MBRWTError) as e:
+            d.get_top_labels_batch(rows, np.array(bad, dtype=np.uint64), 3)
+        assert e.value.status == L.MBRWT_ERR_INVALID
+    rng = np.random.default_rng(2)
+    lens = rng.integers(1, 40, 1000)
+    read_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    rows = rng.integers(0, 50_000, int(read_off[-1])).astype(np.uint64)
+    want = d.get_top_labels_batch(rows, read_off, 7)
+    rt = torch.from_numpy(rows.view(np.int64)).cuda()
+    ot = torch.from_numpy(read_off.view(np.int64)).cuda()
+    lo = torch.empty(len(read_off), dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    with pytest.raises(L.MBRWTError) as e:
+        d.get_top_labels_batch_device(rt, ot, 7, lo, None, None, s)
+    n = e.value.needed
+    assert n == len(want[1])
+    lt = torch.empty(n, dtype=torch.int32, device="cuda")
+    ct = torch.empty(n, dtype=torch.int64, device="cuda")
+    assert d.get_top_labels_batch_device(rt, ot, 7, lo, lt, ct, s) == n
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(lo.cpu().numpy().view(np.uint64), want[0])
+    np.testing.assert_array_equal(lt.cpu().numpy().view(np.uint32), want[1])
+    np.testing.assert_array_equal(ct.cpu().numpy().view(np.uint64), want[2])

@@ -28,6 +28,7 @@ ap.add_argument("--reads", type=int, default=100_000)
 ap.add_argument("--read-len", type=int, default=80)
 ap.add_argument("--ratio", type=float, default=0.0)
 ap.add_argument("--steps", type=int, default=5)
+ap.add_argument("--top", type=int, default=-1, help="get_top_labels(indices, TOP) instead (classify --count-labels)")
 a = ap.parse_args()
 
 from genome_graph_annotation_amd import BRWTDevice, _lib as L  # noqa: E402
@@ -42,37 +43,57 @@ rt = torch.from_numpy(rows_np.view(np.int64)).to(dev)
 ot = torch.from_numpy(read_off.view(np.int64)).to(dev)
 lo = torch.empty(a.reads + 1, dtype=torch.int64, device=dev)
 s = torch.cuda.current_stream(dev).cuda_stream
+top = a.top >= 0
+
+
+def call(lt, ct):
+    if top:
+        return mat.get_top_labels_batch_device(rt, ot, a.top, lo, lt, ct, s)
+    return mat.get_labels_batch_device(rt, ot, a.ratio, lo, lt, s)
+
+
 try:
-    need = mat.get_labels_batch_device(rt, ot, a.ratio, lo, None, s)
+    need = call(None, None)
 except L.MBRWTError as e:
     need = e.needed
 lt = torch.empty(need + 1024, dtype=torch.int32, device=dev)
-mat.get_labels_batch_device(rt, ot, a.ratio, lo, lt, s)  # warm-up
+ct = torch.empty(need + 1024, dtype=torch.int64, device=dev)
+call(lt, ct)  # warm-up
 torch.cuda.synchronize()
 t0 = time.perf_counter()
 for _ in range(a.steps):
-    got = mat.get_labels_batch_device(rt, ot, a.ratio, lo, lt, s)
+    got = call(lt, ct)
 torch.cuda.synchronize()
 el = (time.perf_counter() - t0) / a.steps
 
-# parity: the reference's get_labels over this batch's own rows (get_rows)
+# parity: the reference's get_labels / get_top_labels over this batch's own rows (get_rows)
 off_r, cols_r = mat.get_rows(rows_np)
 lo_h = lo.cpu().numpy().view(np.uint64)
 lt_h = lt[:got].cpu().numpy().view(np.uint32)
+ct_h = ct[:got].cpu().numpy().view(np.uint64)
 ok = True
 for r in range(a.reads):
     x, y = int(read_off[r]), int(read_off[r + 1])
     cnt = np.bincount(cols_r[off_r[x]:off_r[y]], minlength=a.cols)
-    thr = 1 if a.ratio == 0 else math.ceil((y - x) * a.ratio)
-    want = np.nonzero((cnt > 0) & (cnt >= thr))[0]
-    if not np.array_equal(lt_h[lo_h[r]:lo_h[r + 1]], want):
+    sl = slice(int(lo_h[r]), int(lo_h[r + 1]))
+    if top:
+        nz = np.nonzero(cnt)[0]
+        want = nz[np.lexsort((nz, -cnt[nz].astype(np.int64)))][:a.top]
+        good = np.array_equal(lt_h[sl], want) and np.array_equal(ct_h[sl], cnt[want])
+    else:
+        thr = 1 if a.ratio == 0 else math.ceil((y - x) * a.ratio)
+        good = np.array_equal(lt_h[sl], np.nonzero((cnt > 0) & (cnt >= thr))[0])
+    if not good:
         ok = False
         break
+what = ("get_top_labels(indices, num_top)" if top else "get_labels(indices, presence_ratio)")
 print(json.dumps({
-    "metric": "batched get_labels(indices, presence_ratio) on Multi-BRWT (classify), reads/s",
+    "metric": f"batched {what} on Multi-BRWT (classify), reads/s",
     "value": a.reads / el, "unit": "reads/s", "rows_per_s": n / el, "ms_per_step": el * 1e3,
     "config": {"rows": a.rows, "columns": a.cols, "density": a.density, "reads": a.reads,
-               "read_len": a.read_len, "presence_ratio": a.ratio, "labels_out": int(got)},
-    "parity": ("every read identical to annotate_static.cpp:71-94 applied to the batch's get_rows"
+               "read_len": a.read_len, "presence_ratio": None if top else a.ratio,
+               "num_top": a.top if top else None, "labels_out": int(got)},
+    "parity": (f"every read identical to {'annotate.cpp:57-83' if top else 'annotate_static.cpp:71-94'} "
+               "applied to the batch's get_rows"
                if ok else "MISMATCH"),
 }))
