@@ -85,6 +85,9 @@ SIGNATURES = {
     "mbrwt_create": (C.c_int, [C.POINTER(TreeDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "mbrwt_create_synthetic": (C.c_int, [C.POINTER(SynthDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "mbrwt_create_from_columns": (C.c_int, [C.POINTER(ColumnsDesc), C.c_int, C.POINTER(C.c_void_p)]),
+    "mbrwt_create_from_columns_relaxed": (C.c_int, [C.POINTER(ColumnsDesc), C.c_uint64, C.c_int,
+                                                    C.POINTER(C.c_void_p)]),
+    "mbrwt_create_relaxed": (C.c_int, [C.POINTER(TreeDesc), C.c_uint64, C.c_int, C.POINTER(C.c_void_p)]),
     "mbrwt_get_labels_batch": (C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p, C.c_uint64, C.c_double, u64p, u32p,
                                          C.c_uint64, u64p]),
     "mbrwt_get_top_labels_batch": (C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p, C.c_uint64, C.c_uint64, u64p,

@@ -29,10 +29,11 @@ class BRWTDevice:
 
     # -- construction -------------------------------------------------------
     @classmethod
-    def from_tree(cls, tree, device=0):
+    def from_tree(cls, tree, device=0, relax_max_arity=0):
         """`tree`: BFS description (keys as include/mbrwt.h mbrwt_tree_desc:
         num_rows, num_columns, num_children, first_child, leaf_column,
-        vec_size, words = list of uint64 arrays)."""
+        vec_size, words = list of uint64 arrays).  relax_max_arity > 1 runs
+        BRWTOptimizer::relax on it first (mbrwt_create_relaxed)."""
         lib = L.lib()
         N = int(len(tree["num_children"]))
         nc = np.ascontiguousarray(tree["num_children"], dtype=np.uint32)
@@ -53,7 +54,11 @@ class BRWTDevice:
         d.vec_size = _p(vs, C.c_uint64)
         d.vec_words = ptrs
         h = C.c_void_p()
-        L.check(lib.mbrwt_create(C.byref(d), device, C.byref(h)), "mbrwt_create")
+        if relax_max_arity:
+            L.check(lib.mbrwt_create_relaxed(C.byref(d), int(relax_max_arity), device, C.byref(h)),
+                    "mbrwt_create_relaxed")
+        else:
+            L.check(lib.mbrwt_create(C.byref(d), device, C.byref(h)), "mbrwt_create")
         return cls(h)
 
     @classmethod
@@ -65,11 +70,12 @@ class BRWTDevice:
         return cls(h)
 
     @classmethod
-    def from_columns(cls, columns, num_rows, arity=2, device=0):
+    def from_columns(cls, columns, num_rows, arity=2, device=0, relax_max_arity=0):
         """BRWTBottomUpBuilder::build with the basic partitioner on the device
         (include/mbrwt.h mbrwt_create_from_columns).  `columns`: a sequence of
         uint64 arrays (ceil(num_rows/64) LSB-first words each), or a 2-D
-        uint64 array [num_columns, words]."""
+        uint64 array [num_columns, words].  relax_max_arity > 1 then runs
+        BRWTOptimizer::relax (mbrwt_create_from_columns_relaxed)."""
         lib = L.lib()
         cols = [np.ascontiguousarray(c, dtype=np.uint64) for c in columns]
         W = (num_rows + 63) // 64
@@ -80,7 +86,11 @@ class BRWTDevice:
             ptrs[j] = c.ctypes.data_as(L.u64p)
         d = L.ColumnsDesc(num_rows, len(cols), ptrs, arity)
         h = C.c_void_p()
-        L.check(lib.mbrwt_create_from_columns(C.byref(d), device, C.byref(h)), "mbrwt_create_from_columns")
+        if relax_max_arity:
+            L.check(lib.mbrwt_create_from_columns_relaxed(C.byref(d), int(relax_max_arity), device, C.byref(h)),
+                    "mbrwt_create_from_columns_relaxed")
+        else:
+            L.check(lib.mbrwt_create_from_columns(C.byref(d), device, C.byref(h)), "mbrwt_create_from_columns")
         return cls(h)
 
     def close(self):

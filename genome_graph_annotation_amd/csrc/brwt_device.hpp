@@ -90,15 +90,27 @@ class BRWTDevice : public BinaryMatrix {
 
     // BRWTBottomUpBuilder::build(columns, get_basic_partitioner(arity))
     // (BRWT_builders.cpp:20-31, :119-163), run on the device; columns[j] =
-    // ceil(num_rows/64) LSB-first words
+    // ceil(num_rows/64) LSB-first words.  relax_max_arity > 1 then applies
+    // BRWTOptimizer::relax (:166-297) with that arity limit
     static BRWTDevice build_bottom_up(const std::vector<std::vector<uint64_t>> &columns, uint64_t num_rows,
-                                      uint32_t arity, int device = 0) {
+                                      uint32_t arity, int device = 0, uint64_t relax_max_arity = 0) {
         std::vector<const uint64_t *> ptrs(columns.size());
         for (size_t j = 0; j < columns.size(); ++j) ptrs[j] = columns[j].data();
         mbrwt_columns_desc d{num_rows, columns.size(), ptrs.data(), arity};
         BRWTDevice m;
         mbrwt_ctx *c = nullptr;
-        check_status(mbrwt_create_from_columns(&d, device, &c), "mbrwt_create_from_columns");
+        check_status(mbrwt_create_from_columns_relaxed(&d, relax_max_arity, device, &c),
+                     "mbrwt_create_from_columns_relaxed");
+        m.ctx_.reset(c, Deleter());
+        return m;
+    }
+
+    // BRWTOptimizer::relax(brwt, max_arity) of an exported tree
+    // (`annograph relax_brwt`, main.cpp:746)
+    static BRWTDevice relaxed(const mbrwt_tree_desc &desc, uint64_t max_arity, int device = 0) {
+        BRWTDevice m;
+        mbrwt_ctx *c = nullptr;
+        check_status(mbrwt_create_relaxed(&desc, max_arity, device, &c), "mbrwt_create_relaxed");
         m.ctx_.reset(c, Deleter());
         return m;
     }

@@ -104,9 +104,219 @@ struct BNode {
     uint64_t index_len = 0;
 };
 
+// ---- BRWTOptimizer::relax (BRWT_builders.cpp:166-297) ----------------------
+//
+// reassign (:257-297) moves a pruned node's children up to its parent: a
+// grandchild's index column, defined over the pruned node's set positions,
+// becomes a column over the pruned node's own positions -- a parallel bit
+// deposit (pdep) of the grandchild's bits into the set bits of the pruned
+// node's index, word by word at the exclusive prefix of its popcounts.  All
+// grandchildren of one pruned node are expanded by one launch (grid y).
+struct ExpandArgs {
+    const uint64_t *node;              // the pruned node's index column (Wn words)
+    const unsigned long long *pre;     // [Wn + 1] exclusive prefix of its word popcounts
+    const uint64_t *const *grand;      // [k] grandchild index columns (ceil(ones/64) words)
+    uint64_t *const *out;              // [k] expanded columns (Wn words)
+    uint64_t Wn, ones;
+};
+
+__global__ __launch_bounds__(256) void k_popc_words(const uint64_t *__restrict__ v, uint64_t W,
+                                                    unsigned long long *__restrict__ popc) {
+    for (uint64_t w = blockIdx.x * 256ull + threadIdx.x; w < W; w += gridDim.x * 256ull) popc[w] = __popcll(v[w]);
+}
+
+__global__ __launch_bounds__(256) void k_expand(ExpandArgs A) {
+    const uint64_t *g = A.grand[blockIdx.y];
+    uint64_t *o = A.out[blockIdx.y];
+    const uint64_t gw = (A.ones + 63) / 64;
+    for (uint64_t w = blockIdx.x * 256ull + threadIdx.x; w < A.Wn; w += gridDim.x * 256ull) {
+        uint64_t bits = A.node[w];
+        const uint64_t base = A.pre[w], q = base >> 6, r = base & 63;
+        // the grandchild's bits [base, base + popc) from bit 0
+        uint64_t src = q < gw ? g[q] >> r : 0;
+        if (r && q + 1 < gw) src |= g[q + 1] << (64 - r);
+        uint64_t res = 0;
+        while (bits) {
+            const uint64_t low = bits & (~bits + 1);
+            if (src & 1) res |= low;
+            src >>= 1;
+            bits ^= low;
+        }
+        o[w] = res;
+    }
+}
+
+// sizeof(bit_vector_rrr<63>) * 8 in bv_space_taken_rrr (:315-321): sdsl is
+// absent, so the struct size is the oracle's estimate (oracle/brwt_oracle.cpp
+// kRRRObjectBits; parity unpinned against sdsl, pinned against the oracle --
+// it only moves the prune decision, never the query results)
+constexpr double kRRRObjectBits = 184 * 8;
+
+double logbinomial(uint64_t n, uint64_t k) {  // :299-303
+    return (lgamma(n + 1) - lgamma(k + 1) - lgamma(n - k + 1)) / log(2);
+}
+double bv_space_taken_rrr63(uint64_t size, uint64_t ones) {  // :315-321, block 63
+    return logbinomial(size, ones) + std::ceil(log2(63 + 1) / 63) * size + kRRRObjectBits;
+}
+
+uint64_t popcount_words(const std::vector<uint64_t> &v, uint64_t len) {
+    uint64_t c = 0;
+    for (uint64_t w = 0; w < (len + 63) / 64 && w < v.size(); ++w) c += __builtin_popcountll(v[w]);
+    return c;
+}
+
+int relax_nodes(std::vector<BNode> &nodes, uint32_t root, uint64_t max_arity, hipStream_t s) {
+    std::vector<uint64_t> ones(nodes.size());
+    for (size_t u = 0; u < nodes.size(); ++u) ones[u] = popcount_words(nodes[u].index, nodes[u].index_len);
+    // pruning_delta (:351-380)
+    auto delta = [&](uint32_t u) {
+        double d = 0;
+        for (uint32_t c : nodes[u].children) {
+            d += bv_space_taken_rrr63(nodes[u].index_len, ones[c]);
+            d -= bv_space_taken_rrr63(nodes[c].index_len, ones[c]);
+        }
+        return d - bv_space_taken_rrr63(nodes[u].index_len, ones[u]);
+    };
+    // reassign (:257-297) on the device
+    auto reassign = [&](uint32_t u) -> int {
+        BNode &node = nodes[u];
+        const uint64_t Wn = (node.index_len + 63) / 64, k = node.children.size();
+        if (!Wn) {
+            for (uint32_t c : node.children) {
+                nodes[c].index.assign(1, 0);
+                nodes[c].index_len = 0;
+            }
+            return MBRWT_OK;
+        }
+        uint64_t gwords = 0;
+        for (uint32_t c : node.children) gwords += std::max<uint64_t>(1, nodes[c].index.size());
+        const size_t bytes = (Wn + 2 * (Wn + 1) + gwords + k * Wn + 2 * k) * sizeof(uint64_t);
+        void *arena = nullptr;
+        if (hipMalloc(&arena, bytes) != hipSuccess) return hip_fail(hipErrorOutOfMemory, "relax allocation");
+        uint64_t *d_node = reinterpret_cast<uint64_t *>(arena);
+        unsigned long long *d_popc = reinterpret_cast<unsigned long long *>(d_node + Wn);
+        unsigned long long *d_pre = d_popc + Wn + 1;
+        uint64_t *d_grand = reinterpret_cast<uint64_t *>(d_pre + Wn + 1);
+        uint64_t *d_out = d_grand + gwords;
+        uint64_t **d_tab = reinterpret_cast<uint64_t **>(d_out + k * Wn);
+        std::vector<uint64_t *> tab(2 * k);
+        int rc = MBRWT_OK;
+        void *d_scan = nullptr;
+        do {
+            if (hipMemcpyAsync(d_node, node.index.data(), Wn * 8, hipMemcpyHostToDevice, s) != hipSuccess) break;
+            uint64_t at = 0;
+            for (uint64_t i = 0; i < k; ++i) {
+                const auto &gi = nodes[node.children[i]].index;
+                tab[i] = d_grand + at;
+                tab[k + i] = d_out + i * Wn;
+                if (!gi.empty() &&
+                    hipMemcpyAsync(d_grand + at, gi.data(), gi.size() * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+                    rc = MBRWT_ERR_DEVICE;
+                at += std::max<uint64_t>(1, gi.size());
+            }
+            if (rc) break;
+            if (hipMemcpyAsync(d_tab, tab.data(), 2 * k * 8, hipMemcpyHostToDevice, s) != hipSuccess) break;
+            hipLaunchKernelGGL(k_popc_words, dim3(grid_of(Wn)), dim3(256), 0, s, d_node, Wn, d_popc);
+            if (hipMemsetAsync(d_popc + Wn, 0, 8, s) != hipSuccess) break;
+            size_t scan_bytes = 0;
+            if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, d_popc, d_pre, (int)(Wn + 1), s) != hipSuccess ||
+                hipMalloc(&d_scan, scan_bytes + 16) != hipSuccess ||
+                hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_popc, d_pre, (int)(Wn + 1), s) != hipSuccess)
+                break;
+            ExpandArgs A{d_node, d_pre, d_tab, d_tab + k, Wn, ones[u]};
+            for (uint64_t y0 = 0; y0 < k; y0 += 65535) {
+                ExpandArgs B = A;
+                B.grand = d_tab + y0;
+                B.out = d_tab + k + y0;
+                const uint32_t ny = (uint32_t)std::min<uint64_t>(65535, k - y0);
+                hipLaunchKernelGGL(k_expand, dim3(grid_of(Wn, ny), ny), dim3(256), 0, s, B);
+            }
+            if (hipGetLastError() != hipSuccess) break;
+            for (uint64_t i = 0; i < k; ++i) {
+                BNode &gc = nodes[node.children[i]];
+                gc.index.assign(Wn, 0);
+                gc.index_len = node.index_len;
+                if (hipMemcpyAsync(gc.index.data(), d_out + i * Wn, Wn * 8, hipMemcpyDeviceToHost, s) != hipSuccess)
+                    rc = MBRWT_ERR_DEVICE;
+            }
+            if (rc) break;
+            if (hipStreamSynchronize(s) != hipSuccess) break;
+            (void)hipFree(d_scan);
+            (void)hipFree(arena);
+            return MBRWT_OK;
+        } while (false);
+        (void)hipFree(d_scan);
+        (void)hipFree(arena);
+        set_error("relax: HIP error while expanding index columns");
+        return MBRWT_ERR_DEVICE;
+    };
+    // parents in BFT order, pushed to the front: leaves' parents first, root last (:171-179)
+    std::vector<uint32_t> bft{root};
+    for (size_t h = 0; h < bft.size(); ++h)
+        for (uint32_t c : nodes[bft[h]].children) bft.push_back(c);
+    for (auto it = bft.rbegin(); it != bft.rend(); ++it) {
+        BNode &parent = nodes[*it];
+        if (parent.children.empty()) continue;
+        const std::vector<uint32_t> old = parent.children;
+        std::vector<uint32_t> updated;
+        const uint64_t nchild = old.size();
+        for (uint64_t g = 0; g < nchild; ++g) {
+            const uint32_t c = old[g];
+            // add_submatrix (:213-255): the arity budget left for this child
+            const uint64_t used = updated.size() + nchild - g - 1;
+            const uint64_t max_delta = max_arity - std::min<uint64_t>(max_arity, used);
+            bool prune = !nodes[c].children.empty();
+            if (prune && nodes[c].children.size() > max_delta) prune = false;
+            if (!prune || delta(c) > 0) {
+                updated.push_back(c);
+            } else {
+                int rc = reassign(c);
+                if (rc) return rc;
+                for (uint32_t gc : nodes[c].children) updated.push_back(gc);
+                nodes[c].children.clear();
+                nodes[c].index.clear();
+            }
+        }
+        nodes[*it].children = std::move(updated);
+    }
+    return MBRWT_OK;
+}
+
+// breadth-first numbering of the node tree (mbrwt_tree_desc) and the image
+int image_from_nodes(const std::vector<BNode> &nodes, uint32_t root, uint64_t n, uint64_t m, int device, Tree &tree) {
+    std::vector<uint32_t> order{root};
+    for (size_t h = 0; h < order.size(); ++h)
+        for (uint32_t c : nodes[order[h]].children) order.push_back(c);
+    const uint32_t N = (uint32_t)order.size();
+    std::vector<uint32_t> bfs(nodes.size());
+    for (uint32_t i = 0; i < N; ++i) bfs[order[i]] = i;
+    std::vector<uint32_t> num_children(N), first_child(N), leaf_column(N);
+    std::vector<uint64_t> vec_size(N);
+    std::vector<const uint64_t *> vec_words(N);
+    for (uint32_t i = 0; i < N; ++i) {
+        const BNode &b = nodes[order[i]];
+        num_children[i] = (uint32_t)b.children.size();
+        first_child[i] = b.children.empty() ? 0 : bfs[b.children[0]];
+        leaf_column[i] = b.children.empty() ? b.column : UINT32_MAX;
+        vec_size[i] = b.index_len;
+        vec_words[i] = b.index.data();
+    }
+    mbrwt_tree_desc desc{};
+    desc.num_rows = n;
+    desc.num_columns = m;
+    desc.num_nodes = N;
+    desc.num_children = num_children.data();
+    desc.first_child = first_child.data();
+    desc.leaf_column = leaf_column.data();
+    desc.vec_size = vec_size.data();
+    desc.vec_words = vec_words.data();
+    return build_from_desc(desc, device, tree);
+}
+
 }  // namespace
 
-int build_from_columns(const mbrwt_columns_desc &cd, int device, Tree &tree, hipStream_t s) {
+int build_from_columns(const mbrwt_columns_desc &cd, int device, Tree &tree, hipStream_t s,
+                       uint64_t relax_max_arity) {
     MBRWT_HIP(hipSetDevice(device));
     const uint64_t n = cd.num_rows, m = cd.num_columns;
     if (cd.arity < 2 || cd.arity > kMaxArity) {
@@ -315,35 +525,12 @@ int build_from_columns(const mbrwt_columns_desc &cd, int device, Tree &tree, hip
     MBRWT_HIP(hipStreamSynchronize(s));
     cleanup();
 
-    const auto t_index = std::chrono::steady_clock::now();
-    // breadth-first numbering (mbrwt_tree_desc)
-    std::vector<uint32_t> order{level[0]};
-    for (size_t h = 0; h < order.size(); ++h)
-        for (uint32_t c : nodes[order[h]].children) order.push_back(c);
-    const uint32_t N = (uint32_t)order.size();
-    std::vector<uint32_t> bfs(nodes.size());
-    for (uint32_t i = 0; i < N; ++i) bfs[order[i]] = i;
-    std::vector<uint32_t> num_children(N), first_child(N), leaf_column(N);
-    std::vector<uint64_t> vec_size(N);
-    std::vector<const uint64_t *> vec_words(N);
-    for (uint32_t i = 0; i < N; ++i) {
-        const BNode &b = nodes[order[i]];
-        num_children[i] = (uint32_t)b.children.size();
-        first_child[i] = b.children.empty() ? 0 : bfs[b.children[0]];
-        leaf_column[i] = b.children.empty() ? b.column : UINT32_MAX;
-        vec_size[i] = b.index_len;
-        vec_words[i] = b.index.data();
+    if (relax_max_arity > 1 && !root.children.empty()) {  // BRWTOptimizer::relax (:166-211)
+        const int rr = relax_nodes(nodes, level[0], relax_max_arity, s);
+        if (rr) return rr;
     }
-    mbrwt_tree_desc desc{};
-    desc.num_rows = n;
-    desc.num_columns = m;
-    desc.num_nodes = N;
-    desc.num_children = num_children.data();
-    desc.first_child = first_child.data();
-    desc.leaf_column = leaf_column.data();
-    desc.vec_size = vec_size.data();
-    desc.vec_words = vec_words.data();
-    const int rc = build_from_desc(desc, device, tree);
+    const auto t_index = std::chrono::steady_clock::now();
+    const int rc = image_from_nodes(nodes, level[0], n, m, device, tree);
     if (const char *e = std::getenv("MBRWT_BUILD_TIMING"); e && e[0] == '1') {
         const auto t_end = std::chrono::steady_clock::now();
         std::fprintf(stderr, "[mbrwt build] index columns %.1f ms, image layout %.1f ms\n",
@@ -351,6 +538,41 @@ int build_from_columns(const mbrwt_columns_desc &cd, int device, Tree &tree, hip
                      std::chrono::duration<double, std::milli>(t_end - t_index).count());
     }
     return rc;
+}
+
+// BRWTOptimizer::relax(brwt, max_arity) (`annograph relax_brwt`,
+// main.cpp:746) on a tree description: the BFS tree becomes a node tree, the
+// relax above runs, and the relaxed tree becomes the image.
+int build_relaxed_from_desc(const mbrwt_tree_desc &desc, uint64_t max_arity, int device, Tree &tree, hipStream_t s) {
+    MBRWT_HIP(hipSetDevice(device));
+    const uint32_t N = desc.num_nodes;
+    if (N && (!desc.num_children || !desc.first_child || !desc.leaf_column || !desc.vec_size || !desc.vec_words)) {
+        set_error("null array in the tree description");
+        return MBRWT_ERR_INVALID;
+    }
+    if (!N || max_arity <= 1) return build_from_desc(desc, device, tree);
+    std::vector<BNode> nodes(N);
+    for (uint32_t u = 0; u < N; ++u) {
+        const uint32_t k = desc.num_children[u];
+        if (k && ((uint64_t)desc.first_child[u] + k > N || desc.first_child[u] <= u)) {
+            set_error("tree description: children out of range");
+            return MBRWT_ERR_INVALID;
+        }
+        for (uint32_t i = 0; i < k; ++i) nodes[u].children.push_back(desc.first_child[u] + i);
+        nodes[u].column = k ? UINT32_MAX : desc.leaf_column[u];
+        nodes[u].index_len = desc.vec_size[u];
+        const uint64_t w = (desc.vec_size[u] + 63) / 64;
+        if (w && !desc.vec_words[u]) {
+            set_error("tree description: null index column");
+            return MBRWT_ERR_INVALID;
+        }
+        nodes[u].index.assign(std::max<uint64_t>(w, 1), 0);
+        if (w) std::copy(desc.vec_words[u], desc.vec_words[u] + w, nodes[u].index.begin());
+        if (desc.vec_size[u] & 63) nodes[u].index[w - 1] &= (1ull << (desc.vec_size[u] & 63)) - 1;
+    }
+    const int rc = relax_nodes(nodes, 0, max_arity, s);
+    if (rc) return rc;
+    return image_from_nodes(nodes, 0, desc.num_rows, desc.num_columns, device, tree);
 }
 
 }  // namespace mbrwt

@@ -163,6 +163,43 @@ int mbrwt_create_from_columns(const mbrwt_columns_desc *desc, int device, mbrwt_
     }
 }
 
+int mbrwt_create_from_columns_relaxed(const mbrwt_columns_desc *desc, uint64_t relax_max_arity, int device,
+                                      mbrwt_ctx **out) {
+    if (!desc) {
+        set_error("null columns description");
+        return MBRWT_ERR_INVALID;
+    }
+    try {
+        return create_common(device, out, [&](Ctx &c) {
+            return build_from_columns(*desc, device, c.tree, c.stream, relax_max_arity);
+        });
+    } catch (const std::bad_alloc &) {
+        set_error("host allocation failed");
+        return MBRWT_ERR_NOMEM;
+    } catch (...) {
+        set_error("unexpected exception in mbrwt_create_from_columns_relaxed");
+        return MBRWT_ERR_INVALID;
+    }
+}
+
+int mbrwt_create_relaxed(const mbrwt_tree_desc *desc, uint64_t max_arity, int device, mbrwt_ctx **out) {
+    if (!desc) {
+        set_error("null tree description");
+        return MBRWT_ERR_INVALID;
+    }
+    try {
+        return create_common(device, out, [&](Ctx &c) {
+            return build_relaxed_from_desc(*desc, max_arity, device, c.tree, c.stream);
+        });
+    } catch (const std::bad_alloc &) {
+        set_error("host allocation failed");
+        return MBRWT_ERR_NOMEM;
+    } catch (...) {
+        set_error("unexpected exception in mbrwt_create_relaxed");
+        return MBRWT_ERR_INVALID;
+    }
+}
+
 void mbrwt_destroy(mbrwt_ctx *ctx) { release(C(ctx)); }
 
 uint64_t mbrwt_num_rows(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.num_rows : 0; }

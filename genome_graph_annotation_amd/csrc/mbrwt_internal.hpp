@@ -216,7 +216,11 @@ int ensure(Workspace &w, size_t bytes);
 // image construction (image.cpp / synth.hip)
 int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree);
 int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStream_t stream);
-int build_from_columns(const mbrwt_columns_desc &desc, int device, Tree &tree, hipStream_t stream);
+int build_from_columns(const mbrwt_columns_desc &desc, int device, Tree &tree, hipStream_t stream,
+                       uint64_t relax_max_arity = 0);
+// BRWTOptimizer::relax on a tree description (build.hip)
+int build_relaxed_from_desc(const mbrwt_tree_desc &desc, uint64_t max_arity, int device, Tree &tree,
+                            hipStream_t stream);
 void free_tree(Tree &tree);
 // finish a Tree whose nodes/images are set: column paths, stack depth
 int finalize_tree(Tree &tree);

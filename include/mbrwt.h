@@ -111,6 +111,21 @@ typedef struct mbrwt_columns_desc {
 } mbrwt_columns_desc;
 int mbrwt_create_from_columns(const mbrwt_columns_desc *desc, int device, mbrwt_ctx **out);
 
+/*
+ * BRWTOptimizer::relax(brwt, max_arity) (BRWT_builders.cpp:166-297;
+ * `annograph relax_brwt --relax-arity`, main.cpp:746, config.cpp:104):
+ * internal nodes whose removal saves space (pruning_delta, :351-380, with the
+ * RRR size model of :315-321) are removed and their children re-attached to
+ * the parent, within max_arity children per node.  The re-attached children's
+ * index columns are expanded on the device.  Query results are unchanged.
+ * mbrwt_create_from_columns_relaxed = mbrwt_create_from_columns then relax
+ * (the reference's convert + relax_brwt); mbrwt_create_relaxed relaxes an
+ * exported tree.  max_arity <= 1 leaves the tree as built.
+ */
+int mbrwt_create_from_columns_relaxed(const mbrwt_columns_desc *desc, uint64_t relax_max_arity, int device,
+                                      mbrwt_ctx **out);
+int mbrwt_create_relaxed(const mbrwt_tree_desc *desc, uint64_t max_arity, int device, mbrwt_ctx **out);
+
 void mbrwt_destroy(mbrwt_ctx *ctx);
 
 /* ---- properties (BRWT.hpp:33-51) -------------------------------------- */

@@ -94,7 +94,7 @@ TEST(BRWT, OutOfRange) {  // the reference asserts (BRWT.cpp:27); the mirror thr
 }
 // the same grids built from their columns by the device builder
 // (mbrwt_create_from_columns); device backend only
-static void grid_device_built(int kind) {
+static void grid_device_built(int kind, uint64_t relax = 0) {
     if (!g_device) return;
     for (uint64_t n = 1; n < 20; ++n) {
         for (size_t mcols = 1; mcols < 20; ++mcols) {
@@ -108,10 +108,12 @@ static void grid_device_built(int kind) {
                     ones += b;
                     if (b) words[j][i / 64] |= 1ull << (i % 64);
                 }
-            auto m = mbrwt_host::BRWTDevice::build_bottom_up(words, n, 2);
+            auto m = mbrwt_host::BRWTDevice::build_bottom_up(words, n, 2, 0, relax);
             EXPECT_EQ(ones, m.num_relations());
             // same shape as the reference builder's tree (the oracle's restatement)
-            EXPECT_EQ(OracleMatrix(build_oracle(cols, n, 0, 2, 0)).num_relations(), m.num_relations());
+            auto om = OracleMatrix(build_oracle(cols, n, 0, 2, relax));
+            EXPECT_EQ(om.num_relations(), m.num_relations());
+            EXPECT_EQ(to_device(om).num_nodes(), m.num_nodes());
             test_brwt(m, cols, n);
         }
     }
@@ -125,6 +127,10 @@ TEST(BRWT, BuildBottomUPAllMixed) { grid(2, 0); }
 TEST(BRWTOptimizer, BuildBottomUPAllZero) { grid(0, UINT64_MAX); }
 TEST(BRWTOptimizer, BuildBottomUPAllOne) { grid(1, UINT64_MAX); }
 TEST(BRWTOptimizer, BuildBottomUPAllMixed) { grid(2, UINT64_MAX); }
+// BRWTOptimizer::relax on the device (mbrwt_create_from_columns_relaxed)
+TEST(BRWTOptimizer, DeviceBuilderAllZero) { grid_device_built(0, UINT64_MAX); }
+TEST(BRWTOptimizer, DeviceBuilderAllOne) { grid_device_built(1, UINT64_MAX); }
+TEST(BRWTOptimizer, DeviceBuilderAllMixed) { grid_device_built(2, UINT64_MAX); }
 
 int main(int argc, char **argv) {
     g_device = argc > 1 && std::string(argv[1]) == "device";

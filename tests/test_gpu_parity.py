@@ -521,6 +521,58 @@ def test_device_builder_pass_through_nodes(oracle_mod, m):
     _check_rows(t, built, np.arange(n, dtype=np.uint64), variants=(0,))
 
 
+# ---- BRWTOptimizer::relax on the device ----
+
+def _oracle_from_words_relaxed(O, words, n, m, arity, relax):
+    return O.OracleTree(O.lib().oracle_build_from_columns(O._p64(words), n, m, 0, arity, relax))
+
+
+@pytest.mark.parametrize("n,m,d,arity,relax", [(3000, 100, 0.05, 2, 2**64 - 1), (3000, 100, 0.05, 2, 4),
+                                               (5000, 300, 0.01, 2, 8), (2000, 129, 0.3, 2, 10),
+                                               (4096, 513, 0.004, 3, 16), (1000, 37, 0.05, 2, 2)])
+def test_device_relax_matches_reference_relax(oracle_mod, n, m, d, arity, relax):
+    """Builder + relax on the device (mbrwt_create_from_columns_relaxed) and
+    relax of an exported unrelaxed tree (mbrwt_create_relaxed) both give the
+    oracle's relaxed tree (BRWT_builders.cpp:166-297): the same node count and
+    image bytes as the oracle's relaxed tree through mbrwt_create, and the
+    same answers to every query."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    words = O.generate_columns(n, m, d, seed=n + m + 1)
+    W = (n + 63) // 64
+    cols = words[: m * W].reshape(m, W)
+    t = _oracle_from_words_relaxed(O, words, n, m, arity, relax)
+    plain = _oracle_from_words(O, words, n, m, arity)
+    ref = BRWTDevice.from_tree(t.export())
+    built = BRWTDevice.from_columns(cols, n, arity, relax_max_arity=relax)
+    from_desc = BRWTDevice.from_tree(plain.export(), relax_max_arity=relax)
+    for dev in (built, from_desc):
+        assert dev.num_nodes() == ref.num_nodes() and dev.device_bytes() == ref.device_bytes()
+        assert dev.num_relations() == t.num_relations()
+    if relax > 2:
+        assert ref.num_nodes() < BRWTDevice.from_tree(plain.export()).num_nodes()  # relax pruned something
+    rows = np.concatenate([np.arange(n), np.random.default_rng(1).integers(0, n, 2000)]).astype(np.uint64)
+    _agree(t, [built, from_desc], rows, np.unique(np.linspace(0, m - 1, 8).astype(int)), m)
+
+
+@pytest.mark.parametrize("kind", ["zero", "one", "mixed"])
+def test_device_relax_reference_grids(oracle_mod, kind):
+    """test_BRWT_optimizer.cpp:102-163: every grid 1..19 x 1..19, arity 2,
+    relaxed with max arity 2^64-1, through mbrwt_create_relaxed."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    for n in range(1, 20):
+        for m in range(1, 20):
+            dense = _grid(kind, n, m)
+            t = O.OracleTree.from_dense(dense, "basic", 2, 2**64 - 1)
+            plain = O.OracleTree.from_dense(dense, "basic", 2, 0)
+            dev = BRWTDevice.from_tree(plain.export(), relax_max_arity=2**64 - 1)
+            assert dev.num_nodes() == BRWTDevice.from_tree(t.export()).num_nodes()
+            off, cols = _check_rows(t, dev, np.arange(n, dtype=np.uint64), variants=(0,))
+            for i in range(n):
+                assert sorted(cols[off[i]:off[i + 1]].tolist()) == np.nonzero(dense[i])[0].tolist()
+
+
 def test_pack_ids_kernels_match_the_wire_format():
     """mbrwt_pack_ids_device / mbrwt_unpack_ids_device (the all-gatherv's wire
     format) against dist.py's CPU reference implementation."""
