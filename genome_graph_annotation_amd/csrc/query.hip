@@ -1020,6 +1020,22 @@ __global__ __launch_bounds__(256) void k_compact_chunks(const uint32_t *__restri
         if (sub == 0 && r0 + nr == n) gst(offsets + n, base + pre[nr]);
         const uint32_t stored = buf[nr];
         const uint32_t *src = temp + ch * 8 * K;
+        if (stored == pre[nr]) {  // no overflow row in the chunk: packed label i is output label base + i
+            for (uint32_t i0 = 0; i0 < stored; i0 += 64) {
+                uint32_t v[8];
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k) {
+                    const uint32_t i = i0 + sub + 8 * k;
+                    v[k] = i < stored ? gld(src + i) : 0u;
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k) {
+                    const uint32_t i = i0 + sub + 8 * k;
+                    if (i < stored) gst(cols + base + i, v[k]);
+                }
+            }
+            continue;
+        }
         for (uint32_t i0 = 0; i0 < stored; i0 += 64) {
             uint32_t v[8];
 #pragma unroll
