@@ -85,15 +85,16 @@ __global__ __launch_bounds__(kClsThreads) void k_read_labels(const uint64_t *__r
 constexpr uint32_t kTopLabelBits = 14;
 constexpr uint32_t kTopLabelMask = (1u << kTopLabelBits) - 1;
 constexpr uint32_t kTopMaxColumns = 8192;  // P * 8 bytes of LDS <= 64 KB
-constexpr uint32_t kTopCompact = 1024;     // + 8 KB
+constexpr uint32_t kTopCompact = 4 * kClsThreads;  // + 4 KB of u32 keys
 
 // descending bitonic sort of key[0..Q), Q a power of two, one block
 __device__ inline void bitonic_desc(unsigned long long *key, uint32_t Q) {
     const uint32_t t = threadIdx.x;
     for (uint32_t k = 2; k <= Q; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t lj = (uint32_t)__builtin_ctz(j);  // j is a power of two: no division
             for (uint32_t p = t; p < Q / 2; p += kClsThreads) {
-                const uint32_t i = 2 * j * (p / j) + (p % j), l = i + j;
+                const uint32_t i = ((p >> lj) << (lj + 1)) | (p & (j - 1)), l = i + j;
                 const unsigned long long a = key[i], b = key[l];
                 // runs with (i & k) == 0 descend, so the whole array ends descending
                 if (((i & k) == 0) ? (a < b) : (a > b)) {
@@ -106,6 +107,73 @@ __device__ inline void bitonic_desc(unsigned long long *key, uint32_t Q) {
     }
 }
 
+// descending bitonic sort of u32 keys key[0..Q), Q a power of two in
+// [4, 4 * kClsThreads], one block.  Thread t keeps keys 4t..4t+3 in
+// registers: the j = 1, 2 steps of a merge are register compare-exchanges,
+// the 4 <= j < 256 steps pair lanes of one wave (shuffles, no barrier), and
+// only the j >= 256 steps go through LDS with block barriers.
+__device__ inline void bitonic_desc_u32(uint32_t *key, uint32_t Q) {
+    const uint32_t t = threadIdx.x;
+    const bool own = 4 * t < Q;
+    uint32_t v[4] = {0, 0, 0, 0};
+    if (own) {
+        const u32x4_t q = *reinterpret_cast<const u32x4_t *>(key + 4 * t);
+        v[0] = q[0], v[1] = q[1], v[2] = q[2], v[3] = q[3];
+    }
+    auto reg_step = [&](uint32_t k, uint32_t j) {
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) {
+            const uint32_t l = r ^ j;
+            if (l > r) {
+                const bool desc = ((4 * t + r) & k) == 0;
+                const uint32_t a = v[r], b = v[l];
+                if (desc ? (a < b) : (a > b)) {
+                    v[r] = b;
+                    v[l] = a;
+                }
+            }
+        }
+    };
+    // partner key e ^ j (j >= 4) sits in lane t ^ (j / 4), same register
+    auto wave_step = [&](uint32_t k, uint32_t j) {
+        const bool lower = ((4 * t) & j) == 0, desc = ((4 * t) & k) == 0;
+        const bool keep_max = lower == desc;
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) {
+            const uint32_t pv = (uint32_t)__shfl_xor((int)v[r], (int)(j >> 2), 64);
+            v[r] = keep_max ? (v[r] > pv ? v[r] : pv) : (v[r] < pv ? v[r] : pv);
+        }
+    };
+    for (uint32_t k = 2; k <= Q; k <<= 1) {
+        uint32_t j = k >> 1;
+        if (j >= 256) {
+            if (own) *reinterpret_cast<u32x4_t *>(key + 4 * t) = u32x4_t{v[0], v[1], v[2], v[3]};
+            __syncthreads();
+            for (; j >= 256; j >>= 1) {
+                const uint32_t lj = (uint32_t)__builtin_ctz(j);
+                for (uint32_t p = t; p < Q / 2; p += kClsThreads) {
+                    const uint32_t i = ((p >> lj) << (lj + 1)) | (p & (j - 1)), l = i + j;
+                    const uint32_t a = key[i], b = key[l];
+                    if (((i & k) == 0) ? (a < b) : (a > b)) {
+                        key[i] = b;
+                        key[l] = a;
+                    }
+                }
+                __syncthreads();
+            }
+            if (own) {
+                const u32x4_t q = *reinterpret_cast<const u32x4_t *>(key + 4 * t);
+                v[0] = q[0], v[1] = q[1], v[2] = q[2], v[3] = q[3];
+            }
+        }
+        for (; j >= 4; j >>= 1) wave_step(k, j);
+        if (j == 2) reg_step(k, 2), j = 1;
+        reg_step(k, 1);
+    }
+    if (own) *reinterpret_cast<u32x4_t *>(key + 4 * t) = u32x4_t{v[0], v[1], v[2], v[3]};
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(kClsThreads) void k_read_top_labels(const uint64_t *__restrict__ read_off,
                                                                  uint64_t n_reads, uint64_t n_rows,
                                                                  const uint64_t *__restrict__ row_csr,
@@ -114,8 +182,8 @@ __global__ __launch_bounds__(kClsThreads) void k_read_top_labels(const uint64_t 
                                                                  uint64_t *__restrict__ counts_or_offsets,
                                                                  uint32_t *__restrict__ out_labels,
                                                                  uint64_t *__restrict__ out_counts, int pass) {
-    extern __shared__ unsigned long long key[];  // [P] histogram / keys, then [kTopCompact]
-    unsigned long long *compact = key + P;
+    extern __shared__ unsigned long long key[];  // [P] histogram / keys, then u32 [kTopCompact]
+    uint32_t *compact = reinterpret_cast<uint32_t *>(key + P);
     __shared__ uint32_t nz_all;
     const uint32_t t = threadIdx.x;
     for (uint64_t r = blockIdx.x; r < n_reads; r += gridDim.x) {
@@ -134,17 +202,21 @@ __global__ __launch_bounds__(kClsThreads) void k_read_top_labels(const uint64_t 
         const uint64_t l0 = gld(row_csr + rs), l1 = gld(row_csr + re);
         for (uint64_t i = l0 + t; i < l1; i += kClsThreads) atomicAdd(&key[gld(cols + i)], 1ull);
         __syncthreads();
+        // keys in place; the nonzero ones gathered with one LDS atomic per wave
+        // (ballot + popcount; a per-label atomic on one counter serialises)
+        const uint32_t lane = t & 63;
         for (uint32_t c = t; c < m; c += kClsThreads) {
             const unsigned long long k = key[c];
-            if (k) {
-                const unsigned long long kk = (k << kTopLabelBits) | (kTopLabelMask - c);
-                key[c] = kk;
-                if (pass) {
-                    const uint32_t at = atomicAdd(&nz_all, 1u);
-                    if (at < kTopCompact) compact[at] = kk;
-                } else {
-                    atomicAdd(&nz_all, 1u);
-                }
+            const unsigned long long kk = (k << kTopLabelBits) | (kTopLabelMask - c);
+            if (k) key[c] = kk;
+            const uint64_t bal = __ballot(k != 0);
+            if (bal) {
+                const int leader = __ffsll((unsigned long long)bal) - 1;
+                uint32_t b = 0;
+                if ((int)lane == leader) b = atomicAdd(&nz_all, (uint32_t)__popcll(bal));
+                b = (uint32_t)__shfl((int)b, leader, 64);
+                const uint32_t at = b + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+                if (pass && k && at < kTopCompact) compact[at] = (uint32_t)kk;  // used when count < 2^18
             }
         }
         __syncthreads();
@@ -156,22 +228,26 @@ __global__ __launch_bounds__(kClsThreads) void k_read_top_labels(const uint64_t 
             continue;
         }
         if (n_out) {
-            unsigned long long *sorted = key;
-            if (nz <= kTopCompact) {
-                uint32_t Q = 1;
+            const uint64_t o = gld(counts_or_offsets + r);
+            // u32 keys (count < 2^18: a read of fewer than 2^18 rows) in the compact buffer
+            if (nz <= kTopCompact && re - rs < (1ull << (32 - kTopLabelBits))) {
+                uint32_t Q = 4;
                 while (Q < nz) Q <<= 1;
                 for (uint32_t i = nz + t; i < Q; i += kClsThreads) compact[i] = 0;
                 __syncthreads();
-                bitonic_desc(compact, Q);
-                sorted = compact;
+                bitonic_desc_u32(compact, Q);
+                for (uint32_t i = t; i < n_out; i += kClsThreads) {
+                    const uint32_t k = compact[i];
+                    gst(out_labels + o + i, kTopLabelMask - (k & kTopLabelMask));
+                    gst(out_counts + o + i, (uint64_t)(k >> kTopLabelBits));
+                }
             } else {
                 bitonic_desc(key, P);
-            }
-            const uint64_t o = gld(counts_or_offsets + r);
-            for (uint32_t i = t; i < n_out; i += kClsThreads) {
-                const unsigned long long k = sorted[i];
-                gst(out_labels + o + i, kTopLabelMask - (uint32_t)(k & kTopLabelMask));
-                gst(out_counts + o + i, (uint64_t)(k >> kTopLabelBits));
+                for (uint32_t i = t; i < n_out; i += kClsThreads) {
+                    const unsigned long long k = key[i];
+                    gst(out_labels + o + i, kTopLabelMask - (uint32_t)(k & kTopLabelMask));
+                    gst(out_counts + o + i, (uint64_t)(k >> kTopLabelBits));
+                }
             }
         }
         __syncthreads();
@@ -276,7 +352,7 @@ int run_get_top_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, co
     }
     uint32_t P = 2;
     while (P < m) P <<= 1;
-    const size_t lds = (size_t)(P + kTopCompact) * sizeof(unsigned long long);
+    const size_t lds = (size_t)P * sizeof(unsigned long long) + kTopCompact * sizeof(uint32_t);
     return classify_batch(c, d_rows, n_rows, n_reads, d_lab_off, d_labels && d_counts, cap, needed, s,
                           [&](int pass, const uint64_t *d_off, const uint32_t *d_cols, uint64_t *cnt_or_off) {
                               hipLaunchKernelGGL(k_read_top_labels, dim3(grid_of(n_reads)), dim3(kClsThreads), lds,

@@ -56,6 +56,16 @@ def test_null_arguments_fail_cleanly():
     assert lib.mbrwt_wt_get_column(None, 0, None, 0, None) == L.MBRWT_ERR_INVALID
     assert lib.mbrwt_wt_num_rows(None) == 0
     lib.mbrwt_wt_destroy(None)
+    # builder / relax / classify entry points
+    assert lib.mbrwt_create_from_columns(None, 0, C.byref(out)) == L.MBRWT_ERR_INVALID
+    assert lib.mbrwt_create_from_columns_relaxed(None, 10, 0, C.byref(out)) == L.MBRWT_ERR_INVALID
+    assert lib.mbrwt_create_relaxed(None, 10, 0, C.byref(out)) == L.MBRWT_ERR_INVALID
+    assert lib.mbrwt_get_labels_batch(None, None, 0, None, 0, 0.5, None, None, 0, None) == L.MBRWT_ERR_INVALID
+    assert lib.mbrwt_get_labels_batch_device(None, None, 0, None, 0, 0.5, None, None, 0, None,
+                                             None) == L.MBRWT_ERR_INVALID
+    assert lib.mbrwt_get_top_labels_batch(None, None, 0, None, 0, 3, None, None, None, 0, None) == L.MBRWT_ERR_INVALID
+    assert lib.mbrwt_get_top_labels_batch_device(None, None, 0, None, 0, 3, None, None, None, 0, None,
+                                                 None) == L.MBRWT_ERR_INVALID
 
 
 def test_no_device_is_reported_not_faked():

@@ -647,6 +647,14 @@ def test_get_labels_batch_errors(oracle_mod):
         assert e.value.status == L.MBRWT_ERR_INVALID
     off, labs = d.get_labels_batch(np.zeros(0, dtype=np.uint64), np.array([0], dtype=np.uint64), 0.5)  # no reads
     assert off.tolist() == [0] and labs.size == 0
+    none = np.zeros(0, dtype=np.uint64)
+    off, labs = d.get_labels_batch(none, np.array([0, 0, 0], dtype=np.uint64), 0.0)  # reads without rows
+    assert off.tolist() == [0, 0, 0] and labs.size == 0
+    off, labs, cnts = d.get_top_labels_batch(none, np.array([0, 0], dtype=np.uint64), 5)
+    assert off.tolist() == [0, 0] and labs.size == 0 and cnts.size == 0
+    with pytest.raises(L.MBRWTError) as e:  # zero reads but rows: the one offset cannot be 0 and n_rows
+        d.get_labels_batch(rows, np.array([0], dtype=np.uint64), 0.0)
+    assert e.value.status == L.MBRWT_ERR_INVALID
 
 
 def test_get_labels_batch_device_matches_host(oracle_mod):
