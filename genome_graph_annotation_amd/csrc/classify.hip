@@ -28,7 +28,7 @@ __global__ __launch_bounds__(kClsThreads) void k_read_labels(const uint64_t *__r
                                                              uint64_t n_rows, const uint64_t *__restrict__ row_csr,
                                                              const uint32_t *__restrict__ cols, uint32_t m,
                                                              double ratio, uint64_t *__restrict__ counts_or_offsets,
-                                                             uint32_t *__restrict__ out, int pass) {
+                                                             uint32_t *__restrict__ out, int pass, uint64_t cap) {
     extern __shared__ uint32_t hist[];
     using Scan = hipcub::BlockScan<uint32_t, kClsThreads>;
     __shared__ typename Scan::TempStorage scan_tmp;
@@ -60,8 +60,8 @@ __global__ __launch_bounds__(kClsThreads) void k_read_labels(const uint64_t *__r
         }
         uint32_t before, total;
         Scan(scan_tmp).ExclusiveSum(mine, before, total);
-        if (pass == 0) {
-            if (t == 0) gst(counts_or_offsets + r, (uint64_t)total);
+        if (pass == 0) {  // (cap: get_top_labels' num_top, counted by this pass at ratio 0)
+            if (t == 0) gst(counts_or_offsets + r, std::min<uint64_t>(total, cap));
         } else {
             uint64_t o = gld(counts_or_offsets + r) + before;
             for (uint32_t k = 0; k < per; ++k) {
@@ -80,8 +80,9 @@ __global__ __launch_bounds__(kClsThreads) void k_read_labels(const uint64_t *__r
 // order then gives labels by count descending and equal counts by label
 // ascending (one of the orders the reference's unstable std::sort may
 // produce).  A read with more nonzero labels than the buffer holds sorts
-// the whole histogram (P = pow2 >= m keys, zeros last) in place.  Pass 0
-// only writes min(nonzero, num_top).
+// the whole histogram (P = pow2 >= m keys, zeros last) in place.  The
+// per-read output sizes min(nonzero, num_top) come from k_read_labels'
+// counting pass at ratio 0 (a u32 histogram); this kernel is the writing pass.
 constexpr uint32_t kTopLabelBits = 14;
 constexpr uint32_t kTopLabelMask = (1u << kTopLabelBits) - 1;
 constexpr uint32_t kTopMaxColumns = 8192;  // P * 8 bytes of LDS <= 64 KB
@@ -179,9 +180,9 @@ __global__ __launch_bounds__(kClsThreads) void k_read_top_labels(const uint64_t 
                                                                  const uint64_t *__restrict__ row_csr,
                                                                  const uint32_t *__restrict__ cols, uint32_t m,
                                                                  uint32_t P, uint64_t num_top,
-                                                                 uint64_t *__restrict__ counts_or_offsets,
+                                                                 const uint64_t *__restrict__ lab_off,
                                                                  uint32_t *__restrict__ out_labels,
-                                                                 uint64_t *__restrict__ out_counts, int pass) {
+                                                                 uint64_t *__restrict__ out_counts) {
     extern __shared__ unsigned long long key[];  // [P] histogram / keys, then u32 [kTopCompact]
     uint32_t *compact = reinterpret_cast<uint32_t *>(key + P);
     __shared__ uint32_t nz_all;
@@ -191,14 +192,7 @@ __global__ __launch_bounds__(kClsThreads) void k_read_top_labels(const uint64_t 
         if (t == 0) nz_all = 0;
         __syncthreads();
         const uint64_t rs = gld(read_off + r), re = gld(read_off + r + 1);
-        if (rs > re || re > n_rows || (r == 0 && rs != 0) || (r + 1 == n_reads && re != n_rows)) {
-            if (t == 0) {
-                gst(counts_or_offsets + r, (uint64_t)0);
-                gst(counts_or_offsets + n_reads, (uint64_t)1);
-            }
-            __syncthreads();
-            continue;
-        }
+        // (the offsets were validated by the counting pass, k_read_labels)
         const uint64_t l0 = gld(row_csr + rs), l1 = gld(row_csr + re);
         for (uint64_t i = l0 + t; i < l1; i += kClsThreads) atomicAdd(&key[gld(cols + i)], 1ull);
         __syncthreads();
@@ -216,19 +210,14 @@ __global__ __launch_bounds__(kClsThreads) void k_read_top_labels(const uint64_t 
                 if ((int)lane == leader) b = atomicAdd(&nz_all, (uint32_t)__popcll(bal));
                 b = (uint32_t)__shfl((int)b, leader, 64);
                 const uint32_t at = b + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
-                if (pass && k && at < kTopCompact) compact[at] = (uint32_t)kk;  // used when count < 2^18
+                if (k && at < kTopCompact) compact[at] = (uint32_t)kk;  // used when count < 2^18
             }
         }
         __syncthreads();
         const uint32_t nz = nz_all;
         const uint64_t n_out = std::min<uint64_t>(nz, num_top);
-        if (pass == 0) {
-            if (t == 0) gst(counts_or_offsets + r, n_out);
-            __syncthreads();
-            continue;
-        }
         if (n_out) {
-            const uint64_t o = gld(counts_or_offsets + r);
+            const uint64_t o = gld(lab_off + r);
             // u32 keys (count < 2^18: a read of fewer than 2^18 rows) in the compact buffer
             if (nz <= kTopCompact && re - rs < (1ull << (32 - kTopLabelBits))) {
                 uint32_t Q = 4;
@@ -338,7 +327,7 @@ int run_get_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const 
                           [&](int pass, const uint64_t *d_off, const uint32_t *d_cols, uint64_t *cnt_or_off) {
                               hipLaunchKernelGGL(k_read_labels, dim3(grid_of(n_reads)), dim3(kClsThreads), lds, s,
                                                  d_read_off, n_reads, n_rows, d_off, d_cols, (uint32_t)m, ratio,
-                                                 cnt_or_off, pass ? d_labels : nullptr, pass);
+                                                 cnt_or_off, pass ? d_labels : nullptr, pass, ~0ull);
                           });
 }
 
@@ -355,10 +344,16 @@ int run_get_top_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, co
     const size_t lds = (size_t)P * sizeof(unsigned long long) + kTopCompact * sizeof(uint32_t);
     return classify_batch(c, d_rows, n_rows, n_reads, d_lab_off, d_labels && d_counts, cap, needed, s,
                           [&](int pass, const uint64_t *d_off, const uint32_t *d_cols, uint64_t *cnt_or_off) {
+                              if (pass == 0) {  // min(distinct labels, num_top): a u32 histogram suffices
+                                  hipLaunchKernelGGL(k_read_labels, dim3(grid_of(n_reads)), dim3(kClsThreads),
+                                                     std::max<uint64_t>(m, 1) * sizeof(uint32_t), s, d_read_off,
+                                                     n_reads, n_rows, d_off, d_cols, (uint32_t)m, 0.0, cnt_or_off,
+                                                     nullptr, 0, num_top);
+                                  return;
+                              }
                               hipLaunchKernelGGL(k_read_top_labels, dim3(grid_of(n_reads)), dim3(kClsThreads), lds,
                                                  s, d_read_off, n_reads, n_rows, d_off, d_cols, (uint32_t)m, P,
-                                                 num_top, cnt_or_off, pass ? d_labels : nullptr,
-                                                 pass ? d_counts : nullptr, pass);
+                                                 num_top, cnt_or_off, d_labels, d_counts);
                           });
 }
 
