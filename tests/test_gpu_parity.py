@@ -759,3 +759,24 @@ def test_get_top_labels_batch_errors_and_device_form(oracle_mod):
     np.testing.assert_array_equal(lo.cpu().numpy().view(np.uint64), want[0])
     np.testing.assert_array_equal(lt.cpu().numpy().view(np.uint32), want[1])
     np.testing.assert_array_equal(ct.cpu().numpy().view(np.uint64), want[2])
+
+
+@pytest.mark.parametrize("relax", [2, 4, 2**64 - 1])
+def test_device_relax_of_greedy_trees(oracle_mod, relax):
+    """mbrwt_create_relaxed on an exported greedy-partitioned tree (non-contiguous
+    column groups) against the oracle's relax of the same tree
+    (BRWT_builders.cpp:166-297 keeps the column arrangement): same node count,
+    same ordered CSR."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    rng = np.random.default_rng(17 + relax % 97)
+    n, m = 3000, 60
+    dense = rng.random((n, m)) < 0.08
+    t = O.OracleTree.from_dense(dense, "greedy", 2, relax)
+    plain = O.OracleTree.from_dense(dense, "greedy", 2, 0)
+    dev = BRWTDevice.from_tree(plain.export(), relax_max_arity=relax)
+    assert dev.num_nodes() == BRWTDevice.from_tree(t.export()).num_nodes()
+    rows = np.arange(n, dtype=np.uint64)
+    off, cols = _check_rows(t, dev, rows, variants=(0,))
+    for k in range(0, n, 37):
+        assert sorted(cols[off[k]:off[k + 1]].tolist()) == np.nonzero(dense[k])[0].tolist()
