@@ -131,6 +131,16 @@ SIGNATURES = {
     "mbrwt_wt_get_rows": (C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p, u32p, C.c_uint64, u64p]),
     "mbrwt_wt_get_rows_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
                                            u64p, C.c_void_p]),
+    "mbrwt_wt_get_labels_batch": (C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p, C.c_uint64, C.c_double, u64p,
+                                            u32p, C.c_uint64, u64p]),
+    "mbrwt_wt_get_labels_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                                   C.c_double, C.c_void_p, C.c_void_p, C.c_uint64, u64p,
+                                                   C.c_void_p]),
+    "mbrwt_wt_get_top_labels_batch": (C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p, C.c_uint64, C.c_uint64, u64p,
+                                                u32p, u64p, C.c_uint64, u64p]),
+    "mbrwt_wt_get_top_labels_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                                       C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p,
+                                                       C.c_void_p, C.c_uint64, u64p, C.c_void_p]),
     "mbrwt_wt_get_batch": (C.c_int, [C.c_void_p, u64p, u64p, C.c_uint64, u8p]),
     "mbrwt_wt_get_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
                                             C.c_void_p]),

@@ -131,6 +131,28 @@ class BinRelWTDevice:
         L.check(st, "mbrwt_wt_get_rows_device")
         return int(need.value)
 
+    # -- batched classify (include/mbrwt_wt.h; semantics as BRWTDevice's) ------
+    def get_labels_batch(self, rows, read_offsets, presence_ratio):
+        from .brwt import _labels_batch
+        return _labels_batch("mbrwt_wt_get_labels_batch", self._h, rows, read_offsets, presence_ratio)
+
+    def get_top_labels_batch(self, rows, read_offsets, num_top=2**64 - 1):
+        from .brwt import _top_labels_batch
+        return _top_labels_batch("mbrwt_wt_get_top_labels_batch", self._h, rows, read_offsets, num_top)
+
+    def get_labels_batch_device(self, rows_t, read_off_t, presence_ratio, lab_off_t, labels_t, stream=None):
+        need = C.c_uint64(0)
+        st = L.lib().mbrwt_wt_get_labels_batch_device(
+            self._h, rows_t.data_ptr(), rows_t.numel(), read_off_t.data_ptr(), read_off_t.numel() - 1,
+            float(presence_ratio), lab_off_t.data_ptr(), labels_t.data_ptr() if labels_t is not None else None,
+            labels_t.numel() if labels_t is not None else 0, C.byref(need), stream)
+        if st == L.MBRWT_ERR_CAPACITY:
+            e = L.MBRWTError(st, "mbrwt_wt_get_labels_batch_device")
+            e.needed = int(need.value)
+            raise e
+        L.check(st, "mbrwt_wt_get_labels_batch_device")
+        return int(need.value)
+
     def set_option(self, option, value):
         L.check(L.lib().mbrwt_wt_set_option(self._h, option, int(value)), "mbrwt_wt_set_option")
 

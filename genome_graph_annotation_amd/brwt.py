@@ -20,6 +20,48 @@ def _p(a, t):
     return a.ctypes.data_as(C.POINTER(t))
 
 
+def _labels_batch(fn, h, rows, read_offsets, presence_ratio):
+    """Host-buffer batched get_labels through `fn` (mbrwt[_wt]_get_labels_batch)."""
+    rows = np.ascontiguousarray(rows, dtype=np.uint64)
+    ro = np.ascontiguousarray(read_offsets, dtype=np.uint64)
+    if ro.size == 0:
+        raise ValueError("read_offsets needs n_reads + 1 entries")
+    lo = np.zeros(ro.size, dtype=np.uint64)
+    need = C.c_uint64(0)
+    cap = max(16, 4 * rows.size)
+    while True:
+        labs = np.zeros(cap, dtype=np.uint32)
+        st = getattr(L.lib(), fn)(h, _p(rows, C.c_uint64), rows.size, _p(ro, C.c_uint64), ro.size - 1,
+                                  float(presence_ratio), _p(lo, C.c_uint64), _p(labs, C.c_uint32), cap, C.byref(need))
+        if st == L.MBRWT_ERR_CAPACITY:
+            cap = int(need.value)
+            continue
+        L.check(st, fn)
+        return lo, labs[: need.value]
+
+
+def _top_labels_batch(fn, h, rows, read_offsets, num_top):
+    """Host-buffer batched get_top_labels through `fn` (mbrwt[_wt]_get_top_labels_batch)."""
+    rows = np.ascontiguousarray(rows, dtype=np.uint64)
+    ro = np.ascontiguousarray(read_offsets, dtype=np.uint64)
+    if ro.size == 0:
+        raise ValueError("read_offsets needs n_reads + 1 entries")
+    lo = np.zeros(ro.size, dtype=np.uint64)
+    need = C.c_uint64(0)
+    cap = max(16, 4 * rows.size)
+    while True:
+        labs = np.zeros(cap, dtype=np.uint32)
+        cnts = np.zeros(cap, dtype=np.uint64)
+        st = getattr(L.lib(), fn)(h, _p(rows, C.c_uint64), rows.size, _p(ro, C.c_uint64), ro.size - 1,
+                                  int(num_top), _p(lo, C.c_uint64), _p(labs, C.c_uint32), _p(cnts, C.c_uint64), cap,
+                                  C.byref(need))
+        if st == L.MBRWT_ERR_CAPACITY:
+            cap = int(need.value)
+            continue
+        L.check(st, fn)
+        return lo, labs[: need.value], cnts[: need.value]
+
+
 class BRWTDevice:
     """A BRWT held in HBM; every query runs the HIP traversal kernels."""
 
@@ -222,49 +264,14 @@ class BRWTDevice:
     def get_labels_batch(self, rows, read_offsets, presence_ratio):
         """Host-buffer form (include/mbrwt.h mbrwt_get_labels_batch): numpy in,
         (label offsets u64 [n_reads+1], labels u32) out."""
-        lib = L.lib()
-        rows = np.ascontiguousarray(rows, dtype=np.uint64)
-        ro = np.ascontiguousarray(read_offsets, dtype=np.uint64)
-        if ro.size == 0:
-            raise ValueError("read_offsets needs n_reads + 1 entries")
-        lo = np.zeros(ro.size, dtype=np.uint64)
-        need = C.c_uint64(0)
-        cap = max(16, 4 * rows.size)
-        while True:
-            labs = np.zeros(cap, dtype=np.uint32)
-            st = lib.mbrwt_get_labels_batch(self._h, _p(rows, C.c_uint64), rows.size, _p(ro, C.c_uint64),
-                                            ro.size - 1, float(presence_ratio), _p(lo, C.c_uint64),
-                                            _p(labs, C.c_uint32), cap, C.byref(need))
-            if st == L.MBRWT_ERR_CAPACITY:
-                cap = int(need.value)
-                continue
-            L.check(st, "mbrwt_get_labels_batch")
-            return lo, labs[: need.value]
+        return _labels_batch("mbrwt_get_labels_batch", self._h, rows, read_offsets, presence_ratio)
 
     def get_top_labels_batch(self, rows, read_offsets, num_top=2**64 - 1):
         """MultiLabelEncoded::get_top_labels(indices, num_top) for many reads
         (include/mbrwt.h mbrwt_get_top_labels_batch): -> (label offsets u64
         [n_reads+1], labels u32, counts u64), each read by count descending,
         equal counts by label ascending."""
-        lib = L.lib()
-        rows = np.ascontiguousarray(rows, dtype=np.uint64)
-        ro = np.ascontiguousarray(read_offsets, dtype=np.uint64)
-        if ro.size == 0:
-            raise ValueError("read_offsets needs n_reads + 1 entries")
-        lo = np.zeros(ro.size, dtype=np.uint64)
-        need = C.c_uint64(0)
-        cap = max(16, 4 * rows.size)
-        while True:
-            labs = np.zeros(cap, dtype=np.uint32)
-            cnts = np.zeros(cap, dtype=np.uint64)
-            st = lib.mbrwt_get_top_labels_batch(self._h, _p(rows, C.c_uint64), rows.size, _p(ro, C.c_uint64),
-                                                ro.size - 1, int(num_top), _p(lo, C.c_uint64), _p(labs, C.c_uint32),
-                                                _p(cnts, C.c_uint64), cap, C.byref(need))
-            if st == L.MBRWT_ERR_CAPACITY:
-                cap = int(need.value)
-                continue
-            L.check(st, "mbrwt_get_top_labels_batch")
-            return lo, labs[: need.value], cnts[: need.value]
+        return _top_labels_batch("mbrwt_get_top_labels_batch", self._h, rows, read_offsets, num_top)
 
     def get_top_labels_batch_device(self, rows_t, read_off_t, num_top, lab_off_t, labels_t, counts_t, stream=None):
         """Device-buffer form on torch tensors (labels int32, counts int64);

@@ -115,15 +115,10 @@ class StaticBinRelAnnotator {
 
     // get_labels(indices, presence_ratio) for a batch of reads (the classify
     // loop over reads, annotated_dbg.cpp:88-110): one device call for all
-    // reads when the matrix is a BRWTDevice, else one get_labels per read
+    // reads when the matrix offers it (BRWTDevice, BinRelWTDevice), else one
+    // get_labels per read
     std::vector<VLabels> get_labels_batch(const std::vector<std::vector<Index>> &reads,
                                           double presence_ratio) const {
-        std::vector<VLabels> out(reads.size());
-        const auto *dev = dynamic_cast<const BRWTDevice *>(matrix_.get());
-        if (!dev) {
-            for (size_t r = 0; r < reads.size(); ++r) out[r] = get_labels(reads[r], presence_ratio);
-            return out;
-        }
         assert(presence_ratio >= 0 && presence_ratio <= 1);
         std::vector<Index> rows;
         std::vector<uint64_t> read_off{0}, lab_off;
@@ -132,7 +127,11 @@ class StaticBinRelAnnotator {
             read_off.push_back(rows.size());
         }
         std::vector<uint32_t> codes;
-        dev->get_labels_batch_csr(rows, read_off, presence_ratio, &lab_off, &codes);
+        std::vector<VLabels> out(reads.size());
+        if (!matrix_->labels_batch_csr(rows, read_off, presence_ratio, &lab_off, &codes)) {
+            for (size_t r = 0; r < reads.size(); ++r) out[r] = get_labels(reads[r], presence_ratio);
+            return out;
+        }
         for (size_t r = 0; r < reads.size(); ++r)
             for (uint64_t i = lab_off[r]; i < lab_off[r + 1]; ++i) out[r].push_back(label_encoder_.decode(codes[i]));
         return out;
@@ -154,16 +153,10 @@ class StaticBinRelAnnotator {
     }
 
     // get_top_labels for a batch of reads (classify --count-labels,
-    // main.cpp:177): one device call when the matrix is a BRWTDevice, else
-    // one get_top_labels per read
+    // main.cpp:177): one device call when the matrix offers it, else one
+    // get_top_labels per read
     std::vector<std::vector<std::pair<Label, size_t>>> get_top_labels_batch(
         const std::vector<std::vector<Index>> &reads, size_t num_top = static_cast<size_t>(-1)) const {
-        std::vector<std::vector<std::pair<Label, size_t>>> out(reads.size());
-        const auto *dev = dynamic_cast<const BRWTDevice *>(matrix_.get());
-        if (!dev) {
-            for (size_t r = 0; r < reads.size(); ++r) out[r] = get_top_labels(reads[r], num_top);
-            return out;
-        }
         std::vector<Index> rows;
         std::vector<uint64_t> read_off{0}, lab_off, counts;
         for (const auto &read : reads) {
@@ -171,7 +164,11 @@ class StaticBinRelAnnotator {
             read_off.push_back(rows.size());
         }
         std::vector<uint32_t> codes;
-        dev->get_top_labels_batch_csr(rows, read_off, num_top, &lab_off, &codes, &counts);
+        std::vector<std::vector<std::pair<Label, size_t>>> out(reads.size());
+        if (!matrix_->top_labels_batch_csr(rows, read_off, num_top, &lab_off, &codes, &counts)) {
+            for (size_t r = 0; r < reads.size(); ++r) out[r] = get_top_labels(reads[r], num_top);
+            return out;
+        }
         for (size_t r = 0; r < reads.size(); ++r)
             for (uint64_t i = lab_off[r]; i < lab_off[r + 1]; ++i)
                 out[r].emplace_back(label_encoder_.decode(codes[i]), counts[i]);

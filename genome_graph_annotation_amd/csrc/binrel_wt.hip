@@ -381,6 +381,7 @@ struct WtCtx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     Workspace ws_a, ws_b, ws_c, ws_scan, ws_io;
+    Workspace ws_cls_off, ws_cls_cols, ws_cls_cnt;  // classify: the rows' CSR, per-read counts
     uint64_t *h_scalars = nullptr, *d_scalars = nullptr;
     bool timing = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -403,7 +404,7 @@ struct WtCtx {
         for (void *a : allocs) (void)hipFree(a);
         if (d_offsets) (void)hipFree(d_offsets);
         if (d_chunks) (void)hipFree(d_chunks);
-        for (Workspace *ws : {&ws_a, &ws_b, &ws_c, &ws_scan, &ws_io})
+        for (Workspace *ws : {&ws_a, &ws_b, &ws_c, &ws_scan, &ws_io, &ws_cls_off, &ws_cls_cols, &ws_cls_cnt})
             if (ws->buf) (void)hipFree(ws->buf);
         if (h_scalars) (void)hipHostFree(h_scalars);
         if (d_scalars) (void)hipFree(d_scalars);
@@ -722,6 +723,14 @@ int wt_get_column(WtCtx &c, uint64_t column, uint64_t *d_rows, uint64_t cap, uin
     return MBRWT_OK;
 }
 
+// classify over BinRel-WT rows (classify.hip's driver with wt_get_rows)
+ClassifyIo wt_io(WtCtx &c) { return ClassifyIo{&c.ws_cls_off, &c.ws_cls_cols, &c.ws_cls_cnt, &c.ws_scan}; }
+ClassifyRowsFn wt_rows(WtCtx &c, const uint64_t *d_rows, uint64_t n_rows, hipStream_t s) {
+    return [&c, d_rows, n_rows, s](uint64_t *d_off, uint32_t *d_cols, uint64_t cap, uint64_t *need) {
+        return wt_get_rows(c, d_rows, n_rows, d_off, d_cols, cap, need, s);
+    };
+}
+
 WtCtx *W(mbrwt_wt *p) { return reinterpret_cast<WtCtx *>(p); }
 const WtCtx *W(const mbrwt_wt *p) { return reinterpret_cast<const WtCtx *>(p); }
 
@@ -929,6 +938,117 @@ int mbrwt_wt_take_timing(mbrwt_wt *ctx, double *kernel_ms, uint64_t *launches) {
     c.timing_ms = 0;
     c.timing_launches = 0;
     return MBRWT_OK;
+}
+
+
+int mbrwt_wt_get_labels_batch_device(mbrwt_wt *ctx, const uint64_t *d_rows, uint64_t n_rows,
+                                     const uint64_t *d_read_offsets, uint64_t n_reads, double presence_ratio,
+                                     uint64_t *d_label_offsets, uint32_t *d_labels, uint64_t labels_cap,
+                                     uint64_t *labels_needed, void *stream) {
+    if (!ctx || (n_rows && !d_rows) || !d_read_offsets || !d_label_offsets) {
+        mbrwt::set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    WtCtx &c = *W(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    return mbrwt::guarded("mbrwt_wt_get_labels_batch_device", [&] {
+        MBRWT_HIP(hipSetDevice(c.device));
+        const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+        return mbrwt::classify_labels(mbrwt::wt_io(c), mbrwt::wt_rows(c, d_rows, n_rows, s), c.num_columns, n_rows,
+                                      d_read_offsets, n_reads, presence_ratio, d_label_offsets, d_labels,
+                                      d_labels ? labels_cap : 0, labels_needed, s);
+    });
+}
+
+int mbrwt_wt_get_top_labels_batch_device(mbrwt_wt *ctx, const uint64_t *d_rows, uint64_t n_rows,
+                                         const uint64_t *d_read_offsets, uint64_t n_reads, uint64_t num_top,
+                                         uint64_t *d_label_offsets, uint32_t *d_labels, uint64_t *d_counts,
+                                         uint64_t labels_cap, uint64_t *labels_needed, void *stream) {
+    if (!ctx || (n_rows && !d_rows) || !d_read_offsets || !d_label_offsets) {
+        mbrwt::set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    WtCtx &c = *W(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    return mbrwt::guarded("mbrwt_wt_get_top_labels_batch_device", [&] {
+        MBRWT_HIP(hipSetDevice(c.device));
+        const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+        const bool out = d_labels && d_counts;
+        return mbrwt::classify_top_labels(mbrwt::wt_io(c), mbrwt::wt_rows(c, d_rows, n_rows, s), c.num_columns,
+                                          n_rows, d_read_offsets, n_reads, num_top, d_label_offsets, d_labels,
+                                          d_counts, out ? labels_cap : 0, labels_needed, s);
+    });
+}
+
+// host-buffer forms: rows | read offsets | label offsets in ws_a, labels (+ counts) in ws_b
+int mbrwt_wt_get_labels_batch(mbrwt_wt *ctx, const uint64_t *rows, uint64_t n_rows, const uint64_t *read_offsets,
+                              uint64_t n_reads, double presence_ratio, uint64_t *label_offsets, uint32_t *labels,
+                              uint64_t labels_cap, uint64_t *labels_needed) {
+    if (!ctx || (n_rows && !rows) || !read_offsets || !label_offsets) {
+        mbrwt::set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    WtCtx &c = *W(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    return mbrwt::guarded("mbrwt_wt_get_labels_batch", [&] {
+        MBRWT_HIP(hipSetDevice(c.device));
+        int rc;
+        if ((rc = mbrwt::ensure(c.ws_a, (n_rows + 2 * (n_reads + 1)) * sizeof(uint64_t)))) return rc;
+        if ((rc = mbrwt::ensure(c.ws_b, std::max<uint64_t>(labels_cap, 1) * sizeof(uint32_t)))) return rc;
+        uint64_t *d_rows = reinterpret_cast<uint64_t *>(c.ws_a.buf);
+        uint64_t *d_roff = d_rows + n_rows, *d_loff = d_roff + n_reads + 1;
+        if (n_rows) MBRWT_HIP(hipMemcpyAsync(d_rows, rows, n_rows * 8, hipMemcpyHostToDevice, c.stream));
+        MBRWT_HIP(hipMemcpyAsync(d_roff, read_offsets, (n_reads + 1) * 8, hipMemcpyHostToDevice, c.stream));
+        uint64_t need = 0;
+        rc = mbrwt::classify_labels(mbrwt::wt_io(c), mbrwt::wt_rows(c, d_rows, n_rows, c.stream), c.num_columns,
+                                    n_rows, d_roff, n_reads, presence_ratio, d_loff,
+                                    labels ? reinterpret_cast<uint32_t *>(c.ws_b.buf) : nullptr,
+                                    labels ? labels_cap : 0, &need, c.stream);
+        if (labels_needed) *labels_needed = need;
+        if (rc) return rc;
+        MBRWT_HIP(hipMemcpyAsync(label_offsets, d_loff, (n_reads + 1) * 8, hipMemcpyDeviceToHost, c.stream));
+        if (need) MBRWT_HIP(hipMemcpyAsync(labels, c.ws_b.buf, need * 4, hipMemcpyDeviceToHost, c.stream));
+        MBRWT_HIP(hipStreamSynchronize(c.stream));
+        return (int)MBRWT_OK;
+    });
+}
+
+int mbrwt_wt_get_top_labels_batch(mbrwt_wt *ctx, const uint64_t *rows, uint64_t n_rows, const uint64_t *read_offsets,
+                                  uint64_t n_reads, uint64_t num_top, uint64_t *label_offsets, uint32_t *labels,
+                                  uint64_t *counts, uint64_t labels_cap, uint64_t *labels_needed) {
+    if (!ctx || (n_rows && !rows) || !read_offsets || !label_offsets) {
+        mbrwt::set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    WtCtx &c = *W(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    return mbrwt::guarded("mbrwt_wt_get_top_labels_batch", [&] {
+        MBRWT_HIP(hipSetDevice(c.device));
+        int rc;
+        if ((rc = mbrwt::ensure(c.ws_a, (n_rows + 2 * (n_reads + 1)) * sizeof(uint64_t)))) return rc;
+        const uint64_t lab_words = (std::max<uint64_t>(labels_cap, 1) + 1) & ~1ull;
+        if ((rc = mbrwt::ensure(c.ws_b, lab_words * 4 + std::max<uint64_t>(labels_cap, 1) * 8))) return rc;
+        uint64_t *d_rows = reinterpret_cast<uint64_t *>(c.ws_a.buf);
+        uint64_t *d_roff = d_rows + n_rows, *d_loff = d_roff + n_reads + 1;
+        uint32_t *d_lab = reinterpret_cast<uint32_t *>(c.ws_b.buf);
+        uint64_t *d_cnt = reinterpret_cast<uint64_t *>(d_lab + lab_words);
+        if (n_rows) MBRWT_HIP(hipMemcpyAsync(d_rows, rows, n_rows * 8, hipMemcpyHostToDevice, c.stream));
+        MBRWT_HIP(hipMemcpyAsync(d_roff, read_offsets, (n_reads + 1) * 8, hipMemcpyHostToDevice, c.stream));
+        uint64_t need = 0;
+        const bool out = labels && counts;
+        rc = mbrwt::classify_top_labels(mbrwt::wt_io(c), mbrwt::wt_rows(c, d_rows, n_rows, c.stream), c.num_columns,
+                                        n_rows, d_roff, n_reads, num_top, d_loff, out ? d_lab : nullptr,
+                                        out ? d_cnt : nullptr, out ? labels_cap : 0, &need, c.stream);
+        if (labels_needed) *labels_needed = need;
+        if (rc) return rc;
+        MBRWT_HIP(hipMemcpyAsync(label_offsets, d_loff, (n_reads + 1) * 8, hipMemcpyDeviceToHost, c.stream));
+        if (need) {
+            MBRWT_HIP(hipMemcpyAsync(labels, d_lab, need * 4, hipMemcpyDeviceToHost, c.stream));
+            MBRWT_HIP(hipMemcpyAsync(counts, d_cnt, need * 8, hipMemcpyDeviceToHost, c.stream));
+        }
+        MBRWT_HIP(hipStreamSynchronize(c.stream));
+        return (int)MBRWT_OK;
+    });
 }
 
 }  // extern "C"

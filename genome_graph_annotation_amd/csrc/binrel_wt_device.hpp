@@ -79,6 +79,60 @@ class BinRelWTDevice : public BinaryMatrix {
         return out;
     }
 
+    // batched classify (include/mbrwt_wt.h mbrwt_wt_get[_top]_labels_batch)
+    bool labels_batch_csr(const std::vector<Row> &rows, const std::vector<uint64_t> &read_offsets, double ratio,
+                          std::vector<uint64_t> *lab_off, std::vector<uint32_t> *labels) const override {
+        if (read_offsets.empty()) throw std::invalid_argument("read_offsets needs n_reads + 1 entries");
+        lab_off->assign(read_offsets.size(), 0);
+        labels->clear();
+        if (!ctx_) {
+            if (!rows.empty()) throw std::out_of_range("get_labels on an empty BinRelWT");
+            return true;
+        }
+        uint64_t cap = std::max<uint64_t>(16, 4 * rows.size()), need = 0;
+        for (;;) {
+            labels->resize(cap);
+            int st = mbrwt_wt_get_labels_batch(ctx_.get(), rows.data(), rows.size(), read_offsets.data(),
+                                               read_offsets.size() - 1, ratio, lab_off->data(), labels->data(), cap,
+                                               &need);
+            if (st == MBRWT_ERR_CAPACITY) {
+                cap = need;
+                continue;
+            }
+            check_status(st, "BinRelWTDevice::get_labels_batch");
+            labels->resize(need);
+            return true;
+        }
+    }
+    bool top_labels_batch_csr(const std::vector<Row> &rows, const std::vector<uint64_t> &read_offsets,
+                              uint64_t num_top, std::vector<uint64_t> *lab_off, std::vector<uint32_t> *labels,
+                              std::vector<uint64_t> *counts) const override {
+        if (read_offsets.empty()) throw std::invalid_argument("read_offsets needs n_reads + 1 entries");
+        lab_off->assign(read_offsets.size(), 0);
+        labels->clear();
+        counts->clear();
+        if (!ctx_) {
+            if (!rows.empty()) throw std::out_of_range("get_top_labels on an empty BinRelWT");
+            return true;
+        }
+        uint64_t cap = std::max<uint64_t>(16, 4 * rows.size()), need = 0;
+        for (;;) {
+            labels->resize(cap);
+            counts->resize(cap);
+            int st = mbrwt_wt_get_top_labels_batch(ctx_.get(), rows.data(), rows.size(), read_offsets.data(),
+                                                   read_offsets.size() - 1, num_top, lab_off->data(), labels->data(),
+                                                   counts->data(), cap, &need);
+            if (st == MBRWT_ERR_CAPACITY) {
+                cap = need;
+                continue;
+            }
+            check_status(st, "BinRelWTDevice::get_top_labels_batch");
+            labels->resize(need);
+            counts->resize(need);
+            return true;
+        }
+    }
+
     std::vector<Row> get_column(Column column) const override {
         if (!ctx_) throw std::out_of_range("get_column on an empty BinRelWT");
         uint64_t need = 0;

@@ -49,6 +49,19 @@ class BinaryMatrix {
 
     // number of ones in the matrix
     virtual uint64_t num_relations() const = 0;
+
+    // Batched classify on the device (get_labels / get_top_labels for many
+    // reads, CSR over reads); false = not offered by this scheme, and the
+    // annotator answers read by read
+    virtual bool labels_batch_csr(const std::vector<Row> &, const std::vector<uint64_t> &, double,
+                                  std::vector<uint64_t> *, std::vector<uint32_t> *) const {
+        return false;
+    }
+    virtual bool top_labels_batch_csr(const std::vector<Row> &, const std::vector<uint64_t> &, uint64_t,
+                                      std::vector<uint64_t> *, std::vector<uint32_t> *,
+                                      std::vector<uint64_t> *) const {
+        return false;
+    }
 };
 
 class MBRWTException : public std::runtime_error {
@@ -213,6 +226,18 @@ class BRWTDevice : public BinaryMatrix {
             counts->resize(need);
             return;
         }
+    }
+
+    bool labels_batch_csr(const std::vector<Row> &rows, const std::vector<uint64_t> &read_offsets, double ratio,
+                          std::vector<uint64_t> *lab_off, std::vector<uint32_t> *labels) const override {
+        get_labels_batch_csr(rows, read_offsets, ratio, lab_off, labels);
+        return true;
+    }
+    bool top_labels_batch_csr(const std::vector<Row> &rows, const std::vector<uint64_t> &read_offsets,
+                              uint64_t num_top, std::vector<uint64_t> *lab_off, std::vector<uint32_t> *labels,
+                              std::vector<uint64_t> *counts) const override {
+        get_top_labels_batch_csr(rows, read_offsets, num_top, lab_off, labels, counts);
+        return true;
     }
 
     // CSR form: offsets[rows.size()+1], cols in the reference's per-row order

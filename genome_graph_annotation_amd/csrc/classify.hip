@@ -247,27 +247,26 @@ unsigned grid_of(uint64_t n) { return (unsigned)std::max<uint64_t>(1, std::min<u
 
 }  // namespace
 
-// The rows of all reads through run_get_rows (CSR in ws_cls_*), then
-// launch(pass 0, counts) per read, a scan into d_lab_off, the capacity check
-// and launch(pass 1, d_lab_off).  Shared by get_labels and get_top_labels.
+// The rows of all reads through the scheme's get_rows (CSR in io.off /
+// io.cols, grown on MBRWT_ERR_CAPACITY), then launch(pass 0, counts) per
+// read, a scan into d_lab_off, the capacity check and launch(pass 1,
+// d_lab_off).  Shared by get_labels and get_top_labels of both schemes.
 template <class Launch>
-int classify_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, uint64_t n_reads, uint64_t *d_lab_off,
-                   bool have_out, uint64_t cap, uint64_t *needed, hipStream_t s, Launch launch) {
+int classify_batch(const ClassifyIo &io, const ClassifyRowsFn &get_rows, uint64_t n_rows, uint64_t n_reads,
+                   uint64_t *d_lab_off, bool have_out, uint64_t cap, uint64_t *needed, hipStream_t s, Launch launch) {
     if (!n_reads && n_rows) {  // the one offset would have to be both 0 and n_rows
         set_error("read offsets must ascend from 0 to n_rows");
         return MBRWT_ERR_INVALID;
     }
     int rc;
     // 1. the labels of every row of every read
-    if ((rc = ensure(c.ws_cls_off, (n_rows + 1) * sizeof(uint64_t)))) return rc;
-    uint64_t *d_off = reinterpret_cast<uint64_t *>(c.ws_cls_off.buf);
+    if ((rc = ensure(*io.off, (n_rows + 1) * sizeof(uint64_t)))) return rc;
+    uint64_t *d_off = reinterpret_cast<uint64_t *>(io.off->buf);
     uint64_t need = 0;
-    rc = run_get_rows(c, d_rows, n_rows, d_off, reinterpret_cast<uint32_t *>(c.ws_cls_cols.buf),
-                      c.ws_cls_cols.bytes / sizeof(uint32_t), &need, s);
+    rc = get_rows(d_off, reinterpret_cast<uint32_t *>(io.cols->buf), io.cols->bytes / sizeof(uint32_t), &need);
     if (rc == MBRWT_ERR_CAPACITY) {
-        if ((rc = ensure(c.ws_cls_cols, (need + need / 8 + 1024) * sizeof(uint32_t)))) return rc;
-        rc = run_get_rows(c, d_rows, n_rows, d_off, reinterpret_cast<uint32_t *>(c.ws_cls_cols.buf),
-                          c.ws_cls_cols.bytes / sizeof(uint32_t), &need, s);
+        if ((rc = ensure(*io.cols, (need + need / 8 + 1024) * sizeof(uint32_t)))) return rc;
+        rc = get_rows(d_off, reinterpret_cast<uint32_t *>(io.cols->buf), io.cols->bytes / sizeof(uint32_t), &need);
     }
     if (rc) return rc;
     if (!n_reads) {
@@ -276,19 +275,19 @@ int classify_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, uint64_t n_r
         if (needed) *needed = 0;
         return MBRWT_OK;
     }
-    const uint32_t *d_cols = reinterpret_cast<const uint32_t *>(c.ws_cls_cols.buf);
+    const uint32_t *d_cols = reinterpret_cast<const uint32_t *>(io.cols->buf);
     // 2. per-read counts, inclusive scan -> d_lab_off[1..n_reads]
     //    (d_cnt[n_reads] = the malformed-offsets flag)
-    if ((rc = ensure(c.ws_sort, (n_reads + 1) * sizeof(uint64_t)))) return rc;
-    uint64_t *d_cnt = reinterpret_cast<uint64_t *>(c.ws_sort.buf);
+    if ((rc = ensure(*io.cnt, (n_reads + 1) * sizeof(uint64_t)))) return rc;
+    uint64_t *d_cnt = reinterpret_cast<uint64_t *>(io.cnt->buf);
     MBRWT_HIP(hipMemsetAsync(d_cnt + n_reads, 0, sizeof(uint64_t), s));
     launch(0, d_off, d_cols, d_cnt);
     MBRWT_HIP(hipGetLastError());
     MBRWT_HIP(hipMemsetAsync(d_lab_off, 0, sizeof(uint64_t), s));
     size_t scan_bytes = 0;
     MBRWT_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, d_cnt, d_lab_off + 1, (int)n_reads, s));
-    if ((rc = ensure(c.ws_scan, scan_bytes + 16))) return rc;
-    MBRWT_HIP(hipcub::DeviceScan::InclusiveSum(c.ws_scan.buf, scan_bytes, d_cnt, d_lab_off + 1, (int)n_reads, s));
+    if ((rc = ensure(*io.scan, scan_bytes + 16))) return rc;
+    MBRWT_HIP(hipcub::DeviceScan::InclusiveSum(io.scan->buf, scan_bytes, d_cnt, d_lab_off + 1, (int)n_reads, s));
     uint64_t total = 0, bad = 0;
     MBRWT_HIP(hipMemcpyAsync(&total, d_lab_off + n_reads, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     MBRWT_HIP(hipMemcpyAsync(&bad, d_cnt + n_reads, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
@@ -310,10 +309,9 @@ int classify_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, uint64_t n_r
     return MBRWT_OK;
 }
 
-int run_get_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const uint64_t *d_read_off, uint64_t n_reads,
-                         double ratio, uint64_t *d_lab_off, uint32_t *d_labels, uint64_t cap, uint64_t *needed,
-                         hipStream_t s) {
-    const uint64_t m = c.tree.num_columns;
+int classify_labels(const ClassifyIo &io, const ClassifyRowsFn &get_rows, uint64_t m, uint64_t n_rows,
+                    const uint64_t *d_read_off, uint64_t n_reads, double ratio, uint64_t *d_lab_off, uint32_t *d_labels,
+                    uint64_t cap, uint64_t *needed, hipStream_t s) {
     if (!(ratio >= 0.0 && ratio <= 1.0)) {  // an assert in the reference (annotate_static.cpp:76)
         set_error("presence_ratio outside [0, 1]");
         return MBRWT_ERR_INVALID;
@@ -323,7 +321,7 @@ int run_get_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const 
         return MBRWT_ERR_UNSUPPORTED;
     }
     const size_t lds = std::max<uint64_t>(m, 1) * sizeof(uint32_t);
-    return classify_batch(c, d_rows, n_rows, n_reads, d_lab_off, d_labels != nullptr, cap, needed, s,
+    return classify_batch(io, get_rows, n_rows, n_reads, d_lab_off, d_labels != nullptr, cap, needed, s,
                           [&](int pass, const uint64_t *d_off, const uint32_t *d_cols, uint64_t *cnt_or_off) {
                               hipLaunchKernelGGL(k_read_labels, dim3(grid_of(n_reads)), dim3(kClsThreads), lds, s,
                                                  d_read_off, n_reads, n_rows, d_off, d_cols, (uint32_t)m, ratio,
@@ -331,10 +329,9 @@ int run_get_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const 
                           });
 }
 
-int run_get_top_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const uint64_t *d_read_off,
-                             uint64_t n_reads, uint64_t num_top, uint64_t *d_lab_off, uint32_t *d_labels,
-                             uint64_t *d_counts, uint64_t cap, uint64_t *needed, hipStream_t s) {
-    const uint64_t m = c.tree.num_columns;
+int classify_top_labels(const ClassifyIo &io, const ClassifyRowsFn &get_rows, uint64_t m, uint64_t n_rows,
+                        const uint64_t *d_read_off, uint64_t n_reads, uint64_t num_top, uint64_t *d_lab_off,
+                        uint32_t *d_labels, uint64_t *d_counts, uint64_t cap, uint64_t *needed, hipStream_t s) {
     if (m > kTopMaxColumns) {
         set_error("get_top_labels batch: more than 8192 columns is not supported by this build");
         return MBRWT_ERR_UNSUPPORTED;
@@ -342,7 +339,7 @@ int run_get_top_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, co
     uint32_t P = 2;
     while (P < m) P <<= 1;
     const size_t lds = (size_t)P * sizeof(unsigned long long) + kTopCompact * sizeof(uint32_t);
-    return classify_batch(c, d_rows, n_rows, n_reads, d_lab_off, d_labels && d_counts, cap, needed, s,
+    return classify_batch(io, get_rows, n_rows, n_reads, d_lab_off, d_labels && d_counts, cap, needed, s,
                           [&](int pass, const uint64_t *d_off, const uint32_t *d_cols, uint64_t *cnt_or_off) {
                               if (pass == 0) {  // min(distinct labels, num_top): a u32 histogram suffices
                                   hipLaunchKernelGGL(k_read_labels, dim3(grid_of(n_reads)), dim3(kClsThreads),
@@ -355,6 +352,30 @@ int run_get_top_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, co
                                                  s, d_read_off, n_reads, n_rows, d_off, d_cols, (uint32_t)m, P,
                                                  num_top, cnt_or_off, d_labels, d_counts);
                           });
+}
+
+namespace {
+ClassifyIo brwt_io(Ctx &c) { return ClassifyIo{&c.ws_cls_off, &c.ws_cls_cols, &c.ws_sort, &c.ws_scan}; }
+}  // namespace
+
+int run_get_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const uint64_t *d_read_off, uint64_t n_reads,
+                         double ratio, uint64_t *d_lab_off, uint32_t *d_labels, uint64_t cap, uint64_t *needed,
+                         hipStream_t s) {
+    const ClassifyRowsFn rows = [&](uint64_t *d_off, uint32_t *d_cols, uint64_t cols_cap, uint64_t *need) {
+        return run_get_rows(c, d_rows, n_rows, d_off, d_cols, cols_cap, need, s);
+    };
+    return classify_labels(brwt_io(c), rows, c.tree.num_columns, n_rows, d_read_off, n_reads, ratio, d_lab_off,
+                           d_labels, cap, needed, s);
+}
+
+int run_get_top_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const uint64_t *d_read_off,
+                             uint64_t n_reads, uint64_t num_top, uint64_t *d_lab_off, uint32_t *d_labels,
+                             uint64_t *d_counts, uint64_t cap, uint64_t *needed, hipStream_t s) {
+    const ClassifyRowsFn rows = [&](uint64_t *d_off, uint32_t *d_cols, uint64_t cols_cap, uint64_t *need) {
+        return run_get_rows(c, d_rows, n_rows, d_off, d_cols, cols_cap, need, s);
+    };
+    return classify_top_labels(brwt_io(c), rows, c.tree.num_columns, n_rows, d_read_off, n_reads, num_top, d_lab_off,
+                               d_labels, d_counts, cap, needed, s);
 }
 
 }  // namespace mbrwt

@@ -30,6 +30,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../../include/mbrwt.h"
@@ -251,6 +252,19 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
 int run_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n, uint8_t *d_out, hipStream_t s);
 int run_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts, hipStream_t s);
 // batched get_labels(indices, presence_ratio) (classify.hip)
+// the classify driver, shared by both schemes (classify.hip): the rows'
+// labels come from `get_rows` (device CSR; MBRWT_ERR_CAPACITY + need when
+// cols_cap is too small), workspaces from the scheme's context
+struct ClassifyIo {
+    Workspace *off, *cols, *cnt, *scan;
+};
+using ClassifyRowsFn = std::function<int(uint64_t *d_off, uint32_t *d_cols, uint64_t cols_cap, uint64_t *need)>;
+int classify_labels(const ClassifyIo &io, const ClassifyRowsFn &get_rows, uint64_t m, uint64_t n_rows,
+                    const uint64_t *d_read_off, uint64_t n_reads, double ratio, uint64_t *d_lab_off, uint32_t *d_labels,
+                    uint64_t cap, uint64_t *needed, hipStream_t s);
+int classify_top_labels(const ClassifyIo &io, const ClassifyRowsFn &get_rows, uint64_t m, uint64_t n_rows,
+                        const uint64_t *d_read_off, uint64_t n_reads, uint64_t num_top, uint64_t *d_lab_off,
+                        uint32_t *d_labels, uint64_t *d_counts, uint64_t cap, uint64_t *needed, hipStream_t s);
 int run_get_labels_batch(Ctx &c, const uint64_t *d_rows, uint64_t n_rows, const uint64_t *d_read_off, uint64_t n_reads,
                          double ratio, uint64_t *d_lab_off, uint32_t *d_labels, uint64_t cap, uint64_t *needed,
                          hipStream_t s);

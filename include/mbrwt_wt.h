@@ -74,6 +74,28 @@ int mbrwt_wt_get_column_device(mbrwt_wt *ctx, uint64_t column, uint64_t *d_rows,
                                uint64_t *rows_needed, void *stream);
 
 /* MBRWT_OPT_TIMING only: HIP-event time of the decode kernel of get_rows. */
+/*
+ * Batched classify over a BinRel-WT matrix: get_labels(indices,
+ * presence_ratio) (annotate_static.cpp:71-94) and get_top_labels(indices,
+ * num_top) (annotate.cpp:57-83) for many reads; arguments, output and errors
+ * exactly as mbrwt_get_labels_batch[_device] / mbrwt_get_top_labels_batch[_device]
+ * in mbrwt.h (the same device kernels behind mbrwt_wt_get_rows_device).
+ */
+int mbrwt_wt_get_labels_batch(mbrwt_wt *ctx, const uint64_t *rows, uint64_t n_rows, const uint64_t *read_offsets,
+                              uint64_t n_reads, double presence_ratio, uint64_t *label_offsets, uint32_t *labels,
+                              uint64_t labels_cap, uint64_t *labels_needed);
+int mbrwt_wt_get_labels_batch_device(mbrwt_wt *ctx, const uint64_t *d_rows, uint64_t n_rows,
+                                     const uint64_t *d_read_offsets, uint64_t n_reads, double presence_ratio,
+                                     uint64_t *d_label_offsets, uint32_t *d_labels, uint64_t labels_cap,
+                                     uint64_t *labels_needed, void *stream);
+int mbrwt_wt_get_top_labels_batch(mbrwt_wt *ctx, const uint64_t *rows, uint64_t n_rows, const uint64_t *read_offsets,
+                                  uint64_t n_reads, uint64_t num_top, uint64_t *label_offsets, uint32_t *labels,
+                                  uint64_t *counts, uint64_t labels_cap, uint64_t *labels_needed);
+int mbrwt_wt_get_top_labels_batch_device(mbrwt_wt *ctx, const uint64_t *d_rows, uint64_t n_rows,
+                                         const uint64_t *d_read_offsets, uint64_t n_reads, uint64_t num_top,
+                                         uint64_t *d_label_offsets, uint32_t *d_labels, uint64_t *d_counts,
+                                         uint64_t labels_cap, uint64_t *labels_needed, void *stream);
+
 int mbrwt_wt_set_option(mbrwt_wt *ctx, int option, int64_t value);
 int mbrwt_wt_take_timing(mbrwt_wt *ctx, double *kernel_ms, uint64_t *launches);
 
