@@ -1,26 +1,41 @@
 """bench.py -- get_rows()/s on a Kingsford-shaped Multi-BRWT (BASELINE.json).
 
-Workload (config.workload): BASELINE.json configs[3] shape on one GPU per rank
--- a 3.7 B x 2,652 Multi-BRWT (i.i.d. d = 0.3 % columns, basic arity-8
-partitioner, generated top-down on the device: DESIGN.md "Synthetic
-matrices"), replicated on every GPU; each rank queries its own 8 M-row batch
-(uniform 64-bit row ids, seed 42 + rank).  One step = one batched get_rows
-over the rank's batch, device-resident row ids -> CSR in HBM, plus (N > 1)
-the RCCL all-gatherv that reassembles the global CSR on every rank.
+Workload (config.workload): BASELINE.json configs[3] -- a 3.7 B x 2,652
+Multi-BRWT (i.i.d. d = 0.3 % columns, basic arity-8 partitioner, generated
+top-down on the device: DESIGN.md "Synthetic matrices"), replicated on every
+GPU, queried with a GLOBAL batch of 8 M uniform random rows (seed 42) cut into
+contiguous per-rank slices (strong scaling, SURVEY.md §8(d) C4: 8 M / N rows
+per GPU; --scaling weak keeps 8 M rows per GPU instead).  One step = one
+batched get_rows over the rank's slice, device-resident row ids -> CSR in HBM,
+plus (N > 1) the RCCL all-gatherv that reassembles the global CSR on every
+rank (pipelined: step k's exchange overlaps step k+1's traversal).
 
-Prints ONE JSON line (rank 0).  roofline: algorithmic bytes of the traversal
-kernel per launch (64 B x V + 8 + 8 + 4 B x L per row, V and
-L counted exactly on the device for the batch) / its HIP-event-timed average
-duration.  cpu_baseline: the oracle's restatement of BRWT::get_row on the
-same structure (generated on the host from the same spec), timed on a bounded
-row sample on all host cores.
+Prints ONE JSON line (rank 0).
+  roofline  -- the traversal kernel's measured HBM traffic per launch
+               (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, one child pass
+               each over this same workload, at N = 1 before the timed run)
+               / its HIP-event-timed average duration / the 8 TB/s spec
+               (frac); beside it the SURVEY §8(d) algorithmic bytes
+               (64 B x V + 8 + 8 + 4 B x L per row, V and L counted exactly on
+               the device for the batch) as alg_achieved / alg_frac, and the
+               measured ceilings: a streaming read and random 64-byte
+               requests (tools/probe.hip).
+  cpu_baseline -- the oracle's restatement of BRWT::get_row on the same
+               structure (built on the host from the same spec), on a bounded
+               row sample, on the job's host cores and single-threaded.
+  parity    -- the whole global batch's CSR against the oracle, element-wise
+               and by a 64-bit hash (N = 1 and, on rank 0, N > 1).
 """
 from __future__ import annotations
 
 import argparse
+import glob
+import hashlib
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -32,6 +47,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "get_rows()/s on Multi-BRWT, 3.7B×2,652 Kingsford-shape @1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level table (spec)
+# FETCH_SIZE per random 64-byte segment read, calibrated on a known count of
+# exactly that access shape (profiles/r01/calib_gather_probe*: factor 1.000;
+# the guide's 1/2 under-count applies to wide streaming reads)
+FETCH_CALIB = 1.0
 
 
 def parse():
@@ -43,25 +62,124 @@ def parse():
     ap.add_argument("--cols", type=int, default=2652)
     ap.add_argument("--density", type=float, default=0.003)
     ap.add_argument("--arity", type=int, default=8)
-    ap.add_argument("--batch", type=int, default=8_000_000, help="query rows per GPU")
+    ap.add_argument("--batch", type=int, default=8_000_000,
+                    help="query rows: the global batch (strong) or rows per GPU (weak)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the all-gatherv reassembly")
-    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
-    ap.add_argument("--cpu-sample", type=int, default=400_000, help="rows timed on the CPU")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host cores")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the host oracle (CPU baseline and parity)")
+    ap.add_argument("--cpu-sample", type=int, default=400_000, help="rows timed on the CPU (job's cores)")
+    ap.add_argument("--cpu-sample-1t", type=int, default=40_000, help="rows timed on one CPU thread")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the job's CPU share")
     ap.add_argument("--check-rows", type=int, default=0,
-                    help="GPU rows checked element-wise against the oracle (0 = the whole batch)")
+                    help="rows checked element-wise against the oracle (0 = the whole global batch)")
     ap.add_argument("--kernel", type=int, default=0, help="MBRWT_OPT_KERNEL variant (0 = library default)")
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--traffic", choices=["live", "committed", "off"], default="live",
+                    help="roofline traffic: rocprofv3 PMC child passes (N = 1), a committed summary of the "
+                         "same kernel sources, or none")
+    ap.add_argument("--traffic-out", default="", help="write the live traffic summary (JSON) here")
+    ap.add_argument("--no-probe", action="store_true", help="skip the measured ceilings")
+    ap.add_argument("--pmc-pass", action="store_true", help=argparse.SUPPRESS)  # child under rocprofv3
     return ap.parse_args()
 
 
-def committed_traffic(cfg):
-    """Per-launch HBM traffic of the traversal kernel from the committed PMC
-    summary of this exact workload (profiles/*/traffic_*.json, written by
-    tools/pmc_traffic.py from separate rocprofv3 --pmc passes of this script),
-    or None when no summary matches."""
-    import glob
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def kernel_source_hash():
+    """sha256 (16 hex) of the product's HIP/C++ sources: a traffic summary is
+    only valid for the kernels it was measured on."""
+    h = hashlib.sha256()
+    for p in sorted(glob.glob(os.path.join(ROOT, "genome_graph_annotation_amd", "csrc", "*"))):
+        if p.endswith((".hip", ".hpp", ".cpp", ".h")):
+            h.update(os.path.basename(p).encode())
+            with open(p, "rb") as f:
+                h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def workload_args(a):
+    return ["--rows", str(a.rows), "--cols", str(a.cols), "--density", repr(a.density), "--arity", str(a.arity),
+            "--batch", str(a.batch), "--seed", str(a.seed), "--kernel", str(a.kernel)]
+
+
+def pmc_pass(a):
+    """Child under rocprofv3 --pmc: the structure and the rank-0 batch of an
+    N = 1 run, 2 warm-up + 3 counted launches of the traversal."""
+    from genome_graph_annotation_amd import BRWTDevice, _lib as L
+    torch.cuda.set_device(0)
+    mat = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, device=0)
+    if a.kernel:
+        mat.set_option(L.MBRWT_OPT_KERNEL, a.kernel)
+    rows_np = np.random.default_rng(a.seed).integers(0, a.rows, a.batch, dtype=np.uint64)
+    rows_t = torch.from_numpy(rows_np.view(np.int64)).cuda()
+    off_t = torch.empty(a.batch + 1, dtype=torch.int64, device="cuda")
+    cols_t = torch.empty(a.batch * 16 + 1024, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(5):
+        mat.get_rows_device(rows_t, off_t, cols_t, s)
+    torch.cuda.synchronize()
+    print(json.dumps({"kernel_name": mat.traverse_kernel()}), flush=True)
+
+
+def per_dispatch(csv_path, kernel_re, counter):
+    import csv
+    import re
+    vals = {}
+    with open(csv_path, newline="") as f:
+        for r in csv.DictReader(f):
+            if r.get("Counter_Name") != counter or not re.search(kernel_re, r.get("Kernel_Name", "")):
+                continue
+            vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return [vals[k] for k in sorted(vals, key=int)]
+
+
+def live_traffic(a, kernel_re):
+    """Per-launch FETCH_SIZE / WRITE_SIZE of the traversal kernel from two
+    rocprofv3 --pmc child passes (separate passes: FETCH_SIZE takes 3 of the 4
+    TCC slots, WRITE_SIZE 2; MI355X_MICROARCH.md).  KiB -> bytes; the first
+    two dispatches are warm-up."""
+    out = {"counters": {}, "source_hash": kernel_source_hash(), "kernel_regex": kernel_re,
+           "config": {"rows": a.rows, "cols": a.cols, "density": a.density, "arity": a.arity, "batch": a.batch,
+                      "kernel": a.kernel}}
+    env = dict(os.environ, TMPDIR="/tmp")
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="bench_pmc_", dir="/tmp")
+        cmd = ["rocprofv3", "--pmc", counter, "--kernel-include-regex", kernel_re, "-d", d, "-o", "run",
+               "--output-format", "csv", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-pass",
+               *workload_args(a)]
+        t0 = time.time()
+        try:
+            r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=240)
+        except (OSError, subprocess.TimeoutExpired) as e:
+            log(f"PMC pass {counter} failed: {e!r}")
+            return None
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if r.returncode != 0 or not files:
+            log(f"PMC pass {counter} failed (rc {r.returncode}): {r.stderr[-600:]}")
+            return None
+        vals = per_dispatch(files[0], kernel_re, counter)
+        if len(vals) < 3:
+            log(f"PMC pass {counter}: {len(vals)} dispatches of {kernel_re!r}")
+            return None
+        kib = float(np.median(vals[2:]))
+        out["counters"][counter] = {"per_dispatch_kib": vals, "median_kib": kib, "pass_s": round(time.time() - t0, 1)}
+        log(f"PMC {counter}: {kib * 1024 / 1e9:.3f} GB per launch ({len(vals)} dispatches, {time.time() - t0:.0f} s)")
+    out["read_bytes"] = out["counters"]["FETCH_SIZE"]["median_kib"] * 1024 * FETCH_CALIB
+    out["write_bytes"] = out["counters"]["WRITE_SIZE"]["median_kib"] * 1024
+    out["traffic_bytes"] = out["read_bytes"] + out["write_bytes"]
+    out["fetch_calibration"] = FETCH_CALIB
+    return out
+
+
+def committed_traffic(a, kernel_re):
+    """A committed live-traffic summary (profiles/*/traffic_*.json) of this
+    workload measured on the CURRENT kernel sources, or None."""
+    want_cfg = {"rows": a.rows, "cols": a.cols, "density": a.density, "arity": a.arity, "batch": a.batch,
+                "kernel": a.kernel}
+    h = kernel_source_hash()
     hit = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic_*.json"))):
         try:
@@ -69,22 +187,74 @@ def committed_traffic(cfg):
                 t = json.load(f)
         except (OSError, ValueError):
             continue
-        if {k: str(v) for k, v in cfg.items()} == {k: str(v) for k, v in t.get("config", {}).items()}:
-            hit = (t["traffic_bytes"], os.path.relpath(path, ROOT))
+        if t.get("source_hash") == h and t.get("kernel_regex") == kernel_re and t.get("config") == want_cfg:
+            hit = dict(t, source=os.path.relpath(path, ROOT))
     return hit
 
 
-def log(msg):
-    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+def csr_hash(off: np.ndarray, cols: np.ndarray) -> str:
+    h = hashlib.blake2b(digest_size=8)
+    h.update(np.ascontiguousarray(off, dtype=np.uint64).tobytes())
+    h.update(np.ascontiguousarray(cols, dtype=np.uint32).tobytes())
+    return h.hexdigest()
+
+
+def probe_ceilings(dev_t, stream_ptr, free_bytes):
+    """Measured streaming-read GB/s and random-64-byte requests/s on this GPU
+    (tools/probe.hip); None where the probe library is missing."""
+    import ctypes as C
+    path = os.path.join(ROOT, "tools", "_build", "libprobe.so")
+    if not os.path.exists(path):
+        log("tools/_build/libprobe.so missing: no measured ceilings")
+        return None, None
+    lib = C.CDLL(path)
+    lib.probe_stream_read.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_void_p, C.POINTER(C.c_double)]
+    lib.probe_random64.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.POINTER(C.c_double)]
+    stream_gbs = rnd = None
+    buf = torch.empty(4 << 30, dtype=torch.uint8, device=dev_t)
+    v = C.c_double(0)
+    if lib.probe_stream_read(buf.data_ptr(), buf.numel(), 5, stream_ptr, C.byref(v)) == 0:
+        stream_gbs = v.value
+    del buf
+    # random segments over a buffer far past the 256 MiB Infinity Cache
+    big = min(64 << 30, int(free_bytes * 0.8)) // (1 << 30) << 30
+    if big >= (8 << 30):
+        buf = torch.empty(big, dtype=torch.uint8, device=dev_t)
+        if lib.probe_random64(buf.data_ptr(), buf.numel(), stream_ptr, C.byref(v)) == 0:
+            rnd = {"segments_per_s": v.value, "buffer_gib": big >> 30}
+        del buf
+    torch.cuda.empty_cache()
+    return stream_gbs, rnd
 
 
 def main():
     a = parse()
+    if a.pmc_pass:
+        pmc_pass(a)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
     local = local % max(1, ndev)  # (rehearsal only: several ranks may share one GPU under gloo)
+
+    from genome_graph_annotation_amd import BRWTDevice, _lib as L
+    from genome_graph_annotation_amd.dist import AllGatherV, allgatherv_csr, shard_bounds
+
+    # roofline traffic first: the PMC child passes need the GPU's memory for
+    # their own copy of the structure
+    kernel_re = None
+    traffic = None
+    if rank == 0 and world == 1 and a.traffic != "off":
+        kernel_re = "k_traverse_fast2" if a.kernel == 0 else "k_traverse"
+        if a.traffic == "live":
+            traffic = live_traffic(a, kernel_re)
+            if traffic is not None and a.traffic_out:
+                with open(a.traffic_out, "w") as f:
+                    json.dump(traffic, f, indent=1)
+        if traffic is None:
+            traffic = committed_traffic(a, kernel_re)
+
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -94,8 +264,6 @@ def main():
             dist.init_process_group(a.dist_backend)
     else:
         torch.cuda.set_device(local)
-    from genome_graph_annotation_amd import BRWTDevice, _lib as L
-    from genome_graph_annotation_amd.dist import AllGatherV, allgatherv_csr
 
     dev_t = torch.device("cuda", local)
     t0 = time.time()
@@ -105,9 +273,14 @@ def main():
     if a.kernel:
         mat.set_option(L.MBRWT_OPT_KERNEL, a.kernel)
 
-    rows_np = np.random.default_rng(a.seed + 1000 * rank).integers(0, a.rows, a.batch, dtype=np.uint64)
+    # the global batch (one seed) and this rank's contiguous slice of it
+    G = a.batch if a.scaling == "strong" else a.batch * world
+    rows_global = np.random.default_rng(a.seed).integers(0, a.rows, G, dtype=np.uint64)
+    lo, hi = shard_bounds(G, world, rank)
+    rows_np = rows_global[lo:hi]
+    nb = hi - lo
     rows_t = torch.from_numpy(rows_np.view(np.int64)).to(dev_t)
-    off_t = torch.empty(a.batch + 1, dtype=torch.int64, device=dev_t)
+    off_t = torch.empty(nb + 1, dtype=torch.int64, device=dev_t)
     stream = torch.cuda.current_stream(dev_t)
     sptr = stream.cuda_stream
     # size the label buffer once (capacity protocol), outside the timed region
@@ -127,7 +300,7 @@ def main():
     bufs = [(off_t, cols_t)]
     if gather:
         bufs.append((torch.empty_like(off_t), torch.empty_like(cols_t)))
-    state = {"i": 0, "pending": None}
+    state = {"i": 0, "pending": None, "global": None}
 
     def step():
         o, cb = bufs[state["i"] % len(bufs)]
@@ -135,13 +308,13 @@ def main():
         n_lab = mat.get_rows_device(rows_t, o, cb, sptr)
         if gather:
             if state["pending"] is not None:
-                state["pending"].finish()
+                state["global"] = state["pending"].finish()
             state["pending"] = AllGatherV(o, cb, n_labels=n_lab, num_columns=a.cols)
         return n_lab
 
     def drain():
         if state["pending"] is not None:
-            state["pending"].finish()
+            state["global"] = state["pending"].finish()
             state["pending"] = None
 
     for _ in range(a.warmup):
@@ -169,78 +342,109 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # N > 1: the reassembled global CSR must hold this rank's slice verbatim
-    # (every rank checks its own slice; the verdicts are all-reduced)
-    reassembly = None
     last_off, last_cols = bufs[(state["i"] - 1) % len(bufs)]
+    # the global CSR of the last timed step: this rank's slice (N = 1) or the
+    # all-gathered CSR every rank holds (N > 1)
+    reassembly = None
     if gather:
-        g_off, g_cols = allgatherv_csr(last_off, last_cols, n_labels=n_lab, num_columns=a.cols)
-        lo, hi = rank * a.batch, (rank + 1) * a.batch
+        g_off, g_cols = state["global"]
         b0 = int(g_off[lo].item())
         ok = bool(torch.equal(g_off[lo:hi + 1] - b0, last_off) and
-                  torch.equal(g_cols[b0:b0 + n_lab], last_cols[:n_lab]) and
-                  g_off.numel() == world * a.batch + 1)
+                  torch.equal(g_cols[b0:b0 + n_lab], last_cols[:n_lab]) and g_off.numel() == G + 1)
         flag = torch.tensor([0 if ok else 1], dtype=torch.int64, device=dev_t)
         dist.all_reduce(flag, op=dist.ReduceOp.SUM)
         reassembly = (f"all-gatherv CSR ({g_off.numel() - 1:,} rows, {g_cols.numel():,} labels) holds every "
                       f"rank's slice verbatim" if int(flag.item()) == 0 else f"MISMATCH on {int(flag.item())} ranks")
-        del g_off, g_cols
+        glob_off, glob_cols = g_off, g_cols
+    else:
+        glob_off, glob_cols = last_off, last_cols[:n_lab]
+    chk = min(a.check_rows, G) if a.check_rows > 0 else G
+    have_global = world == 1 or gather
+    if rank == 0 and have_global:
+        off_h = glob_off[: chk + 1].cpu().numpy().view(np.uint64)
+        cols_h = glob_cols[: int(off_h[-1])].cpu().numpy().view(np.uint32)
+    if gather:
+        del g_off, g_cols, glob_off, glob_cols
+        state["global"] = None
 
-    # measured streaming-read rate of this GPU (report beside the spec peak)
-    big = torch.ones(1 << 30, dtype=torch.float32, device=dev_t)  # 4 GiB
-    big.sum()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(5):
-        big.sum()
-    e1.record()
-    torch.cuda.synchronize()
-    stream_gbs = 5 * big.numel() * 4 / (e0.elapsed_time(e1) / 1e3) / 1e9
-    del big
+    # measured ceilings of this GPU (streaming read; random 64-B requests)
+    stream_gbs = rnd = None
+    if rank == 0 and not a.no_probe:
+        free, _ = torch.cuda.mem_get_info(dev_t)
+        stream_gbs, rnd = probe_ceilings(dev_t, sptr, free)
 
-    # exact work accounting for the roofline (untimed diagnostic pass)
+    # exact work accounting for the algorithmic roofline (untimed diagnostic pass)
     visits, labels = mat.count_work_device(rows_t, sptr)
     assert labels == n_lab, (labels, n_lab)
-    alg_bytes = 64 * visits + 16 * a.batch + 4 * labels
+    alg_bytes = 64 * visits + 16 * nb + 4 * labels
     kern_ms = kern_ms_total / max(1, launches)
-    achieved = alg_bytes / (kern_ms / 1e3) / 1e9
-
-    # GPU result of the last timed step for the parity gate
-    chk = min(a.check_rows, a.batch) if a.check_rows > 0 else a.batch
-    off_h = last_off[: chk + 1].cpu().numpy().view(np.uint64)
-    cols_h = last_cols[: int(off_h[-1])].cpu().numpy().view(np.uint32)
+    kname = mat.traverse_kernel()
 
     cpu = None
     parity = None
-    if rank == 0 and world == 1 and not a.no_cpu:
+    if rank == 0 and have_global and not a.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle as O  # CPU baseline leg only
+        import oracle as O  # CPU baseline and parity legs only
 
-        threads = a.cpu_threads or len(os.sched_getaffinity(0))
-        threads = min(threads, 16)
+        nproc = os.cpu_count()
+        share = len(os.sched_getaffinity(0))
+        omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+        threads = a.cpu_threads or (min(share, omp) if omp > 0 else share)
         log(f"building the host oracle structure on {threads} threads")
         g0 = time.time()
         ref = O.OracleTree.topdown(a.rows, a.cols, a.density, a.arity, a.seed, threads)
         gen_s = time.time() - g0
-        log(f"host structure built in {gen_s:.1f} s; checking {chk} rows and timing {a.cpu_sample} rows")
-        off_o, cols_o = ref.get_rows(rows_np[:chk], threads)
-        parity = bool(np.array_equal(off_o, off_h) and np.array_equal(cols_o, cols_h))
+        log(f"host structure built in {gen_s:.1f} s; checking {chk:,} rows")
+        off_o, cols_o = ref.get_rows(rows_global[:chk], threads)
+        exact = bool(np.array_equal(off_o, off_h) and np.array_equal(cols_o, cols_h))
+        parity = {"rows_checked": chk, "labels_checked": int(len(cols_o)), "bit_exact": exact,
+                  "csr_hash_gpu": csr_hash(off_h, cols_h), "csr_hash_oracle": csr_hash(off_o, cols_o),
+                  "scope": ("the whole global batch" if chk == G else f"the first {chk:,} rows of the global batch")
+                           + (f", reassembled by the all-gatherv from {world} ranks" if world > 1 else "")}
         del off_o, cols_o
-        sample = rows_np[: a.cpu_sample]
-        c0 = time.perf_counter()
-        ref.time_rows(sample, threads)
-        cpu_s = time.perf_counter() - c0
-        cpu = {"value": len(sample) / cpu_s, "unit": "rows/s", "cores": threads, "kind": "port",
-               "sample": f"first {len(sample):,} rows of the rank-0 batch on the same {a.rows:,} x {a.cols:,} "
-                         f"structure (oracle restatement of BRWT::get_row, plain rank/select; host build {gen_s:.0f} s)"}
+        if world == 1:
+            sample = rows_global[: a.cpu_sample]
+            c0 = time.perf_counter()
+            ref.time_rows(sample, threads)
+            cpu_s = time.perf_counter() - c0
+            s1 = rows_global[: a.cpu_sample_1t]
+            c0 = time.perf_counter()
+            ref.time_rows(s1, 1)
+            cpu1_s = time.perf_counter() - c0
+            cpu = {"value": len(sample) / cpu_s, "unit": "rows/s", "cores": threads, "kind": "port",
+                   "sample": f"first {len(sample):,} rows of the batch on the same {a.rows:,} x {a.cols:,} "
+                             f"structure (oracle restatement of BRWT::get_row, plain rank/select; host build "
+                             f"{gen_s:.0f} s); {threads} threads = the job's CPU share (OMP_NUM_THREADS / "
+                             f"affinity {share}; nproc {nproc})",
+                   "single_thread": {"value": len(s1) / cpu1_s, "unit": "rows/s", "cores": 1,
+                                     "sample": f"first {len(s1):,} rows"},
+                   "nproc": nproc}
         del ref
 
-    kname = mat.traverse_kernel()
-    tcfg = {"rows": a.rows, "cols": a.cols, "density": a.density, "arity": a.arity, "batch": a.batch,
-            "kernel": a.kernel, "kernel_name": kname}
-    traffic = committed_traffic(tcfg)
+    # roofline: measured traffic (frac) and the §8(d) algorithmic bytes (alg_frac)
+    ks = kern_ms / 1e3
+    roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": kname, "kernel_ms": kern_ms,
+            "achieved": None, "frac": None, "traffic": None,
+            "alg_bytes_per_launch": alg_bytes, "alg_achieved": alg_bytes / ks / 1e9,
+            "alg_frac": alg_bytes / ks / 1e9 / HBM_PEAK_GBS,
+            "visits_per_row": visits / max(1, nb), "labels_per_row": labels / max(1, nb),
+            "stream_read_measured": stream_gbs}
+    if traffic is not None and world == 1:
+        tb = traffic["traffic_bytes"]
+        roof.update({"achieved": tb / ks / 1e9, "frac": tb / ks / 1e9 / HBM_PEAK_GBS, "traffic": tb,
+                     "read_bytes": traffic["read_bytes"], "write_bytes": traffic["write_bytes"],
+                     "traffic_source": traffic.get("source", "live rocprofv3 --pmc passes of this run") +
+                                       f" (sources {traffic['source_hash']})"})
+        req = traffic["read_bytes"] / 64.0  # FETCH_SIZE = 64-byte requests (calibrated)
+        roof["read_requests_per_launch"] = req
+        roof["read_requests_per_s"] = req / ks
+        if rnd is not None:
+            roof["ceiling_random64_per_s"] = rnd["segments_per_s"]
+            roof["ceiling_random64_frac"] = req / ks / rnd["segments_per_s"]
+    elif rnd is not None:
+        roof["ceiling_random64_per_s"] = rnd["segments_per_s"]
 
-    value = world * a.batch * a.steps / elapsed
+    value = G * a.steps / elapsed
     line = {
         "metric": METRIC,
         "value": value,
@@ -250,38 +454,29 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": elapsed / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": a.scaling,
         "vs_baseline": None,
         "dtype": "u32/u64",
-        "data": "synthetic (top-down i.i.d. Bernoulli columns, seed 42; uniform random rows)",
+        "data": "synthetic (top-down i.i.d. Bernoulli columns, seed 42; uniform random rows, seed 42)",
         "config": {
             "workload": f"Multi-BRWT {a.rows:,} x {a.cols:,}, d={a.density}, arity {a.arity} "
-                        f"(Kingsford shape, BASELINE configs[3]); batch {a.batch:,} rows per GPU",
+                        f"(Kingsford shape, BASELINE configs[3]); global batch {G:,} rows, "
+                        f"{nb:,} per GPU ({a.scaling} scaling)",
             "num_rows": a.rows, "num_columns": a.cols, "density": a.density, "arity": a.arity,
-            "batch_per_gpu": a.batch, "global_batch": a.batch * world,
+            "global_batch": G, "batch_per_gpu": nb,
             "parallelism": f"batch-sharded x{world}, tree replicated" + ("" if world == 1 or a.no_gather
                                                                          else ", all-gatherv over " + ("RCCL" if a.dist_backend == "nccl" else a.dist_backend)),
             "structure_bytes": mat.device_bytes(), "setup_s": round(setup_s, 2),
         },
-        "roofline": {
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "stream_read_measured": stream_gbs,
-            "traffic": None if traffic is None else traffic[0],
-            "traffic_source": None if traffic is None else traffic[1] + " (rocprofv3 PMC, calibrated; per launch)",
-            "kernel": kname,
-            "kernel_ms": kern_ms,
-            "alg_bytes_per_launch": alg_bytes, "visits_per_row": visits / a.batch,
-            "labels_per_row": labels / a.batch,
-        },
+        "roofline": roof,
         "cpu_baseline": cpu,
         "reassembly": reassembly,
-        "parity": None if parity is None else f"{'bit-exact' if parity else 'MISMATCH'} on {chk:,} rows"
-                                                f"{' (the whole timed batch)' if chk == a.batch else ''}"
-                                                f" vs the oracle, element-wise CSR",
+        "parity": parity,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

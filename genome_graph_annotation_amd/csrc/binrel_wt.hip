@@ -380,6 +380,7 @@ struct WtCtx {
     uint64_t device_bytes = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
+    WsFenceState fence;  // orders workspace use across callers' streams (mbrwt_internal.hpp)
     Workspace ws_a, ws_b, ws_c, ws_scan, ws_io;
     Workspace ws_cls_off, ws_cls_cols, ws_cls_cnt;  // classify: the rows' CSR, per-read counts
     uint64_t *h_scalars = nullptr, *d_scalars = nullptr;
@@ -410,6 +411,7 @@ struct WtCtx {
         if (d_scalars) (void)hipFree(d_scalars);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
+        destroy_fence(fence);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -493,6 +495,7 @@ int init_common(WtCtx &c, int device, uint64_t num_rows, uint64_t num_columns) {
     MBRWT_HIP(hipMalloc(&c.d_scalars, 8 * sizeof(uint64_t)));
     MBRWT_HIP(hipEventCreate(&c.ev0));
     MBRWT_HIP(hipEventCreate(&c.ev1));
+    MBRWT_HIP(create_fence(c.fence));
     c.num_rows = num_rows;
     c.num_columns = num_columns;
     c.w = symbol_bits(num_columns);
@@ -806,6 +809,7 @@ int mbrwt_wt_get_rows_device(mbrwt_wt *ctx, const uint64_t *d_rows, uint64_t n, 
     }
     WtCtx &c = *W(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    mbrwt::WsFence fence_(c.fence, reinterpret_cast<hipStream_t>(stream));
     return mbrwt::guarded("mbrwt_wt_get_rows_device", [&] {
         MBRWT_HIP(hipSetDevice(c.device));
         return mbrwt::wt_get_rows(c, d_rows, n, d_offsets, d_cols, d_cols ? cols_cap : 0, cols_needed,
@@ -821,6 +825,7 @@ int mbrwt_wt_get_rows(mbrwt_wt *ctx, const uint64_t *rows, uint64_t n, uint64_t 
     }
     WtCtx &c = *W(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    mbrwt::WsFence fence_(c.fence, c.stream);
     return mbrwt::guarded("mbrwt_wt_get_rows", [&] {
         MBRWT_HIP(hipSetDevice(c.device));
         int rc;
@@ -849,6 +854,7 @@ int mbrwt_wt_get_batch_device(mbrwt_wt *ctx, const uint64_t *d_rows, const uint6
     }
     WtCtx &c = *W(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    mbrwt::WsFence fence_(c.fence, reinterpret_cast<hipStream_t>(stream));
     return mbrwt::guarded("mbrwt_wt_get_batch_device", [&] {
         MBRWT_HIP(hipSetDevice(c.device));
         return mbrwt::wt_get_batch(c, d_rows, d_cols, n, d_out, reinterpret_cast<hipStream_t>(stream));
@@ -862,6 +868,7 @@ int mbrwt_wt_get_batch(mbrwt_wt *ctx, const uint64_t *rows, const uint64_t *cols
     }
     WtCtx &c = *W(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    mbrwt::WsFence fence_(c.fence, c.stream);
     return mbrwt::guarded("mbrwt_wt_get_batch", [&] {
         MBRWT_HIP(hipSetDevice(c.device));
         if (!n) return (int)MBRWT_OK;
@@ -888,6 +895,7 @@ int mbrwt_wt_get_column_device(mbrwt_wt *ctx, uint64_t column, uint64_t *d_rows,
     }
     WtCtx &c = *W(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    mbrwt::WsFence fence_(c.fence, reinterpret_cast<hipStream_t>(stream));
     return mbrwt::guarded("mbrwt_wt_get_column_device", [&] {
         MBRWT_HIP(hipSetDevice(c.device));
         return mbrwt::wt_get_column(c, column, d_rows, d_rows ? rows_cap : 0, rows_needed,
@@ -902,6 +910,7 @@ int mbrwt_wt_get_column(mbrwt_wt *ctx, uint64_t column, uint64_t *rows, uint64_t
     }
     WtCtx &c = *W(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    mbrwt::WsFence fence_(c.fence, c.stream);
     return mbrwt::guarded("mbrwt_wt_get_column", [&] {
         MBRWT_HIP(hipSetDevice(c.device));
         int rc;
@@ -951,6 +960,7 @@ int mbrwt_wt_get_labels_batch_device(mbrwt_wt *ctx, const uint64_t *d_rows, uint
     }
     WtCtx &c = *W(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    mbrwt::WsFence fence_(c.fence, reinterpret_cast<hipStream_t>(stream));
     return mbrwt::guarded("mbrwt_wt_get_labels_batch_device", [&] {
         MBRWT_HIP(hipSetDevice(c.device));
         const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -970,6 +980,7 @@ int mbrwt_wt_get_top_labels_batch_device(mbrwt_wt *ctx, const uint64_t *d_rows, 
     }
     WtCtx &c = *W(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    mbrwt::WsFence fence_(c.fence, reinterpret_cast<hipStream_t>(stream));
     return mbrwt::guarded("mbrwt_wt_get_top_labels_batch_device", [&] {
         MBRWT_HIP(hipSetDevice(c.device));
         const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -990,6 +1001,7 @@ int mbrwt_wt_get_labels_batch(mbrwt_wt *ctx, const uint64_t *rows, uint64_t n_ro
     }
     WtCtx &c = *W(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    mbrwt::WsFence fence_(c.fence, c.stream);
     return mbrwt::guarded("mbrwt_wt_get_labels_batch", [&] {
         MBRWT_HIP(hipSetDevice(c.device));
         int rc;
@@ -1022,6 +1034,7 @@ int mbrwt_wt_get_top_labels_batch(mbrwt_wt *ctx, const uint64_t *rows, uint64_t 
     }
     WtCtx &c = *W(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    mbrwt::WsFence fence_(c.fence, c.stream);
     return mbrwt::guarded("mbrwt_wt_get_top_labels_batch", [&] {
         MBRWT_HIP(hipSetDevice(c.device));
         int rc;

@@ -99,6 +99,7 @@ class BinRelWTDevice : public BinaryMatrix {
                 cap = need;
                 continue;
             }
+            if (st == MBRWT_ERR_UNSUPPORTED) return false;  // per-read count_labels fallback
             check_status(st, "BinRelWTDevice::get_labels_batch");
             labels->resize(need);
             return true;
@@ -126,6 +127,7 @@ class BinRelWTDevice : public BinaryMatrix {
                 cap = need;
                 continue;
             }
+            if (st == MBRWT_ERR_UNSUPPORTED) return false;  // per-read count_labels fallback
             check_status(st, "BinRelWTDevice::get_top_labels_batch");
             labels->resize(need);
             counts->resize(need);

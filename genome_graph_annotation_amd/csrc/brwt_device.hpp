@@ -230,13 +230,26 @@ class BRWTDevice : public BinaryMatrix {
 
     bool labels_batch_csr(const std::vector<Row> &rows, const std::vector<uint64_t> &read_offsets, double ratio,
                           std::vector<uint64_t> *lab_off, std::vector<uint32_t> *labels) const override {
-        get_labels_batch_csr(rows, read_offsets, ratio, lab_off, labels);
+        // MBRWT_ERR_UNSUPPORTED (more columns than the device histogram holds):
+        // the annotator falls back to per-read count_labels, as the reference
+        // has no column limit there
+        try {
+            get_labels_batch_csr(rows, read_offsets, ratio, lab_off, labels);
+        } catch (const MBRWTException &e) {
+            if (e.status() == MBRWT_ERR_UNSUPPORTED) return false;
+            throw;
+        }
         return true;
     }
     bool top_labels_batch_csr(const std::vector<Row> &rows, const std::vector<uint64_t> &read_offsets,
                               uint64_t num_top, std::vector<uint64_t> *lab_off, std::vector<uint32_t> *labels,
                               std::vector<uint64_t> *counts) const override {
-        get_top_labels_batch_csr(rows, read_offsets, num_top, lab_off, labels, counts);
+        try {
+            get_top_labels_batch_csr(rows, read_offsets, num_top, lab_off, labels, counts);
+        } catch (const MBRWTException &e) {
+            if (e.status() == MBRWT_ERR_UNSUPPORTED) return false;  // per-read fallback
+            throw;
+        }
         return true;
     }
 

@@ -48,6 +48,7 @@ static int upload_tables(Ctx &c) {
     MBRWT_HIP(hipMalloc(&c.d_scalars, 8 * sizeof(uint64_t)));
     MBRWT_HIP(hipEventCreate(&c.ev0));
     MBRWT_HIP(hipEventCreate(&c.ev1));
+    MBRWT_HIP(create_fence(c.fence));
     return MBRWT_OK;
 }
 
@@ -66,6 +67,7 @@ static void release(Ctx *c) {
     if (c->h_scalars) (void)hipHostFree(c->h_scalars);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    destroy_fence(c->fence);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -217,6 +219,7 @@ int mbrwt_get_rows_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, ui
     }
     Ctx &c = *C(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    WsFence fence_(c.fence, reinterpret_cast<hipStream_t>(stream));
     try {
         if (hipSetDevice(c.device) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
         return run_get_rows(c, d_rows, n, d_offsets, d_cols, d_cols ? cols_cap : 0, cols_needed,
@@ -235,6 +238,7 @@ int mbrwt_get_rows(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n, uint64_t *o
     }
     Ctx &c = *C(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    WsFence fence_(c.fence, c.stream);
     try {
         MBRWT_HIP(hipSetDevice(c.device));
         int rc;
@@ -246,7 +250,8 @@ int mbrwt_get_rows(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n, uint64_t *o
         // size the output buffer from a first pass over the batch, then fill
         uint64_t cap = cols_cap;
         if ((rc = ensure(c.ws_out, std::max<uint64_t>(cap, 1) * sizeof(uint32_t)))) return rc;
-        rc = run_get_rows(c, d_rows, n, d_off, reinterpret_cast<uint32_t *>(c.ws_out.buf), cap, &needed, c.stream);
+        rc = run_get_rows(c, d_rows, n, d_off, reinterpret_cast<uint32_t *>(c.ws_out.buf), cols ? cap : 0, &needed,
+                          c.stream);
         if (cols_needed) *cols_needed = needed;
         if (rc) return rc;
         MBRWT_HIP(hipMemcpyAsync(offsets, d_off, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
@@ -268,6 +273,7 @@ int mbrwt_get_column_device(mbrwt_ctx *ctx, uint64_t column, uint64_t *d_rows, u
     }
     Ctx &c = *C(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    WsFence fence_(c.fence, reinterpret_cast<hipStream_t>(stream));
     try {
         MBRWT_HIP(hipSetDevice(c.device));
         return run_get_column(c, column, d_rows, d_rows ? rows_cap : 0, rows_needed,
@@ -285,6 +291,7 @@ int mbrwt_get_column(mbrwt_ctx *ctx, uint64_t column, uint64_t *rows, uint64_t r
     }
     Ctx &c = *C(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    WsFence fence_(c.fence, c.stream);
     try {
         MBRWT_HIP(hipSetDevice(c.device));
         int rc;
@@ -313,6 +320,7 @@ int mbrwt_get_batch_device(mbrwt_ctx *ctx, const uint64_t *d_rows, const uint64_
     }
     Ctx &c = *C(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    WsFence fence_(c.fence, reinterpret_cast<hipStream_t>(stream));
     MBRWT_HIP(hipSetDevice(c.device));
     return run_get_batch(c, d_rows, d_cols, n, d_out, reinterpret_cast<hipStream_t>(stream));
 }
@@ -324,6 +332,7 @@ int mbrwt_get_batch(mbrwt_ctx *ctx, const uint64_t *rows, const uint64_t *cols, 
     }
     Ctx &c = *C(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    WsFence fence_(c.fence, c.stream);
     MBRWT_HIP(hipSetDevice(c.device));
     if (!n) return MBRWT_OK;
     int rc;
@@ -348,6 +357,7 @@ int mbrwt_count_labels_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n
     }
     Ctx &c = *C(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    WsFence fence_(c.fence, reinterpret_cast<hipStream_t>(stream));
     MBRWT_HIP(hipSetDevice(c.device));
     return run_count_labels(c, d_rows, n, d_counts, reinterpret_cast<hipStream_t>(stream));
 }
@@ -362,6 +372,7 @@ int mbrwt_get_labels_batch_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64
     }
     Ctx &c = *C(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    WsFence fence_(c.fence, reinterpret_cast<hipStream_t>(stream));
     try {
         MBRWT_HIP(hipSetDevice(c.device));
         return run_get_labels_batch(c, d_rows, n_rows, d_read_offsets, n_reads, presence_ratio, d_label_offsets,
@@ -382,6 +393,7 @@ int mbrwt_get_labels_batch(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n_rows
     }
     Ctx &c = *C(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    WsFence fence_(c.fence, c.stream);
     try {
         MBRWT_HIP(hipSetDevice(c.device));
         int rc;
@@ -422,6 +434,7 @@ int mbrwt_get_top_labels_batch_device(mbrwt_ctx *ctx, const uint64_t *d_rows, ui
     }
     Ctx &c = *C(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    WsFence fence_(c.fence, reinterpret_cast<hipStream_t>(stream));
     try {
         MBRWT_HIP(hipSetDevice(c.device));
         const bool out = d_labels && d_counts;
@@ -443,6 +456,7 @@ int mbrwt_get_top_labels_batch(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n_
     }
     Ctx &c = *C(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    WsFence fence_(c.fence, c.stream);
     try {
         MBRWT_HIP(hipSetDevice(c.device));
         int rc;
@@ -486,6 +500,7 @@ int mbrwt_count_work_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, 
     }
     Ctx &c = *C(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    WsFence fence_(c.fence, reinterpret_cast<hipStream_t>(stream));
     MBRWT_HIP(hipSetDevice(c.device));
     return run_count_work(c, d_rows, n, sum_visits, sum_labels, reinterpret_cast<hipStream_t>(stream));
 }

@@ -258,6 +258,10 @@ int classify_batch(const ClassifyIo &io, const ClassifyRowsFn &get_rows, uint64_
         set_error("read offsets must ascend from 0 to n_rows");
         return MBRWT_ERR_INVALID;
     }
+    if (n_reads > 0x7FFFFFF0ull) {  // hipCUB scans take int item counts
+        set_error("batch larger than 2^31 reads");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
     int rc;
     // 1. the labels of every row of every read
     if ((rc = ensure(*io.off, (n_rows + 1) * sizeof(uint64_t)))) return rc;

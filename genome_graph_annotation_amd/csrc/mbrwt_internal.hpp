@@ -175,6 +175,41 @@ struct Workspace {
     size_t bytes = 0;
 };
 
+// Cross-stream ordering of a context's workspaces.  A *_device call returns
+// with work still queued on the caller's stream that reads the context's
+// workspaces (compaction, classify pass 1, ...); a later call on ANOTHER
+// stream must not overwrite them before that work has run.  Every entry point
+// that enqueues work holds a WsFence (under the context mutex): it makes the
+// call's stream wait for the previous call's last enqueued work, and records
+// the new call's end on leaving (include/mbrwt.h "Threading").
+struct WsFenceState {
+    hipEvent_t ev = nullptr;
+    bool live = false;
+};
+class WsFence {
+  public:
+    WsFence(WsFenceState &st, hipStream_t s) : st_(st), s_(s) {
+        if (st_.live && st_.ev) (void)hipStreamWaitEvent(s_, st_.ev, 0);
+    }
+    ~WsFence() {
+        if (st_.ev && hipEventRecord(st_.ev, s_) == hipSuccess) st_.live = true;
+    }
+    WsFence(const WsFence &) = delete;
+    WsFence &operator=(const WsFence &) = delete;
+
+  private:
+    WsFenceState &st_;
+    hipStream_t s_;
+};
+inline hipError_t create_fence(WsFenceState &st) {  // on the context's device
+    return hipEventCreateWithFlags(&st.ev, hipEventDisableTiming);
+}
+inline void destroy_fence(WsFenceState &st) {
+    if (st.ev) (void)hipEventDestroy(st.ev);
+    st.ev = nullptr;
+    st.live = false;
+}
+
 struct Ctx {
     int device = 0;
     Tree tree;
@@ -184,6 +219,7 @@ struct Ctx {
     uint32_t *d_col_leaf = nullptr;
     hipStream_t stream = nullptr;       // stream of the host-buffer API
     std::mutex mu;
+    WsFenceState fence;                 // orders workspace use across callers' streams
 
     // reusable device workspace (grown on demand, never inside a timed call
     // once warmed up)

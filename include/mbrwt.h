@@ -30,7 +30,12 @@
  *
  * Threading: a context may be used from several host threads; calls on one
  * context are serialised internally (the reference's get_row is const and
- * called concurrently from a ThreadPool, main.cpp:462-497).
+ * called concurrently from a ThreadPool, main.cpp:462-497).  Device-buffer
+ * calls (*_device) may return with work still queued on the caller's stream;
+ * the context orders its internal workspaces across streams (each call's
+ * stream waits for the previous call's queued work, whichever stream that was
+ * on), so calls on different streams are safe.  The caller's own output
+ * buffers are ready when the caller's stream reaches them.
  */
 #ifndef MBRWT_H
 #define MBRWT_H

@@ -154,6 +154,30 @@ TEST(BRWTCompressed, get_top_labels_batch) {  // test_annotation_BRWT.cpp:344-39
     EXPECT_EQ(all, got[0]);
 }
 
+// More columns than the device's batched histograms hold (8,192 for top labels,
+// 15,360 for get_labels): the batched calls fall back to the per-read path
+// (the reference's get_labels / get_top_labels have no column limit)
+TEST(BRWTCompressed, batch_calls_past_the_device_column_limit) {
+    std::vector<std::pair<uint64_t, VS>> rows;
+    for (uint64_t r = 0; r < 40; ++r) {
+        VS l;
+        for (uint64_t k = 0; k < 1000; ++k) l.push_back("L" + std::to_string((r * 7919 + k * 104729) % 20000));
+        if (r % 3 == 0) l.push_back("L7");
+        rows.push_back({r, l});
+    }
+    auto a = annotator(make_fixture(40, rows));
+    EXPECT_TRUE(a->num_labels() > 15360);
+    const std::vector<std::vector<uint64_t>> reads{{0, 1, 2, 3}, {}, {5, 6, 9, 12, 39}, {7}};
+    auto top = a->get_top_labels_batch(reads, 5);
+    auto lab = a->get_labels_batch(reads, 0.5);
+    EXPECT_EQ(reads.size(), top.size());
+    EXPECT_EQ(reads.size(), lab.size());
+    for (size_t r = 0; r < reads.size(); ++r) {
+        EXPECT_EQ(a->get_top_labels(reads[r], 5), top[r]);
+        EXPECT_EQ(S(a->get_labels(reads[r], 0.5)), S(lab[r]));
+    }
+}
+
 TEST(LabelEncoder, encode_decode) {  // annotate.cpp:12-31, annotate.hpp:128
     mbrwt_host::LabelEncoder<std::string> e;
     EXPECT_EQ(0u, e.insert_and_encode("a"));

@@ -93,3 +93,53 @@ def test_wire_bit_packing_roundtrip():
         out = torch.empty(n, dtype=torch.int32)
         _unpack(words, n, bits, out)
         assert np.array_equal(out.numpy().view(np.uint32), v)
+
+
+def _pipelined_worker(rank, world, port, q):
+    """bench.py's pipelined step shape: batch k's AllGatherV is started, batch
+    k+1 is computed into the other output buffer, then batch k's exchange is
+    finished; every finished global CSR must equal the oracle's answer for
+    its own batch."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle as O
+        from genome_graph_annotation_amd.dist import AllGatherV, shard_bounds
+        t = O.OracleTree.topdown(40_000, 2652, 0.003, 8, 4)
+        batches = [np.random.default_rng(100 + k).integers(0, 40_000, 5_003 + 97 * k, dtype=np.uint64)
+                   for k in range(4)]
+        bufs = [None, None]
+        pending, results = None, []
+        for k, b in enumerate(batches):
+            lo, hi = shard_bounds(len(b), world, rank)
+            off, cols = t.get_rows(b[lo:hi])
+            bufs[k % 2] = (torch.from_numpy(off.view(np.int64)).clone(), torch.from_numpy(cols.view(np.int32)).clone())
+            if pending is not None:
+                results.append(pending.finish())
+            pending = AllGatherV(*bufs[k % 2], n_labels=int(off[-1]), num_columns=2652)
+        results.append(pending.finish())
+        ok = True
+        for b, (g_off, g_cols) in zip(batches, results):
+            ref_off, ref_cols = t.get_rows(b)
+            ok &= np.array_equal(g_off.numpy().view(np.uint64), ref_off) and \
+                np.array_equal(g_cols.numpy().view(np.uint32), ref_cols)
+        q.put((rank, bool(ok), len(results)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipelined_allgatherv_start_finish():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok and n == 4 for _, ok, n in res)

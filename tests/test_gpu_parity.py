@@ -780,3 +780,49 @@ def test_device_relax_of_greedy_trees(oracle_mod, relax):
     off, cols = _check_rows(t, dev, rows, variants=(0,))
     for k in range(0, n, 37):
         assert sorted(cols[off[k]:off[k + 1]].tolist()) == np.nonzero(dense[k])[0].tolist()
+
+
+def test_device_calls_on_two_streams(oracle_mod):
+    """Workspaces are ordered across the callers' streams (include/mbrwt.h
+    "Threading"): a get_rows_device queued on stream A and one issued right
+    after on stream B (no host sync in between) both match the oracle."""
+    import torch
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    n, m = 300_000, 2652
+    dev = BRWTDevice.synthetic(n, m, 0.003, 8, 11)
+    ref = O.OracleTree.topdown(n, m, 0.003, 8, 11)
+    rng = np.random.default_rng(5)
+    batches = [rng.integers(0, n, k).astype(np.uint64) for k in (400_000, 50_000)]
+    want = [ref.get_rows(b) for b in batches]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for b, w, s in zip(batches, want, streams):
+        with torch.cuda.stream(s):
+            rt = torch.from_numpy(b.view(np.int64)).to("cuda", non_blocking=False)
+            ot = torch.empty(len(b) + 1, dtype=torch.int64, device="cuda")
+            ct = torch.empty(len(w[1]) + 16, dtype=torch.int32, device="cuda")
+            s.synchronize()
+            got = dev.get_rows_device(rt, ot, ct, s.cuda_stream)
+            outs.append((got, ot, ct, rt))
+    torch.cuda.synchronize()
+    for (got, ot, ct, _), (off_o, cols_o) in zip(outs, want):
+        assert got == len(cols_o)
+        np.testing.assert_array_equal(ot.cpu().numpy().view(np.uint64), off_o)
+        np.testing.assert_array_equal(ct[:got].cpu().numpy().view(np.uint32), cols_o)
+
+
+def test_get_rows_null_cols_is_a_sizing_call():
+    """mbrwt_get_rows with cols == NULL answers the size (MBRWT_ERR_CAPACITY +
+    cols_needed) whatever cols_cap says, like the other host-form calls."""
+    import ctypes as C
+    from genome_graph_annotation_amd import BRWTDevice, _lib as L
+    d = BRWTDevice.synthetic(10_000, 100, 0.05, 8, 3)
+    rows = np.arange(100, dtype=np.uint64)
+    off_h, cols_h = d.get_rows(rows)
+    offsets = np.zeros(101, dtype=np.uint64)
+    need = C.c_uint64(0)
+    st = L.lib().mbrwt_get_rows(d._h, rows.ctypes.data_as(C.POINTER(C.c_uint64)), 100,
+                                offsets.ctypes.data_as(C.POINTER(C.c_uint64)), None, 1 << 20, C.byref(need))
+    assert st == L.MBRWT_ERR_CAPACITY
+    assert need.value == len(cols_h) > 0
