@@ -345,4 +345,21 @@ int wt_synth_rows(uint64_t row0, uint64_t n, uint64_t num_columns, double densit
     return 0;
 }
 
+int wt_synth_rows_at(const uint64_t *rows, uint64_t n, uint64_t num_columns, double density, uint64_t seed,
+                     uint64_t *offsets, uint32_t *cols, uint64_t cols_cap, uint64_t *cols_needed,
+                     int num_threads) {
+    const uint64_t T = wt_synth_threshold(density);
+    if (num_threads <= 0) num_threads = omp_get_max_threads();
+    std::vector<uint64_t> cnt(n);
+#pragma omp parallel for num_threads(num_threads) schedule(dynamic, 1024)
+    for (int64_t i = 0; i < (int64_t)n; ++i) cnt[i] = wt_synth_row(rows[i], num_columns, T, seed, nullptr, 0);
+    offsets[0] = 0;
+    for (uint64_t i = 0; i < n; ++i) offsets[i + 1] = offsets[i] + cnt[i];
+    if (cols_needed) *cols_needed = offsets[n];
+    if (offsets[n] > cols_cap) return 1;
+#pragma omp parallel for num_threads(num_threads) schedule(dynamic, 1024)
+    for (int64_t i = 0; i < (int64_t)n; ++i) wt_synth_row(rows[i], num_columns, T, seed, cols + offsets[i], cnt[i]);
+    return 0;
+}
+
 }  // extern "C"

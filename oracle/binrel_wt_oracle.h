@@ -62,6 +62,11 @@ uint64_t wt_synth_row(uint64_t row, uint64_t num_columns, uint64_t threshold, ui
 /* CSR of synthetic rows [row0, row0 + n): offsets[n+1] (relative), cols. */
 int wt_synth_rows(uint64_t row0, uint64_t n, uint64_t num_columns, double density, uint64_t seed, uint64_t *offsets,
                   uint32_t *cols, uint64_t cols_cap, uint64_t *cols_needed, int num_threads);
+/* Same for arbitrary rows[0..n) (any order, repeats allowed): the rows of the
+ * full-size parity checks, row-independent by construction. */
+int wt_synth_rows_at(const uint64_t *rows, uint64_t n, uint64_t num_columns, double density, uint64_t seed,
+                     uint64_t *offsets, uint32_t *cols, uint64_t cols_cap, uint64_t *cols_needed,
+                     int num_threads);
 
 #ifdef __cplusplus
 }

@@ -21,6 +21,7 @@
 #include "brwt_oracle.h"
 
 #include <algorithm>
+#include <array>
 #include <cassert>
 #include <cmath>
 #include <cstring>
@@ -697,6 +698,259 @@ std::unique_ptr<Node> generate_topdown(uint64_t n, uint64_t m, double d, uint32_
     return std::move(nodes[0]);
 }
 
+// ---- the same top-down tree queried WITHOUT materialising it ---------------
+// Every index bit of the synthetic tree is a pure function of (node, position):
+// child c of u at position j is bit c of mask(u, j) = T_u(H(K_u, j)), for
+// j < popcount(I_u).  BRWT::get_row (BRWT.cpp:26-53) needs, at a visited node,
+// the bit and the inclusive rank1 (BRWT.cpp:30,43), i.e. the count of bit c over
+// mask(u, 0..j).  So the batch is resolved node by node (depth-first over the
+// shape, so only the lists of one root-to-leaf path of nodes are alive): a node
+// with queries streams its masks over [0, max queried j] in parallel chunks,
+// counting per child, and moves each query down with rank - 1.  Memory is
+// O(batch x depth), time O(sum of streamed lengths): the parity check of the
+// 1 B-row RefSeq shape (158 GB of plain index bits) needs no host structure.
+struct QueryAt {
+    uint64_t pos;  // position in the node's children level (rank1 - 1 at the node)
+    uint32_t qid;  // index of the query row in the batch
+};
+
+// MaskSampler's answer by a branchless binary search (the streamed loops draw
+// ~10^11 masks; the guide table's data-dependent scan mispredicts):
+// k = 1 + #{i < nm-1 : T[i] <= x}, capped at nm (T is nondecreasing).
+struct FlatSampler {
+    std::vector<uint64_t> T;  // padded to a power of two with UINT64_MAX
+    uint32_t P = 1, nm = 1;
+    explicit FlatSampler(const std::vector<uint64_t> &t) : nm((uint32_t)t.size()) {
+        while (P < nm) P <<= 1;
+        T.assign(P, UINT64_MAX);
+        for (uint32_t i = 0; i + 1 < nm; ++i) T[i] = t[i];
+    }
+    inline uint32_t operator()(uint64_t x) const {
+        uint32_t base = 0;
+        for (uint32_t step = P >> 1; step; step >>= 1) base += (T[base + step - 1] <= x) ? step : 0;
+        base += (T[base] <= x) ? 1 : 0;
+        return std::min(base + 1, nm);
+    }
+};
+
+// byte-lane spread of an 8-bit mask: bit c -> byte c (per-child counters)
+static const std::array<uint64_t, 256> kSpread = [] {
+    std::array<uint64_t, 256> s{};
+    for (uint32_t m = 0; m < 256; ++m)
+        for (uint32_t c = 0; c < 8; ++c) s[m] |= (uint64_t)((m >> c) & 1) << (8 * c);
+    return s;
+}();
+
+struct TopdownQuery {
+    const std::vector<ShapeNode> &shape;
+    const std::vector<double> &q;
+    const std::vector<uint32_t> &leaf_col;
+    uint64_t seed;
+    int threads;
+    std::vector<std::pair<uint32_t, uint32_t>> emitted;  // (qid, column) in DFS order
+    uint64_t draws = 0;
+
+    static constexpr uint64_t kChunk = 1ull << 16;
+
+    // Resolve node u's queries (sorted by pos, pos < popcount(I_u)).
+    void visit(int u, std::vector<QueryAt> &&qs) {
+        const auto &sh = shape[u];
+        const size_t a = sh.children.size();
+        std::vector<double> qc(a);
+        for (size_t c = 0; c < a; ++c) qc[c] = q[sh.children[c]];
+        const MaskSampler T(mask_table(qc));
+        const uint64_t K = synth_key(seed, (uint64_t)u);
+        const uint64_t len = qs.back().pos + 1;
+        if (a > 16) throw std::runtime_error("topdown_query: arity > 16");
+        const int64_t nchunks = (int64_t)((len + kChunk - 1) / kChunk);
+        // per chunk: per-child counts, the index of the chunk's first query
+        std::vector<uint64_t> cnt((size_t)nchunks * a, 0);
+        std::vector<size_t> qbeg(nchunks + 1);
+        {
+            size_t i = 0;
+            for (int64_t k = 0; k <= nchunks; ++k) {
+                const uint64_t lo = (uint64_t)k * kChunk;
+                while (i < qs.size() && qs[i].pos < lo) ++i;
+                qbeg[k] = i;
+            }
+        }
+        // children's lists per chunk (positions chunk-local until the scan)
+        std::vector<std::vector<std::vector<QueryAt>>> down(nchunks, std::vector<std::vector<QueryAt>>(a));
+        std::vector<std::vector<std::pair<uint32_t, uint32_t>>> emit(nchunks);
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 4)
+        for (int64_t k = 0; k < nchunks; ++k) {
+            uint64_t local[16] = {0};
+            const uint64_t lo = (uint64_t)k * kChunk, hi = std::min(len, lo + kChunk);
+            size_t i = qbeg[k];
+            const size_t iend = qbeg[k + 1];
+            for (uint64_t j = lo; j < hi;) {
+                const uint64_t next_q = i < iend ? qs[i].pos : hi;
+                if (j < next_q) {
+                    // no query in [j, end): count into byte lanes (<= 255 draws), then flush
+                    const uint64_t end = std::min(next_q, j + 255);
+                    uint64_t acc_lo = 0, acc_hi = 0;
+                    for (; j < end; ++j) {
+                        const uint32_t mk = T(synth_draw(K, j));
+                        acc_lo += kSpread[mk & 255];
+                        acc_hi += kSpread[(mk >> 8) & 255];
+                    }
+                    for (size_t c = 0; c < a; ++c)
+                        local[c] += ((c < 8 ? acc_lo >> (8 * c) : acc_hi >> (8 * (c - 8)))) & 255;
+                    continue;
+                }
+                const uint32_t mask = T(synth_draw(K, j));
+                for (uint32_t m = mask; m; m &= m - 1) ++local[__builtin_ctz(m)];
+                for (; i < iend && qs[i].pos == j; ++i) {
+                    for (uint32_t m = mask; m; m &= m - 1) {
+                        const int c = __builtin_ctz(m);
+                        const int v = sh.children[c];
+                        if (shape[v].children.empty())
+                            emit[k].push_back({qs[i].qid, leaf_col[v]});
+                        else
+                            down[k][c].push_back({local[c] - 1, qs[i].qid});
+                    }
+                }
+                ++j;
+            }
+            for (size_t c = 0; c < a; ++c) cnt[(size_t)k * a + c] = local[c];
+        }
+        draws += len;
+        std::vector<QueryAt>().swap(qs);
+        // concatenate the chunks' outputs in chunk order (parallel copies at
+        // exclusive prefixes): emissions, and per child the positions rebased by
+        // the child's count before the chunk
+        std::vector<size_t> eoff(nchunks + 1, 0);
+        for (int64_t k = 0; k < nchunks; ++k) eoff[k + 1] = eoff[k] + emit[k].size();
+        const size_t e0 = emitted.size();
+        emitted.resize(e0 + eoff[nchunks]);
+        std::vector<uint64_t> base((size_t)nchunks * a), doff((size_t)(nchunks + 1) * a, 0);
+        for (size_t c = 0; c < a; ++c) {
+            uint64_t b = 0;
+            for (int64_t k = 0; k < nchunks; ++k) {
+                base[(size_t)k * a + c] = b;
+                b += cnt[(size_t)k * a + c];
+                doff[(size_t)(k + 1) * a + c] = doff[(size_t)k * a + c] + down[k][c].size();
+            }
+        }
+        std::vector<std::vector<QueryAt>> lists(a);
+        for (size_t c = 0; c < a; ++c) lists[c].resize(doff[(size_t)nchunks * a + c]);
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 16)
+        for (int64_t k = 0; k < nchunks; ++k) {
+            std::copy(emit[k].begin(), emit[k].end(), emitted.begin() + e0 + eoff[k]);
+            std::vector<std::pair<uint32_t, uint32_t>>().swap(emit[k]);
+            for (size_t c = 0; c < a; ++c) {
+                QueryAt *dst = lists[c].data() + doff[(size_t)k * a + c];
+                const uint64_t b = base[(size_t)k * a + c];
+                for (auto &e : down[k][c]) *dst++ = {e.pos + b, e.qid};
+                std::vector<QueryAt>().swap(down[k][c]);
+            }
+        }
+        down.clear();
+        // pre-order: children in order, each child's whole subtree before the next
+        for (size_t c = 0; c < a; ++c)
+            if (!lists[c].empty()) visit(sh.children[c], std::move(lists[c]));
+    }
+};
+
+// Returns 0, or 2 on an out-of-range row.  Output: the reference's order
+// (pre-order of the leaves = ascending columns for the basic partitioner).
+int topdown_query(uint64_t n, uint64_t m, double d, uint32_t arity, uint64_t seed, const uint64_t *rows,
+                  uint64_t nq, int threads, std::vector<uint64_t> &offsets, std::vector<uint32_t> &cols,
+                  uint64_t *draws) {
+    for (uint64_t i = 0; i < nq; ++i)
+        if (rows[i] >= n) return 2;
+    offsets.assign(nq + 1, 0);
+    cols.clear();
+    if (m == 0 || nq == 0) return 0;
+    auto shape = basic_shape(m, arity);
+    std::vector<double> q(shape.size());
+    for (size_t u = 0; u < shape.size(); ++u) q[u] = 1.0 - std::pow(1.0 - d, (double)shape[u].cols);
+    // leaf columns: the basic partitioner keeps the leaves in column order, so
+    // a leaf's column is its pre-order rank among the leaves (RangePartition::get
+    // composed along the path, utils.cpp:689-691)
+    std::vector<uint32_t> leaf_col(shape.size(), UINT32_MAX);
+    {
+        uint32_t next = 0;
+        std::vector<int> st{0};
+        while (!st.empty()) {
+            int u = st.back();
+            st.pop_back();
+            if (shape[u].children.empty()) leaf_col[u] = next++;
+            for (size_t c = shape[u].children.size(); c-- > 0;) st.push_back(shape[u].children[c]);
+        }
+    }
+    threads = resolve_threads(threads);
+    TopdownQuery tq{shape, q, leaf_col, seed, threads, {}, 0};
+
+    // the root's own index bit: Bernoulli(q_root) per row; its inclusive rank
+    // over [0, row] comes from a chunked count of the same draws
+    std::vector<QueryAt> root;
+    {
+        std::vector<std::pair<uint64_t, uint32_t>> sorted(nq);
+        for (uint64_t i = 0; i < nq; ++i) sorted[i] = {rows[i], (uint32_t)i};
+        std::sort(sorted.begin(), sorted.end());
+        const uint64_t Tq = prob_to_threshold(q[0]);
+        const uint64_t K = synth_key(seed, kRootKey);
+        const uint64_t len = sorted.back().first + 1;
+        const uint64_t C = TopdownQuery::kChunk;
+        const int64_t nchunks = (int64_t)((len + C - 1) / C);
+        std::vector<uint64_t> cnt(nchunks);
+        std::vector<size_t> qbeg(nchunks + 1);
+        size_t i = 0;
+        for (int64_t k = 0; k <= nchunks; ++k) {
+            while (i < nq && sorted[i].first < (uint64_t)k * C) ++i;
+            qbeg[k] = i;
+        }
+        std::vector<uint64_t> local_rank(nq, UINT64_MAX);  // by sorted index; MAX = bit unset
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 4)
+        for (int64_t k = 0; k < nchunks; ++k) {
+            const uint64_t lo = (uint64_t)k * C, hi = std::min(len, lo + C);
+            uint64_t ones = 0;
+            size_t ii = qbeg[k];
+            for (uint64_t r = lo; r < hi; ++r) {
+                const bool bit = bern(synth_draw(K, r), Tq);
+                ones += bit;
+                for (; ii < qbeg[k + 1] && sorted[ii].first == r; ++ii) local_rank[ii] = bit ? ones - 1 : UINT64_MAX;
+            }
+            cnt[k] = ones;
+        }
+        tq.draws += len;
+        uint64_t base = 0;
+        for (int64_t k = 0; k < nchunks; ++k) {
+            for (size_t s = qbeg[k]; s < qbeg[k + 1]; ++s)
+                if (local_rank[s] != UINT64_MAX) root.push_back({local_rank[s] + base, sorted[s].second});
+            base += cnt[k];
+        }
+    }
+    if (!root.empty()) {
+        if (shape[0].children.empty()) {  // one-column matrix: the root is the leaf (BRWT.cpp:34-39)
+            for (auto &e : root) tq.emitted.push_back({e.qid, 0});
+        } else {
+            tq.visit(0, std::move(root));
+        }
+    }
+    // bucket the emissions by query (parallel, atomic counters) ...
+    const int64_t ne = (int64_t)tq.emitted.size();
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (int64_t e = 0; e < ne; ++e) __atomic_fetch_add(&offsets[tq.emitted[e].first + 1], 1, __ATOMIC_RELAXED);
+    for (uint64_t i = 0; i < nq; ++i) offsets[i + 1] += offsets[i];
+    cols.resize(tq.emitted.size());
+    {
+        std::vector<uint64_t> fill(offsets.begin(), offsets.end() - 1);
+#pragma omp parallel for num_threads(threads) schedule(static)
+        for (int64_t e = 0; e < ne; ++e)
+            cols[__atomic_fetch_add(&fill[tq.emitted[e].first], 1, __ATOMIC_RELAXED)] = tq.emitted[e].second;
+    }
+    std::vector<std::pair<uint32_t, uint32_t>>().swap(tq.emitted);
+    // ... and order each row by leaf_col, which IS the leaves' pre-order rank,
+    // i.e. the reference's output order (BRWT.cpp:45-51)
+    const int64_t nn = (int64_t)nq;
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1024)
+    for (int64_t r = 0; r < nn; ++r) std::sort(cols.begin() + offsets[r], cols.begin() + offsets[r + 1]);
+    if (draws) *draws = tq.draws;
+    return 0;
+}
+
 // ---- data generation (experiments/data_generation.cpp) -------------------
 
 struct DataGenerator {  // data_generation.hpp:7-79
@@ -968,5 +1222,29 @@ int oracle_bv_get(const OracleBitVec *bv, uint64_t id) { return id < bv->bv.size
 uint64_t oracle_bv_num_set_bits(const OracleBitVec *bv) { return bv->bv.ones; }
 
 uint64_t oracle_synth_hash(uint64_t seed, uint64_t key, uint64_t pos) { return synth_draw(synth_key(seed, key), pos); }
+
+struct OracleCSR {
+    std::vector<uint64_t> offsets;
+    std::vector<uint32_t> cols;
+    uint64_t draws = 0;
+};
+
+OracleCSR *oracle_topdown_get_rows(uint64_t n, uint64_t m, double d, uint32_t arity, uint64_t seed,
+                                   const uint64_t *rows, uint64_t nq, int threads, int *status) {
+    auto r = new OracleCSR();
+    *status = topdown_query(n, m, d, arity, seed, rows, nq, threads, r->offsets, r->cols, &r->draws);
+    if (*status != 0) {
+        delete r;
+        return nullptr;
+    }
+    return r;
+}
+uint64_t oracle_csr_num_labels(const OracleCSR *r) { return r->cols.size(); }
+uint64_t oracle_csr_draws(const OracleCSR *r) { return r->draws; }
+void oracle_csr_copy(const OracleCSR *r, uint64_t *offsets, uint32_t *cols) {
+    std::memcpy(offsets, r->offsets.data(), r->offsets.size() * 8);
+    if (!r->cols.empty()) std::memcpy(cols, r->cols.data(), r->cols.size() * 4);
+}
+void oracle_csr_free(OracleCSR *r) { delete r; }
 
 }  // extern "C"

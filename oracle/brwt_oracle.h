@@ -50,6 +50,23 @@ OracleTree *oracle_generate_topdown(uint64_t num_rows, uint64_t num_cols, double
 
 void oracle_free(OracleTree *t);
 
+/* BRWT::get_row (BRWT.cpp:26-53) over the top-down synthetic tree of the same
+ * spec WITHOUT materialising it: every index bit is a pure function of (node,
+ * position), so each node with queries streams its child masks up to its
+ * largest queried position, counting per child for the inclusive rank1
+ * (BRWT.cpp:30,43).  Memory O(batch x depth): used for the parity checks of
+ * sizes whose plain index bits exceed host RAM (1 B x 3,173 = 158 GB).
+ * *status = 0, or 2 on an out-of-range row (then NULL).  The CSR holds each
+ * row's columns in the reference's order. */
+typedef struct OracleCSR OracleCSR;
+OracleCSR *oracle_topdown_get_rows(uint64_t num_rows, uint64_t num_cols, double density,
+                                   uint32_t arity, uint64_t seed, const uint64_t *rows,
+                                   uint64_t n, int num_threads, int *status);
+uint64_t oracle_csr_num_labels(const OracleCSR *r);
+uint64_t oracle_csr_draws(const OracleCSR *r);  /* mask draws streamed */
+void oracle_csr_copy(const OracleCSR *r, uint64_t *offsets /* n+1 */, uint32_t *cols);
+void oracle_csr_free(OracleCSR *r);
+
 /* ---- BinaryMatrix surface (common/binary_matrix.hpp:9-29, BRWT.hpp:33-51) -- */
 uint64_t oracle_num_rows(const OracleTree *t);
 uint64_t oracle_num_columns(const OracleTree *t);

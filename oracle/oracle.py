@@ -79,6 +79,14 @@ def lib():
         "wt_synth_row": (C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, u32p, C.c_uint64]),
         "wt_synth_rows": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_double, C.c_uint64, u64p, u32p,
                                     C.c_uint64, u64p, C.c_int]),
+        "wt_synth_rows_at": (C.c_int, [u64p, C.c_uint64, C.c_uint64, C.c_double, C.c_uint64, u64p, u32p,
+                                       C.c_uint64, u64p, C.c_int]),
+        "oracle_topdown_get_rows": (vp, [C.c_uint64, C.c_uint64, C.c_double, C.c_uint32, C.c_uint64, u64p,
+                                         C.c_uint64, C.c_int, C.POINTER(C.c_int)]),
+        "oracle_csr_num_labels": (C.c_uint64, [vp]),
+        "oracle_csr_draws": (C.c_uint64, [vp]),
+        "oracle_csr_copy": (None, [vp, u64p, u32p]),
+        "oracle_csr_free": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -284,6 +292,25 @@ def synth_hash(seed, key, pos):
     return lib().oracle_synth_hash(seed, key, pos)
 
 
+def topdown_get_rows(n, m, d, arity, seed, rows, threads=0, with_draws=False):
+    """BRWT::get_row over the top-down synthetic tree (n x m, density d) for
+    rows[], streamed without building the tree (brwt_oracle.h)."""
+    rows = np.ascontiguousarray(rows, dtype=np.uint64)
+    st = C.c_int(0)
+    h = lib().oracle_topdown_get_rows(n, m, d, arity, seed, _p64(rows), len(rows), threads, C.byref(st))
+    if st.value == 2:
+        raise IndexError("row out of range")
+    try:
+        nl = lib().oracle_csr_num_labels(h)
+        off = np.zeros(len(rows) + 1, dtype=np.uint64)
+        cols = np.zeros(max(1, nl), dtype=np.uint32)
+        lib().oracle_csr_copy(h, _p64(off), _p32(cols))
+        draws = lib().oracle_csr_draws(h)
+    finally:
+        lib().oracle_csr_free(h)
+    return (off, cols[:nl], draws) if with_draws else (off, cols[:nl])
+
+
 # ---- BinRel-WT(sdsl) (binrel_wt_oracle.h) ------------------------------------
 
 def dense_to_csr(dense: np.ndarray):
@@ -305,6 +332,22 @@ def wt_synth_rows(row0, n, num_columns, density, seed=42, threads=0):
     cols = np.zeros(max(1, need.value), dtype=np.uint32)
     rc = lib().wt_synth_rows(row0, n, num_columns, density, seed, _p64(offsets), _p32(cols), len(cols),
                              C.byref(need), threads)
+    assert rc == 0
+    return offsets, cols[: need.value]
+
+
+def wt_synth_rows_at(rows, num_columns, density, seed=42, threads=0):
+    """CSR of the synthetic BinRel rows rows[] (any order, repeats allowed)."""
+    rows = np.ascontiguousarray(rows, dtype=np.uint64)
+    n = len(rows)
+    offsets = np.zeros(n + 1, dtype=np.uint64)
+    need = C.c_uint64(0)
+    dummy = np.zeros(1, dtype=np.uint32)
+    lib().wt_synth_rows_at(_p64(rows), n, num_columns, density, seed, _p64(offsets), _p32(dummy), 0,
+                           C.byref(need), threads)
+    cols = np.zeros(max(1, need.value), dtype=np.uint32)
+    rc = lib().wt_synth_rows_at(_p64(rows), n, num_columns, density, seed, _p64(offsets), _p32(cols), len(cols),
+                                C.byref(need), threads)
     assert rc == 0
     return offsets, cols[: need.value]
 

@@ -1,0 +1,42 @@
+"""The streamed top-down oracle (oracle.topdown_get_rows, used by the
+full-size parity checks) against the materialised oracle tree of the same
+spec: identical CSR (BRWT::get_row, BRWT.cpp:26-53) for shapes with
+pass-through leaves, one column, arities 2..12, repeated and unsorted rows,
+and the out-of-range error.  CPU only."""
+import numpy as np
+import pytest
+
+
+@pytest.mark.parametrize("n,m,d,arity", [
+    (1000, 1, 0.3, 8), (5000, 9, 0.1, 8), (20000, 65, 0.02, 8), (50000, 500, 0.01, 2),
+    (100000, 2652, 0.003, 8), (30000, 3173, 0.038, 8), (10000, 17, 0.2, 4), (3000, 130, 0.05, 3),
+    (4000, 300, 0.05, 12), (2000, 40, 0.0, 8), (2000, 40, 1.0, 8),
+])
+def test_stream_matches_materialised_tree(oracle_mod, n, m, d, arity):
+    O = oracle_mod
+    rows = np.random.default_rng(n + m).integers(0, n, 20000).astype(np.uint64)
+    rows[:50] = rows[50]  # repeats
+    rows[-1] = n - 1
+    t = O.OracleTree.topdown(n, m, d, arity, 42)
+    o1, c1 = t.get_rows(rows)
+    o2, c2 = O.topdown_get_rows(n, m, d, arity, 42, rows)
+    assert np.array_equal(o1, o2)
+    assert np.array_equal(c1, c2)
+
+
+def test_stream_edges(oracle_mod):
+    O = oracle_mod
+    off, cols = O.topdown_get_rows(100, 10, 0.1, 8, 1, np.zeros(0, dtype=np.uint64))
+    assert off.tolist() == [0] and len(cols) == 0
+    with pytest.raises(IndexError):
+        O.topdown_get_rows(100, 10, 0.1, 8, 1, np.array([100], dtype=np.uint64))
+
+
+def test_wt_rows_at_matches_range(oracle_mod):
+    O = oracle_mod
+    o1, c1 = O.wt_synth_rows(0, 3000, 500, 0.05, 7)
+    rows = np.random.default_rng(3).integers(0, 3000, 5000).astype(np.uint64)
+    o2, c2 = O.wt_synth_rows_at(rows, 500, 0.05, 7)
+    for i, r in enumerate(rows[:500]):
+        assert np.array_equal(c2[o2[i]:o2[i + 1]], c1[o1[r]:o1[r + 1]])
+    assert o2[-1] == sum(o1[r + 1] - o1[r] for r in rows)
