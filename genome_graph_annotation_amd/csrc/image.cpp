@@ -682,6 +682,7 @@ int finalize_tree(Tree &tree) {
     for (uint32_t v = 0; v < D; ++v)
         if (tree.nodes[v].kind != KIND_LEAF) tree.lds_records = v + 1;
     tree.lds_complete = tree.lds_records <= kLdsNodes;
+    build_p2w_table(tree);
     tree.col_path.assign(tree.num_columns * tree.path_len, 0);
     tree.col_leaf.assign(tree.num_columns, 0);
     for (uint32_t v = 0; v < D; ++v) {
@@ -696,6 +697,55 @@ int finalize_tree(Tree &tree) {
         for (size_t k = 0; k < rev.size(); ++k) tree.col_path[(uint64_t)col * tree.path_len + k] = rev[k];
     }
     return MBRWT_OK;
+}
+
+// The shape k_traverse_p2w takes: dnode 0 a PLANE node of arity <= 8 whose
+// children u are all KIND_PACK2 (arity <= 8), every child A of such u with
+// 1..8 children B, every B a KIND_MASK8 node with consecutive labels -- the
+// basic arity-8 trees at the Kingsford and RefSeq shapes.  A and B nodes are
+// numbered consecutively (BFS), so the table indexes them from the first one.
+void build_p2w_table(Tree &tree) {
+    tree.p2w_table.clear();
+    const auto &N = tree.nodes;
+    if (N.empty() || N[0].kind != KIND_PLANE || N[0].arity == 0 || N[0].arity > 8) return;
+    const uint32_t R = N[0].arity;
+    uint32_t a_lo = UINT32_MAX, a_hi = 0, b_lo = UINT32_MAX, b_hi = 0;
+    for (uint32_t k = 0; k < R; ++k) {
+        const DevNode &u = N[N[0].first_child + k];
+        if (u.kind != KIND_PACK2 || u.arity == 0 || u.arity > 8 || u.stride == 0 || u.stride > kPack2MaxSpan) return;
+        for (uint32_t h = 0; h < u.arity; ++h) {
+            const uint32_t a = u.first_child + h;
+            const DevNode &A = N[a];
+            if (A.arity == 0 || A.arity > 8) return;
+            a_lo = std::min(a_lo, a);
+            a_hi = std::max(a_hi, a);
+            for (uint32_t e = 0; e < A.arity; ++e) {
+                const uint32_t b = A.first_child + e;
+                const DevNode &B = N[b];
+                if (B.kind != KIND_MASK8 || !(B.flags & FLAG_CONSEC_LABELS) || B.arity == 0 || B.arity > 8) return;
+                b_lo = std::min(b_lo, b);
+                b_hi = std::max(b_hi, b);
+            }
+        }
+    }
+    const uint32_t nA = a_hi - a_lo + 1, nB = b_hi - b_lo + 1;
+    if (4 + 4 * R + nA + nB > kP2wMaxWords) return;
+    std::vector<uint32_t> t(4 + 4 * R + nA + nB, 0);
+    t[0] = R;
+    t[1] = nA;
+    t[2] = nB;
+    for (uint32_t k = 0; k < R; ++k) {
+        const DevNode &u = N[N[0].first_child + k];
+        uint32_t lg = 0;
+        while ((1u << lg) < u.stride) ++lg;
+        t[4 + 4 * k + 0] = (uint32_t)u.base;
+        t[4 + 4 * k + 1] = (uint32_t)(u.base >> 32);
+        t[4 + 4 * k + 2] = lg;
+        t[4 + 4 * k + 3] = u.first_child - a_lo;
+    }
+    for (uint32_t a = a_lo; a <= a_hi; ++a) t[4 + 4 * R + (a - a_lo)] = N[a].arity ? N[a].first_child - b_lo : 0;
+    for (uint32_t b = b_lo; b <= b_hi; ++b) t[4 + 4 * R + nA + (b - b_lo)] = N[b].label;
+    tree.p2w_table = std::move(t);
 }
 
 void free_tree(Tree &tree) {

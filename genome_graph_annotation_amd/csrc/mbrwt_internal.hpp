@@ -118,6 +118,12 @@ struct alignas(16) CNode {
 };
 static_assert(sizeof(CNode) == 16, "CNode must be 16 bytes");
 constexpr uint32_t kLdsNodes = 512;
+// P2W table (k_traverse_p2w): u32 words
+//   [0] R = arity of dnode 0, [1] nA, [2] nB, [3] 0,
+//   R x {base lo, base hi, log2(span), index of the node's first child A},
+//   nA x {index (into the B part) of A's first child B},
+//   nB x {label of B's child 0}      (B: KIND_MASK8, consecutive labels)
+constexpr uint32_t kP2wMaxWords = 1024;
 constexpr uint32_t kFastMaxDepth = 4;  // PLANE levels the specialised kernel's stack holds
 
 inline CNode compact(const DevNode &d) {
@@ -165,6 +171,9 @@ struct Tree {
     bool has_mask_children = false;         // some PLANE node has FLAG_MASK_CHILDREN
     uint32_t push_frames = 0;               // max stack frames of the fast kernels (non-TERM PLANE nodes on a path)
     uint32_t lds_records = 0;               // last non-leaf dnode id + 1 (node records worth staging in LDS)
+    // k_traverse_p2w (the super-root's children all KIND_PACK2): the compact
+    // table it stages in LDS (layout: query.hip "P2W table"), empty otherwise
+    std::vector<uint32_t> p2w_table;
     uint32_t max_arity = 0;
     uint64_t num_rows = 0, num_columns = 0, num_relations = 0, num_nodes = 0;
     uint64_t image_bytes = 0;
@@ -215,6 +224,7 @@ struct Ctx {
     Tree tree;
     DevNode *d_nodes = nullptr;
     CNode *d_cnodes = nullptr;
+    uint32_t *d_p2w = nullptr;          // Tree::p2w_table on the device
     uint8_t *d_col_path = nullptr;
     uint32_t *d_col_leaf = nullptr;
     hipStream_t stream = nullptr;       // stream of the host-buffer API
@@ -261,6 +271,8 @@ int build_relaxed_from_desc(const mbrwt_tree_desc &desc, uint64_t max_arity, int
 void free_tree(Tree &tree);
 // finish a Tree whose nodes/images are set: column paths, stack depth
 int finalize_tree(Tree &tree);
+// the P2W table of k_traverse_p2w (empty when the tree has another shape)
+void build_p2w_table(Tree &tree);
 
 // root folding is on unless MBRWT_FOLD_ROOT=0 (A/B measurement switch)
 inline bool fold_root_enabled() {

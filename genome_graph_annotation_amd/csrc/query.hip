@@ -979,6 +979,278 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
     }
 }
 
+// ------------------------------------------------------------------------
+// k_traverse_p2w: the traversal kernel for trees whose super-root's children
+// are all KIND_PACK2 nodes (the basic arity-8 trees at the Kingsford and
+// RefSeq shapes).  A wave resolves a ROWBLOCK of 16 consecutive query rows in
+// wave-uniform phases, so every iteration runs ONE code path for all 16 of
+// its 4-lane groups (k_traverse_fast2 runs the row flush, the root visit and
+// the PACK2 visit in nearly every iteration, for groups at different places):
+//   root phase -- group g reads the super-root's 64-byte block at its row
+//                 (BRWT.cpp:30 + :43 for every child of the root at once);
+//                 its child mask P_g and the children's positions j_k;
+//   items      -- the set (row, child) pairs of the rowblock, numbered in
+//                 (row, child) order = the reference's output order
+//                 (BRWT.cpp:45-51), listed in LDS (prefix of popc(P_g) over
+//                 the groups by 4 ballots);
+//   rounds     -- group g resolves item 16r + g: ONE 64-byte PACK2 block read
+//                 (the child's whole 3-level subtree at j_k), the record walk
+//                 counts the item's labels (quad scans), a wave scan over the
+//                 round's items places them after all earlier items, and the
+//                 labels go to the wave's LDS ring;
+//   flush      -- complete 64-label units of the ring are stored as 256-byte
+//                 wave-wide stores into the rowblock's temp region (full
+//                 lines: no partial-line write amplification), the rest at
+//                 the rowblock's end.
+// Row counts come from the items' label positions; a rowblock with more than
+// C labels stores none and lists its rows for the direct pass.
+// ------------------------------------------------------------------------
+constexpr uint32_t kP2wItems = 128;                      // <= 16 rows x 8 children
+constexpr uint32_t kP2wWaveWords = 2 * kP2wItems + 132 + 16 * 16;  // + ring: items | ipos | blocks
+
+struct P2wParams {
+    const uint64_t *rows;
+    uint64_t n;
+    uint64_t num_rows;
+    uint64_t root_base;       // dnode 0's PLANE image
+    uint32_t root_stride;     // its bytes per 32-position block
+    uint32_t table_words;     // Tree::p2w_table
+    const uint32_t *table;
+    uint32_t C;               // label capacity of a rowblock's temp region
+    uint32_t S;               // LDS ring labels per wave (power of two >= 128)
+    uint32_t *temp;           // [n_blocks][C]
+    uint32_t *counts;         // [n] labels per row
+    uint32_t *block_counts;   // [n_blocks] labels per rowblock
+    uint32_t *ovf_list;       // rows of overflowing rowblocks
+    unsigned long long *scalars;  // [1] overflow rows, [2] error flags
+};
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool NT>
+__global__ __launch_bounds__(256, 8) void k_traverse_p2w(P2wParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_p2w[];
+    const uint32_t lane = threadIdx.x & 63, c = lane & 3, g = lane >> 2, gb = lane & ~3u;
+    const uint32_t wv = threadIdx.x >> 6;
+    for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_p2w[i] = gld(p.table + i);
+    __syncthreads();
+    const AS_LDS uint32_t *tab = (const AS_LDS uint32_t *)lds_p2w;
+    const uint32_t R = tab[0], nA = tab[1];
+    const AS_LDS uint32_t *roots = tab + 4;
+    const AS_LDS uint32_t *afc = roots + 4 * R;
+    const AS_LDS uint32_t *blab = afc + nA;
+    AS_LDS uint32_t *wbase = (AS_LDS uint32_t *)lds_p2w + ((p.table_words + 3) & ~3u) + wv * (kP2wWaveWords + p.S);
+    AS_LDS uint32_t *items = wbase;                  // [128] x {j, child k | group << 8}
+    AS_LDS uint32_t *ipos = wbase + 2 * kP2wItems;   // [129] first label position of each item; [T] = total
+    AS_LDS uint32_t *pk = ipos + 132 + 16 * g;       // the group's staged 64-byte block
+    AS_LDS uint32_t *ring = ipos + 132 + 256;        // S labels
+    const AS_LDS uint8_t *pb = (const AS_LDS uint8_t *)pk;
+    const uint32_t smask = p.S - 1;
+
+    const uint64_t nblocks = (p.n + 15) / 16;
+    const uint64_t wstride = (uint64_t)gridDim.x * 4;
+    for (uint64_t rb = (uint64_t)blockIdx.x * 4 + wv; rb < nblocks; rb += wstride) {
+        const uint64_t r0 = rb * 16;
+        const uint32_t nr = (uint32_t)(p.n - r0 < 16 ? p.n - r0 : 16);
+        uint32_t *const out = p.temp + rb * (uint64_t)p.C;
+
+        // ---- root phase: the super-root's block at group g's row ----
+        uint32_t P = 0, j0 = 0, j1 = 0;
+        if (g < nr) {
+            const uint64_t r = gld(p.rows + r0 + g);
+            if (r >= p.num_rows) {
+                if (c == 0) atomicOr(&p.scalars[2], 1ull);
+            } else if (2 * c < R) {
+                const uint32_t row = (uint32_t)r, t = row & 31, below = (1u << t) - 1u;
+                const uint4 q = gld_at_nt<uint4, NT>(p.root_base + (uint64_t)(row >> 5) * p.root_stride + 16u * c);
+                const uint32_t b0 = (q.y >> t) & 1u, b1 = (2 * c + 1 < R) ? (q.w >> t) & 1u : 0u;
+                j0 = q.x + (uint32_t)__builtin_popcount(q.y & below);
+                j1 = q.z + (uint32_t)__builtin_popcount(q.w & below);
+                P = (b0 | (b1 << 1)) << (2 * c);
+            }
+        }
+        P = quad_or(P);
+        // ---- items in (row, child) order ----
+        const uint32_t ng = (uint32_t)__builtin_popcount(P);
+        uint32_t pre = 0, T = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < 4; ++b) {
+            const uint64_t M = __ballot(c == 0 && ((ng >> b) & 1u));
+            pre += (uint32_t)__popcll(M & ((1ull << gb) - 1ull)) << b;
+            T += (uint32_t)__popcll(M) << b;
+        }
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h) {
+            const uint32_t k = 2 * c + h;
+            if ((P >> k) & 1u) {
+                const uint32_t idx = pre + (uint32_t)__builtin_popcount(P & ((1u << k) - 1u));
+                ((AS_LDS u32x2_t *)items)[idx] = u32x2_t{h ? j1 : j0, k | (g << 8)};
+            }
+        }
+        wave_sync_lds();
+
+        // ---- rounds: group g resolves item ib + g ----
+        uint32_t running = 0, flushed = 0;  // wave-uniform label positions in the rowblock
+        for (uint32_t ib = 0; ib < T; ib += 16) {
+            const uint32_t i = ib + g;
+            const bool act = i < T;
+            uint32_t j = 0, k = 0;
+            if (act) {
+                const u32x2_t it = ((const AS_LDS u32x2_t *)items)[i];
+                j = it.x;
+                k = it.y & 0xFFu;
+            }
+            const uint64_t ubase = (uint64_t)roots[4 * k] | ((uint64_t)roots[4 * k + 1] << 32);
+            const uint32_t lgs = roots[4 * k + 2], aidx = roots[4 * k + 3];
+            const uint32_t t = j & ((1u << lgs) - 1u);
+            if (act) {
+                const uint4 q = gld_at_nt<uint4, NT>(ubase + (uint64_t)(j >> lgs) * kPack2Block + 16u * c);
+                ((AS_LDS u32x4_t *)pk)[c] = u32x4_t{q.x, q.y, q.z, q.w};
+            }
+            wave_sync_lds();
+            uint32_t s = act ? pb[t] : 0u;
+            if (act && pb[0] == 0) {
+                // spilled block: copy the position's record into the group's
+                // slot (list = u16 start[S+1], then the records; <= 64 bytes)
+                const uint64_t la = ((uint64_t)pk[3] << 32) | pk[2];
+                const uint32_t s0 = gld_at<uint16_t>(la + 2ull * t), len = gld_at<uint16_t>(la + 2ull * t + 2) - s0;
+                wave_sync_lds();  // every lane has read the list address
+                AS_LDS uint8_t *pw = (AS_LDS uint8_t *)pk;
+                for (uint32_t o = c; o < len; o += 4) pw[o] = gld_at<uint8_t>(la + s0 + o);
+                wave_sync_lds();
+                s = 0;
+            }
+            // record walk, part 1: this lane's children A = 2c, 2c+1 of the
+            // PACK2 node, their m1 bytes, the count of their labels
+            const uint32_t m2 = act ? pb[s] : 0u;
+            const uint32_t A0 = 2 * c;
+            const uint32_t bA0 = (m2 >> A0) & 1u, bA1 = (m2 >> (A0 + 1)) & 1u;
+            const uint32_t i0 = s + 1 + (uint32_t)__builtin_popcount(m2 & ((1u << A0) - 1u));
+            const uint32_t m10 = bA0 ? pb[i0] : 0u;
+            const uint32_t m11 = bA1 ? pb[i0 + bA0] : 0u;
+            const uint32_t n1 = (uint32_t)__builtin_popcount(m10) + (uint32_t)__builtin_popcount(m11);
+            uint32_t n1_tot;
+            const uint32_t o2 = s + 1 + (uint32_t)__builtin_popcount(m2) + quad_exclusive_sum(n1, c, n1_tot);
+            uint32_t nl = 0;
+#pragma nounroll
+            for (uint32_t e = 0; e < n1; ++e) nl += (uint32_t)__builtin_popcount(pb[o2 + e]);
+            uint32_t ltot;
+            const uint32_t lofs = quad_exclusive_sum(nl, c, ltot);
+            // the item's first label: a wave scan of the items' totals (lanes of
+            // a group hold the same total; groups are in item order)
+            uint32_t x = ltot;
+#pragma unroll
+            for (uint32_t d = 4; d < 64; d <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+                if (lane >= d) x += y;
+            }
+            const uint32_t rtot = (uint32_t)__shfl((int)x, 63, 64);
+            const uint32_t ibase = running + x - ltot;
+            if (act && c == 0) ipos[i] = ibase;
+            // a round that does not fit the ring (rare): pending ring labels
+            // first, then this round's labels straight to the temp region
+            const bool direct = rtot + (running - flushed) > p.S;
+            if (direct) {
+                for (uint32_t q = flushed + lane; q < running; q += 64)
+                    if (q < p.C) gst(out + q, (uint32_t)ring[q & smask]);
+                wave_sync_lds();
+            }
+            // part 2: the labels, in the record's (pre-)order
+            uint32_t pos = ibase + lofs;
+            uint32_t o = o2;
+#pragma unroll
+            for (uint32_t h = 0; h < 2; ++h) {
+                uint32_t xm = h ? m11 : m10;
+                if (!xm) continue;
+                const uint32_t fb = afc[aidx + A0 + h];  // first B of this A (index into blab)
+                for (; xm; xm &= xm - 1) {
+                    const uint32_t l = blab[fb + (uint32_t)__builtin_ctz(xm)];
+                    for (uint32_t lm = pb[o++]; lm; lm &= lm - 1, ++pos) {
+                        const uint32_t label = l + (uint32_t)__builtin_ctz(lm);
+                        if (!direct) ring[pos & smask] = label;
+                        else if (pos < p.C) gst(out + pos, label);
+                    }
+                }
+            }
+            running += rtot;
+            if (direct) {
+                flushed = running;
+            } else {
+                const uint32_t F = running & ~63u;  // complete 64-label units
+                if (F > flushed) {
+                    wave_sync_lds();
+                    for (uint32_t q = flushed + lane; q < F; q += 64)
+                        if (q < p.C) gst(out + q, (uint32_t)ring[q & smask]);
+                    flushed = F;
+                }
+            }
+            wave_sync_lds();  // the group's block slot and the ring are reused
+        }
+        if (lane == 0) ipos[T] = running;
+        wave_sync_lds();
+        for (uint32_t q = flushed + lane; q < running; q += 64)
+            if (q < p.C) gst(out + q, (uint32_t)ring[q & smask]);
+        if (c == 0 && g < nr) gst(p.counts + r0 + g, (uint32_t)(ipos[pre + ng] - ipos[pre]));
+        if (lane == 0) gst(p.block_counts + rb, running);
+        if (running > p.C) {  // rowblock overflow: its rows go to the direct pass
+            unsigned long long k0 = 0;
+            if (lane == 0) k0 = atomicAdd(&p.scalars[1], (unsigned long long)nr);
+            k0 = (unsigned long long)__shfl((long long)k0, 0, 64);
+            if (c == 0 && g < nr) gst(p.ovf_list + k0 + g, (uint32_t)(r0 + g));
+        }
+        wave_sync_lds();
+    }
+}
+
+// k_compact_blocks: output of k_traverse_p2w -> CSR.  16 lanes per 16-row
+// block (4 blocks per wave): the rows' offsets (block offset + in-block
+// prefix) and a contiguous copy of the block's labels, each lane's (up to 8)
+// label reads issued before its stores.  Overflowing blocks (> C labels) are
+// left to the direct pass.
+__global__ __launch_bounds__(256) void k_compact_blocks(const uint32_t *__restrict__ counts,
+                                                        const uint64_t *__restrict__ block_offsets,
+                                                        const uint32_t *__restrict__ temp, uint32_t C,
+                                                        uint64_t *__restrict__ offsets, uint32_t *__restrict__ cols,
+                                                        uint64_t n) {
+    const uint32_t lane = threadIdx.x & 63, sub = lane & 15;
+    const uint64_t nb = (n + 15) / 16;
+    const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) >> 4;
+    for (uint64_t b = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; b < nb; b += stride) {
+        const uint64_t r0 = b * 16;
+        const uint32_t nr = (uint32_t)(n - r0 < 16 ? n - r0 : 16);
+        const uint64_t base = gld(block_offsets + b);
+        const uint32_t mine = sub < nr ? gld(counts + r0 + sub) : 0u;
+        uint32_t x = mine;
+#pragma unroll
+        for (uint32_t d = 1; d < 16; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, d, 16);
+            if (sub >= d) x += y;
+        }
+        const uint32_t total = (uint32_t)__shfl((int)x, 15, 16);
+        if (sub < nr) gst(offsets + r0 + sub, base + (x - mine));
+        if (sub == 0 && r0 + nr == n) gst(offsets + n, base + total);
+        if (total > C) continue;
+        const uint32_t *src = temp + b * (uint64_t)C;
+        for (uint32_t i0 = 0; i0 < total; i0 += 128) {
+            uint32_t v[8];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint32_t i = i0 + sub + 16 * k;
+                v[k] = i < total ? gld(src + i) : 0u;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint32_t i = i0 + sub + 16 * k;
+                if (i < total) gst(cols + base + i, v[k]);
+            }
+        }
+    }
+}
+
 // CSR compaction of the label slots (rows with <= K labels).  A workgroup
 // takes 256 consecutive rows; its threads walk the tile's contiguous output
 // range [offsets[r0], offsets[r0+256]) so the stores are fully coalesced,
@@ -1194,11 +1466,11 @@ Trav pick_traverse(const Ctx &c) {
     Trav t;
     const int kv = c.kernel_variant;
     const bool p2 = c.tree.has_pack2;
-    if (MODE == MODE_SLOTS && c.tree.fast_shape && c.tree.lds_complete && (kv == 0 || kv == 17 || kv == 18) &&
+    if (MODE == MODE_SLOTS && c.tree.fast_shape && c.tree.lds_complete && (kv == 0 || (kv >= 17 && kv <= 20)) &&
         (!p2 || (c.tree.push_frames <= 1 && !c.tree.has_mask_children))) {
         // k_traverse_fast2; 17/18 force plain / non-temporal block reads, the
         // default uses non-temporal reads on images larger than 1 GiB (+2.6 %)
-        const bool nt = kv == 18 || (kv == 0 && c.tree.image_bytes > (1ull << 30));
+        const bool nt = kv == 18 || kv == 20 || (kv == 0 && c.tree.image_bytes > (1ull << 30));
         const bool smallk = auto_slots(c) == kStageLabels;
         t.G = 4;
         t.fast = true;
@@ -1335,9 +1607,125 @@ int ensure(Workspace &w, size_t bytes) {
     return MBRWT_OK;
 }
 
+// k_traverse_p2w for this context?  Default for trees with a P2W table;
+// MBRWT_OPT_KERNEL 19 / 20 force it with plain / non-temporal block reads,
+// 17 / 18 force k_traverse_fast2 (A/B).
+static bool use_p2w(const Ctx &c, bool *nt) {
+    const int kv = c.kernel_variant;
+    if (c.tree.p2w_table.empty() || !c.d_p2w || !(kv == 0 || kv == 19 || kv == 20)) return false;
+    if (nt) *nt = kv == 20 || (kv == 0 && c.tree.image_bytes > (1ull << 30));
+    return true;
+}
+
+static uint32_t p2w_ring(const Ctx &c) {
+    (void)c;
+    return 512;
+}
+
+static size_t p2w_lds_bytes(const Ctx &c) {
+    return ((c.tree.p2w_table.size() + 3) & ~size_t(3)) * 4 + 4 * (size_t)(kP2wWaveWords + p2w_ring(c)) * 4;
+}
+
 const char *traverse_kernel_name(const Ctx &c) {
+    if (use_p2w(c, nullptr)) return "k_traverse_p2w";
     const Trav t = pick_traverse<MODE_SLOTS>(c);
     return t ? t.name : "";
+}
+
+// get_rows through k_traverse_p2w: rowblocks of 16 rows, each written to its
+// own temp region of C = 16 K labels; one scan over the rowblock totals; the
+// compaction; the direct pass for overflowing rowblocks.
+static int run_get_rows_p2w(Ctx &c, bool nt, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets,
+                            uint32_t *d_cols, uint64_t cap, uint64_t *needed, hipStream_t s) {
+    const uint32_t K = auto_slots(c);
+    const uint32_t C = 16 * K;
+    const Trav fn_direct = pick_traverse<MODE_DIRECT>(c);
+    if (!fn_direct) {
+        set_error("tree deeper than 32 levels of internal nodes");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
+    int rc;
+    const uint64_t nb = (n + 15) / 16;
+    // counts: n row counts | nb+1 block counts | (8-byte aligned) nb+1 block offsets
+    const uint64_t bc_off = n, bo_off = ((bc_off + nb + 1) * sizeof(uint32_t) + 7) / 8 * 8;
+    if ((rc = ensure(c.ws_temp, nb * (uint64_t)C * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c.ws_counts, bo_off + (nb + 1) * sizeof(uint64_t)))) return rc;
+    if ((rc = ensure(c.ws_ovf, n * sizeof(uint32_t)))) return rc;
+    uint32_t *d_counts = reinterpret_cast<uint32_t *>(c.ws_counts.buf);
+    uint32_t *d_block_counts = d_counts + bc_off;
+    uint64_t *d_block_offsets = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + bo_off);
+    hipcub::TransformInputIterator<uint64_t, U32ToU64, const uint32_t *> it(d_block_counts, U32ToU64());
+    size_t scan_bytes = 0;
+    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, it, d_block_offsets, nb + 1, s));
+    if ((rc = ensure(c.ws_scan, scan_bytes))) return rc;
+
+    const DevNode &root = c.tree.nodes[0];
+    P2wParams p{};
+    p.rows = d_rows;
+    p.n = n;
+    p.num_rows = c.tree.num_rows;
+    p.root_base = root.base;
+    p.root_stride = root.stride;
+    p.table_words = (uint32_t)c.tree.p2w_table.size();
+    p.table = c.d_p2w;
+    p.C = C;
+    p.S = p2w_ring(c);
+    p.temp = reinterpret_cast<uint32_t *>(c.ws_temp.buf);
+    p.counts = d_counts;
+    p.block_counts = d_block_counts;
+    p.ovf_list = reinterpret_cast<uint32_t *>(c.ws_ovf.buf);
+    p.scalars = reinterpret_cast<unsigned long long *>(c.d_scalars);
+
+    const void *kfn = nt ? reinterpret_cast<const void *>(k_traverse_p2w<true>)
+                         : reinterpret_cast<const void *>(k_traverse_p2w<false>);
+    const size_t lds = p2w_lds_bytes(c);
+    int dev_cus = 0, per_cu = 0;
+    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, lds) != hipSuccess || per_cu <= 0) per_cu = 4;
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((nb + 3) / 4, (uint64_t)std::max(1, dev_cus) * per_cu));
+
+    MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
+    MBRWT_HIP(hipMemsetAsync(d_block_counts + nb, 0, sizeof(uint32_t), s));
+    if (c.timing) MBRWT_HIP(hipEventRecord(c.ev0, s));
+    if (nt) hipLaunchKernelGGL(k_traverse_p2w<true>, dim3((unsigned)grid), dim3(256), lds, s, p);
+    else hipLaunchKernelGGL(k_traverse_p2w<false>, dim3((unsigned)grid), dim3(256), lds, s, p);
+    MBRWT_HIP(hipGetLastError());
+    if (c.timing) MBRWT_HIP(hipEventRecord(c.ev1, s));
+    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_block_offsets, nb + 1, s));
+    MBRWT_HIP(hipMemcpyAsync(c.d_scalars, d_block_offsets + nb, sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+    MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    MBRWT_HIP(hipStreamSynchronize(s));
+    if (c.timing) {
+        float ms = 0;
+        MBRWT_HIP(hipEventElapsedTime(&ms, c.ev0, c.ev1));
+        c.timing_ms += ms;
+        c.timing_launches += 1;
+    }
+    const uint64_t total = c.h_scalars[0], ovf = c.h_scalars[1], err = c.h_scalars[2];
+    if (err & 1) {
+        set_error("row out of range");
+        return MBRWT_ERR_RANGE;
+    }
+    if (needed) *needed = total;
+    if (total > cap) {
+        set_error("cols_cap too small");
+        return MBRWT_ERR_CAPACITY;
+    }
+    const uint64_t g = std::min<uint64_t>((nb + 15) / 16, 8192);
+    hipLaunchKernelGGL(k_compact_blocks, dim3((unsigned)g), dim3(256), 0, s, d_counts, d_block_offsets, p.temp, C,
+                       d_offsets, d_cols, n);
+    MBRWT_HIP(hipGetLastError());
+    if (ovf) {
+        TravParams q = base_params(c);
+        q.rows = d_rows;
+        q.n = ovf;
+        q.K = K;
+        q.slot_list = p.ovf_list;
+        q.offsets = d_offsets;
+        q.cols = d_cols;
+        MBRWT_HIP(launch(c, fn_direct, ovf, s, q));
+    }
+    return MBRWT_OK;
 }
 
 int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
@@ -1356,6 +1744,8 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
         set_error("batch larger than 2^31 rows");
         return MBRWT_ERR_UNSUPPORTED;
     }
+    bool nt = false;
+    if (use_p2w(c, &nt)) return run_get_rows_p2w(c, nt, d_rows, n, d_offsets, d_cols, cap, needed, s);
     const uint32_t K = auto_slots(c);
     const Trav fn = pick_traverse<MODE_SLOTS>(c);
     const Trav fn_direct = pick_traverse<MODE_DIRECT>(c);

@@ -250,11 +250,13 @@ int mbrwt_unpack_ids_device(const uint32_t *d_words, uint64_t n, uint32_t bits, 
 
 #define MBRWT_OPT_TIMING 1       /* 1: time the traversal kernel with HIP events */
 #define MBRWT_OPT_SLOT_LABELS 2  /* per-row label slots of the fast path (0 = auto) */
-#define MBRWT_OPT_KERNEL 4       /* traversal kernel (A/B measurement): 0 default (k_traverse_fast2 where
-                                    eligible, else the group kernel), 1 lane-per-row, 2/3/4 group with
-                                    1/2/4 children per lane, 5/6 group at 8/6 waves per SIMD, 10 group +
-                                    non-temporal reads, 17/18 k_traverse_fast2 plain / non-temporal;
-                                    others rejected */
+#define MBRWT_OPT_KERNEL 4       /* traversal kernel (A/B measurement): 0 default (k_traverse_p2w, else
+                                    k_traverse_fast2 where eligible, else the group kernel), 1 lane-per-row,
+                                    2/3/4 group with 1/2/4 children per lane, 5/6 group at 8/6 waves per
+                                    SIMD, 10 group + non-temporal reads, 17/18 k_traverse_fast2 plain /
+                                    non-temporal, 19/20 k_traverse_p2w plain / non-temporal (each falls
+                                    back to the next kernel where the tree is not eligible); others
+                                    rejected */
 int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value);
 
 /* Traversal-kernel time accumulated while MBRWT_OPT_TIMING is on (ms, launches); resets the sums. */

@@ -20,7 +20,7 @@ def _dev(tree):
     return BRWTDevice.from_tree(tree.export())
 
 
-def _check_rows(oracle_tree, dev, rows, variants=(0, 1, 2, 4, 5, 10, 17, 18)):
+def _check_rows(oracle_tree, dev, rows, variants=(0, 1, 2, 4, 5, 10, 17, 18, 19, 20)):
     """Every traversal kernel (1 lane-per-row; 2/3/4 group-cooperative with
     1/2/4 children per lane; 0 the default) must
     reproduce the oracle's ordered CSR exactly."""
@@ -375,7 +375,7 @@ def test_pack2_layout_with_spills(oracle_mod):
     p2 = _dev(t)
     p1 = _with_env("MBRWT_PACK2", "0", lambda: _dev(t))
     plain = _with_env("MBRWT_PACK", "0", lambda: _dev(t))
-    assert p2.traverse_kernel() == "k_traverse_fast2/pack2"
+    assert p2.traverse_kernel() == "k_traverse_p2w"  # the root's children are all PACK2
     assert p1.traverse_kernel() == plain.traverse_kernel() == "k_traverse_fast2"
     # (the dense run makes PACK decline here: > 1 block in 20 would spill)
     assert p2.device_bytes() not in (p1.device_bytes(), plain.device_bytes())
@@ -414,8 +414,11 @@ def test_pack2_layout_synthetic(oracle_mod, fold):
     p2 = _with_env("MBRWT_FOLD_ROOT", fold, mk)
     p1 = _with_env("MBRWT_FOLD_ROOT", fold, lambda: _with_env("MBRWT_PACK2", "0", mk))
     assert p2.device_bytes() != p1.device_bytes()
+    # folded: the super-root's children are the PACK2 nodes (k_traverse_p2w);
+    # unfolded: the super-root's child is the PLANE root (two stack frames: the
+    # general kernel)
     if fold == "1":
-        assert p2.traverse_kernel() == "k_traverse_fast2/pack2"
+        assert p2.traverse_kernel() == "k_traverse_p2w"
     rows = np.random.default_rng(10).integers(0, n, 100_000).astype(np.uint64)
     _agree(t, [p2, p1], rows, np.random.default_rng(4).integers(0, m, 16), m)
 
@@ -431,7 +434,7 @@ def test_pack2_dense_subtrees_take_a_short_span(oracle_mod):
     t = O.OracleTree.from_dense(dense, "basic", 8)
     p2 = _dev(t)
     p1 = _with_env("MBRWT_PACK2", "0", lambda: _dev(t))
-    assert p2.traverse_kernel() == "k_traverse_fast2/pack2"
+    assert p2.traverse_kernel() == "k_traverse_p2w"
     assert p2.device_bytes() != p1.device_bytes()
     rows = np.concatenate([np.arange(n), rng.integers(0, n, 5000)]).astype(np.uint64)
     _agree(t, [p2, p1], rows, [0, 9, 100, 1023, 2047], m)
@@ -446,7 +449,7 @@ def test_pack2_refseq_shape_synthetic(oracle_mod):
     t = O.OracleTree.topdown(n, m, 0.038, 8, 8)
     p2 = BRWTDevice.synthetic(n, m, 0.038, 8, 8)
     p1 = _with_env("MBRWT_PACK2", "0", lambda: BRWTDevice.synthetic(n, m, 0.038, 8, 8))
-    assert p2.traverse_kernel() == "k_traverse_fast2/pack2"
+    assert p2.traverse_kernel() == "k_traverse_p2w"
     assert p2.device_bytes() != p1.device_bytes()
     rows = np.random.default_rng(11).integers(0, n, 20_000).astype(np.uint64)
     _agree(t, [p2, p1], rows, np.random.default_rng(5).integers(0, m, 6), m)

@@ -43,12 +43,21 @@ alg = 64 * v + 16 * a.batch + 4 * lab
 variants = [int(x) for x in a.variants.split(",")]
 sorts = [0]
 res = {}
+ref = None  # every variant's CSR must equal the first one's (bit-exact)
 for rep in range(a.reps):
   for fold, m in mats.items():
     for var in variants:
         for so in [fold]:
             m.set_option(L.MBRWT_OPT_KERNEL, var)
-            m.get_rows_device(rows, off, cols, s)
+            nl = m.get_rows_device(rows, off, cols, s)
+            if rep == 0:
+                torch.cuda.synchronize()
+                got = (off.clone(), cols[:nl].clone())
+                if ref is None:
+                    ref = got
+                elif not (torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1])):
+                    print(f"MISMATCH: variant {var} differs from variant {variants[0]}", flush=True)
+                    sys.exit(1)
             m.take_timing()
             m.set_option(L.MBRWT_OPT_TIMING, 1)
             torch.cuda.synchronize()
