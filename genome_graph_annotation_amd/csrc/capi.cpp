@@ -523,7 +523,7 @@ int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value) {
         c.slot_labels = (uint32_t)value;
         return MBRWT_OK;
     case MBRWT_OPT_KERNEL:
-        if (!(value >= 0 && value <= 6) && value != 10 && !(value >= 17 && value <= 20)) return MBRWT_ERR_INVALID;
+        if (!(value >= 0 && value <= 6) && value != 10 && !(value >= 17 && value <= 23)) return MBRWT_ERR_INVALID;
         c.kernel_variant = (int)value;
         return MBRWT_OK;
     default:

@@ -1006,7 +1006,7 @@ __global__ __launch_bounds__(256, 8) void k_traverse_fast2(TravParams p) {
 // C labels stores none and lists its rows for the direct pass.
 // ------------------------------------------------------------------------
 constexpr uint32_t kP2wItems = 128;                      // <= 16 rows x 8 children
-constexpr uint32_t kP2wWaveWords = 2 * kP2wItems + 132 + 16 * 16;  // + ring: items | ipos | blocks
+constexpr uint32_t kP2wWaveWords = kP2wItems + 32 + 132 + 20 + 16 * 16;  // + ring: items j | k | ipos | gfirst | blocks
 
 struct P2wParams {
     const uint64_t *rows;
@@ -1031,86 +1031,140 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <bool NT>
-__global__ __launch_bounds__(256, 8) void k_traverse_p2w(P2wParams p) {
+// PF: software pipeline -- the 64-byte block of a group's NEXT visit (the
+// next round's item, or the root block of the next rowblock's row) is
+// requested before the current one is processed, so its latency overlaps the
+// current record walk.  OCC: the waves per SIMD the register budget targets.
+template <bool NT, bool PF, int OCC>
+__global__ __launch_bounds__(256, OCC) void k_traverse_p2w(P2wParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_p2w[];
     const uint32_t lane = threadIdx.x & 63, c = lane & 3, g = lane >> 2, gb = lane & ~3u;
-    const uint32_t wv = threadIdx.x >> 6;
+    // wave-uniform values are made scalar (SGPRs): VGPRs are the occupancy limit
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_p2w[i] = gld(p.table + i);
     __syncthreads();
     const AS_LDS uint32_t *tab = (const AS_LDS uint32_t *)lds_p2w;
-    const uint32_t R = tab[0], nA = tab[1];
+    const uint32_t R = __builtin_amdgcn_readfirstlane(tab[0]), nA = __builtin_amdgcn_readfirstlane(tab[1]);
     const AS_LDS uint32_t *roots = tab + 4;
     const AS_LDS uint32_t *afc = roots + 4 * R;
     const AS_LDS uint32_t *blab = afc + nA;
     AS_LDS uint32_t *wbase = (AS_LDS uint32_t *)lds_p2w + ((p.table_words + 3) & ~3u) + wv * (kP2wWaveWords + p.S);
-    AS_LDS uint32_t *items = wbase;                  // [128] x {j, child k | group << 8}
-    AS_LDS uint32_t *ipos = wbase + 2 * kP2wItems;   // [129] first label position of each item; [T] = total
-    AS_LDS uint32_t *pk = ipos + 132 + 16 * g;       // the group's staged 64-byte block
-    AS_LDS uint32_t *ring = ipos + 132 + 256;        // S labels
+    AS_LDS uint32_t *items_j = wbase;                                 // [128] item position j
+    AS_LDS uint8_t *items_k = (AS_LDS uint8_t *)(wbase + kP2wItems);  // [128] item child k
+    AS_LDS uint32_t *ipos = wbase + kP2wItems + 32;                   // [129] item's first label; [T] = total
+    AS_LDS uint32_t *gfirst = ipos + 132;                             // [17] group's first item; [16] = T
+    AS_LDS uint32_t *pk = gfirst + 20 + 16 * g;                       // the group's staged 64-byte block
+    AS_LDS uint32_t *ring = gfirst + 20 + 256;                        // S labels
     const AS_LDS uint8_t *pb = (const AS_LDS uint8_t *)pk;
     const uint32_t smask = p.S - 1;
+    constexpr uint32_t kNone = 0xFFFFFFFFu;  // no row (ids are < num_rows <= 2^32 - 1)
 
     const uint64_t nblocks = (p.n + 15) / 16;
     const uint64_t wstride = (uint64_t)gridDim.x * 4;
-    for (uint64_t rb = (uint64_t)blockIdx.x * 4 + wv; rb < nblocks; rb += wstride) {
+    // the row of group g in rowblock b (out-of-range ids raise the error flag)
+    auto load_row = [&](uint64_t b) -> uint32_t {
+        const uint64_t r0 = b * 16;
+        if (b >= nblocks || r0 + g >= p.n) return kNone;
+        const uint64_t r = gld(p.rows + r0 + g);
+        if (r < p.num_rows) return (uint32_t)r;
+        if (c == 0) atomicOr(&p.scalars[2], 1ull);
+        return kNone;
+    };
+    // the super-root's 64-byte block at `row` (16 bytes per lane: {rank, bits} of children 2c, 2c+1)
+    auto root_load = [&](uint32_t row) -> uint4 {
+        uint4 q = make_uint4(0, 0, 0, 0);
+        if (row != kNone && 2 * c < R)
+            q = gld_at_nt<uint4, NT>(p.root_base + (uint64_t)(row >> 5) * p.root_stride + 16u * c);
+        return q;
+    };
+    // the PACK2 block of item i (the child's whole 3-level subtree at j)
+    auto item_load = [&](uint32_t i, uint32_t T) -> uint4 {
+        uint4 q = make_uint4(0, 0, 0, 0);
+        if (i < T) {
+            const uint32_t j = items_j[i], k = items_k[i];
+            const uint64_t ubase = (uint64_t)roots[4 * k] | ((uint64_t)roots[4 * k + 1] << 32);
+            q = gld_at_nt<uint4, NT>(ubase + (uint64_t)(j >> roots[4 * k + 2]) * kPack2Block + 16u * c);
+        }
+        return q;
+    };
+
+    uint64_t rb = (uint64_t)blockIdx.x * 4 + wv;
+    uint32_t row_n = 0;          // PF: the group's row in the wave's next rowblock
+    uint4 qn = make_uint4(0, 0, 0, 0);  // PF: the block of the group's next visit
+    if constexpr (PF) {
+        row_n = load_row(rb);
+        qn = root_load(row_n);
+    }
+    for (; rb < nblocks; rb += wstride) {
         const uint64_t r0 = rb * 16;
         const uint32_t nr = (uint32_t)(p.n - r0 < 16 ? p.n - r0 : 16);
         uint32_t *const out = p.temp + rb * (uint64_t)p.C;
 
         // ---- root phase: the super-root's block at group g's row ----
+        uint32_t row;
+        uint4 qr;
+        if constexpr (PF) {
+            row = row_n;
+            qr = qn;
+            row_n = load_row(rb + wstride);
+        } else {
+            row = load_row(rb);
+            qr = root_load(row);
+        }
         uint32_t P = 0, j0 = 0, j1 = 0;
-        if (g < nr) {
-            const uint64_t r = gld(p.rows + r0 + g);
-            if (r >= p.num_rows) {
-                if (c == 0) atomicOr(&p.scalars[2], 1ull);
-            } else if (2 * c < R) {
-                const uint32_t row = (uint32_t)r, t = row & 31, below = (1u << t) - 1u;
-                const uint4 q = gld_at_nt<uint4, NT>(p.root_base + (uint64_t)(row >> 5) * p.root_stride + 16u * c);
-                const uint32_t b0 = (q.y >> t) & 1u, b1 = (2 * c + 1 < R) ? (q.w >> t) & 1u : 0u;
-                j0 = q.x + (uint32_t)__builtin_popcount(q.y & below);
-                j1 = q.z + (uint32_t)__builtin_popcount(q.w & below);
-                P = (b0 | (b1 << 1)) << (2 * c);
-            }
+        if (row != kNone && 2 * c < R) {
+            const uint32_t t = row & 31, below = (1u << t) - 1u;
+            const uint32_t b0 = (qr.y >> t) & 1u, b1 = (2 * c + 1 < R) ? (qr.w >> t) & 1u : 0u;
+            j0 = qr.x + (uint32_t)__builtin_popcount(qr.y & below);
+            j1 = qr.z + (uint32_t)__builtin_popcount(qr.w & below);
+            P = (b0 | (b1 << 1)) << (2 * c);
         }
         P = quad_or(P);
         // ---- items in (row, child) order ----
-        const uint32_t ng = (uint32_t)__builtin_popcount(P);
-        uint32_t pre = 0, T = 0;
+        {
+            const uint32_t ng = (uint32_t)__builtin_popcount(P);
+            uint32_t pre = 0;
 #pragma unroll
-        for (uint32_t b = 0; b < 4; ++b) {
-            const uint64_t M = __ballot(c == 0 && ((ng >> b) & 1u));
-            pre += (uint32_t)__popcll(M & ((1ull << gb) - 1ull)) << b;
-            T += (uint32_t)__popcll(M) << b;
-        }
-#pragma unroll
-        for (uint32_t h = 0; h < 2; ++h) {
-            const uint32_t k = 2 * c + h;
-            if ((P >> k) & 1u) {
-                const uint32_t idx = pre + (uint32_t)__builtin_popcount(P & ((1u << k) - 1u));
-                ((AS_LDS u32x2_t *)items)[idx] = u32x2_t{h ? j1 : j0, k | (g << 8)};
+            for (uint32_t b = 0; b < 4; ++b) {
+                const uint64_t M = __ballot(c == 0 && ((ng >> b) & 1u));
+                pre += (uint32_t)__popcll(M & ((1ull << gb) - 1ull)) << b;
             }
+#pragma unroll
+            for (uint32_t h = 0; h < 2; ++h) {
+                const uint32_t k = 2 * c + h;
+                if ((P >> k) & 1u) {
+                    const uint32_t idx = pre + (uint32_t)__builtin_popcount(P & ((1u << k) - 1u));
+                    items_j[idx] = h ? j1 : j0;
+                    items_k[idx] = (uint8_t)k;
+                }
+            }
+            if (c == 0) gfirst[g] = pre;
+            if (lane == 60) gfirst[16] = pre + ng;
         }
         wave_sync_lds();
+        const uint32_t T = __builtin_amdgcn_readfirstlane(gfirst[16]);
+        if constexpr (PF) qn = T > 0 ? item_load(g, T) : root_load(row_n);
 
         // ---- rounds: group g resolves item ib + g ----
         uint32_t running = 0, flushed = 0;  // wave-uniform label positions in the rowblock
         for (uint32_t ib = 0; ib < T; ib += 16) {
             const uint32_t i = ib + g;
             const bool act = i < T;
+            uint4 q;
+            if constexpr (PF) {
+                q = qn;
+                qn = ib + 16 < T ? item_load(i + 16, T) : root_load(row_n);
+            } else {
+                q = item_load(i, T);
+            }
             uint32_t j = 0, k = 0;
             if (act) {
-                const u32x2_t it = ((const AS_LDS u32x2_t *)items)[i];
-                j = it.x;
-                k = it.y & 0xFFu;
+                j = items_j[i];
+                k = items_k[i];
             }
-            const uint64_t ubase = (uint64_t)roots[4 * k] | ((uint64_t)roots[4 * k + 1] << 32);
             const uint32_t lgs = roots[4 * k + 2], aidx = roots[4 * k + 3];
             const uint32_t t = j & ((1u << lgs) - 1u);
-            if (act) {
-                const uint4 q = gld_at_nt<uint4, NT>(ubase + (uint64_t)(j >> lgs) * kPack2Block + 16u * c);
-                ((AS_LDS u32x4_t *)pk)[c] = u32x4_t{q.x, q.y, q.z, q.w};
-            }
+            if (act) ((AS_LDS u32x4_t *)pk)[c] = u32x4_t{q.x, q.y, q.z, q.w};
             wave_sync_lds();
             uint32_t s = act ? pb[t] : 0u;
             if (act && pb[0] == 0) {
@@ -1148,15 +1202,15 @@ __global__ __launch_bounds__(256, 8) void k_traverse_p2w(P2wParams p) {
                 const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
                 if (lane >= d) x += y;
             }
-            const uint32_t rtot = (uint32_t)__shfl((int)x, 63, 64);
+            const uint32_t rtot = __builtin_amdgcn_readlane(x, 63);
             const uint32_t ibase = running + x - ltot;
             if (act && c == 0) ipos[i] = ibase;
             // a round that does not fit the ring (rare): pending ring labels
             // first, then this round's labels straight to the temp region
             const bool direct = rtot + (running - flushed) > p.S;
             if (direct) {
-                for (uint32_t q = flushed + lane; q < running; q += 64)
-                    if (q < p.C) gst(out + q, (uint32_t)ring[q & smask]);
+                for (uint32_t q2 = flushed + lane; q2 < running; q2 += 64)
+                    if (q2 < p.C) gst(out + q2, (uint32_t)ring[q2 & smask]);
                 wave_sync_lds();
             }
             // part 2: the labels, in the record's (pre-)order
@@ -1183,8 +1237,8 @@ __global__ __launch_bounds__(256, 8) void k_traverse_p2w(P2wParams p) {
                 const uint32_t F = running & ~63u;  // complete 64-label units
                 if (F > flushed) {
                     wave_sync_lds();
-                    for (uint32_t q = flushed + lane; q < F; q += 64)
-                        if (q < p.C) gst(out + q, (uint32_t)ring[q & smask]);
+                    for (uint32_t q2 = flushed + lane; q2 < F; q2 += 64)
+                        if (q2 < p.C) gst(out + q2, (uint32_t)ring[q2 & smask]);
                     flushed = F;
                 }
             }
@@ -1192,9 +1246,9 @@ __global__ __launch_bounds__(256, 8) void k_traverse_p2w(P2wParams p) {
         }
         if (lane == 0) ipos[T] = running;
         wave_sync_lds();
-        for (uint32_t q = flushed + lane; q < running; q += 64)
-            if (q < p.C) gst(out + q, (uint32_t)ring[q & smask]);
-        if (c == 0 && g < nr) gst(p.counts + r0 + g, (uint32_t)(ipos[pre + ng] - ipos[pre]));
+        for (uint32_t q2 = flushed + lane; q2 < running; q2 += 64)
+            if (q2 < p.C) gst(out + q2, (uint32_t)ring[q2 & smask]);
+        if (c == 0 && g < nr) gst(p.counts + r0 + g, (uint32_t)(ipos[gfirst[g + 1]] - ipos[gfirst[g]]));
         if (lane == 0) gst(p.block_counts + rb, running);
         if (running > p.C) {  // rowblock overflow: its rows go to the direct pass
             unsigned long long k0 = 0;
@@ -1466,7 +1520,7 @@ Trav pick_traverse(const Ctx &c) {
     Trav t;
     const int kv = c.kernel_variant;
     const bool p2 = c.tree.has_pack2;
-    if (MODE == MODE_SLOTS && c.tree.fast_shape && c.tree.lds_complete && (kv == 0 || (kv >= 17 && kv <= 20)) &&
+    if (MODE == MODE_SLOTS && c.tree.fast_shape && c.tree.lds_complete && (kv == 0 || (kv >= 17 && kv <= 23)) &&
         (!p2 || (c.tree.push_frames <= 1 && !c.tree.has_mask_children))) {
         // k_traverse_fast2; 17/18 force plain / non-temporal block reads, the
         // default uses non-temporal reads on images larger than 1 GiB (+2.6 %)
@@ -1608,13 +1662,22 @@ int ensure(Workspace &w, size_t bytes) {
 }
 
 // k_traverse_p2w for this context?  Default for trees with a P2W table;
-// MBRWT_OPT_KERNEL 19 / 20 force it with plain / non-temporal block reads,
-// 17 / 18 force k_traverse_fast2 (A/B).
-static bool use_p2w(const Ctx &c, bool *nt) {
+// MBRWT_OPT_KERNEL 19..23 pick a configuration (A/B; 17 / 18 force
+// k_traverse_fast2): 19 plain reads, 20 non-temporal reads, 21 non-temporal +
+// prefetch, 22 the same at 6 waves per SIMD, 23 non-temporal at 7 waves.
+using P2wFn = void (*)(P2wParams);
+static P2wFn p2w_kernel(const Ctx &c) {
     const int kv = c.kernel_variant;
-    if (c.tree.p2w_table.empty() || !c.d_p2w || !(kv == 0 || kv == 19 || kv == 20)) return false;
-    if (nt) *nt = kv == 20 || (kv == 0 && c.tree.image_bytes > (1ull << 30));
-    return true;
+    if (c.tree.p2w_table.empty() || !c.d_p2w || !(kv == 0 || (kv >= 19 && kv <= 23))) return nullptr;
+    const bool big = c.tree.image_bytes > (1ull << 30);
+    switch (kv) {
+    case 19: return k_traverse_p2w<false, false, 8>;
+    case 20: return k_traverse_p2w<true, false, 8>;
+    case 21: return k_traverse_p2w<true, true, 8>;
+    case 22: return k_traverse_p2w<true, true, 6>;
+    case 23: return k_traverse_p2w<true, false, 7>;
+    default: return big ? k_traverse_p2w<true, false, 8> : k_traverse_p2w<false, false, 8>;  // (PF: +1 %, 21)
+    }
 }
 
 static uint32_t p2w_ring(const Ctx &c) {
@@ -1627,7 +1690,7 @@ static size_t p2w_lds_bytes(const Ctx &c) {
 }
 
 const char *traverse_kernel_name(const Ctx &c) {
-    if (use_p2w(c, nullptr)) return "k_traverse_p2w";
+    if (p2w_kernel(c)) return "k_traverse_p2w";
     const Trav t = pick_traverse<MODE_SLOTS>(c);
     return t ? t.name : "";
 }
@@ -1635,7 +1698,7 @@ const char *traverse_kernel_name(const Ctx &c) {
 // get_rows through k_traverse_p2w: rowblocks of 16 rows, each written to its
 // own temp region of C = 16 K labels; one scan over the rowblock totals; the
 // compaction; the direct pass for overflowing rowblocks.
-static int run_get_rows_p2w(Ctx &c, bool nt, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets,
+static int run_get_rows_p2w(Ctx &c, P2wFn kfn, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets,
                             uint32_t *d_cols, uint64_t cap, uint64_t *needed, hipStream_t s) {
     const uint32_t K = auto_slots(c);
     const uint32_t C = 16 * K;
@@ -1676,19 +1739,19 @@ static int run_get_rows_p2w(Ctx &c, bool nt, const uint64_t *d_rows, uint64_t n,
     p.ovf_list = reinterpret_cast<uint32_t *>(c.ws_ovf.buf);
     p.scalars = reinterpret_cast<unsigned long long *>(c.d_scalars);
 
-    const void *kfn = nt ? reinterpret_cast<const void *>(k_traverse_p2w<true>)
-                         : reinterpret_cast<const void *>(k_traverse_p2w<false>);
     const size_t lds = p2w_lds_bytes(c);
     int dev_cus = 0, per_cu = 0;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, lds) != hipSuccess || per_cu <= 0) per_cu = 4;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kfn), 256, lds) !=
+            hipSuccess ||
+        per_cu <= 0)
+        per_cu = 4;
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((nb + 3) / 4, (uint64_t)std::max(1, dev_cus) * per_cu));
 
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
     MBRWT_HIP(hipMemsetAsync(d_block_counts + nb, 0, sizeof(uint32_t), s));
     if (c.timing) MBRWT_HIP(hipEventRecord(c.ev0, s));
-    if (nt) hipLaunchKernelGGL(k_traverse_p2w<true>, dim3((unsigned)grid), dim3(256), lds, s, p);
-    else hipLaunchKernelGGL(k_traverse_p2w<false>, dim3((unsigned)grid), dim3(256), lds, s, p);
+    hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(256), lds, s, p);
     MBRWT_HIP(hipGetLastError());
     if (c.timing) MBRWT_HIP(hipEventRecord(c.ev1, s));
     MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_block_offsets, nb + 1, s));
@@ -1744,8 +1807,7 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
         set_error("batch larger than 2^31 rows");
         return MBRWT_ERR_UNSUPPORTED;
     }
-    bool nt = false;
-    if (use_p2w(c, &nt)) return run_get_rows_p2w(c, nt, d_rows, n, d_offsets, d_cols, cap, needed, s);
+    if (const P2wFn kfn = p2w_kernel(c)) return run_get_rows_p2w(c, kfn, d_rows, n, d_offsets, d_cols, cap, needed, s);
     const uint32_t K = auto_slots(c);
     const Trav fn = pick_traverse<MODE_SLOTS>(c);
     const Trav fn_direct = pick_traverse<MODE_DIRECT>(c);
