@@ -100,6 +100,12 @@ SIGNATURES = {
     "mbrwt_pack_ids_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]),
     "mbrwt_unpack_ids_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]),
     "mbrwt_destroy": (None, [C.c_void_p]),
+    "mbrwt_tree_parse": (C.c_int, [u8p, C.c_uint64, u64p, C.POINTER(C.c_void_p)]),
+    "mbrwt_tree_serialize": (C.c_int, [C.POINTER(TreeDesc), u8p, C.c_uint64, u64p]),
+    "mbrwt_tree_export": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
+    "mbrwt_tree_get_desc": (C.POINTER(TreeDesc), [C.c_void_p]),
+    "mbrwt_tree_free": (None, [C.c_void_p]),
+    "mbrwt_load": (C.c_int, [u8p, C.c_uint64, u64p, C.c_int, C.POINTER(C.c_void_p)]),
     "mbrwt_num_rows": (C.c_uint64, [C.c_void_p]),
     "mbrwt_num_columns": (C.c_uint64, [C.c_void_p]),
     "mbrwt_num_relations": (C.c_uint64, [C.c_void_p]),

@@ -62,6 +62,77 @@ def _top_labels_batch(fn, h, rows, read_offsets, num_top):
         return lo, labs[: need.value], cnts[: need.value]
 
 
+def tree_desc(tree):
+    """mbrwt_tree_desc of a BFS tree dict (keys: num_rows, num_columns,
+    num_children, first_child, leaf_column, vec_size, words); returns the
+    struct and the arrays it points into (keep them alive while it is used)."""
+    N = int(len(tree["num_children"]))
+    nc = np.ascontiguousarray(tree["num_children"], dtype=np.uint32)
+    fc = np.ascontiguousarray(tree["first_child"], dtype=np.uint32)
+    lc = np.ascontiguousarray(tree["leaf_column"], dtype=np.uint32)
+    vs = np.ascontiguousarray(tree["vec_size"], dtype=np.uint64)
+    words = [np.ascontiguousarray(w, dtype=np.uint64) for w in tree["words"]]
+    ptrs = (L.u64p * max(1, N))()
+    for u, w in enumerate(words):
+        ptrs[u] = _p(w, C.c_uint64) if w.size else None
+    d = L.TreeDesc()
+    d.num_rows = int(tree["num_rows"])
+    d.num_columns = int(tree["num_columns"])
+    d.num_nodes = N
+    d.num_children = _p(nc, C.c_uint32)
+    d.first_child = _p(fc, C.c_uint32)
+    d.leaf_column = _p(lc, C.c_uint32)
+    d.vec_size = _p(vs, C.c_uint64)
+    d.vec_words = ptrs
+    return d, (nc, fc, lc, vs, words, ptrs)
+
+
+def _tree_dict(handle):
+    """Copy an mbrwt_tree (include/mbrwt.h) into a BFS tree dict and free it."""
+    lib = L.lib()
+    try:
+        d = lib.mbrwt_tree_get_desc(handle).contents
+        N = int(d.num_nodes)
+        out = dict(num_rows=int(d.num_rows), num_columns=int(d.num_columns), num_nodes=N)
+        for key, dt in (("num_children", np.uint32), ("first_child", np.uint32), ("leaf_column", np.uint32),
+                        ("vec_size", np.uint64)):
+            ptr = getattr(d, key)
+            out[key] = np.ctypeslib.as_array(ptr, shape=(N,)).astype(dt).copy() if N else np.zeros(0, dtype=dt)
+        words = []
+        for u in range(N):
+            W = (int(out["vec_size"][u]) + 63) // 64
+            words.append(np.ctypeslib.as_array(d.vec_words[u], shape=(W,)).copy() if W else
+                         np.zeros(0, dtype=np.uint64))
+        out["words"] = words
+        return out
+    finally:
+        lib.mbrwt_tree_free(handle)
+
+
+def parse_brwt(data: bytes):
+    """BRWT::load (BRWT.cpp:87-111) of a reference BRWT stream -> (tree dict,
+    bytes consumed).  Host only (include/mbrwt.h mbrwt_tree_parse)."""
+    buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, dtype=np.uint8)
+    h = C.c_void_p()
+    used = C.c_uint64(0)
+    L.check(L.lib().mbrwt_tree_parse(_p(buf, C.c_uint8), len(data), C.byref(used), C.byref(h)), "mbrwt_tree_parse")
+    return _tree_dict(h), int(used.value)
+
+
+def serialize_tree(tree) -> bytes:
+    """BRWT::serialize (BRWT.cpp:113-128) of a tree dict.  Host only."""
+    lib = L.lib()
+    d, keep = tree_desc(tree)
+    need = C.c_uint64(0)
+    st = lib.mbrwt_tree_serialize(C.byref(d), None, 0, C.byref(need))
+    if st != L.MBRWT_ERR_CAPACITY:
+        L.check(st, "mbrwt_tree_serialize")
+    buf = np.zeros(max(1, need.value), dtype=np.uint8)
+    L.check(lib.mbrwt_tree_serialize(C.byref(d), _p(buf, C.c_uint8), len(buf), C.byref(need)), "mbrwt_tree_serialize")
+    del keep
+    return buf[: need.value].tobytes()
+
+
 class BRWTDevice:
     """A BRWT held in HBM; every query runs the HIP traversal kernels."""
 
@@ -77,24 +148,7 @@ class BRWTDevice:
         vec_size, words = list of uint64 arrays).  relax_max_arity > 1 runs
         BRWTOptimizer::relax on it first (mbrwt_create_relaxed)."""
         lib = L.lib()
-        N = int(len(tree["num_children"]))
-        nc = np.ascontiguousarray(tree["num_children"], dtype=np.uint32)
-        fc = np.ascontiguousarray(tree["first_child"], dtype=np.uint32)
-        lc = np.ascontiguousarray(tree["leaf_column"], dtype=np.uint32)
-        vs = np.ascontiguousarray(tree["vec_size"], dtype=np.uint64)
-        words = [np.ascontiguousarray(w, dtype=np.uint64) for w in tree["words"]]
-        ptrs = (L.u64p * max(1, N))()
-        for u, w in enumerate(words):
-            ptrs[u] = _p(w, C.c_uint64) if w.size else None
-        d = L.TreeDesc()
-        d.num_rows = int(tree["num_rows"])
-        d.num_columns = int(tree["num_columns"])
-        d.num_nodes = N
-        d.num_children = _p(nc, C.c_uint32)
-        d.first_child = _p(fc, C.c_uint32)
-        d.leaf_column = _p(lc, C.c_uint32)
-        d.vec_size = _p(vs, C.c_uint64)
-        d.vec_words = ptrs
+        d, keep = tree_desc(tree)
         h = C.c_void_p()
         if relax_max_arity:
             L.check(lib.mbrwt_create_relaxed(C.byref(d), int(relax_max_arity), device, C.byref(h)),
@@ -134,6 +188,25 @@ class BRWTDevice:
         else:
             L.check(lib.mbrwt_create_from_columns(C.byref(d), device, C.byref(h)), "mbrwt_create_from_columns")
         return cls(h)
+
+    @classmethod
+    def load(cls, data: bytes, device=0):
+        """BRWT::load of a reference BRWT stream into HBM (mbrwt_load)."""
+        buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, dtype=np.uint8)
+        h = C.c_void_p()
+        L.check(L.lib().mbrwt_load(_p(buf, C.c_uint8), len(data), None, device, C.byref(h)), "mbrwt_load")
+        return cls(h)
+
+    def export(self):
+        """The tree this context holds, read back from its device image
+        (mbrwt_tree_export), as a BFS tree dict."""
+        h = C.c_void_p()
+        L.check(L.lib().mbrwt_tree_export(self._h, C.byref(h)), "mbrwt_tree_export")
+        return _tree_dict(h)
+
+    def serialize(self) -> bytes:
+        """BRWT::serialize (BRWT.cpp:113-128) of this matrix."""
+        return serialize_tree(self.export())
 
     def close(self):
         if getattr(self, "_h", None):

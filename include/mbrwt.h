@@ -133,6 +133,32 @@ int mbrwt_create_relaxed(const mbrwt_tree_desc *desc, uint64_t max_arity, int de
 
 void mbrwt_destroy(mbrwt_ctx *ctx);
 
+/* ---- files: the reference's BRWT stream (the matrix of a .brwt.annodbg) ----
+ * An owned tree description (host memory).  Byte formats of sdsl-lite /
+ * libmaus2 are restated from their published algorithms: PARITY UNPINNED
+ * (no sdsl source or reference-written file exists here).
+ *
+ * mbrwt_tree_parse      BRWT::load (BRWT.cpp:87-111): the pre-order stream of
+ *                       {RangePartition (utils.cpp:702-715), rrr_vector<63>
+ *                       index (bit_vector.cpp:906-925), child count, children}
+ *                       starting at bytes[0]; *consumed (may be NULL) = bytes
+ *                       read.  MBRWT_ERR_INVALID on a malformed stream (the
+ *                       reference's load returns false).  Host only, no GPU.
+ * mbrwt_tree_serialize  BRWT::serialize (BRWT.cpp:113-128) of a description:
+ *                       capacity protocol as mbrwt_get_rows (buf may be NULL
+ *                       for the sizing call).  Host only, no GPU.
+ * mbrwt_tree_export     the tree a context holds, read back from its device
+ *                       image (every node's index column; any image layout).
+ * mbrwt_load            mbrwt_tree_parse + mbrwt_create.
+ */
+typedef struct mbrwt_tree mbrwt_tree;
+int mbrwt_tree_parse(const uint8_t *bytes, uint64_t len, uint64_t *consumed, mbrwt_tree **out);
+int mbrwt_tree_serialize(const mbrwt_tree_desc *desc, uint8_t *buf, uint64_t cap, uint64_t *needed);
+int mbrwt_tree_export(mbrwt_ctx *ctx, mbrwt_tree **out);
+const mbrwt_tree_desc *mbrwt_tree_get_desc(const mbrwt_tree *tree); /* valid until mbrwt_tree_free */
+void mbrwt_tree_free(mbrwt_tree *tree);
+int mbrwt_load(const uint8_t *bytes, uint64_t len, uint64_t *consumed, int device, mbrwt_ctx **out);
+
 /* ---- properties (BRWT.hpp:33-51) -------------------------------------- */
 uint64_t mbrwt_num_rows(const mbrwt_ctx *ctx);
 uint64_t mbrwt_num_columns(const mbrwt_ctx *ctx);
