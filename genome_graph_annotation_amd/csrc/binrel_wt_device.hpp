@@ -149,11 +149,21 @@ class BinRelWTDevice : public BinaryMatrix {
         return rows;
     }
 
+    // BinRelWT_sdsl::load / serialize (bin_rel_wt_sdsl.cpp:85-111): the sdsl
+    // wt_int<rrr_vector<63>> stream is not restated by this build (the file
+    // row of SURVEY §8(f) is the BRWT's); load reports failure as the
+    // reference's does for a stream it cannot read, serialize throws
+    bool load(std::istream &) override { return false; }
+    void serialize(std::ostream &) const override {
+        throw std::runtime_error("BinRelWTDevice::serialize: the BinRel-WT(sdsl) file format is not supported");
+    }
+
   private:
     struct Deleter {
         void operator()(mbrwt_wt *c) const { mbrwt_wt_destroy(c); }
     };
     std::shared_ptr<mbrwt_wt> ctx_{nullptr, Deleter()};
+
 };
 
 }  // namespace mbrwt_host

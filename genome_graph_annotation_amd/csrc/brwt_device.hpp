@@ -13,42 +13,71 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <fstream>
+#include <istream>
+#include <iterator>
 #include <memory>
+#include <ostream>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "../../include/mbrwt.h"
 
+// Built inside the reference tree, define
+// MBRWT_WITH_REFERENCE_BINARY_MATRIX and put the reference's common/ on the
+// include path: BRWTDevice then derives from the reference's own BinaryMatrix.
+#ifdef MBRWT_WITH_REFERENCE_BINARY_MATRIX
+#include "binary_matrix.hpp"
 namespace mbrwt_host {
-
-// common/binary_matrix.hpp:9-29 (load/serialize are not part of the device
-// path; see DESIGN.md "Out of scope")
-class BinaryMatrix {
+typedef ::BinaryMatrix ReferenceBinaryMatrix;
+}
+#else
+namespace mbrwt_host {
+// common/binary_matrix.hpp:9-29, restated (the reference header pulls in
+// sdsl-lite, which this image lacks)
+class ReferenceBinaryMatrix {
   public:
     typedef uint64_t Row;
     typedef uint64_t Column;
 
-    virtual ~BinaryMatrix() {}
+    virtual ~ReferenceBinaryMatrix() {}
 
     virtual uint64_t num_columns() const = 0;
     virtual uint64_t num_rows() const = 0;
 
+    // row is in [0, num_rows), column is in [0, num_columns)
     virtual bool get(Row row, Column column) const = 0;
     virtual std::vector<Column> get_row(Row row) const = 0;
     virtual std::vector<Row> get_column(Column column) const = 0;
+
+    virtual bool load(std::istream &in) = 0;
+    virtual void serialize(std::ostream &out) const = 0;
+
+    // number of ones in the matrix
+    virtual uint64_t num_relations() const = 0;
+};
+}  // namespace mbrwt_host
+#endif
+
+namespace mbrwt_host {
+
+// The reference's BinaryMatrix plus the batched entry points the device path
+// is built for; every other scheme keeps the defaults (a loop over get_row,
+// or "not offered" so the annotator answers read by read).
+class BinaryMatrix : public ReferenceBinaryMatrix {
+  public:
+    typedef uint64_t Row;
+    typedef uint64_t Column;
 
     // Batched get_row: the default loops over get_row (every scheme of the
     // reference); device-backed matrices override it with one launch.
     virtual std::vector<std::vector<Column>> get_rows(const std::vector<Row> &rows) const {
         std::vector<std::vector<Column>> out;
         out.reserve(rows.size());
-        for (Row r : rows) out.push_back(get_row(r));
+        for (Row r : rows) out.push_back(this->get_row(r));
         return out;
     }
-
-    // number of ones in the matrix
-    virtual uint64_t num_relations() const = 0;
 
     // Batched classify on the device (get_labels / get_top_labels for many
     // reads, CSR over reads); false = not offered by this scheme, and the
@@ -63,6 +92,21 @@ class BinaryMatrix {
         return false;
     }
 };
+
+// Reads the rest of `in` into memory for a C-ABI parser and, once the parser
+// has reported how many bytes it used, leaves the stream right after them --
+// where the reference's stream-based load would have left it.
+template <class Parse>
+bool load_from_stream(std::istream &in, Parse &&parse) {
+    if (!in.good()) return false;
+    const std::streampos start = in.tellg();
+    std::vector<char> buf((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+    uint64_t used = 0;
+    if (!parse(reinterpret_cast<const uint8_t *>(buf.data()), (uint64_t)buf.size(), &used)) return false;
+    in.clear();
+    if (start != std::streampos(-1)) in.seekg(start + std::streamoff(used));
+    return in.good();
+}
 
 class MBRWTException : public std::runtime_error {
   public:
@@ -87,14 +131,16 @@ class BRWTDevice : public BinaryMatrix {
   public:
     BRWTDevice() = default;  // the empty BRWT() (test_BRWT.cpp:15-19)
 
-    BRWTDevice(const mbrwt_tree_desc &desc, int device = 0) {
+    explicit BRWTDevice(int device) : device_(device) {}
+
+    BRWTDevice(const mbrwt_tree_desc &desc, int device = 0) : device_(device) {
         mbrwt_ctx *c = nullptr;
         check_status(mbrwt_create(&desc, device, &c), "mbrwt_create");
         ctx_.reset(c, Deleter());
     }
 
     static BRWTDevice synthetic(const mbrwt_synth_desc &desc, int device = 0) {
-        BRWTDevice m;
+        BRWTDevice m(device);
         mbrwt_ctx *c = nullptr;
         check_status(mbrwt_create_synthetic(&desc, device, &c), "mbrwt_create_synthetic");
         m.ctx_.reset(c, Deleter());
@@ -110,7 +156,7 @@ class BRWTDevice : public BinaryMatrix {
         std::vector<const uint64_t *> ptrs(columns.size());
         for (size_t j = 0; j < columns.size(); ++j) ptrs[j] = columns[j].data();
         mbrwt_columns_desc d{num_rows, columns.size(), ptrs.data(), arity};
-        BRWTDevice m;
+        BRWTDevice m(device);
         mbrwt_ctx *c = nullptr;
         check_status(mbrwt_create_from_columns_relaxed(&d, relax_max_arity, device, &c),
                      "mbrwt_create_from_columns_relaxed");
@@ -121,7 +167,7 @@ class BRWTDevice : public BinaryMatrix {
     // BRWTOptimizer::relax(brwt, max_arity) of an exported tree
     // (`annograph relax_brwt`, main.cpp:746)
     static BRWTDevice relaxed(const mbrwt_tree_desc &desc, uint64_t max_arity, int device = 0) {
-        BRWTDevice m;
+        BRWTDevice m(device);
         mbrwt_ctx *c = nullptr;
         check_status(mbrwt_create_relaxed(&desc, max_arity, device, &c), "mbrwt_create_relaxed");
         m.ctx_.reset(c, Deleter());
@@ -277,13 +323,48 @@ class BRWTDevice : public BinaryMatrix {
         }
     }
 
+    // BRWT::load (BRWT.cpp:87-111): the BRWT stream at the stream's position
+    // (mbrwt_load); false on a bad stream, like the reference
+    bool load(std::istream &in) override {
+        try {
+            return load_from_stream(in, [&](const uint8_t *p, uint64_t n, uint64_t *used) {
+                mbrwt_ctx *c = nullptr;
+                if (mbrwt_load(p, n, used, device_, &c) != MBRWT_OK) return false;
+                ctx_.reset(c, Deleter());
+                return true;
+            });
+        } catch (...) {
+            return false;
+        }
+    }
+
+    // BRWT::serialize (BRWT.cpp:113-128): the device image read back
+    // (mbrwt_tree_export) and written in the reference's stream format
+    void serialize(std::ostream &out) const override {
+        if (!out.good()) throw std::ofstream::failure("Error when dumping BRWT");
+        std::vector<uint8_t> bytes;
+        mbrwt_tree *t = nullptr;
+        mbrwt_tree_desc empty{};
+        if (ctx_) check_status(mbrwt_tree_export(ctx_.get(), &t), "BRWTDevice::serialize");
+        std::unique_ptr<mbrwt_tree, void (*)(mbrwt_tree *)> hold(t, mbrwt_tree_free);
+        const mbrwt_tree_desc *d = t ? mbrwt_tree_get_desc(t) : &empty;
+        uint64_t need = 0;
+        int st = mbrwt_tree_serialize(d, nullptr, 0, &need);
+        if (st != MBRWT_ERR_CAPACITY) check_status(st, "BRWTDevice::serialize");
+        bytes.resize(need);
+        check_status(mbrwt_tree_serialize(d, bytes.data(), bytes.size(), &need), "BRWTDevice::serialize");
+        out.write(reinterpret_cast<const char *>(bytes.data()), (std::streamsize)bytes.size());
+    }
+
     mbrwt_ctx *handle() const { return ctx_.get(); }
+    int device() const { return device_; }
 
   private:
     struct Deleter {
         void operator()(mbrwt_ctx *c) const { mbrwt_destroy(c); }
     };
     std::shared_ptr<mbrwt_ctx> ctx_{nullptr, Deleter()};
+    int device_ = 0;
 
   public:
     BRWTDevice(const BRWTDevice &) = default;

@@ -48,28 +48,58 @@ class OracleMatrix : public BinaryMatrix {
     }
     OracleTree *tree() const { return t_.get(); }
 
+    // the oracle is built from columns, not read from streams
+    bool load(std::istream &) override { return false; }
+    // BRWT::serialize of the oracle's tree, through libmbrwt's host-side
+    // writer (mbrwt_tree_serialize; no device involved)
+    void serialize(std::ostream &out) const override;
+
   private:
     std::shared_ptr<OracleTree> t_;
 };
 
-// export the oracle's tree into the C-ABI description and build it on the device
-inline mbrwt_host::BRWTDevice to_device(const OracleMatrix &m) {
+// the oracle's tree as the C-ABI description (arrays held in `st`)
+struct DescStorage {
+    std::vector<uint32_t> nc, fc, lc;
+    std::vector<uint64_t> vs;
+    std::vector<const uint64_t *> words;
+};
+inline mbrwt_tree_desc oracle_desc(const OracleMatrix &m, DescStorage &st) {
     OracleTree *t = m.tree();
     const uint32_t N = oracle_export_num_nodes(t);
-    std::vector<uint32_t> nc(N), fc(N), lc(N);
-    std::vector<uint64_t> vs(N);
-    std::vector<const uint64_t *> words(N);
-    if (N) oracle_export(t, nc.data(), fc.data(), lc.data(), vs.data());
-    for (uint32_t u = 0; u < N; ++u) words[u] = oracle_export_vec_words(t, u);
+    st.nc.resize(N);
+    st.fc.resize(N);
+    st.lc.resize(N);
+    st.vs.resize(N);
+    st.words.resize(N);
+    if (N) oracle_export(t, st.nc.data(), st.fc.data(), st.lc.data(), st.vs.data());
+    for (uint32_t u = 0; u < N; ++u) st.words[u] = oracle_export_vec_words(t, u);
     mbrwt_tree_desc d{};
     d.num_rows = N ? oracle_num_rows(t) : 0;
     d.num_columns = N ? oracle_num_columns(t) : 0;
     d.num_nodes = N;
-    d.num_children = nc.data();
-    d.first_child = fc.data();
-    d.leaf_column = lc.data();
-    d.vec_size = vs.data();
-    d.vec_words = words.data();
+    d.num_children = st.nc.data();
+    d.first_child = st.fc.data();
+    d.leaf_column = st.lc.data();
+    d.vec_size = st.vs.data();
+    d.vec_words = st.words.data();
+    return d;
+}
+
+inline void OracleMatrix::serialize(std::ostream &out) const {
+    DescStorage st;
+    const mbrwt_tree_desc d = oracle_desc(*this, st);
+    uint64_t need = 0;
+    mbrwt_tree_serialize(&d, nullptr, 0, &need);
+    std::vector<uint8_t> buf(need);
+    mbrwt_host::check_status(mbrwt_tree_serialize(&d, buf.data(), buf.size(), &need), "mbrwt_tree_serialize");
+    out.write(reinterpret_cast<const char *>(buf.data()), (std::streamsize)buf.size());
+}
+
+// export the oracle's tree into the C-ABI description and build it on the device
+inline mbrwt_host::BRWTDevice to_device(const OracleMatrix &m) {
+    DescStorage st;
+    const mbrwt_tree_desc d = oracle_desc(m, st);
     return mbrwt_host::BRWTDevice(d, 0);
 }
 

@@ -3,6 +3,7 @@
 //   oracle  -- the CPU restatement (runs without a GPU)
 //   device  -- BRWTDevice, every query through include/mbrwt.h on the GPU
 #include <set>
+#include <sstream>
 
 #include "backends.hpp"
 #include "minitest.hpp"
@@ -19,7 +20,7 @@ static std::set<std::pair<std::string, size_t>> SC(const VectorCounts &v) { retu
 // convert_to_simple_BRWT (annotation_converters.cpp:76-86, grouping arity 2)
 static std::shared_ptr<StaticBinRelAnnotator<BinaryMatrix>> annotator(const LabelFixture &f) {
     auto om = std::make_shared<OracleMatrix>(build_oracle(f.cols, f.n, 0, 2));
-    std::shared_ptr<const BinaryMatrix> m = om;
+    std::shared_ptr<BinaryMatrix> m = om;
     if (g_device) m = std::make_shared<mbrwt_host::BRWTDevice>(to_device(*om));
     return std::make_shared<StaticBinRelAnnotator<BinaryMatrix>>(m, f.enc);
 }
@@ -187,6 +188,45 @@ TEST(LabelEncoder, encode_decode) {  // annotate.cpp:12-31, annotate.hpp:128
     EXPECT_EQ(std::string("a"), e.decode(0));
     EXPECT_THROW(e.encode("c"), std::runtime_error);
     EXPECT_THROW(e.decode(5), std::out_of_range);
+}
+
+// test_annotation_BRWT.cpp:190-215 (BRWTCompressed, Serialization): the
+// annotator is dumped (label encoder + matrix, annotate_static.cpp:96-109)
+// and merge_load'ed into a default-constructed annotator
+// (annotate_static.cpp:111-130); a missing file does not load.  Oracle
+// backend: the label encoder part round-trips and the matrix part parses;
+// device backend: the loaded annotator answers from HBM.
+TEST(BRWTCompressed, Serialization) {
+    const std::string base = "/tmp/mbrwt_test_annotation_dump";
+    auto f = make_fixture(5, {{0, {"Label0", "Label2", "Label8"}}, {2, {"Label1", "Label2"}}, {4, {"Label8"}}});
+    auto a = annotator(f);
+    if (!g_device) {
+        std::stringstream ss;
+        f.enc.serialize(ss);
+        mbrwt_host::LabelEncoder<std::string> e2;
+        ASSERT_TRUE(e2.load(ss));
+        ASSERT_EQ(f.enc.size(), e2.size());
+        for (size_t i = 0; i < e2.size(); ++i) EXPECT_EQ(f.enc.decode(i), e2.decode(i));
+        EXPECT_EQ(2u, e2.encode("Label8"));
+        return;
+    }
+    auto m = std::make_shared<mbrwt_host::BRWTDevice>(
+        to_device(OracleMatrix(build_oracle(f.cols, f.n, 0, 2))));
+    StaticBinRelAnnotator<mbrwt_host::BRWTDevice> dev(m, f.enc);
+    dev.serialize(base);  // writes base + ".brwt.annodbg"
+    StaticBinRelAnnotator<mbrwt_host::BRWTDevice> annotation;
+    EXPECT_TRUE(!annotation.load(base + "_missing"));
+    ASSERT_TRUE(annotation.load(base));
+    EXPECT_EQ(S({"Label0", "Label2", "Label8"}), S(annotation.get(0)));
+    EXPECT_EQ(S({}), S(annotation.get(1)));
+    EXPECT_EQ(S({"Label1", "Label2"}), S(annotation.get(2)));
+    EXPECT_EQ(S({}), S(annotation.get(3)));
+    EXPECT_EQ(S({"Label8"}), S(annotation.get(4)));
+    EXPECT_EQ(5u, annotation.num_objects());
+    EXPECT_EQ(4u, annotation.num_labels());
+    EXPECT_EQ(6u, annotation.num_relations());
+    // the dynamic actions of a static annotator throw (annotate_static.cpp:164-168)
+    EXPECT_THROW(annotation.add_label(0, "Label1"), std::runtime_error);
 }
 
 int main(int argc, char **argv) {

@@ -20,6 +20,8 @@ class OracleWTMatrix : public BinaryMatrix {
     uint64_t num_columns() const override { return wt_oracle_num_columns(t_.get()); }
     uint64_t num_rows() const override { return wt_oracle_num_rows(t_.get()); }
     uint64_t num_relations() const override { return wt_oracle_num_relations(t_.get()); }
+    bool load(std::istream &) override { return false; }
+    void serialize(std::ostream &) const override { throw std::runtime_error("not supported"); }
     bool get(Row r, Column c) const override {
         int v = wt_oracle_get(t_.get(), r, c);
         if (v < 0) throw std::out_of_range("oracle get");

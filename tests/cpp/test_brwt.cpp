@@ -2,7 +2,10 @@
 // (reference) through the C++ mirror's BinaryMatrix interface, on the
 // backend named by argv[1] (oracle | device).
 #include <algorithm>
+#include <fstream>
+#include <iterator>
 #include <set>
+#include <sstream>
 
 #include "backends.hpp"
 #include "minitest.hpp"
@@ -131,6 +134,68 @@ TEST(BRWTOptimizer, BuildBottomUPAllMixed) { grid(2, UINT64_MAX); }
 TEST(BRWTOptimizer, DeviceBuilderAllZero) { grid_device_built(0, UINT64_MAX); }
 TEST(BRWTOptimizer, DeviceBuilderAllOne) { grid_device_built(1, UINT64_MAX); }
 TEST(BRWTOptimizer, DeviceBuilderAllMixed) { grid_device_built(2, UINT64_MAX); }
+
+// test_serialization (test_BRWT.cpp:214-238) over the grids: the dumped
+// matrix loads back (stream still good) with the same shape and every column;
+// a bad stream does not load.  The oracle's tree is dumped by the host-side
+// writer; oracle backend: the stream parses back to the oracle's own tree;
+// device backend: BRWTDevice::load puts it in HBM and is queried, then the
+// device matrix is dumped and loaded again.
+static void grid_serialization(int kind, uint64_t relax) {
+    const std::string good = "/tmp/mbrwt_test_brwt_dump_good", bad = "/tmp/mbrwt_test_brwt_dump_bad_missing";
+    for (uint64_t n = 1; n < 20; n += 3) {
+        for (size_t mcols = 1; mcols < 20; mcols += 2) {
+            Columns cols(mcols, std::vector<bool>(n));
+            for (size_t j = 0; j < mcols; ++j)
+                for (uint64_t i = 0; i < n; ++i)
+                    cols[j][i] = kind == 0 ? false : kind == 1 ? true : ((i + 2 * j) % 2) != 0;
+            auto om = OracleMatrix(build_oracle(cols, n, 0, 2, relax));
+            {
+                std::ofstream out(good, std::ios::binary);
+                om.serialize(out);
+            }
+            if (!g_device) {
+                std::ifstream in(good, std::ios::binary);
+                std::vector<char> buf((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+                mbrwt_tree *t = nullptr;
+                uint64_t used = 0;
+                ASSERT_EQ(MBRWT_OK, mbrwt_tree_parse(reinterpret_cast<const uint8_t *>(buf.data()), buf.size(),
+                                                     &used, &t));
+                ASSERT_EQ(buf.size(), used);
+                const mbrwt_tree_desc *d = mbrwt_tree_get_desc(t);
+                EXPECT_EQ(om.num_rows(), d->num_rows);
+                EXPECT_EQ(om.num_columns(), d->num_columns);
+                EXPECT_EQ(oracle_export_num_nodes(om.tree()), d->num_nodes);
+                mbrwt_tree_free(t);
+                continue;
+            }
+            mbrwt_host::BRWTDevice loaded;
+            {
+                std::ifstream in(bad, std::ios::binary);
+                ASSERT_TRUE(!loaded.load(in));
+            }
+            {
+                std::ifstream in(good, std::ios::binary);
+                ASSERT_TRUE(loaded.load(in));
+                ASSERT_TRUE(in.good());
+            }
+            ASSERT_EQ(om.num_columns(), loaded.num_columns());
+            ASSERT_EQ(om.num_rows(), loaded.num_rows());
+            for (size_t j = 0; j < loaded.num_columns(); ++j) EXPECT_EQ(om.get_column(j), loaded.get_column(j));
+            test_brwt(loaded, cols, n);
+            // and the device matrix's own dump
+            std::stringstream ss;
+            loaded.serialize(ss);
+            mbrwt_host::BRWTDevice again;
+            ASSERT_TRUE(again.load(ss));
+            test_brwt(again, cols, n);
+        }
+    }
+}
+TEST(BRWT, SerializationAllZero) { grid_serialization(0, 0); }
+TEST(BRWT, SerializationAllOne) { grid_serialization(1, 0); }
+TEST(BRWT, SerializationAllMixed) { grid_serialization(2, 0); }
+TEST(BRWTOptimizer, SerializationAllMixed) { grid_serialization(2, UINT64_MAX); }
 
 int main(int argc, char **argv) {
     g_device = argc > 1 && std::string(argv[1]) == "device";
