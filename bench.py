@@ -246,7 +246,7 @@ def main():
     kernel_re = None
     traffic = None
     if rank == 0 and world == 1 and a.traffic != "off":
-        kernel_re = "k_traverse_fast2" if a.kernel == 0 else "k_traverse"
+        kernel_re = "k_traverse_(p2w|fast2)" if a.kernel == 0 or 17 <= a.kernel <= 23 else "k_traverse"
         if a.traffic == "live":
             traffic = live_traffic(a, kernel_re)
             if traffic is not None and a.traffic_out:
@@ -403,21 +403,31 @@ def main():
                            + (f", reassembled by the all-gatherv from {world} ranks" if world > 1 else "")}
         del off_o, cols_o
         if world == 1:
-            sample = rows_global[: a.cpu_sample]
-            c0 = time.perf_counter()
-            ref.time_rows(sample, threads)
-            cpu_s = time.perf_counter() - c0
-            s1 = rows_global[: a.cpu_sample_1t]
-            c0 = time.perf_counter()
-            ref.time_rows(s1, 1)
-            cpu1_s = time.perf_counter() - c0
-            cpu = {"value": len(sample) / cpu_s, "unit": "rows/s", "cores": threads, "kind": "port",
-                   "sample": f"first {len(sample):,} rows of the batch on the same {a.rows:,} x {a.cols:,} "
-                             f"structure (oracle restatement of BRWT::get_row, plain rank/select; host build "
-                             f"{gen_s:.0f} s); {threads} threads = the job's CPU share (OMP_NUM_THREADS / "
-                             f"affinity {share}; nproc {nproc})",
-                   "single_thread": {"value": len(s1) / cpu1_s, "unit": "rows/s", "cores": 1,
-                                     "sample": f"first {len(s1):,} rows"},
+            def timed(n_rows, th):
+                sample = rows_global[:n_rows]
+                c0 = time.perf_counter()
+                ref.time_rows(sample, th)
+                return len(sample) / (time.perf_counter() - c0)
+            plain = timed(a.cpu_sample, threads)
+            plain1 = timed(a.cpu_sample_1t, 1)
+            c0 = time.time()
+            ref.to_rrr(threads)  # the reference's bit_vector_rrr<63> cost profile
+            rrr_s = time.time() - c0
+            rrr = timed(a.cpu_sample // 10, threads)
+            rrr1 = timed(a.cpu_sample_1t // 10, 1)
+            cpu = {"value": rrr, "unit": "rows/s", "cores": threads, "kind": "port",
+                   "sample": f"first {a.cpu_sample // 10:,} rows of the batch on the same {a.rows:,} x {a.cols:,} "
+                             f"structure: the oracle's restatement of BRWT::get_row over sdsl-RRR-like index "
+                             f"vectors (63-bit blocks, class + combinatorial number, samples every 32 blocks: "
+                             f"bit_vector_rrr<63>'s cost profile; host build {gen_s:.0f} s + RRR encode "
+                             f"{rrr_s:.0f} s); {threads} threads = the job's CPU share (OMP_NUM_THREADS "
+                             f"{omp or 'unset'}, affinity {share}; the node's nproc {nproc} is shared by 8 GPU jobs)",
+                   "single_thread": {"value": rrr1, "unit": "rows/s", "cores": 1,
+                                     "sample": f"first {a.cpu_sample_1t // 10:,} rows, RRR-like"},
+                   "plain_rank": {"value": plain, "unit": "rows/s", "cores": threads,
+                                  "sample": f"first {a.cpu_sample:,} rows, plain bit vectors + rank samples"},
+                   "plain_rank_single_thread": {"value": plain1, "unit": "rows/s", "cores": 1,
+                                                "sample": f"first {a.cpu_sample_1t:,} rows"},
                    "nproc": nproc}
         del ref
 

@@ -167,22 +167,149 @@ struct RangePartition {
 };
 
 // ------------------------------------------------------------------------
+// sdsl-RRR-like bit vector (the cost model of the reference's
+// bit_vector_rrr<63>, common/bit_vector.cpp:857-888 over sdsl::rrr_vector<63>):
+// 63-bit blocks stored as {class = popcount (6 bits), the block's number
+// among the blocks of its class (ceil(log2 C(63, class)) bits)}, a rank and a
+// number-pointer sample every 32 blocks.  operator[] / rank1 walk the classes
+// since the sample and decode ONE block by the combinatorial number system --
+// the work an sdsl access does.  Only the CPU baseline uses it (timing); its
+// answers are checked against the plain vector in the KAT tests.
+// ------------------------------------------------------------------------
+struct RRRVec {
+    static constexpr uint32_t B = 63, K = 32;
+    uint64_t size = 0, ones = 0;
+    std::vector<uint8_t> cls;
+    std::vector<uint64_t> nums, srank, sptr;
+
+    struct Tables {
+        uint64_t C[B + 1][B + 1];
+        uint8_t space[B + 1];
+        Tables() {
+            std::memset(C, 0, sizeof(C));
+            for (uint32_t n = 0; n <= B; ++n) {
+                C[n][0] = 1;
+                for (uint32_t k = 1; k <= n; ++k) C[n][k] = C[n - 1][k - 1] + (k < n ? C[n - 1][k] : 0);
+            }
+            for (uint32_t k = 0; k <= B; ++k)
+                space[k] = C[B][k] <= 1 ? 0 : (uint8_t)(64 - __builtin_clzll(C[B][k] - 1));
+        }
+    };
+    static const Tables &T() {
+        static const Tables t;
+        return t;
+    }
+    static uint64_t getbits(const std::vector<uint64_t> &w, uint64_t pos, uint32_t len) {
+        if (!len) return 0;
+        const uint64_t i = pos >> 6, o = pos & 63;
+        uint64_t v = w[i] >> o;
+        if (o && o + len > 64) v |= w[i + 1] << (64 - o);
+        return len == 64 ? v : v & ((1ull << len) - 1);
+    }
+    static void setbits(std::vector<uint64_t> &w, uint64_t pos, uint32_t len, uint64_t v) {
+        if (!len) return;
+        const uint64_t i = pos >> 6, o = pos & 63;
+        w[i] |= v << o;
+        if (o && o + len > 64) w[i + 1] |= v >> (64 - o);
+    }
+
+    explicit RRRVec(const BitVec &bv) : size(bv.size), ones(bv.ones) {
+        const Tables &t = T();
+        const uint64_t nb = (size + B - 1) / B;
+        cls.resize(nb);
+        std::vector<uint64_t> blk(nb);
+        uint64_t bits = 0;
+        for (uint64_t b = 0; b < nb; ++b) {
+            const uint64_t p = b * B;
+            const uint32_t len = (uint32_t)std::min<uint64_t>(B, size - p);
+            uint64_t x = bv.words[p >> 6] >> (p & 63);
+            if ((p & 63) && (p & 63) + len > 64) x |= bv.words[(p >> 6) + 1] << (64 - (p & 63));
+            x &= (len == 64 ? ~0ull : ((1ull << len) - 1));
+            blk[b] = x;
+            cls[b] = (uint8_t)__builtin_popcountll(x);
+            bits += t.space[cls[b]];
+        }
+        nums.assign(bits / 64 + 2, 0);
+        srank.resize(nb / K + 2);
+        sptr.resize(nb / K + 2);
+        uint64_t pos = 0, r = 0;
+        for (uint64_t b = 0; b < nb; ++b) {
+            if (b % K == 0) {
+                srank[b / K] = r;
+                sptr[b / K] = pos;
+            }
+            // number of the block among the blocks of its class (LSB first)
+            uint64_t x = blk[b], nr = 0;
+            uint32_t k = cls[b], nn = B;
+            while (x) {
+                if (x & 1) nr += t.C[nn - 1][k--];
+                x >>= 1;
+                --nn;
+            }
+            setbits(nums, pos, t.space[cls[b]], nr);
+            pos += t.space[cls[b]];
+            r += cls[b];
+        }
+    }
+    // bits [0, o] of block b, decoded from its number (LSB first, stopping
+    // after position o as sdsl's decode_bit / decode_popcount do); *rank_before
+    // = ones before the block (sample + the classes walked since it)
+    uint64_t block_prefix(uint64_t b, uint32_t o, uint64_t *rank_before) const {
+        const Tables &t = T();
+        const uint64_t s = b / K;
+        uint64_t pos = sptr[s], r = srank[s];
+        for (uint64_t j = s * K; j < b; ++j) {
+            pos += t.space[cls[j]];
+            r += cls[j];
+        }
+        if (rank_before) *rank_before = r;
+        uint32_t k = cls[b];
+        const uint64_t upto = o == 63 ? ~0ull : ((2ull << o) - 1);
+        if (k == 0) return 0;
+        if (k == B) return ((1ull << B) - 1) & upto;
+        uint64_t nr = getbits(nums, pos, t.space[k]), x = 0;
+        for (uint32_t p = 0, nn = B; k && p <= o; ++p, --nn) {
+            const uint64_t c = t.C[nn - 1][k];
+            if (nr >= c) {
+                x |= 1ull << p;
+                nr -= c;
+                --k;
+            }
+        }
+        return x;
+    }
+    bool get(uint64_t i) const {
+        const uint32_t o = (uint32_t)(i % B);
+        return (block_prefix(i / B, o, nullptr) >> o) & 1;
+    }
+    uint64_t rank1(uint64_t i) const {  // inclusive, clamped (bit_vector.cpp:857-861)
+        if (i >= size) return ones;
+        uint64_t r = 0;
+        const uint64_t x = block_prefix(i / B, (uint32_t)(i % B), &r);
+        return r + (uint64_t)__builtin_popcountll(x);
+    }
+};
+
+// ------------------------------------------------------------------------
 // BRWT node (annotation/hierarchical_annotation/BRWT.hpp:18-61)
 // ------------------------------------------------------------------------
 struct Node {
     RangePartition assignments;
     BitVec nonzero_rows;
+    std::unique_ptr<RRRVec> rrr;  // set by to_rrr(): the index held RRR-like (CPU baseline)
     std::vector<std::unique_ptr<Node>> children;
 
     uint64_t num_columns() const { return assignments.size(); }
     uint64_t num_rows() const { return nonzero_rows.size; }
+    bool bit(uint64_t i) const { return rrr ? rrr->get(i) : nonzero_rows.get(i); }
+    uint64_t rank(uint64_t i) const { return rrr ? rrr->rank1(i) : nonzero_rows.rank1(i); }
 
     // BRWT::get (BRWT.cpp:9-24)
     bool get(uint64_t row, uint64_t col) const {
-        if (!nonzero_rows.get(row)) return false;
+        if (!bit(row)) return false;
         if (children.empty()) return true;
         uint32_t g = assignments.group((uint32_t)col);
-        return children[g]->get(nonzero_rows.rank1(row) - 1, assignments.rank((uint32_t)col));
+        return children[g]->get(rank(row) - 1, assignments.rank((uint32_t)col));
     }
 
     // BRWT::get_row (BRWT.cpp:26-53), appending to `out` in the reference's
@@ -190,12 +317,12 @@ struct Node {
     // assignments_.get(i, col) exactly as BRWT.cpp:48-50 does.
     void get_row(uint64_t row, std::vector<uint32_t> &out, uint64_t &visits) const {
         ++visits;                                  // nonzero_rows_[row], BRWT.cpp:30
-        if (!nonzero_rows.get(row)) return;
+        if (!bit(row)) return;
         if (children.empty()) {                    // BRWT.cpp:34-39
             out.push_back(0);
             return;
         }
-        uint64_t j = nonzero_rows.rank1(row) - 1;  // BRWT.cpp:43
+        uint64_t j = rank(row) - 1;                // BRWT.cpp:43
         for (size_t i = 0; i < children.size(); ++i) {
             size_t start = out.size();
             children[i]->get_row(j, out, visits);
@@ -1222,6 +1349,24 @@ int oracle_bv_get(const OracleBitVec *bv, uint64_t id) { return id < bv->bv.size
 uint64_t oracle_bv_num_set_bits(const OracleBitVec *bv) { return bv->bv.ones; }
 
 uint64_t oracle_synth_hash(uint64_t seed, uint64_t key, uint64_t pos) { return synth_draw(synth_key(seed, key), pos); }
+
+// Re-encode every node's index RRR-like (RRRVec) and drop the plain words:
+// the CPU baseline's sdsl-like leg.  Afterwards only get / get_row /
+// time_rows are valid on the tree.
+void oracle_to_rrr(OracleTree *t, int threads) {
+    std::vector<Node *> all{t->root.get()};
+    for (size_t h = 0; h < all.size(); ++h)
+        for (auto &c : all[h]->children) all.push_back(c.get());
+    threads = resolve_threads(threads);
+    const int64_t N = (int64_t)all.size();
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1)
+    for (int64_t i = 0; i < N; ++i) {
+        Node *nd = all[i];
+        nd->rrr = std::make_unique<RRRVec>(nd->nonzero_rows);
+        std::vector<uint64_t>().swap(nd->nonzero_rows.words);
+        std::vector<uint64_t>().swap(nd->nonzero_rows.super);
+    }
+}
 
 struct OracleCSR {
     std::vector<uint64_t> offsets;

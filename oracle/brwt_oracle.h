@@ -104,6 +104,13 @@ uint64_t oracle_time_rows(const OracleTree *t, const uint64_t *rows, uint64_t n,
 /* BRWT::get_column (BRWT.cpp:55-85): returns count, writes up to cap rows. */
 uint64_t oracle_get_column(const OracleTree *t, uint64_t col, uint64_t *out, uint64_t cap);
 
+/* The CPU baseline's sdsl-RRR-like leg: re-encode every node's index as
+ * 63-bit blocks {class, combinatorial number} with rank / pointer samples
+ * every 32 blocks (the cost model of bit_vector_rrr<63>,
+ * bit_vector.cpp:857-888) and drop the plain bits.  Afterwards only
+ * oracle_get / oracle_get_row(s) / oracle_time_rows are valid. */
+void oracle_to_rrr(OracleTree *t, int num_threads);
+
 /* ---- export in BFS numbering (the layout of include/mbrwt.h's tree desc) -- */
 uint32_t oracle_export_num_nodes(const OracleTree *t);
 /* arrays of length oracle_export_num_nodes(); leaf_column = UINT32_MAX for

@@ -87,6 +87,7 @@ def lib():
         "oracle_csr_draws": (C.c_uint64, [vp]),
         "oracle_csr_copy": (None, [vp, u64p, u32p]),
         "oracle_csr_free": (None, [vp]),
+        "oracle_to_rrr": (None, [vp, C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -241,6 +242,12 @@ class OracleTree:
     def time_rows(self, rows, threads=0):
         rows = np.ascontiguousarray(rows, dtype=np.uint64)
         return lib().oracle_time_rows(self._h, _p64(rows), len(rows), threads)
+
+    def to_rrr(self, threads=0):
+        """Re-encode the indexes sdsl-RRR-like (CPU baseline); afterwards
+        only get / get_row(s) / time_rows are valid."""
+        lib().oracle_to_rrr(self._h, threads)
+        return self
 
     def get_column(self, col):
         cap = max(1, self.num_rows())

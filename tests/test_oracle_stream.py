@@ -40,3 +40,20 @@ def test_wt_rows_at_matches_range(oracle_mod):
     for i, r in enumerate(rows[:500]):
         assert np.array_equal(c2[o2[i]:o2[i + 1]], c1[o1[r]:o1[r + 1]])
     assert o2[-1] == sum(o1[r + 1] - o1[r] for r in rows)
+
+
+@pytest.mark.parametrize("n,m,d,arity", [(50000, 2652, 0.003, 8), (20000, 3173, 0.038, 8), (3000, 9, 0.5, 2),
+                                         (20000, 50, 0.9, 2), (3000, 7, 0.0, 2), (3000, 7, 1.0, 2), (4033, 5, 0.97, 2)])
+def test_rrr_layout_answers_like_plain(oracle_mod, n, m, d, arity):
+    """The CPU baseline's sdsl-RRR-like index vectors (oracle_to_rrr) give the
+    plain vectors' get_row / get / V accounting exactly."""
+    O = oracle_mod
+    t = O.OracleTree.topdown(n, m, d, arity, 42)
+    rows = np.random.default_rng(n).integers(0, n, 5000).astype(np.uint64)
+    o1, c1, v1 = t.get_rows(rows, with_visits=True)
+    pts = [(int(r), int(c)) for r, c in zip(rows[:300], np.random.default_rng(1).integers(0, m, 300))]
+    g1 = [t.get(r, c) for r, c in pts]
+    t.to_rrr()
+    o2, c2, v2 = t.get_rows(rows, with_visits=True)
+    assert np.array_equal(o1, o2) and np.array_equal(c1, c2) and np.array_equal(v1, v2)
+    assert g1 == [t.get(r, c) for r, c in pts]
