@@ -53,6 +53,15 @@ class SynthDesc(C.Structure):
     ]
 
 
+class ShapeDesc(C.Structure):
+    _fields_ = [
+        ("num_nodes", C.c_uint32),
+        ("num_children", u32p),
+        ("first_child", u32p),
+        ("leaf_column", u32p),
+    ]
+
+
 class ColumnsDesc(C.Structure):
     _fields_ = [
         ("num_rows", C.c_uint64),
@@ -84,6 +93,8 @@ class BinRelSynthDesc(C.Structure):
 SIGNATURES = {
     "mbrwt_create": (C.c_int, [C.POINTER(TreeDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "mbrwt_create_synthetic": (C.c_int, [C.POINTER(SynthDesc), C.c_int, C.POINTER(C.c_void_p)]),
+    "mbrwt_create_synthetic_shaped": (C.c_int, [C.POINTER(SynthDesc), C.POINTER(ShapeDesc), C.c_int,
+                                                C.POINTER(C.c_void_p)]),
     "mbrwt_create_from_columns": (C.c_int, [C.POINTER(ColumnsDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "mbrwt_create_from_columns_relaxed": (C.c_int, [C.POINTER(ColumnsDesc), C.c_uint64, C.c_int,
                                                     C.POINTER(C.c_void_p)]),

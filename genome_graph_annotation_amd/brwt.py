@@ -166,6 +166,23 @@ class BRWTDevice:
         return cls(h)
 
     @classmethod
+    def synthetic_shaped(cls, num_rows, shape, density, seed=42, device=0):
+        """The synthetic law over a given tree shape (mbrwt_create_synthetic_shaped):
+        `shape` = dict with num_children, first_child, leaf_column (BFS), e.g.
+        the export of a greedy + relaxed tree."""
+        lib = L.lib()
+        nc = np.ascontiguousarray(shape["num_children"], dtype=np.uint32)
+        fc = np.ascontiguousarray(shape["first_child"], dtype=np.uint32)
+        lc = np.ascontiguousarray(shape["leaf_column"], dtype=np.uint32)
+        m = int((nc == 0).sum())
+        d = L.SynthDesc(num_rows, m, float(density), 0, seed)
+        sd = L.ShapeDesc(len(nc), _p(nc, C.c_uint32), _p(fc, C.c_uint32), _p(lc, C.c_uint32))
+        h = C.c_void_p()
+        L.check(lib.mbrwt_create_synthetic_shaped(C.byref(d), C.byref(sd), device, C.byref(h)),
+                "mbrwt_create_synthetic_shaped")
+        return cls(h)
+
+    @classmethod
     def from_columns(cls, columns, num_rows, arity=2, device=0, relax_max_arity=0):
         """BRWTBottomUpBuilder::build with the basic partitioner on the device
         (include/mbrwt.h mbrwt_create_from_columns).  `columns`: a sequence of

@@ -410,7 +410,7 @@ int export_tree(const Ctx &c, mbrwt_tree &out) {
         const uint32_t fc = dn.kind == KIND_FOLDED ? t.nodes[0].first_child : dn.first_child;
         out.num_children[u] = a;
         out.first_child[u] = a ? fc - 1 : 0;
-        if (!a) out.leaf_column[u] = dn.label;
+        if (!a) out.leaf_column[u] = t.label_perm.empty() ? dn.label : t.label_perm.at(dn.label);
         out.vec_size[u] = cols[u + 1].n;
         out.words[u] = std::move(cols[u + 1].w);
     }

@@ -36,6 +36,10 @@ static int upload_tables(Ctx &c) {
         MBRWT_HIP(hipMalloc(&c.d_cnodes, cn.size() * sizeof(CNode)));
         MBRWT_HIP(hipMemcpy(c.d_cnodes, cn.data(), cn.size() * sizeof(CNode), hipMemcpyHostToDevice));
     }
+    if (!t.label_perm.empty()) {
+        MBRWT_HIP(hipMalloc(&c.d_label_map, t.label_perm.size() * 4));
+        MBRWT_HIP(hipMemcpy(c.d_label_map, t.label_perm.data(), t.label_perm.size() * 4, hipMemcpyHostToDevice));
+    }
     if (!t.p2w_table.empty()) {
         MBRWT_HIP(hipMalloc(&c.d_p2w, t.p2w_table.size() * 4));
         MBRWT_HIP(hipMemcpy(c.d_p2w, t.p2w_table.data(), t.p2w_table.size() * 4, hipMemcpyHostToDevice));
@@ -66,6 +70,7 @@ static void release(Ctx *c) {
     if (c->d_nodes) (void)hipFree(c->d_nodes);
     if (c->d_cnodes) (void)hipFree(c->d_cnodes);
     if (c->d_p2w) (void)hipFree(c->d_p2w);
+    if (c->d_label_map) (void)hipFree(c->d_label_map);
     if (c->d_col_path) (void)hipFree(c->d_col_path);
     if (c->d_col_leaf) (void)hipFree(c->d_col_leaf);
     if (c->d_scalars) (void)hipFree(c->d_scalars);
@@ -136,6 +141,24 @@ int mbrwt_create(const mbrwt_tree_desc *desc, int device, mbrwt_ctx **out) {
     }
 }
 
+int mbrwt_create_synthetic_shaped(const mbrwt_synth_desc *desc, const mbrwt_shape_desc *shape, int device,
+                                  mbrwt_ctx **out) {
+    if (!desc || !shape) {
+        set_error("null synthetic or shape description");
+        return MBRWT_ERR_INVALID;
+    }
+    try {
+        return create_common(device, out,
+                             [&](Ctx &c) { return build_synthetic(*desc, shape, device, c.tree, c.stream); });
+    } catch (const std::bad_alloc &) {
+        set_error("host allocation failed");
+        return MBRWT_ERR_NOMEM;
+    } catch (...) {
+        set_error("unexpected exception in mbrwt_create_synthetic_shaped");
+        return MBRWT_ERR_INVALID;
+    }
+}
+
 int mbrwt_create_synthetic(const mbrwt_synth_desc *desc, int device, mbrwt_ctx **out) {
     if (!desc) {
         set_error("null synthetic description");
@@ -143,7 +166,7 @@ int mbrwt_create_synthetic(const mbrwt_synth_desc *desc, int device, mbrwt_ctx *
     }
     try {
         return create_common(device, out,
-                             [&](Ctx &c) { return build_synthetic(*desc, device, c.tree, c.stream); });
+                             [&](Ctx &c) { return build_synthetic(*desc, nullptr, device, c.tree, c.stream); });
     } catch (const std::bad_alloc &) {
         set_error("host allocation failed");
         return MBRWT_ERR_NOMEM;

@@ -194,18 +194,17 @@ bool build_pack_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, DevNo
 }
 
 // desc node u may become KIND_PACK: 1..8 children, each with 1..8 leaf
-// children of consecutive columns (MASK8 nodes with FLAG_CONSEC_LABELS)
+// children (MASK8 nodes; their labels are consecutive pre-order indices)
 bool pack_candidate(const mbrwt_tree_desc &desc, uint32_t u) {
     const uint32_t a = desc.num_children[u];
     if (a == 0 || a > 8) return false;
     for (uint32_t c = 0; c < a; ++c) {
         const uint32_t ch = desc.first_child[u] + c, gc = desc.num_children[ch];
         if (gc == 0 || gc > 8) return false;
-        for (uint32_t k = 0; k < gc; ++k) {
-            const uint32_t leaf = desc.first_child[ch] + k;
-            if (desc.num_children[leaf] != 0) return false;
-            if (desc.leaf_column[leaf] != desc.leaf_column[desc.first_child[ch]] + k) return false;
-        }
+        // (any leaf columns: leaves are labelled by pre-order index, so the
+        // leaves below one node are consecutive labels -- finalize_tree)
+        for (uint32_t k = 0; k < gc; ++k)
+            if (desc.num_children[desc.first_child[ch] + k] != 0) return false;
     }
     return true;
 }
@@ -606,6 +605,42 @@ int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
 int finalize_tree(Tree &tree) {
     const uint32_t D = (uint32_t)tree.nodes.size();
     if (D == 0) return MBRWT_OK;
+    // leaves labelled by pre-order index (Tree::label_perm): a DFS from the
+    // super-root in child order (the folded root's children hang off dnode 0)
+    {
+        std::vector<uint32_t> perm;
+        std::vector<uint32_t> st{0};
+        bool identity = true;
+        while (!st.empty()) {
+            const uint32_t v = st.back();
+            st.pop_back();
+            DevNode &dn = tree.nodes[v];
+            if (dn.kind == KIND_LEAF && v != 0) {
+                identity &= dn.label == (uint32_t)perm.size();
+                perm.push_back(dn.label);
+                continue;
+            }
+            if (dn.kind == KIND_FOLDED || dn.kind == KIND_LEAF) continue;
+            for (uint32_t c = dn.arity; c-- > 0;) st.push_back(dn.first_child + c);
+        }
+        tree.label_perm.clear();
+        if (!identity) {
+            uint32_t k = 0;
+            st.assign(1, 0);
+            while (!st.empty()) {
+                const uint32_t v = st.back();
+                st.pop_back();
+                DevNode &dn = tree.nodes[v];
+                if (dn.kind == KIND_LEAF && v != 0) {
+                    dn.label = k++;
+                    continue;
+                }
+                if (dn.kind == KIND_FOLDED || dn.kind == KIND_LEAF) continue;
+                for (uint32_t c = dn.arity; c-- > 0;) st.push_back(dn.first_child + c);
+            }
+            tree.label_perm = std::move(perm);
+        }
+    }
     // consecutive-label flag for MASK nodes
     for (uint32_t v = 0; v < D; ++v) {
         DevNode &dn = tree.nodes[v];
@@ -688,7 +723,7 @@ int finalize_tree(Tree &tree) {
     for (uint32_t v = 0; v < D; ++v) {
         const DevNode &dn = tree.nodes[v];
         if (dn.kind != KIND_LEAF || v == 0) continue;
-        uint32_t col = dn.label;
+        const uint32_t col = tree.label_perm.empty() ? dn.label : tree.label_perm[dn.label];
         tree.col_leaf[col] = v;
         // path from the super-root down to the leaf
         std::vector<uint8_t> rev;

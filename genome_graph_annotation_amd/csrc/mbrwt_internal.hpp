@@ -174,6 +174,12 @@ struct Tree {
     // k_traverse_p2w (the super-root's children all KIND_PACK2): the compact
     // table it stages in LDS (layout: query.hip "P2W table"), empty otherwise
     std::vector<uint32_t> p2w_table;
+    // Leaves are labelled by their PRE-ORDER index (the reference's output
+    // order, BRWT.cpp:45-51), so the leaves below any node are consecutive
+    // labels whatever the partitioner (greedy trees included); label_perm maps
+    // a pre-order index back to the global column (empty = identity, e.g. the
+    // basic partitioner).  Kernels emit pre-order indices; the CSR writers map.
+    std::vector<uint32_t> label_perm;
     uint32_t max_arity = 0;
     uint64_t num_rows = 0, num_columns = 0, num_relations = 0, num_nodes = 0;
     uint64_t image_bytes = 0;
@@ -225,6 +231,7 @@ struct Ctx {
     DevNode *d_nodes = nullptr;
     CNode *d_cnodes = nullptr;
     uint32_t *d_p2w = nullptr;          // Tree::p2w_table on the device
+    uint32_t *d_label_map = nullptr;    // Tree::label_perm on the device (null = identity)
     uint8_t *d_col_path = nullptr;
     uint32_t *d_col_leaf = nullptr;
     hipStream_t stream = nullptr;       // stream of the host-buffer API
@@ -262,7 +269,8 @@ int ensure(Workspace &w, size_t bytes);
 
 // image construction (image.cpp / synth.hip)
 int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree);
-int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStream_t stream);
+int build_synthetic(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape, int device, Tree &tree,
+                    hipStream_t stream);
 int build_from_columns(const mbrwt_columns_desc &desc, int device, Tree &tree, hipStream_t stream,
                        uint64_t relax_max_arity = 0);
 // BRWTOptimizer::relax on a tree description (build.hip)

@@ -49,7 +49,32 @@ struct TravParams {
     const CNode *cnodes;         // compact node records (group kernel)
     uint32_t n_lds;              // records [0, n_lds) are staged in LDS
     uint32_t folded;             // root folded into the super-root (V accounting)
+    const uint32_t *label_map;   // pre-order index -> global column (Tree::label_perm; null = identity)
 };
+
+// MODE_DIRECT / MODE_COUNT write final columns; the slot modes keep pre-order
+// indices and the compaction maps them
+__device__ __forceinline__ uint32_t final_label(const uint32_t *map, uint32_t label) {
+    return map ? gld(map + label) : label;
+}
+
+// The compaction kernels stage the label map in LDS when it is small (one
+// random 4-byte global read per label measured 2.3 ms per 8 M labels on a
+// greedy tree): `lds_entries` > 0 = the first kernel arguments' map copied
+// into the dynamic LDS of the workgroup.
+constexpr uint32_t kMapLdsMax = 16384;  // entries (64 KiB)
+struct LabelMap {
+    const uint32_t *g;
+    const AS_LDS uint32_t *l;
+    __device__ __forceinline__ uint32_t operator()(uint32_t x) const { return l ? l[x] : g ? gld(g + x) : x; }
+};
+__device__ __forceinline__ LabelMap stage_label_map(const uint32_t *map, uint32_t lds_entries) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_label_map[];
+    if (!map || !lds_entries) return LabelMap{map, nullptr};
+    for (uint32_t i = threadIdx.x; i < lds_entries; i += blockDim.x) lds_label_map[i] = gld(map + i);
+    __syncthreads();
+    return LabelMap{map, (const AS_LDS uint32_t *)lds_label_map};
+}
 
 // decoded node record
 struct NodeInfo {
@@ -119,9 +144,9 @@ struct Sink {
         if constexpr (MODE == MODE_SLOTS) {
             if (cnt < p.K) gst(p.temp + slot_base + cnt, label);
         } else if constexpr (MODE == MODE_DIRECT) {
-            gst(p.cols + slot_base + cnt, label);
+            gst(p.cols + slot_base + cnt, final_label(p.label_map, label));
         } else if constexpr (MODE == MODE_COUNT) {
-            atomicAdd(&p.label_counts[label], 1ull);
+            atomicAdd(&p.label_counts[final_label(p.label_map, label)], 1ull);
         }
         ++cnt;
     }
@@ -373,6 +398,7 @@ struct GroupSink {
     // lane-parallel emission: `label` goes to position cnt + rank
     __device__ __forceinline__ void put(const TravParams &p, uint32_t rank, uint32_t label) {
         const uint32_t pos = cnt + rank;
+        if constexpr (MODE == MODE_DIRECT || MODE == MODE_COUNT) label = final_label(p.label_map, label);
         if constexpr (MODE == MODE_SLOTS || MODE == MODE_DIRECT) {
             if (pos < kStageLabels) {
                 stage[pos] = label;
@@ -1269,7 +1295,9 @@ __global__ __launch_bounds__(256) void k_compact_blocks(const uint32_t *__restri
                                                         const uint64_t *__restrict__ block_offsets,
                                                         const uint32_t *__restrict__ temp, uint32_t C,
                                                         uint64_t *__restrict__ offsets, uint32_t *__restrict__ cols,
-                                                        uint64_t n) {
+                                                        uint64_t n, const uint32_t *__restrict__ label_map,
+                                                        uint32_t map_lds) {
+    const LabelMap lmap = stage_label_map(label_map, map_lds);
     const uint32_t lane = threadIdx.x & 63, sub = lane & 15;
     const uint64_t nb = (n + 15) / 16;
     const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) >> 4;
@@ -1294,7 +1322,7 @@ __global__ __launch_bounds__(256) void k_compact_blocks(const uint32_t *__restri
 #pragma unroll
             for (uint32_t k = 0; k < 8; ++k) {
                 const uint32_t i = i0 + sub + 16 * k;
-                v[k] = i < total ? gld(src + i) : 0u;
+                v[k] = i < total ? lmap(gld(src + i)) : 0u;
             }
 #pragma unroll
             for (uint32_t k = 0; k < 8; ++k) {
@@ -1323,7 +1351,9 @@ __global__ __launch_bounds__(256) void k_compact_chunks(const uint32_t *__restri
                                                         const uint64_t *__restrict__ chunk_offsets,
                                                         const uint32_t *__restrict__ temp, uint32_t K,
                                                         uint64_t *__restrict__ offsets, uint32_t *__restrict__ cols,
-                                                        uint64_t n) {
+                                                        uint64_t n, const uint32_t *__restrict__ label_map,
+                                                        uint32_t map_lds) {
+    const LabelMap lmap = stage_label_map(label_map, map_lds);
     const uint32_t lane = threadIdx.x & 63, sub = lane & 7, gb = lane & ~7u;
     const uint64_t nch = (n + 7) / 8;
     const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) >> 3;
@@ -1352,7 +1382,7 @@ __global__ __launch_bounds__(256) void k_compact_chunks(const uint32_t *__restri
 #pragma unroll
                 for (uint32_t k = 0; k < 8; ++k) {
                     const uint32_t i = i0 + sub + 8 * k;
-                    v[k] = i < stored ? gld(src + i) : 0u;
+                    v[k] = i < stored ? lmap(gld(src + i)) : 0u;
                 }
 #pragma unroll
                 for (uint32_t k = 0; k < 8; ++k) {
@@ -1367,7 +1397,7 @@ __global__ __launch_bounds__(256) void k_compact_chunks(const uint32_t *__restri
 #pragma unroll
             for (uint32_t k = 0; k < 8; ++k) {
                 const uint32_t i = i0 + sub + 8 * k;
-                v[k] = i < stored ? gld(src + i) : 0u;
+                v[k] = i < stored ? lmap(gld(src + i)) : 0u;
             }
 #pragma unroll
             for (uint32_t k = 0; k < 8; ++k) {
@@ -1389,8 +1419,10 @@ __global__ __launch_bounds__(256) void k_compact_chunks(const uint32_t *__restri
 
 __global__ __launch_bounds__(kCompactTile) void k_compact(const uint64_t *__restrict__ offsets,
                                                           const uint32_t *__restrict__ temp, uint32_t K,
-                                                          uint32_t *__restrict__ cols, uint64_t n) {
+                                                          uint32_t *__restrict__ cols, uint64_t n,
+                                                          const uint32_t *__restrict__ label_map, uint32_t map_lds) {
     __shared__ uint64_t soff[kCompactTile + 1];
+    const LabelMap lmap = stage_label_map(label_map, map_lds);
     const uint32_t t = threadIdx.x;
     for (uint64_t tile = blockIdx.x; tile * kCompactTile < n; tile += gridDim.x) {
         const uint64_t r0 = tile * kCompactTile;
@@ -1406,7 +1438,7 @@ __global__ __launch_bounds__(kCompactTile) void k_compact(const uint64_t *__rest
                 else hi = mid;
             }
             const uint64_t c = soff[lo + 1] - soff[lo];
-            if (c <= K) gst(cols + q, gld(temp + (r0 + lo) * K + (q - soff[lo])));
+            if (c <= K) gst(cols + q, lmap(gld(temp + (r0 + lo) * K + (q - soff[lo]))));
         }
         __syncthreads();
     }
@@ -1629,6 +1661,12 @@ hipError_t launch(const Ctx &c, const Trav &t, uint64_t n, hipStream_t s, const 
     return hipGetLastError();
 }
 
+// label-map entries the compaction kernels stage in LDS (0: identity or too large)
+uint32_t label_map_lds(const Ctx &c) {
+    const size_t m = c.tree.label_perm.size();
+    return (c.d_label_map && m <= kMapLdsMax) ? (uint32_t)m : 0u;
+}
+
 uint32_t auto_slots(const Ctx &c) {
     if (c.slot_labels) return c.slot_labels;
     const double mean = c.tree.num_rows ? (double)c.tree.num_relations / (double)c.tree.num_rows : 0.0;
@@ -1645,6 +1683,7 @@ TravParams base_params(const Ctx &c) {
     p.folded = c.tree.folded ? 1u : 0u;
     p.num_rows = c.tree.num_rows;
     p.scalars = reinterpret_cast<unsigned long long *>(c.d_scalars);
+    p.label_map = c.d_label_map;
     return p;
 }
 
@@ -1775,8 +1814,9 @@ static int run_get_rows_p2w(Ctx &c, P2wFn kfn, const uint64_t *d_rows, uint64_t 
         return MBRWT_ERR_CAPACITY;
     }
     const uint64_t g = std::min<uint64_t>((nb + 15) / 16, 8192);
-    hipLaunchKernelGGL(k_compact_blocks, dim3((unsigned)g), dim3(256), 0, s, d_counts, d_block_offsets, p.temp, C,
-                       d_offsets, d_cols, n);
+    const uint32_t map_lds = label_map_lds(c);
+    hipLaunchKernelGGL(k_compact_blocks, dim3((unsigned)g), dim3(256), map_lds * 4, s, d_counts, d_block_offsets, p.temp,
+                       C, d_offsets, d_cols, n, (const uint32_t *)c.d_label_map, map_lds);
     MBRWT_HIP(hipGetLastError());
     if (ovf) {
         TravParams q = base_params(c);
@@ -1873,14 +1913,15 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
         return MBRWT_ERR_CAPACITY;
     }
     {
+        const uint32_t map_lds = label_map_lds(c);
         if (fn.fast) {  // chunk-packed output (k_traverse_fast2)
             const uint64_t g = std::min<uint64_t>(((n + 7) / 8 + 31) / 32, 8192);
-            hipLaunchKernelGGL(k_compact_chunks, dim3((unsigned)g), dim3(256), 0, s, d_counts, d_chunk_offsets, p.temp,
-                               K, d_offsets, d_cols, n);
+            hipLaunchKernelGGL(k_compact_chunks, dim3((unsigned)g), dim3(256), map_lds * 4, s, d_counts, d_chunk_offsets, p.temp,
+                               K, d_offsets, d_cols, n, (const uint32_t *)c.d_label_map, map_lds);
         } else {
             const uint64_t g = std::min<uint64_t>((n + kCompactTile - 1) / kCompactTile, 16384);
-            hipLaunchKernelGGL(k_compact, dim3((unsigned)g), dim3(kCompactTile), 0, s, d_offsets, p.temp, K, d_cols,
-                               n);
+            hipLaunchKernelGGL(k_compact, dim3((unsigned)g), dim3(kCompactTile), map_lds * 4, s, d_offsets, p.temp, K,
+                               d_cols, n, (const uint32_t *)c.d_label_map, map_lds);
         }
         MBRWT_HIP(hipGetLastError());
     }

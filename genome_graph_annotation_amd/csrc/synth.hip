@@ -623,14 +623,48 @@ MaskFn mask_fn(uint32_t a) {
     return a <= kSynthMaxArity ? t[a] : nullptr;
 }
 
+// a given tree shape (mbrwt_shape_desc) -> ShapeNode list; empty + error on a malformed one
+std::vector<ShapeNode> shape_from_desc(const mbrwt_shape_desc &sd, uint64_t m) {
+    const uint32_t N = sd.num_nodes;
+    std::vector<ShapeNode> sh(N);
+    if (!N || !sd.num_children || !sd.first_child || !sd.leaf_column) return {};
+    std::vector<uint8_t> seen(N, 0), col_seen(m, 0);
+    uint64_t leaves = 0;
+    for (uint32_t u = 0; u < N; ++u) {
+        const uint32_t a = sd.num_children[u];
+        if (a == 0) {
+            const uint32_t col = sd.leaf_column[u];
+            if (col >= m || col_seen[col]++) return {};
+            sh[u].column = col;
+            ++leaves;
+            continue;
+        }
+        if (a > kSynthMaxArity || sd.first_child[u] <= u || (uint64_t)sd.first_child[u] + a > N) return {};
+        for (uint32_t c = 0; c < a; ++c) {
+            if (seen[sd.first_child[u] + c]++) return {};
+            sh[u].children.push_back(sd.first_child[u] + c);
+        }
+    }
+    if (leaves != m) return {};
+    for (uint32_t u = N; u-- > 0;) {
+        if (sh[u].children.empty()) {
+            sh[u].cols = 1;
+            continue;
+        }
+        for (uint32_t c : sh[u].children) sh[u].cols += sh[c].cols;
+    }
+    return sh;
+}
+
 }  // namespace
 
-int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStream_t s) {
+int build_synthetic(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape_desc, int device, Tree &tree,
+                    hipStream_t s) {
     MBRWT_HIP(hipSetDevice(device));
     tree = Tree();
     const uint64_t n = desc.num_rows, m = desc.num_columns;
     const double d = desc.density;
-    if (desc.arity < 2 || desc.arity > kSynthMaxArity || !(d >= 0.0 && d <= 1.0)) {
+    if ((!shape_desc && (desc.arity < 2 || desc.arity > kSynthMaxArity)) || !(d >= 0.0 && d <= 1.0)) {
         set_error("synthetic: arity must be in [2,12] and density in [0,1]");
         return MBRWT_ERR_INVALID;
     }
@@ -644,7 +678,11 @@ int build_synthetic(const mbrwt_synth_desc &desc, int device, Tree &tree, hipStr
         tree.num_rows = 0;
         return finalize_tree(tree);
     }
-    const auto shape = basic_shape(m, desc.arity);
+    const auto shape = shape_desc ? shape_from_desc(*shape_desc, m) : basic_shape(m, desc.arity);
+    if (shape.empty()) {
+        set_error("synthetic: malformed shape (BFS order, arity <= 12, leaves = num_columns, distinct columns)");
+        return MBRWT_ERR_INVALID;
+    }
     const uint32_t N = (uint32_t)shape.size();
     tree.num_nodes = N;
     std::vector<double> q(N);

@@ -99,6 +99,24 @@ typedef struct mbrwt_synth_desc {
 int mbrwt_create_synthetic(const mbrwt_synth_desc *desc, int device, mbrwt_ctx **out);
 
 /*
+ * The same law over ANY tree shape (e.g. the shape of a greedy + relaxed tree,
+ * the reference's production build path: transform_anno --greedy then
+ * relax_brwt): BFS arrays as in mbrwt_tree_desc (children contiguous,
+ * leaf_column = the leaf's global column, UINT32_MAX for internal nodes),
+ * node arity <= 12; desc->arity is ignored and desc->num_columns must equal
+ * the number of leaves.  q(u) = 1 - (1-density)^(leaves below u); node keys
+ * are BFS ids.
+ */
+typedef struct mbrwt_shape_desc {
+    uint32_t num_nodes;
+    const uint32_t *num_children;
+    const uint32_t *first_child;
+    const uint32_t *leaf_column;
+} mbrwt_shape_desc;
+int mbrwt_create_synthetic_shaped(const mbrwt_synth_desc *desc, const mbrwt_shape_desc *shape, int device,
+                                  mbrwt_ctx **out);
+
+/*
  * Build a BRWT from its columns on the device: BRWTBottomUpBuilder::build
  * (BRWT_builders.cpp:119-163) with the basic partitioner of the given arity
  * (get_basic_partitioner, BRWT_builders.cpp:20-31; groups of one pass

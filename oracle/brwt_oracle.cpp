@@ -691,7 +691,30 @@ struct MaskSampler {
 struct ShapeNode {
     std::vector<int> children;  // indices into shape vector
     uint64_t cols = 0;          // leaves below
+    uint32_t column = UINT32_MAX;  // leaves: the global column
 };
+
+// a tree shape in BFS numbering from arrays (mbrwt_shape_desc's layout);
+// cols by a reverse BFS sweep.  Empty on a malformed shape.
+std::vector<ShapeNode> shape_from_arrays(uint32_t N, const uint32_t *nc, const uint32_t *fc, const uint32_t *lc) {
+    std::vector<ShapeNode> sh(N);
+    for (uint32_t u = 0; u < N; ++u) {
+        if (nc[u] == 0) {
+            sh[u].column = lc[u];
+            continue;
+        }
+        if (fc[u] <= u || (uint64_t)fc[u] + nc[u] > N) return {};
+        for (uint32_t c = 0; c < nc[u]; ++c) sh[u].children.push_back((int)(fc[u] + c));
+    }
+    for (uint32_t u = N; u-- > 0;) {
+        if (sh[u].children.empty()) {
+            sh[u].cols = 1;
+            continue;
+        }
+        for (int c : sh[u].children) sh[u].cols += sh[c].cols;
+    }
+    return sh;
+}
 
 // Shape of BRWTBottomUpBuilder::build with the basic arity-k partitioner,
 // including the pass-through of single-element groups (BRWT_builders.cpp:74-76).
@@ -700,7 +723,7 @@ std::vector<ShapeNode> basic_shape(uint64_t m, uint32_t arity) {
     std::vector<ShapeNode> all;
     std::vector<int> cur;
     for (uint64_t i = 0; i < m; ++i) {
-        all.push_back(ShapeNode{{}, 1});
+        all.push_back(ShapeNode{{}, 1, (uint32_t)i});
         cur.push_back((int)i);
     }
     while (cur.size() > 1) {
@@ -745,13 +768,23 @@ int resolve_threads(int t) {
 #endif
 }
 
+std::unique_ptr<Node> generate_topdown_shape(uint64_t n, const std::vector<ShapeNode> &shape, double d, uint64_t seed,
+                                             int threads);
+
 std::unique_ptr<Node> generate_topdown(uint64_t n, uint64_t m, double d, uint32_t arity, uint64_t seed, int threads) {
     if (m == 0) {
         auto r = std::make_unique<Node>();
         r->nonzero_rows.finalize();
         return r;
     }
-    auto shape = basic_shape(m, arity);
+    return generate_topdown_shape(n, basic_shape(m, arity), d, seed, threads);
+}
+
+// the same law over any shape: node keys are BFS ids, the
+// root's partition lists global columns (pre-order leaves per child), every
+// other node's partition is consecutive ranges (BRWT_builders.cpp:68-107)
+std::unique_ptr<Node> generate_topdown_shape(uint64_t n, const std::vector<ShapeNode> &shape, double d, uint64_t seed,
+                                             int threads) {
     const size_t N = shape.size();
     std::vector<double> q(N);
     for (size_t u = 0; u < N; ++u) q[u] = 1.0 - std::pow(1.0 - d, (double)shape[u].cols);
@@ -806,8 +839,16 @@ std::unique_ptr<Node> generate_topdown(uint64_t n, uint64_t m, double d, uint32_
         }
         for (size_t c = 0; c < a; ++c) nodes[sh.children[c]]->nonzero_rows.finalize();
     }
-    // assemble the BRWT objects: basic partitioner arrangement is the
-    // identity at the root and consecutive ranges below (BRWT_builders.cpp:84-91)
+    // assemble the BRWT objects: global columns at the root (pre-order leaves
+    // of each child), consecutive ranges below (BRWT_builders.cpp:84-91)
+    std::vector<std::vector<uint64_t>> leaves(N);
+    for (size_t uu = N; uu-- > 0;) {
+        if (shape[uu].children.empty()) {
+            leaves[uu] = {shape[uu].column};
+            continue;
+        }
+        for (int c : shape[uu].children) leaves[uu].insert(leaves[uu].end(), leaves[c].begin(), leaves[c].end());
+    }
     for (size_t uu = N; uu-- > 0;) {
         auto &sh = shape[uu];
         Node &nd = *nodes[uu];
@@ -817,6 +858,7 @@ std::unique_ptr<Node> generate_topdown(uint64_t n, uint64_t m, double d, uint32_
         }
         std::vector<uint64_t> arr(sh.cols);
         std::iota(arr.begin(), arr.end(), 0);
+        if (uu == 0) arr = leaves[0];
         std::vector<size_t> gs;
         for (int c : sh.children) gs.push_back(shape[c].cols);
         nd.assignments = RangePartition(arr, gs);
@@ -981,20 +1023,36 @@ struct TopdownQuery {
 
 // Returns 0, or 2 on an out-of-range row.  Output: the reference's order
 // (pre-order of the leaves = ascending columns for the basic partitioner).
+int topdown_query_shape(uint64_t n, const std::vector<ShapeNode> &shape, double d, uint64_t seed,
+                        const uint64_t *rows, uint64_t nq, int threads, std::vector<uint64_t> &offsets,
+                        std::vector<uint32_t> &cols, uint64_t *draws);
+
 int topdown_query(uint64_t n, uint64_t m, double d, uint32_t arity, uint64_t seed, const uint64_t *rows,
                   uint64_t nq, int threads, std::vector<uint64_t> &offsets, std::vector<uint32_t> &cols,
                   uint64_t *draws) {
+    if (m == 0) {
+        for (uint64_t i = 0; i < nq; ++i)
+            if (rows[i] >= n) return 2;
+        offsets.assign(nq + 1, 0);
+        cols.clear();
+        return 0;
+    }
+    return topdown_query_shape(n, basic_shape(m, arity), d, seed, rows, nq, threads, offsets, cols, draws);
+}
+
+int topdown_query_shape(uint64_t n, const std::vector<ShapeNode> &shape, double d, uint64_t seed,
+                        const uint64_t *rows, uint64_t nq, int threads, std::vector<uint64_t> &offsets,
+                        std::vector<uint32_t> &cols, uint64_t *draws) {
     for (uint64_t i = 0; i < nq; ++i)
         if (rows[i] >= n) return 2;
     offsets.assign(nq + 1, 0);
     cols.clear();
-    if (m == 0 || nq == 0) return 0;
-    auto shape = basic_shape(m, arity);
+    if (shape.empty() || nq == 0) return 0;
     std::vector<double> q(shape.size());
     for (size_t u = 0; u < shape.size(); ++u) q[u] = 1.0 - std::pow(1.0 - d, (double)shape[u].cols);
-    // leaf columns: the basic partitioner keeps the leaves in column order, so
-    // a leaf's column is its pre-order rank among the leaves (RangePartition::get
-    // composed along the path, utils.cpp:689-691)
+    // leaves are emitted by their pre-order rank (sorted per row = the
+    // reference's output order, BRWT.cpp:45-51) and mapped to their global
+    // columns at the end (RangePartition::get composed, utils.cpp:689-691)
     std::vector<uint32_t> leaf_col(shape.size(), UINT32_MAX);
     {
         uint32_t next = 0;
@@ -1074,6 +1132,13 @@ int topdown_query(uint64_t n, uint64_t m, double d, uint32_t arity, uint64_t see
     const int64_t nn = (int64_t)nq;
 #pragma omp parallel for num_threads(threads) schedule(dynamic, 1024)
     for (int64_t r = 0; r < nn; ++r) std::sort(cols.begin() + offsets[r], cols.begin() + offsets[r + 1]);
+    // pre-order rank -> the leaf's global column
+    std::vector<uint32_t> col_of(leaf_col.size());
+    for (size_t u = 0; u < shape.size(); ++u)
+        if (shape[u].children.empty()) col_of[leaf_col[u]] = shape[u].column;
+    const int64_t nc = (int64_t)cols.size();
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (int64_t i = 0; i < nc; ++i) cols[i] = col_of[cols[i]];
     if (draws) *draws = tq.draws;
     return 0;
 }
@@ -1373,6 +1438,32 @@ struct OracleCSR {
     std::vector<uint32_t> cols;
     uint64_t draws = 0;
 };
+
+OracleCSR *oracle_topdown_get_rows_shaped(uint64_t n, uint32_t num_nodes, const uint32_t *nc, const uint32_t *fc,
+                                          const uint32_t *lc, double d, uint64_t seed, const uint64_t *rows, uint64_t nq,
+                                          int threads, int *status) {
+    auto shape = shape_from_arrays(num_nodes, nc, fc, lc);
+    if (shape.empty()) {
+        *status = 1;
+        return nullptr;
+    }
+    auto r = new OracleCSR();
+    *status = topdown_query_shape(n, shape, d, seed, rows, nq, threads, r->offsets, r->cols, &r->draws);
+    if (*status != 0) {
+        delete r;
+        return nullptr;
+    }
+    return r;
+}
+
+OracleTree *oracle_generate_topdown_shaped(uint64_t n, uint32_t num_nodes, const uint32_t *nc, const uint32_t *fc,
+                                           const uint32_t *lc, double d, uint64_t seed, int threads) {
+    auto shape = shape_from_arrays(num_nodes, nc, fc, lc);
+    if (shape.empty()) return nullptr;
+    auto t = new OracleTree();
+    t->root = generate_topdown_shape(n, shape, d, seed, resolve_threads(threads));
+    return t;
+}
 
 OracleCSR *oracle_topdown_get_rows(uint64_t n, uint64_t m, double d, uint32_t arity, uint64_t seed,
                                    const uint64_t *rows, uint64_t nq, int threads, int *status) {

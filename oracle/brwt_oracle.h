@@ -62,6 +62,17 @@ typedef struct OracleCSR OracleCSR;
 OracleCSR *oracle_topdown_get_rows(uint64_t num_rows, uint64_t num_cols, double density,
                                    uint32_t arity, uint64_t seed, const uint64_t *rows,
                                    uint64_t n, int num_threads, int *status);
+/* The same two entry points over ANY tree shape (BFS arrays as
+ * mbrwt_shape_desc: num_children, first_child, leaf_column): the law of a BRWT
+ * of that shape over i.i.d. Bernoulli(density) columns (q(u) = 1 - (1-d)^cols(u)),
+ * node keys = BFS ids.  NULL / *status = 1 on a malformed shape. */
+OracleCSR *oracle_topdown_get_rows_shaped(uint64_t num_rows, uint32_t num_nodes, const uint32_t *num_children,
+                                          const uint32_t *first_child, const uint32_t *leaf_column, double density,
+                                          uint64_t seed, const uint64_t *rows, uint64_t n, int num_threads,
+                                          int *status);
+OracleTree *oracle_generate_topdown_shaped(uint64_t num_rows, uint32_t num_nodes, const uint32_t *num_children,
+                                           const uint32_t *first_child, const uint32_t *leaf_column, double density,
+                                           uint64_t seed, int num_threads);
 uint64_t oracle_csr_num_labels(const OracleCSR *r);
 uint64_t oracle_csr_draws(const OracleCSR *r);  /* mask draws streamed */
 void oracle_csr_copy(const OracleCSR *r, uint64_t *offsets /* n+1 */, uint32_t *cols);

@@ -88,6 +88,10 @@ def lib():
         "oracle_csr_copy": (None, [vp, u64p, u32p]),
         "oracle_csr_free": (None, [vp]),
         "oracle_to_rrr": (None, [vp, C.c_int]),
+        "oracle_topdown_get_rows_shaped": (vp, [C.c_uint64, C.c_uint32, u32p, u32p, u32p, C.c_double, C.c_uint64,
+                                                u64p, C.c_uint64, C.c_int, C.POINTER(C.c_int)]),
+        "oracle_generate_topdown_shaped": (vp, [C.c_uint64, C.c_uint32, u32p, u32p, u32p, C.c_double, C.c_uint64,
+                                                C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -181,6 +185,13 @@ class OracleTree:
     @classmethod
     def topdown(cls, n, m, d, arity=8, seed=42, threads=0):
         return cls(lib().oracle_generate_topdown(n, m, d, arity, seed, threads))
+
+    @classmethod
+    def topdown_shaped(cls, n, shape, d, seed=42, threads=0):
+        """The top-down law over a given shape (dict with num_children,
+        first_child, leaf_column in BFS order, e.g. another tree's export)."""
+        nc, fc, lc = _shape_arrays(shape)
+        return cls(lib().oracle_generate_topdown_shaped(n, len(nc), _p32(nc), _p32(fc), _p32(lc), d, seed, threads))
 
     # -- BinaryMatrix surface -------------------------------------------------
     def num_rows(self):
@@ -297,6 +308,39 @@ def generate_columns(n, m, d, seed=42):
 
 def synth_hash(seed, key, pos):
     return lib().oracle_synth_hash(seed, key, pos)
+
+
+def _shape_arrays(shape):
+    return (np.ascontiguousarray(shape["num_children"], dtype=np.uint32),
+            np.ascontiguousarray(shape["first_child"], dtype=np.uint32),
+            np.ascontiguousarray(shape["leaf_column"], dtype=np.uint32))
+
+
+def _csr_out(h, n):
+    try:
+        nl = lib().oracle_csr_num_labels(h)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        cols = np.zeros(max(1, nl), dtype=np.uint32)
+        lib().oracle_csr_copy(h, _p64(off), _p32(cols))
+        draws = lib().oracle_csr_draws(h)
+    finally:
+        lib().oracle_csr_free(h)
+    return off, cols[:nl], draws
+
+
+def topdown_get_rows_shaped(n, shape, d, seed, rows, threads=0):
+    """topdown_get_rows over a given shape (see OracleTree.topdown_shaped)."""
+    rows = np.ascontiguousarray(rows, dtype=np.uint64)
+    nc, fc, lc = _shape_arrays(shape)
+    st = C.c_int(0)
+    h = lib().oracle_topdown_get_rows_shaped(n, len(nc), _p32(nc), _p32(fc), _p32(lc), d, seed, _p64(rows),
+                                             len(rows), threads, C.byref(st))
+    if st.value == 2:
+        raise IndexError("row out of range")
+    if st.value:
+        raise ValueError("malformed shape")
+    off, cols, _ = _csr_out(h, len(rows))
+    return off, cols
 
 
 def topdown_get_rows(n, m, d, arity, seed, rows, threads=0, with_draws=False):

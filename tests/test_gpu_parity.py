@@ -829,3 +829,31 @@ def test_get_rows_null_cols_is_a_sizing_call():
                                 offsets.ctypes.data_as(C.POINTER(C.c_uint64)), None, 1 << 20, C.byref(need))
     assert st == L.MBRWT_ERR_CAPACITY
     assert need.value == len(cols_h) > 0
+
+
+# ---- the production tree shape: greedy + relax (scripts/kingsford/convert.sh:24) ----
+
+@pytest.mark.parametrize("relax,n_rows", [(10, 2_000_000), (0, 500_000), (12, 1_000_000)])
+def test_synthetic_over_greedy_relaxed_shapes(oracle_mod, relax, n_rows):
+    """mbrwt_create_synthetic_shaped over the shape of a greedy (+ relaxed)
+    tree (binary_grouping_greedy, partitionings.cpp:148-201; relax,
+    BRWT_builders.cpp:166-211): leaves labelled by pre-order index, mapped to
+    their columns in the CSR writers.  Every kernel variant vs the oracle's
+    independent implementation of the same law, and the exported image vs the
+    oracle's tree."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    rng = np.random.default_rng(relax + 1)
+    dense = rng.random((4000, 300)) < 0.01
+    shape = O.OracleTree.from_dense(dense, "greedy", 2, relax).export()
+    dev = BRWTDevice.synthetic_shaped(n_rows, shape, 0.003, 7)
+    t = O.OracleTree.topdown_shaped(n_rows, shape, 0.003, 7)
+    assert dev.num_relations() == t.num_relations() and dev.num_columns() == 300
+    rows = rng.integers(0, n_rows, 100_000).astype(np.uint64)
+    _check_rows(t, dev, rows)
+    off_s, cols_s = O.topdown_get_rows_shaped(n_rows, shape, 0.003, 7, rows)
+    off_d, cols_d = dev.get_rows(rows)
+    np.testing.assert_array_equal(off_d, off_s)
+    np.testing.assert_array_equal(cols_d, cols_s)
+    for j in (0, 17, 299):
+        np.testing.assert_array_equal(dev.get_column(j), np.asarray(t.get_column(j), dtype=np.uint64))

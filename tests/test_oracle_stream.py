@@ -57,3 +57,29 @@ def test_rrr_layout_answers_like_plain(oracle_mod, n, m, d, arity):
     o2, c2, v2 = t.get_rows(rows, with_visits=True)
     assert np.array_equal(o1, o2) and np.array_equal(c1, c2) and np.array_equal(v1, v2)
     assert g1 == [t.get(r, c) for r, c in pts]
+
+
+@pytest.mark.parametrize("part,arity,relax", [("greedy", 2, 10), ("greedy", 2, 0), ("basic", 3, 0)])
+def test_shaped_stream_matches_shaped_tree(oracle_mod, part, arity, relax):
+    """The top-down law over an arbitrary shape (a greedy + relaxed tree's, the
+    reference's production build path): streamed query == materialised tree."""
+    O = oracle_mod
+    rng = np.random.default_rng(arity + relax)
+    dense = rng.random((3000, 70)) < 0.02
+    shape = O.OracleTree.from_dense(dense, part, arity, relax).export()
+    N = 1_000_000
+    t = O.OracleTree.topdown_shaped(N, shape, 0.01, 42)
+    rows = rng.integers(0, N, 20000).astype(np.uint64)
+    o1, c1 = t.get_rows(rows)
+    o2, c2 = O.topdown_get_rows_shaped(N, shape, 0.01, 42, rows)
+    assert np.array_equal(o1, o2) and np.array_equal(c1, c2)
+    assert t.num_columns() == 70
+
+
+def test_shaped_law_on_the_basic_shape_is_the_basic_law(oracle_mod):
+    O = oracle_mod
+    t = O.OracleTree.topdown(100000, 2652, 0.003, 8, 42)
+    t2 = O.OracleTree.topdown_shaped(100000, t.export(), 0.003, 42)
+    rows = np.random.default_rng(5).integers(0, 100000, 20000).astype(np.uint64)
+    a, b = t.get_rows(rows), t2.get_rows(rows)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
