@@ -351,6 +351,77 @@ int decode_pack2(const Tree &t, uint32_t v, std::vector<Bits> &cols) {
     return MBRWT_OK;
 }
 
+// KIND_PACKT node: the columns of every node below it, from the DFS records
+// (mbrwt_internal.hpp): visiting internal node x at its position jx with
+// children bits m sets bit jx of each set child's column; an internal child
+// is then visited at its own next position (positions ascend with j)
+int decode_packt(const Tree &t, uint32_t v, std::vector<Bits> &cols) {
+    const DevNode &dn = t.nodes[v];
+    const uint32_t S = dn.stride;
+    const uint64_t L = dn.length, blocks = (L + S - 1) / S;
+    std::vector<uint8_t> img, spill;
+    int rc;
+    if ((rc = copy_down(dn.base, blocks * kPack2Block, img))) return rc;
+    std::vector<uint64_t> next(t.nodes.size(), 0);  // next position of each internal node
+    std::vector<uint32_t> inner{v};
+    for (size_t h = 0; h < inner.size(); ++h) {
+        const DevNode &x = t.nodes[inner[h]];
+        for (uint32_t c = 0; c < x.arity; ++c) {
+            cols[x.first_child + c] = Bits(x.length);
+            if (t.nodes[x.first_child + c].kind != KIND_LEAF) inner.push_back(x.first_child + c);
+        }
+    }
+    struct Frame {
+        uint32_t x;
+        uint64_t jx;
+        uint32_t rem;
+    };
+    std::vector<Frame> st;
+    for (uint64_t b = 0; b < blocks; ++b) {
+        const uint8_t *blk = &img[b * kPack2Block];
+        const uint8_t *rec = blk;
+        std::vector<uint32_t> start(S + 1);
+        const uint32_t npos = (uint32_t)std::min<uint64_t>(S, L - b * S);
+        if (blk[0] == 0) {  // spilled: u16 start[S+1], then the records
+            uint64_t addr = 0;
+            std::memcpy(&addr, blk + 8, 8);
+            std::vector<uint8_t> hdr;
+            if ((rc = copy_down(addr, 2ull * (S + 1), hdr))) return rc;
+            for (uint32_t k = 0; k <= S; ++k) start[k] = hdr[2 * k] | ((uint32_t)hdr[2 * k + 1] << 8);
+            if ((rc = copy_down(addr, start[S], spill))) return rc;
+            rec = spill.data();
+        } else {
+            for (uint32_t k = 0; k < S; ++k) start[k] = blk[k];
+        }
+        for (uint32_t k = 0; k < npos; ++k) {
+            uint32_t o = start[k] + 1;  // (the record's label count)
+            auto mask = [&](uint32_t x) {
+                uint32_t m = rec[o++];
+                if (packt_mask_bytes(t.nodes[x].arity) == 2) m |= (uint32_t)rec[o++] << 8;
+                return m;
+            };
+            ++next[v];
+            st.assign(1, Frame{v, b * S + k, mask(v)});
+            while (!st.empty()) {
+                Frame &f = st.back();
+                if (!f.rem) {
+                    st.pop_back();
+                    continue;
+                }
+                const uint32_t c = (uint32_t)__builtin_ctz(f.rem);
+                f.rem &= f.rem - 1;
+                const uint32_t w = t.nodes[f.x].first_child + c;
+                cols[w].set(f.jx);
+                if (t.nodes[w].kind == KIND_LEAF) continue;
+                const uint64_t jw = next[w]++;
+                const uint32_t mw = mask(w);
+                st.push_back(Frame{w, jw, mw});
+            }
+        }
+    }
+    return MBRWT_OK;
+}
+
 int export_tree(const Ctx &c, mbrwt_tree &out) {
     const Tree &t = c.tree;
     out.num_rows = t.num_rows;
@@ -386,7 +457,9 @@ int export_tree(const Ctx &c, mbrwt_tree &out) {
     for (uint32_t v = 1; v < D; ++v) {
         const DevNode &dn = t.nodes[v];
         if (dn.kind == KIND_LEAF || dn.kind == KIND_FOLDED || dn.base == 0) continue;  // no image of its own
-        if (dn.kind == KIND_PACK2) {
+        if (dn.kind == KIND_PACKT) {
+            if ((rc = decode_packt(t, v, cols))) return rc;
+        } else if (dn.kind == KIND_PACK2) {
             if ((rc = decode_pack2(t, v, cols))) return rc;
         } else if (dn.kind == KIND_PACK) {
             if ((rc = decode_pack(t, v, cols))) return rc;

@@ -44,6 +44,10 @@ static int upload_tables(Ctx &c) {
         MBRWT_HIP(hipMalloc(&c.d_p2w, t.p2w_table.size() * 4));
         MBRWT_HIP(hipMemcpy(c.d_p2w, t.p2w_table.data(), t.p2w_table.size() * 4, hipMemcpyHostToDevice));
     }
+    if (!t.ptw_table.empty()) {
+        MBRWT_HIP(hipMalloc(&c.d_ptw, t.ptw_table.size() * 4));
+        MBRWT_HIP(hipMemcpy(c.d_ptw, t.ptw_table.data(), t.ptw_table.size() * 4, hipMemcpyHostToDevice));
+    }
     if (!t.col_path.empty()) {
         MBRWT_HIP(hipMalloc(&c.d_col_path, t.col_path.size()));
         MBRWT_HIP(hipMemcpy(c.d_col_path, t.col_path.data(), t.col_path.size(), hipMemcpyHostToDevice));
@@ -70,6 +74,7 @@ static void release(Ctx *c) {
     if (c->d_nodes) (void)hipFree(c->d_nodes);
     if (c->d_cnodes) (void)hipFree(c->d_cnodes);
     if (c->d_p2w) (void)hipFree(c->d_p2w);
+    if (c->d_ptw) (void)hipFree(c->d_ptw);
     if (c->d_label_map) (void)hipFree(c->d_label_map);
     if (c->d_col_path) (void)hipFree(c->d_col_path);
     if (c->d_col_leaf) (void)hipFree(c->d_col_leaf);
@@ -546,7 +551,7 @@ int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value) {
         c.slot_labels = (uint32_t)value;
         return MBRWT_OK;
     case MBRWT_OPT_KERNEL:
-        if (!(value >= 0 && value <= 6) && value != 10 && !(value >= 17 && value <= 23)) return MBRWT_ERR_INVALID;
+        if (!(value >= 0 && value <= 6) && value != 10 && !(value >= 17 && value <= 29)) return MBRWT_ERR_INVALID;
         c.kernel_variant = (int)value;
         return MBRWT_OK;
     default:

@@ -31,11 +31,30 @@ constexpr int kColThreads = 256;  // one thread = one 32-position word
 // leaf's positions lifted through the image-less MASK8 child at once); for a
 // KIND_PACK2 node, where child c, its child leaf >> 8 and that child's leaf
 // (leaf & 0xFF) are all set (two image-less levels lifted at once).
-__device__ __forceinline__ uint32_t column_word(const DevNode &nd, uint32_t c, uint64_t w, uint64_t len,
-                                                uint32_t leaf) {
+// For a KIND_PACKT node (dnode v) the word marks the positions whose record
+// holds the leaf with pre-order label `leaf`.
+__device__ __forceinline__ uint32_t column_word(const DevNode *nodes, uint32_t v, const DevNode &nd, uint32_t c,
+                                                uint64_t w, uint64_t len, uint32_t leaf) {
     if (32 * w >= len) return 0;
     uint32_t bits = 0;
-    if (nd.kind == KIND_PACK2) {  // leaf = (B << 8) | leaf slot of the MASK8 grandchild B below child c
+    if (nd.kind == KIND_PACKT) {
+        const uint32_t S = nd.stride;  // positions per block (any of 1..8)
+        Pack2Block pb;
+        uint64_t cur = ~0ull;
+        for (uint32_t h = 0; h < 32; ++h) {
+            const uint64_t j = 32 * w + h;
+            if (j >= len) break;
+            if (j / S != cur) {
+                cur = j / S;
+                pb.load(nd.base, (uint32_t)j, S);
+            }
+            uint32_t hit = 0;
+            (void)packt_walk(
+                nodes, v, [&](uint32_t o) { return pb.byte(o); }, pb.start((uint32_t)(j % S)),
+                [&](uint32_t label) { hit |= label == leaf; }, [](uint32_t) {});
+            bits |= hit << h;
+        }
+    } else if (nd.kind == KIND_PACK2) {  // leaf = (B << 8) | leaf slot of the MASK8 grandchild B below child c
         const uint32_t B = leaf >> 8, lf = leaf & 0xFFu;
         const uint32_t S = nd.stride;  // positions per block
         for (uint32_t h = 0; h < 32; h += S) {
@@ -91,23 +110,24 @@ __device__ __forceinline__ uint32_t column_word(const DevNode &nd, uint32_t c, u
     return bits;
 }
 
-__global__ __launch_bounds__(kColThreads) void k_col_count(DevNode nd, uint32_t c, uint32_t leaf, uint64_t len,
-                                                           uint64_t nwords, uint64_t *block_counts) {
+__global__ __launch_bounds__(kColThreads) void k_col_count(const DevNode *nodes, uint32_t v, DevNode nd, uint32_t c,
+                                                           uint32_t leaf, uint64_t len, uint64_t nwords,
+                                                           uint64_t *block_counts) {
     using Reduce = hipcub::BlockReduce<uint32_t, kColThreads>;
     __shared__ typename Reduce::TempStorage tmp;
     const uint64_t w = (uint64_t)blockIdx.x * kColThreads + threadIdx.x;
-    const uint32_t n = w < nwords ? (uint32_t)__builtin_popcount(column_word(nd, c, w, len, leaf)) : 0u;
+    const uint32_t n = w < nwords ? (uint32_t)__builtin_popcount(column_word(nodes, v, nd, c, w, len, leaf)) : 0u;
     const uint32_t total = Reduce(tmp).Sum(n);
     if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(kColThreads) void k_col_write(DevNode nd, uint32_t c, uint32_t leaf, uint64_t len,
-                                                           uint64_t nwords, const uint64_t *block_offsets,
-                                                           uint32_t *out) {
+__global__ __launch_bounds__(kColThreads) void k_col_write(const DevNode *nodes, uint32_t v, DevNode nd, uint32_t c,
+                                                           uint32_t leaf, uint64_t len, uint64_t nwords,
+                                                           const uint64_t *block_offsets, uint32_t *out) {
     using Scan = hipcub::BlockScan<uint32_t, kColThreads>;
     __shared__ typename Scan::TempStorage tmp;
     const uint64_t w = (uint64_t)blockIdx.x * kColThreads + threadIdx.x;
-    uint32_t bits = w < nwords ? column_word(nd, c, w, len, leaf) : 0u;
+    uint32_t bits = w < nwords ? column_word(nodes, v, nd, c, w, len, leaf) : 0u;
     uint32_t pre;
     Scan(tmp).ExclusiveSum((uint32_t)__builtin_popcount(bits), pre);
     uint64_t o = block_offsets[blockIdx.x] + pre;
@@ -175,7 +195,14 @@ int run_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap,
     // parent is a MASK8 child of a KIND_PACK node, out of the PACK image
     // (positions in the PACK node's space; the MASK8 level has no image)
     uint32_t leaf_bit = 0;
-    if (path.size() >= 3 && t.nodes[path[path.size() - 3].first].kind == KIND_PACK2) {
+    size_t pt = 0;
+    while (pt < path.size() && t.nodes[path[pt].first].kind != KIND_PACKT) ++pt;
+    if (pt < path.size()) {
+        // a KIND_PACKT ancestor: positions come out of its records (the
+        // levels below it have no image); leaf_bit = the leaf's pre-order label
+        leaf_bit = t.nodes[t.col_leaf[column]].label;
+        path.resize(pt + 1);
+    } else if (path.size() >= 3 && t.nodes[path[path.size() - 3].first].kind == KIND_PACK2) {
         // two image-less levels: positions come out of the PACK2 node's records
         leaf_bit = path.back().second;
         path.pop_back();
@@ -185,7 +212,8 @@ int run_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap,
         leaf_bit = path.back().second;
         path.pop_back();
     }
-    const DevNode leaf_parent = t.nodes[path.back().first];
+    const uint32_t leaf_parent_id = path.back().first;
+    const DevNode leaf_parent = t.nodes[leaf_parent_id];
     const uint32_t leaf_slot = path.back().second;
     const uint64_t len = leaf_parent.length;
     const uint64_t nwords = (len + 31) / 32;
@@ -200,7 +228,8 @@ int run_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap,
     uint64_t *d_cnt = reinterpret_cast<uint64_t *>(c.ws_counts.buf);
     uint64_t *d_off = d_cnt + nblk + 1;
     if (nwords) {
-        hipLaunchKernelGGL(k_col_count, dim3((unsigned)nblk), dim3(kColThreads), 0, s, leaf_parent, leaf_slot, leaf_bit,
+        hipLaunchKernelGGL(k_col_count, dim3((unsigned)nblk), dim3(kColThreads), 0, s, (const DevNode *)c.d_nodes,
+                           leaf_parent_id, leaf_parent, leaf_slot, leaf_bit,
                            len, nwords, d_cnt);
         MBRWT_HIP(hipGetLastError());
     } else {
@@ -220,7 +249,8 @@ int run_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap,
 
     if ((rc = ensure(c.ws_temp, total * sizeof(uint32_t)))) return rc;
     uint32_t *d_pos = reinterpret_cast<uint32_t *>(c.ws_temp.buf);
-    hipLaunchKernelGGL(k_col_write, dim3((unsigned)nblk), dim3(kColThreads), 0, s, leaf_parent, leaf_slot, leaf_bit,
+    hipLaunchKernelGGL(k_col_write, dim3((unsigned)nblk), dim3(kColThreads), 0, s, (const DevNode *)c.d_nodes,
+                       leaf_parent_id, leaf_parent, leaf_slot, leaf_bit,
                        len, nwords, d_off, d_pos);
     MBRWT_HIP(hipGetLastError());
     // lift through the ancestors: node path[k+1].first's column lives in the

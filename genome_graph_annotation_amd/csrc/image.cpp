@@ -234,6 +234,81 @@ std::vector<uint8_t> child_masks(const mbrwt_tree_desc &desc, uint32_t v, uint64
     return mk;
 }
 
+// The 64-byte record blocks of KIND_PACK2 / KIND_PACKT (mbrwt_internal.hpp)
+// from the records of positions 0..L-1 (recs, offsets roff[L+1]): the
+// largest span (8, 4, 2, 1 positions per block; any of 8..1 with any_span)
+// at which at most 1 block in 20 spills; false (nothing built) when no span qualifies.  Sets dn's
+// stride (span), length and base.
+bool upload_record_blocks(const std::vector<uint8_t> &recs, const std::vector<uint64_t> &roff, uint64_t L,
+                          DevNode &dn, std::vector<void *> &images, uint64_t &image_bytes, int &rc,
+                          bool any_span = false) {
+    rc = MBRWT_OK;
+    for (uint64_t j = 0; j < L; ++j)
+        if (roff[j + 1] - roff[j] > kPack2Block) return false;  // a record must fit a block (mbrwt_internal.hpp)
+    auto block_bytes = [&](uint64_t b, uint32_t S) {
+        return roff[std::min<uint64_t>(L, (b + 1) * S)] - roff[std::min<uint64_t>(L, b * S)];
+    };
+    uint32_t S = 0;
+    uint64_t blocks = 0;
+    for (uint32_t span = kPack2MaxSpan; span >= 1 && !S; span = any_span ? span - 1 : span / 2) {
+        const uint64_t nb = (L + span - 1) / span;
+        uint64_t spills = 0;
+        for (uint64_t b = 0; b < nb; ++b) spills += block_bytes(b, span) > pack2_inline(span);
+        if (spills * 20 <= nb) {
+            S = span;
+            blocks = nb;
+        }
+    }
+    if (!S) return false;
+    std::vector<uint8_t> host(blocks * kPack2Block + kImagePad, 0);
+    std::vector<uint8_t> spill;
+    std::vector<std::pair<uint64_t, uint64_t>> spilled;  // (block, offset in spill)
+    for (uint64_t b = 0; b < blocks; ++b) {
+        const uint64_t j0 = b * S, r0 = roff[std::min<uint64_t>(L, j0)];
+        const uint64_t bytes = block_bytes(b, S);
+        uint8_t *blk = &host[b * kPack2Block];
+        if (bytes <= pack2_inline(S)) {
+            for (uint32_t t = 0; t < S; ++t) blk[t] = (uint8_t)(S + roff[std::min<uint64_t>(L, j0 + t)] - r0);
+            std::memcpy(blk + S, recs.data() + r0, bytes);
+        } else {  // start[0] = 0 marks the block; list = u16 start[S+1], then the records
+            spilled.emplace_back(b, spill.size());
+            for (uint32_t t = 0; t <= S; ++t) {
+                const uint16_t st = (uint16_t)(2 * (S + 1) + roff[std::min<uint64_t>(L, j0 + t)] - r0);
+                spill.push_back((uint8_t)st);
+                spill.push_back((uint8_t)(st >> 8));
+            }
+            spill.insert(spill.end(), recs.begin() + r0, recs.begin() + r0 + bytes);
+            if (spill.size() & 1) spill.push_back(0);  // keep the u16 starts aligned
+        }
+    }
+    if (!spill.empty()) {
+        void *ds = nullptr;
+        spill.resize(spill.size() + kImagePad, 0);
+        if (hipMalloc(&ds, spill.size()) != hipSuccess || hipMemcpy(ds, spill.data(), spill.size(),
+                                                                      hipMemcpyHostToDevice) != hipSuccess) {
+            rc = hip_fail(hipErrorOutOfMemory, "record spill upload");
+            return true;
+        }
+        images.push_back(ds);
+        image_bytes += spill.size();
+        for (const auto &sb : spilled) {
+            const uint64_t addr = (uint64_t)(uintptr_t)ds + sb.second;
+            std::memcpy(&host[sb.first * kPack2Block + 8], &addr, 8);
+        }
+    }
+    void *d = nullptr;
+    if (upload_bytes(host.data(), host.size(), &d) != hipSuccess) {
+        rc = hip_fail(hipErrorOutOfMemory, "record image upload");
+        return true;
+    }
+    images.push_back(d);
+    image_bytes += host.size();
+    dn.stride = S;  // positions per block
+    dn.length = L;
+    dn.base = (uint64_t)(uintptr_t)d;
+    return true;
+}
+
 // KIND_PACK2 image of desc node u (mbrwt_internal.hpp) with the largest span
 // (8, 4, 2, 1 positions per block) at which at most 1 block in 20 spills;
 // returns false (and builds nothing) when no span qualifies.
@@ -282,74 +357,98 @@ bool build_pack2_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, DevN
         roff[j + 1] = recs.size();
     }
     timer.lap("pack2: masks + records");
-    for (uint64_t j = 0; j < L; ++j)
-        if (roff[j + 1] - roff[j] > kPack2Block) return false;  // a record must fit a block (mbrwt_internal.hpp)
-    auto block_bytes = [&](uint64_t b, uint32_t S) {
-        return roff[std::min<uint64_t>(L, (b + 1) * S)] - roff[std::min<uint64_t>(L, b * S)];
-    };
-    uint32_t S = 0;
-    uint64_t blocks = 0;
-    for (uint32_t span = kPack2MaxSpan; span >= 1 && !S; span /= 2) {
-        const uint64_t nb = (L + span - 1) / span;
-        uint64_t spills = 0;
-        for (uint64_t b = 0; b < nb; ++b) spills += block_bytes(b, span) > pack2_inline(span);
-        if (spills * 20 <= nb) {
-            S = span;
-            blocks = nb;
-        }
-    }
-    if (!S) return false;
-    timer.lap("pack2: span");
-    std::vector<uint8_t> host(blocks * kPack2Block + kImagePad, 0);
-    std::vector<uint8_t> spill;
-    std::vector<std::pair<uint64_t, uint64_t>> spilled;  // (block, offset in spill)
-    for (uint64_t b = 0; b < blocks; ++b) {
-        const uint64_t j0 = b * S, r0 = roff[std::min<uint64_t>(L, j0)];
-        const uint64_t bytes = block_bytes(b, S);
-        uint8_t *blk = &host[b * kPack2Block];
-        if (bytes <= pack2_inline(S)) {
-            for (uint32_t t = 0; t < S; ++t) blk[t] = (uint8_t)(S + roff[std::min<uint64_t>(L, j0 + t)] - r0);
-            std::memcpy(blk + S, recs.data() + r0, bytes);
-        } else {  // start[0] = 0 marks the block; list = u16 start[S+1], then the records
-            spilled.emplace_back(b, spill.size());
-            for (uint32_t t = 0; t <= S; ++t) {
-                const uint16_t st = (uint16_t)(2 * (S + 1) + roff[std::min<uint64_t>(L, j0 + t)] - r0);
-                spill.push_back((uint8_t)st);
-                spill.push_back((uint8_t)(st >> 8));
-            }
-            spill.insert(spill.end(), recs.begin() + r0, recs.begin() + r0 + bytes);
-            if (spill.size() & 1) spill.push_back(0);  // keep the u16 starts aligned
-        }
-    }
-    timer.lap("pack2: blocks");
-    if (!spill.empty()) {
-        void *ds = nullptr;
-        spill.resize(spill.size() + kImagePad, 0);
-        if (hipMalloc(&ds, spill.size()) != hipSuccess || hipMemcpy(ds, spill.data(), spill.size(),
-                                                                      hipMemcpyHostToDevice) != hipSuccess) {
-            rc = hip_fail(hipErrorOutOfMemory, "pack2 spill upload");
-            return true;
-        }
-        images.push_back(ds);
-        image_bytes += spill.size();
-        for (const auto &sb : spilled) {
-            const uint64_t addr = (uint64_t)(uintptr_t)ds + sb.second;
-            std::memcpy(&host[sb.first * kPack2Block + 8], &addr, 8);
-        }
-    }
-    void *d = nullptr;
-    if (upload_bytes(host.data(), host.size(), &d) != hipSuccess) {
-        rc = hip_fail(hipErrorOutOfMemory, "pack2 image upload");
-        return true;
-    }
-    timer.lap("pack2: upload");
-    images.push_back(d);
-    image_bytes += host.size();
+    if (!upload_record_blocks(recs, roff, L, dn, images, image_bytes, rc)) return false;
+    timer.lap("pack2: blocks + upload");
     dn.kind = KIND_PACK2;
     dn.arity = (uint16_t)a;
-    dn.stride = S;  // positions per block
-    dn.length = L;
-    dn.base = (uint64_t)(uintptr_t)d;
+    return true;
+}
+
+// children bits of desc node v (<= 16 children) at each of its len positions
+std::vector<uint16_t> child_masks16(const mbrwt_tree_desc &desc, uint32_t v, uint64_t len) {
+    std::vector<uint16_t> mk(len, 0);
+    const uint64_t W = (len + 63) / 64;
+    for (uint32_t k = 0; k < desc.num_children[v]; ++k) {
+        const uint64_t *cw = desc.vec_words[desc.first_child[v] + k];
+        for (uint64_t w = 0; w < W; ++w) {
+            uint64_t x = cw[w];
+            if (w == W - 1 && (len & 63)) x &= (1ull << (len & 63)) - 1;
+            for (; x; x &= x - 1) mk[w * 64 + (uint64_t)__builtin_ctzll(x)] |= (uint16_t)(1u << k);
+        }
+    }
+    return mk;
+}
+
+// height of desc node u's subtree (0 for a leaf), or UINT32_MAX past
+// kPacktMaxDepth / with an arity above kPacktMaxArity
+uint32_t packt_height(const mbrwt_tree_desc &desc, uint32_t u) {
+    const uint32_t a = desc.num_children[u];
+    if (a == 0) return 0;
+    if (a > kPacktMaxArity) return UINT32_MAX;
+    uint32_t h = 0;
+    for (uint32_t c = 0; c < a; ++c) {
+        const uint32_t hc = packt_height(desc, desc.first_child[u] + c);
+        if (hc == UINT32_MAX) return UINT32_MAX;
+        h = std::max(h, hc);
+    }
+    return h + 1 > kPacktMaxDepth ? UINT32_MAX : h + 1;
+}
+
+// KIND_PACKT image of desc node u (mbrwt_internal.hpp): the DFS records of
+// its whole subtree; false (nothing built) when a record exceeds 64 bytes or
+// no span keeps spills at <= 1 block in 20
+bool build_packt_image(const mbrwt_tree_desc &desc, uint32_t u, uint64_t L, const std::vector<uint64_t> &ones,
+                       DevNode &dn, std::vector<void *> &images, uint64_t &image_bytes, int &rc) {
+    rc = MBRWT_OK;
+    std::vector<uint32_t> inner{u};  // internal nodes of the subtree (BFS)
+    for (size_t h = 0; h < inner.size(); ++h)
+        for (uint32_t c = 0; c < desc.num_children[inner[h]]; ++c) {
+            const uint32_t w = desc.first_child[inner[h]] + c;
+            if (desc.num_children[w]) inner.push_back(w);
+        }
+    std::vector<std::vector<uint16_t>> masks(desc.num_nodes);
+    std::vector<uint64_t> cnt(desc.num_nodes, 0);
+    for (uint32_t v : inner) masks[v] = child_masks16(desc, v, ones[v]);
+    std::vector<uint8_t> recs;
+    recs.reserve(L * 8);
+    std::vector<uint64_t> roff(L + 1, 0);
+    auto put = [&](uint32_t v, uint32_t m) {
+        recs.push_back((uint8_t)m);
+        if (packt_mask_bytes(desc.num_children[v]) == 2) recs.push_back((uint8_t)(m >> 8));
+    };
+    std::vector<std::pair<uint32_t, uint32_t>> st;  // (node, children still to visit)
+    for (uint64_t j = 0; j < L; ++j) {
+        const uint32_t m = masks[u][j];
+        const size_t at = recs.size();
+        recs.push_back(0);  // the label count, set below
+        uint32_t labels = 0;
+        put(u, m);
+        st.assign(1, {u, m});
+        while (!st.empty()) {
+            auto &top = st.back();
+            if (!top.second) {
+                st.pop_back();
+                continue;
+            }
+            const uint32_t c = (uint32_t)__builtin_ctz(top.second);
+            top.second &= top.second - 1;
+            const uint32_t w = desc.first_child[top.first] + c;
+            if (!desc.num_children[w]) {
+                ++labels;
+                continue;
+            }
+            const uint32_t mw = masks[w][cnt[w]++];
+            put(w, mw);
+            st.push_back({w, mw});
+        }
+        if (labels > 255) return false;
+        recs[at] = (uint8_t)labels;
+        roff[j + 1] = recs.size();
+        if (roff[j + 1] - roff[j] > kPack2Block) return false;  // a record must fit a block
+    }
+    if (!upload_record_blocks(recs, roff, L, dn, images, image_bytes, rc, true)) return false;
+    dn.kind = KIND_PACKT;
+    dn.arity = (uint16_t)desc.num_children[u];
     return true;
 }
 
@@ -493,6 +592,76 @@ int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
         if (rc) return rc;
     }
     timer.lap("super-root");
+    // KIND_PACKT: every internal child of the folded root whose subtree fits
+    // (any shape), unless the tree is the PACK2 shape of k_traverse_p2w
+    std::vector<bool> in_packt(N, false);  // PACKT roots and the internal nodes below them
+    if (tree.folded && packt_enabled()) {
+        const uint32_t a0 = desc.num_children[0], fc0 = desc.first_child[0];
+        bool p2_shape = pack2_enabled();
+        for (uint32_t k = 0; k < a0; ++k)
+            if (!desc.num_children[fc0 + k] || !pack2_candidate(desc, fc0 + k)) p2_shape = false;
+        struct PT {
+            uint32_t u;
+            bool built = false;
+            int rc = MBRWT_OK;
+            DevNode dn{};
+            std::vector<void *> images;
+            uint64_t bytes = 0;
+        };
+        std::vector<PT> pt;
+        for (uint32_t k = 0; k < a0 && !p2_shape; ++k)
+            if (desc.num_children[fc0 + k] && packt_height(desc, fc0 + k) != UINT32_MAX) {
+                pt.emplace_back();
+                pt.back().u = fc0 + k;
+            }
+        std::vector<std::thread> pool;
+        for (size_t i = 0; i < pt.size(); ++i)
+            pool.emplace_back([&, i]() {
+                PT &r = pt[i];
+                if (hipSetDevice(device) != hipSuccess) {
+                    r.rc = MBRWT_ERR_DEVICE;
+                    return;
+                }
+                try {
+                    r.built = build_packt_image(desc, r.u, ones[r.u], ones, r.dn, r.images, r.bytes, r.rc);
+                } catch (...) {
+                    r.rc = MBRWT_ERR_NOMEM;
+                }
+            });
+        for (auto &t : pool) t.join();
+        for (const PT &r : pt) {
+            tree.images.insert(tree.images.end(), r.images.begin(), r.images.end());
+            tree.image_bytes += r.bytes;
+        }
+        for (const PT &r : pt) {
+            if (r.rc) return r.rc;
+            if (!r.built) continue;
+            DevNode &dn = tree.nodes[r.u + 1];
+            dn.kind = KIND_PACKT;
+            dn.arity = r.dn.arity;
+            dn.stride = r.dn.stride;
+            dn.length = r.dn.length;
+            dn.base = r.dn.base;
+            in_packt[r.u] = true;
+            std::vector<uint32_t> st{r.u};
+            while (!st.empty()) {
+                const uint32_t v = st.back();
+                st.pop_back();
+                for (uint32_t c = 0; c < desc.num_children[v]; ++c) {
+                    const uint32_t w = desc.first_child[v] + c;
+                    if (!desc.num_children[w]) continue;
+                    in_packt[w] = true;
+                    DevNode &wn = tree.nodes[w + 1];
+                    wn.kind = KIND_PACKT_IN;
+                    wn.arity = (uint16_t)desc.num_children[w];
+                    wn.length = ones[w];
+                    wn.base = 0;
+                    st.push_back(w);
+                }
+            }
+        }
+        timer.lap("packt images");
+    }
     // PACK2 candidates are disjoint subtrees (a candidate's descendants are
     // PACK/MASK8-shaped): their images are built concurrently, one host thread
     // per candidate (at most 16 at a time)
@@ -507,7 +676,7 @@ int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
     std::vector<P2> p2;
     if (pack2_enabled())
         for (uint32_t u = 0; u < N; ++u)
-            if (desc.num_children[u] && !(u == 0 && tree.folded) && pack2_candidate(desc, u)) {
+            if (desc.num_children[u] && !(u == 0 && tree.folded) && !in_packt[u] && pack2_candidate(desc, u)) {
                 p2.emplace_back();
                 p2.back().u = u;
             }
@@ -539,7 +708,7 @@ int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
     std::vector<bool> in_pack(N, false);  // MASK8 children of a KIND_PACK node: no image
     for (uint32_t u = 0; u < N; ++u) {
         const uint32_t a = desc.num_children[u];
-        if (!a || (u == 0 && tree.folded) || in_pack[u]) continue;
+        if (!a || (u == 0 && tree.folded) || in_pack[u] || in_packt[u]) continue;
         if (p2_of[u] >= 0) {
             const P2 &r = p2[p2_of[u]];
             if (r.built) {
@@ -664,9 +833,10 @@ int finalize_tree(Tree &tree) {
         }
         if (all) dn.flags |= FLAG_MASK_CHILDREN;
     }
-    tree.has_pack2 = tree.has_mask_children = false;
+    tree.has_pack2 = tree.has_mask_children = tree.has_packt = false;
     for (uint32_t v = 0; v < D; ++v) {
         tree.has_pack2 |= tree.nodes[v].kind == KIND_PACK2;
+        tree.has_packt |= tree.nodes[v].kind == KIND_PACKT;
         tree.has_mask_children |= tree.nodes[v].kind == KIND_PLANE && (tree.nodes[v].flags & FLAG_MASK_CHILDREN);
     }
     // shape eligible for the specialised kernel: internal nodes PLANE/MASK8 with
@@ -718,6 +888,7 @@ int finalize_tree(Tree &tree) {
         if (tree.nodes[v].kind != KIND_LEAF) tree.lds_records = v + 1;
     tree.lds_complete = tree.lds_records <= kLdsNodes;
     build_p2w_table(tree);
+    build_ptw_table(tree);
     tree.col_path.assign(tree.num_columns * tree.path_len, 0);
     tree.col_leaf.assign(tree.num_columns, 0);
     for (uint32_t v = 0; v < D; ++v) {
@@ -781,6 +952,78 @@ void build_p2w_table(Tree &tree) {
     for (uint32_t a = a_lo; a <= a_hi; ++a) t[4 + 4 * R + (a - a_lo)] = N[a].arity ? N[a].first_child - b_lo : 0;
     for (uint32_t b = b_lo; b <= b_hi; ++b) t[4 + 4 * R + nA + (b - b_lo)] = N[b].label;
     tree.p2w_table = std::move(t);
+}
+
+// The shape k_traverse_ptw takes: dnode 0 a PLANE node of arity <= 16 (the
+// folded root) whose children are leaves or KIND_PACKT nodes; labels and
+// local node indices below 2^15 (u16 entries).  Layout: mbrwt_internal.hpp.
+void build_ptw_table(Tree &tree) {
+    tree.ptw_table.clear();
+    const auto &N = tree.nodes;
+    if (N.empty() || N[0].kind != KIND_PLANE || N[0].arity == 0 || N[0].arity > 16) return;
+    const uint32_t R = N[0].arity;
+    std::vector<uint32_t> local(N.size(), UINT32_MAX), inner;
+    uint32_t height = 0;
+    for (uint32_t k = 0; k < R; ++k) {
+        const uint32_t u = N[0].first_child + k;
+        if (N[u].kind == KIND_LEAF) continue;
+        if (N[u].kind != KIND_PACKT || N[u].stride == 0 || N[u].stride > kPack2MaxSpan) return;
+        // the subtree's internal nodes, BFS
+        const size_t b = inner.size();
+        inner.push_back(u);
+        std::vector<uint32_t> lvl(1, 1);
+        for (size_t h = b; h < inner.size(); ++h) {
+            const DevNode &v = N[inner[h]];
+            height = std::max(height, lvl[h - b]);
+            for (uint32_t c = 0; c < v.arity; ++c)
+                if (N[v.first_child + c].kind != KIND_LEAF) {
+                    inner.push_back(v.first_child + c);
+                    lvl.push_back(lvl[h - b] + 1);
+                }
+        }
+    }
+    if (inner.size() >= 0x8000) return;
+    for (uint32_t i = 0; i < inner.size(); ++i) local[inner[i]] = i;
+    std::vector<uint32_t> nodew(inner.size());
+    std::vector<uint16_t> ent;
+    for (uint32_t i = 0; i < inner.size(); ++i) {
+        const DevNode &v = N[inner[i]];
+        if (ent.size() >= 0x10000 || v.arity > kPacktMaxArity) return;
+        nodew[i] = (uint32_t)ent.size() | ((uint32_t)v.arity << 24);
+        for (uint32_t c = 0; c < v.arity; ++c) {
+            const DevNode &w = N[v.first_child + c];
+            if (w.kind == KIND_LEAF) {
+                if (w.label >= 0x8000) return;
+                ent.push_back((uint16_t)(0x8000u | w.label));
+            } else {
+                ent.push_back((uint16_t)local[v.first_child + c]);
+            }
+        }
+    }
+    const uint32_t nI = (uint32_t)inner.size(), nE = (uint32_t)ent.size();
+    const size_t words = 4 + 4 * (size_t)R + nI + (nE + 1) / 2;
+    if (words > kPtwMaxWords) return;
+    std::vector<uint32_t> t(words, 0);
+    t[0] = R;
+    t[1] = nI;
+    t[2] = nE;
+    t[3] = height;
+    for (uint32_t k = 0; k < R; ++k) {
+        const uint32_t u = N[0].first_child + k;
+        const DevNode &d = N[u];
+        uint32_t *e = &t[4 + 4 * k];
+        if (d.kind == KIND_LEAF) {
+            e[3] = 0x80000000u | d.label;
+            continue;
+        }
+        e[0] = (uint32_t)d.base;
+        e[1] = (uint32_t)(d.base >> 32);
+        e[2] = d.stride;  // span
+        e[3] = local[u];
+    }
+    std::memcpy(&t[4 + 4 * R], nodew.data(), nI * 4);
+    std::memcpy(&t[4 + 4 * R + nI], ent.data(), nE * 2);
+    tree.ptw_table = std::move(t);
 }
 
 void free_tree(Tree &tree) {

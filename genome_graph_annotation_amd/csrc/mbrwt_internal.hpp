@@ -47,6 +47,8 @@ enum : uint8_t {
     KIND_FOLDED = 6,  // the BRWT root when folded into the super-root (never visited)
     KIND_PACK = 7,    // node whose children are all MASK8 nodes: children bits + their masks inline
     KIND_PACK2 = 8,   // node whose children are all PACK-shaped: the whole 3-level subtree inline
+    KIND_PACKT = 9,   // a root child whose whole subtree (any shape) is packed into per-position records
+    KIND_PACKT_IN = 10,  // internal node inside a KIND_PACKT subtree (record only, no image)
 };
 inline bool is_mask_kind(uint8_t k) { return k >= KIND_MASK8 && k <= KIND_MASK64; }
 
@@ -87,6 +89,25 @@ __host__ __device__ inline uint32_t pack_area_byte(uint32_t o) { return 16 * (o 
 constexpr uint32_t kPack2MaxSpan = 8;
 constexpr uint32_t kPack2Block = 64;
 __host__ __device__ inline uint32_t pack2_inline(uint32_t span) { return kPack2Block - span; }
+// KIND_PACKT image (node u, a child of the folded root, whose subtree has
+// height <= kPacktMaxDepth and arities <= kPacktMaxArity -- any partitioner's
+// shape, e.g. the greedy + relaxed trees of the reference's build scripts):
+// the blocks and spill lists of KIND_PACK2 with any span S in 1..8, and the
+// record of position j = its label count and the index bits of u's whole
+// subtree at j in DFS pre-order:
+//   count    the number of leaves set below u at j (<= 255; one byte),
+//   mask(v)  the children bits of internal node v at v's position (1 byte for
+//            arity <= 8, else 2 bytes little-endian), starting with v = u,
+//   then, for every set child of v in child order that is internal, its
+//   record part (recursively).
+// Leaves below u come out in the reference's pre-order (BRWT.cpp:45-51) --
+// ascending pre-order labels (the count lets a reader place an item's labels
+// before walking it).  Internal nodes below u are KIND_PACKT_IN:
+// records (arity, first child, length) without an image.  A record is at
+// most 64 bytes (the builders decline / fail loudly otherwise).
+constexpr uint32_t kPacktMaxDepth = 8;
+constexpr uint32_t kPacktMaxArity = 16;
+__host__ __device__ inline uint32_t packt_mask_bytes(uint32_t arity) { return arity <= 8 ? 1u : 2u; }
 // FLAG_CONSEC_LABELS (MASK nodes): child c's label = label + c.
 // FLAG_MASK_CHILDREN (PLANE nodes): every child is a KIND_MASK8 node with
 // consecutive labels, so the fast kernel resolves the children in the
@@ -124,6 +145,15 @@ constexpr uint32_t kLdsNodes = 512;
 //   nA x {index (into the B part) of A's first child B},
 //   nB x {label of B's child 0}      (B: KIND_MASK8, consecutive labels)
 constexpr uint32_t kP2wMaxWords = 1024;
+// PTW table (k_traverse_ptw: every child of the folded root a leaf or a
+// KIND_PACKT node): u32 words
+//   [0] R = arity of dnode 0, [1] nI, [2] nE, [3] max subtree height,
+//   R x {base lo, base hi, span, entry}   (entry: bit 31 = leaf, then
+//        its label in bits 0..30; else the PACKT node's local index)
+//   nI x {first entry [0:16) | arity [24:29)}   (the internal nodes of the
+//        PACKT subtrees, local indices)
+//   nE u16 child entries (bit 15 = leaf, label in bits 0..14; else the child's local index)
+constexpr uint32_t kPtwMaxWords = 8192;
 constexpr uint32_t kFastMaxDepth = 4;  // PLANE levels the specialised kernel's stack holds
 
 inline CNode compact(const DevNode &d) {
@@ -174,6 +204,8 @@ struct Tree {
     // k_traverse_p2w (the super-root's children all KIND_PACK2): the compact
     // table it stages in LDS (layout: query.hip "P2W table"), empty otherwise
     std::vector<uint32_t> p2w_table;
+    bool has_packt = false;                 // some node is KIND_PACKT (general kernels: lane kernel only)
+    std::vector<uint32_t> ptw_table;        // k_traverse_ptw's table (layout above), empty otherwise
     // Leaves are labelled by their PRE-ORDER index (the reference's output
     // order, BRWT.cpp:45-51), so the leaves below any node are consecutive
     // labels whatever the partitioner (greedy trees included); label_perm maps
@@ -231,6 +263,7 @@ struct Ctx {
     DevNode *d_nodes = nullptr;
     CNode *d_cnodes = nullptr;
     uint32_t *d_p2w = nullptr;          // Tree::p2w_table on the device
+    uint32_t *d_ptw = nullptr;          // Tree::ptw_table on the device
     uint32_t *d_label_map = nullptr;    // Tree::label_perm on the device (null = identity)
     uint8_t *d_col_path = nullptr;
     uint32_t *d_col_leaf = nullptr;
@@ -281,6 +314,8 @@ void free_tree(Tree &tree);
 int finalize_tree(Tree &tree);
 // the P2W table of k_traverse_p2w (empty when the tree has another shape)
 void build_p2w_table(Tree &tree);
+// the PTW table of k_traverse_ptw (empty when the tree has another shape)
+void build_ptw_table(Tree &tree);
 
 // root folding is on unless MBRWT_FOLD_ROOT=0 (A/B measurement switch)
 inline bool fold_root_enabled() {
@@ -295,6 +330,12 @@ inline bool pack_enabled() {
 // KIND_PACK2 nodes are built unless MBRWT_PACK2=0 or MBRWT_PACK=0
 inline bool pack2_enabled() {
     const char *e = std::getenv("MBRWT_PACK2");
+    return pack_enabled() && !(e && e[0] == '0');
+}
+
+// KIND_PACKT nodes are built unless MBRWT_PACKT=0 or MBRWT_PACK=0
+inline bool packt_enabled() {
+    const char *e = std::getenv("MBRWT_PACKT");
     return pack_enabled() && !(e && e[0] == '0');
 }
 

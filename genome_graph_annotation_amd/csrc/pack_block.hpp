@@ -82,3 +82,65 @@ struct Pack2Block {
 };
 
 }  // namespace mbrwt
+
+namespace mbrwt {
+
+// DFS walk of the KIND_PACKT record (mbrwt_internal.hpp) of dnode u starting
+// at byte o of `byte` (the record's bytes: count, then the masks): leaf(label) for every set leaf
+// below u in pre-order (BRWT.cpp:45-51), inner(arity) for every visited
+// internal node BELOW u.  Register shift-stack (static indices only).
+// Returns false when the subtree is deeper than kPacktMaxDepth.
+template <typename ByteFn, typename LeafFn, typename InnerFn>
+__device__ __forceinline__ bool packt_walk(const DevNode *__restrict__ nodes, uint32_t u, ByteFn byte, uint32_t o,
+                                           LeafFn leaf, InnerFn inner) {
+    constexpr int D = (int)kPacktMaxDepth - 1;
+    const DevNode nu = gld(nodes + u);
+    ++o;  // the record's label count
+    uint32_t top_m = byte(o++);
+    if (nu.arity > 8) top_m |= byte(o++) << 8;
+    uint32_t top_fc = nu.first_child;
+    uint32_t sfc[D], sm[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) sfc[k] = sm[k] = 0;
+    int sp = 0;
+    while (true) {
+        if (!top_m) {
+            if (sp == 0) break;
+            top_fc = sfc[0];
+            top_m = sm[0];
+#pragma unroll
+            for (int k = 0; k < D - 1; ++k) {
+                sfc[k] = sfc[k + 1];
+                sm[k] = sm[k + 1];
+            }
+            --sp;
+            continue;
+        }
+        const uint32_t c = (uint32_t)__builtin_ctz(top_m);
+        top_m &= top_m - 1;
+        const DevNode w = gld(nodes + top_fc + c);
+        if (w.kind == KIND_LEAF) {
+            leaf(w.label);
+            continue;
+        }
+        uint32_t mw = byte(o++);
+        if (w.arity > 8) mw |= byte(o++) << 8;
+        inner((uint32_t)w.arity);
+        if (top_m) {  // the parent still has children to visit
+            if (sp == D) return false;
+#pragma unroll
+            for (int k = D - 1; k > 0; --k) {
+                sfc[k] = sfc[k - 1];
+                sm[k] = sm[k - 1];
+            }
+            sfc[0] = top_fc;
+            sm[0] = top_m;
+            ++sp;
+        }
+        top_fc = w.first_child;
+        top_m = mw;
+    }
+    return true;
+}
+
+}  // namespace mbrwt

@@ -167,6 +167,18 @@ __device__ __forceinline__ void enter(const TravParams &p, Frames<MAXD, MaskT> &
     const uint32_t a = nd.arity;
     const uint64_t base = nd.base;
     if constexpr (MODE == MODE_WORK) sk.visits += a;  // operator[] on every child (BRWT.cpp:30)
+    if (kind == KIND_PACKT) {  // the whole subtree below v at j, DFS pre-order
+        Pack2Block pb;
+        pb.load(base, j, nd.stride);
+        const bool ok = packt_walk(
+            p.nodes, v, [&](uint32_t o) { return pb.byte(o); }, pb.start(j % nd.stride),
+            [&](uint32_t label) { sk.emit(p, label); },
+            [&](uint32_t ar) {
+                if constexpr (MODE == MODE_WORK) sk.visits += ar;
+            });
+        if (!ok) atomicOr(&p.scalars[2], 2ull);
+        return;
+    }
     if (kind == KIND_PACK2) {  // the whole subtree below v at j, in pre-order
         Pack2Block pb;
         pb.load(base, j, nd.stride);
@@ -1286,6 +1298,279 @@ __global__ __launch_bounds__(256, OCC) void k_traverse_p2w(P2wParams p) {
     }
 }
 
+// ------------------------------------------------------------------------
+// k_traverse_ptw: the traversal kernel for trees whose folded root's
+// children are leaves or KIND_PACKT nodes -- any partitioner's shape (the
+// greedy + relaxed trees of the reference's build scripts).  The rowblock
+// phases of k_traverse_p2w, with one LANE per item in the rounds:
+//   root phase -- group g reads the super-root's block at its row: up to 16
+//                 children (WIDE: a second 64-byte half), their bits and
+//                 positions (BRWT.cpp:30 + :43 for every child of the root);
+//   items      -- the set (row, child) pairs in (row, child) order; a leaf
+//                 child is an item of one label and no block;
+//   rounds     -- lane L resolves item 64r + L: the 4 lanes of a group read
+//                 the 64-byte KIND_PACKT blocks of the group's 4 items
+//                 together (16 bytes each, one request per block), staged in
+//                 LDS; the record's count byte places the item's labels (a
+//                 wave scan), then the lane walks the DFS record over the PTW
+//                 table in LDS and writes the labels -- in pre-order, the
+//                 reference's order -- into the wave's ring;
+//   flush      -- p2w's: 64-label units as full-line stores.
+// MAXD: stack levels of the walk (>= the PACKT subtrees' height); WPB: waves
+// per workgroup (the PTW table is staged once per workgroup).
+// ------------------------------------------------------------------------
+template <bool WIDE>
+struct PtwLayout {
+    static constexpr uint32_t kItems = WIDE ? 256 : 128;  // 16 rows x R children
+    static constexpr uint32_t kRing = 512;                // labels
+    // items j | items k | row counts | group's first item | blocks (64 x 64 B) | ring
+    static constexpr uint32_t kWords = kItems + kItems / 4 + 16 + 20 + 1024 + kRing;
+};
+
+// the labels of a KIND_PACKT record (masks from byte o on) into the ring
+// (or, `direct`, the rowblock's temp region) from label position pos on
+template <int MAXD>
+__device__ __forceinline__ void ptw_walk(const AS_LDS uint8_t *pb, uint32_t o, uint32_t node,
+                                         const AS_LDS uint32_t *ntab, const AS_LDS uint16_t *etab,
+                                         AS_LDS uint32_t *ring, uint32_t smask, uint32_t pos, bool direct,
+                                         uint32_t *out, uint32_t C, bool &overflow) {
+    uint32_t nw = ntab[node];
+    uint32_t m = pb[o++];
+    if ((nw >> 24) > 8) m |= (uint32_t)pb[o++] << 8;
+    uint32_t top = (nw & 0xFFFFu) | (m << 16);  // {first entry, children still to visit}
+    uint32_t st[MAXD - 1];
+#pragma unroll
+    for (int k = 0; k < MAXD - 1; ++k) st[k] = 0;
+    int sp = 0;
+    while (true) {
+        if ((top >> 16) == 0) {
+            if (sp == 0) break;
+            top = st[0];
+#pragma unroll
+            for (int k = 0; k < MAXD - 2; ++k) st[k] = st[k + 1];
+            --sp;
+            continue;
+        }
+        const uint32_t c = (uint32_t)__builtin_ctz(top >> 16);
+        top &= ~(0x10000u << c);
+        const uint32_t e = etab[(top & 0xFFFFu) + c];
+        if (e & 0x8000u) {
+            const uint32_t label = e & 0x7FFFu;
+            if (!direct) ring[pos & smask] = label;
+            else if (pos < C) gst(out + pos, label);
+            ++pos;
+            continue;
+        }
+        nw = ntab[e];
+        uint32_t mw = pb[o++];
+        if ((nw >> 24) > 8) mw |= (uint32_t)pb[o++] << 8;
+        if (top >> 16) {  // the parent still has children to visit
+            if (sp == MAXD - 1) {
+                overflow = true;
+                break;
+            }
+#pragma unroll
+            for (int k = MAXD - 2; k > 0; --k) st[k] = st[k - 1];
+            st[0] = top;
+            ++sp;
+        }
+        top = (nw & 0xFFFFu) | (mw << 16);
+    }
+}
+
+template <bool NT, bool WIDE, int MAXD, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_traverse_ptw(P2wParams p) {
+    using Lay = PtwLayout<WIDE>;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_ptw[];
+    const uint32_t lane = threadIdx.x & 63, c = lane & 3, g = lane >> 2, gb = lane & ~3u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_ptw[i] = gld(p.table + i);
+    __syncthreads();
+    const AS_LDS uint32_t *tab = (const AS_LDS uint32_t *)lds_ptw;
+    const uint32_t R = __builtin_amdgcn_readfirstlane(tab[0]), nI = __builtin_amdgcn_readfirstlane(tab[1]);
+    const AS_LDS uint32_t *roots = tab + 4;
+    const AS_LDS uint32_t *ntab = roots + 4 * R;
+    const AS_LDS uint16_t *etab = (const AS_LDS uint16_t *)(ntab + nI);
+    AS_LDS uint32_t *wbase = (AS_LDS uint32_t *)lds_ptw + ((p.table_words + 3) & ~3u) + wv * Lay::kWords;
+    AS_LDS uint32_t *items_j = wbase;                                    // item position j
+    AS_LDS uint8_t *items_k = (AS_LDS uint8_t *)(wbase + Lay::kItems);   // item child k
+    AS_LDS uint32_t *rowcnt = wbase + Lay::kItems + Lay::kItems / 4;      // [16] labels per row
+    AS_LDS uint32_t *gfirst = rowcnt + 16;                               // [17] group's first item; [16] = T
+    AS_LDS uint32_t *slots = gfirst + 20;                                // lane L's 64-byte block: [16 L, 16 L + 16)
+    AS_LDS uint32_t *ring = slots + 1024;                                // kRing labels
+    AS_LDS uint32_t *mine = slots + 16 * lane;
+    const AS_LDS uint8_t *pb = (const AS_LDS uint8_t *)mine;
+    constexpr uint32_t smask = Lay::kRing - 1;
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    bool overflow = false;
+
+    const uint64_t nblocks = (p.n + 15) / 16;
+    const uint64_t wstride = (uint64_t)gridDim.x * WPB;
+    for (uint64_t rb = (uint64_t)blockIdx.x * WPB + wv; rb < nblocks; rb += wstride) {
+        const uint64_t r0 = rb * 16;
+        const uint32_t nr = (uint32_t)(p.n - r0 < 16 ? p.n - r0 : 16);
+        uint32_t *const out = p.temp + rb * (uint64_t)p.C;
+
+        // ---- root phase: the super-root's block at group g's row ----
+        uint32_t row = kNone;
+        if (r0 + g < p.n) {
+            const uint64_t r = gld(p.rows + r0 + g);
+            if (r < p.num_rows) row = (uint32_t)r;
+            else if (c == 0) atomicOr(&p.scalars[2], 1ull);
+        }
+        uint4 qa = make_uint4(0, 0, 0, 0), qb = make_uint4(0, 0, 0, 0);
+        const uint64_t rblk = p.root_base + (uint64_t)(row >> 5) * p.root_stride;
+        if (row != kNone && 2 * c < R) qa = gld_at_nt<uint4, NT>(rblk + 16u * c);
+        if (WIDE && row != kNone && 8 + 2 * c < R) qb = gld_at_nt<uint4, NT>(rblk + 64u + 16u * c);
+        uint32_t P = 0, jj[4] = {0, 0, 0, 0};
+        if (row != kNone) {
+            const uint32_t t = row & 31, below = (1u << t) - 1u;
+            const uint32_t k0 = 2 * c;
+            const uint32_t b0 = k0 < R ? (qa.y >> t) & 1u : 0u, b1 = k0 + 1 < R ? (qa.w >> t) & 1u : 0u;
+            jj[0] = qa.x + (uint32_t)__builtin_popcount(qa.y & below);
+            jj[1] = qa.z + (uint32_t)__builtin_popcount(qa.w & below);
+            P = (b0 | (b1 << 1)) << k0;
+            if (WIDE) {
+                const uint32_t b2 = 8 + k0 < R ? (qb.y >> t) & 1u : 0u, b3 = 9 + k0 < R ? (qb.w >> t) & 1u : 0u;
+                jj[2] = qb.x + (uint32_t)__builtin_popcount(qb.y & below);
+                jj[3] = qb.z + (uint32_t)__builtin_popcount(qb.w & below);
+                P |= (b2 | (b3 << 1)) << (8 + k0);
+            }
+        }
+        P = quad_or(P);
+        // ---- items in (row, child) order ----
+        {
+            const uint32_t ng = (uint32_t)__builtin_popcount(P);
+            uint32_t pre = 0;
+#pragma unroll
+            for (uint32_t b = 0; b < (WIDE ? 5u : 4u); ++b) {
+                const uint64_t M = __ballot(c == 0 && ((ng >> b) & 1u));
+                pre += (uint32_t)__popcll(M & ((1ull << gb) - 1ull)) << b;
+            }
+#pragma unroll
+            for (uint32_t h = 0; h < (WIDE ? 4u : 2u); ++h) {
+                const uint32_t k = (h < 2 ? 0u : 8u) + 2 * c + (h & 1u);
+                if ((P >> k) & 1u) {
+                    const uint32_t idx = pre + (uint32_t)__builtin_popcount(P & ((1u << k) - 1u));
+                    items_j[idx] = jj[h];
+                    items_k[idx] = (uint8_t)k;
+                }
+            }
+            if (c == 0) {
+                gfirst[g] = pre;
+                rowcnt[g] = 0;
+            }
+            if (lane == 60) gfirst[16] = pre + ng;
+        }
+        wave_sync_lds();
+        const uint32_t T = __builtin_amdgcn_readfirstlane(gfirst[16]);
+
+        // ---- rounds: lane L resolves item ib + L ----
+        uint32_t running = 0, flushed = 0;
+        for (uint32_t ib = 0; ib < T; ib += 64) {
+            // the group's 4 blocks, quarter c each (all 4 requests in flight together)
+            uint4 q[4];
+#pragma unroll
+            for (uint32_t h = 0; h < 4; ++h) {
+                q[h] = make_uint4(0, 0, 0, 0);
+                const uint32_t ih = ib + 4 * g + h;
+                if (ih < T) {
+                    const uint32_t k = items_k[ih];
+                    if (!(roots[4 * k + 3] >> 31)) {
+                        const uint64_t ubase = (uint64_t)roots[4 * k] | ((uint64_t)roots[4 * k + 1] << 32);
+                        q[h] = gld_at_nt<uint4, NT>(ubase + (uint64_t)(items_j[ih] / roots[4 * k + 2]) * kPack2Block +
+                                                    16u * c);
+                    }
+                }
+            }
+#pragma unroll
+            for (uint32_t h = 0; h < 4; ++h)
+                ((AS_LDS u32x4_t *)(slots + 16 * (4 * g + h)))[c] = u32x4_t{q[h].x, q[h].y, q[h].z, q[h].w};
+            wave_sync_lds();
+            const uint32_t i = ib + lane;
+            const bool act = i < T;
+            uint32_t j = 0, k = 0;
+            if (act) {
+                j = items_j[i];
+                k = items_k[i];
+            }
+            const uint32_t ent = roots[4 * k + 3];
+            const bool blk = act && !(ent >> 31);
+            uint32_t s = 0;
+            if (blk) {
+                const uint32_t t = j % roots[4 * k + 2];
+                s = pb[t];
+                if (pb[0] == 0) {
+                    // spilled block: copy the position's record into the lane's
+                    // slot (list = u16 start[S+1], then the records; <= 64 bytes)
+                    const uint64_t la = ((uint64_t)mine[3] << 32) | mine[2];
+                    const uint32_t s0 = gld_at<uint16_t>(la + 2ull * t), len = gld_at<uint16_t>(la + 2ull * t + 2) - s0;
+                    AS_LDS uint8_t *pw = (AS_LDS uint8_t *)mine;
+                    for (uint32_t o = 0; o < len; o += 4) {
+                        uint8_t b4[4];
+#pragma unroll
+                        for (uint32_t e = 0; e < 4; ++e) b4[e] = o + e < len ? gld_at<uint8_t>(la + s0 + o + e) : 0;
+#pragma unroll
+                        for (uint32_t e = 0; e < 4; ++e)
+                            if (o + e < len) pw[o + e] = b4[e];
+                    }
+                    s = 0;
+                }
+            }
+            const uint32_t nl = blk ? (uint32_t)pb[s] : act ? 1u : 0u;  // the record's label count
+            // the item's first label: a wave scan of the counts (lanes are in item order)
+            uint32_t x = nl;
+#pragma unroll
+            for (uint32_t d = 1; d < 64; d <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+                if (lane >= d) x += y;
+            }
+            const uint32_t rtot = __builtin_amdgcn_readlane(x, 63);
+            const uint32_t ibase = running + x - nl;
+            if (act) {  // the item's row: the last group whose first item is <= i
+                uint32_t gr = 0;
+#pragma unroll
+                for (uint32_t q2 = 1; q2 < 16; ++q2) gr = gfirst[q2] <= i ? q2 : gr;
+                __hip_atomic_fetch_add((uint32_t *)(rowcnt + gr), nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            }
+            const bool direct = rtot + (running - flushed) > Lay::kRing;
+            if (direct) {
+                for (uint32_t q2 = flushed + lane; q2 < running; q2 += 64)
+                    if (q2 < p.C) gst(out + q2, (uint32_t)ring[q2 & smask]);
+                wave_sync_lds();
+            }
+            if (blk) ptw_walk<MAXD>(pb, s + 1, ent, ntab, etab, ring, smask, ibase, direct, out, p.C, overflow);
+            else if (act && !direct) ring[ibase & smask] = ent & 0x7FFFFFFFu;
+            else if (act && ibase < p.C) gst(out + ibase, ent & 0x7FFFFFFFu);
+            running += rtot;
+            if (direct) {
+                flushed = running;
+            } else {
+                const uint32_t F = running & ~63u;  // complete 64-label units
+                if (F > flushed) {
+                    wave_sync_lds();
+                    for (uint32_t q2 = flushed + lane; q2 < F; q2 += 64)
+                        if (q2 < p.C) gst(out + q2, (uint32_t)ring[q2 & smask]);
+                    flushed = F;
+                }
+            }
+            wave_sync_lds();  // the slots and the ring are reused
+        }
+        for (uint32_t q2 = flushed + lane; q2 < running; q2 += 64)
+            if (q2 < p.C) gst(out + q2, (uint32_t)ring[q2 & smask]);
+        if (lane < nr) gst(p.counts + r0 + lane, rowcnt[lane]);
+        if (lane == 0) gst(p.block_counts + rb, running);
+        if (running > p.C) {  // rowblock overflow: its rows go to the direct pass
+            unsigned long long k0 = 0;
+            if (lane == 0) k0 = atomicAdd(&p.scalars[1], (unsigned long long)nr);
+            k0 = (unsigned long long)__shfl((long long)k0, 0, 64);
+            if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(r0 + lane));
+        }
+        wave_sync_lds();
+    }
+    if (overflow) atomicOr(&p.scalars[2], 2ull);
+}
+
 // k_compact_blocks: output of k_traverse_p2w -> CSR.  16 lanes per 16-row
 // block (4 blocks per wave): the rows' offsets (block offset + in-block
 // prefix) and a contiguous copy of the block's labels, each lane's (up to 8)
@@ -1469,6 +1754,22 @@ __global__ __launch_bounds__(256) void k_get(const DevNode *__restrict__ nodes, 
             const DevNode *nd = &ndv;
             const uint32_t c = col_path[col * path_len + k];
             const uint64_t base = nd->base;
+            if (nd->kind == KIND_PACKT) {  // the column's leaf below v (pre-order label), then one record walk
+                uint32_t w = v;
+                for (uint32_t kk = k; kk < path_len; ++kk) {
+                    w = gld(nodes + w).first_child + col_path[col * path_len + kk];
+                    if (gld(nodes + w).kind == KIND_LEAF) break;
+                }
+                const uint32_t want = gld(nodes + w).label;
+                Pack2Block pb;
+                pb.load(base, j, nd->stride);
+                uint32_t hit = 0;
+                (void)packt_walk(
+                    nodes, v, [&](uint32_t o) { return pb.byte(o); }, pb.start(j % nd->stride),
+                    [&](uint32_t label) { hit |= label == want; }, [](uint32_t) {});
+                bit = (uint8_t)hit;
+                break;
+            }
             if (nd->kind == KIND_PACK2) {  // child c, its child c2, leaf c3: one record walk
                 Pack2Block pb;
                 pb.load(base, j, nd->stride);
@@ -1573,7 +1874,7 @@ Trav pick_traverse(const Ctx &c) {
         t.fn = reinterpret_cast<const void *>(t.lane_fn);
         return t;
     }
-    if (c.kernel_variant == 1) {  // lane-per-row kernel (kept for A/B measurement)
+    if (c.kernel_variant == 1 || c.tree.has_packt) {  // lane-per-row kernel (A/B; the general kernel of KIND_PACKT trees)
         const bool wide = max_arity > 32;
         t.name = "k_traverse";
 #define PICK(D)                                                                                      \
@@ -1728,7 +2029,37 @@ static size_t p2w_lds_bytes(const Ctx &c) {
     return ((c.tree.p2w_table.size() + 3) & ~size_t(3)) * 4 + 4 * (size_t)(kP2wWaveWords + p2w_ring(c)) * 4;
 }
 
+// k_traverse_ptw for this context?  Default for trees with a PTW table
+// (MBRWT_OPT_KERNEL 0 or 24..29): 24 plain reads, 25 non-temporal, 26/27 the
+// same with 8 waves per workgroup, 28/29 with 16.
+struct PtwPick {
+    P2wFn fn = nullptr;
+    uint32_t wpb = 4;
+    bool wide = false;
+};
+template <bool NT, bool WIDE, int MAXD>
+static P2wFn ptw_fn(uint32_t wpb) {
+    return wpb == 16 ? k_traverse_ptw<NT, WIDE, MAXD, 16> : wpb == 8 ? k_traverse_ptw<NT, WIDE, MAXD, 8>
+                                                                  : k_traverse_ptw<NT, WIDE, MAXD, 4>;
+}
+static PtwPick ptw_kernel(const Ctx &c) {
+    PtwPick r;
+    const int kv = c.kernel_variant;
+    const auto &t = c.tree.ptw_table;
+    if (t.empty() || !c.d_ptw || !(kv == 0 || (kv >= 24 && kv <= 29))) return r;
+    const bool nt = kv == 0 ? c.tree.image_bytes > (1ull << 30) : (kv & 1) != 0;
+    r.wpb = kv >= 28 ? 16 : kv >= 26 ? 8 : 4;
+    r.wide = t[0] > 8;
+    const bool deep = t[3] > 4;
+#define PTW(NTV, W, D) if (nt == NTV && r.wide == W && deep == D) r.fn = ptw_fn<NTV, W, D ? 8 : 4>(r.wpb);
+    PTW(false, false, false) PTW(false, false, true) PTW(false, true, false) PTW(false, true, true)
+    PTW(true, false, false) PTW(true, false, true) PTW(true, true, false) PTW(true, true, true)
+#undef PTW
+    return r;
+}
+
 const char *traverse_kernel_name(const Ctx &c) {
+    if (ptw_kernel(c).fn) return "k_traverse_ptw";
     if (p2w_kernel(c)) return "k_traverse_p2w";
     const Trav t = pick_traverse<MODE_SLOTS>(c);
     return t ? t.name : "";
@@ -1737,8 +2068,17 @@ const char *traverse_kernel_name(const Ctx &c) {
 // get_rows through k_traverse_p2w: rowblocks of 16 rows, each written to its
 // own temp region of C = 16 K labels; one scan over the rowblock totals; the
 // compaction; the direct pass for overflowing rowblocks.
-static int run_get_rows_p2w(Ctx &c, P2wFn kfn, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets,
-                            uint32_t *d_cols, uint64_t cap, uint64_t *needed, hipStream_t s) {
+// (k_traverse_ptw: the same driver over the PTW table, `wpb` waves per workgroup)
+struct RowblockKernel {
+    P2wFn fn;
+    const uint32_t *table;
+    uint32_t table_words;
+    size_t lds;
+    uint32_t wpb;
+};
+static int run_get_rows_p2w(Ctx &c, const RowblockKernel &kr, const uint64_t *d_rows, uint64_t n,
+                            uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap, uint64_t *needed, hipStream_t s) {
+    const P2wFn kfn = kr.fn;
     const uint32_t K = auto_slots(c);
     const uint32_t C = 16 * K;
     const Trav fn_direct = pick_traverse<MODE_DIRECT>(c);
@@ -1768,8 +2108,8 @@ static int run_get_rows_p2w(Ctx &c, P2wFn kfn, const uint64_t *d_rows, uint64_t 
     p.num_rows = c.tree.num_rows;
     p.root_base = root.base;
     p.root_stride = root.stride;
-    p.table_words = (uint32_t)c.tree.p2w_table.size();
-    p.table = c.d_p2w;
+    p.table_words = kr.table_words;
+    p.table = kr.table;
     p.C = C;
     p.S = p2w_ring(c);
     p.temp = reinterpret_cast<uint32_t *>(c.ws_temp.buf);
@@ -1778,19 +2118,24 @@ static int run_get_rows_p2w(Ctx &c, P2wFn kfn, const uint64_t *d_rows, uint64_t 
     p.ovf_list = reinterpret_cast<uint32_t *>(c.ws_ovf.buf);
     p.scalars = reinterpret_cast<unsigned long long *>(c.d_scalars);
 
-    const size_t lds = p2w_lds_bytes(c);
+    const size_t lds = kr.lds;
+    const uint32_t threads = 64 * kr.wpb;
+    if (lds > 65536)
+        MBRWT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds));
     int dev_cus = 0, per_cu = 0;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kfn), 256, lds) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kfn), threads, lds) !=
             hipSuccess ||
         per_cu <= 0)
-        per_cu = 4;
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((nb + 3) / 4, (uint64_t)std::max(1, dev_cus) * per_cu));
+        per_cu = 1;
+    const uint64_t grid = std::max<uint64_t>(
+        1, std::min<uint64_t>((nb + kr.wpb - 1) / kr.wpb, (uint64_t)std::max(1, dev_cus) * per_cu));
 
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
     MBRWT_HIP(hipMemsetAsync(d_block_counts + nb, 0, sizeof(uint32_t), s));
     if (c.timing) MBRWT_HIP(hipEventRecord(c.ev0, s));
-    hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(256), lds, s, p);
+    hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(threads), lds, s, p);
     MBRWT_HIP(hipGetLastError());
     if (c.timing) MBRWT_HIP(hipEventRecord(c.ev1, s));
     MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_block_offsets, nb + 1, s));
@@ -1807,6 +2152,10 @@ static int run_get_rows_p2w(Ctx &c, P2wFn kfn, const uint64_t *d_rows, uint64_t 
     if (err & 1) {
         set_error("row out of range");
         return MBRWT_ERR_RANGE;
+    }
+    if (err & 2) {
+        set_error("traversal stack overflow");
+        return MBRWT_ERR_UNSUPPORTED;
     }
     if (needed) *needed = total;
     if (total > cap) {
@@ -1847,7 +2196,17 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
         set_error("batch larger than 2^31 rows");
         return MBRWT_ERR_UNSUPPORTED;
     }
-    if (const P2wFn kfn = p2w_kernel(c)) return run_get_rows_p2w(c, kfn, d_rows, n, d_offsets, d_cols, cap, needed, s);
+    if (const PtwPick pk = ptw_kernel(c); pk.fn) {
+        const size_t words = c.tree.ptw_table.size();
+        const size_t per_wave = pk.wide ? PtwLayout<true>::kWords : PtwLayout<false>::kWords;
+        const RowblockKernel kr{pk.fn, c.d_ptw, (uint32_t)words, ((words + 3) & ~size_t(3)) * 4 + pk.wpb * per_wave * 4,
+                                pk.wpb};
+        return run_get_rows_p2w(c, kr, d_rows, n, d_offsets, d_cols, cap, needed, s);
+    }
+    if (const P2wFn kfn = p2w_kernel(c)) {
+        const RowblockKernel kr{kfn, c.d_p2w, (uint32_t)c.tree.p2w_table.size(), p2w_lds_bytes(c), 4};
+        return run_get_rows_p2w(c, kr, d_rows, n, d_offsets, d_cols, cap, needed, s);
+    }
     const uint32_t K = auto_slots(c);
     const Trav fn = pick_traverse<MODE_SLOTS>(c);
     const Trav fn_direct = pick_traverse<MODE_DIRECT>(c);

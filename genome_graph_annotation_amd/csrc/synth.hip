@@ -424,6 +424,137 @@ __global__ __launch_bounds__(256) void k_gen_pack2(uint8_t *img, uint64_t L, uin
     }
 }
 
+// KIND_PACKT image (mbrwt_internal.hpp) of a root child u from temporary
+// KIND_PLANE images of the internal nodes of u's subtree that have internal
+// children; the masks of all-leaf nodes are drawn at their positions (the
+// same draw (key, position) as their own MASK images would hold).  One
+// thread per block of S positions walks each position's DFS record; pass 0
+// sums the spill-list bytes and counts records over 64 bytes, pass 1 writes.
+struct GenNode {
+    uint64_t K;
+    const uint64_t *T;
+    const uint8_t *plane;  // temporary KIND_PLANE image, null = all children leaves (masks drawn)
+    uint32_t nT, stride, arity, child0;  // child0: index of child 0 in the child table
+};
+constexpr uint32_t kGenLeaf = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t gen_mask(const GenNode &v, uint64_t jv) {
+    if (!v.plane) return draw_mask(v.T, v.nT, draw(v.K, jv));
+    uint32_t m = 0, r;
+    for (uint32_t c = 0; c < v.arity; ++c) m |= plane_bit_rank(v.plane, v.stride, c, jv, r) << c;
+    return m;
+}
+
+// the DFS record of u (gen node 0) at position j: put(mask, arity) per
+// visited internal node in pre-order; false past kPacktMaxDepth levels
+template <typename Put>
+__device__ bool gen_packt_record(const GenNode *__restrict__ gn, const uint32_t *__restrict__ gch, uint64_t j, Put put,
+                                 uint64_t &leaves) {
+    uint32_t nd[kPacktMaxDepth], rem[kPacktMaxDepth];
+    uint64_t ps[kPacktMaxDepth];
+    const GenNode u = gn[0];
+    const uint32_t m = gen_mask(u, j);
+    put(m, u.arity);
+    nd[0] = 0;
+    ps[0] = j;
+    rem[0] = m;
+    int sp = 1;
+    while (sp) {
+        const int t = sp - 1;
+        if (!rem[t]) {
+            --sp;
+            continue;
+        }
+        const uint32_t c = (uint32_t)__builtin_ctz(rem[t]);
+        rem[t] &= rem[t] - 1;
+        const GenNode &v = gn[nd[t]];
+        const uint32_t ch = gch[v.child0 + c];
+        if (ch == kGenLeaf) {
+            ++leaves;
+            continue;
+        }
+        uint32_t jc;
+        (void)plane_bit_rank(v.plane, v.stride, c, ps[t], jc);
+        const GenNode w = gn[ch];
+        const uint32_t mw = gen_mask(w, jc);
+        put(mw, w.arity);
+        if (sp == (int)kPacktMaxDepth) return false;
+        nd[sp] = ch;
+        ps[sp] = jc;
+        rem[sp] = mw;
+        ++sp;
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_gen_packt(uint8_t *img, uint64_t L, uint32_t S, const GenNode *gn,
+                                                   const uint32_t *gch, uint8_t *spill,
+                                                   unsigned long long *spill_ctr, unsigned long long *ones, int pass) {
+    const uint64_t nb = (L + S - 1) / S;
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t local = 0;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gs) {
+        uint32_t size = 0;
+        bool big = false;
+        for (uint32_t t = 0; t < S; ++t) {
+            const uint64_t j = b * S + t;
+            if (j >= L) break;
+            uint32_t rs = 1;  // the label count
+            uint64_t labels = 0;
+            if (!gen_packt_record(gn, gch, j, [&](uint32_t, uint32_t a) { rs += packt_mask_bytes(a); }, labels))
+                big = true;
+            size += rs;
+            big |= rs > kPack2Block || labels > 255;
+        }
+        const bool spills = size > pack2_inline(S);
+        const uint32_t list_bytes = (2 * (S + 1) + size + 15) & ~15u;
+        if (pass == 0) {
+            if (spills) atomicAdd(spill_ctr, (unsigned long long)list_bytes);
+            if (big) atomicAdd(spill_ctr + 1, 1ull);
+            continue;
+        }
+        uint8_t *blk = img + b * kPack2Block;
+        uint8_t *dst;
+        uint32_t hdr;
+        if (spills) {
+            uint8_t *list = spill + atomicAdd(spill_ctr, (unsigned long long)list_bytes);
+            const uint64_t addr = (uint64_t)(uintptr_t)list;
+            for (uint32_t k = 0; k < 8; ++k) {
+                blk[k] = 0;
+                blk[8 + k] = (uint8_t)(addr >> (8 * k));
+            }
+            dst = list + 2 * (S + 1);
+            hdr = 2 * (S + 1);
+        } else {
+            dst = blk + S;
+            hdr = S;
+        }
+        uint32_t o = 0;
+        for (uint32_t t = 0; t < S; ++t) {
+            const uint64_t j = b * S + t;
+            if (spills) *reinterpret_cast<uint16_t *>(dst - 2 * (S + 1) + 2 * t) = (uint16_t)(hdr + o);
+            else blk[t] = (uint8_t)(hdr + o);
+            if (j >= L) continue;
+            const uint32_t at = o++;
+            uint64_t labels = 0;
+            (void)gen_packt_record(
+                gn, gch, j,
+                [&](uint32_t m, uint32_t a) {
+                    dst[o++] = (uint8_t)m;
+                    if (a > 8) dst[o++] = (uint8_t)(m >> 8);
+                },
+                labels);
+            dst[at] = (uint8_t)labels;
+            local += labels;
+        }
+        if (spills) *reinterpret_cast<uint16_t *>(dst - 2 * (S + 1) + 2 * S) = (uint16_t)(hdr + o);  // end
+    }
+    if (pass == 1) {
+        for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off);
+        if ((threadIdx.x & 63) == 0 && local) atomicAdd(ones, (unsigned long long)local);
+    }
+}
+
 // ---- per-child rank scan over the blocks of a KIND_PLANE image ----------
 constexpr int kScanTile = 256;  // blocks per tile (one thread per block)
 
@@ -658,6 +789,169 @@ std::vector<ShapeNode> shape_from_desc(const mbrwt_shape_desc &sd, uint64_t m) {
 
 }  // namespace
 
+// KIND_PACKT images of the folded root's internal children (mbrwt_internal.hpp),
+// unless every root child has the PACK2 shape (k_traverse_p2w).  A subtree
+// taller than kPacktMaxDepth, or one whose records would exceed 64 bytes,
+// stays for the per-node generation.  Children lengths of the root's
+// children come from the fold; the rest from the temporary planes' scans.
+static int synth_packt(const std::vector<ShapeNode> &shape, const std::vector<double> &q, const std::vector<uint64_t *> &node_T,
+                uint64_t seed, Tree &tree, std::vector<bool> &in_pack, unsigned long long *d_ctr,
+                unsigned long long *d_ones, hipStream_t s) {
+    const auto &root = shape[0].children;
+    auto internal = [&](uint32_t v) { return !shape[v].children.empty(); };
+    auto p2_struct = [&](uint32_t u) {
+        if (!internal(u) || shape[u].children.size() > 8 || !pack2_enabled()) return false;
+        for (uint32_t a : shape[u].children) {
+            if (!internal(a) || shape[a].children.size() > 8) return false;
+            for (uint32_t b : shape[a].children) {
+                if (!internal(b) || shape[b].children.size() > 8) return false;
+                for (uint32_t l : shape[b].children)
+                    if (internal(l)) return false;
+            }
+        }
+        return true;
+    };
+    if (std::all_of(root.begin(), root.end(), p2_struct)) return MBRWT_OK;
+    int rc = MBRWT_OK;
+    for (uint32_t u : root) {
+        if (!internal(u) || !(q[u] > 0.0)) continue;
+        // the subtree's internal nodes (BFS), their depth and arity bounds
+        std::vector<uint32_t> inner{u}, lvl{1};
+        bool ok = true;
+        for (size_t h = 0; h < inner.size() && ok; ++h) {
+            const auto &sh = shape[inner[h]];
+            ok = sh.children.size() <= std::min<uint32_t>(kPacktMaxArity, kSynthMaxArity) && lvl[h] <= kPacktMaxDepth;
+            for (uint32_t c : sh.children)
+                if (internal(c)) {
+                    inner.push_back(c);
+                    lvl.push_back(lvl[h] + 1);
+                }
+        }
+        if (!ok) continue;
+        std::vector<uint32_t> loc(shape.size(), kGenLeaf);
+        for (uint32_t i = 0; i < inner.size(); ++i) loc[inner[i]] = i;
+        std::vector<GenNode> gn(inner.size());
+        std::vector<uint32_t> gch;
+        std::vector<void *> tmps;
+        auto free_tmps = [&]() {
+            for (void *t : tmps) (void)hipFree(t);
+            tmps.clear();
+        };
+        double rec = 0.0;
+        for (uint32_t i = 0; i < inner.size() && !rc; ++i) {
+            const uint32_t v = inner[i];
+            const auto &sh = shape[v];
+            const uint32_t a = (uint32_t)sh.children.size();
+            const DevNode &vd = tree.nodes[v + 1];
+            GenNode &g = gn[i];
+            g.K = node_key(seed, v);
+            g.T = node_T[v];
+            g.nT = (1u << a) - 1;
+            g.arity = a;
+            g.child0 = (uint32_t)gch.size();
+            g.plane = nullptr;
+            g.stride = 0;
+            rec += q[v] / q[u] * packt_mask_bytes(a);
+            bool all_leaves = true;
+            for (uint32_t c : sh.children) {
+                gch.push_back(loc[c]);
+                all_leaves &= !internal(c);
+            }
+            if (all_leaves) continue;
+            const uint32_t stride = plane_stride(a);
+            const uint64_t L = vd.length, bytes = ((L + 31) / 32) * stride + kImagePad;
+            void *t = nullptr;
+            if (hipMalloc(&t, bytes) != hipSuccess) {
+                rc = MBRWT_ERR_NOMEM;
+                break;
+            }
+            tmps.push_back(t);
+            (void)hipMemsetAsync(t, 0, bytes, s);
+            uint8_t *pl = reinterpret_cast<uint8_t *>(t);
+            plane_fn(a)(pl, L, g.K, g.T, g.nT, stride, s);
+            std::vector<uint64_t> tot;
+            if ((rc = plane_scan(pl, L, a, stride, tot, s))) break;
+            for (uint32_t c = 0; c < a; ++c)
+                if (internal(sh.children[c])) tree.nodes[sh.children[c] + 1].length = tot[c];
+            g.plane = pl;
+            g.stride = stride;
+        }
+        GenNode *d_gn = nullptr;
+        uint32_t *d_gch = nullptr;
+        if (!rc && (hipMalloc(&d_gn, gn.size() * sizeof(GenNode)) != hipSuccess ||
+                    hipMalloc(&d_gch, gch.size() * 4) != hipSuccess ||
+                    hipMemcpyAsync(d_gn, gn.data(), gn.size() * sizeof(GenNode), hipMemcpyHostToDevice, s) != hipSuccess ||
+                    hipMemcpyAsync(d_gch, gch.data(), gch.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess))
+            rc = MBRWT_ERR_NOMEM;
+        auto done = [&]() {
+            (void)hipStreamSynchronize(s);
+            free_tmps();
+            if (d_gn) (void)hipFree(d_gn);
+            if (d_gch) (void)hipFree(d_gch);
+        };
+        if (rc) {
+            done();
+            return rc;
+        }
+        DevNode &dn = tree.nodes[u + 1];
+        const uint64_t L = dn.length;
+        uint32_t S = 1;  // the largest span whose expected block (header + records with counts) fits
+        for (uint32_t span = kPack2MaxSpan; span >= 2; --span)
+            if (span * (rec + 2.0) <= 56.0) {
+                S = span;
+                break;
+            }
+        const uint64_t nb = (L + S - 1) / S;
+        (void)hipMemsetAsync(d_ctr, 0, 2 * sizeof(unsigned long long), s);
+        hipLaunchKernelGGL(k_gen_packt, dim3(launch_grid(nb)), dim3(256), 0, s, nullptr, L, S, d_gn, d_gch, nullptr,
+                           d_ctr, d_ones, 0);
+        unsigned long long ctr[2] = {0, 0};
+        if (hipGetLastError() != hipSuccess || hipMemcpyAsync(ctr, d_ctr, sizeof(ctr), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            done();
+            return MBRWT_ERR_DEVICE;
+        }
+        if (ctr[1]) {  // a record over 64 bytes: this subtree is generated node by node
+            done();
+            continue;
+        }
+        auto alloc = [&](uint64_t bytes) -> uint8_t * {
+            void *p = nullptr;
+            if (hipMalloc(&p, bytes + kImagePad) != hipSuccess) return nullptr;
+            (void)hipMemsetAsync(p, 0, bytes + kImagePad, s);
+            tree.images.push_back(p);
+            tree.image_bytes += bytes + kImagePad;
+            return reinterpret_cast<uint8_t *>(p);
+        };
+        uint8_t *spill = ctr[0] ? alloc(ctr[0]) : nullptr;
+        uint8_t *img = alloc(nb * kPack2Block);
+        if (!img || (ctr[0] && !spill)) {
+            done();
+            return MBRWT_ERR_NOMEM;
+        }
+        (void)hipMemsetAsync(d_ctr, 0, sizeof(unsigned long long), s);
+        hipLaunchKernelGGL(k_gen_packt, dim3(launch_grid(nb)), dim3(256), 0, s, img, L, S, d_gn, d_gch, spill, d_ctr,
+                           d_ones, 1);
+        if (hipGetLastError() != hipSuccess) {
+            done();
+            return MBRWT_ERR_DEVICE;
+        }
+        done();
+        dn.kind = KIND_PACKT;
+        dn.stride = S;
+        dn.base = (uint64_t)(uintptr_t)img;
+        for (uint32_t v : inner) {
+            in_pack[v] = true;
+            if (v == u) continue;
+            DevNode &vd = tree.nodes[v + 1];
+            vd.kind = KIND_PACKT_IN;
+            vd.base = 0;
+            vd.stride = 0;
+        }
+    }
+    return MBRWT_OK;
+}
+
 int build_synthetic(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape_desc, int device, Tree &tree,
                     hipStream_t s) {
     MBRWT_HIP(hipSetDevice(device));
@@ -833,9 +1127,15 @@ int build_synthetic(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape_
         }
     }
     // internal nodes in BFS order: parents are generated before children
-    std::vector<bool> in_pack(N, false);  // MASK8 children of a KIND_PACK node: no image
+    std::vector<bool> in_pack(N, false);  // MASK8 children of a KIND_PACK node, KIND_PACKT subtrees: no image
     unsigned long long *d_ctr = nullptr;
     if (hipMalloc(&d_ctr, 2 * sizeof(unsigned long long)) != hipSuccess) return fail(MBRWT_ERR_NOMEM, "hipMalloc");
+    if (tree.folded && packt_enabled()) {
+        if ((rc = synth_packt(shape, q, node_T, desc.seed, tree, in_pack, d_ctr, d_ones, s))) {
+            (void)hipFree(d_ctr);
+            return fail(rc, "synthetic: KIND_PACKT generation");
+        }
+    }
     for (uint32_t u = 0; u < N; ++u) {
         const auto &sh = shape[u];
         DevNode &dn = tree.nodes[u + 1];

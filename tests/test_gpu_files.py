@@ -29,7 +29,8 @@ def _env(name, value, fn):
             os.environ[name] = old
 
 
-@pytest.mark.parametrize("layout", [{}, {"MBRWT_PACK2": "0"}, {"MBRWT_PACK": "0"}, {"MBRWT_FOLD_ROOT": "0"}])
+@pytest.mark.parametrize("layout", [{}, {"MBRWT_PACK2": "0"}, {"MBRWT_PACK": "0"}, {"MBRWT_FOLD_ROOT": "0"},
+                                    {"MBRWT_PACKT": "0"}])
 def test_export_every_layout(oracle_mod, layout):
     """PLANE, MASK8..64, PACK (with spilled blocks), PACK2 (with spilled
     blocks), folded and unfolded roots: the exported description is the one
@@ -41,7 +42,8 @@ def test_export_every_layout(oracle_mod, layout):
     for n, m, d, part, arity, relax in [(4000, 256, 0.004, "basic", 4, 0), (4000, 64, 0.01, "basic", 8, 0),
                                         (3000, 2048, 0.04, "basic", 8, 0), (2000, 100, 0.05, "greedy", 2, 0),
                                         (2000, 300, 0.02, "basic", 2, 2**64 - 1), (1500, 40, 0.3, "basic", 12, 0),
-                                        (1000, 90, 0.02, "basic", 40, 0)]:
+                                        (1000, 90, 0.02, "basic", 40, 0), (3000, 200, 0.02, "greedy", 2, 10),
+                                        (2000, 65, 0.05, "basic", 8, 0), (2000, 256, 0.02, "basic", 16, 0)]:
         dense = rng.random((n, m)) < d
         dense[n // 2:n // 2 + 24] = True  # dense rows: spilled PACK / PACK2 blocks
         cases.append(O.OracleTree.from_dense(dense, part, arity, relax))
@@ -75,6 +77,19 @@ def test_export_synthetic_images(oracle_mod, n, m, d, arity):
     O = oracle_mod
     dev = BRWTDevice.synthetic(n, m, d, arity, 42)
     _same_tree(O.OracleTree.topdown(n, m, d, arity, 42).export(), dev.export())
+
+
+@pytest.mark.parametrize("relax", [10, 0])
+def test_export_synthetic_packt_images(oracle_mod, relax):
+    """KIND_PACKT images of the generator over a greedy (+ relaxed) shape
+    decode to the oracle's tree of the same law."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    dense = np.random.default_rng(relax).random((3000, 300)) < 0.01
+    shape = O.OracleTree.from_dense(dense, "greedy", 2, relax).export()
+    dev = BRWTDevice.synthetic_shaped(400_000, shape, 0.003, 5)
+    assert dev.traverse_kernel() == "k_traverse_ptw"
+    _same_tree(O.OracleTree.topdown_shaped(400_000, shape, 0.003, 5).export(), dev.export())
 
 
 def test_dump_and_load_answers_like_the_oracle(oracle_mod):

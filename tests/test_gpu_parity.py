@@ -20,7 +20,7 @@ def _dev(tree):
     return BRWTDevice.from_tree(tree.export())
 
 
-def _check_rows(oracle_tree, dev, rows, variants=(0, 1, 2, 4, 5, 10, 17, 18, 19, 20, 21, 22, 23)):
+def _check_rows(oracle_tree, dev, rows, variants=(0, 1, 2, 4, 5, 10, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29)):
     """Every traversal kernel (1 lane-per-row; 2/3/4 group-cooperative with
     1/2/4 children per lane; 0 the default) must
     reproduce the oracle's ordered CSR exactly."""
@@ -308,6 +308,12 @@ def _with_env(name, value, fn):
             os.environ[name] = old
 
 
+@pytest.fixture
+def no_packt(monkeypatch):
+    """The PACK / PACK2 layout tests measure those layouts: no KIND_PACKT."""
+    monkeypatch.setenv("MBRWT_PACKT", "0")
+
+
 def _agree(oracle_tree, devs, rows, cols, m):
     import torch
     off_o, cols_o, vis = oracle_tree.get_rows(rows, with_visits=True)
@@ -324,7 +330,7 @@ def _agree(oracle_tree, devs, rows, cols, m):
         np.testing.assert_array_equal(d.get_batch(ii, jj), want)
 
 
-def test_pack_layout_with_spills(oracle_mod):
+def test_pack_layout_with_spills(oracle_mod, no_packt):
     """A tree whose PACK node has a few blocks with > 48 masks (spill lists):
     packed and unpacked images answer like the oracle (rows, columns, get,
     V/L accounting)."""
@@ -342,7 +348,7 @@ def test_pack_layout_with_spills(oracle_mod):
 
 
 @pytest.mark.parametrize("fold", ["1", "0"])
-def test_pack_layout_synthetic(oracle_mod, fold):
+def test_pack_layout_synthetic(oracle_mod, no_packt, fold):
     """Synthetic Kingsford-shaped trees with and without PACK nodes (and with
     and without root folding) agree with the oracle."""
     from genome_graph_annotation_amd import BRWTDevice
@@ -361,7 +367,7 @@ def test_pack_layout_synthetic(oracle_mod, fold):
 
 # ---- KIND_PACK2 layout: a node's whole 3-level subtree inline per position ----
 
-def test_pack2_layout_with_spills(oracle_mod):
+def test_pack2_layout_with_spills(oracle_mod, no_packt):
     """Arity-4 tree (256 -> 64 -> 16 -> 4 -> root, folded): the 4 nodes under
     the root become KIND_PACK2; a run of dense rows makes a few of their
     blocks spill.  PACK2, PACK-only and plain images answer like the oracle
@@ -383,7 +389,7 @@ def test_pack2_layout_with_spills(oracle_mod):
     _agree(t, [p2, p1, plain], rows, range(m), m)
 
 
-def test_pack2_records_longer_than_a_block(oracle_mod):
+def test_pack2_records_longer_than_a_block(oracle_mod, no_packt):
     """Arity 8, 2048 columns (2048 -> 256 -> 32 -> 4 -> root): a fully set row
     gives a 73-byte record (1 + 8 + 64 masks), longer than a block: the host
     builder declines PACK2 for those nodes (mbrwt_internal.hpp) and the
@@ -401,7 +407,7 @@ def test_pack2_records_longer_than_a_block(oracle_mod):
 
 
 @pytest.mark.parametrize("fold", ["1", "0"])
-def test_pack2_layout_synthetic(oracle_mod, fold):
+def test_pack2_layout_synthetic(oracle_mod, no_packt, fold):
     """Synthetic Kingsford-shaped trees: the generator's PACK2 images (default)
     agree with the oracle, as do PACK-only images."""
     from genome_graph_annotation_amd import BRWTDevice
@@ -423,7 +429,7 @@ def test_pack2_layout_synthetic(oracle_mod, fold):
     _agree(t, [p2, p1], rows, np.random.default_rng(4).integers(0, m, 16), m)
 
 
-def test_pack2_dense_subtrees_take_a_short_span(oracle_mod):
+def test_pack2_dense_subtrees_take_a_short_span(oracle_mod, no_packt):
     """d = 4 %: ~26 record bytes per position, so the host builder picks a
     span of 2 or 1 positions per block (mbrwt_internal.hpp); results as the
     oracle's under every kernel."""
@@ -440,7 +446,7 @@ def test_pack2_dense_subtrees_take_a_short_span(oracle_mod):
     _agree(t, [p2, p1], rows, [0, 9, 100, 1023, 2047], m)
 
 
-def test_pack2_refseq_shape_synthetic(oracle_mod):
+def test_pack2_refseq_shape_synthetic(oracle_mod, no_packt):
     """RefSeq shape (3,173 columns, d = 3.8 %): the generator's span-2 PACK2
     images agree with the oracle's independent implementation of the spec."""
     from genome_graph_annotation_amd import BRWTDevice
@@ -857,3 +863,71 @@ def test_synthetic_over_greedy_relaxed_shapes(oracle_mod, relax, n_rows):
     np.testing.assert_array_equal(cols_d, cols_s)
     for j in (0, 17, 299):
         np.testing.assert_array_equal(dev.get_column(j), np.asarray(t.get_column(j), dtype=np.uint64))
+
+
+# ---- KIND_PACKT: any shape's root children packed to the leaves (k_traverse_ptw) ----
+
+@pytest.mark.parametrize("n,m,d,part,arity,relax", [
+    (6000, 200, 0.02, "greedy", 2, 10),           # the production shape (relax 10)
+    (6000, 200, 0.02, "greedy", 2, 0),            # binary greedy: subtrees of height 7 (8-level walks)
+    (4000, 300, 0.02, "greedy", 2, 2**64 - 1),    # unbounded relax
+    (4000, 65, 0.05, "basic", 8, 0),              # a root child that is a leaf (pass-through)
+    (4000, 1728, 0.002, "basic", 12, 0),          # 12 root children, arity-12 masks (2 bytes)
+    (3000, 256, 0.02, "basic", 16, 0),            # 16 root children of 16 leaves
+    (3000, 600, 0.01, "basic", 2, 0),             # a child of height 9 (no PACKT) beside one of height 7
+])
+def test_packt_layout(oracle_mod, n, m, d, part, arity, relax):
+    """KIND_PACKT images (mbrwt_internal.hpp) against the oracle and against
+    the same tree without them (MBRWT_PACKT=0): rows under every kernel
+    (k_traverse_ptw by default, the lane kernel for the rest), columns, get,
+    V/L accounting; a run of dense rows makes blocks spill."""
+    O = oracle_mod
+    rng = np.random.default_rng(n + m)
+    dense = rng.random((n, m)) < d
+    if arity > 2 or relax:  # (binary subtrees: 0.3-dense rows give records over 64 bytes)
+        dense[n // 3:n // 3 + 12] = rng.random((12, m)) < 0.3
+    t = O.OracleTree.from_dense(dense, part, arity, relax)
+    pt = _dev(t)
+    plain = _with_env("MBRWT_PACKT", "0", lambda: _dev(t))
+    if m == 600:  # the 512-column child is too tall: mixed images, general kernels
+        assert pt.traverse_kernel() != "k_traverse_ptw"
+    else:
+        assert pt.traverse_kernel() == "k_traverse_ptw"
+        assert pt.device_bytes() != plain.device_bytes()
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 20000)]).astype(np.uint64)
+    cols = np.random.default_rng(1).integers(0, m, 12)
+    _agree(t, [pt, plain], rows, cols, m)
+
+
+def test_packt_records_longer_than_a_block(oracle_mod):
+    """Fully set rows make records longer than 64 bytes: the host builder
+    declines KIND_PACKT for those root children; results as the oracle's."""
+    O = oracle_mod
+    rng = np.random.default_rng(31)
+    n, m = 2000, 400
+    dense = rng.random((n, m)) < 0.01
+    dense[[3, 1000]] = True
+    t = O.OracleTree.from_dense(dense, "greedy", 2, 0)  # binary: a full row is one mask per internal node
+    d = _dev(t)
+    assert d.traverse_kernel() != "k_traverse_ptw"
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 5000)]).astype(np.uint64)
+    _agree(t, [d], rows, [0, 5, 399], m)
+
+
+@pytest.mark.parametrize("relax,n_rows", [(10, 3_000_000), (0, 1_000_000)])
+def test_packt_synthetic_shaped(oracle_mod, relax, n_rows):
+    """The generator's KIND_PACKT images over a greedy (+ relaxed) shape
+    (synth.hip synth_packt) against the oracle's independent implementation
+    of the same law, and against the node-by-node images (MBRWT_PACKT=0)."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    rng = np.random.default_rng(relax + 7)
+    dense = rng.random((4000, 500)) < 0.01
+    shape = O.OracleTree.from_dense(dense, "greedy", 2, relax).export()
+    pt = BRWTDevice.synthetic_shaped(n_rows, shape, 0.003, 11)
+    plain = _with_env("MBRWT_PACKT", "0", lambda: BRWTDevice.synthetic_shaped(n_rows, shape, 0.003, 11))
+    assert pt.traverse_kernel() == "k_traverse_ptw"
+    assert pt.device_bytes() != plain.device_bytes()
+    t = O.OracleTree.topdown_shaped(n_rows, shape, 0.003, 11)
+    rows = rng.integers(0, n_rows, 100_000).astype(np.uint64)
+    _agree(t, [pt, plain], rows, [0, 1, 250, 499], 500)
