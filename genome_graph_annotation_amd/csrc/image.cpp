@@ -955,8 +955,10 @@ void build_p2w_table(Tree &tree) {
 }
 
 // The shape k_traverse_ptw takes: dnode 0 a PLANE node of arity <= 16 (the
-// folded root) whose children are leaves or KIND_PACKT nodes; labels and
-// local node indices below 2^15 (u16 entries).  Layout: mbrwt_internal.hpp.
+// folded root) whose children are leaves or KIND_PACKT nodes; columns and
+// local node indices below 2^15 (u16 entries).  The leaf entries hold the
+// GLOBAL columns (the walk's order is the output order; no label map
+// afterwards).  Layout: mbrwt_internal.hpp.
 void build_ptw_table(Tree &tree) {
     tree.ptw_table.clear();
     const auto &N = tree.nodes;
@@ -993,8 +995,9 @@ void build_ptw_table(Tree &tree) {
         for (uint32_t c = 0; c < v.arity; ++c) {
             const DevNode &w = N[v.first_child + c];
             if (w.kind == KIND_LEAF) {
-                if (w.label >= 0x8000) return;
-                ent.push_back((uint16_t)(0x8000u | w.label));
+                const uint32_t col = tree.label_perm.empty() ? w.label : tree.label_perm[w.label];
+                if (col >= 0x8000) return;
+                ent.push_back((uint16_t)(0x8000u | col));
             } else {
                 ent.push_back((uint16_t)local[v.first_child + c]);
             }
@@ -1013,7 +1016,7 @@ void build_ptw_table(Tree &tree) {
         const DevNode &d = N[u];
         uint32_t *e = &t[4 + 4 * k];
         if (d.kind == KIND_LEAF) {
-            e[3] = 0x80000000u | d.label;
+            e[3] = 0x80000000u | (tree.label_perm.empty() ? d.label : tree.label_perm[d.label]);
             continue;
         }
         e[0] = (uint32_t)d.base;

@@ -149,10 +149,10 @@ constexpr uint32_t kP2wMaxWords = 1024;
 // KIND_PACKT node): u32 words
 //   [0] R = arity of dnode 0, [1] nI, [2] nE, [3] max subtree height,
 //   R x {base lo, base hi, span, entry}   (entry: bit 31 = leaf, then
-//        its label in bits 0..30; else the PACKT node's local index)
+//        its global column in bits 0..30; else the PACKT node's local index)
 //   nI x {first entry [0:16) | arity [24:29)}   (the internal nodes of the
 //        PACKT subtrees, local indices)
-//   nE u16 child entries (bit 15 = leaf, label in bits 0..14; else the child's local index)
+//   nE u16 child entries (bit 15 = leaf, global column in bits 0..14; else the child's local index)
 constexpr uint32_t kPtwMaxWords = 8192;
 constexpr uint32_t kFastMaxDepth = 4;  // PLANE levels the specialised kernel's stack holds
 

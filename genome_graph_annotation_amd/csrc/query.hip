@@ -2075,6 +2075,7 @@ struct RowblockKernel {
     uint32_t table_words;
     size_t lds;
     uint32_t wpb;
+    bool final_columns;  // the kernel emits global columns (k_traverse_ptw): no label map afterwards
 };
 static int run_get_rows_p2w(Ctx &c, const RowblockKernel &kr, const uint64_t *d_rows, uint64_t n,
                             uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap, uint64_t *needed, hipStream_t s) {
@@ -2163,9 +2164,9 @@ static int run_get_rows_p2w(Ctx &c, const RowblockKernel &kr, const uint64_t *d_
         return MBRWT_ERR_CAPACITY;
     }
     const uint64_t g = std::min<uint64_t>((nb + 15) / 16, 8192);
-    const uint32_t map_lds = label_map_lds(c);
+    const uint32_t map_lds = kr.final_columns ? 0u : label_map_lds(c);
     hipLaunchKernelGGL(k_compact_blocks, dim3((unsigned)g), dim3(256), map_lds * 4, s, d_counts, d_block_offsets, p.temp,
-                       C, d_offsets, d_cols, n, (const uint32_t *)c.d_label_map, map_lds);
+                       C, d_offsets, d_cols, n, kr.final_columns ? nullptr : (const uint32_t *)c.d_label_map, map_lds);
     MBRWT_HIP(hipGetLastError());
     if (ovf) {
         TravParams q = base_params(c);
@@ -2200,11 +2201,11 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
         const size_t words = c.tree.ptw_table.size();
         const size_t per_wave = pk.wide ? PtwLayout<true>::kWords : PtwLayout<false>::kWords;
         const RowblockKernel kr{pk.fn, c.d_ptw, (uint32_t)words, ((words + 3) & ~size_t(3)) * 4 + pk.wpb * per_wave * 4,
-                                pk.wpb};
+                                pk.wpb, true};
         return run_get_rows_p2w(c, kr, d_rows, n, d_offsets, d_cols, cap, needed, s);
     }
     if (const P2wFn kfn = p2w_kernel(c)) {
-        const RowblockKernel kr{kfn, c.d_p2w, (uint32_t)c.tree.p2w_table.size(), p2w_lds_bytes(c), 4};
+        const RowblockKernel kr{kfn, c.d_p2w, (uint32_t)c.tree.p2w_table.size(), p2w_lds_bytes(c), 4, false};
         return run_get_rows_p2w(c, kr, d_rows, n, d_offsets, d_cols, cap, needed, s);
     }
     const uint32_t K = auto_slots(c);
