@@ -1378,6 +1378,57 @@ __device__ __forceinline__ void ptw_walk(const AS_LDS uint8_t *pb, uint32_t o, u
     }
 }
 
+// The same walk for all 64 lanes of the wave at once, in lockstep and
+// without per-lane branches (the branchy walk's exec-mask and loop handling
+// measured more scalar than vector instructions per launch): each iteration
+// takes one child of every lane's top frame; a leaf stores its column, an
+// internal child pushes its frame (selects over the register stack) and an
+// emptied frame is popped at the end of the iteration.  Lanes with no record
+// (`live` false) idle.  Ring only (the `direct` rounds use ptw_walk).
+template <int MAXD>
+__device__ __forceinline__ void ptw_walk_wave(const AS_LDS uint8_t *pb, uint32_t o, uint32_t node, bool live,
+                                              const AS_LDS uint32_t *ntab, const AS_LDS uint16_t *etab,
+                                              AS_LDS uint32_t *ring, uint32_t smask, uint32_t pos, bool &overflow) {
+    uint32_t nw = ntab[live ? node : 0u];
+    uint32_t m = pb[o];
+    const uint32_t w0 = (nw >> 24) > 8 ? 1u : 0u;
+    m |= w0 ? (uint32_t)pb[o + 1] << 8 : 0u;
+    o += 1 + w0;
+    uint32_t top = live ? ((nw & 0xFFFFu) | (m << 16)) : 0u;
+    uint32_t st[MAXD - 1];
+#pragma unroll
+    for (int k = 0; k < MAXD - 1; ++k) st[k] = 0;
+    uint32_t sp = 0;
+    bool done = !live || (top >> 16) == 0;
+    while (__any(!done)) {
+        const uint32_t mm = top >> 16;
+        const uint32_t c = (uint32_t)__builtin_ctz(mm | 0x10000u);
+        top &= ~(0x10000u << c);
+        const uint32_t e = etab[done ? 0u : (top & 0xFFFFu) + c];
+        const bool leaf = (e & 0x8000u) != 0;
+        if (!done && leaf) ring[pos & smask] = e & 0x7FFFu;
+        pos += (!done && leaf) ? 1u : 0u;
+        const bool inner = !done && !leaf;
+        const uint32_t nw2 = ntab[inner ? e : 0u];
+        const uint32_t w2 = (nw2 >> 24) > 8 ? 1u : 0u;
+        const uint32_t mw = (uint32_t)pb[o] | (w2 ? (uint32_t)pb[o + 1] << 8 : 0u);
+        o += inner ? 1u + w2 : 0u;
+        const bool push = inner && (top >> 16) != 0;
+        overflow |= push && sp == (uint32_t)(MAXD - 1);
+#pragma unroll
+        for (int k = MAXD - 2; k > 0; --k) st[k] = push ? st[k - 1] : st[k];
+        st[0] = push ? top : st[0];
+        sp += push ? 1u : 0u;
+        top = inner ? ((nw2 & 0xFFFFu) | (mw << 16)) : top;
+        const bool pop = !done && (top >> 16) == 0 && sp > 0;  // (pushed frames are never empty)
+        top = pop ? st[0] : top;
+#pragma unroll
+        for (int k = 0; k < MAXD - 2; ++k) st[k] = pop ? st[k + 1] : st[k];
+        sp -= pop ? 1u : 0u;
+        done = done || (top >> 16) == 0;
+    }
+}
+
 template <bool NT, bool WIDE, int MAXD, int WPB>
 __global__ __launch_bounds__(64 * WPB) void k_traverse_ptw(P2wParams p) {
     using Lay = PtwLayout<WIDE>;
@@ -1539,9 +1590,14 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_ptw(P2wParams p) {
                     if (q2 < p.C) gst(out + q2, (uint32_t)ring[q2 & smask]);
                 wave_sync_lds();
             }
-            if (blk) ptw_walk<MAXD>(pb, s + 1, ent, ntab, etab, ring, smask, ibase, direct, out, p.C, overflow);
-            else if (act && !direct) ring[ibase & smask] = ent & 0x7FFFFFFFu;
-            else if (act && ibase < p.C) gst(out + ibase, ent & 0x7FFFFFFFu);
+            if (!direct) {
+                ptw_walk_wave<MAXD>(pb, s + 1, ent, blk, ntab, etab, ring, smask, ibase, overflow);
+                if (act && !blk) ring[ibase & smask] = ent & 0x7FFFFFFFu;
+            } else if (blk) {
+                ptw_walk<MAXD>(pb, s + 1, ent, ntab, etab, ring, smask, ibase, direct, out, p.C, overflow);
+            } else if (act && ibase < p.C) {
+                gst(out + ibase, ent & 0x7FFFFFFFu);
+            }
             running += rtot;
             if (direct) {
                 flushed = running;
@@ -2163,8 +2219,8 @@ static int run_get_rows_p2w(Ctx &c, const RowblockKernel &kr, const uint64_t *d_
         set_error("cols_cap too small");
         return MBRWT_ERR_CAPACITY;
     }
-    const uint64_t g = std::min<uint64_t>((nb + 15) / 16, 8192);
     const uint32_t map_lds = kr.final_columns ? 0u : label_map_lds(c);
+    const uint64_t g = std::min<uint64_t>((nb + 15) / 16, 8192);
     hipLaunchKernelGGL(k_compact_blocks, dim3((unsigned)g), dim3(256), map_lds * 4, s, d_counts, d_block_offsets, p.temp,
                        C, d_offsets, d_cols, n, kr.final_columns ? nullptr : (const uint32_t *)c.d_label_map, map_lds);
     MBRWT_HIP(hipGetLastError());

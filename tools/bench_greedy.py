@@ -79,6 +79,7 @@ def main():
                          "many rows (mbrwt_create_synthetic_shaped; parity by the streamed shaped oracle)")
     ap.add_argument("--scaled-batch", type=int, default=8_000_000)
     ap.add_argument("--skip-small", action="store_true", help="only the scaled shape")
+    ap.add_argument("--shapes", default="greedy+relax,basic arity 8", help="comma-separated subset of the shapes")
     a = ap.parse_args()
     import oracle as O
     from genome_graph_annotation_amd import BRWTDevice
@@ -87,7 +88,10 @@ def main():
     rows_np = np.random.default_rng(42).integers(0, a.rows, a.batch, dtype=np.uint64)
     res = {}
     shapes = {}
+    want = set(a.shapes.split(","))
     for shape, part, arity, relax in [("greedy+relax", "greedy", 2, a.relax), ("basic arity 8", "basic", 8, 0)]:
+        if shape not in want:
+            continue
         if a.skip_small:
             t0 = time.time()
             t = O.OracleTree.norepl(a.rows, a.cols, a.density, 42, part, arity, relax)
