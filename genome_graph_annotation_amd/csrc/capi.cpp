@@ -551,7 +551,7 @@ int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value) {
         c.slot_labels = (uint32_t)value;
         return MBRWT_OK;
     case MBRWT_OPT_KERNEL:
-        if (!(value >= 0 && value <= 6) && value != 10 && !(value >= 17 && value <= 29)) return MBRWT_ERR_INVALID;
+        if (!(value >= 0 && value <= 6) && value != 10 && !(value >= 17 && value <= 30)) return MBRWT_ERR_INVALID;
         c.kernel_variant = (int)value;
         return MBRWT_OK;
     default:

@@ -1319,10 +1319,10 @@ __global__ __launch_bounds__(256, OCC) void k_traverse_p2w(P2wParams p) {
 // MAXD: stack levels of the walk (>= the PACKT subtrees' height); WPB: waves
 // per workgroup (the PTW table is staged once per workgroup).
 // ------------------------------------------------------------------------
-template <bool WIDE>
+template <bool WIDE, uint32_t RING = 512>
 struct PtwLayout {
     static constexpr uint32_t kItems = WIDE ? 256 : 128;  // 16 rows x R children
-    static constexpr uint32_t kRing = 512;                // labels
+    static constexpr uint32_t kRing = RING;               // labels
     // items j | items k | row counts | group's first item | blocks (64 x 64 B) | ring
     static constexpr uint32_t kWords = kItems + kItems / 4 + 16 + 20 + 1024 + kRing;
 };
@@ -1429,9 +1429,9 @@ __device__ __forceinline__ void ptw_walk_wave(const AS_LDS uint8_t *pb, uint32_t
     }
 }
 
-template <bool NT, bool WIDE, int MAXD, int WPB>
+template <bool NT, bool WIDE, int MAXD, int WPB, uint32_t RING = 512>
 __global__ __launch_bounds__(64 * WPB) void k_traverse_ptw(P2wParams p) {
-    using Lay = PtwLayout<WIDE>;
+    using Lay = PtwLayout<WIDE, RING>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_ptw[];
     const uint32_t lane = threadIdx.x & 63, c = lane & 3, g = lane >> 2, gb = lane & ~3u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2086,25 +2086,31 @@ static size_t p2w_lds_bytes(const Ctx &c) {
 }
 
 // k_traverse_ptw for this context?  Default for trees with a PTW table
-// (MBRWT_OPT_KERNEL 0 or 24..29): 24 plain reads, 25 non-temporal, 26/27 the
-// same with 8 waves per workgroup, 28/29 with 16.
+// (MBRWT_OPT_KERNEL 0 or 24..30): 24 plain reads, 25 non-temporal, 26/27 the
+// same with 8 waves per workgroup, 28/29 with 16 (512-label rings: LDS holds
+// 16 waves per CU); 30 and the default: 7 waves per workgroup with a
+// 256-label ring (21 waves per CU; 2.27 vs 2.47 ms at the greedy + relax shape).
 struct PtwPick {
     P2wFn fn = nullptr;
     uint32_t wpb = 4;
+    uint32_t ring = 512;
     bool wide = false;
 };
 template <bool NT, bool WIDE, int MAXD>
 static P2wFn ptw_fn(uint32_t wpb) {
-    return wpb == 16 ? k_traverse_ptw<NT, WIDE, MAXD, 16> : wpb == 8 ? k_traverse_ptw<NT, WIDE, MAXD, 8>
-                                                                  : k_traverse_ptw<NT, WIDE, MAXD, 4>;
+    return wpb == 16  ? k_traverse_ptw<NT, WIDE, MAXD, 16>
+           : wpb == 8 ? k_traverse_ptw<NT, WIDE, MAXD, 8>
+           : wpb == 7 ? k_traverse_ptw<NT, WIDE, MAXD, 7, 256>
+                      : k_traverse_ptw<NT, WIDE, MAXD, 4>;
 }
 static PtwPick ptw_kernel(const Ctx &c) {
     PtwPick r;
     const int kv = c.kernel_variant;
     const auto &t = c.tree.ptw_table;
-    if (t.empty() || !c.d_ptw || !(kv == 0 || (kv >= 24 && kv <= 29))) return r;
-    const bool nt = kv == 0 ? c.tree.image_bytes > (1ull << 30) : (kv & 1) != 0;
-    r.wpb = kv >= 28 ? 16 : kv >= 26 ? 8 : 4;
+    if (t.empty() || !c.d_ptw || !(kv == 0 || (kv >= 24 && kv <= 30))) return r;
+    const bool nt = kv == 0 || kv == 30 ? c.tree.image_bytes > (1ull << 30) : (kv & 1) != 0;
+    r.wpb = (kv == 0 || kv == 30) ? 7 : kv >= 28 ? 16 : kv >= 26 ? 8 : 4;  // default: 7 waves, 256-label ring
+    r.ring = r.wpb == 7 ? 256 : 512;
     r.wide = t[0] > 8;
     const bool deep = t[3] > 4;
 #define PTW(NTV, W, D) if (nt == NTV && r.wide == W && deep == D) r.fn = ptw_fn<NTV, W, D ? 8 : 4>(r.wpb);
@@ -2255,7 +2261,8 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
     }
     if (const PtwPick pk = ptw_kernel(c); pk.fn) {
         const size_t words = c.tree.ptw_table.size();
-        const size_t per_wave = pk.wide ? PtwLayout<true>::kWords : PtwLayout<false>::kWords;
+        const size_t per_wave = pk.ring == 256 ? (pk.wide ? PtwLayout<true, 256>::kWords : PtwLayout<false, 256>::kWords)
+                                               : (pk.wide ? PtwLayout<true>::kWords : PtwLayout<false>::kWords);
         const RowblockKernel kr{pk.fn, c.d_ptw, (uint32_t)words, ((words + 3) & ~size_t(3)) * 4 + pk.wpb * per_wave * 4,
                                 pk.wpb, true};
         return run_get_rows_p2w(c, kr, d_rows, n, d_offsets, d_cols, cap, needed, s);

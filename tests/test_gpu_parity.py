@@ -20,7 +20,7 @@ def _dev(tree):
     return BRWTDevice.from_tree(tree.export())
 
 
-def _check_rows(oracle_tree, dev, rows, variants=(0, 1, 2, 4, 5, 10, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29)):
+def _check_rows(oracle_tree, dev, rows, variants=(0, 1, 2, 4, 5, 10, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30)):
     """Every traversal kernel (1 lane-per-row; 2/3/4 group-cooperative with
     1/2/4 children per lane; 0 the default) must
     reproduce the oracle's ordered CSR exactly."""
