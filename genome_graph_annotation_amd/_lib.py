@@ -123,6 +123,7 @@ SIGNATURES = {
     "mbrwt_num_nodes": (C.c_uint64, [C.c_void_p]),
     "mbrwt_device_bytes": (C.c_uint64, [C.c_void_p]),
     "mbrwt_device": (C.c_int, [C.c_void_p]),
+    "mbrwt_num_shards": (C.c_uint64, [C.c_void_p]),
     "mbrwt_get_rows": (C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p, u32p, C.c_uint64, u64p]),
     "mbrwt_get_rows_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
                                         u64p, C.c_void_p]),

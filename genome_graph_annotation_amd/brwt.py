@@ -249,6 +249,10 @@ class BRWTDevice:
     def num_nodes(self):
         return L.lib().mbrwt_num_nodes(self._h)
 
+    def num_shards(self):
+        """Row shards of the context (1 below 2^32 rows; include/mbrwt.h)."""
+        return L.lib().mbrwt_num_shards(self._h)
+
     def device_bytes(self):
         return L.lib().mbrwt_device_bytes(self._h)
 

@@ -561,8 +561,40 @@ int mbrwt_tree_export(mbrwt_ctx *ctx, mbrwt_tree **out) {
     try {
         MBRWT_HIP(hipSetDevice(c.device));
         auto t = std::make_unique<mbrwt_tree>();
-        const int rc = export_tree(c, *t);
-        if (rc) return rc;
+        if (c.shards.empty()) {
+            const int rc = export_tree(c, *t);
+            if (rc) return rc;
+        } else {
+            // row shards (shards.hip): every node's column is the concatenation
+            // of its columns in the shards, in row order (the inverse of slice_desc)
+            for (size_t k = 0; k < c.shards.size(); ++k) {
+                mbrwt_tree part;
+                const int rc = export_tree(*c.shards[k], part);
+                if (rc) return rc;
+                if (k == 0) {
+                    *t = std::move(part);
+                    continue;
+                }
+                if (part.num_children != t->num_children || part.first_child != t->first_child ||
+                    part.leaf_column != t->leaf_column) {
+                    set_error("export: row shards with different tree shapes");
+                    return MBRWT_ERR_UNSUPPORTED;
+                }
+                t->num_rows += part.num_rows;
+                for (size_t u = 0; u < part.vec_size.size(); ++u) {
+                    auto &w = t->words[u];
+                    const uint64_t at = t->vec_size[u], len = part.vec_size[u];
+                    w.resize((at + len + 63) / 64, 0);
+                    for (uint64_t i = 0; i < (len + 63) / 64; ++i) {
+                        const uint64_t v = part.words[u][i], pos = at + 64 * i;
+                        w[pos >> 6] |= v << (pos & 63);
+                        if ((pos & 63) && (pos >> 6) + 1 < w.size()) w[(pos >> 6) + 1] |= v >> (64 - (pos & 63));
+                    }
+                    t->vec_size[u] = at + len;
+                }
+            }
+            t->num_rows = c.tree.num_rows;
+        }
         t->finish();
         *out = t.release();
         return MBRWT_OK;

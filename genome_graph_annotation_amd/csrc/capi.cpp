@@ -66,10 +66,12 @@ static int upload_tables(Ctx &c) {
 
 static void release(Ctx *c) {
     if (!c) return;
+    for (Ctx *sc : c->shards) release(sc);
     (void)hipSetDevice(c->device);
     free_tree(c->tree);
     for (Workspace *w : {&c->ws_temp, &c->ws_counts, &c->ws_ovf, &c->ws_scan, &c->ws_rows, &c->ws_out, &c->ws_sort,
-                         &c->ws_cls_off, &c->ws_cls_cols})
+                         &c->ws_cls_off, &c->ws_cls_cols, &c->ws_sh_keys, &c->ws_sh_local, &c->ws_sh_cnt,
+                         &c->ws_sh_sort, &c->ws_sh_tmp})
         if (w->buf) (void)hipFree(w->buf);
     if (c->d_nodes) (void)hipFree(c->d_nodes);
     if (c->d_cnodes) (void)hipFree(c->d_cnodes);
@@ -124,6 +126,53 @@ static int create_common(int device, mbrwt_ctx **out, Build &&build) {
 static Ctx *C(mbrwt_ctx *p) { return reinterpret_cast<Ctx *>(p); }
 static const Ctx *C(const mbrwt_ctx *p) { return reinterpret_cast<const Ctx *>(p); }
 
+// A context over row shards (shards.hip): sub-contexts over the rows
+// [k R, min(n, (k+1) R)), built in row order by build_shard(ctx, a, b).
+template <class BuildShard>
+static int create_sharded(int device, uint64_t num_rows, uint64_t num_columns, uint64_t R, mbrwt_ctx **out,
+                          BuildShard &&build_shard) {
+    return create_common(device, out, [&](Ctx &c) {
+        c.tree.num_rows = num_rows;
+        c.tree.num_columns = num_columns;
+        c.shard_rows = R;
+        for (uint64_t a = 0; a < num_rows; a += R) {
+            const uint64_t b = std::min(num_rows, a + R);
+            mbrwt_ctx *sub = nullptr;
+            const int rc = create_common(device, &sub, [&](Ctx &sc) { return build_shard(sc, a, b); });
+            if (rc) return rc;
+            Ctx *sc = C(sub);
+            c.shards.push_back(sc);
+            c.tree.num_relations += sc->tree.num_relations;
+            c.tree.image_bytes += sc->tree.image_bytes;
+            c.tree.num_nodes = sc->tree.num_nodes;
+        }
+        return MBRWT_OK;
+    });
+}
+
+// the synthetic law over row shards: shard k draws node u's masks at the
+// positions after those of shards 0..k-1 (SynthShard, synth.hip)
+static int create_synthetic_any(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape, int device,
+                                mbrwt_ctx **out) {
+    const uint64_t R = desc.num_columns ? shard_rows_for(desc.num_rows) : 0;
+    if (!R)
+        return create_common(device, out,
+                             [&](Ctx &c) { return build_synthetic(desc, shape, device, c.tree, c.stream); });
+    SynthShard st;
+    std::vector<uint64_t> lens;
+    st.len_out = &lens;
+    return create_sharded(device, desc.num_rows, desc.num_columns, R, out, [&](Ctx &sc, uint64_t a, uint64_t b) {
+        mbrwt_synth_desc d = desc;
+        d.num_rows = b - a;
+        st.row0 = a;
+        const int rc = build_synthetic(d, shape, device, sc.tree, sc.stream, &st);
+        if (rc) return rc;
+        if (st.pos0.size() < lens.size()) st.pos0.resize(lens.size(), 0);
+        for (size_t u = 0; u < lens.size(); ++u) st.pos0[u] += lens[u];
+        return MBRWT_OK;
+    });
+}
+
 }  // namespace mbrwt
 
 using namespace mbrwt;
@@ -136,6 +185,14 @@ int mbrwt_create(const mbrwt_tree_desc *desc, int device, mbrwt_ctx **out) {
         return MBRWT_ERR_INVALID;
     }
     try {
+        const uint64_t R = desc->num_nodes ? shard_rows_for(desc->num_rows) : 0;
+        if (R)  // rows >= 2^32: every shard is built from the description's slice
+            return create_sharded(device, desc->num_rows, desc->num_columns, R, out,
+                                  [&](Ctx &sc, uint64_t a, uint64_t b) {
+                                      SlicedDesc sd;
+                                      const int rc = slice_desc(*desc, a, b, sd);
+                                      return rc ? rc : build_from_desc(sd.desc, device, sc.tree);
+                                  });
         return create_common(device, out, [&](Ctx &c) { return build_from_desc(*desc, device, c.tree); });
     } catch (const std::bad_alloc &) {
         set_error("host allocation failed");
@@ -153,8 +210,7 @@ int mbrwt_create_synthetic_shaped(const mbrwt_synth_desc *desc, const mbrwt_shap
         return MBRWT_ERR_INVALID;
     }
     try {
-        return create_common(device, out,
-                             [&](Ctx &c) { return build_synthetic(*desc, shape, device, c.tree, c.stream); });
+        return create_synthetic_any(*desc, shape, device, out);
     } catch (const std::bad_alloc &) {
         set_error("host allocation failed");
         return MBRWT_ERR_NOMEM;
@@ -170,8 +226,7 @@ int mbrwt_create_synthetic(const mbrwt_synth_desc *desc, int device, mbrwt_ctx *
         return MBRWT_ERR_INVALID;
     }
     try {
-        return create_common(device, out,
-                             [&](Ctx &c) { return build_synthetic(*desc, nullptr, device, c.tree, c.stream); });
+        return create_synthetic_any(*desc, nullptr, device, out);
     } catch (const std::bad_alloc &) {
         set_error("host allocation failed");
         return MBRWT_ERR_NOMEM;
@@ -243,6 +298,7 @@ uint64_t mbrwt_num_relations(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.n
 uint64_t mbrwt_num_nodes(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.num_nodes : 0; }
 uint64_t mbrwt_device_bytes(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.image_bytes : 0; }
 int mbrwt_device(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->device : -1; }
+uint64_t mbrwt_num_shards(const mbrwt_ctx *ctx) { return ctx ? std::max<uint64_t>(1, C(ctx)->shards.size()) : 0; }
 
 int mbrwt_get_rows_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols,
                           uint64_t cols_cap, uint64_t *cols_needed, void *stream) {
@@ -538,10 +594,9 @@ int mbrwt_count_work_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, 
     return run_count_work(c, d_rows, n, sum_visits, sum_labels, reinterpret_cast<hipStream_t>(stream));
 }
 
-int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value) {
-    if (!ctx) return MBRWT_ERR_INVALID;
-    Ctx &c = *C(ctx);
-    std::lock_guard<std::mutex> lk(c.mu);
+static int apply_option(Ctx &c, int option, int64_t value) {
+    for (Ctx *sc : c.shards)
+        if (const int rc = apply_option(*sc, option, value)) return rc;
     switch (option) {
     case MBRWT_OPT_TIMING:
         c.timing = value != 0;
@@ -560,10 +615,23 @@ int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value) {
     }
 }
 
+int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value) {
+    if (!ctx) return MBRWT_ERR_INVALID;
+    Ctx &c = *C(ctx);
+    std::lock_guard<std::mutex> lk(c.mu);
+    return apply_option(c, option, value);
+}
+
 int mbrwt_take_timing(mbrwt_ctx *ctx, double *kernel_ms, uint64_t *launches) {
     if (!ctx) return MBRWT_ERR_INVALID;
     Ctx &c = *C(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    for (Ctx *sc : c.shards) {  // a sharded context's kernels run on its shards
+        c.timing_ms += sc->timing_ms;
+        c.timing_launches += sc->timing_launches;
+        sc->timing_ms = 0;
+        sc->timing_launches = 0;
+    }
     if (kernel_ms) *kernel_ms = c.timing_ms;
     if (launches) *launches = c.timing_launches;
     c.timing_ms = 0;
@@ -590,7 +658,7 @@ const char *mbrwt_traverse_kernel(mbrwt_ctx *ctx) {
     if (!ctx) return "";
     Ctx &c = *C(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
-    return traverse_kernel_name(c);
+    return traverse_kernel_name(c.shards.empty() ? c : *c.shards[0]);
 }
 
 }  // extern "C"

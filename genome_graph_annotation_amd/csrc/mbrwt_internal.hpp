@@ -175,6 +175,7 @@ inline CNode compact(const DevNode &d) {
 constexpr uint32_t kMaxArity = 64;       // child masks are held in <= 64 bits
 constexpr uint32_t kImagePad = 64;       // bytes of zero padding after every image
 constexpr uint64_t kMaxRows = 0xFFFFFFFFull;  // positions are 32-bit in the kernels
+constexpr uint64_t kShardRowsMax = 1ull << 31;  // rows per row shard of a larger context (shards.hip)
 
 inline uint32_t plane_stride(uint32_t arity) {  // >= 16: blocks are read as 16-byte pairs
     uint32_t s = 16;
@@ -286,6 +287,15 @@ struct Ctx {
     double timing_ms = 0;
     uint64_t timing_launches = 0;
     int grid_cache = 0;
+
+    // Row shards (rows >= 2^32; DESIGN.md §4 "Rows >= 2^32"): a BRWT restricted
+    // to a row range is again a BRWT, so a context over more rows than one
+    // image's u32 positions holds sub-contexts over consecutive ranges of
+    // shard_rows rows; this context's tree then holds only the totals, and
+    // every query routes its rows to the shards (shards.hip)
+    std::vector<Ctx *> shards;
+    uint64_t shard_rows = 0;
+    Workspace ws_sh_keys, ws_sh_local, ws_sh_cnt, ws_sh_sort, ws_sh_tmp;
 };
 
 // status helpers ---------------------------------------------------------
@@ -302,8 +312,37 @@ int ensure(Workspace &w, size_t bytes);
 
 // image construction (image.cpp / synth.hip)
 int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree);
+// a row shard of a synthetic tree: rows [row0, row0 + desc.num_rows) of the
+// whole tree, node u's positions starting at pos0[u] (empty = 0); len_out
+// (may be null) receives every internal node's positions in the shard
+struct SynthShard {
+    uint64_t row0 = 0;
+    std::vector<uint64_t> pos0;
+    std::vector<uint64_t> *len_out = nullptr;
+};
 int build_synthetic(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape, int device, Tree &tree,
-                    hipStream_t stream);
+                    hipStream_t stream, const SynthShard *shard = nullptr);
+// row shards (shards.hip): rows per shard for a context over num_rows rows
+// (0 = one image); MBRWT_SHARD_ROWS forces smaller shards (tests)
+uint64_t shard_rows_for(uint64_t num_rows);
+// the description of rows [a, b) of a tree (every node's index column cut to
+// the positions of those rows); MBRWT_ERR_INVALID when the columns' sizes do
+// not nest
+struct SlicedDesc {
+    std::vector<uint64_t> sizes;
+    std::vector<std::vector<uint64_t>> words;
+    std::vector<const uint64_t *> ptrs;
+    mbrwt_tree_desc desc{};
+};
+int slice_desc(const mbrwt_tree_desc &in, uint64_t a, uint64_t b, SlicedDesc &out);
+int sharded_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
+                     uint64_t *needed, hipStream_t s);
+int sharded_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n, uint8_t *d_out,
+                      hipStream_t s);
+int sharded_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts, hipStream_t s);
+int sharded_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s);
+int sharded_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap, uint64_t *rows_needed,
+                       hipStream_t s);
 int build_from_columns(const mbrwt_columns_desc &desc, int device, Tree &tree, hipStream_t stream,
                        uint64_t relax_max_arity = 0);
 // BRWTOptimizer::relax on a tree description (build.hip)

@@ -36,8 +36,9 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 __host__ __device__ __forceinline__ uint64_t node_key(uint64_t seed, uint64_t key) {
     return mix64(seed ^ ((key + 1) * 0x9E3779B97F4A7C15ull));
 }
+constexpr uint64_t kDrawMul = 0xD1B54A32D192ED03ull;
 __host__ __device__ __forceinline__ uint64_t draw(uint64_t k, uint64_t pos) {
-    return mix64(k + pos * 0xD1B54A32D192ED03ull);
+    return mix64(k + pos * kDrawMul);
 }
 constexpr uint64_t kRootKey = 0xFFFFFFFFull;
 constexpr uint32_t kSynthMaxArity = 12;
@@ -795,7 +796,7 @@ std::vector<ShapeNode> shape_from_desc(const mbrwt_shape_desc &sd, uint64_t m) {
 // stays for the per-node generation.  Children lengths of the root's
 // children come from the fold; the rest from the temporary planes' scans.
 static int synth_packt(const std::vector<ShapeNode> &shape, const std::vector<double> &q, const std::vector<uint64_t *> &node_T,
-                uint64_t seed, Tree &tree, std::vector<bool> &in_pack, unsigned long long *d_ctr,
+                const std::vector<uint64_t> &keys, Tree &tree, std::vector<bool> &in_pack, unsigned long long *d_ctr,
                 unsigned long long *d_ones, hipStream_t s) {
     const auto &root = shape[0].children;
     auto internal = [&](uint32_t v) { return !shape[v].children.empty(); };
@@ -844,7 +845,7 @@ static int synth_packt(const std::vector<ShapeNode> &shape, const std::vector<do
             const uint32_t a = (uint32_t)sh.children.size();
             const DevNode &vd = tree.nodes[v + 1];
             GenNode &g = gn[i];
-            g.K = node_key(seed, v);
+            g.K = keys[v];
             g.T = node_T[v];
             g.nT = (1u << a) - 1;
             g.arity = a;
@@ -953,7 +954,7 @@ static int synth_packt(const std::vector<ShapeNode> &shape, const std::vector<do
 }
 
 int build_synthetic(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape_desc, int device, Tree &tree,
-                    hipStream_t s) {
+                    hipStream_t s, const SynthShard *shard) {
     MBRWT_HIP(hipSetDevice(device));
     tree = Tree();
     const uint64_t n = desc.num_rows, m = desc.num_columns;
@@ -981,6 +982,13 @@ int build_synthetic(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape_
     tree.num_nodes = N;
     std::vector<double> q(N);
     for (uint32_t u = 0; u < N; ++u) q[u] = 1.0 - std::pow(1.0 - d, (double)shape[u].cols);
+    // node keys; a row shard starting at row0 whose nodes start at positions
+    // pos0[u] draws H(K, pos0 + j) = mix64((K + pos0 * kDrawMul) + j * kDrawMul):
+    // the same bits as the unsharded tree, through a shifted key
+    std::vector<uint64_t> keys(N);
+    for (uint32_t u = 0; u < N; ++u)
+        keys[u] = node_key(desc.seed, u) + (shard && u < shard->pos0.size() ? shard->pos0[u] : 0) * kDrawMul;
+    const uint64_t root_key = node_key(desc.seed, kRootKey) + (shard ? shard->row0 : 0) * kDrawMul;
 
     tree.nodes.assign(N + 1, DevNode{});
     for (uint32_t u = 0; u < N; ++u) {
@@ -1059,7 +1067,7 @@ int build_synthetic(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape_
         sr.arity = 1;
         sr.label = UINT32_MAX;
         sr.length = n;
-        const uint64_t K = node_key(desc.seed, kRootKey);
+        const uint64_t K = root_key;
         const uint64_t T = prob_to_threshold(q[0]);
         if (shape[0].children.empty()) {  // one column: the root is a leaf
             sr.kind = KIND_MASK8;
@@ -1098,7 +1106,7 @@ int build_synthetic(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape_
                     (void)hipFree(tmp);
                     return fail(MBRWT_ERR_NOMEM, "device allocation failed");
                 }
-                fold_fn(a, plane)(fimg, n, reinterpret_cast<const uint8_t *>(tmp), node_key(desc.seed, 0), node_T[0],
+                fold_fn(a, plane)(fimg, n, reinterpret_cast<const uint8_t *>(tmp), keys[0], node_T[0],
                                   nT, sr.stride, d_ones, s);
                 if (hipGetLastError() != hipSuccess) {
                     (void)hipFree(tmp);
@@ -1131,7 +1139,7 @@ int build_synthetic(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape_
     unsigned long long *d_ctr = nullptr;
     if (hipMalloc(&d_ctr, 2 * sizeof(unsigned long long)) != hipSuccess) return fail(MBRWT_ERR_NOMEM, "hipMalloc");
     if (tree.folded && packt_enabled()) {
-        if ((rc = synth_packt(shape, q, node_T, desc.seed, tree, in_pack, d_ctr, d_ones, s))) {
+        if ((rc = synth_packt(shape, q, node_T, keys, tree, in_pack, d_ctr, d_ones, s))) {
             (void)hipFree(d_ctr);
             return fail(rc, "synthetic: KIND_PACKT generation");
         }
@@ -1141,7 +1149,7 @@ int build_synthetic(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape_
         DevNode &dn = tree.nodes[u + 1];
         if (sh.children.empty() || dn.kind == KIND_FOLDED || in_pack[u]) continue;
         const uint64_t L = dn.length;  // positions = popcount of u's own column
-        const uint64_t K = node_key(desc.seed, u);
+        const uint64_t K = keys[u];
         const uint32_t a = dn.arity, nT = (1u << a) - 1;
         // KIND_PACK2 when every child A is a PLANE node of <= 8 MASK8 children
         // with <= 8 leaves; span S = the largest of 8, 4, 2 at which a block
@@ -1213,7 +1221,7 @@ int build_synthetic(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape_
                     (void)hipFree(d_ctr);
                     return fail(MBRWT_ERR_NOMEM, "device allocation failed");
                 }
-                plane_fn(ca)(ap, tot[c], node_key(desc.seed, cu), node_T[cu], (1u << ca) - 1, ch.stride, s);
+                plane_fn(ca)(ap, tot[c], keys[cu], node_T[cu], (1u << ca) - 1, ch.stride, s);
                 if ((rc = plane_scan(ap, tot[c], ca, ch.stride, gtot, s))) {
                     free_tmps();
                     (void)hipFree(d_ctr);
@@ -1231,7 +1239,7 @@ int build_synthetic(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape_
                     gn.length = gtot[g];
                     gn.base = 0;
                     in_pack[gu] = true;
-                    args.KB[8 * c + g] = node_key(desc.seed, gu);
+                    args.KB[8 * c + g] = keys[gu];
                     const uint32_t ti = (uint32_t)(std::find(utab.begin(), utab.end(), node_T[gu]) - utab.begin());
                     args.tB[8 * c + g] = (uint8_t)ti;
                     args.nT[ti] = (1u << gn.arity) - 1;
@@ -1315,7 +1323,7 @@ int build_synthetic(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape_
                 in_pack[cu] = true;
                 args.T[c] = node_T[cu];
                 args.nT[c] = (1u << ch.arity) - 1;
-                args.K[c] = node_key(desc.seed, cu);
+                args.K[c] = keys[cu];
             }
             const uint32_t pstride = dn.stride;
             (void)hipMemsetAsync(d_ctr, 0, sizeof(unsigned long long), s);
@@ -1379,6 +1387,11 @@ int build_synthetic(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape_
     tree.num_relations += ones;
     cleanup();
     (void)hipFree(d_ones);
+    if (shard && shard->len_out) {  // positions of every internal node in this shard
+        shard->len_out->assign(N, 0);
+        for (uint32_t u = 0; u < N; ++u)
+            if (!shape[u].children.empty()) (*shard->len_out)[u] = tree.nodes[u + 1].length;
+    }
     return finalize_tree(tree);
 }
 

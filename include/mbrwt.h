@@ -87,7 +87,7 @@ int mbrwt_create(const mbrwt_tree_desc *desc, int device, mbrwt_ctx **out);
  * basic-partitioner (BRWT_builders.cpp:20-31) BRWT built from i.i.d.
  * Bernoulli(density) columns (experiments/data_generation.cpp:20-29), drawn
  * top-down from a counter-based hash (spec: DESIGN.md "Synthetic matrices").
- * arity in [2, 12]; num_rows < 2^32.
+ * arity in [2, 12]; num_rows >= 2^32 builds row shards (mbrwt_num_shards).
  */
 typedef struct mbrwt_synth_desc {
     uint64_t num_rows;
@@ -184,6 +184,16 @@ uint64_t mbrwt_num_relations(const mbrwt_ctx *ctx);
 uint64_t mbrwt_num_nodes(const mbrwt_ctx *ctx);
 uint64_t mbrwt_device_bytes(const mbrwt_ctx *ctx); /* HBM held by the structure image */
 int mbrwt_device(const mbrwt_ctx *ctx);
+/*
+ * Row shards: the reference's Row is uint64_t (binary_matrix.hpp:11).  One
+ * device image addresses < 2^32 positions, so a context over more rows
+ * (mbrwt_create, mbrwt_load, mbrwt_create_synthetic[_shaped]) holds row
+ * shards of 2^31 rows -- each the BRWT restricted to its row range -- and
+ * routes every query's rows to them; results are those of the whole matrix.
+ * mbrwt_num_shards = 1 for an ordinary context.  (MBRWT_SHARD_ROWS=<rows> in
+ * the environment at creation forces smaller shards: a test hook.)
+ */
+uint64_t mbrwt_num_shards(const mbrwt_ctx *ctx);
 
 /* ---- queries ----------------------------------------------------------- */
 /*
