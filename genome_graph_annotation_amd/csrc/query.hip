@@ -1637,16 +1637,27 @@ __global__ __launch_bounds__(256) void k_compact_blocks(const uint32_t *__restri
                                                         const uint32_t *__restrict__ temp, uint32_t C,
                                                         uint64_t *__restrict__ offsets, uint32_t *__restrict__ cols,
                                                         uint64_t n, const uint32_t *__restrict__ label_map,
-                                                        uint32_t map_lds) {
+                                                        uint32_t map_lds, uint64_t cap) {
     const LabelMap lmap = stage_label_map(label_map, map_lds);
     const uint32_t lane = threadIdx.x & 63, sub = lane & 15;
     const uint64_t nb = (n + 15) / 16;
+    // launched before the host knows the total: a batch over the caller's
+    // capacity writes nothing (the host then returns MBRWT_ERR_CAPACITY)
+    if (gld(block_offsets + nb) > cap) return;
     const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) >> 4;
     for (uint64_t b = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; b < nb; b += stride) {
         const uint64_t r0 = b * 16;
         const uint32_t nr = (uint32_t)(n - r0 < 16 ? n - r0 : 16);
         const uint64_t base = gld(block_offsets + b);
         const uint32_t mine = sub < nr ? gld(counts + r0 + sub) : 0u;
+        // the first 128 labels are read before the block's total is known
+        // (when the temp region holds C >= 128 words; always at the default
+        // slot sizes): the label reads overlap the offset reads instead of
+        // waiting behind them
+        const uint32_t *src = temp + b * (uint64_t)C;
+        uint32_t v0[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) v0[k] = C >= 128 ? gld(src + sub + 16 * k) : 0u;
         uint32_t x = mine;
 #pragma unroll
         for (uint32_t d = 1; d < 16; d <<= 1) {
@@ -1657,13 +1668,12 @@ __global__ __launch_bounds__(256) void k_compact_blocks(const uint32_t *__restri
         if (sub < nr) gst(offsets + r0 + sub, base + (x - mine));
         if (sub == 0 && r0 + nr == n) gst(offsets + n, base + total);
         if (total > C) continue;
-        const uint32_t *src = temp + b * (uint64_t)C;
         for (uint32_t i0 = 0; i0 < total; i0 += 128) {
             uint32_t v[8];
 #pragma unroll
             for (uint32_t k = 0; k < 8; ++k) {
                 const uint32_t i = i0 + sub + 16 * k;
-                v[k] = i < total ? lmap(gld(src + i)) : 0u;
+                v[k] = i < total ? lmap(i0 || C < 128 ? gld(src + i) : v0[k]) : 0u;
             }
 #pragma unroll
             for (uint32_t k = 0; k < 8; ++k) {
@@ -2202,6 +2212,18 @@ static int run_get_rows_p2w(Ctx &c, const RowblockKernel &kr, const uint64_t *d_
     MBRWT_HIP(hipGetLastError());
     if (c.timing) MBRWT_HIP(hipEventRecord(c.ev1, s));
     MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_block_offsets, nb + 1, s));
+    // the compaction is queued right behind the scan, before the host learns
+    // the total (one synchronisation per call, after it; the kernel checks
+    // the capacity itself)
+    const uint32_t map_lds = kr.final_columns ? 0u : label_map_lds(c);
+    // one 16-lane group per rowblock and no grid-stride rounds: with 8192
+    // workgroups each wave walked ~15 rowblocks through two dependent memory
+    // latencies each
+    const uint64_t g = std::min<uint64_t>((nb + 15) / 16, 1u << 20);
+    hipLaunchKernelGGL(k_compact_blocks, dim3((unsigned)g), dim3(256), map_lds * 4, s, d_counts, d_block_offsets, p.temp,
+                       C, d_offsets, d_cols, n, kr.final_columns ? nullptr : (const uint32_t *)c.d_label_map, map_lds,
+                       cap);
+    MBRWT_HIP(hipGetLastError());
     MBRWT_HIP(hipMemcpyAsync(c.d_scalars, d_block_offsets + nb, sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
     MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     MBRWT_HIP(hipStreamSynchronize(s));
@@ -2225,11 +2247,6 @@ static int run_get_rows_p2w(Ctx &c, const RowblockKernel &kr, const uint64_t *d_
         set_error("cols_cap too small");
         return MBRWT_ERR_CAPACITY;
     }
-    const uint32_t map_lds = kr.final_columns ? 0u : label_map_lds(c);
-    const uint64_t g = std::min<uint64_t>((nb + 15) / 16, 8192);
-    hipLaunchKernelGGL(k_compact_blocks, dim3((unsigned)g), dim3(256), map_lds * 4, s, d_counts, d_block_offsets, p.temp,
-                       C, d_offsets, d_cols, n, kr.final_columns ? nullptr : (const uint32_t *)c.d_label_map, map_lds);
-    MBRWT_HIP(hipGetLastError());
     if (ovf) {
         TravParams q = base_params(c);
         q.rows = d_rows;
