@@ -1632,6 +1632,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_ptw(P2wParams p) {
 // prefix) and a contiguous copy of the block's labels, each lane's (up to 8)
 // label reads issued before its stores.  Overflowing blocks (> C labels) are
 // left to the direct pass.
+template <bool BIG>
 __global__ __launch_bounds__(256) void k_compact_blocks(const uint32_t *__restrict__ counts,
                                                         const uint64_t *__restrict__ block_offsets,
                                                         const uint32_t *__restrict__ temp, uint32_t C,
@@ -1668,17 +1669,27 @@ __global__ __launch_bounds__(256) void k_compact_blocks(const uint32_t *__restri
         if (sub < nr) gst(offsets + r0 + sub, base + (x - mine));
         if (sub == 0 && r0 + nr == n) gst(offsets + n, base + total);
         if (total > C) continue;
-        for (uint32_t i0 = 0; i0 < total; i0 += 128) {
-            uint32_t v[8];
 #pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) {
+        for (uint32_t k = 0; k < 8; ++k) {  // the first 128 labels
+            const uint32_t i = sub + 16 * k;
+            if (i < total) gst(cols + base + i, lmap(C < 128 ? gld(src + i) : v0[k]));
+        }
+        // the rest, U labels per lane and round, every lane's reads issued
+        // before its stores: U = 32 for large rows (BIG: e.g. 120 labels per
+        // row at the RefSeq shape, 2.7 -> 2.1 ms per 10 M rows), 8 otherwise
+        // (32 registers cost occupancy: 0.146 -> 0.201 ms at 8 labels per row)
+        constexpr uint32_t U = BIG ? 32 : 8;
+        for (uint32_t i0 = 128; i0 < total; i0 += 16 * U) {
+            uint32_t v[U];
+#pragma unroll
+            for (uint32_t k = 0; k < U; ++k) {
                 const uint32_t i = i0 + sub + 16 * k;
-                v[k] = i < total ? lmap(i0 || C < 128 ? gld(src + i) : v0[k]) : 0u;
+                v[k] = i < total ? gld(src + i) : 0u;
             }
 #pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) {
+            for (uint32_t k = 0; k < U; ++k) {
                 const uint32_t i = i0 + sub + 16 * k;
-                if (i < total) gst(cols + base + i, v[k]);
+                if (i < total) gst(cols + base + i, lmap(v[k]));
             }
         }
     }
@@ -2220,7 +2231,9 @@ static int run_get_rows_p2w(Ctx &c, const RowblockKernel &kr, const uint64_t *d_
     // workgroups each wave walked ~15 rowblocks through two dependent memory
     // latencies each
     const uint64_t g = std::min<uint64_t>((nb + 15) / 16, 1u << 20);
-    hipLaunchKernelGGL(k_compact_blocks, dim3((unsigned)g), dim3(256), map_lds * 4, s, d_counts, d_block_offsets, p.temp,
+    const bool big = c.tree.num_rows && (double)c.tree.num_relations > 32.0 * (double)c.tree.num_rows;
+    hipLaunchKernelGGL(big ? k_compact_blocks<true> : k_compact_blocks<false>, dim3((unsigned)g), dim3(256), map_lds * 4,
+                       s, d_counts, d_block_offsets, p.temp,
                        C, d_offsets, d_cols, n, kr.final_columns ? nullptr : (const uint32_t *)c.d_label_map, map_lds,
                        cap);
     MBRWT_HIP(hipGetLastError());
@@ -2356,7 +2369,7 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
     {
         const uint32_t map_lds = label_map_lds(c);
         if (fn.fast) {  // chunk-packed output (k_traverse_fast2)
-            const uint64_t g = std::min<uint64_t>(((n + 7) / 8 + 31) / 32, 8192);
+            const uint64_t g = std::min<uint64_t>(((n + 7) / 8 + 31) / 32, 1u << 20);  // no grid-stride rounds
             hipLaunchKernelGGL(k_compact_chunks, dim3((unsigned)g), dim3(256), map_lds * 4, s, d_counts, d_chunk_offsets, p.temp,
                                K, d_offsets, d_cols, n, (const uint32_t *)c.d_label_map, map_lds);
         } else {
