@@ -188,6 +188,10 @@ struct Routed {
 
 static int route(Ctx &c, const uint64_t *d_rows, uint64_t n, Routed &r, hipStream_t s) {
     const uint32_t K = (uint32_t)c.shards.size();
+    if (n > 0x7FFFFFF0ull) {  // u32 batch indices, int item counts in hipCUB
+        set_error("batch larger than 2^31 rows");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
     int rc;
     // keys | sorted keys | iota | perm (u32 each)
     if ((rc = ensure(c.ws_sh_keys, 4 * n * sizeof(uint32_t)))) return rc;
