@@ -287,6 +287,12 @@ struct Ctx {
     double timing_ms = 0;
     uint64_t timing_launches = 0;
     int grid_cache = 0;
+    // launch geometry of the last rowblock kernel (query.hip): the occupancy
+    // query and the LDS attribute are host calls paid once, not per batch
+    const void *rb_fn = nullptr;
+    size_t rb_lds = 0;
+    uint32_t rb_threads = 0;
+    int rb_blocks = 0;  // resident workgroups on the device
 
     // Row shards (rows >= 2^32; DESIGN.md §4 "Rows >= 2^32"): a BRWT restricted
     // to a row range is again a BRWT, so a context over more rows than one

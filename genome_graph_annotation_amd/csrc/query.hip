@@ -2204,17 +2204,22 @@ static int run_get_rows_p2w(Ctx &c, const RowblockKernel &kr, const uint64_t *d_
 
     const size_t lds = kr.lds;
     const uint32_t threads = 64 * kr.wpb;
-    if (lds > 65536)
-        MBRWT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds));
-    int dev_cus = 0, per_cu = 0;
-    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kfn), threads, lds) !=
-            hipSuccess ||
-        per_cu <= 0)
-        per_cu = 1;
-    const uint64_t grid = std::max<uint64_t>(
-        1, std::min<uint64_t>((nb + kr.wpb - 1) / kr.wpb, (uint64_t)std::max(1, dev_cus) * per_cu));
+    if (c.rb_fn != reinterpret_cast<const void *>(kfn) || c.rb_lds != lds || c.rb_threads != threads) {
+        if (lds > 65536)
+            MBRWT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kfn),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        int dev_cus = 0, per_cu = 0;
+        (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kfn), threads, lds) !=
+                hipSuccess ||
+            per_cu <= 0)
+            per_cu = 1;
+        c.rb_fn = reinterpret_cast<const void *>(kfn);
+        c.rb_lds = lds;
+        c.rb_threads = threads;
+        c.rb_blocks = std::max(1, dev_cus) * per_cu;
+    }
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((nb + kr.wpb - 1) / kr.wpb, (uint64_t)c.rb_blocks));
 
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
     MBRWT_HIP(hipMemsetAsync(d_block_counts + nb, 0, sizeof(uint32_t), s));
