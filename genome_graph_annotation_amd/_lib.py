@@ -25,6 +25,15 @@ MBRWT_OPT_TIMING = 1
 MBRWT_OPT_SLOT_LABELS = 2
 MBRWT_OPT_KERNEL = 4
 
+MBRWT_BUILD_LAYOUT = 1
+MBRWT_LAYOUT_AUTO = 0
+MBRWT_LAYOUT_NODES = 1
+MBRWT_LAYOUT_ROWS = 2
+MBRWT_LAYOUT_BOTH = 3
+LAYOUTS = {"auto": MBRWT_LAYOUT_AUTO, "nodes": MBRWT_LAYOUT_NODES, "rows": MBRWT_LAYOUT_ROWS,
+           "both": MBRWT_LAYOUT_BOTH}
+LAYOUT_NAMES = {1: "nodes", 2: "rows", 3: "both"}
+
 u64p = C.POINTER(C.c_uint64)
 u32p = C.POINTER(C.c_uint32)
 u8p = C.POINTER(C.c_uint8)
@@ -111,6 +120,9 @@ SIGNATURES = {
     "mbrwt_pack_ids_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]),
     "mbrwt_unpack_ids_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]),
     "mbrwt_destroy": (None, [C.c_void_p]),
+    "mbrwt_set_build_option": (C.c_int, [C.c_int, C.c_int64]),
+    "mbrwt_layout": (C.c_int, [C.c_void_p]),
+    "mbrwt_rows_stats": (C.c_int, [C.c_void_p, u64p]),
     "mbrwt_tree_parse": (C.c_int, [u8p, C.c_uint64, u64p, C.POINTER(C.c_void_p)]),
     "mbrwt_tree_serialize": (C.c_int, [C.POINTER(TreeDesc), u8p, C.c_uint64, u64p]),
     "mbrwt_tree_export": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),

@@ -9,6 +9,7 @@ torch tensors only as plumbing for device memory and streams.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 
 import numpy as np
@@ -133,6 +134,21 @@ def serialize_tree(tree) -> bytes:
     return buf[: need.value].tobytes()
 
 
+@contextlib.contextmanager
+def build_layout(layout):
+    """Device layout of the contexts created inside the block (None: the
+    library default; 'nodes', 'rows', 'both' -- include/mbrwt.h)."""
+    if layout is None:
+        yield
+        return
+    lib = L.lib()
+    L.check(lib.mbrwt_set_build_option(L.MBRWT_BUILD_LAYOUT, L.LAYOUTS[layout]), "mbrwt_set_build_option")
+    try:
+        yield
+    finally:
+        lib.mbrwt_set_build_option(L.MBRWT_BUILD_LAYOUT, 0)
+
+
 class BRWTDevice:
     """A BRWT held in HBM; every query runs the HIP traversal kernels."""
 
@@ -142,7 +158,7 @@ class BRWTDevice:
 
     # -- construction -------------------------------------------------------
     @classmethod
-    def from_tree(cls, tree, device=0, relax_max_arity=0):
+    def from_tree(cls, tree, device=0, relax_max_arity=0, layout=None):
         """`tree`: BFS description (keys as include/mbrwt.h mbrwt_tree_desc:
         num_rows, num_columns, num_children, first_child, leaf_column,
         vec_size, words = list of uint64 arrays).  relax_max_arity > 1 runs
@@ -150,23 +166,25 @@ class BRWTDevice:
         lib = L.lib()
         d, keep = tree_desc(tree)
         h = C.c_void_p()
-        if relax_max_arity:
-            L.check(lib.mbrwt_create_relaxed(C.byref(d), int(relax_max_arity), device, C.byref(h)),
-                    "mbrwt_create_relaxed")
-        else:
-            L.check(lib.mbrwt_create(C.byref(d), device, C.byref(h)), "mbrwt_create")
+        with build_layout(layout):
+            if relax_max_arity:
+                L.check(lib.mbrwt_create_relaxed(C.byref(d), int(relax_max_arity), device, C.byref(h)),
+                        "mbrwt_create_relaxed")
+            else:
+                L.check(lib.mbrwt_create(C.byref(d), device, C.byref(h)), "mbrwt_create")
         return cls(h)
 
     @classmethod
-    def synthetic(cls, num_rows, num_columns, density, arity=8, seed=42, device=0):
+    def synthetic(cls, num_rows, num_columns, density, arity=8, seed=42, device=0, layout=None):
         lib = L.lib()
         d = L.SynthDesc(num_rows, num_columns, float(density), arity, seed)
         h = C.c_void_p()
-        L.check(lib.mbrwt_create_synthetic(C.byref(d), device, C.byref(h)), "mbrwt_create_synthetic")
+        with build_layout(layout):
+            L.check(lib.mbrwt_create_synthetic(C.byref(d), device, C.byref(h)), "mbrwt_create_synthetic")
         return cls(h)
 
     @classmethod
-    def synthetic_shaped(cls, num_rows, shape, density, seed=42, device=0):
+    def synthetic_shaped(cls, num_rows, shape, density, seed=42, device=0, layout=None):
         """The synthetic law over a given tree shape (mbrwt_create_synthetic_shaped):
         `shape` = dict with num_children, first_child, leaf_column (BFS), e.g.
         the export of a greedy + relaxed tree."""
@@ -178,12 +196,13 @@ class BRWTDevice:
         d = L.SynthDesc(num_rows, m, float(density), 0, seed)
         sd = L.ShapeDesc(len(nc), _p(nc, C.c_uint32), _p(fc, C.c_uint32), _p(lc, C.c_uint32))
         h = C.c_void_p()
-        L.check(lib.mbrwt_create_synthetic_shaped(C.byref(d), C.byref(sd), device, C.byref(h)),
-                "mbrwt_create_synthetic_shaped")
+        with build_layout(layout):
+            L.check(lib.mbrwt_create_synthetic_shaped(C.byref(d), C.byref(sd), device, C.byref(h)),
+                    "mbrwt_create_synthetic_shaped")
         return cls(h)
 
     @classmethod
-    def from_columns(cls, columns, num_rows, arity=2, device=0, relax_max_arity=0):
+    def from_columns(cls, columns, num_rows, arity=2, device=0, relax_max_arity=0, layout=None):
         """BRWTBottomUpBuilder::build with the basic partitioner on the device
         (include/mbrwt.h mbrwt_create_from_columns).  `columns`: a sequence of
         uint64 arrays (ceil(num_rows/64) LSB-first words each), or a 2-D
@@ -199,19 +218,21 @@ class BRWTDevice:
             ptrs[j] = c.ctypes.data_as(L.u64p)
         d = L.ColumnsDesc(num_rows, len(cols), ptrs, arity)
         h = C.c_void_p()
-        if relax_max_arity:
-            L.check(lib.mbrwt_create_from_columns_relaxed(C.byref(d), int(relax_max_arity), device, C.byref(h)),
-                    "mbrwt_create_from_columns_relaxed")
-        else:
-            L.check(lib.mbrwt_create_from_columns(C.byref(d), device, C.byref(h)), "mbrwt_create_from_columns")
+        with build_layout(layout):
+            if relax_max_arity:
+                L.check(lib.mbrwt_create_from_columns_relaxed(C.byref(d), int(relax_max_arity), device,
+                                                              C.byref(h)), "mbrwt_create_from_columns_relaxed")
+            else:
+                L.check(lib.mbrwt_create_from_columns(C.byref(d), device, C.byref(h)), "mbrwt_create_from_columns")
         return cls(h)
 
     @classmethod
-    def load(cls, data: bytes, device=0):
+    def load(cls, data: bytes, device=0, layout=None):
         """BRWT::load of a reference BRWT stream into HBM (mbrwt_load)."""
         buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, dtype=np.uint8)
         h = C.c_void_p()
-        L.check(L.lib().mbrwt_load(_p(buf, C.c_uint8), len(data), None, device, C.byref(h)), "mbrwt_load")
+        with build_layout(layout):
+            L.check(L.lib().mbrwt_load(_p(buf, C.c_uint8), len(data), None, device, C.byref(h)), "mbrwt_load")
         return cls(h)
 
     def export(self):
@@ -255,6 +276,19 @@ class BRWTDevice:
 
     def device_bytes(self):
         return L.lib().mbrwt_device_bytes(self._h)
+
+    def layout(self):
+        """'nodes', 'rows' or 'both' (include/mbrwt.h "device layout")."""
+        return L.LAYOUT_NAMES.get(L.lib().mbrwt_layout(self._h), "?")
+
+    def rows_stats(self):
+        """The row-record image (mbrwt_rows_stats) as a dict, None without one."""
+        out = (C.c_uint64 * 8)()
+        if L.lib().mbrwt_rows_stats(self._h, out) != L.MBRWT_OK:
+            return None
+        keys = ("block_bytes", "rows_per_block", "blocks_bytes", "spill_bytes", "record_bytes", "spilled_rows",
+                "long_rows", "height")
+        return dict(zip(keys, [int(v) for v in out]))
 
     # -- host-buffer queries --------------------------------------------------
     def get_rows(self, rows):

@@ -561,6 +561,10 @@ int mbrwt_tree_export(mbrwt_ctx *ctx, mbrwt_tree **out) {
     try {
         MBRWT_HIP(hipSetDevice(c.device));
         auto t = std::make_unique<mbrwt_tree>();
+        if (c.nodes_freed) {
+            set_error("export needs the node image (context built with layout rows)");
+            return MBRWT_ERR_UNSUPPORTED;
+        }
         if (c.shards.empty()) {
             const int rc = export_tree(c, *t);
             if (rc) return rc;

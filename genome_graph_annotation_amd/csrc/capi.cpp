@@ -2,6 +2,7 @@
 // Never throws across the ABI; every failure is an MBRWT_* status plus a
 // thread-local message (mbrwt_last_error_message).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -69,6 +70,7 @@ static void release(Ctx *c) {
     for (Ctx *sc : c->shards) release(sc);
     (void)hipSetDevice(c->device);
     free_tree(c->tree);
+    free_rows(c->rows);
     for (Workspace *w : {&c->ws_temp, &c->ws_counts, &c->ws_ovf, &c->ws_scan, &c->ws_rows, &c->ws_out, &c->ws_sort,
                          &c->ws_cls_off, &c->ws_cls_cols, &c->ws_sh_keys, &c->ws_sh_local, &c->ws_sh_cnt,
                          &c->ws_sh_sort, &c->ws_sh_tmp})
@@ -89,8 +91,16 @@ static void release(Ctx *c) {
     delete c;
 }
 
+static int make_rows(Ctx &c, int layout);
+static int resolve_layout() {
+    const int l = build_layout();
+    return l == LAYOUT_AUTO ? LAYOUT_NODES : l;
+}
+
+// layout_hook: give the finished context the thread's build layout (row
+// records, make_rows); off for the sub-contexts of sharded / ranged builds
 template <class Build>
-static int create_common(int device, mbrwt_ctx **out, Build &&build) {
+static int create_common(int device, mbrwt_ctx **out, Build &&build, bool layout_hook = true) {
     if (!out) {
         set_error("null output pointer");
         return MBRWT_ERR_INVALID;
@@ -115,6 +125,7 @@ static int create_common(int device, mbrwt_ctx **out, Build &&build) {
     }
     if (!rc) rc = build(*c);
     if (!rc) rc = upload_tables(*c);
+    if (!rc && layout_hook) rc = make_rows(*c, resolve_layout());
     if (rc) {
         release(c);
         return rc;
@@ -138,7 +149,7 @@ static int create_sharded(int device, uint64_t num_rows, uint64_t num_columns, u
         for (uint64_t a = 0; a < num_rows; a += R) {
             const uint64_t b = std::min(num_rows, a + R);
             mbrwt_ctx *sub = nullptr;
-            const int rc = create_common(device, &sub, [&](Ctx &sc) { return build_shard(sc, a, b); });
+            const int rc = create_common(device, &sub, [&](Ctx &sc) { return build_shard(sc, a, b); }, false);
             if (rc) return rc;
             Ctx *sc = C(sub);
             c.shards.push_back(sc);
@@ -150,10 +161,123 @@ static int create_sharded(int device, uint64_t num_rows, uint64_t num_columns, u
     });
 }
 
+// Row records (rows.hip) of a finished node context -- unsharded, or over
+// its row shards -- for layouts ROWS and BOTH; ROWS then drops the node
+// images (and the shards).
+constexpr uint64_t kRowsAlign = 360360;  // a multiple of every S <= 15
+// rows per range of a ranged build: 1,073,512,440 (MBRWT_ROWS_RANGE=<rows>,
+// rounded up to a multiple of kRowsAlign, forces smaller ranges: a test hook)
+static uint64_t rows_range_rows() {
+    if (const char *e = std::getenv("MBRWT_ROWS_RANGE")) {
+        const unsigned long long v = std::strtoull(e, nullptr, 10);
+        if (v) return (v + kRowsAlign - 1) / kRowsAlign * kRowsAlign;
+    }
+    return 2979ull * kRowsAlign;
+}
+
+static void drop_nodes(Ctx &c) {
+    for (Ctx *sc : c.shards) release(sc);
+    c.shards.clear();
+    free_tree(c.tree);
+    for (DevNode &d : c.tree.nodes) d.base = 0;
+    c.tree.image_bytes = 0;
+    c.nodes_freed = true;
+}
+
+static int make_rows(Ctx &c, int layout) {
+    if (layout != LAYOUT_ROWS && layout != LAYOUT_BOTH) return MBRWT_OK;
+    if (c.nodes_freed) return MBRWT_OK;
+    if (c.tree.num_rows == 0) {
+        set_error("row records of a matrix without rows");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
+    const bool sharded = !c.shards.empty();
+    RowsBuild *rb = rows_build_begin(c, c.tree.num_rows, sharded ? c.shard_rows : kRowsAlign);
+    if (!rb) return MBRWT_ERR_NOMEM;
+    int rc = MBRWT_OK;
+    if (!sharded) {
+        rc = rows_build_range(rb, c, 0);
+    } else {
+        for (size_t k = 0; k < c.shards.size() && !rc; ++k) {
+            rc = rows_build_range(rb, *c.shards[k], (uint64_t)k * c.shard_rows);
+            if (!rc) (void)hipSetDevice(c.device);
+        }
+    }
+    if (rc) {
+        rows_build_abort(rb);
+        return rc;
+    }
+    if ((rc = rows_build_finish(rb))) return rc;
+    if (layout == LAYOUT_ROWS) drop_nodes(c);
+    return MBRWT_OK;
+}
+
+// Layout ROWS over more than kRowsRangeRows rows: the node image of one
+// range of rows at a time (build_range(ctx, a, b), an ordinary context over
+// rows [a, b)) is turned into its rows' records and released, so the device
+// holds the records plus ONE range's node image.
+template <class BuildRange>
+static int create_rows_ranged(int device, uint64_t num_rows, uint64_t num_columns, mbrwt_ctx **out,
+                              BuildRange &&build_range) {
+    return create_common(
+        device, out,
+        [&](Ctx &c) {
+            c.tree.num_rows = num_rows;
+            c.tree.num_columns = num_columns;
+            const uint64_t R = rows_range_rows();
+            RowsBuild *rb = rows_build_begin(c, num_rows, R);
+            if (!rb) return (int)MBRWT_ERR_NOMEM;
+            for (uint64_t a = 0; a < num_rows; a += R) {
+                const uint64_t b = std::min(num_rows, a + R);
+                mbrwt_ctx *sub = nullptr;
+                int rc = create_common(device, &sub, [&](Ctx &sc) { return build_range(sc, a, b); }, false);
+                if (!rc) rc = rows_build_range(rb, *C(sub), a);
+                if (!rc) {
+                    const Tree &st = C(sub)->tree;
+                    c.tree.num_relations += st.num_relations;
+                    c.tree.num_nodes = st.num_nodes;
+                    c.tree.max_arity = st.max_arity;
+                    if (a == 0) {  // the shape (host tables only; no image)
+                        c.tree.nodes = st.nodes;
+                        c.tree.label_perm = st.label_perm;
+                        c.tree.folded = st.folded;
+                    }
+                }
+                if (sub) release(C(sub));
+                (void)hipSetDevice(device);
+                if (rc) {
+                    rows_build_abort(rb);
+                    return rc;
+                }
+            }
+            const int rc = rows_build_finish(rb);
+            if (rc) return rc;
+            for (DevNode &d : c.tree.nodes) d.base = 0;
+            c.nodes_freed = true;
+            return (int)MBRWT_OK;
+        },
+        false);
+}
+
 // the synthetic law over row shards: shard k draws node u's masks at the
 // positions after those of shards 0..k-1 (SynthShard, synth.hip)
 static int create_synthetic_any(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape, int device,
                                 mbrwt_ctx **out) {
+    if (resolve_layout() == LAYOUT_ROWS && desc.num_rows > rows_range_rows() && desc.num_columns) {
+        SynthShard st;
+        std::vector<uint64_t> lens;
+        st.len_out = &lens;
+        return create_rows_ranged(device, desc.num_rows, desc.num_columns, out, [&](Ctx &sc, uint64_t a, uint64_t b) {
+            mbrwt_synth_desc d = desc;
+            d.num_rows = b - a;
+            st.row0 = a;
+            const int rc = build_synthetic(d, shape, device, sc.tree, sc.stream, &st);
+            if (rc) return rc;
+            if (st.pos0.size() < lens.size()) st.pos0.resize(lens.size(), 0);
+            for (size_t u = 0; u < lens.size(); ++u) st.pos0[u] += lens[u];
+            return (int)MBRWT_OK;
+        });
+    }
     const uint64_t R = desc.num_columns ? shard_rows_for(desc.num_rows) : 0;
     if (!R)
         return create_common(device, out,
@@ -185,6 +309,13 @@ int mbrwt_create(const mbrwt_tree_desc *desc, int device, mbrwt_ctx **out) {
         return MBRWT_ERR_INVALID;
     }
     try {
+        if (resolve_layout() == LAYOUT_ROWS && desc->num_rows > rows_range_rows() && desc->num_nodes)
+            return create_rows_ranged(device, desc->num_rows, desc->num_columns, out,
+                                      [&](Ctx &sc, uint64_t a, uint64_t b) {
+                                          SlicedDesc sd;
+                                          const int rc = slice_desc(*desc, a, b, sd);
+                                          return rc ? rc : build_from_desc(sd.desc, device, sc.tree);
+                                      });
         const uint64_t R = desc->num_nodes ? shard_rows_for(desc->num_rows) : 0;
         if (R)  // rows >= 2^32: every shard is built from the description's slice
             return create_sharded(device, desc->num_rows, desc->num_columns, R, out,
@@ -296,7 +427,40 @@ uint64_t mbrwt_num_rows(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.num_ro
 uint64_t mbrwt_num_columns(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.num_columns : 0; }
 uint64_t mbrwt_num_relations(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.num_relations : 0; }
 uint64_t mbrwt_num_nodes(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.num_nodes : 0; }
-uint64_t mbrwt_device_bytes(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.image_bytes : 0; }
+uint64_t mbrwt_device_bytes(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.image_bytes + C(ctx)->rows.bytes : 0; }
+
+int mbrwt_set_build_option(int option, int64_t value) {
+    if (option != MBRWT_BUILD_LAYOUT || value < MBRWT_LAYOUT_AUTO || value > MBRWT_LAYOUT_BOTH) {
+        set_error("unknown build option or value");
+        return MBRWT_ERR_INVALID;
+    }
+    set_build_layout((int)value);
+    return MBRWT_OK;
+}
+
+int mbrwt_layout(const mbrwt_ctx *ctx) {
+    if (!ctx) return 0;
+    const Ctx &c = *C(ctx);
+    return !c.rows.ready ? MBRWT_LAYOUT_NODES : c.nodes_freed ? MBRWT_LAYOUT_ROWS : MBRWT_LAYOUT_BOTH;
+}
+
+int mbrwt_rows_stats(const mbrwt_ctx *ctx, uint64_t out[8]) {
+    if (!ctx || !out) return MBRWT_ERR_INVALID;
+    const RowsImage &r = C(ctx)->rows;
+    if (!r.ready) {
+        set_error("context has no row records");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
+    out[0] = r.B;
+    out[1] = r.S;
+    out[2] = r.num_blocks * r.B;
+    out[3] = r.spill_bytes;
+    out[4] = r.record_bytes;
+    out[5] = r.spilled_rows;
+    out[6] = r.long_rows;
+    out[7] = r.height;
+    return MBRWT_OK;
+}
 int mbrwt_device(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->device : -1; }
 uint64_t mbrwt_num_shards(const mbrwt_ctx *ctx) { return ctx ? std::max<uint64_t>(1, C(ctx)->shards.size()) : 0; }
 

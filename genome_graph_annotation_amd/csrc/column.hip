@@ -172,6 +172,7 @@ unsigned grid_of(uint64_t n, unsigned per) {
 
 int run_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap, uint64_t *rows_needed,
                    hipStream_t s) {
+    if (c.nodes_freed) return rows_get_column(c, column, d_rows, rows_cap, rows_needed, s);
     if (!c.shards.empty()) return sharded_get_column(c, column, d_rows, rows_cap, rows_needed, s);
     const Tree &t = c.tree;
     if (column >= t.num_columns) {

@@ -223,6 +223,51 @@ struct Workspace {
     size_t bytes = 0;
 };
 
+// ROW RECORDS (rows.hip, DESIGN.md §4 "Row records"): the BRWT's index bits
+// regrouped by row.  Every bit of node u's index column at position j belongs
+// to exactly one row (the row whose descent reaches u at j, BRWT.cpp:30,43),
+// so the bits of a row's whole descent -- the children mask of every internal
+// node the row reaches, in DFS pre-order (BRWT.cpp:45-51) -- form the row's
+// RECORD, and the records of all rows hold exactly the index bits of the tree.
+// get_row(r) is then ONE block read and a walk of the record; the rank1
+// remaps of the reference are resolved when the image is built.
+//   block (B = 64 or 128 bytes, S rows [b S, b S + S)):
+//     bytes 0..S-1  e[t] = offset of row t's entry (< B) | 0x80 if spilled
+//     inline entry  [u8 label count < 255][masks: 1 byte for arity <= 8, 2 bytes LE for <= 16]
+//     spilled entry [u8 min(count, 255)][u32 LE spill offset in 16-byte units]
+//   spill entry (16-byte aligned): [u32 count][u32 mask bytes][masks]
+// An empty row (no label) is the one-byte entry [0].
+// RWT table (the walk's tree, staged in LDS): u32 words
+//   [0] nI internal nodes, [1] nE entries, [2] height (internal levels), [3] 0,
+//   nI x {first entry [0:16) | arity [16:24)}      (local index 0 = the BRWT root)
+//   nE u16 entries: bit 15 = leaf + global column in bits 0..14, else the local index
+constexpr uint32_t kRowsMaxArity = 16;
+constexpr uint32_t kRowsMaxHeight = 16;
+constexpr uint32_t kRowsMaxTableWords = 8192;
+enum : int { LAYOUT_AUTO = 0, LAYOUT_NODES = 1, LAYOUT_ROWS = 2, LAYOUT_BOTH = 3 };
+struct RowsImage {
+    bool ready = false;
+    uint32_t B = 64, S = 1;         // block bytes, rows per block
+    uint64_t magic = 0;             // row / S = umulhi(row, magic) (S > 1)
+    uint64_t num_blocks = 0;
+    uint8_t *blocks = nullptr;      // num_blocks * B
+    uint8_t *spill = nullptr;       // spill entries (+ B bytes of padding)
+    uint64_t spill_cap = 0;         // bytes allocated
+    unsigned long long *d_spill_used = nullptr;  // 16-byte units taken (build)
+    std::vector<uint32_t> table;    // RWT table
+    uint32_t *d_table = nullptr;
+    uint32_t height = 0;
+    uint64_t bytes = 0;             // blocks + spill used
+    // build statistics
+    uint64_t spilled_rows = 0, long_rows = 0, record_bytes = 0, spill_bytes = 0;
+};
+// the RWT table of a finished node tree; false (and an empty table) when the
+// shape is outside the row-record kernels' limits
+bool build_rwt_table(const Tree &tree, std::vector<uint32_t> &table, uint32_t &height);
+// the thread's build layout (mbrwt_set_build_option, else MBRWT_LAYOUT)
+int build_layout();
+void set_build_layout(int layout);
+
 // Cross-stream ordering of a context's workspaces.  A *_device call returns
 // with work still queued on the caller's stream that reads the context's
 // workspaces (compaction, classify pass 1, ...); a later call on ANOTHER
@@ -302,7 +347,33 @@ struct Ctx {
     std::vector<Ctx *> shards;
     uint64_t shard_rows = 0;
     Workspace ws_sh_keys, ws_sh_local, ws_sh_cnt, ws_sh_sort, ws_sh_tmp;
+
+    // Row records (rows.hip): with `rows.ready` every row query runs on them;
+    // `nodes_freed` = the per-node images were dropped after the records were
+    // built (layout ROWS), so only the row-record kernels can answer
+    RowsImage rows;
+    bool nodes_freed = false;
 };
+
+// row-record image construction (rows.hip): records of the rows [row0, row0 +
+// range.num_rows) written from the node image of `range` (a context over
+// those rows, tables uploaded); the first range measured decides the block
+// size and rows per block (S must divide `align`: every later range starts at
+// a multiple of it).  finish_rows uploads the table and marks the image ready.
+struct RowsBuild;
+RowsBuild *rows_build_begin(Ctx &top, uint64_t num_rows, uint64_t align);
+int rows_build_range(RowsBuild *rb, Ctx &range, uint64_t row0);
+int rows_build_finish(RowsBuild *rb);  // frees rb
+void rows_build_abort(RowsBuild *rb);
+void free_rows(RowsImage &r);
+// row-record queries (rows.hip)
+int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
+                  uint64_t *needed, hipStream_t s);
+int rows_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n, uint8_t *d_out, hipStream_t s);
+int rows_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts, hipStream_t s);
+int rows_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s);
+int rows_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap, uint64_t *rows_needed,
+                    hipStream_t s);
 
 // status helpers ---------------------------------------------------------
 void set_error(const std::string &msg);

@@ -2142,6 +2142,8 @@ static PtwPick ptw_kernel(const Ctx &c) {
 }
 
 const char *traverse_kernel_name(const Ctx &c) {
+    if (c.rows.ready && c.kernel_variant == 0) return "k_traverse_rows";
+    if (c.nodes_freed) return "";
     if (ptw_kernel(c).fn) return "k_traverse_ptw";
     if (p2w_kernel(c)) return "k_traverse_p2w";
     const Trav t = pick_traverse<MODE_SLOTS>(c);
@@ -2280,6 +2282,11 @@ static int run_get_rows_p2w(Ctx &c, const RowblockKernel &kr, const uint64_t *d_
 
 int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
                  uint64_t *needed, hipStream_t s) {
+    if (c.rows.ready && c.kernel_variant == 0) return rows_get_rows(c, d_rows, n, d_offsets, d_cols, cap, needed, s);
+    if (c.nodes_freed) {
+        set_error("kernel variant needs the node image (layout rows)");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
     if (!c.shards.empty()) return sharded_get_rows(c, d_rows, n, d_offsets, d_cols, cap, needed, s);
     if (n == 0) {
         MBRWT_HIP(hipMemsetAsync(d_offsets, 0, sizeof(uint64_t), s));
@@ -2396,6 +2403,7 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
 }
 
 int run_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s) {
+    if (c.nodes_freed) return rows_count_work(c, d_rows, n, visits, labels, s);
     if (!c.shards.empty()) return sharded_count_work(c, d_rows, n, visits, labels, s);
     if (c.tree.nodes.empty()) return n ? MBRWT_ERR_RANGE : MBRWT_OK;
     const Trav fn = pick_traverse<MODE_WORK>(c);
@@ -2415,6 +2423,7 @@ int run_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits,
 }
 
 int run_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts, hipStream_t s) {
+    if (c.rows.ready) return rows_count_labels(c, d_rows, n, d_counts, s);
     if (!c.shards.empty()) return sharded_count_labels(c, d_rows, n, d_counts, s);
     if (c.tree.num_columns) MBRWT_HIP(hipMemsetAsync(d_counts, 0, c.tree.num_columns * sizeof(uint64_t), s));
     if (c.tree.nodes.empty()) return n ? MBRWT_ERR_RANGE : MBRWT_OK;
@@ -2434,6 +2443,7 @@ int run_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_cou
 }
 
 int run_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n, uint8_t *d_out, hipStream_t s) {
+    if (c.nodes_freed) return rows_get_batch(c, d_rows, d_cols, n, d_out, s);
     if (!c.shards.empty()) return sharded_get_batch(c, d_rows, d_cols, n, d_out, s);
     if (n == 0) return MBRWT_OK;
     if (c.tree.nodes.empty()) return MBRWT_ERR_RANGE;

@@ -1,0 +1,1309 @@
+// rows.hip -- ROW RECORDS: the BRWT's index bits regrouped by row, and the
+// row-record query kernels (layout in mbrwt_internal.hpp "ROW RECORDS",
+// DESIGN.md §4/§5).
+//
+// The reference answers get_row(r) (BRWT.cpp:26-53) by a descent that reads,
+// at every internal node u it reaches, the index bits of u's children at
+// j = rank1(u, i) - 1 (BRWT.cpp:30, :43).  Those bits -- the children mask of
+// u at the row's position -- belong to row r alone: every bit of every index
+// column is reached by exactly one row.  A row's RECORD is the masks of its
+// descent in DFS pre-order (the order the reference visits them, BRWT.cpp:
+// 45-51), so the records of all rows are a permutation of the tree's index
+// bits, and get_row is one 64- or 128-byte block read plus a walk of the
+// record over the tree's shape (the RWT table, in LDS): the rank1 remaps are
+// resolved once, when the image is built from a node image (any of its
+// layouts), not per query.
+//
+// Build (rows_build_*): per range of rows, one thread per row walks the node
+// image and measures its record (k_rows_measure); the first range decides
+// the block size B and rows per block S from the records' sizes
+// (k_rows_plan: spilled rows and spill bytes per candidate); one thread per
+// block then writes the block and its spill entries (k_rows_write).
+//
+// Query (rows_get_rows): k_traverse_rows -- one wave per tile of 64 query
+// rows: the 64 blocks are read as coalesced 16-byte quarters (one request per
+// block) into LDS, a wave scan of the records' label counts places every
+// row's labels, the 64 lanes walk their records in lockstep over the RWT table
+// writing u16 labels into an LDS stage, which leaves as full-line stores into
+// the tile's temp region; one scan over the tile totals and k_compact_tiles
+// (u16 -> the caller's u32 CSR) follow.  Tiles with more labels than their
+// region, or with a record longer than a block, go to k_rows_direct.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "device_access.hpp"
+#include "mbrwt_internal.hpp"
+#include "pack_block.hpp"
+
+namespace mbrwt {
+
+// ------------------------------------------------------------------------
+// layout selection
+// ------------------------------------------------------------------------
+static thread_local int g_build_layout = -1;  // -1: MBRWT_LAYOUT or auto
+
+int build_layout() {
+    if (g_build_layout >= 0) return g_build_layout;
+    const char *e = std::getenv("MBRWT_LAYOUT");
+    if (!e || !*e) return LAYOUT_AUTO;
+    if (!std::strcmp(e, "nodes")) return LAYOUT_NODES;
+    if (!std::strcmp(e, "rows")) return LAYOUT_ROWS;
+    if (!std::strcmp(e, "both")) return LAYOUT_BOTH;
+    return LAYOUT_AUTO;
+}
+
+void set_build_layout(int layout) { g_build_layout = layout; }
+
+// ------------------------------------------------------------------------
+// RWT table
+// ------------------------------------------------------------------------
+bool build_rwt_table(const Tree &tree, std::vector<uint32_t> &table, uint32_t &height) {
+    table.clear();
+    height = 0;
+    const auto &N = tree.nodes;
+    if (N.size() < 2) return false;
+    // the logical root: the folded root's children hang off dnode 0
+    const bool folded = tree.folded;
+    const uint32_t root = folded ? 0u : 1u;
+    if (!folded && N[0].arity != 1) return false;
+    if (N[root].kind == KIND_LEAF || N[root].arity == 0) return false;  // one-column tree
+    auto column_of = [&](const DevNode &d) { return tree.label_perm.empty() ? d.label : tree.label_perm[d.label]; };
+    std::vector<uint32_t> inner{root}, level{1};
+    std::vector<uint32_t> local(N.size(), UINT32_MAX);
+    local[root] = 0;
+    for (size_t h = 0; h < inner.size(); ++h) {
+        const DevNode &v = N[inner[h]];
+        height = std::max(height, level[h]);
+        if (v.arity == 0 || v.arity > kRowsMaxArity) return false;
+        for (uint32_t c = 0; c < v.arity; ++c) {
+            const uint32_t w = v.first_child + c;
+            if (w >= N.size()) return false;
+            if (N[w].kind != KIND_LEAF) {
+                local[w] = (uint32_t)inner.size();
+                inner.push_back(w);
+                level.push_back(level[h] + 1);
+            }
+        }
+    }
+    if (height > kRowsMaxHeight || inner.size() >= 0x8000) return false;
+    std::vector<uint32_t> nodew(inner.size());
+    std::vector<uint16_t> ent;
+    for (size_t i = 0; i < inner.size(); ++i) {
+        const DevNode &v = N[inner[i]];
+        if (ent.size() + v.arity > 0xFFFF) return false;
+        nodew[i] = (uint32_t)ent.size() | ((uint32_t)v.arity << 16);
+        for (uint32_t c = 0; c < v.arity; ++c) {
+            const DevNode &w = N[v.first_child + c];
+            if (w.kind == KIND_LEAF) {
+                const uint32_t col = column_of(w);
+                if (col >= 0x8000) return false;
+                ent.push_back((uint16_t)(0x8000u | col));
+            } else {
+                ent.push_back((uint16_t)local[v.first_child + c]);
+            }
+        }
+    }
+    const size_t nI = inner.size(), nE = ent.size();
+    const size_t words = 4 + nI + (nE + 1) / 2;
+    if (words > kRowsMaxTableWords) return false;
+    table.assign(words, 0);
+    table[0] = (uint32_t)nI;
+    table[1] = (uint32_t)nE;
+    table[2] = height;
+    std::memcpy(&table[4], nodew.data(), nI * 4);
+    std::memcpy(&table[4 + nI], ent.data(), nE * 2);
+    return true;
+}
+
+namespace {
+
+// ------------------------------------------------------------------------
+// build: the masks of a row's descent over a node image
+// ------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rec_mask_bytes(uint32_t arity) { return arity <= 8 ? 1u : 2u; }
+
+constexpr int kEmitFrames = 34;  // PLANE levels on a path (<= 32) + the super-root
+
+// the children bits of PLANE node image `nd` at position j
+__device__ __forceinline__ uint32_t plane_mask(const DevNode &nd, uint32_t j) {
+    const uint64_t blk = nd.base + (uint64_t)(j >> 5) * nd.stride;
+    const uint32_t t = j & 31;
+    uint32_t m = 0;
+    for (uint32_t c = 0; c < nd.arity; ++c) m |= ((gld_at<uint2>(blk + 8u * c).y >> t) & 1u) << c;
+    return m;
+}
+__device__ __forceinline__ uint32_t mask_at(const DevNode &nd, uint32_t j) {
+    if (nd.kind == KIND_MASK8) return gld_at<uint8_t>(nd.base + j);
+    if (nd.kind == KIND_MASK16) return gld_at<uint16_t>(nd.base + 2ull * j);
+    if (nd.kind == KIND_MASK32) return gld_at<uint32_t>(nd.base + 4ull * j);
+    return (uint32_t)gld_at<uint64_t>(nd.base + 8ull * j);  // (arity <= 16 here)
+}
+
+// Row r of a node image: emit(mask, arity) for the children mask of every
+// internal node its descent reaches, in DFS pre-order -- the row's record.
+// Returns the row's labels (set leaves), or ~0u when the descent is deeper
+// than the walker's frames.  Handles every node kind of the images
+// (PLANE, MASK*, PACK, PACK2, PACKT, a folded root).
+template <class Emit>
+__device__ uint32_t emit_row_masks(const DevNode *__restrict__ nodes, bool folded, uint32_t r, Emit emit) {
+    uint32_t fv[kEmitFrames], fj[kEmitFrames], fm[kEmitFrames];
+    int sp = 0;
+    uint32_t leaves = 0;
+    bool bad = false;
+    auto push = [&](uint32_t v, uint32_t j, uint32_t m) {
+        if (sp == kEmitFrames) {
+            bad = true;
+            return;
+        }
+        fv[sp] = v;
+        fj[sp] = j;
+        fm[sp] = m;
+        ++sp;
+    };
+    // internal dnode v at position j of its image (v's index bit is set there)
+    auto visit = [&](uint32_t v, uint32_t j) {
+        const DevNode nd = gld(nodes + v);
+        const uint32_t a = nd.arity;
+        if (nd.kind == KIND_PLANE) {
+            const uint32_t m = plane_mask(nd, j);
+            emit(m, a);
+            push(v, j, m);
+        } else if (nd.kind >= KIND_MASK8 && nd.kind <= KIND_MASK64) {
+            const uint32_t m = mask_at(nd, j);
+            emit(m, a);
+            leaves += (uint32_t)__builtin_popcount(m);
+        } else if (nd.kind == KIND_PACK) {  // children: MASK8 nodes inline
+            PackBlock pb;
+            pb.load(nd.base, j);
+            const uint32_t t = j % kPackSpan;
+            uint32_t m = 0;
+            for (uint32_t k = 0; k < a; ++k) m |= ((pb.bits(k) >> t) & 1u) << k;
+            emit(m, a);
+            uint32_t o = 0;
+            for (uint32_t k = 0; k < a; ++k) {
+                const uint32_t bk = pb.bits(k);
+                if ((bk >> t) & 1u) {
+                    const uint32_t cm = pb.mask(o + (uint32_t)__builtin_popcount(bk & ((1u << t) - 1u)));
+                    emit(cm, gld(nodes + nd.first_child + k).arity);
+                    leaves += (uint32_t)__builtin_popcount(cm);
+                }
+                o += (uint32_t)__builtin_popcount(bk);
+            }
+        } else if (nd.kind == KIND_PACK2) {  // the 3-level subtree inline (level order in the block)
+            Pack2Block pb;
+            pb.load(nd.base, j, nd.stride);
+            const uint32_t s = pb.start(j % nd.stride);
+            const uint32_t m2 = pb.byte(s);
+            emit(m2, a);
+            uint32_t o1 = s + 1, o2 = s + 1 + (uint32_t)__builtin_popcount(m2);
+            for (uint32_t A = 0; A < a; ++A) {
+                if (!((m2 >> A) & 1u)) continue;
+                const DevNode na = gld(nodes + nd.first_child + A);
+                const uint32_t m1 = pb.byte(o1++);
+                emit(m1, na.arity);
+                for (uint32_t x = m1; x; x &= x - 1) {
+                    const DevNode nb = gld(nodes + na.first_child + (uint32_t)__builtin_ctz(x));
+                    const uint32_t lm = pb.byte(o2++);
+                    emit(lm, nb.arity);
+                    leaves += (uint32_t)__builtin_popcount(lm);
+                }
+            }
+        } else if (nd.kind == KIND_PACKT) {  // the whole subtree inline, already DFS pre-order
+            Pack2Block pb;
+            pb.load(nd.base, j, nd.stride);
+            uint32_t o = pb.start(j % nd.stride) + 1;  // (the record's label count)
+            uint32_t m = pb.byte(o++);
+            if (a > 8) m |= pb.byte(o++) << 8;
+            emit(m, a);
+            constexpr int D = (int)kPacktMaxDepth;
+            uint32_t sfc[D], sm[D];
+            int tp = 0;
+            sfc[0] = nd.first_child;
+            sm[0] = m;
+            tp = 1;
+            while (tp) {
+                const int t = tp - 1;
+                if (!sm[t]) {
+                    --tp;
+                    continue;
+                }
+                const uint32_t c = (uint32_t)__builtin_ctz(sm[t]);
+                sm[t] &= sm[t] - 1;
+                const DevNode w = gld(nodes + sfc[t] + c);
+                if (w.kind == KIND_LEAF) {
+                    ++leaves;
+                    continue;
+                }
+                uint32_t mw = pb.byte(o++);
+                if (w.arity > 8) mw |= pb.byte(o++) << 8;
+                emit(mw, w.arity);
+                if (tp == D) {
+                    bad = true;
+                    return;
+                }
+                sfc[tp] = w.first_child;
+                sm[tp] = mw;
+                ++tp;
+            }
+        } else {
+            bad = true;
+        }
+    };
+    const DevNode d0 = gld(nodes);
+    if (folded) {  // dnode 0 holds the root's children over rows
+        const uint32_t m = d0.kind == KIND_PLANE ? plane_mask(d0, r) : mask_at(d0, r);
+        if (!m) return 0;
+        emit(m, d0.arity);
+        if (d0.kind == KIND_PLANE) push(0, r, m);
+        else leaves += (uint32_t)__builtin_popcount(m);
+    } else {  // dnode 0: the root's own column
+        uint32_t bit, jr = 0;
+        if (d0.kind == KIND_PLANE) {
+            const uint2 rb = gld_at<uint2>(d0.base + (uint64_t)(r >> 5) * d0.stride);
+            bit = (rb.y >> (r & 31)) & 1u;
+            jr = rb.x + (uint32_t)__builtin_popcount(rb.y & ((1u << (r & 31)) - 1u));
+        } else {
+            bit = mask_at(d0, r) & 1u;
+        }
+        if (!bit) return 0;
+        if (gld(nodes + d0.first_child).kind == KIND_LEAF) return 1;
+        visit(d0.first_child, jr);
+    }
+    while (sp > 0 && !bad) {
+        const int t = sp - 1;
+        if (!fm[t]) {
+            --sp;
+            continue;
+        }
+        const uint32_t c = (uint32_t)__builtin_ctz(fm[t]);
+        fm[t] &= fm[t] - 1;
+        const DevNode nu = gld(nodes + fv[t]);
+        const uint32_t w = nu.first_child + c;
+        if (gld(nodes + w).kind == KIND_LEAF) {
+            ++leaves;
+            continue;
+        }
+        const uint32_t j = fj[t];
+        const uint2 rb = gld_at<uint2>(nu.base + (uint64_t)(j >> 5) * nu.stride + 8u * c);
+        visit(w, rb.x + (uint32_t)__builtin_popcount(rb.y & ((1u << (j & 31)) - 1u)));
+    }
+    return bad ? ~0u : leaves;
+}
+
+// per row of a range: record size (1 + mask bytes, < 2^15) | 0x8000 when the
+// row has >= 255 labels (its count does not fit the inline byte)
+__global__ __launch_bounds__(256) void k_rows_measure(const DevNode *nodes, uint32_t folded, uint64_t n, uint16_t *sz,
+                                                      unsigned long long *acc) {
+    unsigned long long lab = 0, bytes = 0, bad = 0;
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gs) {
+        uint32_t b = 1;
+        const uint32_t L = emit_row_masks(nodes, folded != 0, (uint32_t)r, [&](uint32_t, uint32_t a) { b += rec_mask_bytes(a); });
+        if (L == ~0u || b >= 0x8000) {
+            ++bad;
+            sz[r] = 0x7FFF;
+            continue;
+        }
+        sz[r] = (uint16_t)(b | (L >= 255 ? 0x8000u : 0u));
+        lab += L;
+        bytes += b;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        lab += __shfl_down(lab, off);
+        bytes += __shfl_down(bytes, off);
+        bad += __shfl_down(bad, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (lab) atomicAdd(acc + 0, lab);
+        if (bytes) atomicAdd(acc + 1, bytes);
+        if (bad) atomicAdd(acc + 2, bad);
+    }
+}
+
+// which rows of a block spill: rows with >= 255 labels always; then, while
+// the block overflows, the largest inline record (a spilled entry takes 5
+// bytes in the block)
+__device__ __forceinline__ uint32_t block_spills(const uint32_t *s, uint32_t nrows, uint32_t S, uint32_t B) {
+    uint32_t used = S, spilled = 0;
+    for (uint32_t t = 0; t < nrows; ++t) {
+        if (s[t] & 0x8000u) {
+            spilled |= 1u << t;
+            used += 5;
+        } else {
+            used += s[t];
+        }
+    }
+    while (used > B) {
+        uint32_t best = 0, bt = 0;
+        for (uint32_t t = 0; t < nrows; ++t)
+            if (!((spilled >> t) & 1u) && s[t] >= best) {
+                best = s[t];
+                bt = t;
+            }
+        spilled |= 1u << bt;
+        used = used - best + 5;
+    }
+    return spilled;
+}
+__device__ __forceinline__ uint32_t spill_units(uint32_t s) { return (8 + ((s & 0x7FFFu) - 1) + 15) / 16; }
+
+// a candidate (B, S): spilled rows, spill units, rows whose spill entry is
+// longer than a block (direct pass)
+__global__ __launch_bounds__(256) void k_rows_plan(const uint16_t *sz, uint64_t n, uint32_t B, uint32_t S,
+                                                   unsigned long long *acc) {
+    unsigned long long sp = 0, units = 0, lng = 0;
+    const uint64_t nb = (n + S - 1) / S;
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gs) {
+        uint32_t s[16];
+        const uint32_t nr = (uint32_t)std::min<uint64_t>(S, n - b * S);
+        for (uint32_t t = 0; t < nr; ++t) s[t] = gld(sz + b * S + t);
+        const uint32_t m = block_spills(s, nr, S, B);
+        for (uint32_t t = 0; t < nr; ++t)
+            if ((m >> t) & 1u) {
+                ++sp;
+                units += spill_units(s[t]);
+                lng += (8 + (s[t] & 0x7FFFu) - 1 > B) ? 1u : 0u;
+            }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        sp += __shfl_down(sp, off);
+        units += __shfl_down(units, off);
+        lng += __shfl_down(lng, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (sp) atomicAdd(acc + 0, sp);
+        if (units) atomicAdd(acc + 1, units);
+        if (lng) atomicAdd(acc + 2, lng);
+    }
+}
+
+// one thread per block of the range: header, inline records, spill entries
+__global__ __launch_bounds__(256) void k_rows_write(const DevNode *nodes, uint32_t folded, uint64_t nr_range,
+                                                    const uint16_t *sz, uint32_t B, uint32_t S, uint8_t *blocks,
+                                                    uint8_t *spill, unsigned long long *spill_used) {
+    const uint64_t nb = (nr_range + S - 1) / S;
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gs) {
+        uint32_t s[16];
+        const uint32_t nr = (uint32_t)std::min<uint64_t>(S, nr_range - b * S);
+        for (uint32_t t = 0; t < nr; ++t) s[t] = gld(sz + b * S + t);
+        const uint32_t m = block_spills(s, nr, S, B);
+        uint8_t *blk = blocks + b * B;
+        uint32_t o = S;
+        for (uint32_t t = 0; t < nr; ++t) {
+            const uint32_t r = (uint32_t)(b * S + t);
+            if ((m >> t) & 1u) {
+                const uint64_t idx = atomicAdd(spill_used, (unsigned long long)spill_units(s[t]));
+                uint8_t *se = spill + idx * 16;
+                uint32_t w = 8;
+                const uint32_t L = emit_row_masks(nodes, folded != 0, r, [&](uint32_t mk, uint32_t a) {
+                    se[w++] = (uint8_t)mk;
+                    if (a > 8) se[w++] = (uint8_t)(mk >> 8);
+                });
+                *reinterpret_cast<uint32_t *>(se) = L;
+                *reinterpret_cast<uint32_t *>(se + 4) = w - 8;
+                blk[t] = (uint8_t)(o | 0x80u);
+                blk[o] = (uint8_t)std::min<uint32_t>(L, 255);
+                for (uint32_t k = 0; k < 4; ++k) blk[o + 1 + k] = (uint8_t)(idx >> (8 * k));
+                o += 5;
+            } else {
+                blk[t] = (uint8_t)o;
+                uint32_t w = o + 1;
+                const uint32_t L = emit_row_masks(nodes, folded != 0, r, [&](uint32_t mk, uint32_t a) {
+                    blk[w++] = (uint8_t)mk;
+                    if (a > 8) blk[w++] = (uint8_t)(mk >> 8);
+                });
+                blk[o] = (uint8_t)L;
+                o = w;
+            }
+        }
+    }
+}
+
+int build_grid(uint64_t items) { return (int)std::max<uint64_t>(1, std::min<uint64_t>((items + 255) / 256, 65536)); }
+
+}  // namespace
+
+// ------------------------------------------------------------------------
+// build driver
+// ------------------------------------------------------------------------
+struct RowsBuild {
+    Ctx *top = nullptr;
+    uint64_t n = 0, align = 1;
+    bool decided = false;
+    RowsImage img;
+    unsigned long long *d_acc = nullptr;  // [0..3] measure, [4..7] plan
+    uint16_t *d_sz = nullptr;
+    uint64_t sz_cap = 0;
+    hipStream_t s = nullptr;
+};
+
+void free_rows(RowsImage &r) {
+    if (r.blocks) (void)hipFree(r.blocks);
+    if (r.spill) (void)hipFree(r.spill);
+    if (r.d_spill_used) (void)hipFree(r.d_spill_used);
+    if (r.d_table) (void)hipFree(r.d_table);
+    r = RowsImage();
+}
+
+RowsBuild *rows_build_begin(Ctx &top, uint64_t num_rows, uint64_t align) {
+    RowsBuild *rb = new (std::nothrow) RowsBuild();
+    if (!rb) return nullptr;
+    rb->top = &top;
+    rb->n = num_rows;
+    rb->align = std::max<uint64_t>(1, align);
+    rb->s = top.stream;
+    if (hipMalloc(&rb->d_acc, 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&rb->img.d_spill_used, sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(rb->img.d_spill_used, 0, sizeof(unsigned long long)) != hipSuccess) {
+        rows_build_abort(rb);
+        return nullptr;
+    }
+    return rb;
+}
+
+void rows_build_abort(RowsBuild *rb) {
+    if (!rb) return;
+    if (rb->d_acc) (void)hipFree(rb->d_acc);
+    if (rb->d_sz) (void)hipFree(rb->d_sz);
+    free_rows(rb->img);
+    delete rb;
+}
+
+static int read_acc(RowsBuild &rb, unsigned long long *h, int k) {
+    MBRWT_HIP(hipMemcpyAsync(h, rb.d_acc, k * sizeof(unsigned long long), hipMemcpyDeviceToHost, rb.s));
+    MBRWT_HIP(hipStreamSynchronize(rb.s));
+    return MBRWT_OK;
+}
+
+// grow the spill area to hold `bytes` (entries keep their offsets: copy)
+static int ensure_spill(RowsBuild &rb, uint64_t bytes) {
+    RowsImage &im = rb.img;
+    const uint64_t need = bytes + im.B + 256;
+    if (need <= im.spill_cap) return MBRWT_OK;
+    const uint64_t cap = std::max<uint64_t>(need, im.spill_cap + im.spill_cap / 4);
+    uint8_t *p = nullptr;
+    MBRWT_HIP(hipMalloc(&p, cap));
+    MBRWT_HIP(hipMemsetAsync(p, 0, cap, rb.s));
+    if (im.spill) {
+        MBRWT_HIP(hipMemcpyAsync(p, im.spill, im.spill_cap, hipMemcpyDeviceToDevice, rb.s));
+        MBRWT_HIP(hipStreamSynchronize(rb.s));
+        MBRWT_HIP(hipFree(im.spill));
+    }
+    im.spill = p;
+    im.spill_cap = cap;
+    return MBRWT_OK;
+}
+
+int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
+    if (!rbp) return MBRWT_ERR_NOMEM;
+    RowsBuild &rb = *rbp;
+    RowsImage &im = rb.img;
+    const uint64_t nr = range.tree.num_rows;
+    if (!nr) return MBRWT_OK;
+    if (!range.d_nodes || range.tree.nodes.empty()) {
+        set_error("row records need a node image");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
+    if (row0 % rb.align) {
+        set_error("row-record range not aligned");
+        return MBRWT_ERR_INVALID;
+    }
+    if (im.table.empty()) {
+        if (!build_rwt_table(range.tree, im.table, im.height)) {
+            set_error("tree shape outside the row-record limits (arity <= 16, columns < 2^15, height <= 16)");
+            return MBRWT_ERR_UNSUPPORTED;
+        }
+    }
+    if (nr > rb.sz_cap) {
+        if (rb.d_sz) MBRWT_HIP(hipFree(rb.d_sz));
+        rb.d_sz = nullptr;
+        MBRWT_HIP(hipMalloc(&rb.d_sz, nr * sizeof(uint16_t)));
+        rb.sz_cap = nr;
+    }
+    unsigned long long h[8];
+    MBRWT_HIP(hipMemsetAsync(rb.d_acc, 0, 8 * sizeof(unsigned long long), rb.s));
+    hipLaunchKernelGGL(k_rows_measure, dim3(build_grid(nr)), dim3(256), 0, rb.s, range.d_nodes,
+                       range.tree.folded ? 1u : 0u, nr, rb.d_sz, rb.d_acc);
+    MBRWT_HIP(hipGetLastError());
+    if (int rc = read_acc(rb, h, 3)) return rc;
+    if (h[2]) {
+        set_error("row record deeper than the build walker supports");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
+    if (h[0] != range.tree.num_relations) {
+        set_error("row records: label count differs from the node image");
+        return MBRWT_ERR_DEVICE;
+    }
+    im.record_bytes += h[1];
+    auto plan = [&](uint32_t B, uint32_t S, unsigned long long out[3]) -> int {
+        MBRWT_HIP(hipMemsetAsync(rb.d_acc, 0, 8 * sizeof(unsigned long long), rb.s));
+        hipLaunchKernelGGL(k_rows_plan, dim3(build_grid((nr + S - 1) / S)), dim3(256), 0, rb.s, rb.d_sz, nr, B, S,
+                           rb.d_acc);
+        MBRWT_HIP(hipGetLastError());
+        return read_acc(rb, out, 3);
+    };
+    if (!rb.decided) {
+        // (B, S): the fewest requests per row -- one block read plus one per
+        // spilled row, a 128-byte block costing kCost128 of a 64-byte one
+        // (measured ceilings), a record longer than a block a
+        // direct-pass row (x50) -- among the images that fit the device,
+        // then the smallest within 2 % of that
+        constexpr double kCost128 = 1.05;  // random 128-byte reads: 52.6 vs 53.7 G/s (profiles/r03/v01_probe_sweep.json)
+        size_t free_b = 0, total_b = 0;
+        MBRWT_HIP(hipMemGetInfo(&free_b, &total_b));
+        const double budget = (double)free_b - 4.0 * (1ull << 30);
+        struct Cand {
+            uint32_t B, S;
+            double t, mem;
+        };
+        std::vector<Cand> cands;
+        const double scale = (double)rb.n / (double)nr;
+        for (uint32_t B : {64u, 128u})
+            for (uint32_t S = 1; S <= (B == 64 ? 8u : 15u); ++S) {
+                if (rb.align % S) continue;
+                unsigned long long o[3];
+                if (int rc = plan(B, S, o)) return rc;
+                const double fs = (double)o[0] / nr, fl = (double)o[2] / nr;
+                Cand c{B, S, (B == 128 ? kCost128 : 1.0) * (1.0 + fs + 50.0 * fl),
+                       (double)((rb.n + S - 1) / S) * B + (double)o[1] * 16.0 * scale};
+                cands.push_back(c);
+            }
+        double tmin = 1e300;
+        for (const Cand &c : cands)
+            if (c.mem <= budget) tmin = std::min(tmin, c.t);
+        if (tmin == 1e300) {
+            set_error("row-record image does not fit the device");
+            return MBRWT_ERR_NOMEM;
+        }
+        const Cand *best = nullptr;
+        for (const Cand &c : cands)
+            if (c.mem <= budget && c.t <= tmin * 1.02 && (!best || c.mem < best->mem)) best = &c;
+        im.B = best->B;
+        im.S = best->S;
+        if (const char *e = std::getenv("MBRWT_ROWS_BS")) {  // A/B switch: "B,S"
+            unsigned Bv = 0, Sv = 0;
+            if (std::sscanf(e, "%u,%u", &Bv, &Sv) == 2 && (Bv == 64 || Bv == 128) && Sv >= 1 &&
+                Sv <= (Bv == 64 ? 8u : 15u) && rb.align % Sv == 0) {
+                im.B = Bv;
+                im.S = Sv;
+            }
+        }
+        // row / S = umulhi(row, floor(2^64 / S) + 1), exact for rows < 2^59 and S <= 16
+        im.magic = im.S > 1 ? ((uint64_t)((((unsigned __int128)1) << 64) / im.S) + 1) : 0;
+        im.num_blocks = (rb.n + im.S - 1) / im.S;
+        MBRWT_HIP(hipMalloc(&im.blocks, im.num_blocks * im.B));
+        MBRWT_HIP(hipMemsetAsync(im.blocks, 0, im.num_blocks * im.B, rb.s));
+        rb.decided = true;
+    }
+    unsigned long long o[3];
+    if (int rc = plan(im.B, im.S, o)) return rc;
+    unsigned long long used = 0;
+    MBRWT_HIP(hipMemcpyAsync(&used, im.d_spill_used, sizeof(used), hipMemcpyDeviceToHost, rb.s));
+    MBRWT_HIP(hipStreamSynchronize(rb.s));
+    // the first range sizes the area for the whole image (extrapolated)
+    const double scale = row0 == 0 ? (double)rb.n / (double)nr : 1.0;
+    if (int rc = ensure_spill(rb, (uint64_t)(used * 16 + o[1] * 16 * scale * (row0 == 0 ? 1.05 : 1.0)) + 16 * o[1]))
+        return rc;
+    im.spilled_rows += o[0];
+    im.long_rows += o[2];
+    im.spill_bytes += o[1] * 16;
+    hipLaunchKernelGGL(k_rows_write, dim3(build_grid((nr + im.S - 1) / im.S)), dim3(256), 0, rb.s, range.d_nodes,
+                       range.tree.folded ? 1u : 0u, nr, rb.d_sz, im.B, im.S, im.blocks + (row0 / im.S) * im.B,
+                       im.spill, im.d_spill_used);
+    MBRWT_HIP(hipGetLastError());
+    MBRWT_HIP(hipStreamSynchronize(rb.s));
+    return MBRWT_OK;
+}
+
+int rows_build_finish(RowsBuild *rbp) {
+    if (!rbp) return MBRWT_ERR_NOMEM;
+    RowsBuild &rb = *rbp;
+    RowsImage &im = rb.img;
+    int rc = MBRWT_OK;
+    if (!rb.decided) {  // no rows
+        set_error("row records of an empty matrix");
+        rc = MBRWT_ERR_UNSUPPORTED;
+    }
+    if (!rc && (hipMalloc(&im.d_table, im.table.size() * 4) != hipSuccess ||
+                hipMemcpy(im.d_table, im.table.data(), im.table.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
+        rc = hip_fail(hipGetLastError(), "row-record table upload");
+    if (rc) {
+        rows_build_abort(rbp);
+        return rc;
+    }
+    if (!im.spill && ensure_spill(rb, 0)) {
+        rows_build_abort(rbp);
+        return MBRWT_ERR_NOMEM;
+    }
+    im.bytes = im.num_blocks * im.B + im.spill_bytes;
+    im.ready = true;
+    free_rows(rb.top->rows);
+    rb.top->rows = im;
+    rb.img = RowsImage();  // ownership moved
+    if (rb.d_acc) (void)hipFree(rb.d_acc);
+    if (rb.d_sz) (void)hipFree(rb.d_sz);
+    delete rbp;
+    return MBRWT_OK;
+}
+
+
+// ------------------------------------------------------------------------
+// queries
+// ------------------------------------------------------------------------
+namespace {
+
+struct RowsView {
+    uint64_t blocks, spill, magic, num_rows;
+    uint32_t B, S;
+};
+__device__ __forceinline__ uint64_t rows_block(uint64_t r, uint32_t S, uint64_t magic) {
+    return S == 1 ? r : __umul64hi(r, magic);
+}
+// the record of row r (< num_rows): address of its first mask byte, label count
+__device__ __forceinline__ void rows_locate(const RowsView &v, uint64_t r, uint64_t &masks, uint32_t &count) {
+    const uint64_t b = rows_block(r, v.S, v.magic);
+    const uint32_t t = (uint32_t)(r - b * v.S);
+    const uint64_t blk = v.blocks + b * v.B;
+    const uint32_t e = gld_at<uint8_t>(blk + t);
+    const uint32_t o = e & 0x7Fu;
+    if (e & 0x80u) {
+        uint32_t idx = 0;
+        for (uint32_t k = 0; k < 4; ++k) idx |= (uint32_t)gld_at<uint8_t>(blk + o + 1 + k) << (8 * k);
+        const uint64_t se = v.spill + (uint64_t)idx * 16;
+        count = gld_at<uint32_t>(se);
+        masks = se + 8;
+    } else {
+        count = gld_at<uint8_t>(blk + o);
+        masks = blk + o + 1;
+    }
+}
+
+// DFS walk of a record (masks from byte 0 of `byte`) over the RWT table:
+// leaf(column) per set leaf in pre-order (BRWT.cpp:45-51), inner(arity) per
+// mask read (the root's included).  One lane; false past kRowsMaxHeight.
+template <class ByteFn, class LeafFn, class InnerFn>
+__device__ bool rwt_walk(const uint32_t *ntab, const uint16_t *etab, ByteFn byte, LeafFn leaf, InnerFn inner) {
+    uint32_t o = 0;
+    uint32_t nw = ntab[0];
+    uint32_t a = (nw >> 16) & 0xFFu;
+    uint32_t m = byte(o++);
+    if (a > 8) m |= byte(o++) << 8;
+    inner(a);
+    uint32_t first = nw & 0xFFFFu;
+    uint32_t sf[kRowsMaxHeight], sm[kRowsMaxHeight];
+    int sp = 0;
+    while (true) {
+        if (!m) {
+            if (!sp) break;
+            --sp;
+            first = sf[sp];
+            m = sm[sp];
+            continue;
+        }
+        const uint32_t c = (uint32_t)__builtin_ctz(m);
+        m &= m - 1;
+        const uint32_t e = etab[first + c];
+        if (e & 0x8000u) {
+            leaf(e & 0x7FFFu);
+            continue;
+        }
+        nw = ntab[e];
+        a = (nw >> 16) & 0xFFu;
+        uint32_t mw = byte(o++);
+        if (a > 8) mw |= byte(o++) << 8;
+        inner(a);
+        if (m) {
+            if (sp == (int)kRowsMaxHeight) return false;
+            sf[sp] = first;
+            sm[sp] = m;
+            ++sp;
+        }
+        first = nw & 0xFFFFu;
+        m = mw;
+    }
+    return true;
+}
+
+struct RowsParams {
+    const uint64_t *rows;
+    uint64_t n;
+    uint64_t num_rows;
+    uint64_t blocks, spill, magic;
+    uint32_t S;
+    uint32_t table_words;
+    const uint32_t *table;
+    uint32_t C;                   // labels per tile region (multiple of 64)
+    uint8_t *temp;                // tiles x (128 + 2 C) bytes: u16 counts[64], u16 labels[C]
+    uint32_t *tile_counts;        // [tiles] labels (bit 31: the tile goes to the direct pass)
+    uint32_t *ovf_list;           // batch indices of the rows of direct tiles
+    unsigned long long *scalars;  // [1] direct rows, [2] error flags
+};
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The walk of every lane's record at once, in lockstep without per-lane
+// branches: each iteration takes one child of every lane's top frame (frame
+// = first entry | pending children << 16); a leaf stores its column into the
+// stage at the lane's next label position, an internal child reads its mask
+// (the record's next 1 or 2 bytes) and pushes the parent's frame if it has
+// children left; an emptied frame is popped.  MAXD >= the tree's height.
+template <int MAXD>
+__device__ __forceinline__ void rows_walk_wave(const AS_LDS uint8_t *pb, uint32_t o, bool live,
+                                               const AS_LDS uint32_t *ntab, const AS_LDS uint16_t *etab,
+                                               AS_LDS uint16_t *stage, uint32_t pos) {
+    const uint32_t nw = ntab[0];
+    const uint32_t w0 = ((nw >> 16) & 0xFFu) > 8 ? 1u : 0u;
+    const uint32_t m = (uint32_t)pb[o] | (w0 ? (uint32_t)pb[o + 1] << 8 : 0u);
+    o += 1 + w0;
+    uint32_t top = live ? ((nw & 0xFFFFu) | (m << 16)) : 0u;
+    uint32_t st[MAXD > 1 ? MAXD - 1 : 1];
+#pragma unroll
+    for (int k = 0; k < (MAXD > 1 ? MAXD - 1 : 1); ++k) st[k] = 0;
+    uint32_t sp = 0;
+    bool done = (top >> 16) == 0;
+    while (__any(!done)) {
+        const uint32_t mm = top >> 16;
+        const uint32_t c = (uint32_t)__builtin_ctz(mm | 0x10000u);
+        top &= ~(0x10000u << c);
+        const uint32_t e = etab[done ? 0u : (top & 0xFFFFu) + c];
+        const bool leaf = (e & 0x8000u) != 0;
+        if (!done && leaf) stage[pos] = (uint16_t)(e & 0x7FFFu);
+        pos += (!done && leaf) ? 1u : 0u;
+        const bool inner = !done && !leaf;
+        const uint32_t nw2 = ntab[inner ? e : 0u];
+        const uint32_t w2 = ((nw2 >> 16) & 0xFFu) > 8 ? 1u : 0u;
+        const uint32_t mw = (uint32_t)pb[o] | (w2 ? (uint32_t)pb[o + 1] << 8 : 0u);
+        o += inner ? 1u + w2 : 0u;
+        if constexpr (MAXD > 1) {
+            const bool push = inner && (top >> 16) != 0;
+#pragma unroll
+            for (int k = MAXD - 2; k > 0; --k) st[k] = push ? st[k - 1] : st[k];
+            st[0] = push ? top : st[0];
+            sp += push ? 1u : 0u;
+        }
+        top = inner ? ((nw2 & 0xFFFFu) | (mw << 16)) : top;
+        if constexpr (MAXD > 1) {
+            const bool pop = !done && (top >> 16) == 0 && sp > 0;  // (pushed frames are never empty)
+            top = pop ? st[0] : top;
+#pragma unroll
+            for (int k = 0; k < MAXD - 2; ++k) st[k] = pop ? st[k + 1] : st[k];
+            sp -= pop ? 1u : 0u;
+        }
+        done = done || (top >> 16) == 0;
+    }
+}
+
+// k_traverse_rows: one wave per tile of 64 query rows (file comment).
+// B: block bytes; MAXD: stack levels (>= height); WPB: waves per workgroup
+// (the RWT table is staged once per workgroup; the grid is persistent).
+template <int B, int MAXD, int WPB, bool NT>
+__global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows[];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_rows[i] = gld(p.table + i);
+    __syncthreads();
+    const AS_LDS uint32_t *tab = (const AS_LDS uint32_t *)lds_rows;
+    const uint32_t nI = __builtin_amdgcn_readfirstlane(tab[0]);
+    const AS_LDS uint32_t *ntab = tab + 4;
+    const AS_LDS uint16_t *etab = (const AS_LDS uint16_t *)(ntab + nI);
+    const uint32_t C = p.C;
+    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows + ((p.table_words + 3) & ~3u)) + wv * (64u * B + 2u * C);
+    AS_LDS uint8_t *mine = wb + lane * B;
+    AS_LDS uint16_t *stage = (AS_LDS uint16_t *)(wb + 64 * B);
+    constexpr uint32_t LPB = B / 16, RPI = 64 / LPB;
+    const uint64_t ntiles = (p.n + 63) / 64;
+    const uint64_t tstride = (uint64_t)gridDim.x * WPB;
+    const uint32_t S = p.S;
+    for (uint64_t t = (uint64_t)blockIdx.x * WPB + wv; t < ntiles; t += tstride) {
+        const uint64_t r0 = t * 64;
+        const uint32_t nr = (uint32_t)(p.n - r0 < 64 ? p.n - r0 : 64);
+        bool valid = false;
+        uint64_t row = 0;
+        if (lane < nr) {
+            row = gld(p.rows + r0 + lane);
+            valid = row < p.num_rows;
+            if (!valid) atomicOr(&p.scalars[2], 1ull);
+        }
+        const uint64_t b = valid ? rows_block(row, S, p.magic) : 0;
+        const uint32_t sub = (uint32_t)(row - b * S);
+        const uint64_t addr = p.blocks + b * B;
+        // the 64 blocks as coalesced quarters: load k brings rows RPI k ..
+        // RPI k + RPI - 1, lane L its 16 bytes L % LPB; LDS slot of row x = [x B, x B + B)
+        u32x4_t q[LPB];
+#pragma unroll
+        for (uint32_t k = 0; k < LPB; ++k) {
+            const int src = (int)(RPI * k + lane / LPB);
+            const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)addr, src, 64);
+            const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(addr >> 32), src, 64);
+            q[k] = gld_at_nt<u32x4_t, NT>((((uint64_t)hi << 32) | lo) + 16u * (lane % LPB));
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < LPB; ++k) ((AS_LDS u32x4_t *)(wb + 1024 * k))[lane] = q[k];
+        wave_sync();
+        uint32_t cnt = 0, o = 0;
+        bool spl = false;
+        if (valid) {
+            const uint32_t e = mine[sub];
+            o = e & 0x7Fu;
+            spl = (e & 0x80u) != 0;
+            cnt = mine[o];
+            ++o;
+        }
+        bool lng = false;
+        if (__any(spl)) {
+            // spilled rows: the entry (<= B bytes of it) replaces the block in
+            // the lane's own slot; masks from byte 8
+            if (spl) {
+                const uint32_t idx = (uint32_t)mine[o] | ((uint32_t)mine[o + 1] << 8) | ((uint32_t)mine[o + 2] << 16) |
+                                     ((uint32_t)mine[o + 3] << 24);
+                const uint64_t sa = p.spill + (uint64_t)idx * 16;
+                u32x4_t sq[LPB];
+#pragma unroll
+                for (uint32_t k = 0; k < LPB; ++k) sq[k] = gld_at<u32x4_t>(sa + 16u * k);
+#pragma unroll
+                for (uint32_t k = 0; k < LPB; ++k) ((AS_LDS u32x4_t *)mine)[k] = sq[k];
+                cnt = sq[0].x;
+                lng = 8 + sq[0].y > B;
+                o = 8;
+            }
+        }
+        uint32_t x = cnt;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+            if (lane >= d) x += y;
+        }
+        const uint32_t total = __builtin_amdgcn_readlane(x, 63);
+        const uint32_t pos = x - cnt;
+        const bool direct = total > C || __any(lng);
+        uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
+        if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
+        if (!direct) {
+            rows_walk_wave<MAXD>(mine, o, valid && cnt > 0, ntab, etab, stage, pos);
+            wave_sync();
+            const uint32_t nbytes = total * 2;
+            for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
+                gst(reinterpret_cast<u32x4_t *>(treg + 128 + q2), *(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2));
+        }
+        if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u));
+        if (direct) {
+            unsigned long long k0 = 0;
+            if (lane == 0) k0 = atomicAdd(&p.scalars[1], (unsigned long long)nr);
+            k0 = (unsigned long long)__shfl((long long)k0, 0, 64);
+            if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(r0 + lane));
+        }
+        wave_sync();  // the slots and the stage are reused
+    }
+}
+
+// tile regions -> CSR: one wave per tile (offsets by a wave scan of the
+// tile's counts, labels u16 -> u32, reads issued before the offset is known);
+// launched before the host knows the total: over the capacity it writes nothing
+__global__ __launch_bounds__(256) void k_compact_tiles(const uint8_t *__restrict__ temp, uint32_t C,
+                                                       const uint32_t *__restrict__ tile_counts,
+                                                       const uint64_t *__restrict__ tile_offsets,
+                                                       uint64_t *__restrict__ offsets, uint32_t *__restrict__ cols,
+                                                       uint64_t n, uint64_t cap) {
+    const uint64_t ntiles = (n + 63) / 64;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (t >= ntiles) return;
+    if (gld(tile_offsets + ntiles) > cap) return;
+    const uint64_t r0 = t * 64;
+    const uint32_t nr = (uint32_t)(n - r0 < 64 ? n - r0 : 64);
+    const uint8_t *treg = temp + t * (uint64_t)(128 + 2 * C);
+    const uint16_t *lab = reinterpret_cast<const uint16_t *>(treg + 128);
+    const uint32_t tc = gld(tile_counts + t);
+    const uint64_t base = gld(tile_offsets + t);
+    const uint32_t cnt = lane < nr ? (uint32_t)gld(reinterpret_cast<const uint16_t *>(treg) + lane) : 0u;
+    uint32_t v[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) v[k] = gld(lab + lane + 64 * k);  // (C >= 1024: inside the region)
+    uint32_t x = cnt;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane < nr) gst(offsets + r0 + lane, base + (x - cnt));
+    if (t == ntiles - 1 && lane == nr - 1) gst(offsets + n, base + x);
+    if (tc >> 31) return;  // direct tile: k_rows_direct writes its labels
+    const uint32_t total = tc;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t i = lane + 64 * k;
+        if (i < total) gst(cols + base + i, v[k]);
+    }
+    for (uint32_t i0 = 512; i0 < total; i0 += 512) {
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+            const uint32_t i = i0 + lane + 64 * k;
+            v[k] = i < total ? (uint32_t)gld(lab + i) : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+            const uint32_t i = i0 + lane + 64 * k;
+            if (i < total) gst(cols + base + i, v[k]);
+        }
+    }
+}
+
+// rows of direct tiles: one lane per row, its record walked from global
+// memory straight into the CSR
+__global__ __launch_bounds__(256) void k_rows_direct(RowsView v, const uint32_t *table, const uint64_t *rows,
+                                                     const uint32_t *list, uint64_t nlist,
+                                                     const uint64_t *offsets, uint32_t *cols,
+                                                     unsigned long long *scalars) {
+    const uint32_t *ntab = table + 4;
+    const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + table[0]);
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nlist; i += gs) {
+        const uint32_t bi = gld(list + i);
+        const uint64_t row = gld(rows + bi);
+        if (row >= v.num_rows) continue;
+        uint64_t masks;
+        uint32_t count;
+        rows_locate(v, row, masks, count);
+        if (!count) continue;
+        const uint64_t base = gld(offsets + bi);
+        uint32_t k = 0;
+        const bool ok = rwt_walk(
+            ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
+            [&](uint32_t col) { gst(cols + base + k++, col); }, [](uint32_t) {});
+        if (!ok) atomicOr(&scalars[2], 2ull);
+    }
+}
+
+// point queries: the column among the row's labels (BRWT::get, BRWT.cpp:9-24)
+__global__ __launch_bounds__(256) void k_rows_get(RowsView v, const uint32_t *table, const uint64_t *rows,
+                                                  const uint64_t *qcols, uint64_t n, uint64_t num_cols, uint8_t *out,
+                                                  unsigned long long *scalars) {
+    const uint32_t *ntab = table + 4;
+    const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + table[0]);
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
+        const uint64_t row = gld(rows + i), col = gld(qcols + i);
+        if (row >= v.num_rows || col >= num_cols) {
+            atomicOr(&scalars[2], 1ull);
+            gst(out + i, (uint8_t)0);
+            continue;
+        }
+        uint64_t masks;
+        uint32_t count;
+        rows_locate(v, row, masks, count);
+        uint32_t hit = 0;
+        if (count)
+            (void)rwt_walk(
+                ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
+                [&](uint32_t c) { hit |= c == col; }, [](uint32_t) {});
+        gst(out + i, (uint8_t)hit);
+    }
+}
+
+// count_labels (annotate_static.cpp:149-162) and the V / L accounting
+// (V = 1 + the arities of the internal nodes the descent
+// reaches, i.e. of the record's masks)
+template <bool WORK>
+__global__ __launch_bounds__(256) void k_rows_count(RowsView v, const uint32_t *table, const uint64_t *rows,
+                                                    uint64_t n, unsigned long long *counts,
+                                                    unsigned long long *scalars) {
+    const uint32_t *ntab = table + 4;
+    const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + table[0]);
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    unsigned long long vis = 0, lab = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
+        const uint64_t row = gld(rows + i);
+        if (row >= v.num_rows) {
+            atomicOr(&scalars[2], 1ull);
+            continue;
+        }
+        uint64_t masks;
+        uint32_t count;
+        rows_locate(v, row, masks, count);
+        vis += 1;
+        if (!count) continue;
+        (void)rwt_walk(
+            ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
+            [&](uint32_t c) {
+                if constexpr (WORK) ++lab;
+                else atomicAdd(counts + c, 1ull);
+            },
+            [&](uint32_t a) {
+                if constexpr (WORK) vis += a;
+            });
+    }
+    if constexpr (WORK) {
+        for (int off = 32; off > 0; off >>= 1) {
+            vis += __shfl_down(vis, off);
+            lab += __shfl_down(lab, off);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&scalars[3], vis);
+            atomicAdd(&scalars[4], lab);
+        }
+    }
+}
+
+// get_column over row records: every row whose record holds the column,
+// ascending (a select over the row ids; BRWT::get_column, BRWT.cpp:55-85)
+struct RowHasColumn {
+    RowsView v;
+    const uint32_t *table;
+    uint32_t col;
+    __device__ bool operator()(const uint64_t &row) const {
+        uint64_t masks;
+        uint32_t count;
+        rows_locate(v, row, masks, count);
+        if (!count) return false;
+        const uint32_t *ntab = table + 4;
+        const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + table[0]);
+        bool hit = false;
+        (void)rwt_walk(
+            ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
+            [&](uint32_t c) { hit |= c == col; }, [](uint32_t) {});
+        return hit;
+    }
+};
+struct HasColumnCount {
+    RowHasColumn f;
+    __device__ uint64_t operator()(const uint64_t &row) const { return f(row) ? 1u : 0u; }
+};
+
+RowsView view_of(const Ctx &c) {
+    RowsView v;
+    v.blocks = (uint64_t)(uintptr_t)c.rows.blocks;
+    v.spill = (uint64_t)(uintptr_t)c.rows.spill;
+    v.magic = c.rows.magic;
+    v.num_rows = c.tree.num_rows;
+    v.B = c.rows.B;
+    v.S = c.rows.S;
+    return v;
+}
+
+using RowsFn = void (*)(RowsParams);
+constexpr uint32_t kRowsWpb = 4;
+
+template <int B, bool NT>
+RowsFn rows_fn_d(uint32_t height) {
+    return height <= 4 ? k_traverse_rows<B, 4, kRowsWpb, NT>
+           : height <= 8 ? k_traverse_rows<B, 8, kRowsWpb, NT>
+                         : k_traverse_rows<B, 16, kRowsWpb, NT>;
+}
+RowsFn rows_fn(const RowsImage &im) {
+    const bool nt = im.bytes > (1ull << 30);
+    if (im.B == 64) return nt ? rows_fn_d<64, true>(im.height) : rows_fn_d<64, false>(im.height);
+    return nt ? rows_fn_d<128, true>(im.height) : rows_fn_d<128, false>(im.height);
+}
+
+// labels per tile region: room for the tile's mean + 8 sigma
+uint32_t rows_tile_labels(const Ctx &c) {
+    const double mean = c.tree.num_rows ? (double)c.tree.num_relations / (double)c.tree.num_rows : 0.0;
+    const double need = 64.0 * mean + 8.0 * std::sqrt(64.0 * mean + 1.0) + 64.0;
+    uint32_t C = 1024;
+    while (C < need && C < 4096) C <<= 1;
+    return C;
+}
+
+struct MaskTile {
+    __host__ __device__ __forceinline__ uint64_t operator()(const uint32_t &x) const { return x & 0x7FFFFFFFu; }
+};
+
+}  // namespace
+
+int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
+                  uint64_t *needed, hipStream_t s) {
+    const RowsImage &im = c.rows;
+    if (n == 0) {
+        MBRWT_HIP(hipMemsetAsync(d_offsets, 0, sizeof(uint64_t), s));
+        MBRWT_HIP(hipStreamSynchronize(s));
+        if (needed) *needed = 0;
+        return MBRWT_OK;
+    }
+    if (n > 0x7FFFFFF0ull) {
+        set_error("batch larger than 2^31 rows");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
+    int rc;
+    const uint32_t C = rows_tile_labels(c);
+    const uint64_t nt = (n + 63) / 64;
+    const uint64_t region = 128 + 2ull * C;
+    // counts workspace: nt+1 tile counts | (8-byte aligned) nt+1 tile offsets
+    const uint64_t to_off = ((nt + 1) * sizeof(uint32_t) + 7) / 8 * 8;
+    if ((rc = ensure(c.ws_temp, nt * region))) return rc;
+    if ((rc = ensure(c.ws_counts, to_off + (nt + 1) * sizeof(uint64_t)))) return rc;
+    if ((rc = ensure(c.ws_ovf, n * sizeof(uint32_t)))) return rc;
+    uint32_t *d_tc = reinterpret_cast<uint32_t *>(c.ws_counts.buf);
+    uint64_t *d_to = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + to_off);
+    hipcub::TransformInputIterator<uint64_t, MaskTile, const uint32_t *> it(d_tc, MaskTile());
+    size_t scan_bytes = 0;
+    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, it, d_to, nt + 1, s));
+    if ((rc = ensure(c.ws_scan, scan_bytes))) return rc;
+
+    RowsParams p{};
+    p.rows = d_rows;
+    p.n = n;
+    p.num_rows = c.tree.num_rows;
+    p.blocks = (uint64_t)(uintptr_t)im.blocks;
+    p.spill = (uint64_t)(uintptr_t)im.spill;
+    p.magic = im.magic;
+    p.S = im.S;
+    p.table_words = (uint32_t)im.table.size();
+    p.table = im.d_table;
+    p.C = C;
+    p.temp = reinterpret_cast<uint8_t *>(c.ws_temp.buf);
+    p.tile_counts = d_tc;
+    p.ovf_list = reinterpret_cast<uint32_t *>(c.ws_ovf.buf);
+    p.scalars = reinterpret_cast<unsigned long long *>(c.d_scalars);
+
+    const RowsFn kfn = rows_fn(im);
+    const size_t lds = ((im.table.size() + 3) & ~size_t(3)) * 4 + kRowsWpb * (64ull * im.B + 2ull * C);
+    const uint32_t threads = 64 * kRowsWpb;
+    if (c.rb_fn != reinterpret_cast<const void *>(kfn) || c.rb_lds != lds || c.rb_threads != threads) {
+        if (lds > 65536)
+            MBRWT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kfn),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        int dev_cus = 0, per_cu = 0;
+        (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kfn), threads, lds) !=
+                hipSuccess ||
+            per_cu <= 0)
+            per_cu = 1;
+        c.rb_fn = reinterpret_cast<const void *>(kfn);
+        c.rb_lds = lds;
+        c.rb_threads = threads;
+        c.rb_blocks = std::max(1, dev_cus) * per_cu;
+    }
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((nt + kRowsWpb - 1) / kRowsWpb, (uint64_t)c.rb_blocks));
+
+    MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
+    MBRWT_HIP(hipMemsetAsync(d_tc + nt, 0, sizeof(uint32_t), s));
+    if (c.timing) MBRWT_HIP(hipEventRecord(c.ev0, s));
+    hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(threads), lds, s, p);
+    MBRWT_HIP(hipGetLastError());
+    if (c.timing) MBRWT_HIP(hipEventRecord(c.ev1, s));
+    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_to, nt + 1, s));
+    hipLaunchKernelGGL(k_compact_tiles, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s, p.temp, C, d_tc, d_to,
+                       d_offsets, d_cols, n, cap);
+    MBRWT_HIP(hipGetLastError());
+    MBRWT_HIP(hipMemcpyAsync(c.d_scalars, d_to + nt, sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+    MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    MBRWT_HIP(hipStreamSynchronize(s));
+    if (c.timing) {
+        float ms = 0;
+        MBRWT_HIP(hipEventElapsedTime(&ms, c.ev0, c.ev1));
+        c.timing_ms += ms;
+        c.timing_launches += 1;
+    }
+    const uint64_t total = c.h_scalars[0], ovf = c.h_scalars[1], err = c.h_scalars[2];
+    if (err & 1) {
+        set_error("row out of range");
+        return MBRWT_ERR_RANGE;
+    }
+    if (needed) *needed = total;
+    if (total > cap) {
+        set_error("cols_cap too small");
+        return MBRWT_ERR_CAPACITY;
+    }
+    if (ovf) {
+        const uint64_t g = std::min<uint64_t>((ovf + 255) / 256, 65536);
+        hipLaunchKernelGGL(k_rows_direct, dim3((unsigned)g), dim3(256), 0, s, view_of(c), (const uint32_t *)im.d_table,
+                           d_rows, (const uint32_t *)p.ovf_list, ovf, (const uint64_t *)d_offsets, d_cols,
+                           p.scalars);
+        MBRWT_HIP(hipGetLastError());
+    }
+    return MBRWT_OK;
+}
+
+static uint64_t simple_grid(uint64_t n) { return std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 65536)); }
+
+int rows_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n, uint8_t *d_out, hipStream_t s) {
+    if (n == 0) return MBRWT_OK;
+    MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
+    hipLaunchKernelGGL(k_rows_get, dim3((unsigned)simple_grid(n)), dim3(256), 0, s, view_of(c),
+                       (const uint32_t *)c.rows.d_table, d_rows, d_cols, n, c.tree.num_columns, d_out,
+                       reinterpret_cast<unsigned long long *>(c.d_scalars));
+    MBRWT_HIP(hipGetLastError());
+    MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    MBRWT_HIP(hipStreamSynchronize(s));
+    return (c.h_scalars[2] & 1) ? MBRWT_ERR_RANGE : MBRWT_OK;
+}
+
+int rows_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts, hipStream_t s) {
+    if (c.tree.num_columns) MBRWT_HIP(hipMemsetAsync(d_counts, 0, c.tree.num_columns * sizeof(uint64_t), s));
+    MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
+    if (n)
+        hipLaunchKernelGGL(k_rows_count<false>, dim3((unsigned)simple_grid(n)), dim3(256), 0, s, view_of(c),
+                           (const uint32_t *)c.rows.d_table, d_rows, n, reinterpret_cast<unsigned long long *>(d_counts),
+                           reinterpret_cast<unsigned long long *>(c.d_scalars));
+    MBRWT_HIP(hipGetLastError());
+    MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    MBRWT_HIP(hipStreamSynchronize(s));
+    return (c.h_scalars[2] & 1) ? MBRWT_ERR_RANGE : MBRWT_OK;
+}
+
+int rows_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s) {
+    MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
+    if (n)
+        hipLaunchKernelGGL(k_rows_count<true>, dim3((unsigned)simple_grid(n)), dim3(256), 0, s, view_of(c),
+                           (const uint32_t *)c.rows.d_table, d_rows, n, nullptr,
+                           reinterpret_cast<unsigned long long *>(c.d_scalars));
+    MBRWT_HIP(hipGetLastError());
+    MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    MBRWT_HIP(hipStreamSynchronize(s));
+    if (c.h_scalars[2] & 1) return MBRWT_ERR_RANGE;
+    if (visits) *visits = c.h_scalars[3];
+    if (labels) *labels = c.h_scalars[4];
+    return MBRWT_OK;
+}
+
+int rows_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap, uint64_t *rows_needed,
+                    hipStream_t s) {
+    if (column >= c.tree.num_columns) {
+        set_error("column out of range");
+        return MBRWT_ERR_RANGE;
+    }
+    const uint64_t n = c.tree.num_rows;
+    const RowHasColumn f{view_of(c), c.rows.d_table, (uint32_t)column};
+    hipcub::CountingInputIterator<uint64_t> rows_it(0);
+    // the column's size first (a reduce over the rows), then the rows
+    hipcub::TransformInputIterator<uint64_t, HasColumnCount, hipcub::CountingInputIterator<uint64_t>> cnt_it(
+        rows_it, HasColumnCount{f});
+    int rc;
+    size_t red_bytes = 0, sel_bytes = 0;
+    uint64_t *d_num = reinterpret_cast<uint64_t *>(c.d_scalars);
+    MBRWT_HIP(hipcub::DeviceReduce::Sum(nullptr, red_bytes, cnt_it, d_num, n, s));
+    if ((rc = ensure(c.ws_scan, std::max<size_t>(red_bytes, 256)))) return rc;
+    MBRWT_HIP(hipcub::DeviceReduce::Sum(c.ws_scan.buf, red_bytes, cnt_it, d_num, n, s));
+    MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    MBRWT_HIP(hipStreamSynchronize(s));
+    const uint64_t need = c.h_scalars[0];
+    if (rows_needed) *rows_needed = need;
+    if (!d_rows || need > rows_cap) {
+        if (need > rows_cap) {
+            set_error("rows_cap too small");
+            return MBRWT_ERR_CAPACITY;
+        }
+        return MBRWT_OK;
+    }
+    if (!need) return MBRWT_OK;
+    MBRWT_HIP(hipcub::DeviceSelect::If(nullptr, sel_bytes, rows_it, d_rows, d_num, n, f, s));
+    if ((rc = ensure(c.ws_scan, sel_bytes))) return rc;
+    MBRWT_HIP(hipcub::DeviceSelect::If(c.ws_scan.buf, sel_bytes, rows_it, d_rows, d_num, n, f, s));
+    MBRWT_HIP(hipStreamSynchronize(s));
+    return MBRWT_OK;
+}
+
+const char *rows_kernel_name() { return "k_traverse_rows"; }
+
+}  // namespace mbrwt

@@ -151,6 +151,39 @@ int mbrwt_create_relaxed(const mbrwt_tree_desc *desc, uint64_t max_arity, int de
 
 void mbrwt_destroy(mbrwt_ctx *ctx);
 
+/* ---- device layout ------------------------------------------------------
+ * Two layouts of the same tree:
+ *   NODES  per-node, sibling-interleaved index columns with ranks; get_row is
+ *          the reference's rank1 descent (BRWT.cpp:26-53) over them;
+ *   ROWS   ROW RECORDS: the tree's index bits regrouped by row (each row's
+ *          descent -- the children mask of every internal node it reaches, in
+ *          DFS pre-order -- stored with the row), so get_row is one block read
+ *          and a record walk; the rank1 remaps are resolved at build time.
+ *          Trees with arity <= 16, < 2^15 columns, height <= 16.  Built one
+ *          range of rows at a time, so rows >= 2^32 need no row shards.
+ *          get_column scans the records; mbrwt_tree_export is unsupported.
+ *   BOTH   both images: get_rows / count_labels on the records, the rest on
+ *          the node image.
+ * The layout is chosen when a context is created: mbrwt_set_build_option
+ * (MBRWT_BUILD_LAYOUT, value) sets it for the mbrwt_create* / mbrwt_load calls
+ * of the calling thread; MBRWT_LAYOUT_AUTO (the default) takes the
+ * environment variable MBRWT_LAYOUT=nodes|rows|both, else NODES.  Layout ROWS
+ * on a tree outside its limits -> MBRWT_ERR_UNSUPPORTED.  No reference
+ * counterpart (the reference's BRWT has one sdsl layout).
+ */
+#define MBRWT_BUILD_LAYOUT 1
+#define MBRWT_LAYOUT_AUTO 0
+#define MBRWT_LAYOUT_NODES 1
+#define MBRWT_LAYOUT_ROWS 2
+#define MBRWT_LAYOUT_BOTH 3
+int mbrwt_set_build_option(int option, int64_t value);
+int mbrwt_layout(const mbrwt_ctx *ctx); /* MBRWT_LAYOUT_NODES / _ROWS / _BOTH of a context */
+/* Row-record image: out[0] block bytes B, [1] rows per block S, [2] block
+   bytes, [3] spill bytes, [4] record bytes (counts + masks), [5] spilled rows,
+   [6] rows longer than a block, [7] tree height.  MBRWT_ERR_UNSUPPORTED
+   without row records. */
+int mbrwt_rows_stats(const mbrwt_ctx *ctx, uint64_t out[8]);
+
 /* ---- files: the reference's BRWT stream (the matrix of a .brwt.annodbg) ----
  * An owned tree description (host memory).  Byte formats of sdsl-lite /
  * libmaus2 are restated from their published algorithms: PARITY UNPINNED

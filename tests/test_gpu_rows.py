@@ -1,0 +1,293 @@
+"""GPU parity of the ROW-RECORD layout (include/mbrwt.h "device layout",
+csrc/rows.hip): contexts built with layout 'rows' (records only) and 'both'
+against the CPU oracle -- bit-exact ordered CSR, point queries, columns,
+count_labels and the V/L accounting -- on the reference's own grids
+(test_BRWT.cpp:152-212, test_BRWT_optimizer.cpp:102-163), random basic /
+greedy / relaxed trees, the C2 shape, the greedy + relax production shape,
+every block size / rows-per-block choice, spilled and long records (the
+direct pass), ranged builds and rows >= 2^32.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU")]
+
+
+def _dense_grid(kind, n, m):
+    if kind == "zero":
+        return np.zeros((n, m), dtype=bool)
+    if kind == "one":
+        return np.ones((n, m), dtype=bool)
+    i = np.arange(n)[:, None]
+    j = np.arange(m)[None, :]
+    return ((i + 2 * j) % 2).astype(bool)  # test_BRWT.cpp:200
+
+
+def _check_all(t, dev, rows, dense=None, columns=True):
+    """Every row-record query against the oracle tree `t`."""
+    off_o, cols_o = t.get_rows(rows)
+    off_d, cols_d = dev.get_rows(rows)
+    np.testing.assert_array_equal(off_d, off_o)
+    np.testing.assert_array_equal(cols_d, cols_o)
+    n, m = t.num_rows(), t.num_columns()
+    rng = np.random.default_rng(n + 31 * m)
+    k = min(4000, n * m)
+    qr = rng.integers(0, n, k).astype(np.uint64)
+    qc = rng.integers(0, m, k).astype(np.uint64)
+    got = dev.get_batch(qr, qc)
+    exp = np.array([t.get(int(r), int(c)) for r, c in zip(qr, qc)], dtype=np.uint8)
+    np.testing.assert_array_equal(got, exp)
+    if columns:
+        for c in sorted(set(rng.integers(0, m, 6).tolist()) | {0, m - 1}):
+            assert dev.get_column(c).tolist() == t.get_column(c)
+    if dense is not None:
+        for i in range(0, len(rows), max(1, len(rows) // 50)):
+            r = int(rows[i])
+            assert sorted(cols_d[off_d[i]:off_d[i + 1]].tolist()) == np.nonzero(dense[r])[0].tolist()
+    return off_o, cols_o
+
+
+def _count_labels(dev, rows):
+    import torch
+    rt = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.uint64).view(np.int64)).cuda()
+    ct = torch.zeros(max(1, dev.num_columns()), dtype=torch.int64, device="cuda")
+    dev.count_labels_device(rt, ct)
+    torch.cuda.synchronize()
+    return ct.cpu().numpy().view(np.uint64)
+
+
+@pytest.mark.parametrize("kind", ["zero", "one", "mixed"])
+@pytest.mark.parametrize("build", [("basic", 2, 0), ("basic", 2, 2**64 - 1), ("greedy", 2, 0)])
+def test_reference_grids_rows(oracle_mod, kind, build):
+    """test_BRWT.cpp:152-212 / test_BRWT_optimizer.cpp:102-163 on row records."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice, MBRWTError, _lib as L
+    part, arity, relax = build
+    for n in range(1, 20):
+        for m in range(1, 20):
+            dense = _dense_grid(kind, n, m)
+            t = O.OracleTree.from_dense(dense, part, arity, relax)
+            ex = t.export()
+            if m == 1 or int(ex["num_children"].max()) > 16:
+                # a leaf root, or a node wider than 16 (relax without an
+                # arity bound): outside the row-record layout
+                with pytest.raises(MBRWTError) as ei:
+                    BRWTDevice.from_tree(ex, layout="rows")
+                assert ei.value.status == L.MBRWT_ERR_UNSUPPORTED
+                continue
+            d = BRWTDevice.from_tree(ex, layout="rows")
+            assert d.layout() == "rows"
+            assert d.num_rows() == n and d.num_columns() == m and d.num_relations() == int(dense.sum())
+            _check_all(t, d, np.arange(n, dtype=np.uint64), dense)
+
+
+@pytest.mark.parametrize("n,m,d,part,arity,relax", [
+    (5000, 40, 0.1, "basic", 2, 0),
+    (5000, 40, 0.1, "basic", 3, 0),
+    (5000, 40, 0.1, "greedy", 2, 0),
+    (5000, 40, 0.1, "greedy", 2, 4),
+    (3000, 100, 0.05, "basic", 8, 0),
+    (3000, 100, 0.05, "basic", 2, 16),
+    (2000, 200, 0.02, "basic", 16, 0),
+    (6000, 200, 0.02, "greedy", 2, 10),   # the production shape (relax 10)
+    (1000, 7, 1.0, "basic", 2, 0),        # dense rows
+    (1000, 7, 0.0, "basic", 2, 0),        # rows without labels
+])
+@pytest.mark.parametrize("layout", ["rows", "both"])
+def test_random_matrices_rows(oracle_mod, n, m, d, part, arity, relax, layout):
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    rng = np.random.default_rng(n * 7 + m)
+    dense = rng.random((n, m)) < d
+    t = O.OracleTree.from_dense(dense, part, arity, relax)
+    dev = BRWTDevice.from_tree(t.export(), layout=layout)
+    assert dev.layout() == layout
+    assert dev.traverse_kernel() == "k_traverse_rows"
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 5000)]).astype(np.uint64)
+    _check_all(t, dev, rows, dense)
+    np.testing.assert_array_equal(_count_labels(dev, rows), dense[rows.astype(np.int64)].sum(axis=0))
+
+
+def test_arity_limit(oracle_mod):
+    """Nodes wider than 16 children stay on the node layout."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice, MBRWTError, _lib as L
+    dense = np.random.default_rng(1).random((500, 64)) < 0.1
+    t = O.OracleTree.from_dense(dense, "basic", 33)
+    with pytest.raises(MBRWTError) as ei:
+        BRWTDevice.from_tree(t.export(), layout="rows")
+    assert ei.value.status == L.MBRWT_ERR_UNSUPPORTED
+    assert BRWTDevice.from_tree(t.export()).layout() == "nodes"
+
+
+@pytest.mark.parametrize("bs", ["64,1", "64,2", "64,3", "64,5", "64,8", "128,1", "128,3", "128,7", "128,15"])
+def test_every_block_shape(oracle_mod, bs, monkeypatch):
+    """Every (block bytes, rows per block) the builder may pick -- spills,
+    long records and the direct pass included -- answers like the oracle."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    monkeypatch.setenv("MBRWT_ROWS_BS", bs)
+    rng = np.random.default_rng(5)
+    n, m = 30000, 300
+    # rows of very different lengths: most sparse, some dense (long records)
+    u = rng.random(n)
+    p = np.where(u < 0.005, 1.0, np.where(u < 0.025, 0.5, 0.01))
+    dense = rng.random((n, m)) < p[:, None]
+    for part, arity, relax in [("basic", 8, 0), ("greedy", 2, 10)]:
+        t = O.OracleTree.from_dense(dense, part, arity, relax)
+        dev = BRWTDevice.from_tree(t.export(), layout="rows")
+        st = dev.rows_stats()
+        B, S = (int(x) for x in bs.split(","))
+        assert (st["block_bytes"], st["rows_per_block"]) == (B, S)
+        rows = np.concatenate([np.arange(n), rng.integers(0, n, 20000)]).astype(np.uint64)
+        _check_all(t, dev, rows, dense, columns=False)
+
+
+def test_synthetic_c2_shape_rows(oracle_mod):
+    """C2 (1 M x 2,652, d = 0.3 %, arity 8) generated on the device, turned
+    into row records; the whole batch, V/L and count_labels against the
+    oracle's independent generator."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    n, m, d = 1_000_000, 2652, 0.003
+    t = O.OracleTree.topdown(n, m, d, 8, 42)
+    rows = np.random.default_rng(42).integers(0, n, 300_000).astype(np.uint64)
+    both = BRWTDevice.synthetic(n, m, d, 8, 42, layout="both")
+    rec = BRWTDevice.synthetic(n, m, d, 8, 42, layout="rows")
+    assert rec.device_bytes() < both.device_bytes()
+    off_o, cols_o = t.get_rows(rows)
+    for dev in (both, rec):
+        off_d, cols_d = dev.get_rows(rows)
+        np.testing.assert_array_equal(off_d, off_o)
+        np.testing.assert_array_equal(cols_d, cols_o)
+    import torch
+    rt = torch.from_numpy(rows.view(np.int64)).cuda()
+    v_rec = rec.count_work_device(rt)
+    nodes = BRWTDevice.synthetic(n, m, d, 8, 42, layout="nodes")
+    v_nodes = nodes.count_work_device(rt)
+    assert v_rec == v_nodes, (v_rec, v_nodes)
+    np.testing.assert_array_equal(_count_labels(rec, rows), np.bincount(cols_o, minlength=m))
+    for c in (0, 1, 1000, m - 1):
+        assert rec.get_column(c).tolist() == t.get_column(c)
+
+
+def test_greedy_relax_shape_rows(oracle_mod):
+    """The production shape (greedy + relax 10 from C2's columns, the
+    reference's build scripts) under the synthetic law, as row records."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    dense = np.random.default_rng(11).random((20000, 2652)) < 0.003
+    shape = O.OracleTree.from_dense(dense, "greedy", 2, 10).export()
+    n = 400_000
+    dev = BRWTDevice.synthetic_shaped(n, shape, 0.003, 7, layout="rows")
+    t = O.OracleTree.topdown_shaped(n, shape, 0.003, 7)
+    rows = np.random.default_rng(3).integers(0, n, 200_000).astype(np.uint64)
+    off_o, cols_o = t.get_rows(rows)
+    off_d, cols_d = dev.get_rows(rows)
+    np.testing.assert_array_equal(off_d, off_o)
+    np.testing.assert_array_equal(cols_d, cols_o)
+
+
+def test_ranged_build(oracle_mod, monkeypatch):
+    """Layout rows built one range of rows at a time (synthetic law across
+    the ranges, and a tree description sliced per range)."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    monkeypatch.setenv("MBRWT_ROWS_RANGE", "360360")
+    n, m, d = 1_500_000, 700, 0.004
+    dev = BRWTDevice.synthetic(n, m, d, 8, 9, layout="rows")
+    t = O.OracleTree.topdown(n, m, d, 8, 9)
+    rows = np.concatenate([np.arange(360350, 360370), np.arange(720710, 720730),
+                           np.random.default_rng(1).integers(0, n, 200_000)]).astype(np.uint64)
+    off_o, cols_o = t.get_rows(rows)
+    off_d, cols_d = dev.get_rows(rows)
+    np.testing.assert_array_equal(off_d, off_o)
+    np.testing.assert_array_equal(cols_d, cols_o)
+    # from a description (slice_desc per range)
+    rng = np.random.default_rng(2)
+    dense = rng.random((800_000, 40)) < 0.05
+    t2 = O.OracleTree.from_dense(dense, "greedy", 2, 4)
+    dev2 = BRWTDevice.from_tree(t2.export(), layout="rows")
+    _check_all(t2, dev2, rng.integers(0, 800_000, 100_000).astype(np.uint64), dense, columns=False)
+
+
+def test_errors_and_capacity_rows(oracle_mod):
+    O = oracle_mod
+    import ctypes as C
+    from genome_graph_annotation_amd import BRWTDevice, MBRWTError, _lib as L
+    rng = np.random.default_rng(3)
+    dense = rng.random((100, 20)) < 0.5
+    t = O.OracleTree.from_dense(dense, "basic", 4)
+    d = BRWTDevice.from_tree(t.export(), layout="rows")
+    with pytest.raises(MBRWTError) as ei:
+        d.get_rows(np.array([0, 100], dtype=np.uint64))
+    assert ei.value.status == L.MBRWT_ERR_RANGE
+    with pytest.raises(MBRWTError):
+        d.get_batch([0], [20])
+    with pytest.raises(MBRWTError):
+        d.get_column(20)
+    with pytest.raises(MBRWTError) as ei:
+        d.export()
+    assert ei.value.status == L.MBRWT_ERR_UNSUPPORTED
+    # capacity retry protocol
+    rows = np.arange(100, dtype=np.uint64)
+    off = np.zeros(101, dtype=np.uint64)
+    cols = np.zeros(5, dtype=np.uint32)
+    need = C.c_uint64(0)
+    rc = L.lib().mbrwt_get_rows(d._h, rows.ctypes.data_as(L.u64p), 100, off.ctypes.data_as(L.u64p),
+                                cols.ctypes.data_as(L.u32p), 5, C.byref(need))
+    assert rc == L.MBRWT_ERR_CAPACITY and need.value == int(dense.sum())
+    off_d, cols_d = d.get_rows(rows)
+    off_o, cols_o = t.get_rows(rows)
+    np.testing.assert_array_equal(off_d, off_o)
+    np.testing.assert_array_equal(cols_d, cols_o)
+    e, c2 = d.get_rows(np.zeros(0, dtype=np.uint64))
+    assert e.tolist() == [0] and len(c2) == 0
+
+
+def test_classify_on_rows(oracle_mod):
+    """get_labels / get_top_labels batches (classify) over row records."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    rng = np.random.default_rng(8)
+    n, m = 20000, 300
+    dense = rng.random((n, m)) < 0.03
+    t = O.OracleTree.from_dense(dense, "basic", 8)
+    dev = BRWTDevice.from_tree(t.export(), layout="rows")
+    nodes = BRWTDevice.from_tree(t.export(), layout="nodes")
+    lens = rng.integers(0, 40, 1000)
+    roff = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    rows = rng.integers(0, n, int(roff[-1])).astype(np.uint64)
+    for ratio in (0.0, 0.5, 1.0):
+        a = dev.get_labels_batch(rows, roff, ratio)
+        b = nodes.get_labels_batch(rows, roff, ratio)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    a = dev.get_top_labels_batch(rows, roff, 5)
+    b = nodes.get_top_labels_batch(rows, roff, 5)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.slow
+def test_rows_beyond_2_32_rows(oracle_mod):
+    """Rows >= 2^32 without row shards: a 4.5 B-row x 16-column tree as row
+    records (ranged build), against the streamed oracle."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    n, m, d = 4_500_000_000, 16, 0.01
+    dev = BRWTDevice.synthetic(n, m, d, 4, 5, layout="rows")
+    assert dev.num_shards() == 1 and dev.layout() == "rows"
+    rng = np.random.default_rng(4)
+    edges = []
+    for e in (2**31, 2**32, 3 * 2**31, n):
+        edges += list(range(e - 8, min(e + 8, n)))
+    rows = np.concatenate([np.array(edges), rng.integers(0, n, 300_000)]).astype(np.uint64)
+    off_o, cols_o = O.topdown_get_rows(n, m, d, 4, 5, rows)
+    off_d, cols_d = dev.get_rows(rows)
+    np.testing.assert_array_equal(off_d, off_o)
+    np.testing.assert_array_equal(cols_d, cols_o)
