@@ -53,17 +53,35 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level table (spec)
 FETCH_CALIB = 1.0
 
 
+# BASELINE.json configs: (rows, columns, density, batch, layout).  Row records
+# (layout rows) at the Kingsford shape; the RefSeq shape's records (~180
+# bytes, 120 labels per row) are longer than a block, so it keeps the
+# per-node layout (k_traverse_p2w).
+WORKLOADS = {
+    "c4": dict(rows=3_700_000_000, cols=2652, density=0.003, batch=8_000_000, layout="rows"),
+    "c3": dict(rows=1_000_000_000, cols=3173, density=0.038, batch=10_000_000, layout="nodes"),
+    "c2": dict(rows=1_000_000, cols=2652, density=0.003, batch=1_000_000, layout="rows"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--rows", type=int, default=3_700_000_000)
-    ap.add_argument("--cols", type=int, default=2652)
-    ap.add_argument("--density", type=float, default=0.003)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c4",
+                    help="BASELINE config preset (c4 = configs[3], the driver's default; c3 = configs[2]; "
+                         "c2 = configs[1]); --rows/--cols/--density/--batch/--layout override it")
+    ap.add_argument("--rows", type=int, default=None)
+    ap.add_argument("--cols", type=int, default=None)
+    ap.add_argument("--density", type=float, default=None)
     ap.add_argument("--arity", type=int, default=8)
-    ap.add_argument("--batch", type=int, default=8_000_000,
+    ap.add_argument("--batch", type=int, default=None,
                     help="query rows: the global batch (strong) or rows per GPU (weak)")
+    ap.add_argument("--batches", type=int, default=4,
+                    help="distinct seeded batches; timed step i queries batch i mod this (no replayed batch)")
+    ap.add_argument("--layout", choices=["rows", "nodes", "both"], default=None,
+                    help="device layout (include/mbrwt.h): row records or per-node images")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the all-gatherv reassembly")
@@ -81,7 +99,12 @@ def parse():
     ap.add_argument("--traffic-out", default="", help="write the live traffic summary (JSON) here")
     ap.add_argument("--no-probe", action="store_true", help="skip the measured ceilings")
     ap.add_argument("--pmc-pass", action="store_true", help=argparse.SUPPRESS)  # child under rocprofv3
-    return ap.parse_args()
+    a = ap.parse_args()
+    w = WORKLOADS[a.workload]
+    for k in ("rows", "cols", "density", "batch", "layout"):
+        if getattr(a, k) is None:
+            setattr(a, k, w[k])
+    return a
 
 
 def log(msg):
@@ -102,7 +125,7 @@ def kernel_source_hash():
 
 def workload_args(a):
     return ["--rows", str(a.rows), "--cols", str(a.cols), "--density", repr(a.density), "--arity", str(a.arity),
-            "--batch", str(a.batch), "--seed", str(a.seed), "--kernel", str(a.kernel)]
+            "--batch", str(a.batch), "--seed", str(a.seed), "--kernel", str(a.kernel), "--layout", a.layout]
 
 
 def pmc_pass(a):
@@ -110,13 +133,13 @@ def pmc_pass(a):
     N = 1 run, 2 warm-up + 3 counted launches of the traversal."""
     from genome_graph_annotation_amd import BRWTDevice, _lib as L
     torch.cuda.set_device(0)
-    mat = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, device=0)
+    mat = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, device=0, layout=a.layout)
     if a.kernel:
         mat.set_option(L.MBRWT_OPT_KERNEL, a.kernel)
     rows_np = np.random.default_rng(a.seed).integers(0, a.rows, a.batch, dtype=np.uint64)
     rows_t = torch.from_numpy(rows_np.view(np.int64)).cuda()
     off_t = torch.empty(a.batch + 1, dtype=torch.int64, device="cuda")
-    cols_t = torch.empty(a.batch * 16 + 1024, dtype=torch.int32, device="cuda")
+    cols_t = torch.empty(int(a.batch * max(16.0, 3.0 * a.cols * a.density)) + 1024, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     for _ in range(5):
         mat.get_rows_device(rows_t, off_t, cols_t, s)
@@ -143,7 +166,7 @@ def live_traffic(a, kernel_re):
     two dispatches are warm-up."""
     out = {"counters": {}, "source_hash": kernel_source_hash(), "kernel_regex": kernel_re,
            "config": {"rows": a.rows, "cols": a.cols, "density": a.density, "arity": a.arity, "batch": a.batch,
-                      "kernel": a.kernel}}
+                      "kernel": a.kernel, "layout": a.layout}}
     env = dict(os.environ, TMPDIR="/tmp")
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="bench_pmc_", dir="/tmp")
@@ -178,7 +201,7 @@ def committed_traffic(a, kernel_re):
     """A committed live-traffic summary (profiles/*/traffic_*.json) of this
     workload measured on the CURRENT kernel sources, or None."""
     want_cfg = {"rows": a.rows, "cols": a.cols, "density": a.density, "arity": a.arity, "batch": a.batch,
-                "kernel": a.kernel}
+                "kernel": a.kernel, "layout": a.layout}
     h = kernel_source_hash()
     hit = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic_*.json"))):
@@ -200,8 +223,12 @@ def csr_hash(off: np.ndarray, cols: np.ndarray) -> str:
 
 
 def probe_ceilings(dev_t, stream_ptr, free_bytes):
-    """Measured streaming-read GB/s and random-64-byte requests/s on this GPU
-    (tools/probe.hip); None where the probe library is missing."""
+    """Measured ceilings of this GPU (tools/probe.hip): streaming-read GB/s,
+    and random-segment requests/s -- the MAXIMUM over a sweep of requests in
+    flight and resident waves (the full sweep:
+    tools/probe_sweep.py, profiles/r03/v01_probe_sweep.json) for 64-byte and
+    128-byte segments (the row-record blocks); None where the probe library is
+    missing."""
     import ctypes as C
     path = os.path.join(ROOT, "tools", "_build", "libprobe.so")
     if not os.path.exists(path):
@@ -209,7 +236,8 @@ def probe_ceilings(dev_t, stream_ptr, free_bytes):
         return None, None
     lib = C.CDLL(path)
     lib.probe_stream_read.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_void_p, C.POINTER(C.c_double)]
-    lib.probe_random64.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.POINTER(C.c_double)]
+    lib.probe_random_seg.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                     C.POINTER(C.c_double)]
     stream_gbs = rnd = None
     buf = torch.empty(4 << 30, dtype=torch.uint8, device=dev_t)
     v = C.c_double(0)
@@ -219,9 +247,19 @@ def probe_ceilings(dev_t, stream_ptr, free_bytes):
     # random segments over a buffer far past the 256 MiB Infinity Cache
     big = min(64 << 30, int(free_bytes * 0.8)) // (1 << 30) << 30
     if big >= (8 << 30):
+        cus = torch.cuda.get_device_properties(dev_t).multi_processor_count
         buf = torch.empty(big, dtype=torch.uint8, device=dev_t)
-        if lib.probe_random64(buf.data_ptr(), buf.numel(), stream_ptr, C.byref(v)) == 0:
-            rnd = {"segments_per_s": v.value, "buffer_gib": big >> 30}
+        rnd = {"buffer_gib": big >> 30}
+        for seg, sweep in ((64, [(2, 16), (4, 16), (8, 16), (4, 32), (16, 32)]), (128, [(8, 32), (16, 32), (8, 16)])):
+            best = None
+            for inflight, wpc in sweep:
+                if lib.probe_random_seg(buf.data_ptr(), buf.numel(), seg, inflight, cus * wpc // 4, 256, stream_ptr,
+                                        C.byref(v)) == 0 and (best is None or v.value > best[0]):
+                    best = (v.value, inflight, wpc)
+            if best is not None:
+                rnd[f"seg{seg}_per_s"] = best[0]
+                rnd[f"seg{seg}_best"] = {"inflight": best[1], "waves_per_cu": best[2]}
+        rnd["segments_per_s"] = rnd.get("seg64_per_s")
         del buf
     torch.cuda.empty_cache()
     return stream_gbs, rnd
@@ -239,14 +277,17 @@ def main():
     local = local % max(1, ndev)  # (rehearsal only: several ranks may share one GPU under gloo)
 
     from genome_graph_annotation_amd import BRWTDevice, _lib as L
-    from genome_graph_annotation_amd.dist import AllGatherV, allgatherv_csr, shard_bounds
+    from genome_graph_annotation_amd.dist import AllGatherV, shard_bounds
 
     # roofline traffic first: the PMC child passes need the GPU's memory for
     # their own copy of the structure
     kernel_re = None
     traffic = None
     if rank == 0 and world == 1 and a.traffic != "off":
-        kernel_re = "k_traverse_(p2w|fast2)" if a.kernel == 0 or 17 <= a.kernel <= 23 else "k_traverse"
+        if a.layout in ("rows", "both") and a.kernel == 0:
+            kernel_re = "k_traverse_rows"
+        else:
+            kernel_re = "k_traverse_(p2w|fast2)" if a.kernel == 0 or 17 <= a.kernel <= 23 else "k_traverse"
         if a.traffic == "live":
             traffic = live_traffic(a, kernel_re)
             if traffic is not None and a.traffic_out:
@@ -255,11 +296,15 @@ def main():
         if traffic is None:
             traffic = committed_traffic(a, kernel_re)
 
+    size_group = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         if a.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            # the all-gatherv's sizes travel as host integers over gloo (no
+            # device read-back in the step: dist.AllGatherV)
+            size_group = dist.new_group(backend="gloo")
         else:
             dist.init_process_group(a.dist_backend)
     else:
@@ -267,30 +312,37 @@ def main():
 
     dev_t = torch.device("cuda", local)
     t0 = time.time()
-    mat = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, device=local)
+    mat = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, device=local, layout=a.layout)
     setup_s = time.time() - t0
-    log(f"device structure built in {setup_s:.1f} s ({mat.device_bytes() / 1e9:.1f} GB)")
+    struct_bytes = mat.device_bytes()
+    log(f"device structure built in {setup_s:.1f} s ({mat.device_bytes() / 1e9:.1f} GB, layout {mat.layout()}, "
+        f"{mat.rows_stats()})")
     if a.kernel:
         mat.set_option(L.MBRWT_OPT_KERNEL, a.kernel)
 
-    # the global batch (one seed) and this rank's contiguous slice of it
+    # K distinct global batches (batch k: seed + k; batch 0 is the r01/r02
+    # batch) and this rank's contiguous slice of each; timed step i queries
+    # batch i mod K, so no timed step replays the previous step's rows
     G = a.batch if a.scaling == "strong" else a.batch * world
-    rows_global = np.random.default_rng(a.seed).integers(0, a.rows, G, dtype=np.uint64)
+    K = max(1, a.batches)
     lo, hi = shard_bounds(G, world, rank)
-    rows_np = rows_global[lo:hi]
     nb = hi - lo
-    rows_t = torch.from_numpy(rows_np.view(np.int64)).to(dev_t)
+    globals_np = [np.random.default_rng(a.seed + k).integers(0, a.rows, G, dtype=np.uint64) for k in range(K)]
+    rows_ts = [torch.from_numpy(np.ascontiguousarray(g[lo:hi]).view(np.int64)).to(dev_t) for g in globals_np]
     off_t = torch.empty(nb + 1, dtype=torch.int64, device=dev_t)
     stream = torch.cuda.current_stream(dev_t)
     sptr = stream.cuda_stream
     # size the label buffer once (capacity protocol), outside the timed region
     probe = torch.empty(1, dtype=torch.int32, device=dev_t)
-    try:
-        need = mat.get_rows_device(rows_t, off_t, probe, sptr)
-    except L.MBRWTError as e:
-        if e.status != L.MBRWT_ERR_CAPACITY:
-            raise
-        need = e.needed
+    need = 0
+    for rt in rows_ts:
+        try:
+            nk = mat.get_rows_device(rt, off_t, probe, sptr)
+        except L.MBRWTError as e:
+            if e.status != L.MBRWT_ERR_CAPACITY:
+                raise
+            nk = e.needed
+        need = max(need, nk)
     cols_t = torch.empty(int(need * 1.02) + 1024, dtype=torch.int32, device=dev_t)
 
     # N > 1: steps are pipelined -- batch k's all-gatherv (RCCL stream) runs
@@ -300,16 +352,23 @@ def main():
     bufs = [(off_t, cols_t)]
     if gather:
         bufs.append((torch.empty_like(off_t), torch.empty_like(cols_t)))
-    state = {"i": 0, "pending": None, "global": None}
+    state = {"i": 0, "pending": None, "global": None, "timed": False, "exchanges": [], "get_rows_host": []}
 
     def step():
-        o, cb = bufs[state["i"] % len(bufs)]
+        i = state["i"]
+        o, cb = bufs[i % len(bufs)]
         state["i"] += 1
-        n_lab = mat.get_rows_device(rows_t, o, cb, sptr)
+        h0 = time.perf_counter()
+        n_lab = mat.get_rows_device(rows_ts[i % K], o, cb, sptr)
+        if state["timed"]:
+            state["get_rows_host"].append((time.perf_counter() - h0) * 1e3)
         if gather:
             if state["pending"] is not None:
                 state["global"] = state["pending"].finish()
-            state["pending"] = AllGatherV(o, cb, n_labels=n_lab, num_columns=a.cols)
+            state["pending"] = AllGatherV(o, cb, n_labels=n_lab, num_columns=a.cols, size_group=size_group,
+                                          timing=state["timed"])
+            if state["timed"]:
+                state["exchanges"].append(state["pending"])
         return n_lab
 
     def drain():
@@ -323,6 +382,7 @@ def main():
     torch.cuda.synchronize()
     mat.take_timing()
     mat.set_option(L.MBRWT_OPT_TIMING, 1)
+    state["timed"] = True
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -334,6 +394,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    state["timed"] = False
     log(f"timed {a.steps} steps: {elapsed / a.steps * 1e3:.3f} ms/step")
     mat.set_option(L.MBRWT_OPT_TIMING, 0)
     kern_ms_total, launches = mat.take_timing()
@@ -341,6 +402,28 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    last_k = (state["i"] - 1) % K
+    rows_global = globals_np[last_k]
+    rows_t = rows_ts[last_k]
+
+    # per-phase times of the multi-GPU step (this rank; max over ranks below)
+    phases = None
+    if world > 1:
+        ph = {"traverse_kernel_ms": kern_ms_total / max(1, launches),
+              "get_rows_host_ms": float(np.mean(state["get_rows_host"])) if state["get_rows_host"] else None}
+        if state["exchanges"]:
+            ex = [x.phases() for x in state["exchanges"]]
+            for k in ex[0]:
+                ph[k] = float(np.mean([e[k] for e in ex]))
+            ph["wire_bytes_sent_per_rank"] = int(state["exchanges"][-1].wire_bytes)
+            ph["wire_bytes_received_per_rank"] = int(state["exchanges"][-1].wire_bytes) * (world - 1)
+        keys = sorted(k for k, v in ph.items() if v is not None)
+        t = torch.tensor([float(ph[k]) for k in keys], dtype=torch.float64, device=dev_t)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        phases = {k: float(v) for k, v in zip(keys, t.tolist())}
+        phases["note"] = ("max over ranks of each rank's mean over the timed steps; device times from HIP events "
+                          "on the streams that run them; host_ms are wall times of the host calls")
+        state["exchanges"] = []
 
     last_off, last_cols = bufs[(state["i"] - 1) % len(bufs)]
     # the global CSR of the last timed step: this rank's slice (N = 1) or the
@@ -367,7 +450,7 @@ def main():
         del g_off, g_cols, glob_off, glob_cols
         state["global"] = None
 
-    # measured ceilings of this GPU (streaming read; random 64-B requests)
+    # measured ceilings of this GPU (streaming read; random 64-/128-B requests)
     stream_gbs = rnd = None
     if rank == 0 and not a.no_probe:
         free, _ = torch.cuda.mem_get_info(dev_t)
@@ -379,6 +462,7 @@ def main():
     alg_bytes = 64 * visits + 16 * nb + 4 * labels
     kern_ms = kern_ms_total / max(1, launches)
     kname = mat.traverse_kernel()
+    rstats = mat.rows_stats()
 
     cpu = None
     parity = None
@@ -400,6 +484,7 @@ def main():
         parity = {"rows_checked": chk, "labels_checked": int(len(cols_o)), "bit_exact": exact,
                   "csr_hash_gpu": csr_hash(off_h, cols_h), "csr_hash_oracle": csr_hash(off_o, cols_o),
                   "scope": ("the whole global batch" if chk == G else f"the first {chk:,} rows of the global batch")
+                           + f" of the last timed step (batch {last_k}, seed {a.seed + last_k})"
                            + (f", reassembled by the all-gatherv from {world} ranks" if world > 1 else "")}
         del off_o, cols_o
         if world == 1:
@@ -434,25 +519,37 @@ def main():
     # roofline: measured traffic (frac) and the §8(d) algorithmic bytes (alg_frac)
     ks = kern_ms / 1e3
     roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": kname, "kernel_ms": kern_ms,
+            "step_minus_kernel_ms": elapsed / a.steps * 1e3 - kern_ms if world == 1 else None,
             "achieved": None, "frac": None, "traffic": None,
             "alg_bytes_per_launch": alg_bytes, "alg_achieved": alg_bytes / ks / 1e9,
             "alg_frac": alg_bytes / ks / 1e9 / HBM_PEAK_GBS,
             "visits_per_row": visits / max(1, nb), "labels_per_row": labels / max(1, nb),
             "stream_read_measured": stream_gbs}
+    seg = 64
+    if rstats is not None:
+        seg = rstats["block_bytes"]
+        roof["row_records"] = dict(rstats, spilled_fraction=rstats["spilled_rows"] / a.rows)
+        # one block per row, plus one spill entry per spilled row
+        roof["block_requests_per_launch"] = nb * (1.0 + rstats["spilled_rows"] / a.rows)
+        roof["block_requests_per_s"] = roof["block_requests_per_launch"] / ks
     if traffic is not None and world == 1:
         tb = traffic["traffic_bytes"]
         roof.update({"achieved": tb / ks / 1e9, "frac": tb / ks / 1e9 / HBM_PEAK_GBS, "traffic": tb,
                      "read_bytes": traffic["read_bytes"], "write_bytes": traffic["write_bytes"],
                      "traffic_source": traffic.get("source", "live rocprofv3 --pmc passes of this run") +
                                        f" (sources {traffic['source_hash']})"})
-        req = traffic["read_bytes"] / 64.0  # FETCH_SIZE = 64-byte requests (calibrated)
+        req = traffic["read_bytes"] / 64.0  # FETCH_SIZE in 64-byte units (calibrated on random 64-B segments)
         roof["read_requests_per_launch"] = req
         roof["read_requests_per_s"] = req / ks
-        if rnd is not None:
-            roof["ceiling_random64_per_s"] = rnd["segments_per_s"]
-            roof["ceiling_random64_frac"] = req / ks / rnd["segments_per_s"]
-    elif rnd is not None:
-        roof["ceiling_random64_per_s"] = rnd["segments_per_s"]
+    if rnd is not None:
+        roof["ceiling_random64_per_s"] = rnd.get("seg64_per_s")
+        roof["ceiling_random128_per_s"] = rnd.get("seg128_per_s")
+        roof["ceiling_sweep_best"] = {k: v for k, v in rnd.items() if k.endswith("_best")}
+        ceil = rnd.get(f"seg{seg}_per_s")
+        if rstats is not None and ceil:
+            roof[f"ceiling_random{seg}_frac"] = roof["block_requests_per_s"] / ceil
+        elif traffic is not None and world == 1 and ceil:
+            roof["ceiling_random64_frac"] = roof["read_requests_per_s"] / ceil
 
     value = G * a.steps / elapsed
     line = {
@@ -467,18 +564,21 @@ def main():
         "scaling": a.scaling,
         "vs_baseline": None,
         "dtype": "u32/u64",
-        "data": "synthetic (top-down i.i.d. Bernoulli columns, seed 42; uniform random rows, seed 42)",
+        "data": f"synthetic (top-down i.i.d. Bernoulli columns, seed {a.seed}; {K} batches of uniform random rows, "
+                f"seeds {a.seed}..{a.seed + K - 1}, rotated over the steps)",
         "config": {
             "workload": f"Multi-BRWT {a.rows:,} x {a.cols:,}, d={a.density}, arity {a.arity} "
-                        f"(Kingsford shape, BASELINE configs[3]); global batch {G:,} rows, "
-                        f"{nb:,} per GPU ({a.scaling} scaling)",
+                        f"({a.workload}: BASELINE configs[{ {'c2': 1, 'c3': 2, 'c4': 3}[a.workload] }]); "
+                        f"global batch {G:,} rows, {nb:,} per GPU ({a.scaling} scaling)",
             "num_rows": a.rows, "num_columns": a.cols, "density": a.density, "arity": a.arity,
-            "global_batch": G, "batch_per_gpu": nb,
+            "global_batch": G, "batch_per_gpu": nb, "batches": K, "layout": a.layout,
             "parallelism": f"batch-sharded x{world}, tree replicated" + ("" if world == 1 or a.no_gather
                                                                          else ", all-gatherv over " + ("RCCL" if a.dist_backend == "nccl" else a.dist_backend)),
-            "structure_bytes": mat.device_bytes(), "setup_s": round(setup_s, 2),
+            "structure_bytes": struct_bytes,
+            "setup_s": round(setup_s, 2),
         },
         "roofline": roof,
+        "phases": phases,
         "cpu_baseline": cpu,
         "reassembly": reassembly,
         "parity": parity,

@@ -119,6 +119,8 @@ SIGNATURES = {
                                                 C.c_double, C.c_void_p, C.c_void_p, C.c_uint64, u64p, C.c_void_p]),
     "mbrwt_pack_ids_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]),
     "mbrwt_unpack_ids_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]),
+    "mbrwt_unpack_segments_device": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64, u64p, C.c_uint32, C.c_void_p,
+                                               C.c_void_p]),
     "mbrwt_destroy": (None, [C.c_void_p]),
     "mbrwt_set_build_option": (C.c_int, [C.c_int, C.c_int64]),
     "mbrwt_layout": (C.c_int, [C.c_void_p]),

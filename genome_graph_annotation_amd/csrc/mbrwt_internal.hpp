@@ -254,9 +254,12 @@ struct RowsImage {
     uint8_t *spill = nullptr;       // spill entries (+ B bytes of padding)
     uint64_t spill_cap = 0;         // bytes allocated
     unsigned long long *d_spill_used = nullptr;  // 16-byte units taken (build)
-    std::vector<uint32_t> table;    // RWT table
+    std::vector<uint32_t> table;    // RWT table (the simple kernels, the direct pass)
     uint32_t *d_table = nullptr;
     uint32_t height = 0;
+    std::vector<uint32_t> table2;   // RWT2 table (k_traverse_rows: one word per child, leaf parents inline)
+    uint32_t *d_table2 = nullptr;
+    uint32_t frames = 0;            // its stack levels
     uint64_t bytes = 0;             // blocks + spill used
     // build statistics
     uint64_t spilled_rows = 0, long_rows = 0, record_bytes = 0, spill_bytes = 0;
@@ -264,6 +267,7 @@ struct RowsImage {
 // the RWT table of a finished node tree; false (and an empty table) when the
 // shape is outside the row-record kernels' limits
 bool build_rwt_table(const Tree &tree, std::vector<uint32_t> &table, uint32_t &height);
+bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &table2, uint32_t &frames);
 // the thread's build layout (mbrwt_set_build_option, else MBRWT_LAYOUT)
 int build_layout();
 void set_build_layout(int layout);

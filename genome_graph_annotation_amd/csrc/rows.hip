@@ -119,6 +119,91 @@ bool build_rwt_table(const Tree &tree, std::vector<uint32_t> &table, uint32_t &h
     return true;
 }
 
+// RWT2 table (k_traverse_rows): one u32 ENTRY per child of every internal
+// node that is not a leaf parent with consecutive columns ("LP" nodes, whose
+// labels are base column + bit: no entries, no frame), u32 words
+//   [0] the root's entry, [1] nE, [2] frames (non-LP internal levels on a
+//   path), [3] 0, nE entries; an entry is
+//     leaf      0x80000000 | column
+//     LP node   0xC0000000 | arity << 16 | first column
+//     internal  arity << 16 | first entry of its children
+// so the walk reads ONE table word per visited child.
+bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &t2, uint32_t &frames) {
+    t2.clear();
+    frames = 0;
+    const auto &N = tree.nodes;
+    if (N.size() < 2) return false;
+    const bool folded = tree.folded;
+    const uint32_t root = folded ? 0u : 1u;
+    if (N[root].kind == KIND_LEAF || N[root].arity == 0) return false;
+    auto column_of = [&](const DevNode &d) { return tree.label_perm.empty() ? d.label : tree.label_perm[d.label]; };
+    auto is_lp = [&](uint32_t v, uint32_t &base) {
+        const DevNode &d = N[v];
+        for (uint32_t c = 0; c < d.arity; ++c) {
+            const DevNode &w = N[d.first_child + c];
+            if (w.kind != KIND_LEAF) return false;
+            if (c == 0) base = column_of(w);
+            else if (column_of(w) != base + c) return false;
+        }
+        return true;
+    };
+    // non-LP internal nodes in BFS order, each with its first entry
+    std::vector<uint32_t> order{root}, depth{1}, first;
+    uint32_t nE = 0;
+    std::vector<uint32_t> first_of(N.size(), 0);
+    uint32_t rb = 0;
+    const bool root_lp = is_lp(root, rb);
+    if (!root_lp) {
+        for (size_t h = 0; h < order.size(); ++h) {
+            const uint32_t v = order[h];
+            const DevNode &d = N[v];
+            if (d.arity == 0 || d.arity > kRowsMaxArity) return false;
+            frames = std::max(frames, depth[h]);
+            first_of[v] = nE;
+            nE += d.arity;
+            for (uint32_t c = 0; c < d.arity; ++c) {
+                const uint32_t w = d.first_child + c;
+                uint32_t b;
+                if (N[w].kind == KIND_LEAF || is_lp(w, b)) continue;
+                order.push_back(w);
+                depth.push_back(depth[h] + 1);
+            }
+        }
+    } else if (N[root].arity > kRowsMaxArity) {
+        return false;
+    }
+    if (nE >= 0x10000 || 4 + (size_t)nE > kRowsMaxTableWords) return false;
+    auto entry = [&](uint32_t w, uint32_t &out) -> bool {
+        const DevNode &d = N[w];
+        if (d.kind == KIND_LEAF) {
+            const uint32_t col = column_of(d);
+            if (col >= 0x8000) return false;
+            out = 0x80000000u | col;
+            return true;
+        }
+        if (d.arity == 0 || d.arity > kRowsMaxArity) return false;
+        uint32_t b;
+        if (is_lp(w, b)) {
+            if (b + d.arity > 0x8000) return false;
+            out = 0xC0000000u | ((uint32_t)d.arity << 16) | b;
+            return true;
+        }
+        out = ((uint32_t)d.arity << 16) | first_of[w];
+        return true;
+    };
+    t2.assign(4 + nE, 0);
+    if (!entry(root, t2[0])) return false;
+    t2[1] = nE;
+    t2[2] = frames;
+    if (!root_lp)
+        for (const uint32_t v : order) {
+            const DevNode &d = N[v];
+            for (uint32_t c = 0; c < d.arity; ++c)
+                if (!entry(d.first_child + c, t2[4 + first_of[v] + c])) return false;
+        }
+    return true;
+}
+
 namespace {
 
 // ------------------------------------------------------------------------
@@ -448,6 +533,7 @@ void free_rows(RowsImage &r) {
     if (r.spill) (void)hipFree(r.spill);
     if (r.d_spill_used) (void)hipFree(r.d_spill_used);
     if (r.d_table) (void)hipFree(r.d_table);
+    if (r.d_table2) (void)hipFree(r.d_table2);
     r = RowsImage();
 }
 
@@ -515,7 +601,8 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         return MBRWT_ERR_INVALID;
     }
     if (im.table.empty()) {
-        if (!build_rwt_table(range.tree, im.table, im.height)) {
+        if (!build_rwt_table(range.tree, im.table, im.height) || !build_rwt2_table(range.tree, im.table2, im.frames)) {
+            im.table.clear();
             set_error("tree shape outside the row-record limits (arity <= 16, columns < 2^15, height <= 16)");
             return MBRWT_ERR_UNSUPPORTED;
         }
@@ -631,7 +718,9 @@ int rows_build_finish(RowsBuild *rbp) {
         rc = MBRWT_ERR_UNSUPPORTED;
     }
     if (!rc && (hipMalloc(&im.d_table, im.table.size() * 4) != hipSuccess ||
-                hipMemcpy(im.d_table, im.table.data(), im.table.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
+                hipMemcpy(im.d_table, im.table.data(), im.table.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMalloc(&im.d_table2, im.table2.size() * 4) != hipSuccess ||
+                hipMemcpy(im.d_table2, im.table2.data(), im.table2.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
         rc = hip_fail(hipGetLastError(), "row-record table upload");
     if (rc) {
         rows_build_abort(rbp);
@@ -743,6 +832,8 @@ struct RowsParams {
     uint32_t *tile_counts;        // [tiles] labels (bit 31: the tile goes to the direct pass)
     uint32_t *ovf_list;           // batch indices of the rows of direct tiles
     unsigned long long *scalars;  // [1] direct rows, [2] error flags
+    uint32_t diag;                // MBRWT_ROWS_DIAG (timing experiments; WRONG results): 1 no walk,
+                                  // 2 walk without label stores, 4 no spill reads
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -904,6 +995,326 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
             if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(r0 + lane));
         }
         wave_sync();  // the slots and the stage are reused
+    }
+}
+
+// k_traverse_rows (v2, the default): the RWT2 table (one word per child,
+// leaf parents with consecutive columns expanded inline: no table word, no
+// frame, all their labels in one iteration), labels stored straight into the
+// tile's temp region (no LDS stage: the slots are the only per-wave LDS, so 8
+// waves per SIMD fit), and the next tile's row ids requested before the
+// current tile's walk.
+template <int MAXD>
+__device__ __forceinline__ void rows_walk2(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
+                                           const AS_LDS uint32_t *ent, uint16_t *out, uint32_t pos,
+                                           bool store = true) {
+    // the root: an internal node (a frame) or, for a one-level tree, a leaf parent
+    const uint32_t ra = (root >> 16) & 0x1Fu;
+    const uint32_t rw = ra > 8 ? 1u : 0u;
+    const uint32_t rm = (uint32_t)pb[o] | (rw ? (uint32_t)pb[o + 1] << 8 : 0u);
+    o += 1 + rw;
+    if ((root >> 30) == 3u) {  // root is a leaf parent: label = first column + bit
+        if (live)
+            for (uint32_t x = rm; x; x &= x - 1) gst(out + pos++, (uint16_t)((root & 0xFFFFu) + (uint32_t)__builtin_ctz(x)));
+        return;
+    }
+    uint32_t top = live ? ((root & 0xFFFFu) | (rm << 16)) : 0u;
+    uint32_t st[MAXD > 1 ? MAXD - 1 : 1];
+#pragma unroll
+    for (int k = 0; k < (MAXD > 1 ? MAXD - 1 : 1); ++k) st[k] = 0;
+    uint32_t sp = 0;
+    bool done = (top >> 16) == 0;
+    while (__any(!done)) {
+        const uint32_t c = (uint32_t)__builtin_ctz((top >> 16) | 0x10000u);
+        top &= ~(0x10000u << c);
+        const uint32_t e = ent[done ? 0u : (top & 0xFFFFu) + c];
+        const bool leaf = (e >> 30) == 2u;
+        const bool lp = (e >> 30) == 3u;
+        const bool inner = !done && (e >> 31) == 0u;
+        const uint32_t w = ((e >> 16) & 0x1Fu) > 8 ? 1u : 0u;
+        const uint32_t mw = (uint32_t)pb[o] | (w ? (uint32_t)pb[o + 1] << 8 : 0u);
+        const bool reads = !done && !leaf;  // an internal node's or a leaf parent's mask
+        o += reads ? 1u + w : 0u;
+        if (!done && leaf) {
+            if (store) gst(out + pos, (uint16_t)(e & 0xFFFFu));
+            ++pos;
+        }
+        if (!done && lp)
+            for (uint32_t x = mw; x; x &= x - 1) {
+                if (store) gst(out + pos, (uint16_t)((e & 0xFFFFu) + (uint32_t)__builtin_ctz(x)));
+                ++pos;
+            }
+        if constexpr (MAXD > 1) {
+            const bool push = inner && (top >> 16) != 0;
+#pragma unroll
+            for (int k = MAXD - 2; k > 0; --k) st[k] = push ? st[k - 1] : st[k];
+            st[0] = push ? top : st[0];
+            sp += push ? 1u : 0u;
+        }
+        top = inner ? ((e & 0xFFFFu) | (mw << 16)) : top;
+        if constexpr (MAXD > 1) {
+            const bool pop = !done && (top >> 16) == 0 && sp > 0;
+            top = pop ? st[0] : top;
+#pragma unroll
+            for (int k = 0; k < MAXD - 2; ++k) st[k] = pop ? st[k + 1] : st[k];
+            sp -= pop ? 1u : 0u;
+        }
+        done = done || (top >> 16) == 0;
+    }
+}
+
+template <int B, int MAXD, int WPB, bool NT>
+__global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows2[];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_rows2[i] = gld(p.table + i);
+    __syncthreads();
+    const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows2[0]);
+    const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows2 + 4;
+    const uint32_t C = p.C;
+    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows2 + ((p.table_words + 3) & ~3u)) + wv * (64u * B);
+    AS_LDS uint8_t *mine = wb + lane * B;
+    constexpr uint32_t LPB = B / 16, RPI = 64 / LPB;
+    const uint64_t ntiles = (p.n + 63) / 64;
+    const uint64_t tstride = (uint64_t)gridDim.x * WPB;
+    const uint32_t S = p.S;
+    uint64_t t = (uint64_t)blockIdx.x * WPB + wv;
+    uint64_t row_n = 0;  // the row of this lane in the wave's next tile
+    if (t < ntiles && t * 64 + lane < p.n) row_n = gld(p.rows + t * 64 + lane);
+    for (; t < ntiles; t += tstride) {
+        const uint64_t r0 = t * 64;
+        const uint32_t nr = (uint32_t)(p.n - r0 < 64 ? p.n - r0 : 64);
+        const uint64_t row = row_n;
+        const uint64_t tn = t + tstride;
+        if (tn < ntiles && tn * 64 + lane < p.n) row_n = gld(p.rows + tn * 64 + lane);
+        const bool valid = lane < nr && row < p.num_rows;
+        if (lane < nr && !valid) atomicOr(&p.scalars[2], 1ull);
+        const uint64_t b = valid ? rows_block(row, S, p.magic) : 0;
+        const uint32_t sub = (uint32_t)(row - b * S);
+        const uint64_t addr = p.blocks + b * B;
+        u32x4_t q[LPB];
+#pragma unroll
+        for (uint32_t k = 0; k < LPB; ++k) {
+            const int src = (int)(RPI * k + lane / LPB);
+            const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)addr, src, 64);
+            const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(addr >> 32), src, 64);
+            q[k] = gld_at_nt<u32x4_t, NT>((((uint64_t)hi << 32) | lo) + 16u * (lane % LPB));
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < LPB; ++k) ((AS_LDS u32x4_t *)(wb + 1024 * k))[lane] = q[k];
+        wave_sync();
+        uint32_t cnt = 0, o = 0;
+        bool spl = false;
+        if (valid) {
+            const uint32_t e = mine[sub];
+            o = e & 0x7Fu;
+            spl = (e & 0x80u) != 0;
+            cnt = mine[o];
+            ++o;
+        }
+        bool lng = false;
+        if (__any(spl) && !(p.diag & 4)) {
+            if (spl) {
+                const uint32_t idx = (uint32_t)mine[o] | ((uint32_t)mine[o + 1] << 8) | ((uint32_t)mine[o + 2] << 16) |
+                                     ((uint32_t)mine[o + 3] << 24);
+                const uint64_t sa = p.spill + (uint64_t)idx * 16;
+                u32x4_t sq[LPB];
+#pragma unroll
+                for (uint32_t k = 0; k < LPB; ++k) sq[k] = gld_at<u32x4_t>(sa + 16u * k);
+#pragma unroll
+                for (uint32_t k = 0; k < LPB; ++k) ((AS_LDS u32x4_t *)mine)[k] = sq[k];
+                cnt = sq[0].x;
+                lng = 8 + sq[0].y > B;
+                o = 8;
+            }
+        }
+        uint32_t x = cnt;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+            if (lane >= d) x += y;
+        }
+        const uint32_t total = __builtin_amdgcn_readlane(x, 63);
+        const uint32_t pos = x - cnt;
+        const bool direct = total > C || __any(lng);
+        uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
+        if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
+        if (!direct && !(p.diag & 1))
+            rows_walk2<MAXD>(mine, o, valid && cnt > 0, root, ent, reinterpret_cast<uint16_t *>(treg + 128), pos,
+                             !(p.diag & 2));
+        if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u));
+        if (direct) {
+            unsigned long long k0 = 0;
+            if (lane == 0) k0 = atomicAdd(&p.scalars[1], (unsigned long long)nr);
+            k0 = (unsigned long long)__shfl((long long)k0, 0, 64);
+            if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(r0 + lane));
+        }
+        wave_sync();  // the slots are reused
+    }
+}
+
+// k_traverse_rows (v3, the default): v2's walk, software-pipelined over the
+// wave's tiles -- the blocks of tile t+1 (and the row ids of tile t+2) are
+// requested into registers BEFORE tile t is walked, and the spilled entries of
+// tile t+1 right after its blocks land, so the memory latency of the next
+// tile overlaps the walk of this one (v2 ran load phase, then walk phase:
+// diagnostics 0.22 ms of loads + 0.28 ms of walk per 8 M rows, not overlapped).
+template <int B>
+struct RowsTileIo {
+    static constexpr uint32_t LPB = B / 16, RPI = 64 / LPB;
+    // the 64 blocks of a tile as coalesced quarters (row RPI k + lane / LPB in load k)
+    template <bool NT>
+    static __device__ __forceinline__ void load(u32x4_t (&q)[LPB], uint64_t addr, uint32_t lane, bool any) {
+#pragma unroll
+        for (uint32_t k = 0; k < LPB; ++k) {
+            const int src = (int)(RPI * k + lane / LPB);
+            const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)addr, src, 64);
+            const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(addr >> 32), src, 64);
+            if (any) q[k] = gld_at_nt<u32x4_t, NT>((((uint64_t)hi << 32) | lo) + 16u * (lane % LPB));
+        }
+    }
+    static __device__ __forceinline__ void store(AS_LDS uint8_t *wb, const u32x4_t (&q)[LPB], uint32_t lane) {
+#pragma unroll
+        for (uint32_t k = 0; k < LPB; ++k) ((AS_LDS u32x4_t *)(wb + 1024 * k))[lane] = q[k];
+    }
+};
+
+template <int B, int MAXD, int WPB, bool NT>
+__global__ __launch_bounds__(64 * WPB) void k_traverse_rows3(RowsParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows3[];
+    using Io = RowsTileIo<B>;
+    constexpr uint32_t LPB = Io::LPB;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_rows3[i] = gld(p.table + i);
+    __syncthreads();
+    const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows3[0]);
+    const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows3 + 4;
+    const uint32_t C = p.C;
+    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows3 + ((p.table_words + 3) & ~3u)) + wv * (64u * B);
+    AS_LDS uint8_t *mine = wb + lane * B;
+    const uint64_t ntiles = (p.n + 63) / 64;
+    const uint64_t tstride = (uint64_t)gridDim.x * WPB;
+    const uint32_t S = p.S;
+    // tile t's row of this lane -> {valid, block address, slot index}
+    auto row_of = [&](uint64_t t, uint64_t &row) -> bool {
+        row = 0;
+        if (t >= ntiles || t * 64 + lane >= p.n) return false;
+        row = gld(p.rows + t * 64 + lane);
+        return true;
+    };
+    auto place = [&](uint64_t row, bool in, bool &valid, uint64_t &addr, uint32_t &sub) {
+        valid = in && row < p.num_rows;
+        if (in && !valid) atomicOr(&p.scalars[2], 1ull);
+        const uint64_t b = valid ? rows_block(row, S, p.magic) : 0;
+        sub = (uint32_t)(row - b * S);
+        addr = p.blocks + b * B;
+    };
+    // this lane's entry in its slot: label count, first mask byte, spilled?
+    auto parse = [&](bool valid, uint32_t sub, uint32_t &cnt, uint32_t &o, bool &spl, uint64_t &sa) {
+        cnt = 0;
+        o = 0;
+        spl = false;
+        sa = 0;
+        if (!valid) return;
+        const uint32_t e = mine[sub];
+        o = e & 0x7Fu;
+        spl = (e & 0x80u) != 0;
+        cnt = mine[o];
+        if (spl) {
+            const uint32_t idx = (uint32_t)mine[o + 1] | ((uint32_t)mine[o + 2] << 8) | ((uint32_t)mine[o + 3] << 16) |
+                                 ((uint32_t)mine[o + 4] << 24);
+            sa = p.spill + (uint64_t)idx * 16;
+        }
+        ++o;
+    };
+
+    uint64_t t = (uint64_t)blockIdx.x * WPB + wv;
+    if (t >= ntiles) return;
+    // prologue: tile t in the slots, its spill entries requested
+    uint64_t row;
+    bool in = row_of(t, row);
+    bool valid;
+    uint64_t addr;
+    uint32_t sub;
+    place(row, in, valid, addr, sub);
+    u32x4_t q[LPB];
+    Io::template load<NT>(q, addr, lane, true);
+    uint64_t row_n;
+    bool in_n = row_of(t + tstride, row_n);
+    Io::store(wb, q, lane);
+    wave_sync();
+    uint32_t cnt, o;
+    bool spl;
+    uint64_t sa;
+    parse(valid, sub, cnt, o, spl, sa);
+    u32x4_t sq[LPB];
+    bool any_spl = __any(spl) && !(p.diag & 4);
+    if (any_spl && spl) {
+#pragma unroll
+        for (uint32_t k = 0; k < LPB; ++k) sq[k] = gld_at<u32x4_t>(sa + 16u * k);
+    }
+    while (true) {
+        const uint64_t r0 = t * 64;
+        const uint32_t nr = (uint32_t)(p.n - r0 < 64 ? p.n - r0 : 64);
+        const uint64_t tn = t + tstride;
+        const bool more = tn < ntiles;  // wave-uniform
+        // the next tile's blocks and the row ids after it, in flight during this walk
+        bool valid_n;
+        uint64_t addr_n;
+        uint32_t sub_n;
+        place(row_n, in_n, valid_n, addr_n, sub_n);
+        u32x4_t qn[LPB];
+        Io::template load<NT>(qn, addr_n, lane, more);
+        uint64_t row_nn;
+        const bool in_nn = row_of(tn + tstride, row_nn);
+        // this tile's spilled entries replace the block in the lane's own slot
+        bool lng = false;
+        if (any_spl && spl) {
+#pragma unroll
+            for (uint32_t k = 0; k < LPB; ++k) ((AS_LDS u32x4_t *)mine)[k] = sq[k];
+            cnt = sq[0].x;
+            lng = 8 + sq[0].y > B;
+            o = 8;
+        }
+        uint32_t x = cnt;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+            if (lane >= d) x += y;
+        }
+        const uint32_t total = __builtin_amdgcn_readlane(x, 63);
+        const uint32_t pos = x - cnt;
+        const bool direct = total > C || __any(lng);
+        uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
+        if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
+        if (!direct && !(p.diag & 1))
+            rows_walk2<MAXD>(mine, o, valid && cnt > 0, root, ent, reinterpret_cast<uint16_t *>(treg + 128), pos,
+                             !(p.diag & 2));
+        if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u));
+        if (direct) {
+            unsigned long long k0 = 0;
+            if (lane == 0) k0 = atomicAdd(&p.scalars[1], (unsigned long long)nr);
+            k0 = (unsigned long long)__shfl((long long)k0, 0, 64);
+            if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(r0 + lane));
+        }
+        wave_sync();  // every lane is done with its slot
+        if (!more) break;
+        // the next tile into the slots; its spill entries requested
+        Io::store(wb, qn, lane);
+        wave_sync();
+        t = tn;
+        valid = valid_n;
+        sub = sub_n;
+        row_n = row_nn;
+        in_n = in_nn;
+        parse(valid, sub, cnt, o, spl, sa);
+        any_spl = __any(spl) && !(p.diag & 4);
+        if (any_spl && spl) {
+#pragma unroll
+            for (uint32_t k = 0; k < LPB; ++k) sq[k] = gld_at<u32x4_t>(sa + 16u * k);
+        }
     }
 }
 
@@ -1093,6 +1504,32 @@ RowsView view_of(const Ctx &c) {
 
 using RowsFn = void (*)(RowsParams);
 constexpr uint32_t kRowsWpb = 4;
+constexpr uint32_t kRows2Wpb = 8;
+constexpr uint32_t kRows3Wpb = 4;  // (72 VGPRs: 7 waves per SIMD in 4-wave workgroups)
+// MBRWT_ROWS_KERNEL=1 / 2: the first / second version, for A/B (3 = default)
+int rows_version() {
+    const char *e = std::getenv("MBRWT_ROWS_KERNEL");
+    return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 3;
+}
+bool rows_v1() { return rows_version() == 1; }
+template <int B, bool NT, int V>
+RowsFn rows2_fn_d(uint32_t frames) {
+    if constexpr (V == 2)
+        return frames <= 4 ? k_traverse_rows2<B, 4, kRows2Wpb, NT>
+               : frames <= 8 ? k_traverse_rows2<B, 8, kRows2Wpb, NT>
+                             : k_traverse_rows2<B, 16, kRows2Wpb, NT>;
+    else
+        return frames <= 4 ? k_traverse_rows3<B, 4, kRows3Wpb, NT>
+               : frames <= 8 ? k_traverse_rows3<B, 8, kRows3Wpb, NT>
+                             : k_traverse_rows3<B, 16, kRows3Wpb, NT>;
+}
+template <int V>
+RowsFn rows2_fn_v(const RowsImage &im) {
+    const bool nt = im.bytes > (1ull << 30);
+    if (im.B == 64) return nt ? rows2_fn_d<64, true, V>(im.frames) : rows2_fn_d<64, false, V>(im.frames);
+    return nt ? rows2_fn_d<128, true, V>(im.frames) : rows2_fn_d<128, false, V>(im.frames);
+}
+RowsFn rows2_fn(const RowsImage &im) { return rows_version() == 2 ? rows2_fn_v<2>(im) : rows2_fn_v<3>(im); }
 
 template <int B, bool NT>
 RowsFn rows_fn_d(uint32_t height) {
@@ -1158,17 +1595,21 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     p.spill = (uint64_t)(uintptr_t)im.spill;
     p.magic = im.magic;
     p.S = im.S;
-    p.table_words = (uint32_t)im.table.size();
-    p.table = im.d_table;
+    const bool v1 = rows_v1();
+    p.table_words = (uint32_t)(v1 ? im.table.size() : im.table2.size());
+    p.table = v1 ? im.d_table : im.d_table2;
     p.C = C;
     p.temp = reinterpret_cast<uint8_t *>(c.ws_temp.buf);
     p.tile_counts = d_tc;
     p.ovf_list = reinterpret_cast<uint32_t *>(c.ws_ovf.buf);
     p.scalars = reinterpret_cast<unsigned long long *>(c.d_scalars);
+    if (const char *e = std::getenv("MBRWT_ROWS_DIAG")) p.diag = (uint32_t)std::atoi(e);
 
-    const RowsFn kfn = rows_fn(im);
-    const size_t lds = ((im.table.size() + 3) & ~size_t(3)) * 4 + kRowsWpb * (64ull * im.B + 2ull * C);
-    const uint32_t threads = 64 * kRowsWpb;
+    const RowsFn kfn = v1 ? rows_fn(im) : rows2_fn(im);
+    const uint32_t wpb = v1 ? kRowsWpb : rows_version() == 2 ? kRows2Wpb : kRows3Wpb;
+    const size_t lds = v1 ? ((im.table.size() + 3) & ~size_t(3)) * 4 + kRowsWpb * (64ull * im.B + 2ull * C)
+                          : ((im.table2.size() + 3) & ~size_t(3)) * 4 + wpb * 64ull * im.B;
+    const uint32_t threads = 64 * wpb;
     if (c.rb_fn != reinterpret_cast<const void *>(kfn) || c.rb_lds != lds || c.rb_threads != threads) {
         if (lds > 65536)
             MBRWT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kfn),
@@ -1184,7 +1625,7 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         c.rb_threads = threads;
         c.rb_blocks = std::max(1, dev_cus) * per_cu;
     }
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((nt + kRowsWpb - 1) / kRowsWpb, (uint64_t)c.rb_blocks));
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((nt + wpb - 1) / wpb, (uint64_t)c.rb_blocks));
 
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
     MBRWT_HIP(hipMemsetAsync(d_tc + nt, 0, sizeof(uint32_t), s));

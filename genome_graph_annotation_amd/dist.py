@@ -7,16 +7,16 @@ slice and the per-row label sets are reassembled into one global CSR by an
 all-gatherv over RCCL (backend "nccl" on ROCm).
 
 RCCL has no all-gatherv, so the exchange is:
-  1. one tiny all-gather of every rank's (rows, labels) sizes (the only host
-     synchronisation);
+  1. one tiny all-gather of every rank's (rows, labels) sizes -- host
+     integers over a CPU (gloo) group, so no device read-back;
   2. ONE all_gather_into_tensor of a packed byte buffer per rank, padded to
      the largest rank: [per-row label counts | labels], both bit-packed at
      ceil(log2(num_columns)) bits (mbrwt_pack_ids_device) -- the Kingsford
      shape (2,652 columns) ships 12 bits per label and per row instead of
      32 + 64, i.e. ~2.9x fewer bytes over xGMI than u32 labels + u64 offsets;
-  3. unpacking with contiguous slice copies: one scan of the gathered counts
-     gives the global offsets, each rank's label slice is widened into its
-     place of the global label array.
+  3. unpacking every rank's segment in ONE launch per array
+     (mbrwt_unpack_segments_device: counts, then labels widened to int32 in
+     their global places) and one scan of the counts for the global offsets.
 AllGatherV splits 1-2 from 3 so that a batch's exchange overlaps the next
 batch's traversal (bench.py pipelines its steps this way); on GPUs the
 unpacking is queued behind the all-gather on a side stream and overlaps too.
@@ -98,27 +98,49 @@ def _unpack(words: torch.Tensor, n: int, bits: int, out_values: torch.Tensor):
 
 class AllGatherV:
     """One all-gatherv of per-rank CSR slices, split so that the exchange can
-    overlap the next batch's traversal: start() exchanges the sizes (the only
-    host synchronisation), packs the wire buffer and launches the all-gather
-    asynchronously; finish() waits for it and unpacks.  Between the two the
-    caller may run other GPU work on the current stream (RCCL runs the
-    all-gather on its own stream)."""
+    overlap the next batch's traversal: start() exchanges the sizes, packs the
+    wire buffer and launches the all-gather asynchronously; finish() waits for
+    it and unpacks.  Between the two the caller may run other GPU work on the
+    current stream (RCCL runs the all-gather on its own stream).
 
-    def __init__(self, offsets: torch.Tensor, cols: torch.Tensor, n_labels=None, num_columns=None, group=None):
+    size_group: a CPU (gloo) process group for the sizes exchange -- host
+    integers the caller already has (get_rows_device returns the label count),
+    so a GPU step synchronises the host once (inside get_rows) instead of
+    also reading the sizes back from the device.  timing: HIP events around
+    the pack, the all-gather and the unpack (phases())."""
+
+    def __init__(self, offsets: torch.Tensor, cols: torch.Tensor, n_labels=None, num_columns=None, group=None,
+                 size_group=None, timing=False):
+        import time
         self.group = group
         world = dist.get_world_size(group)
         dev = offsets.device
         n_r = offsets.numel() - 1
         l_r = int(offsets[-1].item()) if n_labels is None else int(n_labels)
-        sizes = torch.tensor([n_r, l_r], dtype=torch.int64, device=dev)
-        all_sizes = torch.empty(world * 2, dtype=torch.int64, device=dev)
-        _all_gather(all_sizes, sizes, group)
-        table = all_sizes.view(world, 2).cpu().tolist()
+        h0 = time.perf_counter()
+        if size_group is not None or dev.type != "cuda":
+            sizes = torch.tensor([n_r, l_r], dtype=torch.int64)
+            parts = [torch.empty(2, dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(parts, sizes, group=size_group if size_group is not None else group)
+            table = [p.tolist() for p in parts]
+        else:
+            sizes = torch.tensor([n_r, l_r], dtype=torch.int64, device=dev)
+            all_sizes = torch.empty(world * 2, dtype=torch.int64, device=dev)
+            _all_gather(all_sizes, sizes, group)
+            table = all_sizes.view(world, 2).cpu().tolist()
+        self.sizes_ms = (time.perf_counter() - h0) * 1e3
         self.ns, self.ls = [t[0] for t in table], [t[1] for t in table]
         max_n, max_l = max(self.ns), max(self.ls)
         self.bits_l, self.bits_c = wire_bits(num_columns)
         self.cnt_bytes = _round16(max(1, _words(max_n, self.bits_c)) * 4)
         self.per = self.cnt_bytes + _round16(max(1, _words(max_l, self.bits_l)) * 4)
+        self.wire_bytes = self.per  # sent by this rank (received: (world - 1) x per)
+        cuda = dev.type == "cuda"
+        self.ev = {}
+        if cuda and timing:
+            for k in ("t0", "packed", "gathered", "done"):
+                self.ev[k] = torch.cuda.Event(enable_timing=True)
+            self.ev["t0"].record(torch.cuda.current_stream(dev))
         # pack: row counts (offsets deltas), then labels, bit-packed
         send = torch.empty(self.per, dtype=torch.uint8, device=dev)
         if n_r:
@@ -126,6 +148,8 @@ class AllGatherV:
             _pack(cnt, n_r, self.bits_c, send[:self.cnt_bytes].view(torch.int32))
         if l_r:
             _pack(cols, l_r, self.bits_l, send[self.cnt_bytes:].view(torch.int32))
+        if self.ev:
+            self.ev["packed"].record(torch.cuda.current_stream(dev))
         self.recv = torch.empty(world * self.per, dtype=torch.uint8, device=dev)
         self.send = send  # kept alive until the exchange is done
         if dist.get_backend(group) == "nccl":
@@ -134,15 +158,17 @@ class AllGatherV:
             self.work = dist.all_gather(list(self.recv.chunk(world)), send, group=group, async_op=True)
         self.result = None
         self.done = None
-        if dev.type == "cuda":
+        if cuda:
             # the unpacking is queued right behind the all-gather on a side
             # stream, so it too overlaps whatever the caller runs next
             side = _side_stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 self.work.wait()
+                if self.ev:
+                    self.ev["gathered"].record(side)
                 self.result = self._unpack()
-                self.done = torch.cuda.Event()
+                self.done = self.ev["done"] if self.ev else torch.cuda.Event()
                 self.done.record(side)
             for t in (self.send, self.recv):
                 t.record_stream(side)
@@ -161,20 +187,46 @@ class AllGatherV:
         self.send = self.recv = self.result = None
         return g_off, g_cols
 
+    def phases(self):
+        """Device times (ms) of the exchange's phases -- pack, all-gather
+        (from the packed buffer to the gathered one: RCCL's time plus any
+        wait for the stream), unpack -- and the host time of the sizes
+        exchange; valid once the exchange has completed (timing=True)."""
+        out = {"sizes_host_ms": self.sizes_ms}
+        if self.ev:
+            self.ev["done"].synchronize()
+            out["pack_ms"] = self.ev["t0"].elapsed_time(self.ev["packed"])
+            out["all_gather_ms"] = self.ev["packed"].elapsed_time(self.ev["gathered"])
+            out["unpack_ms"] = self.ev["gathered"].elapsed_time(self.ev["done"])
+        return out
+
     def _unpack(self):
         world = len(self.ns)
         dev = self.recv.device
-        R = self.recv.view(world, self.per)
-        # unpack: global offsets by one scan over the ranks' counts in rank order
         N, L = sum(self.ns), sum(self.ls)
         g_cnt = torch.empty(max(1, N), dtype=torch.int32, device=dev)
         g_cols = torch.empty(L, dtype=torch.int32, device=dev)
-        rb = lb = 0
-        for r in range(world):
-            _unpack(R[r, :self.cnt_bytes].view(torch.int32), self.ns[r], self.bits_c, g_cnt[rb:])
-            _unpack(R[r, self.cnt_bytes:].view(torch.int32), self.ls[r], self.bits_l, g_cols[lb:])
-            rb += self.ns[r]
-            lb += self.ls[r]
+        if dev.type == "cuda":
+            # every rank's segment in one launch each (include/mbrwt.h
+            # mbrwt_unpack_segments_device): counts, then labels
+            import ctypes as C
+            from . import _lib as LB
+            s = torch.cuda.current_stream(dev).cuda_stream
+            base = self.recv.data_ptr()
+            for off, counts, bits, out in ((0, self.ns, self.bits_c, g_cnt),
+                                           (self.cnt_bytes, self.ls, self.bits_l, g_cols)):
+                arr = (C.c_uint64 * world)(*counts)
+                LB.check(LB.lib().mbrwt_unpack_segments_device(base + off, world, self.per, arr, bits,
+                                                               out.data_ptr(), s), "mbrwt_unpack_segments_device")
+        else:
+            R = self.recv.view(world, self.per)
+            rb = lb = 0
+            for r in range(world):
+                _unpack(R[r, :self.cnt_bytes].view(torch.int32), self.ns[r], self.bits_c, g_cnt[rb:])
+                _unpack(R[r, self.cnt_bytes:].view(torch.int32), self.ls[r], self.bits_l, g_cols[lb:])
+                rb += self.ns[r]
+                lb += self.ls[r]
+        # global offsets: one scan of the gathered counts in rank order
         g_off = torch.zeros(N + 1, dtype=torch.int64, device=dev)
         if N:
             torch.cumsum(g_cnt[:N], 0, dtype=torch.int64, out=g_off[1:])
@@ -190,11 +242,12 @@ def _side_stream(dev):
     return _SIDE[dev]
 
 
-def allgatherv_csr(offsets: torch.Tensor, cols: torch.Tensor, n_labels=None, num_columns=None, group=None):
+def allgatherv_csr(offsets: torch.Tensor, cols: torch.Tensor, n_labels=None, num_columns=None, group=None,
+                   size_group=None):
     """Reassemble per-rank CSR slices (offsets: int64 [n_r + 1] starting at 0;
     cols: int32 [>= offsets[-1]]) into the global CSR of the concatenated
     batch, on every rank.  `n_labels` (= offsets[-1], if the caller already
     has it on the host) saves a device read; `num_columns` (the same on every
     rank) sets the wire's bit width.  Returns (offsets [N + 1] int64,
     cols [L] int32)."""
-    return AllGatherV(offsets, cols, n_labels, num_columns, group).finish()
+    return AllGatherV(offsets, cols, n_labels, num_columns, group, size_group).finish()

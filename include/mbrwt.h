@@ -334,6 +334,12 @@ int mbrwt_count_work_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, 
  */
 int mbrwt_pack_ids_device(const uint32_t *d_values, uint64_t n, uint32_t bits, uint32_t *d_words, void *stream);
 int mbrwt_unpack_ids_device(const uint32_t *d_words, uint64_t n, uint32_t bits, uint32_t *d_values, void *stream);
+/* The unpacking of a whole all-gathered wire buffer in one launch: segment r
+   (r < nseg) starts at d_base + r * seg_stride bytes (a multiple of 4) and
+   holds counts[r] (host array) packed values; they are written to d_values
+   back to back in segment order. */
+int mbrwt_unpack_segments_device(const void *d_base, uint32_t nseg, uint64_t seg_stride, const uint64_t *counts,
+                                 uint32_t bits, uint32_t *d_values, void *stream);
 
 #define MBRWT_OPT_TIMING 1       /* 1: time the traversal kernel with HIP events */
 #define MBRWT_OPT_SLOT_LABELS 2  /* per-row label slots of the fast path (0 = auto) */

@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_rows.py -k "not beyond" > gpurun_out/rows_tests.log 2>&1 || exit 1
+timeout -k 10 300 python -u tools/rows_ab.py --rows 3700000000 --batch 8000000 --configs "rows@+v2+diag1+diag2;rows:128,4@+v2" > gpurun_out/v3_c4.log 2>&1 || exit 1
+timeout -k 10 120 python -u tools/rows_ab.py --rows 1000000 --batch 1000000 --configs "rows@+v2" > gpurun_out/v3_c2.log 2>&1 || exit 1

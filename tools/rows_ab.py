@@ -1,0 +1,102 @@
+"""Layout A/B on one synthetic structure (calibration tool, not the bench):
+builds the same tree as per-node images and as row records (several block
+shapes), times get_rows on the same batch and checks that every
+configuration returns the identical CSR.
+
+    python tools/rows_ab.py --rows 3700000000 --batch 8000000 --configs nodes,rows,rows:64,2,rows:128,4
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from genome_graph_annotation_amd import BRWTDevice, _lib as L  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--rows", type=int, default=3_700_000_000)
+ap.add_argument("--cols", type=int, default=2652)
+ap.add_argument("--density", type=float, default=0.003)
+ap.add_argument("--arity", type=int, default=8)
+ap.add_argument("--batch", type=int, default=8_000_000)
+ap.add_argument("--steps", type=int, default=10)
+ap.add_argument("--seed", type=int, default=42)
+ap.add_argument("--shape", default="", help="npz with num_children/first_child/leaf_column: synthetic_shaped")
+ap.add_argument("--configs", default="nodes,rows")
+a = ap.parse_args()
+
+rows_np = np.random.default_rng(a.seed).integers(0, a.rows, a.batch, dtype=np.uint64)
+rows = torch.from_numpy(rows_np.view(np.int64)).cuda()
+off = torch.empty(a.batch + 1, dtype=torch.int64, device="cuda")
+s = torch.cuda.current_stream().cuda_stream
+shape = dict(np.load(a.shape)) if a.shape else None
+ref = None
+cols = None
+def set_variant(kv):
+    """'' default, 'v1' / 'v2' the first / second row-record kernel, 'diagN' MBRWT_ROWS_DIAG=N"""
+    os.environ.pop("MBRWT_ROWS_KERNEL", None)
+    os.environ.pop("MBRWT_ROWS_DIAG", None)
+    if kv in ("v1", "v2"):
+        os.environ["MBRWT_ROWS_KERNEL"] = kv[1]
+    elif kv.startswith("diag"):
+        os.environ["MBRWT_ROWS_DIAG"] = kv[4:]
+
+
+# config = layout[:B,S][@variant+variant...]: one build, every variant timed on it
+for cfg in a.configs.split(";") if ";" in a.configs else a.configs.split(","):
+    cfg_k, _, kvs = cfg.partition("@")
+    layout, _, bs = cfg_k.partition(":")
+    if bs:
+        os.environ["MBRWT_ROWS_BS"] = bs
+    else:
+        os.environ.pop("MBRWT_ROWS_BS", None)
+    set_variant("")
+    t0 = time.time()
+    if shape is not None:
+        m = BRWTDevice.synthetic_shaped(a.rows, shape, a.density, a.seed, layout=layout)
+    else:
+        m = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, layout=layout)
+    build_s = time.time() - t0
+    if cols is None:
+        try:
+            need = m.get_rows_device(rows, off, torch.empty(1, dtype=torch.int32, device="cuda"), s)
+        except L.MBRWTError as e:
+            need = e.needed
+        cols = torch.empty(int(need) + 1024, dtype=torch.int32, device="cuda")
+    for kv in (kvs.split("+") if kvs else [""]):
+        set_variant(kv)
+        for _ in range(3):
+            nl = m.get_rows_device(rows, off, cols, s)
+        torch.cuda.synchronize()
+        h = hashlib.blake2b(digest_size=8)
+        h.update(off.cpu().numpy().tobytes())
+        h.update(cols[:nl].cpu().numpy().tobytes())
+        hx = h.hexdigest()
+        if ref is None:
+            ref = hx
+        m.take_timing()
+        m.set_option(L.MBRWT_OPT_TIMING, 1)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(a.steps):
+            m.get_rows_device(rows, off, cols, s)
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t1) / a.steps
+        m.set_option(L.MBRWT_OPT_TIMING, 0)
+        kms, k = m.take_timing()
+        out = {"config": cfg_k + ("@" + kv if kv else ""), "kernel": m.traverse_kernel(), "layout": m.layout(),
+               "build_s": round(build_s, 1), "device_gb": m.device_bytes() / 1e9, "kernel_ms": kms / max(1, k),
+               "step_ms": el * 1e3, "rows_per_s": a.batch / el, "labels": int(nl), "csr_hash": hx,
+               "same_as_first": hx == ref, "rows_stats": m.rows_stats()}
+        print(json.dumps(out), flush=True)
+        if hx != ref and not kv.startswith("diag"):
+            print("MISMATCH", flush=True)
+            sys.exit(1)
+    set_variant("")
+    del m
+    torch.cuda.empty_cache()
