@@ -7,6 +7,6 @@ and bench.py; there is no CPU fallback anywhere in the package.
 """
 from ._lib import MBRWTError, lib  # noqa: F401
 from .binrel_wt import BinRelWTDevice  # noqa: F401
-from .brwt import BRWTDevice  # noqa: F401
+from .brwt import BRWTDevice, BRWTMulti  # noqa: F401
 
-__all__ = ["BRWTDevice", "BinRelWTDevice", "MBRWTError", "lib"]
+__all__ = ["BRWTDevice", "BRWTMulti", "BinRelWTDevice", "MBRWTError", "lib"]

@@ -123,6 +123,16 @@ SIGNATURES = {
                                                C.c_void_p]),
     "mbrwt_destroy": (None, [C.c_void_p]),
     "mbrwt_set_build_option": (C.c_int, [C.c_int, C.c_int64]),
+    "mbrwt_multi_create": (C.c_int, [C.POINTER(TreeDesc), C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_void_p)]),
+    "mbrwt_multi_create_synthetic": (C.c_int, [C.POINTER(SynthDesc), C.POINTER(C.c_int), C.c_int,
+                                               C.POINTER(C.c_void_p)]),
+    "mbrwt_multi_load": (C.c_int, [u8p, C.c_uint64, u64p, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_void_p)]),
+    "mbrwt_multi_destroy": (None, [C.c_void_p]),
+    "mbrwt_multi_size": (C.c_int, [C.c_void_p]),
+    "mbrwt_multi_replica": (C.c_void_p, [C.c_void_p, C.c_int]),
+    "mbrwt_multi_get_rows": (C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p, u32p, C.c_uint64, u64p]),
+    "mbrwt_multi_get_rows_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                              C.c_uint64, u64p, C.c_void_p]),
     "mbrwt_layout": (C.c_int, [C.c_void_p]),
     "mbrwt_rows_stats": (C.c_int, [C.c_void_p, u64p]),
     "mbrwt_tree_parse": (C.c_int, [u8p, C.c_uint64, u64p, C.POINTER(C.c_void_p)]),
@@ -141,6 +151,8 @@ SIGNATURES = {
     "mbrwt_get_rows": (C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p, u32p, C.c_uint64, u64p]),
     "mbrwt_get_rows_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
                                         u64p, C.c_void_p]),
+    "mbrwt_get_rows_device_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                              C.c_uint64, C.c_void_p, C.c_void_p]),
     "mbrwt_get_column": (C.c_int, [C.c_void_p, C.c_uint64, u64p, C.c_uint64, u64p]),
     "mbrwt_get_column_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, u64p, C.c_void_p]),
     "mbrwt_get_batch": (C.c_int, [C.c_void_p, u64p, u64p, C.c_uint64, u8p]),

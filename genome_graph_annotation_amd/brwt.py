@@ -365,6 +365,13 @@ class BRWTDevice:
         L.check(st, "mbrwt_get_rows_device")
         return int(need.value)
 
+    def get_rows_device_async(self, rows_t, offsets_t, cols_t, status_t, stream=None):
+        """mbrwt_get_rows_device_async: enqueue only; status_t (device, 3 x
+        int64) receives {labels needed, status, sticky status bits}."""
+        L.check(L.lib().mbrwt_get_rows_device_async(self._h, rows_t.data_ptr(), rows_t.numel(), offsets_t.data_ptr(),
+                                                    cols_t.data_ptr(), cols_t.numel(), status_t.data_ptr(), stream),
+                "mbrwt_get_rows_device_async")
+
     def get_batch_device(self, rows_t, cols_t, out_t, stream=None):
         L.check(L.lib().mbrwt_get_batch_device(self._h, rows_t.data_ptr(), cols_t.data_ptr(), rows_t.numel(),
                                                out_t.data_ptr(), stream), "mbrwt_get_batch_device")
@@ -437,3 +444,87 @@ class BRWTDevice:
         k = C.c_uint64(0)
         L.check(L.lib().mbrwt_take_timing(self._h, C.byref(ms), C.byref(k)), "mbrwt_take_timing")
         return ms.value, int(k.value)
+
+
+class BRWTMulti:
+    """One replica per device, get_rows over all of them (include/mbrwt.h
+    "multi-device"): the batch is cut into contiguous slices, one per replica,
+    and reassembled into one CSR."""
+
+    def __init__(self, handle, keepalive=None):
+        self._h = handle
+        self._keep = keepalive
+
+    @classmethod
+    def from_tree(cls, tree, devices=(0,), layout=None):
+        lib = L.lib()
+        d, keep = tree_desc(tree)
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        with build_layout(layout):
+            L.check(lib.mbrwt_multi_create(C.byref(d), devs, len(devices), C.byref(h)), "mbrwt_multi_create")
+        return cls(h)
+
+    @classmethod
+    def synthetic(cls, num_rows, num_columns, density, arity=8, seed=42, devices=(0,), layout=None):
+        lib = L.lib()
+        d = L.SynthDesc(num_rows, num_columns, float(density), arity, seed)
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        with build_layout(layout):
+            L.check(lib.mbrwt_multi_create_synthetic(C.byref(d), devs, len(devices), C.byref(h)),
+                    "mbrwt_multi_create_synthetic")
+        return cls(h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            L.lib().mbrwt_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def size(self):
+        return L.lib().mbrwt_multi_size(self._h)
+
+    def replica(self, i):
+        """Replica i as a BRWTDevice view (owned by this handle)."""
+        h = L.lib().mbrwt_multi_replica(self._h, i)
+        if not h:
+            raise IndexError(i)
+        dev = BRWTDevice.__new__(BRWTDevice)
+        dev._h = C.c_void_p(h)
+        dev._keep = self
+        dev.close = lambda: None  # the multi handle owns it
+        return dev
+
+    def get_rows(self, rows):
+        lib = L.lib()
+        rows = np.ascontiguousarray(rows, dtype=np.uint64)
+        n = len(rows)
+        offsets = np.zeros(n + 1, dtype=np.uint64)
+        need = C.c_uint64(0)
+        cap = max(16, n * 16)
+        while True:
+            cols = np.zeros(cap, dtype=np.uint32)
+            st = lib.mbrwt_multi_get_rows(self._h, _p(rows, C.c_uint64), n, _p(offsets, C.c_uint64),
+                                          _p(cols, C.c_uint32), cap, C.byref(need))
+            if st == L.MBRWT_ERR_CAPACITY:
+                cap = int(need.value)
+                continue
+            L.check(st, "mbrwt_multi_get_rows")
+            return offsets, cols[: need.value]
+
+    def get_rows_device(self, rows_t, offsets_t, cols_t, stream=None):
+        need = C.c_uint64(0)
+        st = L.lib().mbrwt_multi_get_rows_device(self._h, rows_t.data_ptr(), rows_t.numel(), offsets_t.data_ptr(),
+                                                 cols_t.data_ptr(), cols_t.numel(), C.byref(need), stream)
+        if st == L.MBRWT_ERR_CAPACITY:
+            e = L.MBRWTError(st, "mbrwt_multi_get_rows_device")
+            e.needed = int(need.value)
+            raise e
+        L.check(st, "mbrwt_multi_get_rows_device")
+        return int(need.value)

@@ -371,4 +371,120 @@ class BRWTDevice : public BinaryMatrix {
     BRWTDevice &operator=(const BRWTDevice &) = default;
 };
 
+// A BRWT replicated on several GPUs of one process (mbrwt_multi_*): get_rows
+// batches are cut into one contiguous slice per replica and reassembled into
+// one CSR; point and column queries and serialisation use replica 0.  The
+// reference's `annograph classify` (one process, a ThreadPool,
+// main.cpp:462-497) runs StaticBinRelAnnotator<BRWTMultiDevice> to use every
+// GPU of the node.
+class BRWTMultiDevice : public BinaryMatrix {
+  public:
+    BRWTMultiDevice() = default;
+    BRWTMultiDevice(const mbrwt_tree_desc &desc, const std::vector<int> &devices) {
+        mbrwt_multi *m = nullptr;
+        check_status(mbrwt_multi_create(&desc, devices.data(), (int)devices.size(), &m), "mbrwt_multi_create");
+        m_.reset(m, Deleter());
+    }
+    static BRWTMultiDevice synthetic(const mbrwt_synth_desc &desc, const std::vector<int> &devices) {
+        BRWTMultiDevice x;
+        mbrwt_multi *m = nullptr;
+        check_status(mbrwt_multi_create_synthetic(&desc, devices.data(), (int)devices.size(), &m),
+                     "mbrwt_multi_create_synthetic");
+        x.m_.reset(m, Deleter());
+        return x;
+    }
+    explicit BRWTMultiDevice(const std::vector<int> &devices) : devices_(devices) {}
+
+    int replicas() const { return m_ ? mbrwt_multi_size(m_.get()) : 0; }
+
+    uint64_t num_columns() const override { return m_ ? mbrwt_num_columns(r0()) : 0; }
+    uint64_t num_rows() const override { return m_ ? mbrwt_num_rows(r0()) : 0; }
+    uint64_t num_relations() const override { return m_ ? mbrwt_num_relations(r0()) : 0; }
+
+    bool get(Row row, Column column) const override {
+        if (!m_) throw std::out_of_range("get on an empty BRWT");
+        uint8_t out = 0;
+        check_status(mbrwt_get_batch(r0(), &row, &column, 1, &out), "BRWTMultiDevice::get");
+        return out != 0;
+    }
+    std::vector<Column> get_row(Row row) const override { return get_rows({row}).at(0); }
+    std::vector<Row> get_column(Column column) const override {
+        if (!m_) throw std::out_of_range("get_column on an empty BRWT");
+        uint64_t need = 0;
+        int st = mbrwt_get_column(r0(), column, nullptr, 0, &need);
+        std::vector<Row> rows;
+        if (st == MBRWT_OK) return rows;
+        if (st != MBRWT_ERR_CAPACITY) check_status(st, "BRWTMultiDevice::get_column");
+        rows.resize(need);
+        check_status(mbrwt_get_column(r0(), column, rows.data(), rows.size(), &need), "BRWTMultiDevice::get_column");
+        rows.resize(need);
+        return rows;
+    }
+    std::vector<std::vector<Column>> get_rows(const std::vector<Row> &rows) const override {
+        std::vector<uint64_t> offsets;
+        std::vector<uint32_t> cols;
+        get_rows_csr(rows, &offsets, &cols);
+        std::vector<std::vector<Column>> out(rows.size());
+        for (size_t i = 0; i < rows.size(); ++i) out[i].assign(cols.begin() + offsets[i], cols.begin() + offsets[i + 1]);
+        return out;
+    }
+    void get_rows_csr(const std::vector<Row> &rows, std::vector<uint64_t> *offsets, std::vector<uint32_t> *cols) const {
+        if (!m_) {
+            if (!rows.empty()) throw std::out_of_range("get_row on an empty BRWT");
+            offsets->assign(1, 0);
+            cols->clear();
+            return;
+        }
+        offsets->assign(rows.size() + 1, 0);
+        uint64_t cap = std::max<uint64_t>(16, 16 * rows.size()), need = 0;
+        for (;;) {
+            cols->resize(cap);
+            int st = mbrwt_multi_get_rows(m_.get(), rows.data(), rows.size(), offsets->data(), cols->data(), cap, &need);
+            if (st == MBRWT_ERR_CAPACITY) {
+                cap = need;
+                continue;
+            }
+            check_status(st, "BRWTMultiDevice::get_rows");
+            cols->resize(need);
+            return;
+        }
+    }
+    // BRWT::load onto every replica (mbrwt_multi_load); false on a bad stream
+    bool load(std::istream &in) override {
+        try {
+            return load_from_stream(in, [&](const uint8_t *p, uint64_t n, uint64_t *used) {
+                mbrwt_multi *m = nullptr;
+                const std::vector<int> devs = devices_.empty() ? std::vector<int>{0} : devices_;
+                if (mbrwt_multi_load(p, n, used, devs.data(), (int)devs.size(), &m) != MBRWT_OK) return false;
+                m_.reset(m, Deleter());
+                return true;
+            });
+        } catch (...) {
+            return false;
+        }
+    }
+    void serialize(std::ostream &out) const override {
+        if (!out.good()) throw std::ofstream::failure("Error when dumping BRWT");
+        mbrwt_tree *t = nullptr;
+        mbrwt_tree_desc empty{};
+        if (m_) check_status(mbrwt_tree_export(r0(), &t), "BRWTMultiDevice::serialize");
+        std::unique_ptr<mbrwt_tree, void (*)(mbrwt_tree *)> hold(t, mbrwt_tree_free);
+        const mbrwt_tree_desc *d = t ? mbrwt_tree_get_desc(t) : &empty;
+        uint64_t need = 0;
+        int st = mbrwt_tree_serialize(d, nullptr, 0, &need);
+        if (st != MBRWT_ERR_CAPACITY) check_status(st, "BRWTMultiDevice::serialize");
+        std::vector<uint8_t> bytes(need);
+        check_status(mbrwt_tree_serialize(d, bytes.data(), bytes.size(), &need), "BRWTMultiDevice::serialize");
+        out.write(reinterpret_cast<const char *>(bytes.data()), (std::streamsize)bytes.size());
+    }
+
+  private:
+    mbrwt_ctx *r0() const { return mbrwt_multi_replica(m_.get(), 0); }
+    struct Deleter {
+        void operator()(mbrwt_multi *m) const { mbrwt_multi_destroy(m); }
+    };
+    std::shared_ptr<mbrwt_multi> m_{nullptr, Deleter()};
+    std::vector<int> devices_;
+};
+
 }  // namespace mbrwt_host

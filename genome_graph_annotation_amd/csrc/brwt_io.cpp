@@ -521,6 +521,12 @@ int mbrwt_tree_parse(const uint8_t *bytes, uint64_t len, uint64_t *consumed, mbr
     } catch (const std::bad_alloc &) {
         set_error("out of host memory");
         return MBRWT_ERR_NOMEM;
+    } catch (const std::exception &e) {  // e.g. length_error from a size no stream can back
+        set_error(std::string("BRWT stream: ") + e.what());
+        return MBRWT_ERR_INVALID;
+    } catch (...) {
+        set_error("BRWT stream: unexpected exception");
+        return MBRWT_ERR_INVALID;
     }
 }
 

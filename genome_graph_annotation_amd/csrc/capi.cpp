@@ -86,6 +86,10 @@ static void release(Ctx *c) {
     if (c->h_scalars) (void)hipHostFree(c->h_scalars);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (auto &pr : c->async_ev) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
     destroy_fence(c->fence);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -483,6 +487,31 @@ int mbrwt_get_rows_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, ui
     }
 }
 
+int mbrwt_get_rows_device_async(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets,
+                                uint32_t *d_cols, uint64_t cols_cap, uint64_t *d_status, void *stream) {
+    if (!ctx || !d_status || (n && (!d_rows || !d_offsets)) || (!n && !d_offsets)) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    Ctx &c = *C(ctx);
+    const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(c.mu);
+    WsFence fence_(c.fence, s);
+    try {
+        if (hipSetDevice(c.device) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
+        if (c.rows.ready && c.kernel_variant == 0 && n > 0)
+            return rows_get_rows(c, d_rows, n, d_offsets, d_cols, d_cols ? cols_cap : 0, nullptr, s, d_status);
+        // other images: the synchronous call, then its status on the stream
+        uint64_t need = 0;
+        const int rc = run_get_rows(c, d_rows, n, d_offsets, d_cols, d_cols ? cols_cap : 0, &need, s);
+        if (rc != MBRWT_OK && rc != MBRWT_ERR_CAPACITY && rc != MBRWT_ERR_RANGE) return rc;
+        return rows_set_status(d_status, need, rc, s);
+    } catch (...) {
+        set_error("unexpected exception in mbrwt_get_rows_device_async");
+        return MBRWT_ERR_INVALID;
+    }
+}
+
 int mbrwt_get_rows(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n, uint64_t *offsets, uint32_t *cols,
                    uint64_t cols_cap, uint64_t *cols_needed) {
     if (!ctx || !offsets || (n && !rows)) {
@@ -790,6 +819,14 @@ int mbrwt_take_timing(mbrwt_ctx *ctx, double *kernel_ms, uint64_t *launches) {
     if (!ctx) return MBRWT_ERR_INVALID;
     Ctx &c = *C(ctx);
     std::lock_guard<std::mutex> lk(c.mu);
+    for (size_t i = 0; i < c.async_used; ++i) {  // asynchronous calls' event pairs
+        float ms = 0;
+        MBRWT_HIP(hipEventSynchronize(c.async_ev[i].second));
+        MBRWT_HIP(hipEventElapsedTime(&ms, c.async_ev[i].first, c.async_ev[i].second));
+        c.timing_ms += ms;
+        c.timing_launches += 1;
+    }
+    c.async_used = 0;
     for (Ctx *sc : c.shards) {  // a sharded context's kernels run on its shards
         c.timing_ms += sc->timing_ms;
         c.timing_launches += sc->timing_launches;

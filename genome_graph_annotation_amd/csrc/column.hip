@@ -226,6 +226,7 @@ int run_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap,
     MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr,
                                                (int)nblk, s));
     if ((rc = ensure(c.ws_counts, 2 * (nblk + 1) * sizeof(uint64_t)))) return rc;
+    c.rows_sc_dirty = true;  // (the row-record kernels' counters live in ws_counts)
     if ((rc = ensure(c.ws_scan, scan_bytes + 16))) return rc;
     uint64_t *d_cnt = reinterpret_cast<uint64_t *>(c.ws_counts.buf);
     uint64_t *d_off = d_cnt + nblk + 1;

@@ -609,26 +609,38 @@ int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
             uint64_t bytes = 0;
         };
         std::vector<PT> pt;
-        for (uint32_t k = 0; k < a0 && !p2_shape; ++k)
+        // (k_traverse_ptw reads at most 16 root children: a wider root keeps
+        // the per-node layout)
+        for (uint32_t k = 0; k < a0 && !p2_shape && a0 <= kPacktMaxArity; ++k)
             if (desc.num_children[fc0 + k] && packt_height(desc, fc0 + k) != UINT32_MAX) {
                 pt.emplace_back();
                 pt.back().u = fc0 + k;
             }
-        std::vector<std::thread> pool;
-        for (size_t i = 0; i < pt.size(); ++i)
-            pool.emplace_back([&, i]() {
-                PT &r = pt[i];
-                if (hipSetDevice(device) != hipSuccess) {
-                    r.rc = MBRWT_ERR_DEVICE;
-                    return;
+        // one host thread per candidate, at most 16 at a time; the started
+        // threads are joined on every path (a failed thread start included)
+        for (size_t i0 = 0; i0 < pt.size(); i0 += 16) {
+            std::vector<std::thread> pool;
+            struct Joiner {
+                std::vector<std::thread> &p;
+                ~Joiner() {
+                    for (auto &t : p)
+                        if (t.joinable()) t.join();
                 }
-                try {
-                    r.built = build_packt_image(desc, r.u, ones[r.u], ones, r.dn, r.images, r.bytes, r.rc);
-                } catch (...) {
-                    r.rc = MBRWT_ERR_NOMEM;
-                }
-            });
-        for (auto &t : pool) t.join();
+            } joiner{pool};
+            for (size_t i = i0; i < std::min(pt.size(), i0 + 16); ++i)
+                pool.emplace_back([&, i]() {
+                    PT &r = pt[i];
+                    if (hipSetDevice(device) != hipSuccess) {
+                        r.rc = MBRWT_ERR_DEVICE;
+                        return;
+                    }
+                    try {
+                        r.built = build_packt_image(desc, r.u, ones[r.u], ones, r.dn, r.images, r.bytes, r.rc);
+                    } catch (...) {
+                        r.rc = MBRWT_ERR_NOMEM;
+                    }
+                });
+        }
         for (const PT &r : pt) {
             tree.images.insert(tree.images.end(), r.images.begin(), r.images.end());
             tree.image_bytes += r.bytes;
@@ -682,6 +694,13 @@ int build_from_desc(const mbrwt_tree_desc &desc, int device, Tree &tree) {
             }
     for (size_t i0 = 0; i0 < p2.size(); i0 += 16) {
         std::vector<std::thread> pool;
+        struct Joiner {
+            std::vector<std::thread> &p;
+            ~Joiner() {
+                for (auto &t : p)
+                    if (t.joinable()) t.join();
+            }
+        } joiner{pool};
         for (size_t i = i0; i < std::min(p2.size(), i0 + 16); ++i)
             pool.emplace_back([&, i]() {
                 P2 &r = p2[i];

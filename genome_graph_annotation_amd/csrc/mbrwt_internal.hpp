@@ -357,6 +357,10 @@ struct Ctx {
     // built (layout ROWS), so only the row-record kernels can answer
     RowsImage rows;
     bool nodes_freed = false;
+    bool rows_sc_dirty = true;   // the row-record kernels' counters (in ws_counts) need clearing
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> async_ev;  // timing of asynchronous calls
+    size_t async_used = 0;
+    uint64_t rows_sc_at = 0;     // their byte offset in ws_counts
 };
 
 // row-record image construction (rows.hip): records of the rows [row0, row0 +
@@ -371,8 +375,12 @@ int rows_build_finish(RowsBuild *rb);  // frees rb
 void rows_build_abort(RowsBuild *rb);
 void free_rows(RowsImage &r);
 // row-record queries (rows.hip)
+// d_status != null: asynchronous (no host synchronisation; the call's
+// {labels needed, status, sticky status bits} land in d_status on the stream)
 int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
-                  uint64_t *needed, hipStream_t s);
+                  uint64_t *needed, hipStream_t s, uint64_t *d_status = nullptr);
+// {need, rc, sticky |= 1 << rc} into a caller's status block on the stream
+int rows_set_status(uint64_t *d_status, uint64_t need, int rc, hipStream_t s);
 int rows_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n, uint8_t *d_out, hipStream_t s);
 int rows_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts, hipStream_t s);
 int rows_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s);

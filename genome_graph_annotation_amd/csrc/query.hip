@@ -2287,6 +2287,7 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
         set_error("kernel variant needs the node image (layout rows)");
         return MBRWT_ERR_UNSUPPORTED;
     }
+    c.rows_sc_dirty = true;  // the node kernels reuse ws_counts
     if (!c.shards.empty()) return sharded_get_rows(c, d_rows, n, d_offsets, d_cols, cap, needed, s);
     if (n == 0) {
         MBRWT_HIP(hipMemsetAsync(d_offsets, 0, sizeof(uint64_t), s));

@@ -832,6 +832,7 @@ struct RowsParams {
     uint32_t *tile_counts;        // [tiles] labels (bit 31: the tile goes to the direct pass)
     uint32_t *ovf_list;           // batch indices of the rows of direct tiles
     unsigned long long *scalars;  // [1] direct rows, [2] error flags
+    uint32_t walk4;               // 1: rows_walk4 (default), 2: rows_walk5 (MBRWT_ROWS_WALK=5), 0: rows_walk2 (=2)
     uint32_t diag;                // MBRWT_ROWS_DIAG (timing experiments; WRONG results): 1 no walk,
                                   // 2 walk without label stores, 4 no spill reads
 };
@@ -1063,6 +1064,103 @@ __device__ __forceinline__ void rows_walk2(const AS_LDS uint8_t *pb, uint32_t o,
     }
 }
 
+// v4 walk: rows_walk2's steps with fewer vector instructions (the walk is
+// VALU-bound: 1,700 VALU per 64-row tile in v2, SQ counters): the top frame
+// in two registers, the pending frames in a per-lane LDS stack (one write /
+// one read instead of shifting registers), one emission loop for leaves and
+// leaf parents, mask bytes read as two bytes masked by the arity.
+// a u16 store at a 32-bit byte offset from a wave-uniform base (the saddr +
+// 32-bit voffset form of global_store_short: no 64-bit address arithmetic)
+__device__ __forceinline__ void st16(uint16_t *base, uint32_t idx, uint32_t v) {
+    *(AS_GLOBAL uint16_t *)((uintptr_t)base + (uint64_t)(idx * 2u)) = (uint16_t)v;
+}
+
+template <int MAXD>
+__device__ __forceinline__ void rows_walk4(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
+                                           const AS_LDS uint32_t *ent, AS_LDS uint32_t *stk, uint16_t *out,
+                                           uint32_t pos) {
+    const uint32_t ra = (root >> 16) & 0x1Fu;
+    const uint32_t rm = ((uint32_t)pb[o] | ((uint32_t)pb[o + 1] << 8)) & ((1u << ra) - 1u);
+    o += ra > 8 ? 2u : 1u;
+    if ((root >> 30) == 3u) {  // a one-level tree: the root is a leaf parent
+        if (live)
+            for (uint32_t x = rm; x; x &= x - 1) st16(out, pos++, (root & 0xFFFFu) + (uint32_t)__builtin_ctz(x));
+        return;
+    }
+    uint32_t f = root & 0xFFFFu, m = live ? rm : 0u;
+    uint32_t sp = 0;
+    while (__any(m != 0)) {
+        const bool act = m != 0;
+        const uint32_t c = (uint32_t)__builtin_ctz(m | 0x10000u);
+        m &= m - 1;
+        const uint32_t e = ent[act ? f + c : 0u];
+        const uint32_t a = act ? (e >> 16) & 0x1Fu : 0u;  // leaf: 0
+        const uint32_t mw = ((uint32_t)pb[o] | ((uint32_t)pb[o + 1] << 8)) & ((1u << a) - 1u);
+        o += a ? (a > 8 ? 2u : 1u) : 0u;
+        const bool inner = act && (e >> 31) == 0u;
+        uint32_t x = (act && (e >> 31)) ? (a ? mw : 1u) : 0u;  // a leaf: its column; a leaf parent: its set children
+        const uint32_t base = e & 0xFFFFu;
+        for (; x; x &= x - 1) st16(out, pos++, base + (uint32_t)__builtin_ctz(x));
+        if (inner && m) {
+            stk[sp * 64] = f | (m << 16);
+            ++sp;
+        }
+        if (inner) {
+            f = base;
+            m = mw;
+        }
+        if (act && !m && sp) {
+            --sp;
+            const uint32_t w = stk[sp * 64];
+            f = w & 0xFFFFu;
+            m = w >> 16;
+        }
+    }
+}
+
+// v5 walk: rows_walk4 without divergent branches around the stack -- the
+// push writes the next free slot unconditionally and the pop reads the top
+// slot unconditionally (selects keep what applies), so a step costs vector
+// selects instead of exec-mask juggling; only the label loop diverges.
+template <int MAXD>
+__device__ __forceinline__ void rows_walk5(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
+                                           const AS_LDS uint32_t *ent, AS_LDS uint32_t *stk, uint16_t *out,
+                                           uint32_t pos) {
+    const uint32_t ra = (root >> 16) & 0x1Fu;
+    const uint32_t rm = ((uint32_t)pb[o] | ((uint32_t)pb[o + 1] << 8)) & ((1u << ra) - 1u);
+    o += ra > 8 ? 2u : 1u;
+    if ((root >> 30) == 3u) {
+        if (live)
+            for (uint32_t x = rm; x; x &= x - 1) st16(out, pos++, (root & 0xFFFFu) + (uint32_t)__builtin_ctz(x));
+        return;
+    }
+    uint32_t f = root & 0xFFFFu, m = live ? rm : 0u;
+    uint32_t sp = 1;  // stk[(sp - 1) * 64] is the top pending frame; slot 0 is a dummy
+    while (__any(m != 0)) {
+        const bool act = m != 0;
+        const uint32_t c = (uint32_t)__builtin_ctz(m | 0x10000u);
+        m &= m - 1;
+        const uint32_t e = ent[act ? f + c : 0u];
+        const uint32_t a = act ? (e >> 16) & 0x1Fu : 0u;
+        const uint32_t mw = ((uint32_t)pb[o] | ((uint32_t)pb[o + 1] << 8)) & ((1u << a) - 1u);
+        o += a ? (a > 8 ? 2u : 1u) : 0u;
+        const bool inner = act && (e >> 31) == 0u;
+        uint32_t x = (act && (e >> 31)) ? (a ? mw : 1u) : 0u;
+        const uint32_t base = e & 0xFFFFu;
+        for (; x; x &= x - 1) st16(out, pos++, base + (uint32_t)__builtin_ctz(x));
+        const bool push = inner && m != 0;
+        stk[sp * 64] = f | (m << 16);  // (a slot past the top when not pushing: harmless)
+        sp += push ? 1u : 0u;
+        f = inner ? base : f;
+        m = inner ? mw : m;
+        const uint32_t w = stk[(sp - 1) * 64];
+        const bool pop = act && m == 0 && sp > 1;
+        f = pop ? (w & 0xFFFFu) : f;
+        m = pop ? (w >> 16) : m;
+        sp -= pop ? 1u : 0u;
+    }
+}
+
 template <int B, int MAXD, int WPB, bool NT>
 __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows2[];
@@ -1073,8 +1171,9 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
     const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows2[0]);
     const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows2 + 4;
     const uint32_t C = p.C;
-    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows2 + ((p.table_words + 3) & ~3u)) + wv * (64u * B);
+    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows2 + ((p.table_words + 3) & ~3u)) + wv * (64u * B + 64u * 4 * (MAXD + 1));
     AS_LDS uint8_t *mine = wb + lane * B;
+    AS_LDS uint32_t *stk = (AS_LDS uint32_t *)(wb + 64u * B) + lane;
     constexpr uint32_t LPB = B / 16, RPI = 64 / LPB;
     const uint64_t ntiles = (p.n + 63) / 64;
     const uint64_t tstride = (uint64_t)gridDim.x * WPB;
@@ -1140,9 +1239,17 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
         const bool direct = total > C || __any(lng);
         uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
         if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
-        if (!direct && !(p.diag & 1))
-            rows_walk2<MAXD>(mine, o, valid && cnt > 0, root, ent, reinterpret_cast<uint16_t *>(treg + 128), pos,
-                             !(p.diag & 2));
+        if (!direct && !(p.diag & 1)) {
+            if (p.walk4 == 2)
+                rows_walk5<MAXD>(mine, o, valid && cnt > 0, root, ent, stk, reinterpret_cast<uint16_t *>(treg + 128),
+                                 pos);
+            else if (p.walk4)
+                rows_walk4<MAXD>(mine, o, valid && cnt > 0, root, ent, stk, reinterpret_cast<uint16_t *>(treg + 128),
+                                 pos);
+            else
+                rows_walk2<MAXD>(mine, o, valid && cnt > 0, root, ent, reinterpret_cast<uint16_t *>(treg + 128), pos,
+                                 !(p.diag & 2));
+        }
         if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u));
         if (direct) {
             unsigned long long k0 = 0;
@@ -1192,8 +1299,9 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows3(RowsParams p) {
     const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows3[0]);
     const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows3 + 4;
     const uint32_t C = p.C;
-    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows3 + ((p.table_words + 3) & ~3u)) + wv * (64u * B);
+    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows3 + ((p.table_words + 3) & ~3u)) + wv * (64u * B + 64u * 4 * (MAXD + 1));
     AS_LDS uint8_t *mine = wb + lane * B;
+    AS_LDS uint32_t *stk = (AS_LDS uint32_t *)(wb + 64u * B) + lane;
     const uint64_t ntiles = (p.n + 63) / 64;
     const uint64_t tstride = (uint64_t)gridDim.x * WPB;
     const uint32_t S = p.S;
@@ -1289,9 +1397,17 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows3(RowsParams p) {
         const bool direct = total > C || __any(lng);
         uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
         if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
-        if (!direct && !(p.diag & 1))
-            rows_walk2<MAXD>(mine, o, valid && cnt > 0, root, ent, reinterpret_cast<uint16_t *>(treg + 128), pos,
-                             !(p.diag & 2));
+        if (!direct && !(p.diag & 1)) {
+            if (p.walk4 == 2)
+                rows_walk5<MAXD>(mine, o, valid && cnt > 0, root, ent, stk, reinterpret_cast<uint16_t *>(treg + 128),
+                                 pos);
+            else if (p.walk4)
+                rows_walk4<MAXD>(mine, o, valid && cnt > 0, root, ent, stk, reinterpret_cast<uint16_t *>(treg + 128),
+                                 pos);
+            else
+                rows_walk2<MAXD>(mine, o, valid && cnt > 0, root, ent, reinterpret_cast<uint16_t *>(treg + 128), pos,
+                                 !(p.diag & 2));
+        }
         if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u));
         if (direct) {
             unsigned long long k0 = 0;
@@ -1318,67 +1434,113 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows3(RowsParams p) {
     }
 }
 
-// tile regions -> CSR: one wave per tile (offsets by a wave scan of the
-// tile's counts, labels u16 -> u32, reads issued before the offset is known);
-// launched before the host knows the total: over the capacity it writes nothing
+// tile regions -> CSR: one wave per TPW consecutive tiles (every load of
+// the group -- counts, the tile offsets, the first 512 labels of each tile --
+// issued before any store, so a wave pays one memory latency for TPW tiles);
+// offsets by a wave scan of each tile's counts, labels u16 -> u32.  Launched
+// before the host knows the total: over the capacity it writes no CSR.  The
+// scan is exclusive over the tiles, so the batch total is offset + count of
+// the last tile; workgroup 0 publishes {total, direct rows, error flags} to
+// res[0..2] and clears the kernel's counters (sc[1], sc[2]) for the next call.
+constexpr uint32_t kCompactTpw = 4;
 __global__ __launch_bounds__(256) void k_compact_tiles(const uint8_t *__restrict__ temp, uint32_t C,
                                                        const uint32_t *__restrict__ tile_counts,
                                                        const uint64_t *__restrict__ tile_offsets,
                                                        uint64_t *__restrict__ offsets, uint32_t *__restrict__ cols,
-                                                       uint64_t n, uint64_t cap) {
+                                                       uint64_t n, uint64_t cap, unsigned long long *sc,
+                                                       unsigned long long *res) {
     const uint64_t ntiles = (n + 63) / 64;
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (t >= ntiles) return;
-    if (gld(tile_offsets + ntiles) > cap) return;
-    const uint64_t r0 = t * 64;
-    const uint32_t nr = (uint32_t)(n - r0 < 64 ? n - r0 : 64);
-    const uint8_t *treg = temp + t * (uint64_t)(128 + 2 * C);
-    const uint16_t *lab = reinterpret_cast<const uint16_t *>(treg + 128);
-    const uint32_t tc = gld(tile_counts + t);
-    const uint64_t base = gld(tile_offsets + t);
-    const uint32_t cnt = lane < nr ? (uint32_t)gld(reinterpret_cast<const uint16_t *>(treg) + lane) : 0u;
-    uint32_t v[8];
-#pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) v[k] = gld(lab + lane + 64 * k);  // (C >= 1024: inside the region)
-    uint32_t x = cnt;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-        if (lane >= d) x += y;
+    const uint64_t total = gld(tile_offsets + ntiles - 1) + (gld(tile_counts + ntiles - 1) & 0x7FFFFFFFu);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        res[0] = total;
+        res[1] = sc[1];
+        res[2] = sc[2];
+        sc[1] = 0;
+        sc[2] = 0;
     }
-    if (lane < nr) gst(offsets + r0 + lane, base + (x - cnt));
-    if (t == ntiles - 1 && lane == nr - 1) gst(offsets + n, base + x);
-    if (tc >> 31) return;  // direct tile: k_rows_direct writes its labels
-    const uint32_t total = tc;
+    if (total > cap) return;
+    const uint64_t t0 = (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * kCompactTpw;
+    if (t0 >= ntiles) return;
+    const uint32_t region = 128 + 2 * C;
+    uint32_t tc[kCompactTpw], cnt[kCompactTpw], v[kCompactTpw][8];
+    uint64_t base[kCompactTpw];
 #pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) {
-        const uint32_t i = lane + 64 * k;
-        if (i < total) gst(cols + base + i, v[k]);
+    for (uint32_t k = 0; k < kCompactTpw; ++k) {
+        const uint64_t t = t0 + k;
+        const bool in = t < ntiles;
+        const uint8_t *treg = temp + (in ? t : 0) * (uint64_t)region;
+        const uint64_t r0 = t * 64;
+        tc[k] = in ? gld(tile_counts + t) : 0x80000000u;
+        base[k] = in ? gld(tile_offsets + t) : 0;
+        cnt[k] = (in && r0 + lane < n) ? (uint32_t)gld(reinterpret_cast<const uint16_t *>(treg) + lane) : 0u;
+        const uint16_t *lab = reinterpret_cast<const uint16_t *>(treg + 128);
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) v[k][j] = gld(lab + lane + 64 * j);  // (C >= 1024: inside the region)
     }
-    for (uint32_t i0 = 512; i0 < total; i0 += 512) {
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {
-            const uint32_t i = i0 + lane + 64 * k;
-            v[k] = i < total ? (uint32_t)gld(lab + i) : 0u;
+    for (uint32_t k = 0; k < kCompactTpw; ++k) {
+        const uint64_t t = t0 + k;
+        if (t >= ntiles) break;
+        const uint64_t r0 = t * 64;
+        const uint32_t nr = (uint32_t)(n - r0 < 64 ? n - r0 : 64);
+        uint32_t x = cnt[k];
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+            if (lane >= d) x += y;
         }
+        if (lane < nr) gst(offsets + r0 + lane, base[k] + (x - cnt[k]));
+        if (t == ntiles - 1 && lane == nr - 1) gst(offsets + n, base[k] + x);
+        if (tc[k] >> 31) continue;  // direct tile: k_rows_direct writes its labels
+        const uint32_t tot = tc[k];
+        uint32_t *dst = cols + base[k];
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {
-            const uint32_t i = i0 + lane + 64 * k;
-            if (i < total) gst(cols + base + i, v[k]);
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t i = lane + 64 * j;
+            if (i < tot) gst(dst + i, v[k][j]);
+        }
+        const uint16_t *lab = reinterpret_cast<const uint16_t *>(temp + t * (uint64_t)region + 128);
+        for (uint32_t i0 = 512; i0 < tot; i0 += 512) {
+            uint32_t w[8];
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t i = i0 + lane + 64 * j;
+                w[j] = i < tot ? (uint32_t)gld(lab + i) : 0u;
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t i = i0 + lane + 64 * j;
+                if (i < tot) gst(dst + i, w[j]);
+            }
         }
     }
 }
 
 // rows of direct tiles: one lane per row, its record walked from global
 // memory straight into the CSR
+// (asynchronous calls: res = k_compact_tiles' {total, direct rows, error
+// flags} on the device -- the count of listed rows comes from there, and
+// workgroup 0 publishes the call's status to status[0..2])
 __global__ __launch_bounds__(256) void k_rows_direct(RowsView v, const uint32_t *table, const uint64_t *rows,
                                                      const uint32_t *list, uint64_t nlist,
                                                      const uint64_t *offsets, uint32_t *cols,
-                                                     unsigned long long *scalars) {
+                                                     unsigned long long *scalars, const unsigned long long *res,
+                                                     uint64_t cap, unsigned long long *status) {
     const uint32_t *ntab = table + 4;
     const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + table[0]);
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    if (res) {
+        const uint64_t total = res[0], err = res[2];
+        const uint64_t st = (err & 1) ? MBRWT_ERR_RANGE : total > cap ? MBRWT_ERR_CAPACITY : MBRWT_OK;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            status[0] = total;
+            status[1] = st;
+            status[2] |= 1ull << st;
+        }
+        if (st != MBRWT_OK) return;
+        nlist = res[1];
+    }
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nlist; i += gs) {
         const uint32_t bi = gld(list + i);
         const uint64_t row = gld(rows + bi);
@@ -1506,10 +1668,11 @@ using RowsFn = void (*)(RowsParams);
 constexpr uint32_t kRowsWpb = 4;
 constexpr uint32_t kRows2Wpb = 8;
 constexpr uint32_t kRows3Wpb = 4;  // (72 VGPRs: 7 waves per SIMD in 4-wave workgroups)
-// MBRWT_ROWS_KERNEL=1 / 2: the first / second version, for A/B (3 = default)
+// MBRWT_ROWS_KERNEL=1 / 3: the first version / the software-pipelined one,
+// for A/B (2 = the default)
 int rows_version() {
     const char *e = std::getenv("MBRWT_ROWS_KERNEL");
-    return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 3;
+    return (e && (e[0] == '1' || e[0] == '3')) ? e[0] - '0' : 2;
 }
 bool rows_v1() { return rows_version() == 1; }
 template <int B, bool NT, int V>
@@ -1523,6 +1686,7 @@ RowsFn rows2_fn_d(uint32_t frames) {
                : frames <= 8 ? k_traverse_rows3<B, 8, kRows3Wpb, NT>
                              : k_traverse_rows3<B, 16, kRows3Wpb, NT>;
 }
+uint32_t rows_maxd(const RowsImage &im) { return im.frames <= 4 ? 4 : im.frames <= 8 ? 8 : 16; }
 template <int V>
 RowsFn rows2_fn_v(const RowsImage &im) {
     const bool nt = im.bytes > (1ull << 30);
@@ -1559,8 +1723,9 @@ struct MaskTile {
 }  // namespace
 
 int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
-                  uint64_t *needed, hipStream_t s) {
+                  uint64_t *needed, hipStream_t s, uint64_t *d_status) {
     const RowsImage &im = c.rows;
+    if (n == 0 && d_status) return MBRWT_ERR_UNSUPPORTED;  // (the caller's generic path handles it)
     if (n == 0) {
         MBRWT_HIP(hipMemsetAsync(d_offsets, 0, sizeof(uint64_t), s));
         MBRWT_HIP(hipStreamSynchronize(s));
@@ -1578,13 +1743,22 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     // counts workspace: nt+1 tile counts | (8-byte aligned) nt+1 tile offsets
     const uint64_t to_off = ((nt + 1) * sizeof(uint32_t) + 7) / 8 * 8;
     if ((rc = ensure(c.ws_temp, nt * region))) return rc;
-    if ((rc = ensure(c.ws_counts, to_off + (nt + 1) * sizeof(uint64_t)))) return rc;
+    // [tile counts | tile offsets | the kernel's own counters (4 x u64)]
+    const uint64_t sc_off = to_off + (nt + 1) * sizeof(uint64_t);
+    const bool fresh = c.ws_counts.bytes < sc_off + 32;
+    if ((rc = ensure(c.ws_counts, sc_off + 32))) return rc;
+    unsigned long long *d_sc = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + sc_off);
+    if (fresh || c.rows_sc_dirty || c.rows_sc_at != sc_off) {  // the counters are cleared by k_compact_tiles
+        MBRWT_HIP(hipMemsetAsync(d_sc, 0, 32, s));
+        c.rows_sc_dirty = false;
+        c.rows_sc_at = sc_off;
+    }
     if ((rc = ensure(c.ws_ovf, n * sizeof(uint32_t)))) return rc;
     uint32_t *d_tc = reinterpret_cast<uint32_t *>(c.ws_counts.buf);
     uint64_t *d_to = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + to_off);
     hipcub::TransformInputIterator<uint64_t, MaskTile, const uint32_t *> it(d_tc, MaskTile());
     size_t scan_bytes = 0;
-    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, it, d_to, nt + 1, s));
+    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, it, d_to, nt, s));
     if ((rc = ensure(c.ws_scan, scan_bytes))) return rc;
 
     RowsParams p{};
@@ -1602,13 +1776,17 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     p.temp = reinterpret_cast<uint8_t *>(c.ws_temp.buf);
     p.tile_counts = d_tc;
     p.ovf_list = reinterpret_cast<uint32_t *>(c.ws_ovf.buf);
-    p.scalars = reinterpret_cast<unsigned long long *>(c.d_scalars);
+    p.scalars = d_sc;
     if (const char *e = std::getenv("MBRWT_ROWS_DIAG")) p.diag = (uint32_t)std::atoi(e);
+    {
+        const char *e = std::getenv("MBRWT_ROWS_WALK");
+        p.walk4 = (e && e[0] == '2') ? 0u : (e && e[0] == '5') ? 2u : 1u;  // default: the v4 walk
+    }
 
     const RowsFn kfn = v1 ? rows_fn(im) : rows2_fn(im);
     const uint32_t wpb = v1 ? kRowsWpb : rows_version() == 2 ? kRows2Wpb : kRows3Wpb;
     const size_t lds = v1 ? ((im.table.size() + 3) & ~size_t(3)) * 4 + kRowsWpb * (64ull * im.B + 2ull * C)
-                          : ((im.table2.size() + 3) & ~size_t(3)) * 4 + wpb * 64ull * im.B;
+                          : ((im.table2.size() + 3) & ~size_t(3)) * 4 + wpb * (64ull * im.B + 64ull * 4 * (rows_maxd(im) + 1));
     const uint32_t threads = 64 * wpb;
     if (c.rb_fn != reinterpret_cast<const void *>(kfn) || c.rb_lds != lds || c.rb_threads != threads) {
         if (lds > 65536)
@@ -1627,17 +1805,42 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     }
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((nt + wpb - 1) / wpb, (uint64_t)c.rb_blocks));
 
-    MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
-    MBRWT_HIP(hipMemsetAsync(d_tc + nt, 0, sizeof(uint32_t), s));
-    if (c.timing) MBRWT_HIP(hipEventRecord(c.ev0, s));
+    c.rows_sc_dirty = true;  // until k_compact_tiles has run
+    hipEvent_t e0 = c.ev0, e1 = c.ev1;
+    if (c.timing && d_status) {  // asynchronous calls: one event pair per call, summed by mbrwt_take_timing
+        if (c.async_ev.size() <= c.async_used) {
+            hipEvent_t a = nullptr, b = nullptr;
+            MBRWT_HIP(hipEventCreate(&a));
+            MBRWT_HIP(hipEventCreate(&b));
+            c.async_ev.push_back({a, b});
+        }
+        e0 = c.async_ev[c.async_used].first;
+        e1 = c.async_ev[c.async_used].second;
+        ++c.async_used;
+    }
+    if (c.timing) MBRWT_HIP(hipEventRecord(e0, s));
     hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(threads), lds, s, p);
     MBRWT_HIP(hipGetLastError());
-    if (c.timing) MBRWT_HIP(hipEventRecord(c.ev1, s));
-    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_to, nt + 1, s));
-    hipLaunchKernelGGL(k_compact_tiles, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s, p.temp, C, d_tc, d_to,
-                       d_offsets, d_cols, n, cap);
-    MBRWT_HIP(hipGetLastError());
-    MBRWT_HIP(hipMemcpyAsync(c.d_scalars, d_to + nt, sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+    if (c.timing) MBRWT_HIP(hipEventRecord(e1, s));
+    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_to, nt, s));
+    {
+        const uint64_t waves = (nt + kCompactTpw - 1) / kCompactTpw;
+        hipLaunchKernelGGL(k_compact_tiles, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, p.temp, C, d_tc, d_to,
+                           d_offsets, d_cols, n, cap, d_sc, reinterpret_cast<unsigned long long *>(c.d_scalars));
+        MBRWT_HIP(hipGetLastError());
+    }
+    c.rows_sc_dirty = false;
+    if (d_status) {
+        // no host synchronisation: the rows of direct tiles (their count on
+        // the device) and the call's status, both behind the compaction
+        hipLaunchKernelGGL(k_rows_direct, dim3(64), dim3(256), 0, s, view_of(c), (const uint32_t *)im.d_table, d_rows,
+                           (const uint32_t *)p.ovf_list, (uint64_t)0, (const uint64_t *)d_offsets, d_cols,
+                           reinterpret_cast<unsigned long long *>(c.d_scalars) + 4,
+                           (const unsigned long long *)c.d_scalars, cap,
+                           reinterpret_cast<unsigned long long *>(d_status));
+        MBRWT_HIP(hipGetLastError());
+        return MBRWT_OK;
+    }
     MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     MBRWT_HIP(hipStreamSynchronize(s));
     if (c.timing) {
@@ -1660,9 +1863,25 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         const uint64_t g = std::min<uint64_t>((ovf + 255) / 256, 65536);
         hipLaunchKernelGGL(k_rows_direct, dim3((unsigned)g), dim3(256), 0, s, view_of(c), (const uint32_t *)im.d_table,
                            d_rows, (const uint32_t *)p.ovf_list, ovf, (const uint64_t *)d_offsets, d_cols,
-                           p.scalars);
+                           reinterpret_cast<unsigned long long *>(c.d_scalars), (const unsigned long long *)nullptr,
+                           (uint64_t)0, (unsigned long long *)nullptr);
         MBRWT_HIP(hipGetLastError());
     }
+    return MBRWT_OK;
+}
+
+namespace {
+__global__ void k_set_status(unsigned long long *status, uint64_t need, uint64_t st) {
+    status[0] = need;
+    status[1] = st;
+    status[2] |= 1ull << st;
+}
+}  // namespace
+
+int rows_set_status(uint64_t *d_status, uint64_t need, int rc, hipStream_t s) {
+    hipLaunchKernelGGL(k_set_status, dim3(1), dim3(1), 0, s, reinterpret_cast<unsigned long long *>(d_status), need,
+                       (uint64_t)rc);
+    MBRWT_HIP(hipGetLastError());
     return MBRWT_OK;
 }
 

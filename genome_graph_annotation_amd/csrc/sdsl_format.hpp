@@ -57,6 +57,13 @@ struct Reader {
     void need(uint64_t k) const {
         if (k > n - pos) throw FormatError("unexpected end of stream");
     }
+    // words of 64 bits for `bits` bits, checked against the rest of the stream
+    // BEFORE anything is sized from the (untrusted) header
+    uint64_t words_for(uint64_t bits) const {
+        const uint64_t W = bits / 64 + (bits % 64 != 0);
+        if (W > (n - pos) / 8) throw FormatError("vector longer than the stream");
+        return W;
+    }
     uint8_t u8() {
         need(1);
         return p[pos++];
@@ -155,11 +162,10 @@ inline IntVector get_int_vector(Reader &r) {
     const uint64_t bits = r.u64le();
     const uint8_t width = r.u8();
     if (width == 0 || width > 64 || bits % width) throw FormatError("int_vector: bad size/width");
+    const uint64_t W = r.words_for(bits);
     IntVector v;
     v.len = bits / width;
     v.width = width;
-    const uint64_t W = (bits + 63) / 64;
-    r.need(W * 8);
     v.words.resize(W);
     for (uint64_t k = 0; k < W; ++k) v.words[k] = r.u64le();
     return v;
@@ -171,8 +177,7 @@ inline void put_bit_vector(Writer &w, const std::vector<uint64_t> &words, uint64
 }
 inline std::vector<uint64_t> get_bit_vector(Reader &r, uint64_t *bits) {
     *bits = r.u64le();
-    const uint64_t W = (*bits + 63) / 64;
-    r.need(W * 8);
+    const uint64_t W = r.words_for(*bits);
     std::vector<uint64_t> words(W);
     for (uint64_t k = 0; k < W; ++k) words[k] = r.u64le();
     return words;
@@ -296,6 +301,8 @@ inline std::vector<uint64_t> get_rrr(Reader &r, uint64_t *size_out) {
     (void)get_int_vector(r);  // btnrp: samples, recomputed while decoding
     (void)get_int_vector(r);  // rank samples
     const std::vector<uint64_t> invert = get_bit_vector(r, &inv_bits);
+    // the size is untrusted: the block classes (read from the stream) bound it
+    if (size / kRrrBlock > bt.len) throw FormatError("rrr_vector: size larger than its blocks");
     const uint64_t nblocks = (size + kRrrBlock) / kRrrBlock;
     if (bt.len < nblocks || (size > 0 && bt.len > nblocks + 1)) throw FormatError("rrr_vector: block count");
     std::vector<uint64_t> out((size + 63) / 64 + 1, 0);

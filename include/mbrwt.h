@@ -184,6 +184,33 @@ int mbrwt_layout(const mbrwt_ctx *ctx); /* MBRWT_LAYOUT_NODES / _ROWS / _BOTH of
    without row records. */
 int mbrwt_rows_stats(const mbrwt_ctx *ctx, uint64_t out[8]);
 
+/* ---- multi-device (one process, N GPUs) --------------------------------
+ * A replica of the tree on every device of `devices` (n entries; a device
+ * may repeat), built concurrently with the calling thread's build layout,
+ * and get_rows over a batch cut into n contiguous slices -- slice r on
+ * replica r -- reassembled into the caller's ONE CSR: host buffers
+ * (mbrwt_multi_get_rows: device-to-host copies at each slice's label offset)
+ * or device buffers on devices[0] (mbrwt_multi_get_rows_device: peer copies
+ * over xGMI, `stream` on devices[0]).  Results, order and the capacity
+ * protocol are those of mbrwt_get_rows over the whole batch.  The
+ * reference's `annograph classify` runs its ThreadPool in one process
+ * (main.cpp:462-497): this is how its host drives every GPU of a node.
+ * mbrwt_multi_replica gives replica i's context (point / column queries,
+ * properties, export); it is owned by the multi handle.
+ */
+typedef struct mbrwt_multi mbrwt_multi;
+int mbrwt_multi_create(const mbrwt_tree_desc *desc, const int *devices, int n, mbrwt_multi **out);
+int mbrwt_multi_create_synthetic(const mbrwt_synth_desc *desc, const int *devices, int n, mbrwt_multi **out);
+int mbrwt_multi_load(const uint8_t *bytes, uint64_t len, uint64_t *consumed, const int *devices, int n,
+                     mbrwt_multi **out);
+void mbrwt_multi_destroy(mbrwt_multi *m);
+int mbrwt_multi_size(const mbrwt_multi *m);
+mbrwt_ctx *mbrwt_multi_replica(mbrwt_multi *m, int i);
+int mbrwt_multi_get_rows(mbrwt_multi *m, const uint64_t *rows, uint64_t n, uint64_t *offsets, uint32_t *cols,
+                         uint64_t cols_cap, uint64_t *cols_needed);
+int mbrwt_multi_get_rows_device(mbrwt_multi *m, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets,
+                                uint32_t *d_cols, uint64_t cols_cap, uint64_t *cols_needed, void *stream);
+
 /* ---- files: the reference's BRWT stream (the matrix of a .brwt.annodbg) ----
  * An owned tree description (host memory).  Byte formats of sdsl-lite /
  * libmaus2 are restated from their published algorithms: PARITY UNPINNED
@@ -247,6 +274,21 @@ int mbrwt_get_rows(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n, uint64_t *o
  */
 int mbrwt_get_rows_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets,
                           uint32_t *d_cols, uint64_t cols_cap, uint64_t *cols_needed, void *stream);
+
+/*
+ * The same without any host synchronisation, for pipelines that keep the
+ * device busy (consecutive batches, the multi-GPU exchange): the call only
+ * enqueues work on `stream`.  When the stream reaches its end, d_status
+ * (device memory, 3 uint64) holds {labels needed, MBRWT_* status of the
+ * call, sticky bits |= 1 << status} -- the caller clears word 2 and checks
+ * it after synchronising.  Over cols_cap the status is MBRWT_ERR_CAPACITY
+ * and no label is written (offsets may be); out-of-range rows give
+ * MBRWT_ERR_RANGE.  The return value reports only argument and launch errors.
+ * On a per-node image the call runs the synchronous path (one host sync)
+ * and then writes the same status block.
+ */
+int mbrwt_get_rows_device_async(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets,
+                                uint32_t *d_cols, uint64_t cols_cap, uint64_t *d_status, void *stream);
 
 /* Batched BRWT::get (BRWT.cpp:9-24): out[i] = bit (rows[i], cols[i]). Host buffers. */
 int mbrwt_get_batch(mbrwt_ctx *ctx, const uint64_t *rows, const uint64_t *cols, uint64_t n, uint8_t *out);

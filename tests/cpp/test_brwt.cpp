@@ -121,6 +121,31 @@ static void grid_device_built(int kind, uint64_t relax = 0) {
         }
     }
 }
+// the grids on two replicas of one device (mbrwt_multi_*: slices of the
+// batch on each replica, reassembled into one CSR); device backend only
+static void grid_multi(int kind) {
+    if (!g_device) return;
+    for (uint64_t n = 1; n < 20; ++n) {
+        for (size_t mcols = 1; mcols < 20; ++mcols) {
+            Columns cols(mcols, std::vector<bool>(n));
+            for (size_t j = 0; j < mcols; ++j)
+                for (uint64_t i = 0; i < n; ++i) cols[j][i] = kind == 0 ? false : kind == 1 ? true : ((i + 2 * j) % 2) != 0;
+            auto om = OracleMatrix(build_oracle(cols, n, 0, 2, 0));
+            DescStorage st;
+            const mbrwt_tree_desc d = oracle_desc(om, st);
+            mbrwt_host::BRWTMultiDevice m(d, {0, 0});
+            EXPECT_EQ(2, m.replicas());
+            test_brwt(m, cols, n);
+            std::vector<uint64_t> rows;
+            for (uint64_t i = 0; i < n; ++i) rows.push_back(n - 1 - i);
+            const auto got = m.get_rows(rows);
+            for (size_t i = 0; i < rows.size(); ++i) EXPECT_TRUE(got[i] == om.get_row(rows[i]));
+        }
+    }
+}
+TEST(MultiDevice, AllZero) { grid_multi(0); }
+TEST(MultiDevice, AllOne) { grid_multi(1); }
+TEST(MultiDevice, AllMixed) { grid_multi(2); }
 TEST(BRWT, DeviceBuilderAllZero) { grid_device_built(0); }
 TEST(BRWT, DeviceBuilderAllOne) { grid_device_built(1); }
 TEST(BRWT, DeviceBuilderAllMixed) { grid_device_built(2); }

@@ -166,3 +166,23 @@ def test_bad_partition_is_rejected(oracle_mod):
     data[first_word + 4:first_word + 8] = (0).to_bytes(4, "little")
     with pytest.raises(MBRWTError):
         parse_brwt(bytes(data))
+
+
+def test_oversized_size_fields_are_rejected(oracle_mod):
+    """Header size fields the stream cannot back (an int_vector /
+    bit_vector / rrr size near 2^64 wrapped the word count) are rejected with
+    MBRWT_ERR_INVALID -- never a crash, an out-of-bounds read or an exception
+    through the ABI: every 8 bytes of a small stream overwritten in turn by
+    huge values."""
+    O = oracle_mod
+    rng = np.random.default_rng(17)
+    dense = rng.random((300, 11)) < 0.2
+    data = serialize_tree(O.OracleTree.from_dense(dense, "basic", 3).export())
+    for big in (2**64 - 1, 2**64 - 64, 2**63, 2**40 + 7):
+        for off in range(0, len(data) - 8):
+            b = bytearray(data)
+            b[off:off + 8] = int(big).to_bytes(8, "little")
+            try:
+                parse_brwt(bytes(b))
+            except MBRWTError as e:
+                assert e.status in (L.MBRWT_ERR_INVALID,), (off, big, e.status)

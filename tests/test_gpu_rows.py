@@ -291,3 +291,61 @@ def test_rows_beyond_2_32_rows(oracle_mod):
     off_d, cols_d = dev.get_rows(rows)
     np.testing.assert_array_equal(off_d, off_o)
     np.testing.assert_array_equal(cols_d, cols_o)
+
+
+@pytest.mark.parametrize("layout", ["rows", "nodes"])
+def test_get_rows_device_async(oracle_mod, layout):
+    """mbrwt_get_rows_device_async: several batches enqueued back to back with
+    no host synchronisation, the status block {needed, status, sticky bits}
+    read once at the end; capacity and range errors reported through it."""
+    O = oracle_mod
+    import torch
+    from genome_graph_annotation_amd import BRWTDevice, _lib as L
+    rng = np.random.default_rng(11)
+    n, m = 30000, 200
+    dense = rng.random((n, m)) < 0.04
+    t = O.OracleTree.from_dense(dense, "basic", 8)
+    d = BRWTDevice.from_tree(t.export(), layout=layout)
+    s = torch.cuda.current_stream().cuda_stream
+    st = torch.zeros(3, dtype=torch.int64, device="cuda")
+    outs = []
+    for k in (1, 63, 64, 65, 5000, 40000):
+        rows = rng.integers(0, n, k).astype(np.uint64)
+        rt = torch.from_numpy(rows.view(np.int64)).cuda()
+        ot = torch.empty(k + 1, dtype=torch.int64, device="cuda")
+        ct = torch.empty(k * m // 10 + 64, dtype=torch.int32, device="cuda")
+        d.get_rows_device_async(rt, ot, ct, st, s)
+        outs.append((rows, ot, ct, st.clone()))
+    torch.cuda.synchronize()
+    for rows, ot, ct, st_k in outs:
+        off_o, cols_o = t.get_rows(rows)
+        need, status, sticky = st_k.cpu().tolist()
+        assert status == L.MBRWT_OK and need == len(cols_o)
+        assert sticky == 1 << L.MBRWT_OK
+        np.testing.assert_array_equal(ot.cpu().numpy().view(np.uint64), off_o)
+        np.testing.assert_array_equal(ct[:need].cpu().numpy().view(np.uint32), cols_o)
+    rows = rng.integers(0, n, 3000).astype(np.uint64)
+    off_o, cols_o = t.get_rows(rows)
+    rt = torch.from_numpy(rows.view(np.int64)).cuda()
+    ot = torch.empty(3001, dtype=torch.int64, device="cuda")
+    small = torch.empty(5, dtype=torch.int32, device="cuda")
+    st.zero_()
+    d.get_rows_device_async(rt, ot, small, st, s)
+    torch.cuda.synchronize()
+    need, status, sticky = st.cpu().tolist()
+    assert status == L.MBRWT_ERR_CAPACITY and need == len(cols_o)
+    assert sticky & (1 << L.MBRWT_ERR_CAPACITY)
+    bad = torch.tensor([0, n], dtype=torch.int64, device="cuda")
+    ot2 = torch.empty(3, dtype=torch.int64, device="cuda")
+    ct2 = torch.empty(1000, dtype=torch.int32, device="cuda")
+    st.zero_()
+    d.get_rows_device_async(bad, ot2, ct2, st, s)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist()[1] == L.MBRWT_ERR_RANGE
+    # a good call after the errors
+    ct = torch.empty(len(cols_o) + 1, dtype=torch.int32, device="cuda")
+    st.zero_()
+    d.get_rows_device_async(rt, ot, ct, st, s)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [len(cols_o), L.MBRWT_OK, 1 << L.MBRWT_OK]
+    np.testing.assert_array_equal(ct[:len(cols_o)].cpu().numpy().view(np.uint32), cols_o)

@@ -37,14 +37,26 @@ s = torch.cuda.current_stream().cuda_stream
 shape = dict(np.load(a.shape)) if a.shape else None
 ref = None
 cols = None
+ASYNC = [False]
+status = torch.zeros(3, dtype=torch.int64, device="cuda")
+
+
 def set_variant(kv):
-    """'' default, 'v1' / 'v2' the first / second row-record kernel, 'diagN' MBRWT_ROWS_DIAG=N"""
+    """'' default, 'v1' / 'v2' the first / second row-record kernel, 'diagN'
+    MBRWT_ROWS_DIAG=N, 'async' the timed steps through mbrwt_get_rows_device_async"""
+    ASYNC[0] = False
     os.environ.pop("MBRWT_ROWS_KERNEL", None)
     os.environ.pop("MBRWT_ROWS_DIAG", None)
-    if kv in ("v1", "v2"):
-        os.environ["MBRWT_ROWS_KERNEL"] = kv[1]
-    elif kv.startswith("diag"):
-        os.environ["MBRWT_ROWS_DIAG"] = kv[4:]
+    os.environ.pop("MBRWT_ROWS_WALK", None)
+    for part in kv.split("."):  # e.g. "w2.v2.diag1"
+        if part.startswith("w"):  # w2: the v2 walk
+            os.environ["MBRWT_ROWS_WALK"] = part[1:]
+        elif part in ("v1", "v2", "v3"):
+            os.environ["MBRWT_ROWS_KERNEL"] = part[1]
+        elif part == "async":
+            ASYNC[0] = True
+        elif part.startswith("diag"):
+            os.environ["MBRWT_ROWS_DIAG"] = part[4:]
 
 
 # config = layout[:B,S][@variant+variant...]: one build, every variant timed on it
@@ -83,9 +95,15 @@ for cfg in a.configs.split(";") if ";" in a.configs else a.configs.split(","):
         m.set_option(L.MBRWT_OPT_TIMING, 1)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
+        status.zero_()
         for _ in range(a.steps):
-            m.get_rows_device(rows, off, cols, s)
+            if ASYNC[0]:
+                m.get_rows_device_async(rows, off, cols, status, s)
+            else:
+                m.get_rows_device(rows, off, cols, s)
         torch.cuda.synchronize()
+        if ASYNC[0]:
+            assert status.cpu().tolist()[1:] == [0, 1], status
         el = (time.perf_counter() - t1) / a.steps
         m.set_option(L.MBRWT_OPT_TIMING, 0)
         kms, k = m.take_timing()
@@ -94,7 +112,7 @@ for cfg in a.configs.split(";") if ";" in a.configs else a.configs.split(","):
                "step_ms": el * 1e3, "rows_per_s": a.batch / el, "labels": int(nl), "csr_hash": hx,
                "same_as_first": hx == ref, "rows_stats": m.rows_stats()}
         print(json.dumps(out), flush=True)
-        if hx != ref and not kv.startswith("diag"):
+        if hx != ref and "diag" not in kv:
             print("MISMATCH", flush=True)
             sys.exit(1)
     set_variant("")
