@@ -92,6 +92,9 @@ def parse():
     ap.add_argument("--check-rows", type=int, default=0,
                     help="rows checked element-wise against the oracle (0 = the whole global batch)")
     ap.add_argument("--kernel", type=int, default=0, help="MBRWT_OPT_KERNEL variant (0 = library default)")
+    ap.add_argument("--sync", action="store_true",
+                    help="N = 1: time the synchronous mbrwt_get_rows_device (default: the asynchronous call, "
+                         "status checked after the timed region)")
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--traffic", choices=["live", "committed", "off"], default="live",
                     help="roofline traffic: rocprofv3 PMC child passes (N = 1), a committed summary of the "
@@ -222,7 +225,7 @@ def csr_hash(off: np.ndarray, cols: np.ndarray) -> str:
     return h.hexdigest()
 
 
-def probe_ceilings(dev_t, stream_ptr, free_bytes):
+def probe_ceilings(dev_t, stream_ptr, free_bytes, struct_bytes=64 << 30):
     """Measured ceilings of this GPU (tools/probe.hip): streaming-read GB/s,
     and random-segment requests/s -- the MAXIMUM over a sweep of requests in
     flight and resident waves (the full sweep:
@@ -244,8 +247,11 @@ def probe_ceilings(dev_t, stream_ptr, free_bytes):
     if lib.probe_stream_read(buf.data_ptr(), buf.numel(), 5, stream_ptr, C.byref(v)) == 0:
         stream_gbs = v.value
     del buf
-    # random segments over a buffer far past the 256 MiB Infinity Cache
-    big = min(64 << 30, int(free_bytes * 0.8)) // (1 << 30) << 30
+    # random segments over a buffer far past the 256 MiB Infinity Cache, as
+    # large as the structure where memory allows: the request rate falls with
+    # the buffer's span (address translation; 54.2 G/s over 4 GiB, 49.4 G/s
+    # over 118 GiB: profiles/r03/v05_probe_random64_*gib.json)
+    big = min(max(struct_bytes, 8 << 30), int(free_bytes * 0.8)) // (1 << 30) << 30
     if big >= (8 << 30):
         cus = torch.cuda.get_device_properties(dev_t).multi_processor_count
         buf = torch.empty(big, dtype=torch.uint8, device=dev_t)
@@ -354,11 +360,20 @@ def main():
         bufs.append((torch.empty_like(off_t), torch.empty_like(cols_t)))
     state = {"i": 0, "pending": None, "global": None, "timed": False, "exchanges": [], "get_rows_host": []}
 
+    # N = 1: the asynchronous call (include/mbrwt.h mbrwt_get_rows_device_async:
+    # no host synchronisation per step; the status block -- labels, status,
+    # sticky status bits -- is read once after the timed region)
+    use_async = world == 1 and not a.sync
+    status_t = torch.zeros(3, dtype=torch.int64, device=dev_t)
+
     def step():
         i = state["i"]
         o, cb = bufs[i % len(bufs)]
         state["i"] += 1
         h0 = time.perf_counter()
+        if use_async:
+            mat.get_rows_device_async(rows_ts[i % K], o, cb, status_t, sptr)
+            return None
         n_lab = mat.get_rows_device(rows_ts[i % K], o, cb, sptr)
         if state["timed"]:
             state["get_rows_host"].append((time.perf_counter() - h0) * 1e3)
@@ -395,6 +410,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     state["timed"] = False
+    if use_async:
+        need_l, st_l, sticky = status_t.cpu().tolist()
+        if sticky != 1 << L.MBRWT_OK:
+            raise RuntimeError(f"asynchronous get_rows reported status bits {sticky:#x} (last status {st_l})")
+        n_lab = int(need_l)
     log(f"timed {a.steps} steps: {elapsed / a.steps * 1e3:.3f} ms/step")
     mat.set_option(L.MBRWT_OPT_TIMING, 0)
     kern_ms_total, launches = mat.take_timing()
@@ -454,7 +474,7 @@ def main():
     stream_gbs = rnd = None
     if rank == 0 and not a.no_probe:
         free, _ = torch.cuda.mem_get_info(dev_t)
-        stream_gbs, rnd = probe_ceilings(dev_t, sptr, free)
+        stream_gbs, rnd = probe_ceilings(dev_t, sptr, free, struct_bytes)
 
     # exact work accounting for the algorithmic roofline (untimed diagnostic pass)
     visits, labels = mat.count_work_device(rows_t, sptr)
@@ -572,6 +592,7 @@ def main():
                         f"global batch {G:,} rows, {nb:,} per GPU ({a.scaling} scaling)",
             "num_rows": a.rows, "num_columns": a.cols, "density": a.density, "arity": a.arity,
             "global_batch": G, "batch_per_gpu": nb, "batches": K, "layout": a.layout,
+            "api": "mbrwt_get_rows_device_async" if use_async else "mbrwt_get_rows_device",
             "parallelism": f"batch-sharded x{world}, tree replicated" + ("" if world == 1 or a.no_gather
                                                                          else ", all-gatherv over " + ("RCCL" if a.dist_backend == "nccl" else a.dist_backend)),
             "structure_bytes": struct_bytes,

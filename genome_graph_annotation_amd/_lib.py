@@ -167,6 +167,12 @@ SIGNATURES = {
     # include/mbrwt_wt.h (BinRel-WT)
     "mbrwt_wt_create": (C.c_int, [C.POINTER(BinRelDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "mbrwt_wt_create_synthetic": (C.c_int, [C.POINTER(BinRelSynthDesc), C.c_int, C.POINTER(C.c_void_p)]),
+    "mbrwt_wt_parse": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p)]),
+    "mbrwt_binrel_get_desc": (C.POINTER(BinRelDesc), [C.c_void_p]),
+    "mbrwt_binrel_free": (None, [C.c_void_p]),
+    "mbrwt_wt_serialize_desc": (C.c_int, [C.POINTER(BinRelDesc), C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "mbrwt_wt_load": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64), C.c_int, C.POINTER(C.c_void_p)]),
+    "mbrwt_wt_serialize": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]),
     "mbrwt_wt_destroy": (None, [C.c_void_p]),
     "mbrwt_wt_num_rows": (C.c_uint64, [C.c_void_p]),
     "mbrwt_wt_num_columns": (C.c_uint64, [C.c_void_p]),

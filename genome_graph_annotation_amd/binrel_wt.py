@@ -18,6 +18,56 @@ def _p(a, t):
     return a.ctypes.data_as(C.POINTER(t))
 
 
+def _bytes_call(fn, what):
+    """Capacity protocol for a byte stream: size, then fill."""
+    need = C.c_uint64(0)
+    rc = fn(None, 0, C.byref(need))
+    if rc not in (L.MBRWT_OK, L.MBRWT_ERR_CAPACITY):
+        L.check(rc, what)
+    buf = (C.c_uint8 * max(1, need.value))()
+    L.check(fn(buf, need.value, C.byref(need)), what)
+    return bytes(buf[: need.value])
+
+
+def _binrel_desc(offsets, cols, num_columns):
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    cols = np.ascontiguousarray(cols, dtype=np.uint32)
+    if not cols.size:
+        cols = np.zeros(1, dtype=np.uint32)
+    d = L.BinRelDesc()
+    d.num_rows = len(offsets) - 1
+    d.num_columns = int(num_columns)
+    d.offsets = _p(offsets, C.c_uint64)
+    d.cols = _p(cols, C.c_uint32)
+    return d, (offsets, cols)
+
+
+def serialize_csr(offsets, cols, num_columns) -> bytes:
+    """BinRelWT_sdsl::serialize (bin_rel_wt_sdsl.cpp:124-132) of CSR rows, host
+    only (mbrwt_wt_serialize_desc; byte layout parity unpinned)."""
+    d, keep = _binrel_desc(offsets, cols, num_columns)
+    return _bytes_call(lambda b, c, n: L.lib().mbrwt_wt_serialize_desc(C.byref(d), b, c, n),
+                       "mbrwt_wt_serialize_desc")
+
+
+def parse_stream(data: bytes):
+    """BinRelWT_sdsl::load (bin_rel_wt_sdsl.cpp:113-122) into CSR, host only:
+    (offsets, cols, num_columns, bytes consumed)."""
+    buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+    h = C.c_void_p()
+    used = C.c_uint64(0)
+    L.check(L.lib().mbrwt_wt_parse(buf, len(data), C.byref(used), C.byref(h)), "mbrwt_wt_parse")
+    try:
+        d = L.lib().mbrwt_binrel_get_desc(h).contents
+        n = d.num_rows
+        off = np.ctypeslib.as_array(d.offsets, shape=(n + 1,)).copy()
+        nrel = int(off[-1])
+        cols = np.ctypeslib.as_array(d.cols, shape=(nrel,)).copy() if nrel else np.zeros(0, dtype=np.uint32)
+        return off, cols, int(d.num_columns), int(used.value)
+    finally:
+        L.lib().mbrwt_binrel_free(h)
+
+
 class BinRelWTDevice:
     """A BinRel-WT held in HBM; queries run the HIP wavelet-matrix kernels."""
 
@@ -57,6 +107,18 @@ class BinRelWTDevice:
         h = C.c_void_p()
         L.check(L.lib().mbrwt_wt_create_synthetic(C.byref(d), device, C.byref(h)), "mbrwt_wt_create_synthetic")
         return cls(h)
+
+    @classmethod
+    def load(cls, data: bytes, device=0):
+        """BinRelWT_sdsl::load (bin_rel_wt_sdsl.cpp:113-122): mbrwt_wt_load."""
+        buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+        h = C.c_void_p()
+        L.check(L.lib().mbrwt_wt_load(buf, len(data), None, device, C.byref(h)), "mbrwt_wt_load")
+        return cls(h)
+
+    def serialize(self) -> bytes:
+        """BinRelWT_sdsl::serialize (bin_rel_wt_sdsl.cpp:124-132): mbrwt_wt_serialize."""
+        return _bytes_call(lambda b, c, n: L.lib().mbrwt_wt_serialize(self._h, b, c, n), "mbrwt_wt_serialize")
 
     def __del__(self):
         if getattr(self, "_h", None):

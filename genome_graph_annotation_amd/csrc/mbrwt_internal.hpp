@@ -341,6 +341,7 @@ struct Ctx {
     const void *rb_fn = nullptr;
     size_t rb_lds = 0;
     uint32_t rb_threads = 0;
+    int rb_cap = 0;
     int rb_blocks = 0;  // resident workgroups on the device
 
     // Row shards (rows >= 2^32; DESIGN.md §4 "Rows >= 2^32"): a BRWT restricted

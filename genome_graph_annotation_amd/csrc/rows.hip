@@ -833,6 +833,7 @@ struct RowsParams {
     uint32_t *ovf_list;           // batch indices of the rows of direct tiles
     unsigned long long *scalars;  // [1] direct rows, [2] error flags
     uint32_t walk4;               // 1: rows_walk4 (default), 2: rows_walk5 (MBRWT_ROWS_WALK=5), 0: rows_walk2 (=2)
+    uint32_t stk_words;           // per-lane LDS stack slots of the v2/v3 kernels (rows_stack_words)
     uint32_t diag;                // MBRWT_ROWS_DIAG (timing experiments; WRONG results): 1 no walk,
                                   // 2 walk without label stores, 4 no spill reads
 };
@@ -1171,7 +1172,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
     const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows2[0]);
     const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows2 + 4;
     const uint32_t C = p.C;
-    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows2 + ((p.table_words + 3) & ~3u)) + wv * (64u * B + 64u * 4 * (MAXD + 1));
+    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows2 + ((p.table_words + 3) & ~3u)) + wv * (64u * B + 256u * p.stk_words);
     AS_LDS uint8_t *mine = wb + lane * B;
     AS_LDS uint32_t *stk = (AS_LDS uint32_t *)(wb + 64u * B) + lane;
     constexpr uint32_t LPB = B / 16, RPI = 64 / LPB;
@@ -1299,7 +1300,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows3(RowsParams p) {
     const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows3[0]);
     const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows3 + 4;
     const uint32_t C = p.C;
-    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows3 + ((p.table_words + 3) & ~3u)) + wv * (64u * B + 64u * 4 * (MAXD + 1));
+    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows3 + ((p.table_words + 3) & ~3u)) + wv * (64u * B + 256u * p.stk_words);
     AS_LDS uint8_t *mine = wb + lane * B;
     AS_LDS uint32_t *stk = (AS_LDS uint32_t *)(wb + 64u * B) + lane;
     const uint64_t ntiles = (p.n + 63) / 64;
@@ -1686,14 +1687,21 @@ RowsFn rows2_fn_d(uint32_t frames) {
                : frames <= 8 ? k_traverse_rows3<B, 8, kRows3Wpb, NT>
                              : k_traverse_rows3<B, 16, kRows3Wpb, NT>;
 }
-uint32_t rows_maxd(const RowsImage &im) { return im.frames <= 4 ? 4 : im.frames <= 8 ? 8 : 16; }
+// per-lane stack slots: rows_walk4 keeps the current frame in registers and
+// pushes only on a descent, so at most frames - 1 are pending; rows_walk5
+// also writes one slot past the top (slot 0 is its dummy).  Exact sizing
+// keeps a workgroup of 8 waves within a quarter of the CU's LDS at the
+// Kingsford shape (3 frames: 8 x (4096 + 512) B + the table).
+uint32_t rows_stack_words(const RowsImage &im, uint32_t walk) {
+    return walk == 2 ? im.frames + 2 : std::max(1u, im.frames ? im.frames - 1 : 1u);
+}
 template <int V>
 RowsFn rows2_fn_v(const RowsImage &im) {
     const bool nt = im.bytes > (1ull << 30);
     if (im.B == 64) return nt ? rows2_fn_d<64, true, V>(im.frames) : rows2_fn_d<64, false, V>(im.frames);
     return nt ? rows2_fn_d<128, true, V>(im.frames) : rows2_fn_d<128, false, V>(im.frames);
 }
-RowsFn rows2_fn(const RowsImage &im) { return rows_version() == 2 ? rows2_fn_v<2>(im) : rows2_fn_v<3>(im); }
+RowsFn rows2_fn(const RowsImage &im) { return rows_version() == 3 ? rows2_fn_v<3>(im) : rows2_fn_v<2>(im); }
 
 template <int B, bool NT>
 RowsFn rows_fn_d(uint32_t height) {
@@ -1782,13 +1790,21 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         const char *e = std::getenv("MBRWT_ROWS_WALK");
         p.walk4 = (e && e[0] == '2') ? 0u : (e && e[0] == '5') ? 2u : 1u;  // default: the v4 walk
     }
+    p.stk_words = rows_stack_words(im, p.walk4);
 
     const RowsFn kfn = v1 ? rows_fn(im) : rows2_fn(im);
-    const uint32_t wpb = v1 ? kRowsWpb : rows_version() == 2 ? kRows2Wpb : kRows3Wpb;
+    const uint32_t wpb = v1 ? kRowsWpb : rows_version() == 3 ? kRows3Wpb : kRows2Wpb;
     const size_t lds = v1 ? ((im.table.size() + 3) & ~size_t(3)) * 4 + kRowsWpb * (64ull * im.B + 2ull * C)
-                          : ((im.table2.size() + 3) & ~size_t(3)) * 4 + wpb * (64ull * im.B + 64ull * 4 * (rows_maxd(im) + 1));
+                          : ((im.table2.size() + 3) & ~size_t(3)) * 4 + wpb * (64ull * im.B + 256ull * p.stk_words);
     const uint32_t threads = 64 * wpb;
-    if (c.rb_fn != reinterpret_cast<const void *>(kfn) || c.rb_lds != lds || c.rb_threads != threads) {
+    // at most 3 workgroups (24 waves) per CU: more waves make the walk phase
+    // slower than the extra loads in flight gain (C4 0.426 ms at 3 against
+    // 0.456 at 4, C2 0.068 against 0.073: profiles/r03/v06_rows_occupancy_*);
+    // MBRWT_ROWS_WGS_PER_CU overrides (sweeps)
+    const char *occ_e = std::getenv("MBRWT_ROWS_WGS_PER_CU");
+    const int occ_cap = occ_e ? std::max(1, std::atoi(occ_e)) : 3;
+    if (c.rb_fn != reinterpret_cast<const void *>(kfn) || c.rb_lds != lds || c.rb_threads != threads ||
+        c.rb_cap != occ_cap) {
         if (lds > 65536)
             MBRWT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kfn),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1798,6 +1814,8 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
                 hipSuccess ||
             per_cu <= 0)
             per_cu = 1;
+        if (occ_cap) per_cu = std::min(per_cu, occ_cap);
+        c.rb_cap = occ_cap;
         c.rb_fn = reinterpret_cast<const void *>(kfn);
         c.rb_lds = lds;
         c.rb_threads = threads;

@@ -331,3 +331,122 @@ inline std::vector<uint64_t> get_rrr(Reader &r, uint64_t *size_out) {
 
 }  // namespace fmt
 }  // namespace mbrwt
+
+namespace mbrwt {
+namespace fmt {
+
+// ---- sdsl int_vector<64> (fixed width: the header has no width byte) -----
+inline void put_int_vector64(Writer &w, const std::vector<uint64_t> &v) {
+    w.u64le((uint64_t)v.size() * 64);
+    for (uint64_t x : v) w.u64le(x);
+}
+inline std::vector<uint64_t> get_int_vector64(Reader &r) {
+    const uint64_t bits = r.u64le();
+    if (bits % 64) throw FormatError("int_vector<64>: size not a multiple of 64 bits");
+    const uint64_t W = r.words_for(bits);
+    std::vector<uint64_t> v(W);
+    for (uint64_t k = 0; k < W; ++k) v[k] = r.u64le();
+    return v;
+}
+
+// ---- sdsl wt_int<rrr_vector<63>> ------------------------------------------
+// (BinRelWT_sdsl::wt_, bin_rel_wt_sdsl.hpp:40; construct_im at
+// bin_rel_wt_sdsl.cpp:39.)  sdsl-lite's published layout: {u64 size, u64
+// sigma (the effective alphabet: distinct symbols), rrr_vector<63> tree of
+// size * max_level bits, the rrr rank/select supports (no bytes), u32
+// max_level, int_vector<64> zero_cnt (zeros per level), int_vector<64>
+// rank_level (ones before each level)}.  Level l of the tree holds bit
+// max_level - 1 - l of every symbol, the symbols stably ordered by their top l
+// bits (the wavelet tree's nodes side by side); max_level = bits of
+// max(1, largest symbol).  PARITY UNPINNED like the rest of this file.
+inline void put_wt_int(Writer &w, const std::vector<uint64_t> &seq) {
+    const uint64_t n = seq.size();
+    uint64_t mx = 1;
+    for (uint64_t x : seq) mx = std::max(mx, x);
+    const uint32_t levels = hi_bit(mx) + 1;
+    std::vector<uint64_t> sorted(seq);
+    std::sort(sorted.begin(), sorted.end());
+    const uint64_t sigma = n ? (uint64_t)(std::unique(sorted.begin(), sorted.end()) - sorted.begin()) : 0;
+    std::vector<uint64_t> tree((n * levels + 63) / 64 + 1, 0), zero_cnt(levels, 0), rank_level(levels, 0);
+    std::vector<uint64_t> cur(seq), nxt(n);
+    uint64_t ones = 0;
+    for (uint32_t l = 0; l < levels; ++l) {
+        const uint32_t bit = levels - 1 - l;
+        rank_level[l] = ones;
+        // nodes: runs of equal top-l prefixes in `cur`; each is split stably
+        uint64_t i = 0;
+        while (i < n) {
+            const uint64_t pre = (l ? cur[i] >> (bit + 1) : 0);
+            uint64_t j = i;
+            while (j < n && (l ? cur[j] >> (bit + 1) : 0) == pre) ++j;
+            uint64_t z = i;
+            for (uint64_t k = i; k < j; ++k) {
+                const uint64_t b = (cur[k] >> bit) & 1;
+                if (b) {
+                    tree[(l * n + k) >> 6] |= 1ull << ((l * n + k) & 63);
+                    ++ones;
+                } else {
+                    nxt[z++] = cur[k];
+                }
+            }
+            zero_cnt[l] += z - i;
+            for (uint64_t k = i; k < j; ++k)
+                if ((cur[k] >> bit) & 1) nxt[z++] = cur[k];
+            i = j;
+        }
+        cur.swap(nxt);
+    }
+    w.u64le(n);
+    w.u64le(sigma);
+    tree.resize((n * levels + 63) / 64);
+    put_rrr(w, tree, n * levels);
+    const uint32_t ml = levels;
+    w.bytes(&ml, 4);
+    put_int_vector64(w, zero_cnt);
+    put_int_vector64(w, rank_level);
+}
+
+inline std::vector<uint64_t> get_wt_int(Reader &r) {
+    const uint64_t n = r.u64le();
+    (void)r.u64le();  // sigma
+    uint64_t tbits = 0;
+    const std::vector<uint64_t> tree = get_rrr(r, &tbits);
+    uint32_t levels = 0;
+    r.bytes(&levels, 4);
+    const std::vector<uint64_t> zero_cnt = get_int_vector64(r), rank_level = get_int_vector64(r);
+    if (levels == 0 || levels > 64) throw FormatError("wt_int: bad max_level");
+    if (tbits % levels || tbits / levels != n) throw FormatError("wt_int: tree size != size * max_level");
+    if (zero_cnt.size() != levels || rank_level.size() != levels) throw FormatError("wt_int: level vectors");
+    // decode: order[k] = the sequence position of the k-th symbol of the
+    // current level; every level's stable split refines the order
+    std::vector<uint64_t> val(n, 0), order(n), nxt(n), pre(n, 0);
+    for (uint64_t k = 0; k < n; ++k) order[k] = k;
+    uint64_t ones = 0;
+    for (uint32_t l = 0; l < levels; ++l) {
+        if (rank_level[l] != ones) throw FormatError("wt_int: rank_level mismatch");
+        uint64_t i = 0, zeros = 0;
+        while (i < n) {
+            uint64_t j = i;
+            while (j < n && pre[order[j]] == pre[order[i]]) ++j;
+            uint64_t z = i;
+            for (uint64_t k = i; k < j; ++k) {
+                const uint64_t p = l * n + k;
+                const uint64_t b = (tree[p >> 6] >> (p & 63)) & 1;
+                val[order[k]] = (val[order[k]] << 1) | b;
+                if (!b) nxt[z++] = order[k];
+                ones += b;
+            }
+            zeros += z - i;
+            for (uint64_t k = i; k < j; ++k)
+                if (val[order[k]] & 1) nxt[z++] = order[k];
+            i = j;
+        }
+        if (zero_cnt[l] != zeros) throw FormatError("wt_int: zero_cnt mismatch");
+        order.swap(nxt);
+        for (uint64_t k = 0; k < n; ++k) pre[k] = val[k];
+    }
+    return val;
+}
+
+}  // namespace fmt
+}  // namespace mbrwt

@@ -11,6 +11,7 @@
  *   BinRelWT_sdsl::get_row                         bin_rel_wt_sdsl.cpp:51-83   -> mbrwt_wt_get_rows[_device]
  *   BinRelWT_sdsl::get                             bin_rel_wt_sdsl.cpp:98-109  -> mbrwt_wt_get_batch[_device]
  *   BinRelWT_sdsl::get_column                      bin_rel_wt_sdsl.cpp:85-96   -> mbrwt_wt_get_column[_device]
+ *   BinRelWT_sdsl::load / serialize                bin_rel_wt_sdsl.cpp:113-132 -> mbrwt_wt_load / mbrwt_wt_serialize
  *
  * Semantics: rows are sets of column ids (BinaryMatrix rows).  get_row
  * returns the row's ids ascending (sdsl wt_int::interval_symbols order);
@@ -95,6 +96,29 @@ int mbrwt_wt_get_top_labels_batch_device(mbrwt_wt *ctx, const uint64_t *d_rows, 
                                          const uint64_t *d_read_offsets, uint64_t n_reads, uint64_t num_top,
                                          uint64_t *d_label_offsets, uint32_t *d_labels, uint64_t *d_counts,
                                          uint64_t labels_cap, uint64_t *labels_needed, void *stream);
+
+/*
+ * The reference's file stream (BinRelWT_sdsl::load / serialize,
+ * bin_rel_wt_sdsl.cpp:113-132): {num_columns as a libmaus2 number, the
+ * concatenated rows' ids as sdsl wt_int<rrr_vector<63>>, bit_vector_rrr
+ * delimiters -- a 1, then per row a 0 per id and a 1}.  Byte layouts restated
+ * from sdsl-lite's / libmaus2's published formats: PARITY UNPINNED (DESIGN.md
+ * §13).  Host only except mbrwt_wt_load (creates a device context) and
+ * mbrwt_wt_serialize (reads a context's rows back, ids ascending per row).
+ *
+ * mbrwt_wt_parse         stream -> an owned CSR (mbrwt_binrel_get_desc);
+ *                        MBRWT_ERR_INVALID on a malformed stream (the
+ *                        reference's load returns false); *consumed = bytes read
+ * mbrwt_wt_serialize_desc  CSR -> stream, ids in the given order; capacity
+ *                        protocol as mbrwt_tree_serialize (buf may be NULL)
+ */
+typedef struct mbrwt_binrel mbrwt_binrel;
+int mbrwt_wt_parse(const uint8_t *bytes, uint64_t len, uint64_t *consumed, mbrwt_binrel **out);
+const mbrwt_binrel_desc *mbrwt_binrel_get_desc(const mbrwt_binrel *b);
+void mbrwt_binrel_free(mbrwt_binrel *b);
+int mbrwt_wt_serialize_desc(const mbrwt_binrel_desc *desc, uint8_t *buf, uint64_t cap, uint64_t *needed);
+int mbrwt_wt_load(const uint8_t *bytes, uint64_t len, uint64_t *consumed, int device, mbrwt_wt **out);
+int mbrwt_wt_serialize(mbrwt_wt *ctx, uint8_t *buf, uint64_t cap, uint64_t *needed);
 
 int mbrwt_wt_set_option(mbrwt_wt *ctx, int option, int64_t value);
 int mbrwt_wt_take_timing(mbrwt_wt *ctx, double *kernel_ms, uint64_t *launches);

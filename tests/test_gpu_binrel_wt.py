@@ -171,3 +171,24 @@ def test_classify_batches_over_binrel_wt(oracle_mod, ratio, num_top):
     assert got == len(labs)
     np.testing.assert_array_equal(lot.cpu().numpy().view(np.uint64), lo)
     np.testing.assert_array_equal(lt[:got].cpu().numpy().view(np.uint32), labs)
+
+
+@pytest.mark.parametrize("n,m,dens", [(0, 3, 0.0), (9, 7, 0.5), (4000, 2652, 0.003), (3000, 257, 0.2)])
+def test_load_and_serialize(oracle_mod, n, m, dens):
+    """BinRelWT_sdsl::load / serialize (bin_rel_wt_sdsl.cpp:113-132): a stream
+    written from CSR loads into a device matrix that answers like the oracle,
+    and the device matrix serialises back to the same bytes (byte layout
+    parity unpinned: sdsl absent)."""
+    from genome_graph_annotation_amd import BinRelWTDevice
+    from genome_graph_annotation_amd.binrel_wt import serialize_csr
+    O = oracle_mod
+    rng = np.random.default_rng(n + 7 * m)
+    dense = rng.random((n, m)) < dens
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(dense.sum(1), out=off[1:])
+    cols = np.nonzero(dense)[1].astype(np.uint32)
+    data = serialize_csr(off, cols, m)
+    d = BinRelWTDevice.load(data)
+    if n:
+        _compare(O, O.OracleWT.from_dense(dense), d, cols=range(min(m, 40)))
+    assert d.serialize() == data

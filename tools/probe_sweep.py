@@ -21,6 +21,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=float, default=64.0)
     ap.add_argument("--out", default="")
+    ap.add_argument("--segs", default="64,0,32,128,256", help="segment bytes (0: one 64-B segment per lane)")
     a = ap.parse_args()
     import torch
 
@@ -36,7 +37,7 @@ def main() -> int:
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     res = []
     best = {}
-    for seg in (64, 0, 32, 128, 256):
+    for seg in [int(x) for x in a.segs.split(",")]:
         for u in (1, 2, 4, 8, 16):
             if seg == 0 and u > 4:
                 continue
