@@ -8,7 +8,9 @@
 // the reference) throw std::out_of_range.
 #pragma once
 
+#include <fstream>
 #include <functional>
+#include <iterator>
 
 #include "../../include/mbrwt_wt.h"
 #include "brwt_device.hpp"
@@ -149,13 +151,44 @@ class BinRelWTDevice : public BinaryMatrix {
         return rows;
     }
 
-    // BinRelWT_sdsl::load / serialize (bin_rel_wt_sdsl.cpp:85-111): the sdsl
-    // wt_int<rrr_vector<63>> stream is not restated by this build (the file
-    // row of SURVEY §8(f) is the BRWT's); load reports failure as the
-    // reference's does for a stream it cannot read, serialize throws
-    bool load(std::istream &) override { return false; }
-    void serialize(std::ostream &) const override {
-        throw std::runtime_error("BinRelWTDevice::serialize: the BinRel-WT(sdsl) file format is not supported");
+    // BinRelWT_sdsl::load / serialize (bin_rel_wt_sdsl.cpp:113-132) through
+    // mbrwt_wt_load / mbrwt_wt_serialize (include/mbrwt_wt.h; byte layout
+    // parity unpinned).  load reads the rest of the stream, returns false on
+    // a malformed one as the reference's does; serialize throws on a bad stream.
+    bool load(std::istream &in) override {
+        if (!in.good()) return false;
+        const std::streampos at = in.tellg();
+        std::vector<uint8_t> bytes((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+        mbrwt_binrel *b = nullptr;
+        uint64_t used = 0;
+        if (mbrwt_wt_parse(bytes.data(), bytes.size(), &used, &b) != MBRWT_OK) return false;
+        std::unique_ptr<mbrwt_binrel, void (*)(mbrwt_binrel *)> owned(b, mbrwt_binrel_free);
+        const mbrwt_binrel_desc *d = mbrwt_binrel_get_desc(b);
+        if (d->num_rows == 0) {  // BinRelWT_sdsl(): the empty matrix
+            ctx_.reset();
+        } else {
+            mbrwt_wt *c = nullptr;
+            if (mbrwt_wt_create(d, 0, &c) != MBRWT_OK) return false;
+            ctx_.reset(c, Deleter());
+        }
+        in.clear();
+        if (at != std::streampos(-1)) in.seekg(at + std::streamoff(used));  // just past what was read
+        return true;
+    }
+    void serialize(std::ostream &out) const override {
+        if (!out.good()) throw std::ofstream::failure("Bad stream");
+        uint64_t need = 0;
+        const uint64_t zero = 0;
+        const mbrwt_binrel_desc empty{0, 0, &zero, nullptr};
+        auto write = [&](uint8_t *buf, uint64_t cap) {
+            return ctx_ ? mbrwt_wt_serialize(ctx_.get(), buf, cap, &need)
+                        : mbrwt_wt_serialize_desc(&empty, buf, cap, &need);
+        };
+        int st = write(nullptr, 0);
+        if (st != MBRWT_ERR_CAPACITY && st != MBRWT_OK) check_status(st, "BinRelWTDevice::serialize");
+        std::vector<uint8_t> buf(need);
+        check_status(write(buf.data(), buf.size()), "BinRelWTDevice::serialize");
+        out.write(reinterpret_cast<const char *>(buf.data()), (std::streamsize)need);
     }
 
   private:

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <functional>
 #include <set>
+#include <sstream>
 
 #include "../../genome_graph_annotation_amd/csrc/binrel_wt_device.hpp"
 #include "../../oracle/binrel_wt_oracle.h"
@@ -134,6 +135,38 @@ TEST(BinRelWT_sdsl, OutOfRange) {  // an assert / UB in the reference; the mirro
     EXPECT_THROW(m->get_row(3), std::out_of_range);
     EXPECT_THROW(m->get(0, 4), std::out_of_range);
     EXPECT_THROW(m->get_column(4), std::out_of_range);
+}
+
+// test_serialization (test_bin_rel_wt_sdsl.cpp:182-208) on the device mirror
+// (the oracle has no stream): dump, a bad stream does not load, the dump
+// loads back with the same shape and columns.  Byte layout parity unpinned.
+static void check_serialization(const BinaryMatrix &m) {
+    std::stringstream good;
+    m.serialize(good);
+    {
+        mbrwt_host::BinRelWTDevice loaded;
+        std::stringstream bad("not a BinRelWT stream");
+        ASSERT_TRUE(!loaded.load(bad));
+    }
+    mbrwt_host::BinRelWTDevice loaded;
+    ASSERT_TRUE(loaded.load(good));
+    ASSERT_TRUE(good.good());
+    ASSERT_EQ(m.num_columns(), loaded.num_columns());
+    ASSERT_EQ(m.num_rows(), loaded.num_rows());
+    for (size_t j = 0; j < loaded.num_columns(); ++j) EXPECT_EQ(m.get_column(j), loaded.get_column(j));
+}
+TEST(BinRelWT_sdsl, Serialization) {  // :210-272: empty, all zero, all one, mixed
+    if (!g_device) return;
+    check_serialization(mbrwt_host::BinRelWTDevice());
+    for (size_t nc = 1; nc < 8; ++nc)
+        for (size_t nr = 1; nr < 8; nr += 2) {
+            Rows zero(nr, std::vector<bool>(nc, false)), one(nr, std::vector<bool>(nc, true)), mixed = zero;
+            for (size_t j = 0; j < nr; ++j)
+                for (size_t i = 1; i + 1 < nc; ++i) mixed[j][i] = (i + j) % 2;
+            check_serialization(*build(zero, nc));
+            check_serialization(*build(one, nc));
+            check_serialization(*build(mixed, nc));
+        }
 }
 
 int main(int argc, char **argv) {
