@@ -260,6 +260,7 @@ struct RowsImage {
     std::vector<uint32_t> table2;   // RWT2 table (k_traverse_rows: one word per child, leaf parents inline)
     uint32_t *d_table2 = nullptr;
     uint32_t frames = 0;            // its stack levels
+    bool mask1 = false;             // every internal node (leaf parents too) has arity <= 8: one-byte masks
     uint64_t bytes = 0;             // blocks + spill used
     // build statistics
     uint64_t spilled_rows = 0, long_rows = 0, record_bytes = 0, spill_bytes = 0;

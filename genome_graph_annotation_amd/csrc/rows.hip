@@ -606,6 +606,11 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
             set_error("tree shape outside the row-record limits (arity <= 16, columns < 2^15, height <= 16)");
             return MBRWT_ERR_UNSUPPORTED;
         }
+        // one-byte masks everywhere (rows_walk6): the root and every internal
+        // or leaf-parent entry of arity <= 8
+        auto ar8 = [](uint32_t e) { return (e >> 30) == 2u || ((e >> 16) & 0x1Fu) <= 8; };
+        im.mask1 = ar8(im.table2[0]);
+        for (size_t i = 4; i < im.table2.size(); ++i) im.mask1 = im.mask1 && ar8(im.table2[i]);
     }
     if (nr > rb.sz_cap) {
         if (rb.d_sz) MBRWT_HIP(hipFree(rb.d_sz));
@@ -834,6 +839,7 @@ struct RowsParams {
     unsigned long long *scalars;  // [1] direct rows, [2] error flags
     uint32_t walk4;               // 1: rows_walk4 (default), 2: rows_walk5 (MBRWT_ROWS_WALK=5), 0: rows_walk2 (=2)
     uint32_t stk_words;           // per-lane LDS stack slots of the v2/v3 kernels (rows_stack_words)
+    uint32_t stage;               // v2 + walk 6: labels staged in LDS, stored as 16-byte vectors
     uint32_t diag;                // MBRWT_ROWS_DIAG (timing experiments; WRONG results): 1 no walk,
                                   // 2 walk without label stores, 4 no spill reads
 };
@@ -1119,6 +1125,66 @@ __device__ __forceinline__ void rows_walk4(const AS_LDS uint8_t *pb, uint32_t o,
     }
 }
 
+// v6 walk (the default when every internal node has arity <= 8, so every
+// mask is one byte): rows_walk4's steps in about half the vector
+// instructions -- the walk is VALU-bound (r03 SQ counters: 186 M of the
+// kernel's 196 M VALU wave-instructions per 8 M rows are the walk; a wave64
+// VALU instruction occupies the SIMD 4 cycles).  The record cursor is an LDS
+// byte address, the stack pointer a per-lane LDS address (slot stride 256
+// bytes), the table index is one add-shift, finished lanes leave the loop
+// (exec mask) instead of being carried by selects, and leaves / leaf parents
+// and internal children take exec-masked branches.
+// OUT = a global u16 pointer (labels stored one by one into the tile's temp
+// region) or an LDS u16 pointer (the wave's label stage, MBRWT_ROWS_STAGE=1)
+template <typename OUT>
+__device__ __forceinline__ void rows_walk6(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
+                                           const AS_LDS uint32_t *ent, AS_LDS uint32_t *stk, OUT out,
+                                           uint32_t pos) {
+    const AS_LDS uint8_t *rc = pb + o;  // record cursor
+    const uint32_t rm = rc[0];
+    ++rc;
+    if ((root >> 30) == 3u) {  // a one-level tree: the root is a leaf parent
+        if (live)
+            for (uint32_t x = rm; x; x &= x - 1) out[pos++] = (uint16_t)((root & 0xFFFFu) + (uint32_t)__builtin_ctz(x));
+        return;
+    }
+    if (!live) return;
+    uint32_t f = root & 0xFFFFu, m = rm;
+    AS_LDS uint32_t *sp = stk;
+    uint32_t ob = pos * 2u;  // byte offset of the next label
+    while (m != 0u) {
+        const uint32_t c = (uint32_t)__builtin_ctz(m);
+        m &= m - 1u;
+        const uint32_t e = ent[f + c];
+        const uint32_t mw = *rc;
+        if ((int32_t)e < 0) {  // a leaf (its column) or a leaf parent (its set children)
+            const bool lp = (e >> 30) & 1u;
+            uint32_t x = lp ? mw : 1u;
+            rc += lp ? 1 : 0;
+            const uint32_t base = e & 0xFFFFu;
+            do {
+                *(OUT)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));
+                ob += 2u;
+                x &= x - 1u;
+            } while (x);
+        } else {  // an internal child: push the rest of this frame, descend
+            if (m) {
+                *sp = f | (m << 16);
+                sp += 64;
+            }
+            f = e & 0xFFFFu;
+            m = mw;
+            ++rc;
+        }
+        if (m == 0u && sp != stk) {
+            sp -= 64;
+            const uint32_t w = *sp;
+            f = w & 0xFFFFu;
+            m = w >> 16;
+        }
+    }
+}
+
 // v5 walk: rows_walk4 without divergent branches around the stack -- the
 // push writes the next free slot unconditionally and the pop reads the top
 // slot unconditionally (selects keep what applies), so a step costs vector
@@ -1172,9 +1238,14 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
     const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows2[0]);
     const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows2 + 4;
     const uint32_t C = p.C;
-    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows2 + ((p.table_words + 3) & ~3u)) + wv * (64u * B + 256u * p.stk_words);
-    AS_LDS uint8_t *mine = wb + lane * B;
-    AS_LDS uint32_t *stk = (AS_LDS uint32_t *)(wb + 64u * B) + lane;
+    // a row's block at a stride of B + 4 bytes: lanes reading their records
+    // at similar offsets hit different LDS banks (a B-byte stride puts every
+    // other lane in the same bank)
+    constexpr uint32_t PB = B + 4;
+    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows2 + ((p.table_words + 3) & ~3u)) +
+                         wv * (64u * PB + 256u * p.stk_words + (p.stage ? 2u * p.C : 0u));
+    AS_LDS uint8_t *mine = wb + lane * PB;
+    AS_LDS uint32_t *stk = (AS_LDS uint32_t *)(wb + 64u * PB) + lane;
     constexpr uint32_t LPB = B / 16, RPI = 64 / LPB;
     const uint64_t ntiles = (p.n + 63) / 64;
     const uint64_t tstride = (uint64_t)gridDim.x * WPB;
@@ -1202,7 +1273,13 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
             q[k] = gld_at_nt<u32x4_t, NT>((((uint64_t)hi << 32) | lo) + 16u * (lane % LPB));
         }
 #pragma unroll
-        for (uint32_t k = 0; k < LPB; ++k) ((AS_LDS u32x4_t *)(wb + 1024 * k))[lane] = q[k];
+        for (uint32_t k = 0; k < LPB; ++k) {
+            AS_LDS uint32_t *d = (AS_LDS uint32_t *)(wb + (RPI * k + lane / LPB) * PB + 16u * (lane % LPB));
+            d[0] = q[k].x;
+            d[1] = q[k].y;
+            d[2] = q[k].z;
+            d[3] = q[k].w;
+        }
         wave_sync();
         uint32_t cnt = 0, o = 0;
         bool spl = false;
@@ -1223,7 +1300,13 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
 #pragma unroll
                 for (uint32_t k = 0; k < LPB; ++k) sq[k] = gld_at<u32x4_t>(sa + 16u * k);
 #pragma unroll
-                for (uint32_t k = 0; k < LPB; ++k) ((AS_LDS u32x4_t *)mine)[k] = sq[k];
+                for (uint32_t k = 0; k < LPB; ++k) {
+                    AS_LDS uint32_t *d = (AS_LDS uint32_t *)mine + 4 * k;
+                    d[0] = sq[k].x;
+                    d[1] = sq[k].y;
+                    d[2] = sq[k].z;
+                    d[3] = sq[k].w;
+                }
                 cnt = sq[0].x;
                 lng = 8 + sq[0].y > B;
                 o = 8;
@@ -1241,7 +1324,18 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
         uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
         if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
         if (!direct && !(p.diag & 1)) {
-            if (p.walk4 == 2)
+            if (p.walk4 == 3 && p.stage) {
+                AS_LDS uint16_t *stage = (AS_LDS uint16_t *)(wb + 64u * PB + 256u * p.stk_words);
+                rows_walk6(mine, o, valid && cnt > 0, root, ent, stk, stage, pos);
+                wave_sync();
+                const uint32_t nbytes = total * 2;
+                for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
+                    gst(reinterpret_cast<u32x4_t *>(treg + 128 + q2),
+                        *(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2));
+            } else if (p.walk4 == 3)
+                rows_walk6(mine, o, valid && cnt > 0, root, ent, stk,
+                           (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128), pos);
+            else if (p.walk4 == 2)
                 rows_walk5<MAXD>(mine, o, valid && cnt > 0, root, ent, stk, reinterpret_cast<uint16_t *>(treg + 128),
                                  pos);
             else if (p.walk4)
@@ -1259,6 +1353,167 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
             if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(r0 + lane));
         }
         wave_sync();  // the slots are reused
+    }
+}
+
+// k_traverse_rows (v5): loader and walker waves.  In v2 every wave loads a
+// tile, waits, then walks it, and the two phases hardly overlap (C4: 0.21 ms
+// of loads alone, 0.44 ms with the walk; neither the request rate nor the
+// VALU is saturated).  Here a workgroup's NL loader waves only fetch tiles
+// (blocks -> an LDS slot, entries, spills, count scan, temp counts, direct
+// tiles) and its NW walker waves only walk them, through a ring of NS tile
+// slots in LDS with a state word per slot (2k+1: the workgroup's k-th tile is
+// ready in slot k % NS; 2k+2: it has been walked).  Loader l takes the
+// workgroup's tiles l, l + NL, ..., walker w the tiles w, w + NW, ...; a
+// loader waits for slot k % NS to be released by tile k - NS, a walker for
+// tile k to be ready -- every wait is on a smaller k, so the ring cannot
+// deadlock (all waves of a workgroup are resident), and every wave's loop
+// ends with the workgroup's last tile.  Workgroup tile k = global tile
+// blockIdx.x + k gridDim.x.
+// a ring wait: spin (with s_sleep) on a slot's state word.  Bounded: a wait
+// that outlasts ~2^24 polls (seconds) flags error bit 4 and gives up, so a
+// logic error can never leave the kernel spinning on the GPU.
+__device__ __forceinline__ void rows5_wait(AS_LDS uint32_t *st, uint32_t want, unsigned long long *scalars) {
+    for (uint32_t it = 0;; ++it) {
+        const uint32_t v = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(st, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (v == want) return;
+        if (it > (1u << 24)) {
+            if ((threadIdx.x & 63) == 0) atomicOr(&scalars[2], 4ull);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+template <int B, int NL, int NW, int NS, bool NT>
+__global__ __launch_bounds__(64 * (NL + NW)) void k_traverse_rows5(RowsParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows5[];
+    constexpr uint32_t LPB = B / 16, RPI = 64 / LPB;
+    constexpr uint32_t SLOT = 64u * B + 256u + 16u;  // blocks | per-lane walk words | tile header
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_rows5[i] = gld(p.table + i);
+    const uint32_t slots0 = ((p.table_words + 3) & ~3u) * 4;
+    AS_LDS uint8_t *const lds0 = (AS_LDS uint8_t *)lds_rows5;
+    AS_LDS uint32_t *state = (AS_LDS uint32_t *)(lds0 + slots0 + NS * SLOT);
+    AS_LDS uint32_t *stacks = state + ((NS + 3) & ~3u);
+    if (threadIdx.x < NS) state[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t ntiles = (p.n + 63) / 64;
+    const uint64_t G = gridDim.x;
+    const uint32_t C = p.C;
+    const uint64_t region = 128 + 2ull * C;
+    if (wv < NL) {
+        // ---- loader ---------------------------------------------------------
+        const uint32_t S = p.S;
+        uint64_t k = wv;
+        uint64_t t = blockIdx.x + k * G;
+        uint64_t row_n = 0;
+        if (t < ntiles && t * 64 + lane < p.n) row_n = gld(p.rows + t * 64 + lane);
+        for (; t < ntiles; k += NL, t += NL * G) {
+            const uint64_t r0 = t * 64;
+            const uint32_t nr = (uint32_t)(p.n - r0 < 64 ? p.n - r0 : 64);
+            const uint64_t row = row_n;
+            const uint64_t tn = t + NL * G;
+            if (tn < ntiles && tn * 64 + lane < p.n) row_n = gld(p.rows + tn * 64 + lane);
+            const bool valid = lane < nr && row < p.num_rows;
+            if (lane < nr && !valid) atomicOr(&p.scalars[2], 1ull);
+            const uint64_t b = valid ? rows_block(row, S, p.magic) : 0;
+            const uint32_t sub = (uint32_t)(row - b * S);
+            const uint64_t addr = p.blocks + b * B;
+            u32x4_t q[LPB];
+#pragma unroll
+            for (uint32_t j = 0; j < LPB; ++j) {
+                const int src = (int)(RPI * j + lane / LPB);
+                const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)addr, src, 64);
+                const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(addr >> 32), src, 64);
+                q[j] = gld_at_nt<u32x4_t, NT>((((uint64_t)hi << 32) | lo) + 16u * (lane % LPB));
+            }
+            // the slot of tile k - NS must have been walked
+            const uint32_t si = (uint32_t)(k % NS);
+            const uint32_t want = k >= NS ? (uint32_t)(2 * (k - NS) + 2) : 0u;
+            rows5_wait(&state[si], want, p.scalars);
+            AS_LDS uint8_t *wb = lds0 + slots0 + si * SLOT;
+            AS_LDS uint8_t *mine = wb + lane * B;
+#pragma unroll
+            for (uint32_t j = 0; j < LPB; ++j) ((AS_LDS u32x4_t *)(wb + 1024 * j))[lane] = q[j];
+            wave_sync();
+            uint32_t cnt = 0, o = 0;
+            bool spl = false;
+            if (valid) {
+                const uint32_t e = mine[sub];
+                o = e & 0x7Fu;
+                spl = (e & 0x80u) != 0;
+                cnt = mine[o];
+                ++o;
+            }
+            bool lng = false;
+            if (__any(spl)) {
+                if (spl) {
+                    const uint32_t idx = (uint32_t)mine[o] | ((uint32_t)mine[o + 1] << 8) |
+                                         ((uint32_t)mine[o + 2] << 16) | ((uint32_t)mine[o + 3] << 24);
+                    const uint64_t sa = p.spill + (uint64_t)idx * 16;
+                    u32x4_t sq[LPB];
+#pragma unroll
+                    for (uint32_t j = 0; j < LPB; ++j) sq[j] = gld_at<u32x4_t>(sa + 16u * j);
+#pragma unroll
+                    for (uint32_t j = 0; j < LPB; ++j) ((AS_LDS u32x4_t *)mine)[j] = sq[j];
+                    cnt = sq[0].x;
+                    lng = 8 + sq[0].y > B;
+                    o = 8;
+                }
+            }
+            uint32_t x = cnt;
+#pragma unroll
+            for (uint32_t d = 1; d < 64; d <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+                if (lane >= d) x += y;
+            }
+            const uint32_t total = __builtin_amdgcn_readlane(x, 63);
+            const uint32_t pos = x - cnt;
+            const bool direct = total > C || __any(lng);
+            uint8_t *treg = p.temp + t * region;
+            if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
+            if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u));
+            if (direct) {
+                unsigned long long k0 = 0;
+                if (lane == 0) k0 = atomicAdd(&p.scalars[1], (unsigned long long)nr);
+                k0 = (unsigned long long)__shfl((long long)k0, 0, 64);
+                if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(r0 + lane));
+            }
+            // walk word: record offset | pos << 8 | live << 31; header: tile, walk flag
+            const bool live = valid && cnt > 0 && !direct && !(p.diag & 1);
+            ((AS_LDS uint32_t *)(wb + 64u * B))[lane] = o | ((pos & 0xFFFFu) << 8) | (live ? 0x80000000u : 0u);
+            if (lane == 0) {
+                ((AS_LDS uint64_t *)(wb + 64u * B + 256u))[0] = t;
+                ((AS_LDS uint32_t *)(wb + 64u * B + 256u))[2] = (direct || (p.diag & 1)) ? 0u : 1u;
+            }
+            wave_sync();
+            if (lane == 0)
+                __hip_atomic_store(&state[si], (uint32_t)(2 * k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    } else {
+        // ---- walker ---------------------------------------------------------
+        const uint32_t w = wv - NL;
+        const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows5[0]);
+        const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows5 + 4;
+        AS_LDS uint32_t *stk = stacks + w * 64u * p.stk_words + lane;
+        for (uint64_t k = w, t = blockIdx.x + k * G; t < ntiles; k += NW, t += NW * G) {
+            const uint32_t si = (uint32_t)(k % NS);
+            const uint32_t want = (uint32_t)(2 * k + 1);
+            rows5_wait(&state[si], want, p.scalars);
+            AS_LDS uint8_t *wb = lds0 + slots0 + si * SLOT;
+            const uint32_t walk = __builtin_amdgcn_readfirstlane(((AS_LDS uint32_t *)(wb + 64u * B + 256u))[2]);
+            if (walk) {
+                const uint32_t ww = ((AS_LDS uint32_t *)(wb + 64u * B))[lane];
+                uint16_t *out = reinterpret_cast<uint16_t *>(p.temp + t * region + 128);
+                rows_walk4<1>(wb + lane * B, ww & 0xFFu, (ww >> 31) != 0, root, ent, stk, out, (ww >> 8) & 0xFFFFu);
+            }
+            wave_sync();
+            if (lane == 0)
+                __hip_atomic_store(&state[si], (uint32_t)(2 * k + 2), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
     }
 }
 
@@ -1399,7 +1654,10 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows3(RowsParams p) {
         uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
         if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
         if (!direct && !(p.diag & 1)) {
-            if (p.walk4 == 2)
+            if (p.walk4 == 3)
+                rows_walk6(mine, o, valid && cnt > 0, root, ent, stk,
+                           (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128), pos);
+            else if (p.walk4 == 2)
                 rows_walk5<MAXD>(mine, o, valid && cnt > 0, root, ent, stk, reinterpret_cast<uint16_t *>(treg + 128),
                                  pos);
             else if (p.walk4)
@@ -1533,7 +1791,10 @@ __global__ __launch_bounds__(256) void k_rows_direct(RowsView v, const uint32_t 
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     if (res) {
         const uint64_t total = res[0], err = res[2];
-        const uint64_t st = (err & 1) ? MBRWT_ERR_RANGE : total > cap ? MBRWT_ERR_CAPACITY : MBRWT_OK;
+        const uint64_t st = (err & 4)   ? MBRWT_ERR_DEVICE
+                            : (err & 1) ? MBRWT_ERR_RANGE
+                            : total > cap ? MBRWT_ERR_CAPACITY
+                                          : MBRWT_OK;
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             status[0] = total;
             status[1] = st;
@@ -1673,7 +1934,7 @@ constexpr uint32_t kRows3Wpb = 4;  // (72 VGPRs: 7 waves per SIMD in 4-wave work
 // for A/B (2 = the default)
 int rows_version() {
     const char *e = std::getenv("MBRWT_ROWS_KERNEL");
-    return (e && (e[0] == '1' || e[0] == '3')) ? e[0] - '0' : 2;
+    return (e && (e[0] == '1' || e[0] == '3' || e[0] == '5')) ? e[0] - '0' : 2;
 }
 bool rows_v1() { return rows_version() == 1; }
 template <int B, bool NT, int V>
@@ -1693,7 +1954,7 @@ RowsFn rows2_fn_d(uint32_t frames) {
 // keeps a workgroup of 8 waves within a quarter of the CU's LDS at the
 // Kingsford shape (3 frames: 8 x (4096 + 512) B + the table).
 uint32_t rows_stack_words(const RowsImage &im, uint32_t walk) {
-    return walk == 2 ? im.frames + 2 : std::max(1u, im.frames ? im.frames - 1 : 1u);
+    return walk == 2 ? im.frames + 2 : std::max(1u, im.frames ? im.frames - 1 : 1u);  // (walks 4 and 6)
 }
 template <int V>
 RowsFn rows2_fn_v(const RowsImage &im) {
@@ -1701,7 +1962,23 @@ RowsFn rows2_fn_v(const RowsImage &im) {
     if (im.B == 64) return nt ? rows2_fn_d<64, true, V>(im.frames) : rows2_fn_d<64, false, V>(im.frames);
     return nt ? rows2_fn_d<128, true, V>(im.frames) : rows2_fn_d<128, false, V>(im.frames);
 }
-RowsFn rows2_fn(const RowsImage &im) { return rows_version() == 3 ? rows2_fn_v<3>(im) : rows2_fn_v<2>(im); }
+// v5 shape: NL loaders + NW walkers over NS slots (B = 64: 8 x 4.4 KB of slots)
+constexpr int kR5L = 4, kR5W = 4, kR5S = 8;
+template <bool NT>
+RowsFn rows5_fn_d(uint32_t B) {
+    return B == 64 ? k_traverse_rows5<64, kR5L, kR5W, kR5S, NT> : k_traverse_rows5<128, 2, 2, 4, NT>;
+}
+uint32_t rows5_wpb(const RowsImage &im) { return im.B == 64 ? kR5L + kR5W : 4u; }
+size_t rows5_lds(const RowsImage &im, uint32_t stk_words) {
+    const uint32_t ns = im.B == 64 ? kR5S : 4, nw = im.B == 64 ? kR5W : 2;
+    return ((im.table2.size() + 3) & ~size_t(3)) * 4 + ns * (64ull * im.B + 272) + ((ns + 3) & ~3u) * 4 +
+           nw * 256ull * stk_words;
+}
+RowsFn rows2_fn(const RowsImage &im) {
+    const int v = rows_version();
+    if (v == 5) return im.bytes > (1ull << 30) ? rows5_fn_d<true>(im.B) : rows5_fn_d<false>(im.B);
+    return v == 3 ? rows2_fn_v<3>(im) : rows2_fn_v<2>(im);
+}
 
 template <int B, bool NT>
 RowsFn rows_fn_d(uint32_t height) {
@@ -1788,21 +2065,32 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     if (const char *e = std::getenv("MBRWT_ROWS_DIAG")) p.diag = (uint32_t)std::atoi(e);
     {
         const char *e = std::getenv("MBRWT_ROWS_WALK");
-        p.walk4 = (e && e[0] == '2') ? 0u : (e && e[0] == '5') ? 2u : 1u;  // default: the v4 walk
+        // default: the v6 walk when every mask is one byte, else the v4 walk
+        p.walk4 = (e && e[0] == '2')   ? 0u
+                  : (e && e[0] == '5') ? 2u
+                  : (e && e[0] == '4') ? 1u
+                  : im.mask1           ? 3u
+                                       : 1u;
     }
     p.stk_words = rows_stack_words(im, p.walk4);
+    if (const char *e = std::getenv("MBRWT_ROWS_STAGE")) p.stage = (p.walk4 == 3 && e[0] == '1') ? 1u : 0u;
 
     const RowsFn kfn = v1 ? rows_fn(im) : rows2_fn(im);
-    const uint32_t wpb = v1 ? kRowsWpb : rows_version() == 3 ? kRows3Wpb : kRows2Wpb;
-    const size_t lds = v1 ? ((im.table.size() + 3) & ~size_t(3)) * 4 + kRowsWpb * (64ull * im.B + 2ull * C)
-                          : ((im.table2.size() + 3) & ~size_t(3)) * 4 + wpb * (64ull * im.B + 256ull * p.stk_words);
+    const bool v5 = rows_version() == 5;
+    if (v5) p.stk_words = rows_stack_words(im, 1);  // (v5 walks with rows_walk4)
+    const uint32_t wpb = v1 ? kRowsWpb : v5 ? rows5_wpb(im) : rows_version() == 3 ? kRows3Wpb : kRows2Wpb;
+    const size_t lds = v1   ? ((im.table.size() + 3) & ~size_t(3)) * 4 + kRowsWpb * (64ull * im.B + 2ull * C)
+                       : v5 ? rows5_lds(im, p.stk_words)
+                            : ((im.table2.size() + 3) & ~size_t(3)) * 4 +
+                                  wpb * (64ull * (im.B + (rows_version() == 2 ? 4 : 0)) + 256ull * p.stk_words +
+                                         (p.stage ? 2ull * C : 0ull));
     const uint32_t threads = 64 * wpb;
-    // at most 3 workgroups (24 waves) per CU: more waves make the walk phase
+    // at most 24 waves (3 workgroups of 8) per CU: more waves make the walk phase
     // slower than the extra loads in flight gain (C4 0.426 ms at 3 against
     // 0.456 at 4, C2 0.068 against 0.073: profiles/r03/v06_rows_occupancy_*);
     // MBRWT_ROWS_WGS_PER_CU overrides (sweeps)
     const char *occ_e = std::getenv("MBRWT_ROWS_WGS_PER_CU");
-    const int occ_cap = occ_e ? std::max(1, std::atoi(occ_e)) : 3;
+    const int occ_cap = occ_e ? std::max(1, std::atoi(occ_e)) : v5 ? 0 : (int)std::max(1u, 24u / wpb);
     if (c.rb_fn != reinterpret_cast<const void *>(kfn) || c.rb_lds != lds || c.rb_threads != threads ||
         c.rb_cap != occ_cap) {
         if (lds > 65536)
@@ -1814,7 +2102,7 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
                 hipSuccess ||
             per_cu <= 0)
             per_cu = 1;
-        if (occ_cap) per_cu = std::min(per_cu, occ_cap);
+        if (occ_cap > 0) per_cu = std::min(per_cu, occ_cap);
         c.rb_cap = occ_cap;
         c.rb_fn = reinterpret_cast<const void *>(kfn);
         c.rb_lds = lds;
@@ -1868,6 +2156,10 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         c.timing_launches += 1;
     }
     const uint64_t total = c.h_scalars[0], ovf = c.h_scalars[1], err = c.h_scalars[2];
+    if (err & 4) {
+        set_error("row-record kernel: a tile ring wait timed out");
+        return MBRWT_ERR_DEVICE;
+    }
     if (err & 1) {
         set_error("row out of range");
         return MBRWT_ERR_RANGE;

@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--scaled-batch", type=int, default=8_000_000)
     ap.add_argument("--skip-small", action="store_true", help="only the scaled shape")
     ap.add_argument("--shapes", default="greedy+relax,basic arity 8", help="comma-separated subset of the shapes")
+    ap.add_argument("--layout", default="nodes", choices=["nodes", "rows", "both"],
+                    help="device layout (include/mbrwt.h MBRWT_BUILD_LAYOUT)")
     a = ap.parse_args()
     import oracle as O
     from genome_graph_annotation_amd import BRWTDevice
@@ -103,12 +105,12 @@ def main():
         build_s = time.time() - t0
         exp = t.export()
         nc = np.asarray(exp["num_children"])
-        dev = BRWTDevice.from_tree(exp)
+        dev = BRWTDevice.from_tree(exp, layout=a.layout)
         log(f"{shape}: oracle build {build_s:.0f} s, {t.num_nodes()} nodes, depth {t.depth()}, "
             f"avg arity {t.avg_arity():.2f}, max arity {int(nc.max())}; device {dev.device_bytes() / 1e6:.1f} MB, "
             f"kernel {dev.traverse_kernel()}")
         r = measure(dev, rows_np, t.get_rows(rows_np), variants, a.reps)
-        r.update({"nodes": int(t.num_nodes()), "depth": int(t.depth()), "avg_arity": t.avg_arity(),
+        r.update({"layout": dev.layout(), "rows_stats": dev.rows_stats(), "nodes": int(t.num_nodes()), "depth": int(t.depth()), "avg_arity": t.avg_arity(),
                   "max_arity": int(nc.max()), "device_bytes": int(dev.device_bytes()), "oracle_build_s": build_s})
         res[shape] = r
         shapes[shape] = (exp, build_s)
@@ -119,7 +121,7 @@ def main():
             keep = {k: exp[k] for k in ("num_children", "first_child", "leaf_column")}
             nc = np.asarray(keep["num_children"])
             t0 = time.time()
-            dev = BRWTDevice.synthetic_shaped(a.scaled_rows, keep, a.density, 42)
+            dev = BRWTDevice.synthetic_shaped(a.scaled_rows, keep, a.density, 42, layout=a.layout)
             torch.cuda.synchronize()
             gen_s = time.time() - t0
             t0 = time.time()
@@ -128,7 +130,7 @@ def main():
                 f"{dev.device_bytes() / 1e9:.2f} GB (generated in {gen_s:.1f} s), kernel {dev.traverse_kernel()}, "
                 f"streamed oracle {time.time() - t0:.0f} s")
             r = measure(dev, srows, ref, variants, a.reps)
-            r.update({"nodes": len(nc), "max_arity": int(nc.max()), "device_bytes": int(dev.device_bytes()),
+            r.update({"layout": dev.layout(), "rows_stats": dev.rows_stats(), "nodes": len(nc), "max_arity": int(nc.max()), "device_bytes": int(dev.device_bytes()),
                       "generate_s": gen_s, "rows": a.scaled_rows, "batch": a.scaled_batch,
                       "num_relations": int(dev.num_relations())})
             res[f"scaled {shape}"] = r
