@@ -1245,6 +1245,86 @@ void oracle_generate_columns(uint64_t n, uint64_t m, double d, uint32_t seed, ui
     for (uint64_t j = 0; j < m; ++j) g.column(n, d, col_words + j * W);
 }
 
+// experiments/main.cpp:232-264 "uniform_rows": `unique` distinct rows drawn
+// as columns over `unique` rows (generate_random_columns), each repeated
+// n / unique times, the repeated rows shuffled (replicate_shuffle,
+// data_generation.cpp:66-86, std::shuffle with the same engine) -- rows of
+// the result = n_out = unique * (n / unique).  Column-major words like
+// oracle_generate_columns.
+uint64_t oracle_generate_uniform_rows(uint64_t n, uint64_t m, double d, uint64_t unique, uint32_t seed,
+                                      uint64_t *col_words) {
+    if (!unique || unique > n) return 0;
+    DataGenerator g;
+    g.set_seed(seed);
+    const uint64_t Wu = (unique + 63) / 64;
+    std::vector<uint64_t> gen((size_t)Wu * m, 0);
+    for (uint64_t j = 0; j < m; ++j) g.column(unique, d, gen.data() + j * Wu);  // generate_random_columns
+    const uint64_t freq = n / unique, n_out = unique * freq;
+    std::vector<uint64_t> src(n_out);  // replicate: row i repeated freq times, in order
+    for (uint64_t i = 0; i < n_out; ++i) src[i] = i / freq;
+    std::shuffle(src.begin(), src.end(), g.gen);
+    if (col_words) {
+        const uint64_t W = (n_out + 63) / 64;
+        std::memset(col_words, 0, W * m * 8);
+        for (uint64_t j = 0; j < m; ++j)
+            for (uint64_t r = 0; r < n_out; ++r)
+                if ((gen[j * Wu + (src[r] >> 6)] >> (src[r] & 63)) & 1) col_words[j * W + (r >> 6)] |= 1ull << (r & 63);
+    }
+    return n_out;
+}
+
+// experiments/main.cpp:249-264 "uniform_columns": `unique` distinct columns,
+// each repeated m / unique times, the repeated columns shuffled; columns of
+// the result = unique * (m / unique).
+uint64_t oracle_generate_uniform_columns(uint64_t n, uint64_t m, double d, uint64_t unique, uint32_t seed,
+                                         uint64_t *col_words) {
+    if (!unique || unique > m) return 0;
+    DataGenerator g;
+    g.set_seed(seed);
+    const uint64_t W = (n + 63) / 64;
+    std::vector<uint64_t> gen((size_t)W * unique, 0);
+    for (uint64_t j = 0; j < unique; ++j) g.column(n, d, gen.data() + j * W);
+    const uint64_t freq = m / unique, m_out = unique * freq;
+    std::vector<uint64_t> src(m_out);
+    for (uint64_t i = 0; i < m_out; ++i) src[i] = i / freq;
+    std::shuffle(src.begin(), src.end(), g.gen);
+    if (col_words)
+        for (uint64_t j = 0; j < m_out; ++j) std::memcpy(col_words + j * W, gen.data() + src[j] * W, W * 8);
+    return m_out;
+}
+
+// Bytes of every node's index as an sdsl rrr_vector<63> stream
+// (sdsl_format.hpp's layout: size, block classes at 6 bits, the blocks'
+// numbers, number-pointer and rank samples every 32 blocks, invert bits) --
+// the reference's compressed index size (README.md:26-37 reports the files).
+uint64_t oracle_rrr_bytes(OracleTree *t) {
+    if (!t || !t->root) return 0;
+    const auto &T = RRRVec::T();
+    auto words = [](uint64_t bits) { return (bits + 63) / 64 * 8; };
+    auto width = [](uint64_t v) -> uint64_t { return v ? 64 - __builtin_clzll(v) : 64; };
+    uint64_t total = 0;
+    std::vector<const Node *> all{t->root.get()};
+    for (size_t h = 0; h < all.size(); ++h)
+        for (auto &c : all[h]->children) all.push_back(c.get());
+    for (const Node *nd : all) {
+        const BitVec &bv = nd->nonzero_rows;
+        const uint64_t size = bv.size, nb = (size + 63) / 63, ns = (nb + 31) / 32;
+        uint64_t btnr = 0;
+        for (uint64_t b = 0; b < nb; ++b) {
+            const uint64_t p = b * 63;
+            if (p >= size) break;
+            const uint32_t len = (uint32_t)std::min<uint64_t>(63, size - p);
+            uint64_t x = bv.words[p >> 6] >> (p & 63);
+            if ((p & 63) && (p & 63) + len > 64) x |= bv.words[(p >> 6) + 1] << (64 - (p & 63));
+            x &= (1ull << len) - 1;
+            btnr += T.space[__builtin_popcountll(x)];
+        }
+        total += 8 + (9 + words(nb * 6)) + (8 + words(std::max<uint64_t>(btnr, 64))) + (9 + words(ns * width(btnr))) +
+                 (9 + words((ns + 1) * width(bv.ones))) + (8 + words(ns));
+    }
+    return total;
+}
+
 OracleTree *oracle_generate_norepl(uint64_t n, uint64_t m, double d, uint32_t seed, int partitioner,
                                    uint32_t arity, uint64_t relax_max_arity) {
     try {

@@ -38,6 +38,11 @@ OracleTree *oracle_build_from_columns(const uint64_t *col_words, uint64_t num_ro
  * DataGenerator seeded `seed` draws `num_cols` Bernoulli(density) columns
  * column-major from one std::mt19937 (experiments/data_generation.cpp:20-29,
  * :103-110), then builds as oracle_build_from_columns. */
+uint64_t oracle_generate_uniform_rows(uint64_t n, uint64_t m, double d, uint64_t unique, uint32_t seed,
+                                      uint64_t *col_words);
+uint64_t oracle_generate_uniform_columns(uint64_t n, uint64_t m, double d, uint64_t unique, uint32_t seed,
+                                         uint64_t *col_words);
+uint64_t oracle_rrr_bytes(OracleTree *t);
 OracleTree *oracle_generate_norepl(uint64_t num_rows, uint64_t num_cols, double density,
                                    uint32_t seed, int partitioner, uint32_t arity,
                                    uint64_t relax_max_arity);

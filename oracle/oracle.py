@@ -36,6 +36,9 @@ def lib():
     sig = {
         "oracle_build_from_columns": (vp, [u64p, C.c_uint64, C.c_uint64, C.c_int, C.c_uint32, C.c_uint64]),
         "oracle_generate_norepl": (vp, [C.c_uint64, C.c_uint64, C.c_double, C.c_uint32, C.c_int, C.c_uint32, C.c_uint64]),
+        "oracle_generate_uniform_rows": (C.c_uint64, [C.c_uint64, C.c_uint64, C.c_double, C.c_uint64, C.c_uint32, vp]),
+        "oracle_generate_uniform_columns": (C.c_uint64, [C.c_uint64, C.c_uint64, C.c_double, C.c_uint64, C.c_uint32, vp]),
+        "oracle_rrr_bytes": (C.c_uint64, [vp]),
         "oracle_generate_topdown": (vp, [C.c_uint64, C.c_uint64, C.c_double, C.c_uint32, C.c_uint64, C.c_int]),
         "oracle_free": (None, [vp]),
         "oracle_num_rows": (C.c_uint64, [vp]),
@@ -178,6 +181,12 @@ class OracleTree:
         return cls(lib().oracle_build_from_columns(_p64(words), n, m, p, arity, relax))
 
     @classmethod
+    def from_words(cls, words, n, m, partitioner="basic", arity=2, relax=0):
+        """From column-major packed words (generate_columns and friends)."""
+        p = {"basic": 0, "greedy": 1}[partitioner]
+        return cls(lib().oracle_build_from_columns(_p64(words), n, m, p, arity, relax))
+
+    @classmethod
     def norepl(cls, n, m, d, seed=42, partitioner="basic", arity=2, relax=0):
         p = {"basic": 0, "greedy": 1}[partitioner]
         return cls(lib().oracle_generate_norepl(n, m, d, seed, p, arity, relax))
@@ -254,6 +263,10 @@ class OracleTree:
         rows = np.ascontiguousarray(rows, dtype=np.uint64)
         return lib().oracle_time_rows(self._h, _p64(rows), len(rows), threads)
 
+    def rrr_bytes(self):
+        """Bytes of every node's index as an sdsl rrr_vector<63> stream."""
+        return lib().oracle_rrr_bytes(self._h)
+
     def to_rrr(self, threads=0):
         """Re-encode the indexes sdsl-RRR-like (CPU baseline); afterwards
         only get / get_row(s) / time_rows are valid."""
@@ -297,6 +310,26 @@ def generate_random_ints(n, begin, end, seed=42):
     out = np.zeros(max(1, n), dtype=np.uint64)
     lib().oracle_generate_random_ints(n, begin, end, seed, _p64(out))
     return out[:n]
+
+
+def generate_uniform_rows(n, m, d, unique, seed=42):
+    """experiments/main.cpp "uniform_rows": (column-major words, rows)."""
+    rows = (n // unique) * unique
+    W = (rows + 63) // 64
+    out = np.zeros(max(1, W * m), dtype=np.uint64)
+    got = lib().oracle_generate_uniform_rows(n, m, d, unique, seed, out.ctypes.data)
+    assert got == rows
+    return out, rows
+
+
+def generate_uniform_columns(n, m, d, unique, seed=42):
+    """experiments/main.cpp "uniform_columns": (column-major words, columns)."""
+    cols = (m // unique) * unique
+    W = (n + 63) // 64
+    out = np.zeros(max(1, W * cols), dtype=np.uint64)
+    got = lib().oracle_generate_uniform_columns(n, m, d, unique, seed, out.ctypes.data)
+    assert got == cols
+    return out, cols
 
 
 def generate_columns(n, m, d, seed=42):
