@@ -247,9 +247,26 @@ int sharded_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_off
     int rc;
     if ((rc = route(c, d_rows, n, r, s))) return rc;
     const uint32_t K = (uint32_t)c.shards.size();
+    uint64_t total = 0;
+    if (!d_cols || cap == 0) {
+        // a sizing call: count the labels per shard (the V/L pass, no label
+        // is materialised) instead of answering the whole query twice
+        for (uint32_t k = 0; k < K; ++k) {
+            const uint64_t b = r.begin[k], ns = r.begin[k + 1] - b;
+            if (!ns) continue;
+            uint64_t visits = 0, labels = 0;
+            if ((rc = run_count_work(*c.shards[k], r.local + b, ns, &visits, &labels, s))) return rc;
+            total += labels;
+        }
+        if (needed) *needed = total;
+        if (total > 0) {
+            set_error("cols_cap too small");
+            return MBRWT_ERR_CAPACITY;
+        }
+    }
     // each shard answers its rows into its own workspaces (offsets in ws_rows,
     // labels in ws_out; the host-buffer API of a shard context is never used)
-    uint64_t total = 0;
+    total = 0;
     for (uint32_t k = 0; k < K; ++k) {
         const uint64_t b = r.begin[k], ns = r.begin[k + 1] - b;
         if (!ns) continue;
