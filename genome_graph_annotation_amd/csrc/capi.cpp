@@ -71,7 +71,10 @@ static void release(Ctx *c) {
     (void)hipSetDevice(c->device);
     free_tree(c->tree);
     free_rows(c->rows);
-    for (Workspace *w : {&c->ws_temp, &c->ws_counts, &c->ws_ovf, &c->ws_scan, &c->ws_rows, &c->ws_out, &c->ws_sort,
+    if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->sev_a) (void)hipEventDestroy(c->sev_a);
+    if (c->sev_b) (void)hipEventDestroy(c->sev_b);
+    for (Workspace *w : {&c->ws_temp, &c->ws_counts, &c->ws_ovf, &c->ws_scan, &c->ws_scan2, &c->ws_rows, &c->ws_out, &c->ws_sort,
                          &c->ws_cls_off, &c->ws_cls_cols, &c->ws_sh_keys, &c->ws_sh_local, &c->ws_sh_cnt,
                          &c->ws_sh_sort, &c->ws_sh_tmp})
         if (w->buf) (void)hipFree(w->buf);

@@ -325,6 +325,9 @@ struct Ctx {
     // reusable device workspace (grown on demand, never inside a timed call
     // once warmed up)
     Workspace ws_temp, ws_counts, ws_ovf, ws_scan, ws_rows, ws_out, ws_sort;
+    Workspace ws_scan2;                 // row records: the first half's scan (split batches)
+    hipStream_t side = nullptr;         // row records: the first half's compaction (split batches)
+    hipEvent_t sev_a = nullptr, sev_b = nullptr;
     Workspace ws_cls_off, ws_cls_cols;  // get_labels batch: the rows' CSR
     uint64_t *h_scalars = nullptr;      // pinned: [0] total, [1] overflow count, [2] error
     uint64_t *d_scalars = nullptr;      // device twin

@@ -840,6 +840,7 @@ struct RowsParams {
     uint32_t walk4;               // 1: rows_walk4 (default), 2: rows_walk5 (MBRWT_ROWS_WALK=5), 0: rows_walk2 (=2)
     uint32_t stk_words;           // per-lane LDS stack slots of the v2/v3 kernels (rows_stack_words)
     uint32_t stage;               // v2 + walk 6: labels staged in LDS, stored as 16-byte vectors
+    uint64_t row_base;            // batch index of p.rows[0] (the direct list holds batch indices)
     uint32_t diag;                // MBRWT_ROWS_DIAG (timing experiments; WRONG results): 1 no walk,
                                   // 2 walk without label stores, 4 no spill reads
 };
@@ -1000,7 +1001,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
             unsigned long long k0 = 0;
             if (lane == 0) k0 = atomicAdd(&p.scalars[1], (unsigned long long)nr);
             k0 = (unsigned long long)__shfl((long long)k0, 0, 64);
-            if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(r0 + lane));
+            if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(p.row_base + r0 + lane));
         }
         wave_sync();  // the slots and the stage are reused
     }
@@ -1350,7 +1351,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
             unsigned long long k0 = 0;
             if (lane == 0) k0 = atomicAdd(&p.scalars[1], (unsigned long long)nr);
             k0 = (unsigned long long)__shfl((long long)k0, 0, 64);
-            if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(r0 + lane));
+            if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(p.row_base + r0 + lane));
         }
         wave_sync();  // the slots are reused
     }
@@ -1480,7 +1481,7 @@ __global__ __launch_bounds__(64 * (NL + NW)) void k_traverse_rows5(RowsParams p)
                 unsigned long long k0 = 0;
                 if (lane == 0) k0 = atomicAdd(&p.scalars[1], (unsigned long long)nr);
                 k0 = (unsigned long long)__shfl((long long)k0, 0, 64);
-                if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(r0 + lane));
+                if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(p.row_base + r0 + lane));
             }
             // walk word: record offset | pos << 8 | live << 31; header: tile, walk flag
             const bool live = valid && cnt > 0 && !direct && !(p.diag & 1);
@@ -1672,7 +1673,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows3(RowsParams p) {
             unsigned long long k0 = 0;
             if (lane == 0) k0 = atomicAdd(&p.scalars[1], (unsigned long long)nr);
             k0 = (unsigned long long)__shfl((long long)k0, 0, 64);
-            if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(r0 + lane));
+            if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(p.row_base + r0 + lane));
         }
         wave_sync();  // every lane is done with its slot
         if (!more) break;
@@ -1702,16 +1703,23 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows3(RowsParams p) {
 // the last tile; workgroup 0 publishes {total, direct rows, error flags} to
 // res[0..2] and clears the kernel's counters (sc[1], sc[2]) for the next call.
 constexpr uint32_t kCompactTpw = 4;
+// Split batches (rows_get_rows): the tiles [tb, te) of the batch, their scan
+// relative to `*base_to + (*base_tc & mask)` (the previous half's last tile;
+// null: 0); only the call's last compaction (res != null) publishes and
+// clears, an earlier half writes when its own end fits the capacity.
 __global__ __launch_bounds__(256) void k_compact_tiles(const uint8_t *__restrict__ temp, uint32_t C,
                                                        const uint32_t *__restrict__ tile_counts,
                                                        const uint64_t *__restrict__ tile_offsets,
                                                        uint64_t *__restrict__ offsets, uint32_t *__restrict__ cols,
-                                                       uint64_t n, uint64_t cap, unsigned long long *sc,
+                                                       uint64_t n, uint64_t tb, uint64_t te,
+                                                       const uint32_t *base_tc, const uint64_t *base_to,
+                                                       uint64_t cap, unsigned long long *sc,
                                                        unsigned long long *res) {
     const uint64_t ntiles = (n + 63) / 64;
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t total = gld(tile_offsets + ntiles - 1) + (gld(tile_counts + ntiles - 1) & 0x7FFFFFFFu);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint64_t add = base_to ? gld(base_to) + (gld(base_tc) & 0x7FFFFFFFu) : 0;
+    const uint64_t total = add + gld(tile_offsets + te - 1) + (gld(tile_counts + te - 1) & 0x7FFFFFFFu);
+    if (res && blockIdx.x == 0 && threadIdx.x == 0) {
         res[0] = total;
         res[1] = sc[1];
         res[2] = sc[2];
@@ -1719,19 +1727,19 @@ __global__ __launch_bounds__(256) void k_compact_tiles(const uint8_t *__restrict
         sc[2] = 0;
     }
     if (total > cap) return;
-    const uint64_t t0 = (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * kCompactTpw;
-    if (t0 >= ntiles) return;
+    const uint64_t t0 = tb + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * kCompactTpw;
+    if (t0 >= te) return;
     const uint32_t region = 128 + 2 * C;
     uint32_t tc[kCompactTpw], cnt[kCompactTpw], v[kCompactTpw][8];
     uint64_t base[kCompactTpw];
 #pragma unroll
     for (uint32_t k = 0; k < kCompactTpw; ++k) {
         const uint64_t t = t0 + k;
-        const bool in = t < ntiles;
+        const bool in = t < te;
         const uint8_t *treg = temp + (in ? t : 0) * (uint64_t)region;
         const uint64_t r0 = t * 64;
         tc[k] = in ? gld(tile_counts + t) : 0x80000000u;
-        base[k] = in ? gld(tile_offsets + t) : 0;
+        base[k] = in ? add + gld(tile_offsets + t) : 0;
         cnt[k] = (in && r0 + lane < n) ? (uint32_t)gld(reinterpret_cast<const uint16_t *>(treg) + lane) : 0u;
         const uint16_t *lab = reinterpret_cast<const uint16_t *>(treg + 128);
 #pragma unroll
@@ -1740,7 +1748,7 @@ __global__ __launch_bounds__(256) void k_compact_tiles(const uint8_t *__restrict
 #pragma unroll
     for (uint32_t k = 0; k < kCompactTpw; ++k) {
         const uint64_t t = t0 + k;
-        if (t >= ntiles) break;
+        if (t >= te) break;
         const uint64_t r0 = t * 64;
         const uint32_t nr = (uint32_t)(n - r0 < 64 ? n - r0 : 64);
         uint32_t x = cnt[k];
@@ -2109,31 +2117,74 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         c.rb_threads = threads;
         c.rb_blocks = std::max(1, dev_cus) * per_cu;
     }
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((nt + wpb - 1) / wpb, (uint64_t)c.rb_blocks));
+    // Split batches (MBRWT_ROWS_SPLIT=k > 1: batches of >= k tiles): the
+    // batch is traversed in two halves and the first half's scan +
+    // compaction run on a side stream while the second half is traversed.
+    // Measured and left off: at C4 the overlapped compaction slows the
+    // second traversal by as much as it hides (step 0.534 vs 0.537 ms,
+    // profiles/r03/v09_split_c4.log); C2 is slower.
+    const char *split_e = std::getenv("MBRWT_ROWS_SPLIT");
+    const uint64_t split_min = split_e ? (uint64_t)std::strtoull(split_e, nullptr, 10) : 0;
+    const bool split = split_min > 1 && nt >= split_min;
+    const uint64_t nt0 = split ? nt / 2 : nt;
+    auto launch = [&](uint64_t tb, uint64_t te) -> int {
+        RowsParams q = p;
+        q.rows = d_rows + tb * 64;
+        q.n = std::min<uint64_t>(n, te * 64) - tb * 64;
+        q.temp = p.temp + tb * region;
+        q.tile_counts = d_tc + tb;
+        q.row_base = tb * 64;
+        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((te - tb + wpb - 1) / wpb, (uint64_t)c.rb_blocks));
+        hipLaunchKernelGGL(kfn, dim3((unsigned)g), dim3(threads), lds, s, q);
+        MBRWT_HIP(hipGetLastError());
+        return MBRWT_OK;
+    };
+    auto compact = [&](uint64_t tb, uint64_t te, bool last, hipStream_t st) -> int {
+        const uint64_t waves = (te - tb + kCompactTpw - 1) / kCompactTpw;
+        hipLaunchKernelGGL(k_compact_tiles, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, p.temp, C, d_tc, d_to,
+                           d_offsets, d_cols, n, tb, te, tb ? d_tc + tb - 1 : (const uint32_t *)nullptr,
+                           tb ? d_to + tb - 1 : (const uint64_t *)nullptr, cap, d_sc,
+                           last ? reinterpret_cast<unsigned long long *>(c.d_scalars) : (unsigned long long *)nullptr);
+        MBRWT_HIP(hipGetLastError());
+        return MBRWT_OK;
+    };
+    if (split && !c.side) {
+        MBRWT_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+        MBRWT_HIP(hipEventCreateWithFlags(&c.sev_a, hipEventDisableTiming));
+        MBRWT_HIP(hipEventCreateWithFlags(&c.sev_b, hipEventDisableTiming));
+    }
+    if (split && (rc = ensure(c.ws_scan2, scan_bytes))) return rc;
 
     c.rows_sc_dirty = true;  // until k_compact_tiles has run
     hipEvent_t e0 = c.ev0, e1 = c.ev1;
     if (c.timing && d_status) {  // asynchronous calls: one event pair per call, summed by mbrwt_take_timing
         if (c.async_ev.size() <= c.async_used) {
-            hipEvent_t a = nullptr, b = nullptr;
-            MBRWT_HIP(hipEventCreate(&a));
-            MBRWT_HIP(hipEventCreate(&b));
-            c.async_ev.push_back({a, b});
+            hipEvent_t ea = nullptr, eb = nullptr;
+            MBRWT_HIP(hipEventCreate(&ea));
+            MBRWT_HIP(hipEventCreate(&eb));
+            c.async_ev.push_back({ea, eb});
         }
         e0 = c.async_ev[c.async_used].first;
         e1 = c.async_ev[c.async_used].second;
         ++c.async_used;
     }
     if (c.timing) MBRWT_HIP(hipEventRecord(e0, s));
-    hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(threads), lds, s, p);
-    MBRWT_HIP(hipGetLastError());
-    if (c.timing) MBRWT_HIP(hipEventRecord(e1, s));
-    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_to, nt, s));
-    {
-        const uint64_t waves = (nt + kCompactTpw - 1) / kCompactTpw;
-        hipLaunchKernelGGL(k_compact_tiles, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, p.temp, C, d_tc, d_to,
-                           d_offsets, d_cols, n, cap, d_sc, reinterpret_cast<unsigned long long *>(c.d_scalars));
-        MBRWT_HIP(hipGetLastError());
+    if ((rc = launch(0, nt0))) return rc;
+    if (!split) {
+        if (c.timing) MBRWT_HIP(hipEventRecord(e1, s));
+        MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_to, nt, s));
+        if ((rc = compact(0, nt, true, s))) return rc;
+    } else {
+        MBRWT_HIP(hipEventRecord(c.sev_a, s));
+        if ((rc = launch(nt0, nt))) return rc;
+        if (c.timing) MBRWT_HIP(hipEventRecord(e1, s));
+        MBRWT_HIP(hipStreamWaitEvent(c.side, c.sev_a, 0));
+        MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan2.buf, scan_bytes, it, d_to, nt0, c.side));
+        if ((rc = compact(0, nt0, false, c.side))) return rc;
+        MBRWT_HIP(hipEventRecord(c.sev_b, c.side));
+        MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it + nt0, d_to + nt0, nt - nt0, s));
+        MBRWT_HIP(hipStreamWaitEvent(s, c.sev_b, 0));
+        if ((rc = compact(nt0, nt, true, s))) return rc;
     }
     c.rows_sc_dirty = false;
     if (d_status) {

@@ -50,6 +50,7 @@ def set_variant(kv):
     os.environ.pop("MBRWT_ROWS_WALK", None)
     os.environ.pop("MBRWT_ROWS_WGS_PER_CU", None)
     os.environ.pop("MBRWT_ROWS_STAGE", None)
+    os.environ.pop("MBRWT_ROWS_SPLIT", None)
     for part in kv.split("."):  # e.g. "w2.v2.diag1"
         if part.startswith("w"):  # w2: the v2 walk
             os.environ["MBRWT_ROWS_WALK"] = part[1:]
@@ -57,6 +58,8 @@ def set_variant(kv):
             os.environ["MBRWT_ROWS_KERNEL"] = part[1]
         elif part.startswith("occ"):  # occN: at most N workgroups per CU
             os.environ["MBRWT_ROWS_WGS_PER_CU"] = part[3:]
+        elif part == "nosplit":
+            os.environ["MBRWT_ROWS_SPLIT"] = "0"
         elif part == "stage":
             os.environ["MBRWT_ROWS_STAGE"] = "1"
         elif part == "async":
