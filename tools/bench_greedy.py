@@ -47,6 +47,12 @@ def measure(dev, rows_np, ref, variants, reps):
         torch.cuda.synchronize()
         exact = (nl == len(cols_o) and np.array_equal(off_t.cpu().numpy().view(np.uint64), off_o)
                  and np.array_equal(cols_t[:nl].cpu().numpy().view(np.uint32), cols_o))
+        # warm-up of >= 0.2 s: the oracle ran on the host for seconds before,
+        # and an idle GPU's first milliseconds of work run at idle clocks
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.2:
+            dev.get_rows_device(rows_t, off_t, cols_t, s)
+        torch.cuda.synchronize()
         dev.take_timing()
         dev.set_option(L.MBRWT_OPT_TIMING, 1)
         torch.cuda.synchronize()

@@ -28,6 +28,8 @@ ap.add_argument("--steps", type=int, default=10)
 ap.add_argument("--seed", type=int, default=42)
 ap.add_argument("--shape", default="", help="npz with num_children/first_child/leaf_column: synthetic_shaped")
 ap.add_argument("--configs", default="nodes,rows")
+ap.add_argument("--oracle", action="store_true",
+                help="check the first configuration's CSR against the streamed top-down oracle (whole batch)")
 a = ap.parse_args()
 
 rows_np = np.random.default_rng(a.seed).integers(0, a.rows, a.batch, dtype=np.uint64)
@@ -100,6 +102,22 @@ for cfg in a.configs.split(";") if ";" in a.configs else a.configs.split(","):
         hx = h.hexdigest()
         if ref is None:
             ref = hx
+            if a.oracle:
+                sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+                import oracle as O  # checker only
+                t2 = time.time()
+                if shape is not None:
+                    off_o, cols_o = O.topdown_get_rows_shaped(a.rows, shape, a.density, a.seed, rows_np)
+                else:
+                    off_o, cols_o = O.topdown_get_rows(a.rows, a.cols, a.density, a.arity, a.seed, rows_np)
+                exact = (np.array_equal(off.cpu().numpy().view(np.uint64), off_o)
+                         and np.array_equal(cols[:nl].cpu().numpy().view(np.uint32), cols_o))
+                print(json.dumps({"oracle": "streamed top-down", "rows_checked": a.batch,
+                                  "labels_checked": int(len(cols_o)), "bit_exact": bool(exact),
+                                  "oracle_s": round(time.time() - t2, 1)}), flush=True)
+                if not exact:
+                    print("MISMATCH vs oracle", flush=True)
+                    sys.exit(1)
         m.take_timing()
         m.set_option(L.MBRWT_OPT_TIMING, 1)
         torch.cuda.synchronize()
