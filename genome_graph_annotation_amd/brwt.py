@@ -288,7 +288,10 @@ class BRWTDevice:
             return None
         keys = ("block_bytes", "rows_per_block", "blocks_bytes", "spill_bytes", "record_bytes", "spilled_rows",
                 "long_rows", "height")
-        return dict(zip(keys, [int(v) for v in out]))
+        d = dict(zip(keys, [int(v) for v in out]))
+        d["uniform_levels"] = d["height"] >> 32  # odometer walk when > 0
+        d["height"] &= 0xFFFFFFFF
+        return d
 
     # -- host-buffer queries --------------------------------------------------
     def get_rows(self, rows):

@@ -465,7 +465,7 @@ int mbrwt_rows_stats(const mbrwt_ctx *ctx, uint64_t out[8]) {
     out[4] = r.record_bytes;
     out[5] = r.spilled_rows;
     out[6] = r.long_rows;
-    out[7] = r.height;
+    out[7] = r.height | (uint64_t)r.uni << 32;
     return MBRWT_OK;
 }
 int mbrwt_device(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->device : -1; }

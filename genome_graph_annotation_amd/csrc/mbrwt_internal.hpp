@@ -261,6 +261,7 @@ struct RowsImage {
     uint32_t *d_table2 = nullptr;
     uint32_t frames = 0;            // its stack levels
     bool mask1 = false;             // every internal node (leaf parents too) has arity <= 8: one-byte masks
+    uint32_t uni = 0;               // K internal levels above leaf parents on every path (rows_walk_uni), else 0
     uint64_t bytes = 0;             // blocks + spill used
     // build statistics
     uint64_t spilled_rows = 0, long_rows = 0, record_bytes = 0, spill_bytes = 0;
@@ -269,6 +270,7 @@ struct RowsImage {
 // shape is outside the row-record kernels' limits
 bool build_rwt_table(const Tree &tree, std::vector<uint32_t> &table, uint32_t &height);
 bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &table2, uint32_t &frames);
+uint32_t rwt2_uniform_levels(const std::vector<uint32_t> &table2);
 // the thread's build layout (mbrwt_set_build_option, else MBRWT_LAYOUT)
 int build_layout();
 void set_build_layout(int layout);

@@ -1073,7 +1073,7 @@ __device__ __forceinline__ void wave_sync_lds() {
 // next round's item, or the root block of the next rowblock's row) is
 // requested before the current one is processed, so its latency overlaps the
 // current record walk.  OCC: the waves per SIMD the register budget targets.
-template <bool NT, bool PF, int OCC>
+template <bool NT, bool PF, int OCC, typename LT = uint32_t>
 __global__ __launch_bounds__(256, OCC) void k_traverse_p2w(P2wParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_p2w[];
     const uint32_t lane = threadIdx.x & 63, c = lane & 3, g = lane >> 2, gb = lane & ~3u;
@@ -1136,7 +1136,9 @@ __global__ __launch_bounds__(256, OCC) void k_traverse_p2w(P2wParams p) {
     for (; rb < nblocks; rb += wstride) {
         const uint64_t r0 = rb * 16;
         const uint32_t nr = (uint32_t)(p.n - r0 < 16 ? p.n - r0 : 16);
-        uint32_t *const out = p.temp + rb * (uint64_t)p.C;
+        // LT: the temp region's label type (u16 when every label is < 2^16:
+        // half the traversal's writes and the compaction's reads)
+        LT *const out = reinterpret_cast<LT *>(p.temp) + rb * (uint64_t)p.C;
 
         // ---- root phase: the super-root's block at group g's row ----
         uint32_t row;
@@ -1248,7 +1250,7 @@ __global__ __launch_bounds__(256, OCC) void k_traverse_p2w(P2wParams p) {
             const bool direct = rtot + (running - flushed) > p.S;
             if (direct) {
                 for (uint32_t q2 = flushed + lane; q2 < running; q2 += 64)
-                    if (q2 < p.C) gst(out + q2, (uint32_t)ring[q2 & smask]);
+                    if (q2 < p.C) gst(out + q2, (LT)ring[q2 & smask]);
                 wave_sync_lds();
             }
             // part 2: the labels, in the record's (pre-)order
@@ -1264,7 +1266,7 @@ __global__ __launch_bounds__(256, OCC) void k_traverse_p2w(P2wParams p) {
                     for (uint32_t lm = pb[o++]; lm; lm &= lm - 1, ++pos) {
                         const uint32_t label = l + (uint32_t)__builtin_ctz(lm);
                         if (!direct) ring[pos & smask] = label;
-                        else if (pos < p.C) gst(out + pos, label);
+                        else if (pos < p.C) gst(out + pos, (LT)label);
                     }
                 }
             }
@@ -1276,7 +1278,7 @@ __global__ __launch_bounds__(256, OCC) void k_traverse_p2w(P2wParams p) {
                 if (F > flushed) {
                     wave_sync_lds();
                     for (uint32_t q2 = flushed + lane; q2 < F; q2 += 64)
-                        if (q2 < p.C) gst(out + q2, (uint32_t)ring[q2 & smask]);
+                        if (q2 < p.C) gst(out + q2, (LT)ring[q2 & smask]);
                     flushed = F;
                 }
             }
@@ -1285,7 +1287,7 @@ __global__ __launch_bounds__(256, OCC) void k_traverse_p2w(P2wParams p) {
         if (lane == 0) ipos[T] = running;
         wave_sync_lds();
         for (uint32_t q2 = flushed + lane; q2 < running; q2 += 64)
-            if (q2 < p.C) gst(out + q2, (uint32_t)ring[q2 & smask]);
+            if (q2 < p.C) gst(out + q2, (LT)ring[q2 & smask]);
         if (c == 0 && g < nr) gst(p.counts + r0 + g, (uint32_t)(ipos[gfirst[g + 1]] - ipos[gfirst[g]]));
         if (lane == 0) gst(p.block_counts + rb, running);
         if (running > p.C) {  // rowblock overflow: its rows go to the direct pass
@@ -1329,11 +1331,11 @@ struct PtwLayout {
 
 // the labels of a KIND_PACKT record (masks from byte o on) into the ring
 // (or, `direct`, the rowblock's temp region) from label position pos on
-template <int MAXD>
+template <int MAXD, typename LT>
 __device__ __forceinline__ void ptw_walk(const AS_LDS uint8_t *pb, uint32_t o, uint32_t node,
                                          const AS_LDS uint32_t *ntab, const AS_LDS uint16_t *etab,
                                          AS_LDS uint32_t *ring, uint32_t smask, uint32_t pos, bool direct,
-                                         uint32_t *out, uint32_t C, bool &overflow) {
+                                         LT *out, uint32_t C, bool &overflow) {
     uint32_t nw = ntab[node];
     uint32_t m = pb[o++];
     if ((nw >> 24) > 8) m |= (uint32_t)pb[o++] << 8;
@@ -1357,7 +1359,7 @@ __device__ __forceinline__ void ptw_walk(const AS_LDS uint8_t *pb, uint32_t o, u
         if (e & 0x8000u) {
             const uint32_t label = e & 0x7FFFu;
             if (!direct) ring[pos & smask] = label;
-            else if (pos < C) gst(out + pos, label);
+            else if (pos < C) gst(out + pos, (LT)label);
             ++pos;
             continue;
         }
@@ -1429,7 +1431,7 @@ __device__ __forceinline__ void ptw_walk_wave(const AS_LDS uint8_t *pb, uint32_t
     }
 }
 
-template <bool NT, bool WIDE, int MAXD, int WPB, uint32_t RING = 512>
+template <bool NT, bool WIDE, int MAXD, int WPB, uint32_t RING = 512, typename LT = uint32_t>
 __global__ __launch_bounds__(64 * WPB) void k_traverse_ptw(P2wParams p) {
     using Lay = PtwLayout<WIDE, RING>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_ptw[];
@@ -1460,7 +1462,9 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_ptw(P2wParams p) {
     for (uint64_t rb = (uint64_t)blockIdx.x * WPB + wv; rb < nblocks; rb += wstride) {
         const uint64_t r0 = rb * 16;
         const uint32_t nr = (uint32_t)(p.n - r0 < 16 ? p.n - r0 : 16);
-        uint32_t *const out = p.temp + rb * (uint64_t)p.C;
+        // LT: the temp region's label type (u16 when every label is < 2^16:
+        // half the traversal's writes and the compaction's reads)
+        LT *const out = reinterpret_cast<LT *>(p.temp) + rb * (uint64_t)p.C;
 
         // ---- root phase: the super-root's block at group g's row ----
         uint32_t row = kNone;
@@ -1587,16 +1591,16 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_ptw(P2wParams p) {
             const bool direct = rtot + (running - flushed) > Lay::kRing;
             if (direct) {
                 for (uint32_t q2 = flushed + lane; q2 < running; q2 += 64)
-                    if (q2 < p.C) gst(out + q2, (uint32_t)ring[q2 & smask]);
+                    if (q2 < p.C) gst(out + q2, (LT)ring[q2 & smask]);
                 wave_sync_lds();
             }
             if (!direct) {
                 ptw_walk_wave<MAXD>(pb, s + 1, ent, blk, ntab, etab, ring, smask, ibase, overflow);
                 if (act && !blk) ring[ibase & smask] = ent & 0x7FFFFFFFu;
             } else if (blk) {
-                ptw_walk<MAXD>(pb, s + 1, ent, ntab, etab, ring, smask, ibase, direct, out, p.C, overflow);
+                ptw_walk<MAXD, LT>(pb, s + 1, ent, ntab, etab, ring, smask, ibase, direct, out, p.C, overflow);
             } else if (act && ibase < p.C) {
-                gst(out + ibase, ent & 0x7FFFFFFFu);
+                gst(out + ibase, (LT)(ent & 0x7FFFFFFFu));
             }
             running += rtot;
             if (direct) {
@@ -1606,14 +1610,14 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_ptw(P2wParams p) {
                 if (F > flushed) {
                     wave_sync_lds();
                     for (uint32_t q2 = flushed + lane; q2 < F; q2 += 64)
-                        if (q2 < p.C) gst(out + q2, (uint32_t)ring[q2 & smask]);
+                        if (q2 < p.C) gst(out + q2, (LT)ring[q2 & smask]);
                     flushed = F;
                 }
             }
             wave_sync_lds();  // the slots and the ring are reused
         }
         for (uint32_t q2 = flushed + lane; q2 < running; q2 += 64)
-            if (q2 < p.C) gst(out + q2, (uint32_t)ring[q2 & smask]);
+            if (q2 < p.C) gst(out + q2, (LT)ring[q2 & smask]);
         if (lane < nr) gst(p.counts + r0 + lane, rowcnt[lane]);
         if (lane == 0) gst(p.block_counts + rb, running);
         if (running > p.C) {  // rowblock overflow: its rows go to the direct pass
@@ -1632,10 +1636,10 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_ptw(P2wParams p) {
 // prefix) and a contiguous copy of the block's labels, each lane's (up to 8)
 // label reads issued before its stores.  Overflowing blocks (> C labels) are
 // left to the direct pass.
-template <bool BIG>
+template <bool BIG, typename LT = uint32_t>
 __global__ __launch_bounds__(256) void k_compact_blocks(const uint32_t *__restrict__ counts,
                                                         const uint64_t *__restrict__ block_offsets,
-                                                        const uint32_t *__restrict__ temp, uint32_t C,
+                                                        const LT *__restrict__ temp, uint32_t C,
                                                         uint64_t *__restrict__ offsets, uint32_t *__restrict__ cols,
                                                         uint64_t n, const uint32_t *__restrict__ label_map,
                                                         uint32_t map_lds, uint64_t cap) {
@@ -1655,10 +1659,10 @@ __global__ __launch_bounds__(256) void k_compact_blocks(const uint32_t *__restri
         // (when the temp region holds C >= 128 words; always at the default
         // slot sizes): the label reads overlap the offset reads instead of
         // waiting behind them
-        const uint32_t *src = temp + b * (uint64_t)C;
+        const LT *src = temp + b * (uint64_t)C;
         uint32_t v0[8];
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) v0[k] = C >= 128 ? gld(src + sub + 16 * k) : 0u;
+        for (uint32_t k = 0; k < 8; ++k) v0[k] = C >= 128 ? (uint32_t)gld(src + sub + 16 * k) : 0u;
         uint32_t x = mine;
 #pragma unroll
         for (uint32_t d = 1; d < 16; d <<= 1) {
@@ -1672,7 +1676,7 @@ __global__ __launch_bounds__(256) void k_compact_blocks(const uint32_t *__restri
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) {  // the first 128 labels
             const uint32_t i = sub + 16 * k;
-            if (i < total) gst(cols + base + i, lmap(C < 128 ? gld(src + i) : v0[k]));
+            if (i < total) gst(cols + base + i, lmap(C < 128 ? (uint32_t)gld(src + i) : v0[k]));
         }
         // the rest, U labels per lane and round, every lane's reads issued
         // before its stores: U = 32 for large rows (BIG: e.g. 120 labels per
@@ -1684,7 +1688,7 @@ __global__ __launch_bounds__(256) void k_compact_blocks(const uint32_t *__restri
 #pragma unroll
             for (uint32_t k = 0; k < U; ++k) {
                 const uint32_t i = i0 + sub + 16 * k;
-                v[k] = i < total ? gld(src + i) : 0u;
+                v[k] = i < total ? (uint32_t)gld(src + i) : 0u;
             }
 #pragma unroll
             for (uint32_t k = 0; k < U; ++k) {
@@ -2093,9 +2097,15 @@ static P2wFn p2w_kernel(const Ctx &c) {
     case 21: return k_traverse_p2w<true, true, 8>;
     case 22: return k_traverse_p2w<true, true, 6>;
     case 23: return k_traverse_p2w<true, false, 7>;
-    default: return big ? k_traverse_p2w<true, false, 8> : k_traverse_p2w<false, false, 8>;  // (PF: +1 %, 21)
+    default:  // (PF: +1 %, 21); u16 temp labels when they fit (p2w_label16)
+        if (c.tree.num_columns <= 0x10000u)
+            return big ? k_traverse_p2w<true, false, 8, uint16_t> : k_traverse_p2w<false, false, 8, uint16_t>;
+        return big ? k_traverse_p2w<true, false, 8> : k_traverse_p2w<false, false, 8>;
     }
 }
+
+// the default p2w kernel stores u16 temp labels (label indices < num_columns)
+static bool p2w_label16(const Ctx &c) { return c.kernel_variant == 0 && c.tree.num_columns <= 0x10000u; }
 
 static uint32_t p2w_ring(const Ctx &c) {
     (void)c;
@@ -2116,12 +2126,13 @@ struct PtwPick {
     uint32_t wpb = 4;
     uint32_t ring = 512;
     bool wide = false;
+    bool label16 = false;  // u16 temp labels (the default 7-wave kernel; PTW columns are < 2^15)
 };
 template <bool NT, bool WIDE, int MAXD>
 static P2wFn ptw_fn(uint32_t wpb) {
     return wpb == 16  ? k_traverse_ptw<NT, WIDE, MAXD, 16>
            : wpb == 8 ? k_traverse_ptw<NT, WIDE, MAXD, 8>
-           : wpb == 7 ? k_traverse_ptw<NT, WIDE, MAXD, 7, 256>
+           : wpb == 7 ? k_traverse_ptw<NT, WIDE, MAXD, 7, 256, uint16_t>
                       : k_traverse_ptw<NT, WIDE, MAXD, 4>;
 }
 static PtwPick ptw_kernel(const Ctx &c) {
@@ -2132,6 +2143,7 @@ static PtwPick ptw_kernel(const Ctx &c) {
     const bool nt = kv == 0 || kv == 30 ? c.tree.image_bytes > (1ull << 30) : (kv & 1) != 0;
     r.wpb = (kv == 0 || kv == 30) ? 7 : kv >= 28 ? 16 : kv >= 26 ? 8 : 4;  // default: 7 waves, 256-label ring
     r.ring = r.wpb == 7 ? 256 : 512;
+    r.label16 = r.wpb == 7;
     r.wide = t[0] > 8;
     const bool deep = t[3] > 4;
 #define PTW(NTV, W, D) if (nt == NTV && r.wide == W && deep == D) r.fn = ptw_fn<NTV, W, D ? 8 : 4>(r.wpb);
@@ -2161,6 +2173,7 @@ struct RowblockKernel {
     size_t lds;
     uint32_t wpb;
     bool final_columns;  // the kernel emits global columns (k_traverse_ptw): no label map afterwards
+    bool label16;        // u16 temp labels
 };
 static int run_get_rows_p2w(Ctx &c, const RowblockKernel &kr, const uint64_t *d_rows, uint64_t n,
                             uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap, uint64_t *needed, hipStream_t s) {
@@ -2176,7 +2189,7 @@ static int run_get_rows_p2w(Ctx &c, const RowblockKernel &kr, const uint64_t *d_
     const uint64_t nb = (n + 15) / 16;
     // counts: n row counts | nb+1 block counts | (8-byte aligned) nb+1 block offsets
     const uint64_t bc_off = n, bo_off = ((bc_off + nb + 1) * sizeof(uint32_t) + 7) / 8 * 8;
-    if ((rc = ensure(c.ws_temp, nb * (uint64_t)C * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c.ws_temp, nb * (uint64_t)C * (kr.label16 ? 2u : 4u)))) return rc;
     if ((rc = ensure(c.ws_counts, bo_off + (nb + 1) * sizeof(uint64_t)))) return rc;
     if ((rc = ensure(c.ws_ovf, n * sizeof(uint32_t)))) return rc;
     uint32_t *d_counts = reinterpret_cast<uint32_t *>(c.ws_counts.buf);
@@ -2239,10 +2252,15 @@ static int run_get_rows_p2w(Ctx &c, const RowblockKernel &kr, const uint64_t *d_
     // latencies each
     const uint64_t g = std::min<uint64_t>((nb + 15) / 16, 1u << 20);
     const bool big = c.tree.num_rows && (double)c.tree.num_relations > 32.0 * (double)c.tree.num_rows;
-    hipLaunchKernelGGL(big ? k_compact_blocks<true> : k_compact_blocks<false>, dim3((unsigned)g), dim3(256), map_lds * 4,
-                       s, d_counts, d_block_offsets, p.temp,
-                       C, d_offsets, d_cols, n, kr.final_columns ? nullptr : (const uint32_t *)c.d_label_map, map_lds,
-                       cap);
+    const uint32_t *lm = kr.final_columns ? nullptr : (const uint32_t *)c.d_label_map;
+    if (kr.label16) {
+        auto *cfn = big ? k_compact_blocks<true, uint16_t> : k_compact_blocks<false, uint16_t>;
+        hipLaunchKernelGGL(cfn, dim3((unsigned)g), dim3(256), map_lds * 4, s, d_counts, d_block_offsets,
+                           reinterpret_cast<const uint16_t *>(p.temp), C, d_offsets, d_cols, n, lm, map_lds, cap);
+    } else
+        hipLaunchKernelGGL(big ? k_compact_blocks<true> : k_compact_blocks<false>, dim3((unsigned)g), dim3(256),
+                           map_lds * 4, s, d_counts, d_block_offsets, (const uint32_t *)p.temp, C, d_offsets, d_cols, n,
+                           lm, map_lds, cap);
     MBRWT_HIP(hipGetLastError());
     MBRWT_HIP(hipMemcpyAsync(c.d_scalars, d_block_offsets + nb, sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
     MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
@@ -2308,11 +2326,12 @@ int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
         const size_t per_wave = pk.ring == 256 ? (pk.wide ? PtwLayout<true, 256>::kWords : PtwLayout<false, 256>::kWords)
                                                : (pk.wide ? PtwLayout<true>::kWords : PtwLayout<false>::kWords);
         const RowblockKernel kr{pk.fn, c.d_ptw, (uint32_t)words, ((words + 3) & ~size_t(3)) * 4 + pk.wpb * per_wave * 4,
-                                pk.wpb, true};
+                                pk.wpb, true, pk.label16};
         return run_get_rows_p2w(c, kr, d_rows, n, d_offsets, d_cols, cap, needed, s);
     }
     if (const P2wFn kfn = p2w_kernel(c)) {
-        const RowblockKernel kr{kfn, c.d_p2w, (uint32_t)c.tree.p2w_table.size(), p2w_lds_bytes(c), 4, false};
+        const RowblockKernel kr{kfn, c.d_p2w, (uint32_t)c.tree.p2w_table.size(), p2w_lds_bytes(c), 4, false,
+                                p2w_label16(c)};
         return run_get_rows_p2w(c, kr, d_rows, n, d_offsets, d_cols, cap, needed, s);
     }
     const uint32_t K = auto_slots(c);

@@ -204,6 +204,29 @@ bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &t2, uint32_t &fra
     return true;
 }
 
+// K when every root-to-leaf path of the RWT2 table crosses exactly K internal
+// entries (the root included) and then a leaf parent (rows_walk_uni), else 0
+uint32_t rwt2_uniform_levels(const std::vector<uint32_t> &t2) {
+    if (t2.size() < 4 || (t2[0] >> 30) != 0u) return 0;  // the root is a leaf parent (or a leaf)
+    const uint32_t K = t2[2];
+    if (K < 1 || K > 5) return 0;
+    std::vector<uint32_t> lev{t2[0]};
+    for (uint32_t d = 1; d <= K; ++d) {
+        std::vector<uint32_t> next;
+        for (const uint32_t w : lev) {
+            const uint32_t a = (w >> 16) & 0x1Fu, f = w & 0xFFFFu;
+            for (uint32_t c = 0; c < a; ++c) {
+                if (4 + (size_t)f + c >= t2.size()) return 0;
+                const uint32_t e = t2[4 + f + c];
+                if ((e >> 30) != (d == K ? 3u : 0u)) return 0;  // leaf parents exactly at depth K + 1
+                if (d < K) next.push_back(e);
+            }
+        }
+        lev.swap(next);
+    }
+    return K;
+}
+
 namespace {
 
 // ------------------------------------------------------------------------
@@ -611,6 +634,7 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         auto ar8 = [](uint32_t e) { return (e >> 30) == 2u || ((e >> 16) & 0x1Fu) <= 8; };
         im.mask1 = ar8(im.table2[0]);
         for (size_t i = 4; i < im.table2.size(); ++i) im.mask1 = im.mask1 && ar8(im.table2[i]);
+        im.uni = im.mask1 ? rwt2_uniform_levels(im.table2) : 0u;
     }
     if (nr > rb.sz_cap) {
         if (rb.d_sz) MBRWT_HIP(hipFree(rb.d_sz));
@@ -839,6 +863,7 @@ struct RowsParams {
     unsigned long long *scalars;  // [1] direct rows, [2] error flags
     uint32_t walk4;               // 1: rows_walk4 (default), 2: rows_walk5 (MBRWT_ROWS_WALK=5), 0: rows_walk2 (=2)
     uint32_t stk_words;           // per-lane LDS stack slots of the v2/v3 kernels (rows_stack_words)
+    uint32_t uni;                 // walk 4 (rows_walk_uni): the tree's internal levels K (1..5)
     uint32_t stage;               // v2 + walk 6: labels staged in LDS, stored as 16-byte vectors
     uint64_t row_base;            // batch index of p.rows[0] (the direct list holds batch indices)
     uint32_t diag;                // MBRWT_ROWS_DIAG (timing experiments; WRONG results): 1 no walk,
@@ -1186,6 +1211,62 @@ __device__ __forceinline__ void rows_walk6(const AS_LDS uint8_t *pb, uint32_t o,
     }
 }
 
+// v7 walk ("odometer", the default for uniform trees: every root-to-leaf path
+// crosses K internal levels and then a leaf parent with consecutive columns,
+// one-byte masks -- the basic partitioner's trees without singleton groups,
+// i.e. C2-C4).  rows_walk6 spends one lock-step iteration per reached node
+// (19.3 per C4 row, 34 per 64-row tile in lock step); here one iteration
+// reaches the NEXT LEAF PARENT of the row in pre-order (7.9 per C4 row, 15
+// per tile): the remaining-children masks r[0..K-1] of the current path form
+// an odometer -- level k takes its next child when every level below it is
+// exhausted (top-down, so a level refilled in this iteration feeds the level
+// under it), reading that child's mask as the record's next byte, which is
+// exactly BRWT::get_row's pre-order (BRWT.cpp:43-51); the leaf-parent step
+// then reads the leaf mask and stores base + bit for its set bits.  No stack,
+// no per-lane frame state beyond 2K registers.
+template <int K, typename OUT>
+__device__ __forceinline__ void rows_walk_uni(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
+                                              const AS_LDS uint32_t *ent, OUT out, uint32_t pos) {
+    const AS_LDS uint8_t *rc = pb + o;  // record cursor
+    uint32_t r[K], f[K];
+    f[0] = root & 0xFFFFu;
+    r[0] = live ? (uint32_t)rc[0] : 0u;
+    ++rc;
+#pragma unroll
+    for (int k = 1; k < K; ++k) r[k] = f[k] = 0u;
+    uint32_t ob = pos * 2u;  // byte offset of the next label
+    while (true) {
+        uint32_t any = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) any |= r[k];
+        if (!any) break;
+        bool nd[K];  // nd[k]: levels k..K-1 are exhausted
+        nd[K - 1] = r[K - 1] == 0u;
+#pragma unroll
+        for (int k = K - 2; k >= 1; --k) nd[k] = nd[k + 1] && r[k] == 0u;
+#pragma unroll
+        for (int k = 1; k < K; ++k) {
+            if (nd[k]) {
+                const uint32_t c = (uint32_t)__builtin_ctz(r[k - 1]);
+                r[k - 1] &= r[k - 1] - 1u;
+                f[k] = ent[f[k - 1] + c] & 0xFFFFu;
+                r[k] = *rc;
+                ++rc;
+            }
+        }
+        const uint32_t c = (uint32_t)__builtin_ctz(r[K - 1]);
+        r[K - 1] &= r[K - 1] - 1u;
+        const uint32_t base = ent[f[K - 1] + c] & 0xFFFFu;  // a leaf parent: its first column
+        uint32_t x = *rc;
+        ++rc;
+        do {
+            *(OUT)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));
+            ob += 2u;
+            x &= x - 1u;
+        } while (x);
+    }
+}
+
 // v5 walk: rows_walk4 without divergent branches around the stack -- the
 // push writes the next free slot unconditionally and the pop reads the top
 // slot unconditionally (selects keep what applies), so a step costs vector
@@ -1333,6 +1414,16 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
                 for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
                     gst(reinterpret_cast<u32x4_t *>(treg + 128 + q2),
                         *(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2));
+            } else if (p.walk4 == 4) {
+                AS_GLOBAL uint16_t *out = (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128);
+                const bool live = valid && cnt > 0;
+                switch (p.uni) {
+                    case 1: rows_walk_uni<1>(mine, o, live, root, ent, out, pos); break;
+                    case 2: rows_walk_uni<2>(mine, o, live, root, ent, out, pos); break;
+                    case 3: rows_walk_uni<3>(mine, o, live, root, ent, out, pos); break;
+                    case 4: rows_walk_uni<4>(mine, o, live, root, ent, out, pos); break;
+                    default: rows_walk_uni<5>(mine, o, live, root, ent, out, pos); break;
+                }
             } else if (p.walk4 == 3)
                 rows_walk6(mine, o, valid && cnt > 0, root, ent, stk,
                            (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128), pos);
@@ -2077,9 +2168,12 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         p.walk4 = (e && e[0] == '2')   ? 0u
                   : (e && e[0] == '5') ? 2u
                   : (e && e[0] == '4') ? 1u
+                  : (e && e[0] == '6') ? (im.mask1 ? 3u : 1u)
+                  : im.uni             ? 4u
                   : im.mask1           ? 3u
                                        : 1u;
     }
+    p.uni = im.uni;
     p.stk_words = rows_stack_words(im, p.walk4);
     if (const char *e = std::getenv("MBRWT_ROWS_STAGE")) p.stage = (p.walk4 == 3 && e[0] == '1') ? 1u : 0u;
 

@@ -180,8 +180,10 @@ int mbrwt_set_build_option(int option, int64_t value);
 int mbrwt_layout(const mbrwt_ctx *ctx); /* MBRWT_LAYOUT_NODES / _ROWS / _BOTH of a context */
 /* Row-record image: out[0] block bytes B, [1] rows per block S, [2] block
    bytes, [3] spill bytes, [4] record bytes (counts + masks), [5] spilled rows,
-   [6] rows longer than a block, [7] tree height.  MBRWT_ERR_UNSUPPORTED
-   without row records. */
+   [6] rows longer than a block, [7] tree height | K << 32, K = the internal
+   levels above the leaf parents when every path has that many (the
+   odometer walk of csrc/rows.hip), else 0.  MBRWT_ERR_UNSUPPORTED without
+   row records. */
 int mbrwt_rows_stats(const mbrwt_ctx *ctx, uint64_t out[8]);
 
 /* ---- multi-device (one process, N GPUs) --------------------------------

@@ -112,6 +112,43 @@ def test_random_matrices_rows(oracle_mod, n, m, d, part, arity, relax, layout):
     np.testing.assert_array_equal(_count_labels(dev, rows), dense[rows.astype(np.int64)].sum(axis=0))
 
 
+@pytest.mark.parametrize("n,m,d,arity,levels", [
+    (20000, 512, 0.02, 8, 2),      # root -> 8 -> 64 leaf parents
+    (20000, 2652, 0.003, 8, 3),    # the Kingsford shape (C2-C4)
+    (5000, 2652, 0.3, 8, 3),       # long records: spills and the direct pass
+    (20000, 64, 0.05, 2, 5),       # binary, 5 internal levels
+    (20000, 128, 0.05, 2, 0),      # binary, 6 levels: beyond the odometer (walk 6)
+    (20000, 9, 0.2, 3, 1),         # the root's children are leaf parents
+    (20000, 40, 0.1, 8, 1),
+    (20000, 100, 0.05, 8, 2),      # 100 = 12 x 8 + 4: a short last group is still uniform
+    (3000, 7, 1.0, 2, 0),          # singleton groups pass through: mixed depths
+])
+def test_odometer_walk(oracle_mod, n, m, d, arity, levels, monkeypatch):
+    """rows_walk_uni (one lock-step iteration per reached leaf parent) and the
+    general walk (MBRWT_ROWS_WALK=6) return the oracle's CSR on uniform trees;
+    non-uniform trees report 0 levels and keep the general walk."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    rng = np.random.default_rng(n + m)
+    dense = rng.random((n, m)) < d
+    t = O.OracleTree.from_dense(dense, "basic", arity)
+    dev = BRWTDevice.from_tree(t.export(), layout="rows")
+    st = dev.rows_stats()
+    ex = t.export()
+    nc = np.asarray(ex["num_children"])
+    assert st["uniform_levels"] == levels, (st, int(nc.max()))
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 20000)]).astype(np.uint64)
+    off_o, cols_o = t.get_rows(rows)
+    for walk in ("", "6"):
+        if walk:
+            monkeypatch.setenv("MBRWT_ROWS_WALK", walk)
+        else:
+            monkeypatch.delenv("MBRWT_ROWS_WALK", raising=False)
+        off_d, cols_d = dev.get_rows(rows)
+        np.testing.assert_array_equal(off_d, off_o)
+        np.testing.assert_array_equal(cols_d, cols_o)
+
+
 def test_arity_limit(oracle_mod):
     """Nodes wider than 16 children stay on the node layout."""
     O = oracle_mod
