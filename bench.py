@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the all-gatherv reassembly")
+    ap.add_argument("--host-sizes", action="store_true",
+                    help="N>1: the all-gatherv with host-side sizes (a gloo exchange and a host sync per step) "
+                         "instead of the device-sized wire (dist.DeviceAllGatherV)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the host oracle (CPU baseline and parity)")
     ap.add_argument("--cpu-sample", type=int, default=400_000, help="rows timed on the CPU (job's cores)")
     ap.add_argument("--cpu-sample-1t", type=int, default=40_000, help="rows timed on one CPU thread")
@@ -283,7 +286,7 @@ def main():
     local = local % max(1, ndev)  # (rehearsal only: several ranks may share one GPU under gloo)
 
     from genome_graph_annotation_amd import BRWTDevice, _lib as L
-    from genome_graph_annotation_amd.dist import AllGatherV, shard_bounds
+    from genome_graph_annotation_amd.dist import AllGatherV, DeviceAllGatherV, shard_bounds
 
     # roofline traffic first: the PMC child passes need the GPU's memory for
     # their own copy of the structure
@@ -350,6 +353,14 @@ def main():
             nk = e.needed
         need = max(need, nk)
     cols_t = torch.empty(int(need * 1.02) + 1024, dtype=torch.int32, device=dev_t)
+    wire = None
+    if world > 1 and not a.no_gather and not a.host_sizes:
+        # the device-sized all-gatherv: every rank's wire segment holds up to
+        # labels_cap labels, agreed once here (max over ranks and batches)
+        cap_t = torch.tensor([int(need * 1.02) + 1024], dtype=torch.int64, device=dev_t)
+        dist.all_reduce(cap_t, op=dist.ReduceOp.MAX)
+        rows_per_rank = [shard_bounds(G, world, r)[1] - shard_bounds(G, world, r)[0] for r in range(world)]
+        wire = DeviceAllGatherV(rows_per_rank, int(cap_t.item()), a.cols, dev_t, timing=True)
 
     # N > 1: steps are pipelined -- batch k's all-gatherv (RCCL stream) runs
     # while batch k+1 is traversed, so the outputs are double-buffered; drain()
@@ -363,7 +374,7 @@ def main():
     # N = 1: the asynchronous call (include/mbrwt.h mbrwt_get_rows_device_async:
     # no host synchronisation per step; the status block -- labels, status,
     # sticky status bits -- is read once after the timed region)
-    use_async = world == 1 and not a.sync
+    use_async = (world == 1 or wire is not None) and not a.sync
     status_t = torch.zeros(3, dtype=torch.int64, device=dev_t)
 
     def step():
@@ -373,6 +384,14 @@ def main():
         h0 = time.perf_counter()
         if use_async:
             mat.get_rows_device_async(rows_ts[i % K], o, cb, status_t, sptr)
+            if state["timed"]:
+                state["get_rows_host"].append((time.perf_counter() - h0) * 1e3)
+            if wire is not None:
+                # no host synchronisation: the label count travels from the
+                # status block on the device into the wire header
+                if state["pending"] is not None:
+                    state["global"] = wire.finish(state["pending"])
+                state["pending"] = wire.start(o, cb, status_t)
             return None
         n_lab = mat.get_rows_device(rows_ts[i % K], o, cb, sptr)
         if state["timed"]:
@@ -388,13 +407,15 @@ def main():
 
     def drain():
         if state["pending"] is not None:
-            state["global"] = state["pending"].finish()
+            state["global"] = wire.finish(state["pending"]) if wire is not None else state["pending"].finish()
             state["pending"] = None
 
     for _ in range(a.warmup):
         step()
     drain()
     torch.cuda.synchronize()
+    if wire is not None:
+        wire.last_phases = []
     mat.take_timing()
     mat.set_option(L.MBRWT_OPT_TIMING, 1)
     state["timed"] = True
@@ -437,6 +458,11 @@ def main():
                 ph[k] = float(np.mean([e[k] for e in ex]))
             ph["wire_bytes_sent_per_rank"] = int(state["exchanges"][-1].wire_bytes)
             ph["wire_bytes_received_per_rank"] = int(state["exchanges"][-1].wire_bytes) * (world - 1)
+        if wire is not None:
+            ph.update(wire.phases())
+            ph["sizes_host_ms"] = 0.0  # (device-side sizes: no host exchange)
+            ph["wire_bytes_sent_per_rank"] = int(wire.wire_bytes)
+            ph["wire_bytes_received_per_rank"] = int(wire.wire_bytes) * (world - 1)
         keys = sorted(k for k, v in ph.items() if v is not None)
         t = torch.tensor([float(ph[k]) for k in keys], dtype=torch.float64, device=dev_t)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -450,7 +476,15 @@ def main():
     # all-gathered CSR every rank holds (N > 1)
     reassembly = None
     if gather:
-        g_off, g_cols = state["global"]
+        if wire is not None:
+            g_off, g_cols, g_st = state["global"]
+            tot, bad = g_st.tolist()
+            if bad or tot != int(g_off[-1].item()):
+                raise RuntimeError(f"device all-gatherv status: total {tot}, overflow flag {bad}, "
+                                   f"offsets end {int(g_off[-1].item())}")
+            g_cols = g_cols[:tot]
+        else:
+            g_off, g_cols = state["global"]
         b0 = int(g_off[lo].item())
         ok = bool(torch.equal(g_off[lo:hi + 1] - b0, last_off) and
                   torch.equal(g_cols[b0:b0 + n_lab], last_cols[:n_lab]) and g_off.numel() == G + 1)
@@ -594,7 +628,8 @@ def main():
             "global_batch": G, "batch_per_gpu": nb, "batches": K, "layout": a.layout,
             "api": "mbrwt_get_rows_device_async" if use_async else "mbrwt_get_rows_device",
             "parallelism": f"batch-sharded x{world}, tree replicated" + ("" if world == 1 or a.no_gather
-                                                                         else ", all-gatherv over " + ("RCCL" if a.dist_backend == "nccl" else a.dist_backend)),
+                                                                         else ", all-gatherv over " + ("RCCL" if a.dist_backend == "nccl" else a.dist_backend)
+                                                                         + (" (device-sized wire, no host sync)" if wire is not None else " (host-sized)")),
             "structure_bytes": struct_bytes,
             "setup_s": round(setup_s, 2),
         },

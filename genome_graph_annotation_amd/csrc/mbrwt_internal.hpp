@@ -289,6 +289,9 @@ struct WsFenceState {
 class WsFence {
   public:
     WsFence(WsFenceState &st, hipStream_t s) : st_(st), s_(s) {
+        // a stale error of an earlier, unrelated HIP call in this thread
+        // would otherwise be reported by the first launch check of this call
+        (void)hipGetLastError();
         if (st_.live && st_.ev) (void)hipStreamWaitEvent(s_, st_.ev, 0);
     }
     ~WsFence() {

@@ -53,7 +53,10 @@ void slice(uint64_t n, uint32_t k, uint32_t r, uint64_t &lo, uint64_t &hi) {
 void destroy(mbrwt_multi *m) {
     if (!m) return;
     for (size_t r = 0; r < m->ctx.size(); ++r) {
-        (void)hipSetDevice(m->dev[r]);
+        if (hipSetDevice(m->dev[r]) != hipSuccess) {  // no such device: nothing was created there
+            (void)hipGetLastError();                   // (and no sticky error left for the caller)
+            continue;
+        }
         for (Workspace *w : {&m->rows[r], &m->off[r], &m->cols[r]})
             if (w->buf) (void)hipFree(w->buf);
         if (m->stream[r]) (void)hipStreamDestroy(m->stream[r]);

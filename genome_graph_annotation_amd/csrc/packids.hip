@@ -72,6 +72,87 @@ __global__ __launch_bounds__(256) void k_unpack_segments(const uint8_t *__restri
     }
 }
 
+// a rank's wire segment with its label count on the device (include/mbrwt.h
+// mbrwt_pack_csr_device): header, row counts from the offsets, labels; one
+// grid-stride pass over the count words and the label words
+__global__ __launch_bounds__(256) void k_pack_csr(const uint64_t *__restrict__ offsets, uint64_t n_rows,
+                                                  const uint32_t *__restrict__ cols,
+                                                  const uint64_t *__restrict__ num_labels, uint64_t cap,
+                                                  uint32_t bits_c, uint32_t bits_l, uint32_t *__restrict__ wire,
+                                                  uint64_t lab_word0, uint64_t cnt_words, uint64_t lab_words) {
+    const uint64_t L = gld(num_labels);
+    const uint64_t nl = L < cap ? L : cap;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        gst(wire, (uint32_t)L);
+        gst(wire + 1, (uint32_t)(L >> 32));
+    }
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t total = cnt_words + lab_words;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gstride) {
+        const bool lab = k >= cnt_words;
+        const uint64_t kk = lab ? k - cnt_words : k;
+        const uint32_t bits = lab ? bits_l : bits_c;
+        const uint64_t n = lab ? nl : n_rows;
+        const uint32_t mask = bits == 32 ? 0xFFFFFFFFu : (1u << bits) - 1u;
+        const uint64_t b0 = 32 * kk, b1 = b0 + 32;
+        uint32_t w = 0;
+        for (uint64_t i = b0 / bits; i < n && i * bits < b1; ++i) {
+            const uint64_t pos = i * bits;
+            const uint32_t v = (lab ? gld(cols + i) : (uint32_t)(gld(offsets + i + 1) - gld(offsets + i))) & mask;
+            if (pos >= b0) w |= v << (pos - b0);
+            else w |= v >> (b0 - pos);
+        }
+        gst(wire + (lab ? lab_word0 + kk : 2 + kk), w);
+    }
+}
+
+// the labels of every segment, the segments' sizes from their headers
+__global__ __launch_bounds__(256) void k_unpack_labels_dev(const uint8_t *__restrict__ base, uint64_t stride,
+                                                           uint32_t nseg, uint64_t lab_off, uint64_t cap,
+                                                           uint32_t bits, uint32_t *__restrict__ out,
+                                                           uint64_t out_cap, unsigned long long *status) {
+    __shared__ uint64_t first[kMaxSegs + 1];
+    __shared__ uint32_t bad;
+    if (threadIdx.x == 0) {
+        uint64_t acc = 0;
+        uint32_t b = 0;
+        first[0] = 0;
+        for (uint32_t r = 0; r < nseg; ++r) {
+            const uint32_t *h = reinterpret_cast<const uint32_t *>(base + r * stride);
+            const uint64_t L = (uint64_t)gld(h) | ((uint64_t)gld(h + 1) << 32);
+            b |= L > cap ? 1u : 0u;
+            acc += L < cap ? L : cap;
+            first[r + 1] = acc;
+        }
+        b |= acc > out_cap ? 1u : 0u;
+        bad = b;
+        if (blockIdx.x == 0) {
+            status[0] = acc;
+            status[1] = b;
+        }
+    }
+    __syncthreads();
+    if (bad) return;
+    const uint64_t N = first[nseg];
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    const uint32_t mask = bits == 32 ? 0xFFFFFFFFu : (1u << bits) - 1u;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gstride) {
+        uint32_t lo = 0, hi = nseg;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (first[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+        const uint32_t *words = reinterpret_cast<const uint32_t *>(base + lo * stride + lab_off);
+        const uint64_t pos = (i - first[lo]) * bits;
+        const uint64_t w = pos >> 5;
+        const uint32_t off = (uint32_t)(pos & 31);
+        uint32_t x = gld(words + w) >> off;
+        if (off + bits > 32) x |= gld(words + w + 1) << (32 - off);
+        gst(out + i, x & mask);
+    }
+}
+
 unsigned grid_of(uint64_t n) { return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 16384)); }
 
 }  // namespace
@@ -131,6 +212,53 @@ int mbrwt_unpack_segments_device(const void *d_base, uint32_t nseg, uint64_t seg
         }
         done += sg.first[k];
     }
+    return MBRWT_OK;
+}
+
+uint64_t mbrwt_wire_labels_offset(uint64_t n_rows, uint32_t bits_count) {
+    if (bits_count < 1 || bits_count > 32) return 0;
+    return (8 + (n_rows * bits_count + 31) / 32 * 4 + 15) / 16 * 16;
+}
+
+int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint32_t *d_cols,
+                          const uint64_t *d_num_labels, uint64_t labels_cap, uint32_t bits_count, uint32_t bits_label,
+                          uint64_t labels_offset, void *d_wire, uint64_t wire_bytes, void *stream) {
+    if (bits_count < 1 || bits_count > 32 || bits_label < 1 || bits_label > 32 || !d_wire || !d_num_labels ||
+        (n_rows && !d_offsets) || (labels_cap && !d_cols) || wire_bytes % 16 || labels_offset % 16 ||
+        labels_offset < mbrwt_wire_labels_offset(n_rows, bits_count)) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    const uint64_t lab_off = labels_offset;
+    const uint64_t lab_words = (labels_cap * bits_label + 31) / 32;
+    if (lab_off + lab_words * 4 > wire_bytes) {
+        set_error("wire segment too small for the rows and the label capacity");
+        return MBRWT_ERR_INVALID;
+    }
+    const hipStream_t s = (hipStream_t)stream;
+    // the pads and the unused label words are zero (the wire is deterministic)
+    MBRWT_HIP(hipMemsetAsync(d_wire, 0, wire_bytes, s));
+    const uint64_t cnt_words = (n_rows * bits_count + 31) / 32;
+    hipLaunchKernelGGL(k_pack_csr, dim3(grid_of(std::max<uint64_t>(1, cnt_words + lab_words))), dim3(256), 0, s,
+                       d_offsets, n_rows, d_cols, d_num_labels, labels_cap, bits_count, bits_label,
+                       reinterpret_cast<uint32_t *>(d_wire), lab_off / 4, cnt_words, lab_words);
+    MBRWT_HIP(hipGetLastError());
+    return MBRWT_OK;
+}
+
+int mbrwt_unpack_labels_device(const void *d_base, uint32_t nseg, uint64_t seg_stride, uint64_t labels_offset,
+                               uint64_t labels_cap, uint32_t bits, uint32_t *d_values, uint64_t values_cap,
+                               uint64_t *d_status, void *stream) {
+    if (bits < 1 || bits > 32 || !d_base || !d_status || nseg < 1 || nseg > kMaxSegs || seg_stride % 4 ||
+        labels_offset % 4 || (values_cap && !d_values)) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    const uint64_t bound = std::min<uint64_t>(values_cap, (uint64_t)nseg * labels_cap);
+    hipLaunchKernelGGL(k_unpack_labels_dev, dim3(grid_of(std::max<uint64_t>(1, bound))), dim3(256), 0,
+                       (hipStream_t)stream, reinterpret_cast<const uint8_t *>(d_base), seg_stride, nseg, labels_offset,
+                       labels_cap, bits, d_values, values_cap, reinterpret_cast<unsigned long long *>(d_status));
+    MBRWT_HIP(hipGetLastError());
     return MBRWT_OK;
 }
 

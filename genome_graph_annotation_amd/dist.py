@@ -233,6 +233,128 @@ class AllGatherV:
         return g_off, g_cols
 
 
+class DeviceAllGatherV:
+    """The all-gatherv with DEVICE-side sizes: no host synchronisation per
+    exchange, so a GPU step (asynchronous get_rows + this exchange) never
+    waits on the host.  Every rank's wire segment has a fixed size, agreed
+    once (outside the timed region): [u64 label count][row counts at
+    bits_count][labels at bits_label, up to labels_cap] (include/mbrwt.h
+    mbrwt_pack_csr_device).  The label count is read from the device (the
+    status block of mbrwt_get_rows_device_async), the row counts of every
+    rank are static (the batch split), and the segments' label prefix is
+    computed on the device by the unpacking (mbrwt_unpack_labels_device).  A
+    label count above labels_cap sets status[1]; the caller reads the status
+    after its timed region.  GPU tensors and RCCL (or gloo) only.
+
+    rows_per_rank: every rank's slice length (host ints, the same on every
+    rank); labels_cap: the per-rank label capacity (the same on every rank);
+    slots: output double-buffering for pipelined steps."""
+
+    def __init__(self, rows_per_rank, labels_cap, num_columns, device, group=None, timing=False, slots=2):
+        from . import _lib as L
+        self.L = L
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        assert len(rows_per_rank) == self.world
+        self.ns = [int(x) for x in rows_per_rank]
+        self.cap = int(labels_cap)
+        self.bits_l, self.bits_c = wire_bits(num_columns)
+        n_max = max(self.ns)
+        self.lab_off = int(L.lib().mbrwt_wire_labels_offset(n_max, self.bits_c))
+        self.per = _round16(self.lab_off + max(1, _words(self.cap, self.bits_l)) * 4)
+        self.wire_bytes = self.per
+        self.device = device
+        self.timing = timing
+        N = sum(self.ns)
+        self.N = N
+        self.slots = []
+        for _ in range(slots):
+            self.slots.append({
+                "send": torch.empty(self.per, dtype=torch.uint8, device=device),
+                "recv": torch.empty(self.world * self.per, dtype=torch.uint8, device=device),
+                "cnt": torch.empty(max(1, N), dtype=torch.int32, device=device),
+                "off": torch.zeros(N + 1, dtype=torch.int64, device=device),
+                "cols": torch.empty(max(1, self.world * self.cap), dtype=torch.int32, device=device),
+                "status": torch.zeros(2, dtype=torch.int64, device=device),
+                "done": torch.cuda.Event(),
+                "ev": {k: torch.cuda.Event(enable_timing=True) for k in ("t0", "packed", "gathered", "done")}
+                if timing else {},
+            })
+        self.k = 0
+        self.side = _side_stream(device)
+        self.last_phases = []
+
+    def start(self, offsets, cols, d_num_labels):
+        """Queue the exchange of this rank's slice (offsets [n_r + 1] int64,
+        cols int32, d_num_labels: a device u64/int64 holding offsets[-1]);
+        returns the slot handle for finish()."""
+        L = self.L
+        sl = self.slots[self.k % len(self.slots)]
+        self.k += 1
+        cur = torch.cuda.current_stream(self.device)
+        s = cur.cuda_stream
+        if sl["ev"]:
+            sl["ev"]["t0"].record(cur)
+        L.check(L.lib().mbrwt_pack_csr_device(offsets.data_ptr(), self.ns[self.rank], cols.data_ptr(),
+                                              d_num_labels.data_ptr(), self.cap, self.bits_c, self.bits_l,
+                                              self.lab_off, sl["send"].data_ptr(), self.per, s),
+                "mbrwt_pack_csr_device")
+        if sl["ev"]:
+            sl["ev"]["packed"].record(cur)
+        if dist.get_backend(self.group) == "nccl":
+            work = dist.all_gather_into_tensor(sl["recv"], sl["send"], group=self.group, async_op=True)
+        else:  # (gloo: the rehearsal of several ranks on one GPU)
+            work = dist.all_gather(list(sl["recv"].chunk(self.world)), sl["send"], group=self.group, async_op=True)
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            work.wait()
+            if sl["ev"]:
+                sl["ev"]["gathered"].record(self.side)
+            ss = self.side.cuda_stream
+            import ctypes as C
+            arr = (C.c_uint64 * self.world)(*self.ns)
+            base = sl["recv"].data_ptr()
+            # row counts (static per rank) at byte 8 of every segment, then the
+            # labels with their device-side prefix, then the global offsets
+            L.check(L.lib().mbrwt_unpack_segments_device(base + 8, self.world, self.per, arr, self.bits_c,
+                                                         sl["cnt"].data_ptr(), ss), "mbrwt_unpack_segments_device")
+            L.check(L.lib().mbrwt_unpack_labels_device(base, self.world, self.per, self.lab_off, self.cap,
+                                                       self.bits_l, sl["cols"].data_ptr(), sl["cols"].numel(),
+                                                       sl["status"].data_ptr(), ss), "mbrwt_unpack_labels_device")
+            if self.N:
+                torch.cumsum(sl["cnt"][:self.N], 0, dtype=torch.int64, out=sl["off"][1:])
+            if sl["ev"]:
+                sl["ev"]["done"].record(self.side)
+            sl["done"].record(self.side)
+        return sl
+
+    def finish(self, sl):
+        """Make the current stream wait for the slot's exchange; returns the
+        global CSR (offsets [N + 1] int64, cols int32 with offsets[-1] valid
+        entries) and the exchange's status (device int64 [2]: total labels,
+        capacity overflow flag)."""
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(sl["done"])
+        if sl["ev"]:
+            self.last_phases.append(sl)
+        return sl["off"], sl["cols"], sl["status"]
+
+    def phases(self):
+        """Mean device times (ms) of the timed exchanges' phases."""
+        out = {}
+        if not self.last_phases:
+            return out
+        acc = {"pack_ms": [], "all_gather_ms": [], "unpack_ms": []}
+        for sl in self.last_phases:
+            e = sl["ev"]
+            e["done"].synchronize()
+            acc["pack_ms"].append(e["t0"].elapsed_time(e["packed"]))
+            acc["all_gather_ms"].append(e["packed"].elapsed_time(e["gathered"]))
+            acc["unpack_ms"].append(e["gathered"].elapsed_time(e["done"]))
+        return {k: float(sum(v) / len(v)) for k, v in acc.items()}
+
+
 _SIDE = {}
 
 

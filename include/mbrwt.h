@@ -384,6 +384,32 @@ int mbrwt_unpack_ids_device(const uint32_t *d_words, uint64_t n, uint32_t bits, 
    back to back in segment order. */
 int mbrwt_unpack_segments_device(const void *d_base, uint32_t nseg, uint64_t seg_stride, const uint64_t *counts,
                                  uint32_t bits, uint32_t *d_values, void *stream);
+/* The all-gatherv with DEVICE-side sizes (no host synchronisation per
+   exchange; dist.py AllGatherV(device_sizes=True)).  A rank's wire segment of
+   `wire_bytes` (a multiple of 16) is
+     [u64 num_labels][n_rows row counts at bits_count][zero pad to 16 bytes]
+     [min(num_labels, labels_cap) labels at bits_label][zero pad]
+   with num_labels read from the device (*d_num_labels, e.g. word 0 of the
+   status block of mbrwt_get_rows_device_async) and the row counts taken
+   from the CSR offsets (offsets[i+1] - offsets[i]); the label field starts
+   at byte labels_offset (a multiple of 16, at least
+   mbrwt_wire_labels_offset(n_rows, bits_count): every rank of an exchange
+   uses the offset of the largest slice) and needs
+   ceil(labels_cap * bits_label / 32) words.  MBRWT_ERR_INVALID when the
+   layout does not fit wire_bytes. */
+uint64_t mbrwt_wire_labels_offset(uint64_t n_rows, uint32_t bits_count);
+int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint32_t *d_cols,
+                          const uint64_t *d_num_labels, uint64_t labels_cap, uint32_t bits_count, uint32_t bits_label,
+                          uint64_t labels_offset, void *d_wire, uint64_t wire_bytes, void *stream);
+/* The labels of every segment of an all-gathered buffer of such segments
+   (segment r at d_base + r * seg_stride; its label field at labels_offset
+   bytes), written back to back in segment order: the segments' label counts
+   and their prefix are read from the headers ON THE DEVICE.  d_status[0] =
+   the total, d_status[1] = 0, or 1 when a header exceeds labels_cap or the
+   total exceeds values_cap (nothing is written past values_cap). */
+int mbrwt_unpack_labels_device(const void *d_base, uint32_t nseg, uint64_t seg_stride, uint64_t labels_offset,
+                               uint64_t labels_cap, uint32_t bits, uint32_t *d_values, uint64_t values_cap,
+                               uint64_t *d_status, void *stream);
 
 #define MBRWT_OPT_TIMING 1       /* 1: time the traversal kernel with HIP events */
 #define MBRWT_OPT_SLOT_LABELS 2  /* per-row label slots of the fast path (0 = auto) */

@@ -79,3 +79,16 @@ def test_no_device_is_reported_not_faked():
     from genome_graph_annotation_amd import BinRelWTDevice
     with pytest.raises(MBRWTError):
         BinRelWTDevice.synthetic(1000, 10, 0.1, 1)
+
+
+def test_wire_layout_errors():
+    """The device-sized wire's layout and argument checks (no GPU needed)."""
+    import ctypes as C
+    from genome_graph_annotation_amd import _lib as L
+    assert L.lib().mbrwt_wire_labels_offset(0, 12) == 16
+    assert L.lib().mbrwt_wire_labels_offset(10, 12) == 32  # 8 + 16 bytes of counts -> 32
+    # a wire too small for its label capacity, a misaligned label offset
+    assert L.lib().mbrwt_pack_csr_device(None, 0, None, C.c_void_p(16), 1000, 12, 12, 16, C.c_void_p(16), 64,
+                                         None) == L.MBRWT_ERR_INVALID
+    assert L.lib().mbrwt_pack_csr_device(None, 0, None, C.c_void_p(16), 0, 12, 12, 8, C.c_void_p(16), 64,
+                                         None) == L.MBRWT_ERR_INVALID

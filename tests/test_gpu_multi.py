@@ -65,3 +65,10 @@ def test_multi_synthetic_and_errors(oracle_mod):
     assert ei.value.status == L.MBRWT_ERR_RANGE
     with pytest.raises(MBRWTError):
         BRWTMulti.synthetic(n, m, d, 8, 42, devices=(0, 99))
+    # the failed creation leaves no sticky HIP error behind: the next query of
+    # an ordinary context in this thread still succeeds (r03 regression: a
+    # hipSetDevice(99) in the cleanup made the next launch check fail)
+    from genome_graph_annotation_amd import BRWTDevice
+    one = BRWTDevice.from_tree(O.OracleTree.from_dense(np.eye(5, dtype=bool), "basic", 2).export())
+    off1, cols1 = one.get_rows(np.arange(5, dtype=np.uint64))
+    assert cols1.tolist() == [0, 1, 2, 3, 4]
