@@ -1518,6 +1518,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows4(RowsParams p) {
         if (lane < nr && !valid) atomicOr(&p.scalars[2], 1ull);
         const uint64_t b = valid ? rows_block(row, S, p.magic) : 0;
         const uint32_t sub = (uint32_t)(row - b * S);
+        const uint64_t addr_c = p.blocks + b * B;  // (the address issue() used for this lane's row)
         uint32_t cnt = 0, o = 0;
         bool spl = false;
         if (valid) {
@@ -1531,23 +1532,28 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows4(RowsParams p) {
         if (any_spl) {
             // spilled rows: the entry (its first 64 bytes) replaces the block in
             // the row's slot, by LDS-DMA like the blocks (instruction k: slots
-            // 16k .. 16k + 15, lane L quarter L % 4 of slot 16k + L / 4; lanes
-            // of unspilled rows are masked off and leave their slots alone)
-            uint64_t sa = 0;
+            // 16k .. 16k + 15, lane L quarter L % 4 of slot 16k + L / 4).  An
+            // instruction runs with every lane active (measured: lanes masked
+            // off an LDS-DMA do not leave their LDS bytes alone), so the lanes
+            // of unspilled rows in a group with a spill re-read their row's
+            // block -- the same bytes; groups without a spill are skipped.
+            uint64_t sa = addr_c;  // this lane's row: its spill entry or its block
             if (spl) {
                 const uint32_t idx = (uint32_t)mine[o] | ((uint32_t)mine[o + 1] << 8) |
                                      ((uint32_t)mine[o + 2] << 16) | ((uint32_t)mine[o + 3] << 24);
                 sa = p.spill + (uint64_t)idx * 16;
             }
+            const uint64_t gmask = __ballot(spl);
             wave_sync();  // every entry is read before a slot is overwritten
 #pragma unroll
             for (uint32_t k = 0; k < 4; ++k) {
+                if (!((gmask >> (16 * k)) & 0xFFFFull)) continue;  // (wave-uniform)
                 const int src = (int)(16 * k + lane / 4);
                 const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)sa, src, 64);
                 const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(sa >> 32), src, 64);
                 const uint64_t ga = ((uint64_t)hi << 32) | lo;
-                if (ga) __builtin_amdgcn_global_load_lds((const AS_GLOBAL void *)(ga + 16u * (lane % 4)),
-                                                         (AS_LDS void *)(wb + 1024u * k), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((const AS_GLOBAL void *)(ga + 16u * (lane % 4)),
+                                                 (AS_LDS void *)(wb + 1024u * k), 16, 0, 0);
             }
         }
         // the next tile's blocks and the row ids of the tile after it

@@ -1,7 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out/v4
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_wire.py tests/test_gpu_multi.py > gpurun_out/v4/tests_wire.log 2>&1 || exit 1
+timeout -k 10 60 ./tools/_build/glds_exec_probe > gpurun_out/v4/glds_exec_probe.json 2>&1 || exit 1
 MBRWT_ROWS_KERNEL=4 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_rows.py > gpurun_out/v4/tests_v4.log 2>&1 || exit 1
 timeout -k 10 200 python tools/rows_ab.py --rows 1000000 --batch 1000000 --steps 50 --configs "rows@async+v4.async" > gpurun_out/v4/c2.log 2>&1 || exit 1
 timeout -k 10 300 python tools/rows_ab.py --rows 3700000000 --batch 8000000 --steps 20 --configs "rows@async+v4.async+v4.occ2.async+v4+async" > gpurun_out/v4/c4.log 2>&1 || exit 1
