@@ -62,6 +62,8 @@ def set_variant(kv):
             os.environ["MBRWT_ROWS_WGS_PER_CU"] = part[3:]
         elif part == "nosplit":
             os.environ["MBRWT_ROWS_SPLIT"] = "0"
+        elif part == "split":  # two halves, the first half's compaction on a side stream
+            os.environ["MBRWT_ROWS_SPLIT"] = "64"
         elif part == "stage":
             os.environ["MBRWT_ROWS_STAGE"] = "1"
         elif part == "async":
