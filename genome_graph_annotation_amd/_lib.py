@@ -26,6 +26,10 @@ MBRWT_OPT_SLOT_LABELS = 2
 MBRWT_OPT_KERNEL = 4
 
 MBRWT_BUILD_LAYOUT = 1
+MBRWT_BUILD_PARTITIONER = 2
+MBRWT_PARTITIONER_BASIC = 0
+MBRWT_PARTITIONER_GREEDY = 1
+PARTITIONERS = {"basic": MBRWT_PARTITIONER_BASIC, "greedy": MBRWT_PARTITIONER_GREEDY}
 MBRWT_LAYOUT_AUTO = 0
 MBRWT_LAYOUT_NODES = 1
 MBRWT_LAYOUT_ROWS = 2

@@ -202,12 +202,15 @@ class BRWTDevice:
         return cls(h)
 
     @classmethod
-    def from_columns(cls, columns, num_rows, arity=2, device=0, relax_max_arity=0, layout=None):
-        """BRWTBottomUpBuilder::build with the basic partitioner on the device
-        (include/mbrwt.h mbrwt_create_from_columns).  `columns`: a sequence of
-        uint64 arrays (ceil(num_rows/64) LSB-first words each), or a 2-D
-        uint64 array [num_columns, words].  relax_max_arity > 1 then runs
-        BRWTOptimizer::relax (mbrwt_create_from_columns_relaxed)."""
+    def from_columns(cls, columns, num_rows, arity=2, device=0, relax_max_arity=0, layout=None,
+                     partitioner="basic"):
+        """BRWTBottomUpBuilder::build on the device (include/mbrwt.h
+        mbrwt_create_from_columns) with the basic partitioner of `arity` or,
+        partitioner='greedy', binary_grouping_greedy (MBRWT_BUILD_PARTITIONER).
+        `columns`: a sequence of uint64 arrays (ceil(num_rows/64) LSB-first
+        words each), or a 2-D uint64 array [num_columns, words].
+        relax_max_arity > 1 then runs BRWTOptimizer::relax
+        (mbrwt_create_from_columns_relaxed)."""
         lib = L.lib()
         cols = [np.ascontiguousarray(c, dtype=np.uint64) for c in columns]
         W = (num_rows + 63) // 64
@@ -218,12 +221,18 @@ class BRWTDevice:
             ptrs[j] = c.ctypes.data_as(L.u64p)
         d = L.ColumnsDesc(num_rows, len(cols), ptrs, arity)
         h = C.c_void_p()
-        with build_layout(layout):
-            if relax_max_arity:
-                L.check(lib.mbrwt_create_from_columns_relaxed(C.byref(d), int(relax_max_arity), device,
-                                                              C.byref(h)), "mbrwt_create_from_columns_relaxed")
-            else:
-                L.check(lib.mbrwt_create_from_columns(C.byref(d), device, C.byref(h)), "mbrwt_create_from_columns")
+        L.check(lib.mbrwt_set_build_option(L.MBRWT_BUILD_PARTITIONER, L.PARTITIONERS[partitioner]),
+                "mbrwt_set_build_option")
+        try:
+            with build_layout(layout):
+                if relax_max_arity:
+                    L.check(lib.mbrwt_create_from_columns_relaxed(C.byref(d), int(relax_max_arity), device,
+                                                                  C.byref(h)), "mbrwt_create_from_columns_relaxed")
+                else:
+                    L.check(lib.mbrwt_create_from_columns(C.byref(d), device, C.byref(h)),
+                            "mbrwt_create_from_columns")
+        finally:
+            lib.mbrwt_set_build_option(L.MBRWT_BUILD_PARTITIONER, 0)
         return cls(h)
 
     @classmethod

@@ -164,6 +164,18 @@ class BRWTDevice : public BinaryMatrix {
         return m;
     }
 
+    // BRWTBottomUpBuilder::build with binary_grouping_greedy
+    // (partitionings.cpp:148-196; `transform_anno --greedy`), then relax --
+    // the reference's production build (scripts/kingsford/convert.sh:24)
+    static BRWTDevice build_greedy(const std::vector<std::vector<uint64_t>> &columns, uint64_t num_rows,
+                                   int device = 0, uint64_t relax_max_arity = 0) {
+        check_status(mbrwt_set_build_option(MBRWT_BUILD_PARTITIONER, MBRWT_PARTITIONER_GREEDY), "build option");
+        struct Reset {
+            ~Reset() { (void)mbrwt_set_build_option(MBRWT_BUILD_PARTITIONER, MBRWT_PARTITIONER_BASIC); }
+        } reset_;
+        return build_bottom_up(columns, num_rows, 2, device, relax_max_arity);
+    }
+
     // BRWTOptimizer::relax(brwt, max_arity) of an exported tree
     // (`annograph relax_brwt`, main.cpp:746)
     static BRWTDevice relaxed(const mbrwt_tree_desc &desc, uint64_t max_arity, int device = 0) {

@@ -17,12 +17,19 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <random>
+#include <tuple>
 #include <vector>
 
 #include "device_access.hpp"
 #include "mbrwt_internal.hpp"
 
 namespace mbrwt {
+
+static thread_local int g_build_partitioner = MBRWT_PARTITIONER_BASIC;
+int build_partitioner() { return g_build_partitioner; }
+void set_build_partitioner(int partitioner) { g_build_partitioner = partitioner; }
+
 namespace {
 
 // One level of the bottom-up build, batched: every group of >= 2 nodes of the
@@ -91,6 +98,88 @@ __global__ void k_clear_tails(uint64_t *cols, uint64_t m, uint64_t W, uint64_t k
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gstride) cols[j * W + W - 1] &= keep;
 }
 
+// ---- binary_grouping_greedy (partitionings.cpp:148-196) ---------------------
+//
+// The partitioner of the reference's production build (`transform_anno
+// --greedy`, scripts/kingsford/convert.sh:24).  At every level the
+// similarity of two columns is their inner product over a fixed row sample
+// (random_submatrix, partitionings.cpp:37-58: a fresh mt19937 seeded 1,
+// utils::sample_indexes of min(10^6, rows) rows, sorted); the pairs are
+// taken greedily by (similarity descending, index distance ascending).  The
+// m(m-1)/2 inner products -- the whole cost of the reference's greedy build
+// -- are an AND-popcount "GEMM" over the sampled words: k_gather_sample
+// compacts the sampled bits of every column, k_similarity computes 64 x 64
+// tiles of the lower triangle with both column blocks staged in LDS.  The
+// candidate order and the matching stay on the host with the reference's own
+// std::sort and comparator: std::sort is not stable, so equal (similarity,
+// distance) candidates come out in its order, which only the same algorithm
+// reproduces, and that order can decide the matching.
+
+// sampled bits: sub[c][w] bit b = column c at row idx[64 w + b]
+__global__ __launch_bounds__(256) void k_gather_sample(const uint64_t *const *cols, const uint64_t *__restrict__ idx,
+                                                       uint64_t ns, uint64_t SW, uint64_t *__restrict__ sub) {
+    const uint32_t c = blockIdx.y;
+    const uint64_t *col = cols[c];
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < SW; w += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t x = 0;
+        const uint64_t k0 = 64 * w;
+        for (uint32_t b = 0; b < 64 && k0 + b < ns; ++b) {
+            const uint64_t r = gld(idx + k0 + b);
+            x |= ((gld(col + (r >> 6)) >> (r & 63)) & 1ull) << b;
+        }
+        sub[(uint64_t)c * SW + w] = x;
+    }
+}
+
+// inner products of every pair j > k of the m sampled columns (SW words
+// each; column c at cols[c]), 64 x 64 tiles of the lower triangle (tile
+// (J, K), K <= J, from blockIdx.x), 4 x 4 products per thread, the words in
+// chunks of 32 through LDS.  out[j (j - 1) / 2 + k] = <col j, col k>.
+constexpr uint32_t kSimTile = 64, kSimChunk = 32;
+__global__ __launch_bounds__(256) void k_similarity(const uint64_t *const *cols, uint32_t m, uint64_t SW,
+                                                    uint32_t *__restrict__ out) {
+    __shared__ uint64_t sa[kSimChunk][kSimTile + 1], sb[kSimChunk][kSimTile + 1];
+    // tile index -> (J, K) with K <= J
+    uint32_t t = blockIdx.x, J = 0;
+    while (t > J) {
+        t -= J + 1;
+        ++J;
+    }
+    const uint32_t K = t;
+    const uint32_t tx = threadIdx.x & 15, ty = threadIdx.x >> 4;  // 16 x 16 threads, 4 x 4 each
+    uint32_t acc[4][4] = {};
+    for (uint64_t w0 = 0; w0 < SW; w0 += kSimChunk) {
+        for (uint32_t i = threadIdx.x; i < kSimChunk * kSimTile; i += 256) {
+            const uint32_t col = i / kSimChunk, w = i % kSimChunk;  // consecutive threads: consecutive words
+            const uint32_t ja = J * kSimTile + col, kb = K * kSimTile + col;
+            sa[w][col] = (ja < m && w0 + w < SW) ? gld(cols[ja] + w0 + w) : 0ull;
+            sb[w][col] = (kb < m && w0 + w < SW) ? gld(cols[kb] + w0 + w) : 0ull;
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (uint32_t w = 0; w < kSimChunk; ++w) {
+            uint64_t a[4], b[4];
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i) {
+                a[i] = sa[w][ty + 16 * i];
+                b[i] = sb[w][tx + 16 * i];
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i)
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) acc[i][q] += (uint32_t)__popcll(a[i] & b[q]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i)
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t j = J * kSimTile + ty + 16 * i, k = K * kSimTile + tx + 16 * q;
+            if (j < m && k < j) out[(uint64_t)j * (j - 1) / 2 + k] = acc[i][q];
+        }
+}
+
 unsigned grid_of(uint64_t n, uint64_t ys = 1) {  // keep x * y moderate for 2-D grids
     const uint64_t cap = std::max<uint64_t>(1, 65536 / std::max<uint64_t>(1, ys));
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, cap));
@@ -103,6 +192,66 @@ struct BNode {
     std::vector<uint64_t> index;     // host: the node's index column
     uint64_t index_len = 0;
 };
+
+// utils::sample_indexes (utils.cpp:777-816) as random_submatrix calls it
+// (partitionings.cpp:37-58): a fresh mt19937 seeded 1, min(10^6, n) rows
+// (kNumRowsSampled, partitionings.cpp:5), returned sorted
+std::vector<uint64_t> greedy_sample_rows(uint64_t n) {
+    std::vector<uint64_t> idx;
+    if (!n) return idx;
+    std::mt19937 gen;
+    gen.seed(1);
+    const uint64_t want = std::min<uint64_t>(n, 1000000);
+    idx.reserve(3 * want);
+    if (want * 10 < n) {
+        std::uniform_int_distribution<uint64_t> dis(0, n - 1);
+        while (idx.size() < want) {
+            idx.clear();
+            for (size_t i = 0; i < 1.5 * want; ++i) idx.push_back(dis(gen));
+            std::sort(idx.begin(), idx.end());
+            idx.erase(std::unique(idx.begin(), idx.end()), idx.end());
+        }
+    } else {
+        std::bernoulli_distribution dis(2.0 * want / n);
+        while (idx.size() < want) {
+            idx.clear();
+            for (uint64_t i = 0; i < n; ++i)
+                if (dis(gen)) idx.push_back(i);
+        }
+    }
+    std::shuffle(idx.begin(), idx.end(), gen);
+    idx.resize(want);
+    std::sort(idx.begin(), idx.end());
+    return idx;
+}
+
+// the greedy pairs of one level (parallel_binary_grouping_greedy,
+// partitionings.cpp:148-196) from the lower-triangle inner products
+std::vector<std::vector<size_t>> greedy_groups(const std::vector<uint32_t> &sim, size_t m) {
+    std::vector<std::tuple<size_t, size_t, uint64_t>> cand;
+    cand.reserve(m * (m - 1) / 2);
+    for (size_t j = 1; j < m; ++j)
+        for (size_t k = 0; k < j; ++k) cand.emplace_back(j, k, (uint64_t)sim[j * (j - 1) / 2 + k]);
+    auto dist = [](size_t a, size_t b) { return a > b ? a - b : b - a; };
+    std::sort(cand.begin(), cand.end(), [&](const auto &f, const auto &g) {
+        return std::get<2>(f) > std::get<2>(g) ||
+               (std::get<2>(f) == std::get<2>(g) &&
+                dist(std::get<0>(f), std::get<1>(f)) < dist(std::get<0>(g), std::get<1>(g)));
+    });
+    std::vector<std::vector<size_t>> groups;
+    groups.reserve((m + 1) / 2);
+    std::vector<bool> matched(m, false);
+    for (const auto &c : cand) {
+        const size_t i = std::get<0>(c), j = std::get<1>(c);
+        if (!matched[i] && !matched[j]) {
+            matched[i] = matched[j] = true;
+            groups.push_back({i, j});
+        }
+    }
+    for (size_t i = 0; i < m; ++i)
+        if (!matched[i]) groups.push_back({i});
+    return groups;
+}
 
 // ---- BRWTOptimizer::relax (BRWT_builders.cpp:166-297) ----------------------
 //
@@ -319,7 +468,8 @@ int build_from_columns(const mbrwt_columns_desc &cd, int device, Tree &tree, hip
                        uint64_t relax_max_arity) {
     MBRWT_HIP(hipSetDevice(device));
     const uint64_t n = cd.num_rows, m = cd.num_columns;
-    if (cd.arity < 2 || cd.arity > kMaxArity) {
+    const bool greedy = build_partitioner() == MBRWT_PARTITIONER_GREEDY;
+    if (!greedy && (cd.arity < 2 || cd.arity > kMaxArity)) {
         set_error("arity must be in [2, 64]");
         return MBRWT_ERR_INVALID;
     }
@@ -391,13 +541,84 @@ int build_from_columns(const mbrwt_columns_desc &cd, int device, Tree &tree, hip
         level[j] = j;
     }
     void *prev_parents = nullptr;  // row columns of the previous level's parents
+    // greedy: the row sample (the same every level: seed 1 each call) and its words
+    std::vector<uint64_t> sample;
+    uint64_t *d_sample = nullptr;
+    const bool sample_all = greedy && n <= 1000000;  // every row, in order: the columns themselves
+    if (greedy && !sample_all) {
+        sample = greedy_sample_rows(n);
+        d_sample = reinterpret_cast<uint64_t *>(dalloc(sample.size() * sizeof(uint64_t)));
+        if (!d_sample) {
+            cleanup();
+            return hip_fail(hipErrorOutOfMemory, "builder allocation");
+        }
+        MBRWT_HIP(hipMemcpyAsync(d_sample, sample.data(), sample.size() * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    }
+    const uint64_t ns = sample_all ? n : sample.size(), SW = (ns + 63) / 64;
+    double t_sim_ms = 0, t_sort_ms = 0;
     while (level.size() > 1) {  // BRWT_builders.cpp:134-158
-        // groups of the basic partitioner; singletons pass through (:75-77)
+        // the partition of this level: the basic partitioner's consecutive
+        // groups (:20-31) or the greedy pairs; singletons pass through (:75-77)
+        std::vector<std::vector<size_t>> part;
+        if (!greedy) {
+            for (size_t g0 = 0; g0 < level.size(); g0 += cd.arity) {
+                std::vector<size_t> grp;
+                for (size_t i = g0; i < std::min<size_t>(level.size(), g0 + cd.arity); ++i) grp.push_back(i);
+                part.push_back(std::move(grp));
+            }
+        } else {
+            const size_t L = level.size();
+            const auto t0 = std::chrono::steady_clock::now();
+            // the level's columns (pointer table), the sampled words, the products
+            std::vector<const uint64_t *> hp(L);
+            for (size_t i = 0; i < L; ++i) hp[i] = nodes[level[i]].rowcol;
+            const uint64_t **d_ptr = reinterpret_cast<const uint64_t **>(dalloc(L * sizeof(void *) * 2));
+            uint64_t *d_sub = sample_all ? nullptr : reinterpret_cast<uint64_t *>(dalloc(L * SW * sizeof(uint64_t)));
+            const uint64_t npairs = (uint64_t)L * (L - 1) / 2;
+            uint32_t *d_sim = reinterpret_cast<uint32_t *>(dalloc(npairs * sizeof(uint32_t)));
+            if (!d_ptr || (!sample_all && !d_sub) || !d_sim) {
+                cleanup();
+                return hip_fail(hipErrorOutOfMemory, "builder allocation");
+            }
+            MBRWT_HIP(hipMemcpyAsync(d_ptr, hp.data(), L * sizeof(void *), hipMemcpyHostToDevice, s));
+            const uint64_t *const *simcols = d_ptr;
+            if (!sample_all) {
+                for (uint32_t y0 = 0; y0 < L; y0 += 65535) {
+                    const uint32_t ny = (uint32_t)std::min<size_t>(65535, L - y0);
+                    hipLaunchKernelGGL(k_gather_sample, dim3(grid_of(SW, ny), ny), dim3(256), 0, s, d_ptr + y0,
+                                       (const uint64_t *)d_sample, ns, SW, d_sub + (uint64_t)y0 * SW);
+                }
+                MBRWT_HIP(hipGetLastError());
+                std::vector<const uint64_t *> hs(L);
+                for (size_t i = 0; i < L; ++i) hs[i] = d_sub + i * SW;
+                MBRWT_HIP(hipMemcpyAsync(d_ptr + L, hs.data(), L * sizeof(void *), hipMemcpyHostToDevice, s));
+                simcols = d_ptr + L;
+            }
+            const uint64_t T = (L + kSimTile - 1) / kSimTile, tiles = T * (T + 1) / 2;
+            if (tiles > 0x7FFFFFFFull) {
+                cleanup();
+                set_error("too many columns for the greedy partitioner");
+                return MBRWT_ERR_UNSUPPORTED;
+            }
+            hipLaunchKernelGGL(k_similarity, dim3((unsigned)tiles), dim3(256), 0, s, simcols, (uint32_t)L, SW, d_sim);
+            MBRWT_HIP(hipGetLastError());
+            std::vector<uint32_t> sim(npairs);
+            MBRWT_HIP(hipMemcpyAsync(sim.data(), d_sim, npairs * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            MBRWT_HIP(hipStreamSynchronize(s));
+            const auto t1 = std::chrono::steady_clock::now();
+            part = greedy_groups(sim, L);
+            const auto t2 = std::chrono::steady_clock::now();
+            t_sim_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+            t_sort_ms += std::chrono::duration<double, std::milli>(t2 - t1).count();
+            dfree(d_sim);
+            if (d_sub) dfree(d_sub);
+            dfree(d_ptr);
+        }
         std::vector<uint32_t> next, gchild{0}, child_group, child_node;
         std::vector<size_t> group_slot;  // position in `next` of each parent
-        for (size_t g0 = 0; g0 < level.size(); g0 += cd.arity) {
-            const size_t g1 = std::min<size_t>(level.size(), g0 + cd.arity);
-            if (g1 - g0 == 1) {
+        for (const auto &grp : part) {
+            const size_t g0 = grp[0];
+            if (grp.size() == 1) {
                 // a passed-through internal node keeps its row column: move it
                 // out of the previous level's parent arena, freed below
                 BNode &single = nodes[level[g0]];
@@ -414,7 +635,7 @@ int build_from_columns(const mbrwt_columns_desc &cd, int device, Tree &tree, hip
                 continue;
             }
             const uint32_t g = (uint32_t)group_slot.size();
-            for (size_t i = g0; i < g1; ++i) {
+            for (const size_t i : grp) {  // (the group's order: the reference's child order)
                 child_group.push_back(g);
                 child_node.push_back(level[i]);
             }
@@ -533,8 +754,9 @@ int build_from_columns(const mbrwt_columns_desc &cd, int device, Tree &tree, hip
     const int rc = image_from_nodes(nodes, level[0], n, m, device, tree);
     if (const char *e = std::getenv("MBRWT_BUILD_TIMING"); e && e[0] == '1') {
         const auto t_end = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "[mbrwt build] index columns %.1f ms, image layout %.1f ms\n",
-                     std::chrono::duration<double, std::milli>(t_index - t_start).count(),
+        std::fprintf(stderr, "[mbrwt build] index columns %.1f ms (greedy: similarities %.1f ms, sort + matching "
+                     "%.1f ms), image layout %.1f ms\n",
+                     std::chrono::duration<double, std::milli>(t_index - t_start).count(), t_sim_ms, t_sort_ms,
                      std::chrono::duration<double, std::milli>(t_end - t_index).count());
     }
     return rc;

@@ -437,6 +437,11 @@ uint64_t mbrwt_num_nodes(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.num_n
 uint64_t mbrwt_device_bytes(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.image_bytes + C(ctx)->rows.bytes : 0; }
 
 int mbrwt_set_build_option(int option, int64_t value) {
+    if (option == MBRWT_BUILD_PARTITIONER &&
+        (value == MBRWT_PARTITIONER_BASIC || value == MBRWT_PARTITIONER_GREEDY)) {
+        set_build_partitioner((int)value);
+        return MBRWT_OK;
+    }
     if (option != MBRWT_BUILD_LAYOUT || value < MBRWT_LAYOUT_AUTO || value > MBRWT_LAYOUT_BOTH) {
         set_error("unknown build option or value");
         return MBRWT_ERR_INVALID;

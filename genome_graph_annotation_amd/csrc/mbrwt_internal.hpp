@@ -442,6 +442,9 @@ int sharded_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d
 int sharded_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s);
 int sharded_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap, uint64_t *rows_needed,
                        hipStream_t s);
+// the calling thread's partitioner for build_from_columns (mbrwt_set_build_option)
+int build_partitioner();
+void set_build_partitioner(int partitioner);
 int build_from_columns(const mbrwt_columns_desc &desc, int device, Tree &tree, hipStream_t stream,
                        uint64_t relax_max_arity = 0);
 // BRWTOptimizer::relax on a tree description (build.hip)

@@ -172,6 +172,17 @@ void mbrwt_destroy(mbrwt_ctx *ctx);
  * counterpart (the reference's BRWT has one sdsl layout).
  */
 #define MBRWT_BUILD_LAYOUT 1
+/* (MBRWT_BUILD_PARTITIONER, value): the partitioner of the calling thread's
+   mbrwt_create_from_columns[_relaxed] -- MBRWT_PARTITIONER_BASIC (default:
+   groups of desc->arity consecutive nodes) or MBRWT_PARTITIONER_GREEDY
+   (binary_grouping_greedy, partitionings.cpp:148-196, the `--greedy` build of
+   scripts/kingsford/convert.sh:24; desc->arity is ignored): per level the
+   inner products of every column pair over the reference's row sample
+   (min(10^6, rows) rows, mt19937 seed 1) on the device, the candidate sort
+   and the matching on the host as the reference does them. */
+#define MBRWT_BUILD_PARTITIONER 2
+#define MBRWT_PARTITIONER_BASIC 0
+#define MBRWT_PARTITIONER_GREEDY 1
 #define MBRWT_LAYOUT_AUTO 0
 #define MBRWT_LAYOUT_NODES 1
 #define MBRWT_LAYOUT_ROWS 2

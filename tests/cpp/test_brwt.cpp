@@ -97,7 +97,7 @@ TEST(BRWT, OutOfRange) {  // the reference asserts (BRWT.cpp:27); the mirror thr
 }
 // the same grids built from their columns by the device builder
 // (mbrwt_create_from_columns); device backend only
-static void grid_device_built(int kind, uint64_t relax = 0) {
+static void grid_device_built(int kind, uint64_t relax = 0, bool greedy = false) {
     if (!g_device) return;
     for (uint64_t n = 1; n < 20; ++n) {
         for (size_t mcols = 1; mcols < 20; ++mcols) {
@@ -111,10 +111,11 @@ static void grid_device_built(int kind, uint64_t relax = 0) {
                     ones += b;
                     if (b) words[j][i / 64] |= 1ull << (i % 64);
                 }
-            auto m = mbrwt_host::BRWTDevice::build_bottom_up(words, n, 2, 0, relax);
+            auto m = greedy ? mbrwt_host::BRWTDevice::build_greedy(words, n, 0, relax)
+                            : mbrwt_host::BRWTDevice::build_bottom_up(words, n, 2, 0, relax);
             EXPECT_EQ(ones, m.num_relations());
             // same shape as the reference builder's tree (the oracle's restatement)
-            auto om = OracleMatrix(build_oracle(cols, n, 0, 2, relax));
+            auto om = OracleMatrix(build_oracle(cols, n, greedy ? 1 : 0, 2, relax));
             EXPECT_EQ(om.num_relations(), m.num_relations());
             EXPECT_EQ(to_device(om).num_nodes(), m.num_nodes());
             test_brwt(m, cols, n);
@@ -155,6 +156,12 @@ TEST(BRWT, BuildBottomUPAllMixed) { grid(2, 0); }
 TEST(BRWTOptimizer, BuildBottomUPAllZero) { grid(0, UINT64_MAX); }
 TEST(BRWTOptimizer, BuildBottomUPAllOne) { grid(1, UINT64_MAX); }
 TEST(BRWTOptimizer, BuildBottomUPAllMixed) { grid(2, UINT64_MAX); }
+// binary_grouping_greedy on the device (MBRWT_PARTITIONER_GREEDY) over the
+// same grids (test_BRWT.cpp:152-212), against the oracle's greedy tree
+TEST(BRWT, DeviceGreedyBuilderAllZero) { grid_device_built(0, 0, true); }
+TEST(BRWT, DeviceGreedyBuilderAllOne) { grid_device_built(1, 0, true); }
+TEST(BRWT, DeviceGreedyBuilderAllMixed) { grid_device_built(2, 0, true); }
+TEST(BRWTOptimizer, DeviceGreedyBuilderAllMixed) { grid_device_built(2, UINT64_MAX, true); }
 // BRWTOptimizer::relax on the device (mbrwt_create_from_columns_relaxed)
 TEST(BRWTOptimizer, DeviceBuilderAllZero) { grid_device_built(0, UINT64_MAX); }
 TEST(BRWTOptimizer, DeviceBuilderAllOne) { grid_device_built(1, UINT64_MAX); }

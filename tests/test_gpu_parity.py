@@ -530,6 +530,57 @@ def test_device_builder_pass_through_nodes(oracle_mod, m):
     _check_rows(t, built, np.arange(n, dtype=np.uint64), variants=(0,))
 
 
+# ---- binary_grouping_greedy on the device (partitionings.cpp:148-196) ----
+
+def _same_tree(a, b):
+    for k in ("num_children", "first_child", "leaf_column"):
+        np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
+
+
+@pytest.mark.parametrize("n,m,d,relax", [
+    (3000, 100, 0.05, 0), (3000, 100, 0.05, 10), (5000, 257, 0.02, 0), (20000, 64, 0.1, 10),
+    (2000, 40, 0.0, 0),             # all-zero columns: every similarity ties
+    (2_500_000, 24, 0.001, 10),     # 1e6 < rows <= 1e7: the Bernoulli row sample
+    (12_000_000, 12, 0.0005, 0),    # rows > 1e7: the uniform row sample
+])
+def test_device_greedy_builder_matches_reference(oracle_mod, n, m, d, relax):
+    """mbrwt_create_from_columns[_relaxed] with MBRWT_PARTITIONER_GREEDY builds
+    the oracle's greedy (+ relax) tree: the same tree (exported shape), the same
+    image bytes, the same answers."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    words = O.generate_columns(n, m, d, seed=n + m + 7)
+    W = (n + 63) // 64
+    t = O.OracleTree(O.lib().oracle_build_from_columns(O._p64(words), n, m, 1, 2, relax))
+    built = BRWTDevice.from_columns(words[: m * W].reshape(m, W), n, 2, relax_max_arity=relax, partitioner="greedy")
+    ref = BRWTDevice.from_tree(t.export())
+    _same_tree(built.export(), t.export())
+    assert built.device_bytes() == ref.device_bytes()
+    rows = np.random.default_rng(3).integers(0, n, 20000).astype(np.uint64)
+    _check_rows(t, built, rows, variants=(0,))
+
+
+def test_device_greedy_builder_c2_production_shape(oracle_mod):
+    """The reference's production build (greedy + relax 10,
+    scripts/kingsford/convert.sh:24) of the C2 columns (1 M x 2,652, d = 0.3 %,
+    the reference's own mt19937 generator) on the device: the oracle's tree."""
+    import time
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    n, m = 1_000_000, 2652
+    words = O.generate_columns(n, m, 0.003, seed=42)
+    W = (n + 63) // 64
+    t0 = time.time()
+    built = BRWTDevice.from_columns(words.reshape(m, W), n, 2, relax_max_arity=10, partitioner="greedy")
+    dev_s = time.time() - t0
+    t0 = time.time()
+    t = O.OracleTree(O.lib().oracle_build_from_columns(O._p64(words), n, m, 1, 2, 10))
+    print(f"greedy + relax 10 of C2: device {dev_s:.2f} s, oracle {time.time() - t0:.1f} s")
+    _same_tree(built.export(), t.export())
+    rows = np.random.default_rng(4).integers(0, n, 100_000).astype(np.uint64)
+    _check_rows(t, built, rows, variants=(0,))
+
+
 # ---- BRWTOptimizer::relax on the device (SURVEY §8(f) row 4) ----
 
 def _oracle_from_words_relaxed(O, words, n, m, arity, relax):
