@@ -1448,167 +1448,6 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
     }
 }
 
-// k_traverse_rows (v4): v2 with the NEXT tile's 64 blocks in flight while the
-// current tile is walked.  The blocks go global -> LDS directly
-// (global_load_lds_dwordx4: no VGPRs held across the walk, which is what sank
-// the register-staged prefetch of v3), into the second of two 4 KiB slot
-// buffers per wave; the slots are unpadded (64-byte stride), as an LDS-DMA
-// instruction writes 64 lanes x 16 bytes contiguously.  Per tile:
-//   wait for everything issued so far (the tile's blocks and the next tile's
-//   row ids) -> parse the entries; spilled records are requested global ->
-//   LDS into their rows' slots -> issue the next tile's 4 block loads and the
-//   row ids of the tile after it -> wait for the spilled records only
-//   (vmcnt(5): the 5 newer requests stay in flight) -> scan, counts,
-//   odometer walk (rows_walk_uni: uniform trees, 64-byte blocks).
-// Row ids are loaded unconditionally (index clamped into the batch) and
-// checked where they are used: a conditional load would make the compiler
-// copy the result at the join, i.e. wait for it -- and for the LDS-DMA
-// requests issued before it -- right away.
-template <int WPB, bool NT>
-__global__ __launch_bounds__(64 * WPB) void k_traverse_rows4(RowsParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows4[];
-    constexpr uint32_t B = 64, TILE = 64 * B;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_rows4[i] = gld(p.table + i);
-    __syncthreads();
-    const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows4[0]);
-    const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows4 + 4;
-    const uint32_t C = p.C;
-    AS_LDS uint8_t *wb0 = (AS_LDS uint8_t *)(lds_rows4 + ((p.table_words + 3) & ~3u)) + wv * (2u * TILE);
-    const uint64_t ntiles = (p.n + 63) / 64;
-    const uint64_t tstride = (uint64_t)gridDim.x * WPB;
-    const uint32_t S = p.S;
-    // the block loads of tile `tt` (rows `rw` of its lanes) into slot buffer `wb`
-    auto issue = [&](uint64_t tt, uint64_t rw, AS_LDS uint8_t *wb) {
-        const bool v = tt * 64 + lane < p.n && rw < p.num_rows;
-        const uint64_t b = v ? rows_block(rw, S, p.magic) : 0;
-        const uint64_t addr = p.blocks + b * B;
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            const int src = (int)(16 * k + lane / 4);
-            const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)addr, src, 64);
-            const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(addr >> 32), src, 64);
-            const uint64_t ga = (((uint64_t)hi << 32) | lo) + 16u * (lane % 4);
-            __builtin_amdgcn_global_load_lds((const AS_GLOBAL void *)ga, (AS_LDS void *)(wb + 1024u * k), 16, 0,
-                                             NT ? 2 : 0);
-        }
-    };
-    auto row_id = [&](uint64_t tt) -> uint64_t {  // (clamped: see above)
-        const uint64_t i = tt * 64 + lane;
-        return gld(p.rows + (i < p.n ? i : p.n - 1));
-    };
-    uint64_t t = (uint64_t)blockIdx.x * WPB + wv;
-    uint64_t row_c = 0, row_n = 0;  // this lane's row in the current / next tile
-    uint32_t buf = 0;
-    if (t < ntiles) {
-        row_c = row_id(t);
-        issue(t, row_c, wb0);
-        row_n = row_id(t + tstride);
-    }
-    for (; t < ntiles; t += tstride) {
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this tile's blocks and the next tile's row ids
-        wave_sync();
-        AS_LDS uint8_t *wb = wb0 + buf * TILE;
-        AS_LDS uint8_t *mine = wb + lane * B;
-        const uint64_t r0 = t * 64;
-        const uint32_t nr = (uint32_t)(p.n - r0 < 64 ? p.n - r0 : 64);
-        const uint64_t row = row_c;
-        const bool valid = lane < nr && row < p.num_rows;  // (row ids past the batch are clamped copies)
-        if (lane < nr && !valid) atomicOr(&p.scalars[2], 1ull);
-        const uint64_t b = valid ? rows_block(row, S, p.magic) : 0;
-        const uint32_t sub = (uint32_t)(row - b * S);
-        const uint64_t addr_c = p.blocks + b * B;  // (the address issue() used for this lane's row)
-        uint32_t cnt = 0, o = 0;
-        bool spl = false;
-        if (valid) {
-            const uint32_t e = mine[sub];
-            o = e & 0x7Fu;
-            spl = (e & 0x80u) != 0;
-            cnt = mine[o];
-            ++o;
-        }
-        const bool any_spl = __any(spl);
-        if (any_spl) {
-            // spilled rows: the entry (its first 64 bytes) replaces the block in
-            // the row's slot, by LDS-DMA like the blocks (instruction k: slots
-            // 16k .. 16k + 15, lane L quarter L % 4 of slot 16k + L / 4).  An
-            // instruction runs with every lane active (measured: lanes masked
-            // off an LDS-DMA do not leave their LDS bytes alone), so the lanes
-            // of unspilled rows in a group with a spill re-read their row's
-            // block -- the same bytes; groups without a spill are skipped.
-            uint64_t sa = addr_c;  // this lane's row: its spill entry or its block
-            if (spl) {
-                const uint32_t idx = (uint32_t)mine[o] | ((uint32_t)mine[o + 1] << 8) |
-                                     ((uint32_t)mine[o + 2] << 16) | ((uint32_t)mine[o + 3] << 24);
-                sa = p.spill + (uint64_t)idx * 16;
-            }
-            const uint64_t gmask = __ballot(spl);
-            wave_sync();  // every entry is read before a slot is overwritten
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                if (!((gmask >> (16 * k)) & 0xFFFFull)) continue;  // (wave-uniform)
-                const int src = (int)(16 * k + lane / 4);
-                const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)sa, src, 64);
-                const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(sa >> 32), src, 64);
-                const uint64_t ga = ((uint64_t)hi << 32) | lo;
-                __builtin_amdgcn_global_load_lds((const AS_GLOBAL void *)(ga + 16u * (lane % 4)),
-                                                 (AS_LDS void *)(wb + 1024u * k), 16, 0, 0);
-            }
-        }
-        // the next tile's blocks and the row ids of the tile after it
-        const uint64_t tn = t + tstride;
-        if (tn < ntiles) issue(tn, row_n, wb0 + (buf ^ 1u) * TILE);  // (its last reader, tile t - 1, ended in wave_sync)
-        const uint64_t row_nn = row_id(tn + tstride);  // (unconditional: no join copy, see above)
-        bool lng = false;
-        if (any_spl) {
-            // the spilled entries have landed once at most the 5 requests
-            // issued after them are outstanding (none when there is no next tile)
-            if (tn < ntiles) __builtin_amdgcn_s_waitcnt(0x0F75);  // vmcnt(5)
-            else __builtin_amdgcn_s_waitcnt(0x0F70);                // vmcnt(0)
-            wave_sync();
-            if (spl) {
-                cnt = ((const AS_LDS uint32_t *)mine)[0];
-                lng = 8 + ((const AS_LDS uint32_t *)mine)[1] > B;
-                o = 8;
-            }
-        }
-        uint32_t x = cnt;
-#pragma unroll
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-            if (lane >= d) x += y;
-        }
-        const uint32_t total = __builtin_amdgcn_readlane(x, 63);
-        const uint32_t pos = x - cnt;
-        const bool direct = total > C || __any(lng);
-        uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
-        if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
-        if (!direct) {
-            AS_GLOBAL uint16_t *out = (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128);
-            const bool live = valid && cnt > 0;
-            switch (p.uni) {
-                case 1: rows_walk_uni<1>(mine, o, live, root, ent, out, pos); break;
-                case 2: rows_walk_uni<2>(mine, o, live, root, ent, out, pos); break;
-                case 3: rows_walk_uni<3>(mine, o, live, root, ent, out, pos); break;
-                case 4: rows_walk_uni<4>(mine, o, live, root, ent, out, pos); break;
-                default: rows_walk_uni<5>(mine, o, live, root, ent, out, pos); break;
-            }
-        }
-        if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u));
-        if (direct) {
-            unsigned long long k0 = 0;
-            if (lane == 0) k0 = atomicAdd(&p.scalars[1], (unsigned long long)nr);
-            k0 = (unsigned long long)__shfl((long long)k0, 0, 64);
-            if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(p.row_base + r0 + lane));
-        }
-        wave_sync();  // this buffer is refilled two tiles on
-        buf ^= 1u;
-        row_c = row_n;
-        row_n = row_nn;
-    }
-}
-
 // k_traverse_rows (v5): loader and walker waves.  In v2 every wave loads a
 // tile, waits, then walks it, and the two phases hardly overlap (C4: 0.21 ms
 // of loads alone, 0.44 ms with the walk; neither the request rate nor the
@@ -2194,7 +2033,7 @@ constexpr uint32_t kRows3Wpb = 4;  // (72 VGPRs: 7 waves per SIMD in 4-wave work
 // for A/B (2 = the default)
 int rows_version() {
     const char *e = std::getenv("MBRWT_ROWS_KERNEL");
-    return (e && (e[0] == '1' || e[0] == '3' || e[0] == '4' || e[0] == '5')) ? e[0] - '0' : 2;
+    return (e && (e[0] == '1' || e[0] == '3' || e[0] == '5')) ? e[0] - '0' : 2;
 }
 bool rows_v1() { return rows_version() == 1; }
 template <int B, bool NT, int V>
@@ -2234,12 +2073,8 @@ size_t rows5_lds(const RowsImage &im, uint32_t stk_words) {
     return ((im.table2.size() + 3) & ~size_t(3)) * 4 + ns * (64ull * im.B + 272) + ((ns + 3) & ~3u) * 4 +
            nw * 256ull * stk_words;
 }
-// v4 (LDS-DMA double buffer): uniform trees with 64-byte blocks only
-constexpr uint32_t kRows4Wpb = 6;  // 2 x 4 KiB per wave: 3 workgroups (18 waves) per CU
-bool rows_v4(const RowsImage &im) { return rows_version() == 4 && im.uni && im.B == 64; }
 RowsFn rows2_fn(const RowsImage &im) {
     const int v = rows_version();
-    if (rows_v4(im)) return im.bytes > (1ull << 30) ? k_traverse_rows4<kRows4Wpb, true> : k_traverse_rows4<kRows4Wpb, false>;
     if (v == 5) return im.bytes > (1ull << 30) ? rows5_fn_d<true>(im.B) : rows5_fn_d<false>(im.B);
     return v == 3 ? rows2_fn_v<3>(im) : rows2_fn_v<2>(im);
 }
@@ -2345,12 +2180,9 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     const RowsFn kfn = v1 ? rows_fn(im) : rows2_fn(im);
     const bool v5 = rows_version() == 5;
     if (v5) p.stk_words = rows_stack_words(im, 1);  // (v5 walks with rows_walk4)
-    const bool v4 = rows_v4(im);
-    if (v4) p.walk4 = 4;
-    const uint32_t wpb = v1 ? kRowsWpb : v5 ? rows5_wpb(im) : v4 ? kRows4Wpb : rows_version() == 3 ? kRows3Wpb : kRows2Wpb;
+    const uint32_t wpb = v1 ? kRowsWpb : v5 ? rows5_wpb(im) : rows_version() == 3 ? kRows3Wpb : kRows2Wpb;
     const size_t lds = v1   ? ((im.table.size() + 3) & ~size_t(3)) * 4 + kRowsWpb * (64ull * im.B + 2ull * C)
                        : v5 ? rows5_lds(im, p.stk_words)
-                       : v4 ? ((im.table2.size() + 3) & ~size_t(3)) * 4 + kRows4Wpb * 2ull * 64 * 64
                             : ((im.table2.size() + 3) & ~size_t(3)) * 4 +
                                   wpb * (64ull * (im.B + (rows_version() == 2 ? 4 : 0)) + 256ull * p.stk_words +
                                          (p.stage ? 2ull * C : 0ull));

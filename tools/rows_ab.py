@@ -56,7 +56,7 @@ def set_variant(kv):
     for part in kv.split("."):  # e.g. "w2.v2.diag1"
         if part.startswith("w"):  # w2: the v2 walk
             os.environ["MBRWT_ROWS_WALK"] = part[1:]
-        elif part in ("v1", "v2", "v3", "v4", "v5"):
+        elif part in ("v1", "v2", "v3", "v5"):
             os.environ["MBRWT_ROWS_KERNEL"] = part[1]
         elif part.startswith("occ"):  # occN: at most N workgroups per CU
             os.environ["MBRWT_ROWS_WGS_PER_CU"] = part[3:]
