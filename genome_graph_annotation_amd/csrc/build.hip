@@ -432,7 +432,7 @@ int relax_nodes(std::vector<BNode> &nodes, uint32_t root, uint64_t max_arity, hi
 }
 
 // breadth-first numbering of the node tree (mbrwt_tree_desc) and the image
-int image_from_nodes(const std::vector<BNode> &nodes, uint32_t root, uint64_t n, uint64_t m, int device, Tree &tree) {
+int desc_from_nodes(const std::vector<BNode> &nodes, uint32_t root, uint64_t n, uint64_t m, const DescSink &emit) {
     std::vector<uint32_t> order{root};
     for (size_t h = 0; h < order.size(); ++h)
         for (uint32_t c : nodes[order[h]].children) order.push_back(c);
@@ -459,13 +459,23 @@ int image_from_nodes(const std::vector<BNode> &nodes, uint32_t root, uint64_t n,
     desc.leaf_column = leaf_column.data();
     desc.vec_size = vec_size.data();
     desc.vec_words = vec_words.data();
-    return build_from_desc(desc, device, tree);
+    return emit(desc);
 }
 
 }  // namespace
 
 int build_from_columns(const mbrwt_columns_desc &cd, int device, Tree &tree, hipStream_t s,
                        uint64_t relax_max_arity) {
+    if (cd.num_rows > kMaxRows) {  // (the caller routes these through desc_from_columns + the sharded create)
+        set_error("num_rows >= 2^32: build through the row-sharded path");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
+    return desc_from_columns(cd, device, s, relax_max_arity,
+                             [&](const mbrwt_tree_desc &d) { return build_from_desc(d, device, tree); });
+}
+
+int desc_from_columns(const mbrwt_columns_desc &cd, int device, hipStream_t s, uint64_t relax_max_arity,
+                      const DescSink &emit) {
     MBRWT_HIP(hipSetDevice(device));
     const uint64_t n = cd.num_rows, m = cd.num_columns;
     const bool greedy = build_partitioner() == MBRWT_PARTITIONER_GREEDY;
@@ -477,13 +487,13 @@ int build_from_columns(const mbrwt_columns_desc &cd, int device, Tree &tree, hip
         set_error("null column array");
         return MBRWT_ERR_INVALID;
     }
-    if (m > 0xFFFFFFFFull || n > kMaxRows) {
-        set_error("num_rows >= 2^32 or num_columns >= 2^32 is not supported by this build");
+    if (m > 0xFFFFFFFFull) {
+        set_error("num_columns >= 2^32 is not supported by this build");
         return MBRWT_ERR_UNSUPPORTED;
     }
     if (m == 0) {  // BRWTBottomUpBuilder::build of no columns is BRWT() (BRWT_builders.cpp:122-123)
         mbrwt_tree_desc empty{};
-        return build_from_desc(empty, device, tree);
+        return emit(empty);
     }
     for (uint64_t j = 0; j < m; ++j)
         if (n && !cd.columns[j]) {
@@ -751,7 +761,7 @@ int build_from_columns(const mbrwt_columns_desc &cd, int device, Tree &tree, hip
         if (rr) return rr;
     }
     const auto t_index = std::chrono::steady_clock::now();
-    const int rc = image_from_nodes(nodes, level[0], n, m, device, tree);
+    const int rc = desc_from_nodes(nodes, level[0], n, m, emit);
     if (const char *e = std::getenv("MBRWT_BUILD_TIMING"); e && e[0] == '1') {
         const auto t_end = std::chrono::steady_clock::now();
         std::fprintf(stderr, "[mbrwt build] index columns %.1f ms (greedy: similarities %.1f ms, sort + matching "
@@ -766,13 +776,18 @@ int build_from_columns(const mbrwt_columns_desc &cd, int device, Tree &tree, hip
 // main.cpp:746) on a tree description: the BFS tree becomes a node tree, the
 // relax above runs, and the relaxed tree becomes the image.
 int build_relaxed_from_desc(const mbrwt_tree_desc &desc, uint64_t max_arity, int device, Tree &tree, hipStream_t s) {
+    return relaxed_desc(desc, max_arity, device, s,
+                        [&](const mbrwt_tree_desc &d) { return build_from_desc(d, device, tree); });
+}
+
+int relaxed_desc(const mbrwt_tree_desc &desc, uint64_t max_arity, int device, hipStream_t s, const DescSink &emit) {
     MBRWT_HIP(hipSetDevice(device));
     const uint32_t N = desc.num_nodes;
     if (N && (!desc.num_children || !desc.first_child || !desc.leaf_column || !desc.vec_size || !desc.vec_words)) {
         set_error("null array in the tree description");
         return MBRWT_ERR_INVALID;
     }
-    if (!N || max_arity <= 1) return build_from_desc(desc, device, tree);
+    if (!N || max_arity <= 1) return emit(desc);
     std::vector<BNode> nodes(N);
     for (uint32_t u = 0; u < N; ++u) {
         const uint32_t k = desc.num_children[u];
@@ -794,7 +809,7 @@ int build_relaxed_from_desc(const mbrwt_tree_desc &desc, uint64_t max_arity, int
     }
     const int rc = relax_nodes(nodes, 0, max_arity, s);
     if (rc) return rc;
-    return image_from_nodes(nodes, 0, desc.num_rows, desc.num_columns, device, tree);
+    return desc_from_nodes(nodes, 0, desc.num_rows, desc.num_columns, emit);
 }
 
 }  // namespace mbrwt

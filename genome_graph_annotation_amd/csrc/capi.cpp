@@ -374,12 +374,34 @@ int mbrwt_create_synthetic(const mbrwt_synth_desc *desc, int device, mbrwt_ctx *
     }
 }
 
+// rows >= 2^32 (Row = uint64_t, binary_matrix.hpp:11): the device builders
+// produce the tree description on a temporary stream and hand it to
+// mbrwt_create, which builds row shards (or row-record ranges) from it
+static int create_via_desc(int device, mbrwt_ctx **out,
+                           const std::function<int(hipStream_t, const DescSink &)> &build) {
+    if (!out) {
+        set_error("null output pointer");
+        return MBRWT_ERR_INVALID;
+    }
+    MBRWT_HIP(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    MBRWT_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const int rc = build(s, [&](const mbrwt_tree_desc &d) { return mbrwt_create(&d, device, out); });
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+    return rc;
+}
+
 int mbrwt_create_from_columns(const mbrwt_columns_desc *desc, int device, mbrwt_ctx **out) {
     if (!desc) {
         set_error("null columns description");
         return MBRWT_ERR_INVALID;
     }
     try {
+        if (desc->num_rows > kMaxRows)
+            return create_via_desc(device, out, [&](hipStream_t s, const DescSink &emit) {
+                return desc_from_columns(*desc, device, s, 0, emit);
+            });
         return create_common(device, out,
                              [&](Ctx &c) { return build_from_columns(*desc, device, c.tree, c.stream); });
     } catch (const std::bad_alloc &) {
@@ -398,6 +420,10 @@ int mbrwt_create_from_columns_relaxed(const mbrwt_columns_desc *desc, uint64_t r
         return MBRWT_ERR_INVALID;
     }
     try {
+        if (desc->num_rows > kMaxRows)
+            return create_via_desc(device, out, [&](hipStream_t s, const DescSink &emit) {
+                return desc_from_columns(*desc, device, s, relax_max_arity, emit);
+            });
         return create_common(device, out, [&](Ctx &c) {
             return build_from_columns(*desc, device, c.tree, c.stream, relax_max_arity);
         });
@@ -416,6 +442,10 @@ int mbrwt_create_relaxed(const mbrwt_tree_desc *desc, uint64_t max_arity, int de
         return MBRWT_ERR_INVALID;
     }
     try {
+        if (desc->num_rows > kMaxRows)
+            return create_via_desc(device, out, [&](hipStream_t s, const DescSink &emit) {
+                return relaxed_desc(*desc, max_arity, device, s, emit);
+            });
         return create_common(device, out, [&](Ctx &c) {
             return build_relaxed_from_desc(*desc, max_arity, device, c.tree, c.stream);
         });

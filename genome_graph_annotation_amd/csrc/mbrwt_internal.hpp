@@ -442,6 +442,13 @@ int sharded_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d
 int sharded_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s);
 int sharded_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap, uint64_t *rows_needed,
                        hipStream_t s);
+// the device builders' output: a tree description handed to a sink (the
+// image builder, or -- rows >= 2^32 -- the row-sharded / ranged create)
+using DescSink = std::function<int(const mbrwt_tree_desc &)>;
+int desc_from_columns(const mbrwt_columns_desc &desc, int device, hipStream_t stream, uint64_t relax_max_arity,
+                      const DescSink &emit);
+int relaxed_desc(const mbrwt_tree_desc &desc, uint64_t max_arity, int device, hipStream_t stream,
+                 const DescSink &emit);
 // the calling thread's partitioner for build_from_columns (mbrwt_set_build_option)
 int build_partitioner();
 void set_build_partitioner(int partitioner);

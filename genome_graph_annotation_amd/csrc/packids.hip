@@ -73,13 +73,29 @@ __global__ __launch_bounds__(256) void k_unpack_segments(const uint8_t *__restri
 }
 
 // a rank's wire segment with its label count on the device (include/mbrwt.h
-// mbrwt_pack_csr_device): header, row counts from the offsets, labels; one
-// grid-stride pass over the count words and the label words
+// mbrwt_pack_csr_device).  Thread q packs values [32q, 32q + 32) of one
+// field into exactly `bits` words (32 values x bits bits), reading them as
+// 16-byte vectors: the row counts (deltas of 33 offsets) for q < cnt_chunks,
+// then the labels.  Values past the field's count are 0.
+__device__ __forceinline__ void pack32(const uint32_t (&v)[32], uint32_t bits, uint32_t *__restrict__ out) {
+    uint64_t acc = 0;
+    uint32_t have = 0, k = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 32; ++i) {
+        acc |= (uint64_t)v[i] << have;
+        have += bits;
+        while (have >= 32) {
+            gst(out + k++, (uint32_t)acc);
+            acc >>= 32;
+            have -= 32;
+        }
+    }
+}
 __global__ __launch_bounds__(256) void k_pack_csr(const uint64_t *__restrict__ offsets, uint64_t n_rows,
                                                   const uint32_t *__restrict__ cols,
                                                   const uint64_t *__restrict__ num_labels, uint64_t cap,
                                                   uint32_t bits_c, uint32_t bits_l, uint32_t *__restrict__ wire,
-                                                  uint64_t lab_word0, uint64_t cnt_words, uint64_t lab_words) {
+                                                  uint64_t lab_word0, uint64_t cnt_chunks, uint64_t lab_chunks) {
     const uint64_t L = gld(num_labels);
     const uint64_t nl = L < cap ? L : cap;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -87,48 +103,76 @@ __global__ __launch_bounds__(256) void k_pack_csr(const uint64_t *__restrict__ o
         gst(wire + 1, (uint32_t)(L >> 32));
     }
     const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t total = cnt_words + lab_words;
-    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gstride) {
-        const bool lab = k >= cnt_words;
-        const uint64_t kk = lab ? k - cnt_words : k;
-        const uint32_t bits = lab ? bits_l : bits_c;
-        const uint64_t n = lab ? nl : n_rows;
-        const uint32_t mask = bits == 32 ? 0xFFFFFFFFu : (1u << bits) - 1u;
-        const uint64_t b0 = 32 * kk, b1 = b0 + 32;
-        uint32_t w = 0;
-        for (uint64_t i = b0 / bits; i < n && i * bits < b1; ++i) {
-            const uint64_t pos = i * bits;
-            const uint32_t v = (lab ? gld(cols + i) : (uint32_t)(gld(offsets + i + 1) - gld(offsets + i))) & mask;
-            if (pos >= b0) w |= v << (pos - b0);
-            else w |= v >> (b0 - pos);
+    const uint32_t mc = bits_c == 32 ? 0xFFFFFFFFu : (1u << bits_c) - 1u;
+    const uint32_t ml = bits_l == 32 ? 0xFFFFFFFFu : (1u << bits_l) - 1u;
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < cnt_chunks + lab_chunks; q += gstride) {
+        uint32_t v[32];
+        if (q < cnt_chunks) {
+            const uint64_t i0 = 32 * q;
+            uint64_t prev = i0 < n_rows ? gld(offsets + i0) : 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 32; ++i) {
+                const uint64_t nx = i0 + i < n_rows ? gld(offsets + i0 + i + 1) : prev;
+                v[i] = (uint32_t)(nx - prev) & mc;
+                prev = nx;
+            }
+            pack32(v, bits_c, wire + 2 + q * bits_c);
+        } else {
+            const uint64_t qq = q - cnt_chunks, i0 = 32 * qq;
+            if (i0 + 32 <= nl) {
+                const u32x4_t *src = reinterpret_cast<const u32x4_t *>(cols + i0);  // (cols: 16-byte aligned)
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k) {
+                    const u32x4_t x = gld(src + k);
+                    v[4 * k] = x.x & ml;
+                    v[4 * k + 1] = x.y & ml;
+                    v[4 * k + 2] = x.z & ml;
+                    v[4 * k + 3] = x.w & ml;
+                }
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < 32; ++i) v[i] = i0 + i < nl ? gld(cols + i0 + i) & ml : 0u;
+            }
+            pack32(v, bits_l, wire + lab_word0 + qq * bits_l);
         }
-        gst(wire + (lab ? lab_word0 + kk : 2 + kk), w);
     }
 }
 
-// the labels of every segment, the segments' sizes from their headers
+// the labels of every segment, the segments' sizes from their headers.
+// Thread q writes global labels [32q, 32q + 32): when they lie in one
+// segment (nearly always), from bits + 1 consecutive words with 16-byte
+// stores; else label by label.
 __global__ __launch_bounds__(256) void k_unpack_labels_dev(const uint8_t *__restrict__ base, uint64_t stride,
                                                            uint32_t nseg, uint64_t lab_off, uint64_t cap,
                                                            uint32_t bits, uint32_t *__restrict__ out,
                                                            uint64_t out_cap, unsigned long long *status) {
     __shared__ uint64_t first[kMaxSegs + 1];
     __shared__ uint32_t bad;
-    if (threadIdx.x == 0) {
-        uint64_t acc = 0;
-        uint32_t b = 0;
-        first[0] = 0;
-        for (uint32_t r = 0; r < nseg; ++r) {
+    if (threadIdx.x < 64) {  // the headers, one lane each, then a wave scan
+        const uint32_t r = threadIdx.x;
+        uint64_t L = 0;
+        if (r < nseg) {
             const uint32_t *h = reinterpret_cast<const uint32_t *>(base + r * stride);
-            const uint64_t L = (uint64_t)gld(h) | ((uint64_t)gld(h + 1) << 32);
-            b |= L > cap ? 1u : 0u;
-            acc += L < cap ? L : cap;
-            first[r + 1] = acc;
+            L = (uint64_t)gld(h) | ((uint64_t)gld(h + 1) << 32);
         }
-        b |= acc > out_cap ? 1u : 0u;
-        bad = b;
-        if (blockIdx.x == 0) {
-            status[0] = acc;
-            status[1] = b;
+        const bool over = L > cap;
+        const uint64_t Lc = L < cap ? L : cap;
+        uint64_t x = Lc;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(x, d, 64);
+            if (r >= d) x += y;
+        }
+        if (r < nseg) first[r + 1] = x;
+        if (r == 0) first[0] = 0;
+        const uint64_t tot = __shfl(x, 63, 64);
+        const bool any_over = __any(over);
+        if (r == 0) {
+            bad = (any_over || tot > out_cap) ? 1u : 0u;
+            if (blockIdx.x == 0) {
+                status[0] = tot;
+                status[1] = bad;
+            }
         }
     }
     __syncthreads();
@@ -136,20 +180,47 @@ __global__ __launch_bounds__(256) void k_unpack_labels_dev(const uint8_t *__rest
     const uint64_t N = first[nseg];
     const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
     const uint32_t mask = bits == 32 ? 0xFFFFFFFFu : (1u << bits) - 1u;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gstride) {
-        uint32_t lo = 0, hi = nseg;
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; 32 * q < N; q += gstride) {
+        const uint64_t i0 = 32 * q;
+        uint32_t lo = 0, hi = nseg;  // the segment of label i0
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
-            if (first[mid] <= i) lo = mid;
+            if (first[mid] <= i0) lo = mid;
             else hi = mid;
         }
-        const uint32_t *words = reinterpret_cast<const uint32_t *>(base + lo * stride + lab_off);
-        const uint64_t pos = (i - first[lo]) * bits;
-        const uint64_t w = pos >> 5;
-        const uint32_t off = (uint32_t)(pos & 31);
-        uint32_t x = gld(words + w) >> off;
-        if (off + bits > 32) x |= gld(words + w + 1) << (32 - off);
-        gst(out + i, x & mask);
+        if (i0 + 32 <= first[lo + 1]) {
+            const uint32_t *words = reinterpret_cast<const uint32_t *>(base + lo * stride + lab_off);
+            const uint64_t b0 = (i0 - first[lo]) * bits;
+            const uint64_t w0 = b0 >> 5;
+            const uint32_t sh = (uint32_t)(b0 & 31);
+            uint32_t v[32];
+            uint64_t acc = gld(words + w0) >> sh;
+            uint32_t have = 32 - sh, k = 1;
+#pragma unroll
+            for (uint32_t i = 0; i < 32; ++i) {
+                if (have < bits) {
+                    acc |= (uint64_t)gld(words + w0 + k++) << have;
+                    have += 32;
+                }
+                v[i] = (uint32_t)acc & mask;
+                acc >>= bits;
+                have -= bits;
+            }
+            u32x4_t *dst = reinterpret_cast<u32x4_t *>(out + i0);  // (out: 16-byte aligned, i0 % 32 == 0)
+#pragma unroll
+            for (uint32_t k2 = 0; k2 < 8; ++k2) gst(dst + k2, u32x4_t{v[4 * k2], v[4 * k2 + 1], v[4 * k2 + 2], v[4 * k2 + 3]});
+        } else {
+            for (uint64_t i = i0; i < i0 + 32 && i < N; ++i) {
+                while (lo + 1 < nseg && first[lo + 1] <= i) ++lo;
+                const uint32_t *words = reinterpret_cast<const uint32_t *>(base + lo * stride + lab_off);
+                const uint64_t pos = (i - first[lo]) * bits;
+                const uint64_t w = pos >> 5;
+                const uint32_t off = (uint32_t)(pos & 31);
+                uint32_t x = gld(words + w) >> off;
+                if (off + bits > 32) x |= gld(words + w + 1) << (32 - off);
+                gst(out + i, x & mask);
+            }
+        }
     }
 }
 
@@ -217,7 +288,7 @@ int mbrwt_unpack_segments_device(const void *d_base, uint32_t nseg, uint64_t seg
 
 uint64_t mbrwt_wire_labels_offset(uint64_t n_rows, uint32_t bits_count) {
     if (bits_count < 1 || bits_count > 32) return 0;
-    return (8 + (n_rows * bits_count + 31) / 32 * 4 + 15) / 16 * 16;
+    return (8 + (n_rows + 31) / 32 * bits_count * 4 + 15) / 16 * 16;  // (whole 32-value chunks)
 }
 
 int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint32_t *d_cols,
@@ -238,10 +309,20 @@ int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint
     const hipStream_t s = (hipStream_t)stream;
     // the pads and the unused label words are zero (the wire is deterministic)
     MBRWT_HIP(hipMemsetAsync(d_wire, 0, wire_bytes, s));
-    const uint64_t cnt_words = (n_rows * bits_count + 31) / 32;
-    hipLaunchKernelGGL(k_pack_csr, dim3(grid_of(std::max<uint64_t>(1, cnt_words + lab_words))), dim3(256), 0, s,
+    // 32 values per thread = `bits` words; the fields' last chunks may run past
+    // their words: the layout keeps room for whole chunks (checked below)
+    const uint64_t cnt_chunks = (n_rows + 31) / 32, lab_chunks = (labels_cap + 31) / 32;
+    if (8 + cnt_chunks * bits_count * 4 > lab_off || lab_off + lab_chunks * bits_label * 4 > wire_bytes) {
+        set_error("wire segment too small for whole 32-value chunks");
+        return MBRWT_ERR_INVALID;
+    }
+    if (((uintptr_t)d_cols) % 16) {
+        set_error("cols must be 16-byte aligned");
+        return MBRWT_ERR_INVALID;
+    }
+    hipLaunchKernelGGL(k_pack_csr, dim3(grid_of(std::max<uint64_t>(1, cnt_chunks + lab_chunks))), dim3(256), 0, s,
                        d_offsets, n_rows, d_cols, d_num_labels, labels_cap, bits_count, bits_label,
-                       reinterpret_cast<uint32_t *>(d_wire), lab_off / 4, cnt_words, lab_words);
+                       reinterpret_cast<uint32_t *>(d_wire), lab_off / 4, cnt_chunks, lab_chunks);
     MBRWT_HIP(hipGetLastError());
     return MBRWT_OK;
 }
@@ -254,8 +335,12 @@ int mbrwt_unpack_labels_device(const void *d_base, uint32_t nseg, uint64_t seg_s
         set_error("invalid argument");
         return MBRWT_ERR_INVALID;
     }
+    if (((uintptr_t)d_values) % 16) {
+        set_error("values must be 16-byte aligned");
+        return MBRWT_ERR_INVALID;
+    }
     const uint64_t bound = std::min<uint64_t>(values_cap, (uint64_t)nseg * labels_cap);
-    hipLaunchKernelGGL(k_unpack_labels_dev, dim3(grid_of(std::max<uint64_t>(1, bound))), dim3(256), 0,
+    hipLaunchKernelGGL(k_unpack_labels_dev, dim3(grid_of(std::max<uint64_t>(1, (bound + 31) / 32))), dim3(256), 0,
                        (hipStream_t)stream, reinterpret_cast<const uint8_t *>(d_base), seg_stride, nseg, labels_offset,
                        labels_cap, bits, d_values, values_cap, reinterpret_cast<unsigned long long *>(d_status));
     MBRWT_HIP(hipGetLastError());

@@ -1414,6 +1414,25 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
                 for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
                     gst(reinterpret_cast<u32x4_t *>(treg + 128 + q2),
                         *(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2));
+            } else if (p.walk4 == 4 && p.stage) {
+                // the odometer into the wave's LDS label stage, then the tile's
+                // labels as 16-byte vector stores (a few wide stores instead of
+                // one scattered 2-byte store per label: r03 SQ/TA counters show
+                // the texture-address unit, not the VALU, as the busiest unit)
+                AS_LDS uint16_t *stage = (AS_LDS uint16_t *)(wb + 64u * PB + 256u * p.stk_words);
+                const bool live = valid && cnt > 0;
+                switch (p.uni) {
+                    case 1: rows_walk_uni<1>(mine, o, live, root, ent, stage, pos); break;
+                    case 2: rows_walk_uni<2>(mine, o, live, root, ent, stage, pos); break;
+                    case 3: rows_walk_uni<3>(mine, o, live, root, ent, stage, pos); break;
+                    case 4: rows_walk_uni<4>(mine, o, live, root, ent, stage, pos); break;
+                    default: rows_walk_uni<5>(mine, o, live, root, ent, stage, pos); break;
+                }
+                wave_sync();
+                const uint32_t nbytes = total * 2;
+                for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
+                    gst(reinterpret_cast<u32x4_t *>(treg + 128 + q2),
+                        *(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2));
             } else if (p.walk4 == 4) {
                 AS_GLOBAL uint16_t *out = (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128);
                 const bool live = valid && cnt > 0;
@@ -2174,8 +2193,13 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
                                        : 1u;
     }
     p.uni = im.uni;
-    p.stk_words = rows_stack_words(im, p.walk4);
-    if (const char *e = std::getenv("MBRWT_ROWS_STAGE")) p.stage = (p.walk4 == 3 && e[0] == '1') ? 1u : 0u;
+    p.stk_words = p.walk4 == 4 ? 0u : rows_stack_words(im, p.walk4);  // (the odometer keeps no stack)
+    // the LDS label stage: the default for the odometer (C4 kernel 0.312 ->
+    // 0.287 ms, profiles/r03/v18_stage/), opt-in for walk 6 (no gain there);
+    // MBRWT_ROWS_STAGE=0/1 overrides
+    p.stage = p.walk4 == 4 ? 1u : 0u;
+    if (const char *e = std::getenv("MBRWT_ROWS_STAGE"))
+        p.stage = ((p.walk4 == 3 || p.walk4 == 4) && e[0] == '1') ? 1u : 0u;
 
     const RowsFn kfn = v1 ? rows_fn(im) : rows2_fn(im);
     const bool v5 = rows_version() == 5;

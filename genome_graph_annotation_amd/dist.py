@@ -262,7 +262,7 @@ class DeviceAllGatherV:
         self.bits_l, self.bits_c = wire_bits(num_columns)
         n_max = max(self.ns)
         self.lab_off = int(L.lib().mbrwt_wire_labels_offset(n_max, self.bits_c))
-        self.per = _round16(self.lab_off + max(1, _words(self.cap, self.bits_l)) * 4)
+        self.per = _round16(self.lab_off + max(1, (self.cap + 31) // 32 * self.bits_l) * 4)  # (whole 32-value chunks)
         self.wire_bytes = self.per
         self.device = device
         self.timing = timing
@@ -275,7 +275,7 @@ class DeviceAllGatherV:
                 "recv": torch.empty(self.world * self.per, dtype=torch.uint8, device=device),
                 "cnt": torch.empty(max(1, N), dtype=torch.int32, device=device),
                 "off": torch.zeros(N + 1, dtype=torch.int64, device=device),
-                "cols": torch.empty(max(1, self.world * self.cap), dtype=torch.int32, device=device),
+                "cols": torch.empty(max(1, self.world * self.cap) + 32, dtype=torch.int32, device=device),
                 "status": torch.zeros(2, dtype=torch.int64, device=device),
                 "done": torch.cuda.Event(),
                 "ev": {k: torch.cuda.Event(enable_timing=True) for k in ("t0", "packed", "gathered", "done")}

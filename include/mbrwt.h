@@ -400,14 +400,16 @@ int mbrwt_unpack_segments_device(const void *d_base, uint32_t nseg, uint64_t seg
    `wire_bytes` (a multiple of 16) is
      [u64 num_labels][n_rows row counts at bits_count][zero pad to 16 bytes]
      [min(num_labels, labels_cap) labels at bits_label][zero pad]
+   with both fields in whole chunks of 32 values (a chunk = bits words;
+   value i at bits [i*bits, (i+1)*bits) of the field, LSB-first)
    with num_labels read from the device (*d_num_labels, e.g. word 0 of the
    status block of mbrwt_get_rows_device_async) and the row counts taken
    from the CSR offsets (offsets[i+1] - offsets[i]); the label field starts
    at byte labels_offset (a multiple of 16, at least
    mbrwt_wire_labels_offset(n_rows, bits_count): every rank of an exchange
    uses the offset of the largest slice) and needs
-   ceil(labels_cap * bits_label / 32) words.  MBRWT_ERR_INVALID when the
-   layout does not fit wire_bytes. */
+   ceil(labels_cap / 32) * bits_label words; d_cols 16-byte aligned.
+   MBRWT_ERR_INVALID when the layout does not fit wire_bytes. */
 uint64_t mbrwt_wire_labels_offset(uint64_t n_rows, uint32_t bits_count);
 int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint32_t *d_cols,
                           const uint64_t *d_num_labels, uint64_t labels_cap, uint32_t bits_count, uint32_t bits_label,
@@ -417,7 +419,8 @@ int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint
    bytes), written back to back in segment order: the segments' label counts
    and their prefix are read from the headers ON THE DEVICE.  d_status[0] =
    the total, d_status[1] = 0, or 1 when a header exceeds labels_cap or the
-   total exceeds values_cap (nothing is written past values_cap). */
+   total exceeds values_cap (nothing is written then); d_values 16-byte
+   aligned, with room for the total rounded up to 32. */
 int mbrwt_unpack_labels_device(const void *d_base, uint32_t nseg, uint64_t seg_stride, uint64_t labels_offset,
                                uint64_t labels_cap, uint32_t bits, uint32_t *d_values, uint64_t values_cap,
                                uint64_t *d_status, void *stream);

@@ -982,3 +982,35 @@ def test_packt_synthetic_shaped(oracle_mod, relax, n_rows):
     t = O.OracleTree.topdown_shaped(n_rows, shape, 0.003, 11)
     rows = rng.integers(0, n_rows, 100_000).astype(np.uint64)
     _agree(t, [pt, plain], rows, [0, 1, 250, 499], 500)
+
+
+@pytest.mark.parametrize("partitioner,relax", [("basic", 0), ("greedy", 10)])
+def test_device_builder_beyond_2_32_rows(oracle_mod, partitioner, relax):
+    """The column builders at Row = uint64_t (binary_matrix.hpp:11): 2^32 +
+    3,000 rows x 5 sparse columns built on the device (the description goes
+    through the row-sharded create) against the oracle's tree of the same
+    columns, on the rows either side of 2^31 and 2^32, every set position and
+    random rows."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    n, m = 2**32 + 3000, 5
+    W = (n + 63) // 64
+    rng = np.random.default_rng(77)
+    words = np.zeros((m, W), dtype=np.uint64)
+    setpos = []
+    for j in range(m):
+        pos = np.unique(np.concatenate([rng.integers(0, n, 100_000), rng.integers(2**32 - 50, n, 40)]))
+        np.bitwise_or.at(words[j], pos // 64, np.left_shift(np.uint64(1), (pos % 64).astype(np.uint64)))
+        setpos.append(pos)
+    t = O.OracleTree.from_words(words.ravel(), n, m, partitioner, 2, relax)
+    built = BRWTDevice.from_columns(words, n, 2, relax_max_arity=relax, partitioner=partitioner)
+    assert built.num_rows() == n and built.num_relations() == t.num_relations()
+    edges = []
+    for e in (2**31, 2**32, n):
+        edges += list(range(e - 6, min(e + 6, n)))
+    rows = np.concatenate([np.array(edges), np.concatenate(setpos)[::7], rng.integers(0, n, 50_000)])
+    rows = rows.astype(np.uint64)
+    off_o, cols_o = t.get_rows(rows)
+    off_d, cols_d = built.get_rows(rows)
+    np.testing.assert_array_equal(off_d, off_o)
+    np.testing.assert_array_equal(cols_d, cols_o)

@@ -48,7 +48,7 @@ def test_wire_segments_reassemble(oracle_mod, world, n_batch, num_columns):
     ns = [x[0] for x in sl]
     cap = max(int(x[3][0].item()) for x in sl) + 5
     lab_off = int(L.lib().mbrwt_wire_labels_offset(max(ns), bits_c))
-    per = _round16(lab_off + max(1, _words(cap, bits_l)) * 4)
+    per = _round16(lab_off + max(1, (cap + 31) // 32 * bits_l) * 4)
     recv = torch.full((world * per,), 0xAB, dtype=torch.uint8, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     for r, (nr, off, cols, st) in enumerate(sl):
@@ -57,7 +57,7 @@ def test_wire_segments_reassemble(oracle_mod, world, n_batch, num_columns):
                                               bits_l, lab_off, seg.data_ptr(), per, s), "pack")
     N = sum(ns)
     cnt = torch.zeros(max(1, N), dtype=torch.int32, device="cuda")
-    g_cols = torch.zeros(world * cap, dtype=torch.int32, device="cuda")
+    g_cols = torch.zeros(world * cap + 32, dtype=torch.int32, device="cuda")
     status = torch.full((2,), -1, dtype=torch.int64, device="cuda")
     arr = (C.c_uint64 * world)(*ns)
     L.check(L.lib().mbrwt_unpack_segments_device(recv.data_ptr() + 8, world, per, arr, bits_c, cnt.data_ptr(), s),
@@ -76,13 +76,13 @@ def test_wire_segments_reassemble(oracle_mod, world, n_batch, num_columns):
     small = min(int(x[3][0].item()) for x in sl if x[0] > 0)
     if small > 1:
         cap2 = small - 1
-        per2 = _round16(lab_off + max(1, _words(cap2, bits_l)) * 4)
+        per2 = _round16(lab_off + max(1, (cap2 + 31) // 32 * bits_l) * 4)
         recv2 = torch.zeros(world * per2, dtype=torch.uint8, device="cuda")
         for r, (nr, off, cols, st) in enumerate(sl):
             seg = recv2[r * per2:(r + 1) * per2]
             L.check(L.lib().mbrwt_pack_csr_device(off.data_ptr(), nr, cols.data_ptr(), st.data_ptr(), cap2, bits_c,
                                                   bits_l, lab_off, seg.data_ptr(), per2, s), "pack")
-        g2 = torch.full((world * cap2,), 7, dtype=torch.int32, device="cuda")
+        g2 = torch.full((world * cap2 + 32,), 7, dtype=torch.int32, device="cuda")
         L.check(L.lib().mbrwt_unpack_labels_device(recv2.data_ptr(), world, per2, lab_off, cap2, bits_l,
                                                    g2.data_ptr(), g2.numel(), status.data_ptr(), s), "unpack")
         torch.cuda.synchronize()
