@@ -73,29 +73,15 @@ __global__ __launch_bounds__(256) void k_unpack_segments(const uint8_t *__restri
 }
 
 // a rank's wire segment with its label count on the device (include/mbrwt.h
-// mbrwt_pack_csr_device).  Thread q packs values [32q, 32q + 32) of one
-// field into exactly `bits` words (32 values x bits bits), reading them as
-// 16-byte vectors: the row counts (deltas of 33 offsets) for q < cnt_chunks,
-// then the labels.  Values past the field's count are 0.
-__device__ __forceinline__ void pack32(const uint32_t (&v)[32], uint32_t bits, uint32_t *__restrict__ out) {
-    uint64_t acc = 0;
-    uint32_t have = 0, k = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < 32; ++i) {
-        acc |= (uint64_t)v[i] << have;
-        have += bits;
-        while (have >= 32) {
-            gst(out + k++, (uint32_t)acc);
-            acc >>= 32;
-            have -= 32;
-        }
-    }
-}
+// mbrwt_pack_csr_device): header, row counts from the offsets, labels; one
+// grid-stride pass over the count words and the label words, one output word
+// per thread (measured faster than 32-value chunks per thread with 16-byte
+// loads: 0.19 vs 0.24 ms for 8 M rows -- lanes 128 bytes apart coalesce badly)
 __global__ __launch_bounds__(256) void k_pack_csr(const uint64_t *__restrict__ offsets, uint64_t n_rows,
                                                   const uint32_t *__restrict__ cols,
                                                   const uint64_t *__restrict__ num_labels, uint64_t cap,
                                                   uint32_t bits_c, uint32_t bits_l, uint32_t *__restrict__ wire,
-                                                  uint64_t lab_word0, uint64_t cnt_chunks, uint64_t lab_chunks) {
+                                                  uint64_t lab_word0, uint64_t cnt_words, uint64_t lab_words) {
     const uint64_t L = gld(num_labels);
     const uint64_t nl = L < cap ? L : cap;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -103,38 +89,22 @@ __global__ __launch_bounds__(256) void k_pack_csr(const uint64_t *__restrict__ o
         gst(wire + 1, (uint32_t)(L >> 32));
     }
     const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
-    const uint32_t mc = bits_c == 32 ? 0xFFFFFFFFu : (1u << bits_c) - 1u;
-    const uint32_t ml = bits_l == 32 ? 0xFFFFFFFFu : (1u << bits_l) - 1u;
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < cnt_chunks + lab_chunks; q += gstride) {
-        uint32_t v[32];
-        if (q < cnt_chunks) {
-            const uint64_t i0 = 32 * q;
-            uint64_t prev = i0 < n_rows ? gld(offsets + i0) : 0;
-#pragma unroll
-            for (uint32_t i = 0; i < 32; ++i) {
-                const uint64_t nx = i0 + i < n_rows ? gld(offsets + i0 + i + 1) : prev;
-                v[i] = (uint32_t)(nx - prev) & mc;
-                prev = nx;
-            }
-            pack32(v, bits_c, wire + 2 + q * bits_c);
-        } else {
-            const uint64_t qq = q - cnt_chunks, i0 = 32 * qq;
-            if (i0 + 32 <= nl) {
-                const u32x4_t *src = reinterpret_cast<const u32x4_t *>(cols + i0);  // (cols: 16-byte aligned)
-#pragma unroll
-                for (uint32_t k = 0; k < 8; ++k) {
-                    const u32x4_t x = gld(src + k);
-                    v[4 * k] = x.x & ml;
-                    v[4 * k + 1] = x.y & ml;
-                    v[4 * k + 2] = x.z & ml;
-                    v[4 * k + 3] = x.w & ml;
-                }
-            } else {
-#pragma unroll
-                for (uint32_t i = 0; i < 32; ++i) v[i] = i0 + i < nl ? gld(cols + i0 + i) & ml : 0u;
-            }
-            pack32(v, bits_l, wire + lab_word0 + qq * bits_l);
+    const uint64_t total = cnt_words + lab_words;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gstride) {
+        const bool lab = k >= cnt_words;
+        const uint64_t kk = lab ? k - cnt_words : k;
+        const uint32_t bits = lab ? bits_l : bits_c;
+        const uint64_t n = lab ? nl : n_rows;
+        const uint32_t mask = bits == 32 ? 0xFFFFFFFFu : (1u << bits) - 1u;
+        const uint64_t b0 = 32 * kk, b1 = b0 + 32;
+        uint32_t w = 0;
+        for (uint64_t i = b0 / bits; i < n && i * bits < b1; ++i) {
+            const uint64_t pos = i * bits;
+            const uint32_t v = (lab ? gld(cols + i) : (uint32_t)(gld(offsets + i + 1) - gld(offsets + i))) & mask;
+            if (pos >= b0) w |= v << (pos - b0);
+            else w |= v >> (b0 - pos);
         }
+        gst(wire + (lab ? lab_word0 + kk : 2 + kk), w);
     }
 }
 
@@ -316,13 +286,10 @@ int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint
         set_error("wire segment too small for whole 32-value chunks");
         return MBRWT_ERR_INVALID;
     }
-    if (((uintptr_t)d_cols) % 16) {
-        set_error("cols must be 16-byte aligned");
-        return MBRWT_ERR_INVALID;
-    }
-    hipLaunchKernelGGL(k_pack_csr, dim3(grid_of(std::max<uint64_t>(1, cnt_chunks + lab_chunks))), dim3(256), 0, s,
+    const uint64_t cnt_words = (n_rows * bits_count + 31) / 32, lab_words_used = (labels_cap * bits_label + 31) / 32;
+    hipLaunchKernelGGL(k_pack_csr, dim3(grid_of(std::max<uint64_t>(1, cnt_words + lab_words_used))), dim3(256), 0, s,
                        d_offsets, n_rows, d_cols, d_num_labels, labels_cap, bits_count, bits_label,
-                       reinterpret_cast<uint32_t *>(d_wire), lab_off / 4, cnt_chunks, lab_chunks);
+                       reinterpret_cast<uint32_t *>(d_wire), lab_off / 4, cnt_words, lab_words_used);
     MBRWT_HIP(hipGetLastError());
     return MBRWT_OK;
 }

@@ -408,7 +408,7 @@ int mbrwt_unpack_segments_device(const void *d_base, uint32_t nseg, uint64_t seg
    at byte labels_offset (a multiple of 16, at least
    mbrwt_wire_labels_offset(n_rows, bits_count): every rank of an exchange
    uses the offset of the largest slice) and needs
-   ceil(labels_cap / 32) * bits_label words; d_cols 16-byte aligned.
+   ceil(labels_cap / 32) * bits_label words.
    MBRWT_ERR_INVALID when the layout does not fit wire_bytes. */
 uint64_t mbrwt_wire_labels_offset(uint64_t n_rows, uint32_t bits_count);
 int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint32_t *d_cols,
