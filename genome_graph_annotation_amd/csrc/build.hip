@@ -578,6 +578,14 @@ int desc_from_columns(const mbrwt_columns_desc &cd, int device, hipStream_t s, u
             }
         } else {
             const size_t L = level.size();
+            if ((uint64_t)L * (L - 1) / 2 > (1ull << 31)) {
+                // the reference keeps every pair as a candidate too
+                // (partitionings.cpp:154-160): > 2^31 pairs is > 50 GB of host
+                // candidates -- refuse instead of exhausting the host
+                cleanup();
+                set_error("greedy partitioner: more than 65,536 columns on one level");
+                return MBRWT_ERR_UNSUPPORTED;
+            }
             const auto t0 = std::chrono::steady_clock::now();
             // the level's columns (pointer table), the sampled words, the products
             std::vector<const uint64_t *> hp(L);
