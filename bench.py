@@ -360,7 +360,10 @@ def main():
         cap_t = torch.tensor([int(need * 1.02) + 1024], dtype=torch.int64, device=dev_t)
         dist.all_reduce(cap_t, op=dist.ReduceOp.MAX)
         rows_per_rank = [shard_bounds(G, world, r)[1] - shard_bounds(G, world, r)[0] for r in range(world)]
-        wire = DeviceAllGatherV(rows_per_rank, int(cap_t.item()), a.cols, dev_t, timing=True)
+        # 3 slots: up to 2 exchanges in flight behind the current step, so
+        # step k's pack + all-gather (RCCL stream) and step k-1's unpack (side
+        # stream) overlap instead of chaining through the main stream
+        wire = DeviceAllGatherV(rows_per_rank, int(cap_t.item()), a.cols, dev_t, timing=True, slots=3)
 
     # N > 1: steps are pipelined -- batch k's all-gatherv (RCCL stream) runs
     # while batch k+1 is traversed, so the outputs are double-buffered; drain()
@@ -369,7 +372,8 @@ def main():
     bufs = [(off_t, cols_t)]
     if gather:
         bufs.append((torch.empty_like(off_t), torch.empty_like(cols_t)))
-    state = {"i": 0, "pending": None, "global": None, "timed": False, "exchanges": [], "get_rows_host": []}
+    state = {"i": 0, "pending": None, "inflight": [], "global": None, "timed": False, "exchanges": [],
+             "get_rows_host": []}
 
     # N = 1: the asynchronous call (include/mbrwt.h mbrwt_get_rows_device_async:
     # no host synchronisation per step; the status block -- labels, status,
@@ -389,9 +393,11 @@ def main():
             if wire is not None:
                 # no host synchronisation: the label count travels from the
                 # status block on the device into the wire header
-                if state["pending"] is not None:
-                    state["global"] = wire.finish(state["pending"])
-                state["pending"] = wire.start(o, cb, status_t)
+                # finish the oldest exchange only when its slot comes round
+                # again (it then gates this step's pack on its unpack)
+                if len(state["inflight"]) == len(wire.slots) - 1:
+                    state["global"] = wire.finish(state["inflight"].pop(0))
+                state["inflight"].append(wire.start(o, cb, status_t))
             return None
         n_lab = mat.get_rows_device(rows_ts[i % K], o, cb, sptr)
         if state["timed"]:
@@ -406,8 +412,10 @@ def main():
         return n_lab
 
     def drain():
+        while state["inflight"]:
+            state["global"] = wire.finish(state["inflight"].pop(0))
         if state["pending"] is not None:
-            state["global"] = wire.finish(state["pending"]) if wire is not None else state["pending"].finish()
+            state["global"] = state["pending"].finish()
             state["pending"] = None
 
     for _ in range(a.warmup):

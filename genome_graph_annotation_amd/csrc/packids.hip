@@ -109,15 +109,18 @@ __global__ __launch_bounds__(256) void k_pack_csr(const uint64_t *__restrict__ o
 }
 
 // the labels of every segment, the segments' sizes from their headers.
-// Thread q writes global labels [32q, 32q + 32): when they lie in one
-// segment (nearly always), from bits + 1 consecutive words with 16-byte
-// stores; else label by label.
+// A workgroup writes global labels [2048 g, 2048 g + 2048): when they lie in
+// one segment (nearly always), their packed bits are staged in LDS by
+// coalesced word loads and every thread extracts labels t, t + 256, ...
+// (coalesced stores); else label by label.
+constexpr uint32_t kUnpackTile = 2048;
 __global__ __launch_bounds__(256) void k_unpack_labels_dev(const uint8_t *__restrict__ base, uint64_t stride,
                                                            uint32_t nseg, uint64_t lab_off, uint64_t cap,
                                                            uint32_t bits, uint32_t *__restrict__ out,
                                                            uint64_t out_cap, unsigned long long *status) {
     __shared__ uint64_t first[kMaxSegs + 1];
     __shared__ uint32_t bad;
+    __shared__ uint32_t stage[kUnpackTile + 2];  // (bits <= 32: at most 2048 + 1 words)
     if (threadIdx.x < 64) {  // the headers, one lane each, then a wave scan
         const uint32_t r = threadIdx.x;
         uint64_t L = 0;
@@ -148,46 +151,41 @@ __global__ __launch_bounds__(256) void k_unpack_labels_dev(const uint8_t *__rest
     __syncthreads();
     if (bad) return;
     const uint64_t N = first[nseg];
-    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
     const uint32_t mask = bits == 32 ? 0xFFFFFFFFu : (1u << bits) - 1u;
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; 32 * q < N; q += gstride) {
-        const uint64_t i0 = 32 * q;
+    for (uint64_t g = blockIdx.x; (uint64_t)kUnpackTile * g < N; g += gridDim.x) {
+        const uint64_t i0 = (uint64_t)kUnpackTile * g;
+        const uint64_t i1 = i0 + kUnpackTile < N ? i0 + kUnpackTile : N;
         uint32_t lo = 0, hi = nseg;  // the segment of label i0
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
             if (first[mid] <= i0) lo = mid;
             else hi = mid;
         }
-        if (i0 + 32 <= first[lo + 1]) {
-            const uint32_t *words = reinterpret_cast<const uint32_t *>(base + lo * stride + lab_off);
+        const uint32_t *words = reinterpret_cast<const uint32_t *>(base + lo * stride + lab_off);
+        if (i1 <= first[lo + 1]) {
             const uint64_t b0 = (i0 - first[lo]) * bits;
             const uint64_t w0 = b0 >> 5;
             const uint32_t sh = (uint32_t)(b0 & 31);
-            uint32_t v[32];
-            uint64_t acc = gld(words + w0) >> sh;
-            uint32_t have = 32 - sh, k = 1;
-#pragma unroll
-            for (uint32_t i = 0; i < 32; ++i) {
-                if (have < bits) {
-                    acc |= (uint64_t)gld(words + w0 + k++) << have;
-                    have += 32;
-                }
-                v[i] = (uint32_t)acc & mask;
-                acc >>= bits;
-                have -= bits;
+            const uint32_t nw = (uint32_t)(((i1 - i0) * bits + sh + 31) >> 5);
+            for (uint32_t k = threadIdx.x; k < nw; k += 256) stage[k] = gld(words + w0 + k);
+            __syncthreads();
+            for (uint32_t j = threadIdx.x; j < (uint32_t)(i1 - i0); j += 256) {
+                const uint32_t pos = sh + j * bits, w = pos >> 5, off = pos & 31;
+                uint32_t x = stage[w] >> off;
+                if (off + bits > 32) x |= stage[w + 1] << (32 - off);
+                gst(out + i0 + j, x & mask);
             }
-            u32x4_t *dst = reinterpret_cast<u32x4_t *>(out + i0);  // (out: 16-byte aligned, i0 % 32 == 0)
-#pragma unroll
-            for (uint32_t k2 = 0; k2 < 8; ++k2) gst(dst + k2, u32x4_t{v[4 * k2], v[4 * k2 + 1], v[4 * k2 + 2], v[4 * k2 + 3]});
+            __syncthreads();  // the stage is refilled for the next tile
         } else {
-            for (uint64_t i = i0; i < i0 + 32 && i < N; ++i) {
-                while (lo + 1 < nseg && first[lo + 1] <= i) ++lo;
-                const uint32_t *words = reinterpret_cast<const uint32_t *>(base + lo * stride + lab_off);
-                const uint64_t pos = (i - first[lo]) * bits;
+            for (uint64_t i = i0 + threadIdx.x; i < i1; i += 256) {
+                uint32_t s2 = lo;
+                while (s2 + 1 < nseg && first[s2 + 1] <= i) ++s2;
+                const uint32_t *wd = reinterpret_cast<const uint32_t *>(base + s2 * stride + lab_off);
+                const uint64_t pos = (i - first[s2]) * bits;
                 const uint64_t w = pos >> 5;
                 const uint32_t off = (uint32_t)(pos & 31);
-                uint32_t x = gld(words + w) >> off;
-                if (off + bits > 32) x |= gld(words + w + 1) << (32 - off);
+                uint32_t x = gld(wd + w) >> off;
+                if (off + bits > 32) x |= gld(wd + w + 1) << (32 - off);
                 gst(out + i, x & mask);
             }
         }
@@ -302,12 +300,9 @@ int mbrwt_unpack_labels_device(const void *d_base, uint32_t nseg, uint64_t seg_s
         set_error("invalid argument");
         return MBRWT_ERR_INVALID;
     }
-    if (((uintptr_t)d_values) % 16) {
-        set_error("values must be 16-byte aligned");
-        return MBRWT_ERR_INVALID;
-    }
     const uint64_t bound = std::min<uint64_t>(values_cap, (uint64_t)nseg * labels_cap);
-    hipLaunchKernelGGL(k_unpack_labels_dev, dim3(grid_of(std::max<uint64_t>(1, (bound + 31) / 32))), dim3(256), 0,
+    const unsigned tiles = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((bound + kUnpackTile - 1) / kUnpackTile, 8192));
+    hipLaunchKernelGGL(k_unpack_labels_dev, dim3(tiles), dim3(256), 0,
                        (hipStream_t)stream, reinterpret_cast<const uint8_t *>(d_base), seg_stride, nseg, labels_offset,
                        labels_cap, bits, d_values, values_cap, reinterpret_cast<unsigned long long *>(d_status));
     MBRWT_HIP(hipGetLastError());

@@ -419,8 +419,7 @@ int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint
    bytes), written back to back in segment order: the segments' label counts
    and their prefix are read from the headers ON THE DEVICE.  d_status[0] =
    the total, d_status[1] = 0, or 1 when a header exceeds labels_cap or the
-   total exceeds values_cap (nothing is written then); d_values 16-byte
-   aligned, with room for the total rounded up to 32. */
+   total exceeds values_cap (nothing is written then). */
 int mbrwt_unpack_labels_device(const void *d_base, uint32_t nseg, uint64_t seg_stride, uint64_t labels_offset,
                                uint64_t labels_cap, uint32_t bits, uint32_t *d_values, uint64_t values_cap,
                                uint64_t *d_status, void *stream);
