@@ -1666,7 +1666,8 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows3(RowsParams p) {
     const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows3[0]);
     const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows3 + 4;
     const uint32_t C = p.C;
-    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows3 + ((p.table_words + 3) & ~3u)) + wv * (64u * B + 256u * p.stk_words);
+    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows3 + ((p.table_words + 3) & ~3u)) +
+                         wv * (64u * B + 256u * p.stk_words + (p.stage ? 2u * p.C : 0u));
     AS_LDS uint8_t *mine = wb + lane * B;
     AS_LDS uint32_t *stk = (AS_LDS uint32_t *)(wb + 64u * B) + lane;
     const uint64_t ntiles = (p.n + 63) / 64;
@@ -1765,7 +1766,33 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows3(RowsParams p) {
         uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
         if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
         if (!direct && !(p.diag & 1)) {
-            if (p.walk4 == 3)
+            if (p.walk4 == 4) {  // the odometer (uniform trees), LDS label stage or direct stores
+                const bool live = valid && cnt > 0;
+                AS_LDS uint16_t *stage = (AS_LDS uint16_t *)(wb + 64u * B + 256u * p.stk_words);
+                AS_GLOBAL uint16_t *out = (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128);
+                if (p.stage) {
+                    switch (p.uni) {
+                        case 1: rows_walk_uni<1>(mine, o, live, root, ent, stage, pos); break;
+                        case 2: rows_walk_uni<2>(mine, o, live, root, ent, stage, pos); break;
+                        case 3: rows_walk_uni<3>(mine, o, live, root, ent, stage, pos); break;
+                        case 4: rows_walk_uni<4>(mine, o, live, root, ent, stage, pos); break;
+                        default: rows_walk_uni<5>(mine, o, live, root, ent, stage, pos); break;
+                    }
+                    wave_sync();
+                    const uint32_t nbytes = total * 2;
+                    for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
+                        gst(reinterpret_cast<u32x4_t *>(treg + 128 + q2),
+                            *(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2));
+                } else {
+                    switch (p.uni) {
+                        case 1: rows_walk_uni<1>(mine, o, live, root, ent, out, pos); break;
+                        case 2: rows_walk_uni<2>(mine, o, live, root, ent, out, pos); break;
+                        case 3: rows_walk_uni<3>(mine, o, live, root, ent, out, pos); break;
+                        case 4: rows_walk_uni<4>(mine, o, live, root, ent, out, pos); break;
+                        default: rows_walk_uni<5>(mine, o, live, root, ent, out, pos); break;
+                    }
+                }
+            } else if (p.walk4 == 3)
                 rows_walk6(mine, o, valid && cnt > 0, root, ent, stk,
                            (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128), pos);
             else if (p.walk4 == 2)
