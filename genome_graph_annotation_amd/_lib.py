@@ -24,6 +24,7 @@ MBRWT_ERR_NOMEM = 6
 MBRWT_OPT_TIMING = 1
 MBRWT_OPT_SLOT_LABELS = 2
 MBRWT_OPT_KERNEL = 4
+MBRWT_OPT_ROWS_WALK = 8
 
 MBRWT_BUILD_LAYOUT = 1
 MBRWT_BUILD_PARTITIONER = 2
@@ -126,12 +127,13 @@ SIGNATURES = {
     "mbrwt_unpack_segments_device": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64, u64p, C.c_uint32, C.c_void_p,
                                                C.c_void_p]),
     "mbrwt_wire_labels_offset": (C.c_uint64, [C.c_uint64, C.c_uint32]),
-    "mbrwt_pack_csr_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
+    "mbrwt_pack_csr_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint32,
                                         C.c_uint32, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]),
     "mbrwt_unpack_labels_device": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32,
                                              C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
     "mbrwt_destroy": (None, [C.c_void_p]),
     "mbrwt_set_build_option": (C.c_int, [C.c_int, C.c_int64]),
+    "mbrwt_get_build_option": (C.c_int, [C.c_int, C.POINTER(C.c_int64)]),
     "mbrwt_multi_create": (C.c_int, [C.POINTER(TreeDesc), C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_void_p)]),
     "mbrwt_multi_create_synthetic": (C.c_int, [C.POINTER(SynthDesc), C.POINTER(C.c_int), C.c_int,
                                                C.POINTER(C.c_void_p)]),

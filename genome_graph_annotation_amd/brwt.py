@@ -141,12 +141,22 @@ def build_layout(layout):
     if layout is None:
         yield
         return
+    with build_option(L.MBRWT_BUILD_LAYOUT, L.LAYOUTS[layout]):
+        yield
+
+
+@contextlib.contextmanager
+def build_option(option, value):
+    """mbrwt_set_build_option for the block; the calling thread's previous
+    value is restored afterwards (mbrwt_get_build_option)."""
     lib = L.lib()
-    L.check(lib.mbrwt_set_build_option(L.MBRWT_BUILD_LAYOUT, L.LAYOUTS[layout]), "mbrwt_set_build_option")
+    prev = C.c_int64(0)
+    L.check(lib.mbrwt_get_build_option(option, C.byref(prev)), "mbrwt_get_build_option")
+    L.check(lib.mbrwt_set_build_option(option, int(value)), "mbrwt_set_build_option")
     try:
         yield
     finally:
-        lib.mbrwt_set_build_option(L.MBRWT_BUILD_LAYOUT, 0)
+        lib.mbrwt_set_build_option(option, prev.value)
 
 
 class BRWTDevice:
@@ -221,18 +231,12 @@ class BRWTDevice:
             ptrs[j] = c.ctypes.data_as(L.u64p)
         d = L.ColumnsDesc(num_rows, len(cols), ptrs, arity)
         h = C.c_void_p()
-        L.check(lib.mbrwt_set_build_option(L.MBRWT_BUILD_PARTITIONER, L.PARTITIONERS[partitioner]),
-                "mbrwt_set_build_option")
-        try:
-            with build_layout(layout):
-                if relax_max_arity:
-                    L.check(lib.mbrwt_create_from_columns_relaxed(C.byref(d), int(relax_max_arity), device,
-                                                                  C.byref(h)), "mbrwt_create_from_columns_relaxed")
-                else:
-                    L.check(lib.mbrwt_create_from_columns(C.byref(d), device, C.byref(h)),
-                            "mbrwt_create_from_columns")
-        finally:
-            lib.mbrwt_set_build_option(L.MBRWT_BUILD_PARTITIONER, 0)
+        with build_option(L.MBRWT_BUILD_PARTITIONER, L.PARTITIONERS[partitioner]), build_layout(layout):
+            if relax_max_arity:
+                L.check(lib.mbrwt_create_from_columns_relaxed(C.byref(d), int(relax_max_arity), device,
+                                                              C.byref(h)), "mbrwt_create_from_columns_relaxed")
+            else:
+                L.check(lib.mbrwt_create_from_columns(C.byref(d), device, C.byref(h)), "mbrwt_create_from_columns")
         return cls(h)
 
     @classmethod

@@ -169,10 +169,13 @@ class BRWTDevice : public BinaryMatrix {
     // the reference's production build (scripts/kingsford/convert.sh:24)
     static BRWTDevice build_greedy(const std::vector<std::vector<uint64_t>> &columns, uint64_t num_rows,
                                    int device = 0, uint64_t relax_max_arity = 0) {
+        int64_t prev = MBRWT_PARTITIONER_BASIC;
+        check_status(mbrwt_get_build_option(MBRWT_BUILD_PARTITIONER, &prev), "build option");
         check_status(mbrwt_set_build_option(MBRWT_BUILD_PARTITIONER, MBRWT_PARTITIONER_GREEDY), "build option");
-        struct Reset {
-            ~Reset() { (void)mbrwt_set_build_option(MBRWT_BUILD_PARTITIONER, MBRWT_PARTITIONER_BASIC); }
-        } reset_;
+        struct Restore {  // the caller's own setting, not a fixed value
+            int64_t v;
+            ~Restore() { (void)mbrwt_set_build_option(MBRWT_BUILD_PARTITIONER, v); }
+        } restore_{prev};
         return build_bottom_up(columns, num_rows, 2, device, relax_max_arity);
     }
 

@@ -71,10 +71,7 @@ static void release(Ctx *c) {
     (void)hipSetDevice(c->device);
     free_tree(c->tree);
     free_rows(c->rows);
-    if (c->side) (void)hipStreamDestroy(c->side);
-    if (c->sev_a) (void)hipEventDestroy(c->sev_a);
-    if (c->sev_b) (void)hipEventDestroy(c->sev_b);
-    for (Workspace *w : {&c->ws_temp, &c->ws_counts, &c->ws_ovf, &c->ws_scan, &c->ws_scan2, &c->ws_rows, &c->ws_out, &c->ws_sort,
+    for (Workspace *w : {&c->ws_temp, &c->ws_counts, &c->ws_ovf, &c->ws_scan, &c->ws_rows, &c->ws_out, &c->ws_sort,
                          &c->ws_cls_off, &c->ws_cls_cols, &c->ws_sh_keys, &c->ws_sh_local, &c->ws_sh_cnt,
                          &c->ws_sh_sort, &c->ws_sh_tmp})
         if (w->buf) (void)hipFree(w->buf);
@@ -480,6 +477,15 @@ int mbrwt_set_build_option(int option, int64_t value) {
     return MBRWT_OK;
 }
 
+int mbrwt_get_build_option(int option, int64_t *value) {
+    if (!value || (option != MBRWT_BUILD_LAYOUT && option != MBRWT_BUILD_PARTITIONER)) {
+        set_error("unknown build option or null output");
+        return MBRWT_ERR_INVALID;
+    }
+    *value = option == MBRWT_BUILD_LAYOUT ? thread_build_layout() : build_partitioner();
+    return MBRWT_OK;
+}
+
 int mbrwt_layout(const mbrwt_ctx *ctx) {
     if (!ctx) return 0;
     const Ctx &c = *C(ctx);
@@ -836,8 +842,13 @@ static int apply_option(Ctx &c, int option, int64_t value) {
         if (value < 0 || value > 4096) return MBRWT_ERR_INVALID;
         c.slot_labels = (uint32_t)value;
         return MBRWT_OK;
+    case MBRWT_OPT_ROWS_WALK:
+        if (value != 0 && value != 6) return MBRWT_ERR_INVALID;
+        c.rows_walk = (int)value;
+        return MBRWT_OK;
     case MBRWT_OPT_KERNEL:
-        if (!(value >= 0 && value <= 6) && value != 10 && !(value >= 17 && value <= 30)) return MBRWT_ERR_INVALID;
+        if (!(value >= 0 && value <= 6) && value != 10 && !(value >= 17 && value <= 20) && !(value >= 24 && value <= 30))
+            return MBRWT_ERR_INVALID;
         c.kernel_variant = (int)value;
         return MBRWT_OK;
     default:

@@ -263,6 +263,7 @@ struct RowsImage {
     bool mask1 = false;             // every internal node (leaf parents too) has arity <= 8: one-byte masks
     uint32_t uni = 0;               // K internal levels above leaf parents on every path (rows_walk_uni), else 0
     uint64_t bytes = 0;             // blocks + spill used
+    uint32_t occ_cap = 0;           // workgroups per CU of k_traverse_rows (0 = the default; MBRWT_ROWS_WGS_PER_CU)
     // build statistics
     uint64_t spilled_rows = 0, long_rows = 0, record_bytes = 0, spill_bytes = 0;
 };
@@ -274,6 +275,7 @@ uint32_t rwt2_uniform_levels(const std::vector<uint32_t> &table2);
 // the thread's build layout (mbrwt_set_build_option, else MBRWT_LAYOUT)
 int build_layout();
 void set_build_layout(int layout);
+int thread_build_layout();  // the value set for the calling thread (AUTO when unset)
 
 // Cross-stream ordering of a context's workspaces.  A *_device call returns
 // with work still queued on the caller's stream that reads the context's
@@ -330,9 +332,6 @@ struct Ctx {
     // reusable device workspace (grown on demand, never inside a timed call
     // once warmed up)
     Workspace ws_temp, ws_counts, ws_ovf, ws_scan, ws_rows, ws_out, ws_sort;
-    Workspace ws_scan2;                 // row records: the first half's scan (split batches)
-    hipStream_t side = nullptr;         // row records: the first half's compaction (split batches)
-    hipEvent_t sev_a = nullptr, sev_b = nullptr;
     Workspace ws_cls_off, ws_cls_cols;  // get_labels batch: the rows' CSR
     uint64_t *h_scalars = nullptr;      // pinned: [0] total, [1] overflow count, [2] error
     uint64_t *d_scalars = nullptr;      // device twin
@@ -341,6 +340,7 @@ struct Ctx {
     bool timing = false;
     uint32_t slot_labels = 0;           // 0 = auto
     int kernel_variant = 0;             // MBRWT_OPT_KERNEL (0 = default = 5)
+    int rows_walk = 0;                  // MBRWT_OPT_ROWS_WALK (6: the non-odometer walk on uniform trees)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double timing_ms = 0;
     uint64_t timing_launches = 0;

@@ -78,16 +78,23 @@ __global__ __launch_bounds__(256) void k_unpack_segments(const uint8_t *__restri
 // per thread (measured faster than 32-value chunks per thread with 16-byte
 // loads: 0.19 vs 0.24 ms for 8 M rows -- lanes 128 bytes apart coalesce badly)
 __global__ __launch_bounds__(256) void k_pack_csr(const uint64_t *__restrict__ offsets, uint64_t n_rows,
-                                                  const uint32_t *__restrict__ cols,
+                                                  const uint32_t *__restrict__ cols, uint64_t cols_cap,
                                                   const uint64_t *__restrict__ num_labels, uint64_t cap,
                                                   uint32_t bits_c, uint32_t bits_l, uint32_t *__restrict__ wire,
                                                   uint64_t lab_word0, uint64_t cnt_words, uint64_t lab_words) {
     const uint64_t L = gld(num_labels);
-    const uint64_t nl = L < cap ? L : cap;
+    // more labels than the rank's own CSR holds: its get_rows failed with
+    // MBRWT_ERR_CAPACITY and left the CSR unwritten -- the header carries a
+    // count over every capacity (the unpack flags the exchange) and nothing
+    // is read from the CSR
+    const bool lost = L > cols_cap;
+    const uint64_t nl = lost ? 0 : L < cap ? L : cap;
+    const uint64_t hdr = lost ? ~0ull : L;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        gst(wire, (uint32_t)L);
-        gst(wire + 1, (uint32_t)(L >> 32));
+        gst(wire, (uint32_t)hdr);
+        gst(wire + 1, (uint32_t)(hdr >> 32));
     }
+    if (lost) return;
     const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t total = cnt_words + lab_words;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gstride) {
@@ -259,11 +266,11 @@ uint64_t mbrwt_wire_labels_offset(uint64_t n_rows, uint32_t bits_count) {
     return (8 + (n_rows + 31) / 32 * bits_count * 4 + 15) / 16 * 16;  // (whole 32-value chunks)
 }
 
-int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint32_t *d_cols,
+int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint32_t *d_cols, uint64_t cols_cap,
                           const uint64_t *d_num_labels, uint64_t labels_cap, uint32_t bits_count, uint32_t bits_label,
                           uint64_t labels_offset, void *d_wire, uint64_t wire_bytes, void *stream) {
     if (bits_count < 1 || bits_count > 32 || bits_label < 1 || bits_label > 32 || !d_wire || !d_num_labels ||
-        (n_rows && !d_offsets) || (labels_cap && !d_cols) || wire_bytes % 16 || labels_offset % 16 ||
+        (n_rows && !d_offsets) || (cols_cap && !d_cols) || wire_bytes % 16 || labels_offset % 16 ||
         labels_offset < mbrwt_wire_labels_offset(n_rows, bits_count)) {
         set_error("invalid argument");
         return MBRWT_ERR_INVALID;
@@ -286,7 +293,7 @@ int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint
     }
     const uint64_t cnt_words = (n_rows * bits_count + 31) / 32, lab_words_used = (labels_cap * bits_label + 31) / 32;
     hipLaunchKernelGGL(k_pack_csr, dim3(grid_of(std::max<uint64_t>(1, cnt_words + lab_words_used))), dim3(256), 0, s,
-                       d_offsets, n_rows, d_cols, d_num_labels, labels_cap, bits_count, bits_label,
+                       d_offsets, n_rows, d_cols, cols_cap, d_num_labels, labels_cap, bits_count, bits_label,
                        reinterpret_cast<uint32_t *>(d_wire), lab_off / 4, cnt_words, lab_words_used);
     MBRWT_HIP(hipGetLastError());
     return MBRWT_OK;

@@ -1069,12 +1069,10 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// PF: software pipeline -- the 64-byte block of a group's NEXT visit (the
-// next round's item, or the root block of the next rowblock's row) is
-// requested before the current one is processed, so its latency overlaps the
-// current record walk.  OCC: the waves per SIMD the register budget targets.
-template <bool NT, bool PF, int OCC, typename LT = uint32_t>
-__global__ __launch_bounds__(256, OCC) void k_traverse_p2w(P2wParams p) {
+// (A register prefetch of a group's next block measured +1 % at 8 waves per
+// SIMD and -7 % at 6: removed)
+template <bool NT, typename LT = uint32_t>
+__global__ __launch_bounds__(256, 8) void k_traverse_p2w(P2wParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_p2w[];
     const uint32_t lane = threadIdx.x & 63, c = lane & 3, g = lane >> 2, gb = lane & ~3u;
     // wave-uniform values are made scalar (SGPRs): VGPRs are the occupancy limit
@@ -1127,12 +1125,6 @@ __global__ __launch_bounds__(256, OCC) void k_traverse_p2w(P2wParams p) {
     };
 
     uint64_t rb = (uint64_t)blockIdx.x * 4 + wv;
-    uint32_t row_n = 0;          // PF: the group's row in the wave's next rowblock
-    uint4 qn = make_uint4(0, 0, 0, 0);  // PF: the block of the group's next visit
-    if constexpr (PF) {
-        row_n = load_row(rb);
-        qn = root_load(row_n);
-    }
     for (; rb < nblocks; rb += wstride) {
         const uint64_t r0 = rb * 16;
         const uint32_t nr = (uint32_t)(p.n - r0 < 16 ? p.n - r0 : 16);
@@ -1141,16 +1133,8 @@ __global__ __launch_bounds__(256, OCC) void k_traverse_p2w(P2wParams p) {
         LT *const out = reinterpret_cast<LT *>(p.temp) + rb * (uint64_t)p.C;
 
         // ---- root phase: the super-root's block at group g's row ----
-        uint32_t row;
-        uint4 qr;
-        if constexpr (PF) {
-            row = row_n;
-            qr = qn;
-            row_n = load_row(rb + wstride);
-        } else {
-            row = load_row(rb);
-            qr = root_load(row);
-        }
+        const uint32_t row = load_row(rb);
+        const uint4 qr = root_load(row);
         uint32_t P = 0, j0 = 0, j1 = 0;
         if (row != kNone && 2 * c < R) {
             const uint32_t t = row & 31, below = (1u << t) - 1u;
@@ -1183,20 +1167,13 @@ __global__ __launch_bounds__(256, OCC) void k_traverse_p2w(P2wParams p) {
         }
         wave_sync_lds();
         const uint32_t T = __builtin_amdgcn_readfirstlane(gfirst[16]);
-        if constexpr (PF) qn = T > 0 ? item_load(g, T) : root_load(row_n);
 
         // ---- rounds: group g resolves item ib + g ----
         uint32_t running = 0, flushed = 0;  // wave-uniform label positions in the rowblock
         for (uint32_t ib = 0; ib < T; ib += 16) {
             const uint32_t i = ib + g;
             const bool act = i < T;
-            uint4 q;
-            if constexpr (PF) {
-                q = qn;
-                qn = ib + 16 < T ? item_load(i + 16, T) : root_load(row_n);
-            } else {
-                q = item_load(i, T);
-            }
+            const uint4 q = item_load(i, T);
             uint32_t j = 0, k = 0;
             if (act) {
                 j = items_j[i];
@@ -2083,24 +2060,19 @@ int ensure(Workspace &w, size_t bytes) {
 }
 
 // k_traverse_p2w for this context?  Default for trees with a P2W table;
-// MBRWT_OPT_KERNEL 19..23 pick a configuration (A/B; 17 / 18 force
-// k_traverse_fast2): 19 plain reads, 20 non-temporal reads, 21 non-temporal +
-// prefetch, 22 the same at 6 waves per SIMD, 23 non-temporal at 7 waves.
+// MBRWT_OPT_KERNEL 19 / 20 force plain / non-temporal reads (A/B; 17 / 18
+// force k_traverse_fast2).
 using P2wFn = void (*)(P2wParams);
 static P2wFn p2w_kernel(const Ctx &c) {
     const int kv = c.kernel_variant;
-    if (c.tree.p2w_table.empty() || !c.d_p2w || !(kv == 0 || (kv >= 19 && kv <= 23))) return nullptr;
+    if (c.tree.p2w_table.empty() || !c.d_p2w || !(kv == 0 || kv == 19 || kv == 20)) return nullptr;
     const bool big = c.tree.image_bytes > (1ull << 30);
     switch (kv) {
-    case 19: return k_traverse_p2w<false, false, 8>;
-    case 20: return k_traverse_p2w<true, false, 8>;
-    case 21: return k_traverse_p2w<true, true, 8>;
-    case 22: return k_traverse_p2w<true, true, 6>;
-    case 23: return k_traverse_p2w<true, false, 7>;
-    default:  // (PF: +1 %, 21); u16 temp labels when they fit (p2w_label16)
-        if (c.tree.num_columns <= 0x10000u)
-            return big ? k_traverse_p2w<true, false, 8, uint16_t> : k_traverse_p2w<false, false, 8, uint16_t>;
-        return big ? k_traverse_p2w<true, false, 8> : k_traverse_p2w<false, false, 8>;
+    case 19: return k_traverse_p2w<false>;
+    case 20: return k_traverse_p2w<true>;
+    default:  // u16 temp labels when they fit (p2w_label16)
+        if (c.tree.num_columns <= 0x10000u) return big ? k_traverse_p2w<true, uint16_t> : k_traverse_p2w<false, uint16_t>;
+        return big ? k_traverse_p2w<true> : k_traverse_p2w<false>;
     }
 }
 

@@ -26,8 +26,9 @@
 // row's labels, the 64 lanes walk their records in lockstep over the RWT table
 // writing u16 labels into an LDS stage, which leaves as full-line stores into
 // the tile's temp region; one scan over the tile totals and k_compact_tiles
-// (u16 -> the caller's u32 CSR) follow.  Tiles with more labels than their
-// region, or with a record longer than a block, go to k_rows_direct.
+// (u16 -> the caller's u32 CSR, the call's status) follow.  Tiles with more
+// labels than their region, or with a record longer than a block, are walked
+// by k_compact_tiles itself from the records in global memory.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -44,10 +45,10 @@ namespace mbrwt {
 // ------------------------------------------------------------------------
 // layout selection
 // ------------------------------------------------------------------------
-static thread_local int g_build_layout = -1;  // -1: MBRWT_LAYOUT or auto
+static thread_local int g_build_layout = LAYOUT_AUTO;  // AUTO: MBRWT_LAYOUT, else the automatic choice
 
 int build_layout() {
-    if (g_build_layout >= 0) return g_build_layout;
+    if (g_build_layout != LAYOUT_AUTO) return g_build_layout;
     const char *e = std::getenv("MBRWT_LAYOUT");
     if (!e || !*e) return LAYOUT_AUTO;
     if (!std::strcmp(e, "nodes")) return LAYOUT_NODES;
@@ -57,6 +58,7 @@ int build_layout() {
 }
 
 void set_build_layout(int layout) { g_build_layout = layout; }
+int thread_build_layout() { return g_build_layout; }
 
 // ------------------------------------------------------------------------
 // RWT table
@@ -722,6 +724,12 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
     unsigned long long used = 0;
     MBRWT_HIP(hipMemcpyAsync(&used, im.d_spill_used, sizeof(used), hipMemcpyDeviceToHost, rb.s));
     MBRWT_HIP(hipStreamSynchronize(rb.s));
+    // a spilled entry stores its offset as u32 16-byte units: the spill area
+    // addresses 64 GiB
+    if (used + o[1] >= (1ull << 32)) {
+        set_error("row-record spill area beyond 64 GiB");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
     // the first range sizes the area for the whole image (extrapolated)
     const double scale = row0 == 0 ? (double)rb.n / (double)nr : 1.0;
     if (int rc = ensure_spill(rb, (uint64_t)(used * 16 + o[1] * 16 * scale * (row0 == 0 ? 1.05 : 1.0)) + 16 * o[1]))
@@ -760,6 +768,8 @@ int rows_build_finish(RowsBuild *rbp) {
         return MBRWT_ERR_NOMEM;
     }
     im.bytes = im.num_blocks * im.B + im.spill_bytes;
+    if (const char *e = std::getenv("MBRWT_ROWS_WGS_PER_CU"))  // occupancy sweeps (read once per image)
+        im.occ_cap = (uint32_t)std::max(0, std::atoi(e));
     im.ready = true;
     free_rows(rb.top->rows);
     rb.top->rows = im;
@@ -848,6 +858,9 @@ __device__ bool rwt_walk(const uint32_t *ntab, const uint16_t *etab, ByteFn byte
     return true;
 }
 
+// walk families of k_traverse_rows (RowsImage::walk)
+enum : uint32_t { WALK_GENERAL = 0, WALK_MASK1 = 1, WALK_ODOMETER = 2 };
+
 struct RowsParams {
     const uint64_t *rows;
     uint64_t n;
@@ -855,19 +868,14 @@ struct RowsParams {
     uint64_t blocks, spill, magic;
     uint32_t S;
     uint32_t table_words;
-    const uint32_t *table;
+    const uint32_t *table;        // RWT2
     uint32_t C;                   // labels per tile region (multiple of 64)
     uint8_t *temp;                // tiles x (128 + 2 C) bytes: u16 counts[64], u16 labels[C]
     uint32_t *tile_counts;        // [tiles] labels (bit 31: the tile goes to the direct pass)
-    uint32_t *ovf_list;           // batch indices of the rows of direct tiles
-    unsigned long long *scalars;  // [1] direct rows, [2] error flags
-    uint32_t walk4;               // 1: rows_walk4 (default), 2: rows_walk5 (MBRWT_ROWS_WALK=5), 0: rows_walk2 (=2)
-    uint32_t stk_words;           // per-lane LDS stack slots of the v2/v3 kernels (rows_stack_words)
-    uint32_t uni;                 // walk 4 (rows_walk_uni): the tree's internal levels K (1..5)
-    uint32_t stage;               // v2 + walk 6: labels staged in LDS, stored as 16-byte vectors
-    uint64_t row_base;            // batch index of p.rows[0] (the direct list holds batch indices)
-    uint32_t diag;                // MBRWT_ROWS_DIAG (timing experiments; WRONG results): 1 no walk,
-                                  // 2 walk without label stores, 4 no spill reads
+    unsigned long long *scalars;  // the kernel's counters: [2] error flags (bit 0: row out of range)
+    unsigned long long *status;   // the call's {needed, status, sticky}: status is reset here
+    uint32_t uni;                 // the odometer: the tree's internal levels K (1..5)
+    uint32_t stk_words;           // per-lane LDS stack slots (general walks)
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -876,239 +884,17 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// The walk of every lane's record at once, in lockstep without per-lane
-// branches: each iteration takes one child of every lane's top frame (frame
-// = first entry | pending children << 16); a leaf stores its column into the
-// stage at the lane's next label position, an internal child reads its mask
-// (the record's next 1 or 2 bytes) and pushes the parent's frame if it has
-// children left; an emptied frame is popped.  MAXD >= the tree's height.
-template <int MAXD>
-__device__ __forceinline__ void rows_walk_wave(const AS_LDS uint8_t *pb, uint32_t o, bool live,
-                                               const AS_LDS uint32_t *ntab, const AS_LDS uint16_t *etab,
-                                               AS_LDS uint16_t *stage, uint32_t pos) {
-    const uint32_t nw = ntab[0];
-    const uint32_t w0 = ((nw >> 16) & 0xFFu) > 8 ? 1u : 0u;
-    const uint32_t m = (uint32_t)pb[o] | (w0 ? (uint32_t)pb[o + 1] << 8 : 0u);
-    o += 1 + w0;
-    uint32_t top = live ? ((nw & 0xFFFFu) | (m << 16)) : 0u;
-    uint32_t st[MAXD > 1 ? MAXD - 1 : 1];
-#pragma unroll
-    for (int k = 0; k < (MAXD > 1 ? MAXD - 1 : 1); ++k) st[k] = 0;
-    uint32_t sp = 0;
-    bool done = (top >> 16) == 0;
-    while (__any(!done)) {
-        const uint32_t mm = top >> 16;
-        const uint32_t c = (uint32_t)__builtin_ctz(mm | 0x10000u);
-        top &= ~(0x10000u << c);
-        const uint32_t e = etab[done ? 0u : (top & 0xFFFFu) + c];
-        const bool leaf = (e & 0x8000u) != 0;
-        if (!done && leaf) stage[pos] = (uint16_t)(e & 0x7FFFu);
-        pos += (!done && leaf) ? 1u : 0u;
-        const bool inner = !done && !leaf;
-        const uint32_t nw2 = ntab[inner ? e : 0u];
-        const uint32_t w2 = ((nw2 >> 16) & 0xFFu) > 8 ? 1u : 0u;
-        const uint32_t mw = (uint32_t)pb[o] | (w2 ? (uint32_t)pb[o + 1] << 8 : 0u);
-        o += inner ? 1u + w2 : 0u;
-        if constexpr (MAXD > 1) {
-            const bool push = inner && (top >> 16) != 0;
-#pragma unroll
-            for (int k = MAXD - 2; k > 0; --k) st[k] = push ? st[k - 1] : st[k];
-            st[0] = push ? top : st[0];
-            sp += push ? 1u : 0u;
-        }
-        top = inner ? ((nw2 & 0xFFFFu) | (mw << 16)) : top;
-        if constexpr (MAXD > 1) {
-            const bool pop = !done && (top >> 16) == 0 && sp > 0;  // (pushed frames are never empty)
-            top = pop ? st[0] : top;
-#pragma unroll
-            for (int k = 0; k < MAXD - 2; ++k) st[k] = pop ? st[k + 1] : st[k];
-            sp -= pop ? 1u : 0u;
-        }
-        done = done || (top >> 16) == 0;
-    }
-}
-
-// k_traverse_rows: one wave per tile of 64 query rows (file comment).
-// B: block bytes; MAXD: stack levels (>= height); WPB: waves per workgroup
-// (the RWT table is staged once per workgroup; the grid is persistent).
-template <int B, int MAXD, int WPB, bool NT>
-__global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows[];
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_rows[i] = gld(p.table + i);
-    __syncthreads();
-    const AS_LDS uint32_t *tab = (const AS_LDS uint32_t *)lds_rows;
-    const uint32_t nI = __builtin_amdgcn_readfirstlane(tab[0]);
-    const AS_LDS uint32_t *ntab = tab + 4;
-    const AS_LDS uint16_t *etab = (const AS_LDS uint16_t *)(ntab + nI);
-    const uint32_t C = p.C;
-    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows + ((p.table_words + 3) & ~3u)) + wv * (64u * B + 2u * C);
-    AS_LDS uint8_t *mine = wb + lane * B;
-    AS_LDS uint16_t *stage = (AS_LDS uint16_t *)(wb + 64 * B);
-    constexpr uint32_t LPB = B / 16, RPI = 64 / LPB;
-    const uint64_t ntiles = (p.n + 63) / 64;
-    const uint64_t tstride = (uint64_t)gridDim.x * WPB;
-    const uint32_t S = p.S;
-    for (uint64_t t = (uint64_t)blockIdx.x * WPB + wv; t < ntiles; t += tstride) {
-        const uint64_t r0 = t * 64;
-        const uint32_t nr = (uint32_t)(p.n - r0 < 64 ? p.n - r0 : 64);
-        bool valid = false;
-        uint64_t row = 0;
-        if (lane < nr) {
-            row = gld(p.rows + r0 + lane);
-            valid = row < p.num_rows;
-            if (!valid) atomicOr(&p.scalars[2], 1ull);
-        }
-        const uint64_t b = valid ? rows_block(row, S, p.magic) : 0;
-        const uint32_t sub = (uint32_t)(row - b * S);
-        const uint64_t addr = p.blocks + b * B;
-        // the 64 blocks as coalesced quarters: load k brings rows RPI k ..
-        // RPI k + RPI - 1, lane L its 16 bytes L % LPB; LDS slot of row x = [x B, x B + B)
-        u32x4_t q[LPB];
-#pragma unroll
-        for (uint32_t k = 0; k < LPB; ++k) {
-            const int src = (int)(RPI * k + lane / LPB);
-            const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)addr, src, 64);
-            const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(addr >> 32), src, 64);
-            q[k] = gld_at_nt<u32x4_t, NT>((((uint64_t)hi << 32) | lo) + 16u * (lane % LPB));
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < LPB; ++k) ((AS_LDS u32x4_t *)(wb + 1024 * k))[lane] = q[k];
-        wave_sync();
-        uint32_t cnt = 0, o = 0;
-        bool spl = false;
-        if (valid) {
-            const uint32_t e = mine[sub];
-            o = e & 0x7Fu;
-            spl = (e & 0x80u) != 0;
-            cnt = mine[o];
-            ++o;
-        }
-        bool lng = false;
-        if (__any(spl)) {
-            // spilled rows: the entry (<= B bytes of it) replaces the block in
-            // the lane's own slot; masks from byte 8
-            if (spl) {
-                const uint32_t idx = (uint32_t)mine[o] | ((uint32_t)mine[o + 1] << 8) | ((uint32_t)mine[o + 2] << 16) |
-                                     ((uint32_t)mine[o + 3] << 24);
-                const uint64_t sa = p.spill + (uint64_t)idx * 16;
-                u32x4_t sq[LPB];
-#pragma unroll
-                for (uint32_t k = 0; k < LPB; ++k) sq[k] = gld_at<u32x4_t>(sa + 16u * k);
-#pragma unroll
-                for (uint32_t k = 0; k < LPB; ++k) ((AS_LDS u32x4_t *)mine)[k] = sq[k];
-                cnt = sq[0].x;
-                lng = 8 + sq[0].y > B;
-                o = 8;
-            }
-        }
-        uint32_t x = cnt;
-#pragma unroll
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-            if (lane >= d) x += y;
-        }
-        const uint32_t total = __builtin_amdgcn_readlane(x, 63);
-        const uint32_t pos = x - cnt;
-        const bool direct = total > C || __any(lng);
-        uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
-        if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
-        if (!direct) {
-            rows_walk_wave<MAXD>(mine, o, valid && cnt > 0, ntab, etab, stage, pos);
-            wave_sync();
-            const uint32_t nbytes = total * 2;
-            for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
-                gst(reinterpret_cast<u32x4_t *>(treg + 128 + q2), *(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2));
-        }
-        if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u));
-        if (direct) {
-            unsigned long long k0 = 0;
-            if (lane == 0) k0 = atomicAdd(&p.scalars[1], (unsigned long long)nr);
-            k0 = (unsigned long long)__shfl((long long)k0, 0, 64);
-            if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(p.row_base + r0 + lane));
-        }
-        wave_sync();  // the slots and the stage are reused
-    }
-}
-
-// k_traverse_rows (v2, the default): the RWT2 table (one word per child,
-// leaf parents with consecutive columns expanded inline: no table word, no
-// frame, all their labels in one iteration), labels stored straight into the
-// tile's temp region (no LDS stage: the slots are the only per-wave LDS, so 8
-// waves per SIMD fit), and the next tile's row ids requested before the
-// current tile's walk.
-template <int MAXD>
-__device__ __forceinline__ void rows_walk2(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
-                                           const AS_LDS uint32_t *ent, uint16_t *out, uint32_t pos,
-                                           bool store = true) {
-    // the root: an internal node (a frame) or, for a one-level tree, a leaf parent
-    const uint32_t ra = (root >> 16) & 0x1Fu;
-    const uint32_t rw = ra > 8 ? 1u : 0u;
-    const uint32_t rm = (uint32_t)pb[o] | (rw ? (uint32_t)pb[o + 1] << 8 : 0u);
-    o += 1 + rw;
-    if ((root >> 30) == 3u) {  // root is a leaf parent: label = first column + bit
-        if (live)
-            for (uint32_t x = rm; x; x &= x - 1) gst(out + pos++, (uint16_t)((root & 0xFFFFu) + (uint32_t)__builtin_ctz(x)));
-        return;
-    }
-    uint32_t top = live ? ((root & 0xFFFFu) | (rm << 16)) : 0u;
-    uint32_t st[MAXD > 1 ? MAXD - 1 : 1];
-#pragma unroll
-    for (int k = 0; k < (MAXD > 1 ? MAXD - 1 : 1); ++k) st[k] = 0;
-    uint32_t sp = 0;
-    bool done = (top >> 16) == 0;
-    while (__any(!done)) {
-        const uint32_t c = (uint32_t)__builtin_ctz((top >> 16) | 0x10000u);
-        top &= ~(0x10000u << c);
-        const uint32_t e = ent[done ? 0u : (top & 0xFFFFu) + c];
-        const bool leaf = (e >> 30) == 2u;
-        const bool lp = (e >> 30) == 3u;
-        const bool inner = !done && (e >> 31) == 0u;
-        const uint32_t w = ((e >> 16) & 0x1Fu) > 8 ? 1u : 0u;
-        const uint32_t mw = (uint32_t)pb[o] | (w ? (uint32_t)pb[o + 1] << 8 : 0u);
-        const bool reads = !done && !leaf;  // an internal node's or a leaf parent's mask
-        o += reads ? 1u + w : 0u;
-        if (!done && leaf) {
-            if (store) gst(out + pos, (uint16_t)(e & 0xFFFFu));
-            ++pos;
-        }
-        if (!done && lp)
-            for (uint32_t x = mw; x; x &= x - 1) {
-                if (store) gst(out + pos, (uint16_t)((e & 0xFFFFu) + (uint32_t)__builtin_ctz(x)));
-                ++pos;
-            }
-        if constexpr (MAXD > 1) {
-            const bool push = inner && (top >> 16) != 0;
-#pragma unroll
-            for (int k = MAXD - 2; k > 0; --k) st[k] = push ? st[k - 1] : st[k];
-            st[0] = push ? top : st[0];
-            sp += push ? 1u : 0u;
-        }
-        top = inner ? ((e & 0xFFFFu) | (mw << 16)) : top;
-        if constexpr (MAXD > 1) {
-            const bool pop = !done && (top >> 16) == 0 && sp > 0;
-            top = pop ? st[0] : top;
-#pragma unroll
-            for (int k = 0; k < MAXD - 2; ++k) st[k] = pop ? st[k + 1] : st[k];
-            sp -= pop ? 1u : 0u;
-        }
-        done = done || (top >> 16) == 0;
-    }
-}
-
-// v4 walk: rows_walk2's steps with fewer vector instructions (the walk is
-// VALU-bound: 1,700 VALU per 64-row tile in v2, SQ counters): the top frame
-// in two registers, the pending frames in a per-lane LDS stack (one write /
-// one read instead of shifting registers), one emission loop for leaves and
-// leaf parents, mask bytes read as two bytes masked by the arity.
 // a u16 store at a 32-bit byte offset from a wave-uniform base (the saddr +
 // 32-bit voffset form of global_store_short: no 64-bit address arithmetic)
 __device__ __forceinline__ void st16(uint16_t *base, uint32_t idx, uint32_t v) {
     *(AS_GLOBAL uint16_t *)((uintptr_t)base + (uint64_t)(idx * 2u)) = (uint16_t)v;
 }
 
-template <int MAXD>
+// The general walk (masks of 1 or 2 bytes: arity <= 16): one lock-step
+// iteration per reached child, the top frame in two registers, the pending
+// frames in a per-lane LDS stack (one write / one read per push / pop), one
+// emission loop for leaves and leaf parents, mask bytes read as two bytes
+// masked by the arity.
 __device__ __forceinline__ void rows_walk4(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
                                            const AS_LDS uint32_t *ent, AS_LDS uint32_t *stk, uint16_t *out,
                                            uint32_t pos) {
@@ -1151,20 +937,15 @@ __device__ __forceinline__ void rows_walk4(const AS_LDS uint8_t *pb, uint32_t o,
     }
 }
 
-// v6 walk (the default when every internal node has arity <= 8, so every
-// mask is one byte): rows_walk4's steps in about half the vector
-// instructions -- the walk is VALU-bound (r03 SQ counters: 186 M of the
-// kernel's 196 M VALU wave-instructions per 8 M rows are the walk; a wave64
-// VALU instruction occupies the SIMD 4 cycles).  The record cursor is an LDS
+// The walk when every mask is one byte (arity <= 8 everywhere): rows_walk4's
+// steps in about half the vector instructions -- the record cursor is an LDS
 // byte address, the stack pointer a per-lane LDS address (slot stride 256
-// bytes), the table index is one add-shift, finished lanes leave the loop
-// (exec mask) instead of being carried by selects, and leaves / leaf parents
-// and internal children take exec-masked branches.
-// OUT = a global u16 pointer (labels stored one by one into the tile's temp
-// region) or an LDS u16 pointer (the wave's label stage, MBRWT_ROWS_STAGE=1)
-template <typename OUT>
+// bytes), finished lanes leave the loop (exec mask) instead of being carried
+// by selects, and leaves / leaf parents and internal children take
+// exec-masked branches.  Labels are stored one by one into the tile's temp
+// region (global u16).
 __device__ __forceinline__ void rows_walk6(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
-                                           const AS_LDS uint32_t *ent, AS_LDS uint32_t *stk, OUT out,
+                                           const AS_LDS uint32_t *ent, AS_LDS uint32_t *stk, AS_GLOBAL uint16_t *out,
                                            uint32_t pos) {
     const AS_LDS uint8_t *rc = pb + o;  // record cursor
     const uint32_t rm = rc[0];
@@ -1189,7 +970,7 @@ __device__ __forceinline__ void rows_walk6(const AS_LDS uint8_t *pb, uint32_t o,
             rc += lp ? 1 : 0;
             const uint32_t base = e & 0xFFFFu;
             do {
-                *(OUT)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));
+                *(AS_GLOBAL uint16_t *)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));
                 ob += 2u;
                 x &= x - 1u;
             } while (x);
@@ -1211,22 +992,23 @@ __device__ __forceinline__ void rows_walk6(const AS_LDS uint8_t *pb, uint32_t o,
     }
 }
 
-// v7 walk ("odometer", the default for uniform trees: every root-to-leaf path
-// crosses K internal levels and then a leaf parent with consecutive columns,
-// one-byte masks -- the basic partitioner's trees without singleton groups,
-// i.e. C2-C4).  rows_walk6 spends one lock-step iteration per reached node
-// (19.3 per C4 row, 34 per 64-row tile in lock step); here one iteration
-// reaches the NEXT LEAF PARENT of the row in pre-order (7.9 per C4 row, 15
-// per tile): the remaining-children masks r[0..K-1] of the current path form
-// an odometer -- level k takes its next child when every level below it is
+// The odometer walk (uniform trees: every root-to-leaf path crosses K
+// internal levels and then a leaf parent with consecutive columns, one-byte
+// masks -- the basic partitioner's trees without singleton groups, i.e.
+// C2-C4).  rows_walk6 spends one lock-step iteration per reached node (19.3
+// per C4 row, 34 per 64-row tile in lock step); here one iteration reaches
+// the NEXT LEAF PARENT of the row in pre-order (7.9 per C4 row, 15 per tile):
+// the remaining-children masks r[0..K-1] of the current path form an
+// odometer -- level k takes its next child when every level below it is
 // exhausted (top-down, so a level refilled in this iteration feeds the level
 // under it), reading that child's mask as the record's next byte, which is
 // exactly BRWT::get_row's pre-order (BRWT.cpp:43-51); the leaf-parent step
-// then reads the leaf mask and stores base + bit for its set bits.  No stack,
-// no per-lane frame state beyond 2K registers.
-template <int K, typename OUT>
+// then reads the leaf mask and stores base + bit for its set bits into the
+// wave's LDS label stage.  No stack, no per-lane frame state beyond 2K
+// registers.
+template <int K>
 __device__ __forceinline__ void rows_walk_uni(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
-                                              const AS_LDS uint32_t *ent, OUT out, uint32_t pos) {
+                                              const AS_LDS uint32_t *ent, AS_LDS uint16_t *out, uint32_t pos) {
     const AS_LDS uint8_t *rc = pb + o;  // record cursor
     uint32_t r[K], f[K];
     f[0] = root & 0xFFFFu;
@@ -1260,72 +1042,33 @@ __device__ __forceinline__ void rows_walk_uni(const AS_LDS uint8_t *pb, uint32_t
         uint32_t x = *rc;
         ++rc;
         do {
-            *(OUT)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));
+            *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));
             ob += 2u;
             x &= x - 1u;
         } while (x);
     }
 }
 
-// v5 walk: rows_walk4 without divergent branches around the stack -- the
-// push writes the next free slot unconditionally and the pop reads the top
-// slot unconditionally (selects keep what applies), so a step costs vector
-// selects instead of exec-mask juggling; only the label loop diverges.
-template <int MAXD>
-__device__ __forceinline__ void rows_walk5(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
-                                           const AS_LDS uint32_t *ent, AS_LDS uint32_t *stk, uint16_t *out,
-                                           uint32_t pos) {
-    const uint32_t ra = (root >> 16) & 0x1Fu;
-    const uint32_t rm = ((uint32_t)pb[o] | ((uint32_t)pb[o + 1] << 8)) & ((1u << ra) - 1u);
-    o += ra > 8 ? 2u : 1u;
-    if ((root >> 30) == 3u) {
-        if (live)
-            for (uint32_t x = rm; x; x &= x - 1) st16(out, pos++, (root & 0xFFFFu) + (uint32_t)__builtin_ctz(x));
-        return;
-    }
-    uint32_t f = root & 0xFFFFu, m = live ? rm : 0u;
-    uint32_t sp = 1;  // stk[(sp - 1) * 64] is the top pending frame; slot 0 is a dummy
-    while (__any(m != 0)) {
-        const bool act = m != 0;
-        const uint32_t c = (uint32_t)__builtin_ctz(m | 0x10000u);
-        m &= m - 1;
-        const uint32_t e = ent[act ? f + c : 0u];
-        const uint32_t a = act ? (e >> 16) & 0x1Fu : 0u;
-        const uint32_t mw = ((uint32_t)pb[o] | ((uint32_t)pb[o + 1] << 8)) & ((1u << a) - 1u);
-        o += a ? (a > 8 ? 2u : 1u) : 0u;
-        const bool inner = act && (e >> 31) == 0u;
-        uint32_t x = (act && (e >> 31)) ? (a ? mw : 1u) : 0u;
-        const uint32_t base = e & 0xFFFFu;
-        for (; x; x &= x - 1) st16(out, pos++, base + (uint32_t)__builtin_ctz(x));
-        const bool push = inner && m != 0;
-        stk[sp * 64] = f | (m << 16);  // (a slot past the top when not pushing: harmless)
-        sp += push ? 1u : 0u;
-        f = inner ? base : f;
-        m = inner ? mw : m;
-        const uint32_t w = stk[(sp - 1) * 64];
-        const bool pop = act && m == 0 && sp > 1;
-        f = pop ? (w & 0xFFFFu) : f;
-        m = pop ? (w >> 16) : m;
-        sp -= pop ? 1u : 0u;
-    }
-}
-
-template <int B, int MAXD, int WPB, bool NT>
-__global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows2[];
+// k_traverse_rows: one wave per tile of 64 query rows (file comment).
+// B: block bytes; WPB: waves per workgroup (the RWT2 table is staged once per
+// workgroup; the grid is persistent); WALK: the walk family.
+template <int B, int WPB, bool NT, uint32_t WALK>
+__global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows[];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_rows2[i] = gld(p.table + i);
+    for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_rows[i] = gld(p.table + i);
+    if (blockIdx.x == 0 && threadIdx.x == 0) p.status[1] = MBRWT_OK;  // k_compact_tiles raises it
     __syncthreads();
-    const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows2[0]);
-    const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows2 + 4;
+    const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows[0]);
+    const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows + 4;
     const uint32_t C = p.C;
     // a row's block at a stride of B + 4 bytes: lanes reading their records
     // at similar offsets hit different LDS banks (a B-byte stride puts every
     // other lane in the same bank)
     constexpr uint32_t PB = B + 4;
-    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows2 + ((p.table_words + 3) & ~3u)) +
-                         wv * (64u * PB + 256u * p.stk_words + (p.stage ? 2u * p.C : 0u));
+    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows + ((p.table_words + 3) & ~3u)) +
+                         wv * (64u * PB + 256u * p.stk_words + (WALK == WALK_ODOMETER ? 2u * C : 0u));
     AS_LDS uint8_t *mine = wb + lane * PB;
     AS_LDS uint32_t *stk = (AS_LDS uint32_t *)(wb + 64u * PB) + lane;
     constexpr uint32_t LPB = B / 16, RPI = 64 / LPB;
@@ -1346,6 +1089,8 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
         const uint64_t b = valid ? rows_block(row, S, p.magic) : 0;
         const uint32_t sub = (uint32_t)(row - b * S);
         const uint64_t addr = p.blocks + b * B;
+        // the 64 blocks as coalesced quarters: load k brings rows RPI k ..
+        // RPI k + RPI - 1, lane L its 16 bytes L % LPB
         u32x4_t q[LPB];
 #pragma unroll
         for (uint32_t k = 0; k < LPB; ++k) {
@@ -1373,7 +1118,9 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
             ++o;
         }
         bool lng = false;
-        if (__any(spl) && !(p.diag & 4)) {
+        if (__any(spl)) {
+            // spilled rows: the entry (<= B bytes of it) replaces the block in
+            // the lane's own slot; masks from byte 8
             if (spl) {
                 const uint32_t idx = (uint32_t)mine[o] | ((uint32_t)mine[o + 1] << 8) | ((uint32_t)mine[o + 2] << 16) |
                                      ((uint32_t)mine[o + 3] << 24);
@@ -1402,25 +1149,20 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
         }
         const uint32_t total = __builtin_amdgcn_readlane(x, 63);
         const uint32_t pos = x - cnt;
+        // a tile whose labels exceed its region, or holding a record longer
+        // than a block, is walked by k_compact_tiles from global memory
         const bool direct = total > C || __any(lng);
         uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
         if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
-        if (!direct && !(p.diag & 1)) {
-            if (p.walk4 == 3 && p.stage) {
+        if (!direct) {
+            const bool live = valid && cnt > 0;
+            if constexpr (WALK == WALK_ODOMETER) {
+                // the odometer into the wave's LDS label stage, then the
+                // tile's labels as 16-byte vector stores (a few wide stores
+                // instead of one scattered 2-byte store per label: the r03
+                // SQ/TA counters showed the texture-address unit as the
+                // busiest unit)
                 AS_LDS uint16_t *stage = (AS_LDS uint16_t *)(wb + 64u * PB + 256u * p.stk_words);
-                rows_walk6(mine, o, valid && cnt > 0, root, ent, stk, stage, pos);
-                wave_sync();
-                const uint32_t nbytes = total * 2;
-                for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
-                    gst(reinterpret_cast<u32x4_t *>(treg + 128 + q2),
-                        *(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2));
-            } else if (p.walk4 == 4 && p.stage) {
-                // the odometer into the wave's LDS label stage, then the tile's
-                // labels as 16-byte vector stores (a few wide stores instead of
-                // one scattered 2-byte store per label: r03 SQ/TA counters show
-                // the texture-address unit, not the VALU, as the busiest unit)
-                AS_LDS uint16_t *stage = (AS_LDS uint16_t *)(wb + 64u * PB + 256u * p.stk_words);
-                const bool live = valid && cnt > 0;
                 switch (p.uni) {
                     case 1: rows_walk_uni<1>(mine, o, live, root, ent, stage, pos); break;
                     case 2: rows_walk_uni<2>(mine, o, live, root, ent, stage, pos); break;
@@ -1433,450 +1175,75 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows2(RowsParams p) {
                 for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
                     gst(reinterpret_cast<u32x4_t *>(treg + 128 + q2),
                         *(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2));
-            } else if (p.walk4 == 4) {
-                AS_GLOBAL uint16_t *out = (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128);
-                const bool live = valid && cnt > 0;
-                switch (p.uni) {
-                    case 1: rows_walk_uni<1>(mine, o, live, root, ent, out, pos); break;
-                    case 2: rows_walk_uni<2>(mine, o, live, root, ent, out, pos); break;
-                    case 3: rows_walk_uni<3>(mine, o, live, root, ent, out, pos); break;
-                    case 4: rows_walk_uni<4>(mine, o, live, root, ent, out, pos); break;
-                    default: rows_walk_uni<5>(mine, o, live, root, ent, out, pos); break;
-                }
-            } else if (p.walk4 == 3)
-                rows_walk6(mine, o, valid && cnt > 0, root, ent, stk,
-                           (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128), pos);
-            else if (p.walk4 == 2)
-                rows_walk5<MAXD>(mine, o, valid && cnt > 0, root, ent, stk, reinterpret_cast<uint16_t *>(treg + 128),
-                                 pos);
-            else if (p.walk4)
-                rows_walk4<MAXD>(mine, o, valid && cnt > 0, root, ent, stk, reinterpret_cast<uint16_t *>(treg + 128),
-                                 pos);
-            else
-                rows_walk2<MAXD>(mine, o, valid && cnt > 0, root, ent, reinterpret_cast<uint16_t *>(treg + 128), pos,
-                                 !(p.diag & 2));
+            } else if constexpr (WALK == WALK_MASK1) {
+                rows_walk6(mine, o, live, root, ent, stk, (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128),
+                           pos);
+            } else {
+                rows_walk4(mine, o, live, root, ent, stk, reinterpret_cast<uint16_t *>(treg + 128), pos);
+            }
         }
         if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u));
-        if (direct) {
-            unsigned long long k0 = 0;
-            if (lane == 0) k0 = atomicAdd(&p.scalars[1], (unsigned long long)nr);
-            k0 = (unsigned long long)__shfl((long long)k0, 0, 64);
-            if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(p.row_base + r0 + lane));
-        }
         wave_sync();  // the slots are reused
-    }
-}
-
-// k_traverse_rows (v5): loader and walker waves.  In v2 every wave loads a
-// tile, waits, then walks it, and the two phases hardly overlap (C4: 0.21 ms
-// of loads alone, 0.44 ms with the walk; neither the request rate nor the
-// VALU is saturated).  Here a workgroup's NL loader waves only fetch tiles
-// (blocks -> an LDS slot, entries, spills, count scan, temp counts, direct
-// tiles) and its NW walker waves only walk them, through a ring of NS tile
-// slots in LDS with a state word per slot (2k+1: the workgroup's k-th tile is
-// ready in slot k % NS; 2k+2: it has been walked).  Loader l takes the
-// workgroup's tiles l, l + NL, ..., walker w the tiles w, w + NW, ...; a
-// loader waits for slot k % NS to be released by tile k - NS, a walker for
-// tile k to be ready -- every wait is on a smaller k, so the ring cannot
-// deadlock (all waves of a workgroup are resident), and every wave's loop
-// ends with the workgroup's last tile.  Workgroup tile k = global tile
-// blockIdx.x + k gridDim.x.
-// a ring wait: spin (with s_sleep) on a slot's state word.  Bounded: a wait
-// that outlasts ~2^24 polls (seconds) flags error bit 4 and gives up, so a
-// logic error can never leave the kernel spinning on the GPU.
-__device__ __forceinline__ void rows5_wait(AS_LDS uint32_t *st, uint32_t want, unsigned long long *scalars) {
-    for (uint32_t it = 0;; ++it) {
-        const uint32_t v = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(st, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (v == want) return;
-        if (it > (1u << 24)) {
-            if ((threadIdx.x & 63) == 0) atomicOr(&scalars[2], 4ull);
-            return;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-
-template <int B, int NL, int NW, int NS, bool NT>
-__global__ __launch_bounds__(64 * (NL + NW)) void k_traverse_rows5(RowsParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows5[];
-    constexpr uint32_t LPB = B / 16, RPI = 64 / LPB;
-    constexpr uint32_t SLOT = 64u * B + 256u + 16u;  // blocks | per-lane walk words | tile header
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_rows5[i] = gld(p.table + i);
-    const uint32_t slots0 = ((p.table_words + 3) & ~3u) * 4;
-    AS_LDS uint8_t *const lds0 = (AS_LDS uint8_t *)lds_rows5;
-    AS_LDS uint32_t *state = (AS_LDS uint32_t *)(lds0 + slots0 + NS * SLOT);
-    AS_LDS uint32_t *stacks = state + ((NS + 3) & ~3u);
-    if (threadIdx.x < NS) state[threadIdx.x] = 0;
-    __syncthreads();
-    const uint64_t ntiles = (p.n + 63) / 64;
-    const uint64_t G = gridDim.x;
-    const uint32_t C = p.C;
-    const uint64_t region = 128 + 2ull * C;
-    if (wv < NL) {
-        // ---- loader ---------------------------------------------------------
-        const uint32_t S = p.S;
-        uint64_t k = wv;
-        uint64_t t = blockIdx.x + k * G;
-        uint64_t row_n = 0;
-        if (t < ntiles && t * 64 + lane < p.n) row_n = gld(p.rows + t * 64 + lane);
-        for (; t < ntiles; k += NL, t += NL * G) {
-            const uint64_t r0 = t * 64;
-            const uint32_t nr = (uint32_t)(p.n - r0 < 64 ? p.n - r0 : 64);
-            const uint64_t row = row_n;
-            const uint64_t tn = t + NL * G;
-            if (tn < ntiles && tn * 64 + lane < p.n) row_n = gld(p.rows + tn * 64 + lane);
-            const bool valid = lane < nr && row < p.num_rows;
-            if (lane < nr && !valid) atomicOr(&p.scalars[2], 1ull);
-            const uint64_t b = valid ? rows_block(row, S, p.magic) : 0;
-            const uint32_t sub = (uint32_t)(row - b * S);
-            const uint64_t addr = p.blocks + b * B;
-            u32x4_t q[LPB];
-#pragma unroll
-            for (uint32_t j = 0; j < LPB; ++j) {
-                const int src = (int)(RPI * j + lane / LPB);
-                const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)addr, src, 64);
-                const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(addr >> 32), src, 64);
-                q[j] = gld_at_nt<u32x4_t, NT>((((uint64_t)hi << 32) | lo) + 16u * (lane % LPB));
-            }
-            // the slot of tile k - NS must have been walked
-            const uint32_t si = (uint32_t)(k % NS);
-            const uint32_t want = k >= NS ? (uint32_t)(2 * (k - NS) + 2) : 0u;
-            rows5_wait(&state[si], want, p.scalars);
-            AS_LDS uint8_t *wb = lds0 + slots0 + si * SLOT;
-            AS_LDS uint8_t *mine = wb + lane * B;
-#pragma unroll
-            for (uint32_t j = 0; j < LPB; ++j) ((AS_LDS u32x4_t *)(wb + 1024 * j))[lane] = q[j];
-            wave_sync();
-            uint32_t cnt = 0, o = 0;
-            bool spl = false;
-            if (valid) {
-                const uint32_t e = mine[sub];
-                o = e & 0x7Fu;
-                spl = (e & 0x80u) != 0;
-                cnt = mine[o];
-                ++o;
-            }
-            bool lng = false;
-            if (__any(spl)) {
-                if (spl) {
-                    const uint32_t idx = (uint32_t)mine[o] | ((uint32_t)mine[o + 1] << 8) |
-                                         ((uint32_t)mine[o + 2] << 16) | ((uint32_t)mine[o + 3] << 24);
-                    const uint64_t sa = p.spill + (uint64_t)idx * 16;
-                    u32x4_t sq[LPB];
-#pragma unroll
-                    for (uint32_t j = 0; j < LPB; ++j) sq[j] = gld_at<u32x4_t>(sa + 16u * j);
-#pragma unroll
-                    for (uint32_t j = 0; j < LPB; ++j) ((AS_LDS u32x4_t *)mine)[j] = sq[j];
-                    cnt = sq[0].x;
-                    lng = 8 + sq[0].y > B;
-                    o = 8;
-                }
-            }
-            uint32_t x = cnt;
-#pragma unroll
-            for (uint32_t d = 1; d < 64; d <<= 1) {
-                const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-                if (lane >= d) x += y;
-            }
-            const uint32_t total = __builtin_amdgcn_readlane(x, 63);
-            const uint32_t pos = x - cnt;
-            const bool direct = total > C || __any(lng);
-            uint8_t *treg = p.temp + t * region;
-            if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
-            if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u));
-            if (direct) {
-                unsigned long long k0 = 0;
-                if (lane == 0) k0 = atomicAdd(&p.scalars[1], (unsigned long long)nr);
-                k0 = (unsigned long long)__shfl((long long)k0, 0, 64);
-                if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(p.row_base + r0 + lane));
-            }
-            // walk word: record offset | pos << 8 | live << 31; header: tile, walk flag
-            const bool live = valid && cnt > 0 && !direct && !(p.diag & 1);
-            ((AS_LDS uint32_t *)(wb + 64u * B))[lane] = o | ((pos & 0xFFFFu) << 8) | (live ? 0x80000000u : 0u);
-            if (lane == 0) {
-                ((AS_LDS uint64_t *)(wb + 64u * B + 256u))[0] = t;
-                ((AS_LDS uint32_t *)(wb + 64u * B + 256u))[2] = (direct || (p.diag & 1)) ? 0u : 1u;
-            }
-            wave_sync();
-            if (lane == 0)
-                __hip_atomic_store(&state[si], (uint32_t)(2 * k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-    } else {
-        // ---- walker ---------------------------------------------------------
-        const uint32_t w = wv - NL;
-        const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows5[0]);
-        const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows5 + 4;
-        AS_LDS uint32_t *stk = stacks + w * 64u * p.stk_words + lane;
-        for (uint64_t k = w, t = blockIdx.x + k * G; t < ntiles; k += NW, t += NW * G) {
-            const uint32_t si = (uint32_t)(k % NS);
-            const uint32_t want = (uint32_t)(2 * k + 1);
-            rows5_wait(&state[si], want, p.scalars);
-            AS_LDS uint8_t *wb = lds0 + slots0 + si * SLOT;
-            const uint32_t walk = __builtin_amdgcn_readfirstlane(((AS_LDS uint32_t *)(wb + 64u * B + 256u))[2]);
-            if (walk) {
-                const uint32_t ww = ((AS_LDS uint32_t *)(wb + 64u * B))[lane];
-                uint16_t *out = reinterpret_cast<uint16_t *>(p.temp + t * region + 128);
-                rows_walk4<1>(wb + lane * B, ww & 0xFFu, (ww >> 31) != 0, root, ent, stk, out, (ww >> 8) & 0xFFFFu);
-            }
-            wave_sync();
-            if (lane == 0)
-                __hip_atomic_store(&state[si], (uint32_t)(2 * k + 2), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-    }
-}
-
-// k_traverse_rows (v3, the default): v2's walk, software-pipelined over the
-// wave's tiles -- the blocks of tile t+1 (and the row ids of tile t+2) are
-// requested into registers BEFORE tile t is walked, and the spilled entries of
-// tile t+1 right after its blocks land, so the memory latency of the next
-// tile overlaps the walk of this one (v2 ran load phase, then walk phase:
-// diagnostics 0.22 ms of loads + 0.28 ms of walk per 8 M rows, not overlapped).
-template <int B>
-struct RowsTileIo {
-    static constexpr uint32_t LPB = B / 16, RPI = 64 / LPB;
-    // the 64 blocks of a tile as coalesced quarters (row RPI k + lane / LPB in load k)
-    template <bool NT>
-    static __device__ __forceinline__ void load(u32x4_t (&q)[LPB], uint64_t addr, uint32_t lane, bool any) {
-#pragma unroll
-        for (uint32_t k = 0; k < LPB; ++k) {
-            const int src = (int)(RPI * k + lane / LPB);
-            const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)addr, src, 64);
-            const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(addr >> 32), src, 64);
-            if (any) q[k] = gld_at_nt<u32x4_t, NT>((((uint64_t)hi << 32) | lo) + 16u * (lane % LPB));
-        }
-    }
-    static __device__ __forceinline__ void store(AS_LDS uint8_t *wb, const u32x4_t (&q)[LPB], uint32_t lane) {
-#pragma unroll
-        for (uint32_t k = 0; k < LPB; ++k) ((AS_LDS u32x4_t *)(wb + 1024 * k))[lane] = q[k];
-    }
-};
-
-template <int B, int MAXD, int WPB, bool NT>
-__global__ __launch_bounds__(64 * WPB) void k_traverse_rows3(RowsParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows3[];
-    using Io = RowsTileIo<B>;
-    constexpr uint32_t LPB = Io::LPB;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_rows3[i] = gld(p.table + i);
-    __syncthreads();
-    const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows3[0]);
-    const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows3 + 4;
-    const uint32_t C = p.C;
-    AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows3 + ((p.table_words + 3) & ~3u)) +
-                         wv * (64u * B + 256u * p.stk_words + (p.stage ? 2u * p.C : 0u));
-    AS_LDS uint8_t *mine = wb + lane * B;
-    AS_LDS uint32_t *stk = (AS_LDS uint32_t *)(wb + 64u * B) + lane;
-    const uint64_t ntiles = (p.n + 63) / 64;
-    const uint64_t tstride = (uint64_t)gridDim.x * WPB;
-    const uint32_t S = p.S;
-    // tile t's row of this lane -> {valid, block address, slot index}
-    auto row_of = [&](uint64_t t, uint64_t &row) -> bool {
-        row = 0;
-        if (t >= ntiles || t * 64 + lane >= p.n) return false;
-        row = gld(p.rows + t * 64 + lane);
-        return true;
-    };
-    auto place = [&](uint64_t row, bool in, bool &valid, uint64_t &addr, uint32_t &sub) {
-        valid = in && row < p.num_rows;
-        if (in && !valid) atomicOr(&p.scalars[2], 1ull);
-        const uint64_t b = valid ? rows_block(row, S, p.magic) : 0;
-        sub = (uint32_t)(row - b * S);
-        addr = p.blocks + b * B;
-    };
-    // this lane's entry in its slot: label count, first mask byte, spilled?
-    auto parse = [&](bool valid, uint32_t sub, uint32_t &cnt, uint32_t &o, bool &spl, uint64_t &sa) {
-        cnt = 0;
-        o = 0;
-        spl = false;
-        sa = 0;
-        if (!valid) return;
-        const uint32_t e = mine[sub];
-        o = e & 0x7Fu;
-        spl = (e & 0x80u) != 0;
-        cnt = mine[o];
-        if (spl) {
-            const uint32_t idx = (uint32_t)mine[o + 1] | ((uint32_t)mine[o + 2] << 8) | ((uint32_t)mine[o + 3] << 16) |
-                                 ((uint32_t)mine[o + 4] << 24);
-            sa = p.spill + (uint64_t)idx * 16;
-        }
-        ++o;
-    };
-
-    uint64_t t = (uint64_t)blockIdx.x * WPB + wv;
-    if (t >= ntiles) return;
-    // prologue: tile t in the slots, its spill entries requested
-    uint64_t row;
-    bool in = row_of(t, row);
-    bool valid;
-    uint64_t addr;
-    uint32_t sub;
-    place(row, in, valid, addr, sub);
-    u32x4_t q[LPB];
-    Io::template load<NT>(q, addr, lane, true);
-    uint64_t row_n;
-    bool in_n = row_of(t + tstride, row_n);
-    Io::store(wb, q, lane);
-    wave_sync();
-    uint32_t cnt, o;
-    bool spl;
-    uint64_t sa;
-    parse(valid, sub, cnt, o, spl, sa);
-    u32x4_t sq[LPB];
-    bool any_spl = __any(spl) && !(p.diag & 4);
-    if (any_spl && spl) {
-#pragma unroll
-        for (uint32_t k = 0; k < LPB; ++k) sq[k] = gld_at<u32x4_t>(sa + 16u * k);
-    }
-    while (true) {
-        const uint64_t r0 = t * 64;
-        const uint32_t nr = (uint32_t)(p.n - r0 < 64 ? p.n - r0 : 64);
-        const uint64_t tn = t + tstride;
-        const bool more = tn < ntiles;  // wave-uniform
-        // the next tile's blocks and the row ids after it, in flight during this walk
-        bool valid_n;
-        uint64_t addr_n;
-        uint32_t sub_n;
-        place(row_n, in_n, valid_n, addr_n, sub_n);
-        u32x4_t qn[LPB];
-        Io::template load<NT>(qn, addr_n, lane, more);
-        uint64_t row_nn;
-        const bool in_nn = row_of(tn + tstride, row_nn);
-        // this tile's spilled entries replace the block in the lane's own slot
-        bool lng = false;
-        if (any_spl && spl) {
-#pragma unroll
-            for (uint32_t k = 0; k < LPB; ++k) ((AS_LDS u32x4_t *)mine)[k] = sq[k];
-            cnt = sq[0].x;
-            lng = 8 + sq[0].y > B;
-            o = 8;
-        }
-        uint32_t x = cnt;
-#pragma unroll
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-            if (lane >= d) x += y;
-        }
-        const uint32_t total = __builtin_amdgcn_readlane(x, 63);
-        const uint32_t pos = x - cnt;
-        const bool direct = total > C || __any(lng);
-        uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
-        if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
-        if (!direct && !(p.diag & 1)) {
-            if (p.walk4 == 4) {  // the odometer (uniform trees), LDS label stage or direct stores
-                const bool live = valid && cnt > 0;
-                AS_LDS uint16_t *stage = (AS_LDS uint16_t *)(wb + 64u * B + 256u * p.stk_words);
-                AS_GLOBAL uint16_t *out = (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128);
-                if (p.stage) {
-                    switch (p.uni) {
-                        case 1: rows_walk_uni<1>(mine, o, live, root, ent, stage, pos); break;
-                        case 2: rows_walk_uni<2>(mine, o, live, root, ent, stage, pos); break;
-                        case 3: rows_walk_uni<3>(mine, o, live, root, ent, stage, pos); break;
-                        case 4: rows_walk_uni<4>(mine, o, live, root, ent, stage, pos); break;
-                        default: rows_walk_uni<5>(mine, o, live, root, ent, stage, pos); break;
-                    }
-                    wave_sync();
-                    const uint32_t nbytes = total * 2;
-                    for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
-                        gst(reinterpret_cast<u32x4_t *>(treg + 128 + q2),
-                            *(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2));
-                } else {
-                    switch (p.uni) {
-                        case 1: rows_walk_uni<1>(mine, o, live, root, ent, out, pos); break;
-                        case 2: rows_walk_uni<2>(mine, o, live, root, ent, out, pos); break;
-                        case 3: rows_walk_uni<3>(mine, o, live, root, ent, out, pos); break;
-                        case 4: rows_walk_uni<4>(mine, o, live, root, ent, out, pos); break;
-                        default: rows_walk_uni<5>(mine, o, live, root, ent, out, pos); break;
-                    }
-                }
-            } else if (p.walk4 == 3)
-                rows_walk6(mine, o, valid && cnt > 0, root, ent, stk,
-                           (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128), pos);
-            else if (p.walk4 == 2)
-                rows_walk5<MAXD>(mine, o, valid && cnt > 0, root, ent, stk, reinterpret_cast<uint16_t *>(treg + 128),
-                                 pos);
-            else if (p.walk4)
-                rows_walk4<MAXD>(mine, o, valid && cnt > 0, root, ent, stk, reinterpret_cast<uint16_t *>(treg + 128),
-                                 pos);
-            else
-                rows_walk2<MAXD>(mine, o, valid && cnt > 0, root, ent, reinterpret_cast<uint16_t *>(treg + 128), pos,
-                                 !(p.diag & 2));
-        }
-        if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u));
-        if (direct) {
-            unsigned long long k0 = 0;
-            if (lane == 0) k0 = atomicAdd(&p.scalars[1], (unsigned long long)nr);
-            k0 = (unsigned long long)__shfl((long long)k0, 0, 64);
-            if (lane < nr) gst(p.ovf_list + k0 + lane, (uint32_t)(p.row_base + r0 + lane));
-        }
-        wave_sync();  // every lane is done with its slot
-        if (!more) break;
-        // the next tile into the slots; its spill entries requested
-        Io::store(wb, qn, lane);
-        wave_sync();
-        t = tn;
-        valid = valid_n;
-        sub = sub_n;
-        row_n = row_nn;
-        in_n = in_nn;
-        parse(valid, sub, cnt, o, spl, sa);
-        any_spl = __any(spl) && !(p.diag & 4);
-        if (any_spl && spl) {
-#pragma unroll
-            for (uint32_t k = 0; k < LPB; ++k) sq[k] = gld_at<u32x4_t>(sa + 16u * k);
-        }
     }
 }
 
 // tile regions -> CSR: one wave per TPW consecutive tiles (every load of
 // the group -- counts, the tile offsets, the first 512 labels of each tile --
 // issued before any store, so a wave pays one memory latency for TPW tiles);
-// offsets by a wave scan of each tile's counts, labels u16 -> u32.  Launched
-// before the host knows the total: over the capacity it writes no CSR.  The
-// scan is exclusive over the tiles, so the batch total is offset + count of
-// the last tile; workgroup 0 publishes {total, direct rows, error flags} to
-// res[0..2] and clears the kernel's counters (sc[1], sc[2]) for the next call.
+// offsets by a wave scan of each tile's counts, labels u16 -> u32.  A direct
+// tile (bit 31 of its count: more labels than its region, or a record longer
+// than a block) is walked here, one lane per row, from the records in global
+// memory straight into the CSR.  Launched before the host knows the total:
+// over the capacity it writes no CSR.  The scan is exclusive over the tiles,
+// so the batch total is offset + count of the last tile; workgroup 0
+// publishes the call's {total, status, sticky bits} (the traversal reset the
+// status word; a failed record walk raises it to MBRWT_ERR_DEVICE) and
+// clears the traversal's error flags for the next call.
 constexpr uint32_t kCompactTpw = 4;
-// Split batches (rows_get_rows): the tiles [tb, te) of the batch, their scan
-// relative to `*base_to + (*base_tc & mask)` (the previous half's last tile;
-// null: 0); only the call's last compaction (res != null) publishes and
-// clears, an earlier half writes when its own end fits the capacity.
-__global__ __launch_bounds__(256) void k_compact_tiles(const uint8_t *__restrict__ temp, uint32_t C,
-                                                       const uint32_t *__restrict__ tile_counts,
-                                                       const uint64_t *__restrict__ tile_offsets,
-                                                       uint64_t *__restrict__ offsets, uint32_t *__restrict__ cols,
-                                                       uint64_t n, uint64_t tb, uint64_t te,
-                                                       const uint32_t *base_tc, const uint64_t *base_to,
-                                                       uint64_t cap, unsigned long long *sc,
-                                                       unsigned long long *res) {
+struct CompactParams {
+    const uint8_t *temp;
+    uint32_t C;
+    const uint32_t *tile_counts;
+    const uint64_t *tile_offsets;
+    uint64_t *offsets;
+    uint32_t *cols;
+    uint64_t n, cap;
+    unsigned long long *scalars;  // the traversal's counters ([2] error flags)
+    unsigned long long *status;   // {total, status, sticky}
+    const uint64_t *rows;         // the batch (direct tiles)
+    RowsView v;
+    const uint32_t *table;        // RWT (direct tiles)
+};
+__device__ __forceinline__ void publish_status(unsigned long long *status, uint64_t st) {
+    atomicMax(&status[1], (unsigned long long)st);
+    atomicOr(&status[2], 1ull << st);
+}
+__global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
+    const uint64_t n = p.n;
     const uint64_t ntiles = (n + 63) / 64;
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t add = base_to ? gld(base_to) + (gld(base_tc) & 0x7FFFFFFFu) : 0;
-    const uint64_t total = add + gld(tile_offsets + te - 1) + (gld(tile_counts + te - 1) & 0x7FFFFFFFu);
-    if (res && blockIdx.x == 0 && threadIdx.x == 0) {
-        res[0] = total;
-        res[1] = sc[1];
-        res[2] = sc[2];
-        sc[1] = 0;
-        sc[2] = 0;
+    const uint64_t total = gld(p.tile_offsets + ntiles - 1) + (gld(p.tile_counts + ntiles - 1) & 0x7FFFFFFFu);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const uint64_t err = p.scalars[2];
+        p.scalars[2] = 0;
+        p.status[0] = total;
+        publish_status(p.status, (err & 1) ? MBRWT_ERR_RANGE : total > p.cap ? MBRWT_ERR_CAPACITY : MBRWT_OK);
     }
-    if (total > cap) return;
-    const uint64_t t0 = tb + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * kCompactTpw;
-    if (t0 >= te) return;
+    if (total > p.cap) return;
+    const uint64_t t0 = (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * kCompactTpw;
+    if (t0 >= ntiles) return;
+    const uint32_t C = p.C;
     const uint32_t region = 128 + 2 * C;
     uint32_t tc[kCompactTpw], cnt[kCompactTpw], v[kCompactTpw][8];
     uint64_t base[kCompactTpw];
 #pragma unroll
     for (uint32_t k = 0; k < kCompactTpw; ++k) {
         const uint64_t t = t0 + k;
-        const bool in = t < te;
-        const uint8_t *treg = temp + (in ? t : 0) * (uint64_t)region;
+        const bool in = t < ntiles;
+        const uint8_t *treg = p.temp + (in ? t : 0) * (uint64_t)region;
         const uint64_t r0 = t * 64;
-        tc[k] = in ? gld(tile_counts + t) : 0x80000000u;
-        base[k] = in ? add + gld(tile_offsets + t) : 0;
+        tc[k] = in ? gld(p.tile_counts + t) : 0x80000000u;
+        base[k] = in ? gld(p.tile_offsets + t) : 0;
         cnt[k] = (in && r0 + lane < n) ? (uint32_t)gld(reinterpret_cast<const uint16_t *>(treg) + lane) : 0u;
         const uint16_t *lab = reinterpret_cast<const uint16_t *>(treg + 128);
 #pragma unroll
@@ -1885,7 +1252,7 @@ __global__ __launch_bounds__(256) void k_compact_tiles(const uint8_t *__restrict
 #pragma unroll
     for (uint32_t k = 0; k < kCompactTpw; ++k) {
         const uint64_t t = t0 + k;
-        if (t >= te) break;
+        if (t >= ntiles) break;
         const uint64_t r0 = t * 64;
         const uint32_t nr = (uint32_t)(n - r0 < 64 ? n - r0 : 64);
         uint32_t x = cnt[k];
@@ -1894,17 +1261,38 @@ __global__ __launch_bounds__(256) void k_compact_tiles(const uint8_t *__restrict
             const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
             if (lane >= d) x += y;
         }
-        if (lane < nr) gst(offsets + r0 + lane, base[k] + (x - cnt[k]));
-        if (t == ntiles - 1 && lane == nr - 1) gst(offsets + n, base[k] + x);
-        if (tc[k] >> 31) continue;  // direct tile: k_rows_direct writes its labels
+        const uint64_t rbase = base[k] + (x - cnt[k]);
+        if (lane < nr) gst(p.offsets + r0 + lane, rbase);
+        if (t == ntiles - 1 && lane == nr - 1) gst(p.offsets + n, base[k] + x);
+        if (tc[k] >> 31) {  // a direct tile: its rows' records walked from global memory
+            if (lane < nr && cnt[k]) {
+                const uint64_t row = gld(p.rows + r0 + lane);
+                uint64_t masks;
+                uint32_t count;
+                rows_locate(p.v, row, masks, count);  // (count = cnt: rows out of range have none)
+                const uint32_t *ntab = p.table + 4;
+                const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + p.table[0]);
+                uint32_t *dst = p.cols + rbase;
+                uint32_t j = 0;
+                const bool ok = rwt_walk(
+                    ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
+                    [&](uint32_t col) {
+                        if (j < count) gst(dst + j, col);
+                        ++j;
+                    },
+                    [](uint32_t) {});
+                if (!ok || j != count) publish_status(p.status, MBRWT_ERR_DEVICE);
+            }
+            continue;
+        }
         const uint32_t tot = tc[k];
-        uint32_t *dst = cols + base[k];
+        uint32_t *dst = p.cols + base[k];
 #pragma unroll
         for (uint32_t j = 0; j < 8; ++j) {
             const uint32_t i = lane + 64 * j;
             if (i < tot) gst(dst + i, v[k][j]);
         }
-        const uint16_t *lab = reinterpret_cast<const uint16_t *>(temp + t * (uint64_t)region + 128);
+        const uint16_t *lab = reinterpret_cast<const uint16_t *>(p.temp + t * (uint64_t)region + 128);
         for (uint32_t i0 = 512; i0 < tot; i0 += 512) {
             uint32_t w[8];
 #pragma unroll
@@ -1918,50 +1306,6 @@ __global__ __launch_bounds__(256) void k_compact_tiles(const uint8_t *__restrict
                 if (i < tot) gst(dst + i, w[j]);
             }
         }
-    }
-}
-
-// rows of direct tiles: one lane per row, its record walked from global
-// memory straight into the CSR
-// (asynchronous calls: res = k_compact_tiles' {total, direct rows, error
-// flags} on the device -- the count of listed rows comes from there, and
-// workgroup 0 publishes the call's status to status[0..2])
-__global__ __launch_bounds__(256) void k_rows_direct(RowsView v, const uint32_t *table, const uint64_t *rows,
-                                                     const uint32_t *list, uint64_t nlist,
-                                                     const uint64_t *offsets, uint32_t *cols,
-                                                     unsigned long long *scalars, const unsigned long long *res,
-                                                     uint64_t cap, unsigned long long *status) {
-    const uint32_t *ntab = table + 4;
-    const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + table[0]);
-    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
-    if (res) {
-        const uint64_t total = res[0], err = res[2];
-        const uint64_t st = (err & 4)   ? MBRWT_ERR_DEVICE
-                            : (err & 1) ? MBRWT_ERR_RANGE
-                            : total > cap ? MBRWT_ERR_CAPACITY
-                                          : MBRWT_OK;
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            status[0] = total;
-            status[1] = st;
-            status[2] |= 1ull << st;
-        }
-        if (st != MBRWT_OK) return;
-        nlist = res[1];
-    }
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nlist; i += gs) {
-        const uint32_t bi = gld(list + i);
-        const uint64_t row = gld(rows + bi);
-        if (row >= v.num_rows) continue;
-        uint64_t masks;
-        uint32_t count;
-        rows_locate(v, row, masks, count);
-        if (!count) continue;
-        const uint64_t base = gld(offsets + bi);
-        uint32_t k = 0;
-        const bool ok = rwt_walk(
-            ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
-            [&](uint32_t col) { gst(cols + base + k++, col); }, [](uint32_t) {});
-        if (!ok) atomicOr(&scalars[2], 2ull);
     }
 }
 
@@ -2072,70 +1416,23 @@ RowsView view_of(const Ctx &c) {
 }
 
 using RowsFn = void (*)(RowsParams);
-constexpr uint32_t kRowsWpb = 4;
-constexpr uint32_t kRows2Wpb = 8;
-constexpr uint32_t kRows3Wpb = 4;  // (72 VGPRs: 7 waves per SIMD in 4-wave workgroups)
-// MBRWT_ROWS_KERNEL=1 / 3: the first version / the software-pipelined one,
-// for A/B (2 = the default)
-int rows_version() {
-    const char *e = std::getenv("MBRWT_ROWS_KERNEL");
-    return (e && (e[0] == '1' || e[0] == '3' || e[0] == '5')) ? e[0] - '0' : 2;
-}
-bool rows_v1() { return rows_version() == 1; }
-template <int B, bool NT, int V>
-RowsFn rows2_fn_d(uint32_t frames) {
-    if constexpr (V == 2)
-        return frames <= 4 ? k_traverse_rows2<B, 4, kRows2Wpb, NT>
-               : frames <= 8 ? k_traverse_rows2<B, 8, kRows2Wpb, NT>
-                             : k_traverse_rows2<B, 16, kRows2Wpb, NT>;
-    else
-        return frames <= 4 ? k_traverse_rows3<B, 4, kRows3Wpb, NT>
-               : frames <= 8 ? k_traverse_rows3<B, 8, kRows3Wpb, NT>
-                             : k_traverse_rows3<B, 16, kRows3Wpb, NT>;
-}
-// per-lane stack slots: rows_walk4 keeps the current frame in registers and
-// pushes only on a descent, so at most frames - 1 are pending; rows_walk5
-// also writes one slot past the top (slot 0 is its dummy).  Exact sizing
-// keeps a workgroup of 8 waves within a quarter of the CU's LDS at the
-// Kingsford shape (3 frames: 8 x (4096 + 512) B + the table).
-uint32_t rows_stack_words(const RowsImage &im, uint32_t walk) {
-    return walk == 2 ? im.frames + 2 : std::max(1u, im.frames ? im.frames - 1 : 1u);  // (walks 4 and 6)
-}
-template <int V>
-RowsFn rows2_fn_v(const RowsImage &im) {
-    const bool nt = im.bytes > (1ull << 30);
-    if (im.B == 64) return nt ? rows2_fn_d<64, true, V>(im.frames) : rows2_fn_d<64, false, V>(im.frames);
-    return nt ? rows2_fn_d<128, true, V>(im.frames) : rows2_fn_d<128, false, V>(im.frames);
-}
-// v5 shape: NL loaders + NW walkers over NS slots (B = 64: 8 x 4.4 KB of slots)
-constexpr int kR5L = 4, kR5W = 4, kR5S = 8;
-template <bool NT>
-RowsFn rows5_fn_d(uint32_t B) {
-    return B == 64 ? k_traverse_rows5<64, kR5L, kR5W, kR5S, NT> : k_traverse_rows5<128, 2, 2, 4, NT>;
-}
-uint32_t rows5_wpb(const RowsImage &im) { return im.B == 64 ? kR5L + kR5W : 4u; }
-size_t rows5_lds(const RowsImage &im, uint32_t stk_words) {
-    const uint32_t ns = im.B == 64 ? kR5S : 4, nw = im.B == 64 ? kR5W : 2;
-    return ((im.table2.size() + 3) & ~size_t(3)) * 4 + ns * (64ull * im.B + 272) + ((ns + 3) & ~3u) * 4 +
-           nw * 256ull * stk_words;
-}
-RowsFn rows2_fn(const RowsImage &im) {
-    const int v = rows_version();
-    if (v == 5) return im.bytes > (1ull << 30) ? rows5_fn_d<true>(im.B) : rows5_fn_d<false>(im.B);
-    return v == 3 ? rows2_fn_v<3>(im) : rows2_fn_v<2>(im);
-}
-
+constexpr uint32_t kRowsWpb = 8;
 template <int B, bool NT>
-RowsFn rows_fn_d(uint32_t height) {
-    return height <= 4 ? k_traverse_rows<B, 4, kRowsWpb, NT>
-           : height <= 8 ? k_traverse_rows<B, 8, kRowsWpb, NT>
-                         : k_traverse_rows<B, 16, kRowsWpb, NT>;
+RowsFn rows_fn_b(uint32_t walk) {
+    return walk == WALK_ODOMETER ? k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER>
+           : walk == WALK_MASK1  ? k_traverse_rows<B, kRowsWpb, NT, WALK_MASK1>
+                                 : k_traverse_rows<B, kRowsWpb, NT, WALK_GENERAL>;
 }
-RowsFn rows_fn(const RowsImage &im) {
-    const bool nt = im.bytes > (1ull << 30);
-    if (im.B == 64) return nt ? rows_fn_d<64, true>(im.height) : rows_fn_d<64, false>(im.height);
-    return nt ? rows_fn_d<128, true>(im.height) : rows_fn_d<128, false>(im.height);
+RowsFn rows_fn(const RowsImage &im, uint32_t walk) {
+    const bool nt = im.bytes > (1ull << 30);  // non-temporal block reads for images beyond the caches
+    if (im.B == 64) return nt ? rows_fn_b<64, true>(walk) : rows_fn_b<64, false>(walk);
+    return nt ? rows_fn_b<128, true>(walk) : rows_fn_b<128, false>(walk);
 }
+// per-lane stack slots of the general walks: the current frame is held in
+// registers and only a descent pushes, so at most frames - 1 are pending.
+// Exact sizing keeps a workgroup of 8 waves within a quarter of the CU's LDS
+// at the Kingsford shape (3 frames: 8 x (4096 + 512) B + the table).
+uint32_t rows_stack_words(const RowsImage &im) { return std::max(1u, im.frames ? im.frames - 1 : 1u); }
 
 // labels per tile region: room for the tile's mean + 8 sigma
 uint32_t rows_tile_labels(const Ctx &c) {
@@ -2151,6 +1448,15 @@ struct MaskTile {
 };
 
 }  // namespace
+
+// the walk family of a context's get_rows: the odometer on uniform trees,
+// the one-byte-mask walk where every mask is one byte, else the general walk
+// (MBRWT_OPT_ROWS_WALK = 6 forces the non-odometer walk: tests)
+static uint32_t rows_walk_of(const Ctx &c) {
+    const RowsImage &im = c.rows;
+    if (im.uni && c.rows_walk != 6) return WALK_ODOMETER;
+    return im.mask1 ? WALK_MASK1 : WALK_GENERAL;
+}
 
 int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
                   uint64_t *needed, hipStream_t s, uint64_t *d_status) {
@@ -2183,14 +1489,17 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         c.rows_sc_dirty = false;
         c.rows_sc_at = sc_off;
     }
-    if ((rc = ensure(c.ws_ovf, n * sizeof(uint32_t)))) return rc;
     uint32_t *d_tc = reinterpret_cast<uint32_t *>(c.ws_counts.buf);
     uint64_t *d_to = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + to_off);
     hipcub::TransformInputIterator<uint64_t, MaskTile, const uint32_t *> it(d_tc, MaskTile());
     size_t scan_bytes = 0;
     MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, it, d_to, nt, s));
     if ((rc = ensure(c.ws_scan, scan_bytes))) return rc;
+    // the call's status block: the caller's (asynchronous) or the context's
+    unsigned long long *st_blk =
+        reinterpret_cast<unsigned long long *>(d_status ? d_status : c.d_scalars);
 
+    const uint32_t walk = rows_walk_of(c);
     RowsParams p{};
     p.rows = d_rows;
     p.n = n;
@@ -2199,51 +1508,26 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     p.spill = (uint64_t)(uintptr_t)im.spill;
     p.magic = im.magic;
     p.S = im.S;
-    const bool v1 = rows_v1();
-    p.table_words = (uint32_t)(v1 ? im.table.size() : im.table2.size());
-    p.table = v1 ? im.d_table : im.d_table2;
+    p.table_words = (uint32_t)im.table2.size();
+    p.table = im.d_table2;
     p.C = C;
     p.temp = reinterpret_cast<uint8_t *>(c.ws_temp.buf);
     p.tile_counts = d_tc;
-    p.ovf_list = reinterpret_cast<uint32_t *>(c.ws_ovf.buf);
     p.scalars = d_sc;
-    if (const char *e = std::getenv("MBRWT_ROWS_DIAG")) p.diag = (uint32_t)std::atoi(e);
-    {
-        const char *e = std::getenv("MBRWT_ROWS_WALK");
-        // default: the v6 walk when every mask is one byte, else the v4 walk
-        p.walk4 = (e && e[0] == '2')   ? 0u
-                  : (e && e[0] == '5') ? 2u
-                  : (e && e[0] == '4') ? 1u
-                  : (e && e[0] == '6') ? (im.mask1 ? 3u : 1u)
-                  : im.uni             ? 4u
-                  : im.mask1           ? 3u
-                                       : 1u;
-    }
+    p.status = st_blk;
     p.uni = im.uni;
-    p.stk_words = p.walk4 == 4 ? 0u : rows_stack_words(im, p.walk4);  // (the odometer keeps no stack)
-    // the LDS label stage: the default for the odometer (C4 kernel 0.312 ->
-    // 0.287 ms, profiles/r03/v18_stage/), opt-in for walk 6 (no gain there);
-    // MBRWT_ROWS_STAGE=0/1 overrides
-    p.stage = p.walk4 == 4 ? 1u : 0u;
-    if (const char *e = std::getenv("MBRWT_ROWS_STAGE"))
-        p.stage = ((p.walk4 == 3 || p.walk4 == 4) && e[0] == '1') ? 1u : 0u;
+    p.stk_words = walk == WALK_ODOMETER ? 0u : rows_stack_words(im);  // (the odometer keeps no stack)
 
-    const RowsFn kfn = v1 ? rows_fn(im) : rows2_fn(im);
-    const bool v5 = rows_version() == 5;
-    if (v5) p.stk_words = rows_stack_words(im, 1);  // (v5 walks with rows_walk4)
-    const uint32_t wpb = v1 ? kRowsWpb : v5 ? rows5_wpb(im) : rows_version() == 3 ? kRows3Wpb : kRows2Wpb;
-    const size_t lds = v1   ? ((im.table.size() + 3) & ~size_t(3)) * 4 + kRowsWpb * (64ull * im.B + 2ull * C)
-                       : v5 ? rows5_lds(im, p.stk_words)
-                            : ((im.table2.size() + 3) & ~size_t(3)) * 4 +
-                                  wpb * (64ull * (im.B + (rows_version() == 2 ? 4 : 0)) + 256ull * p.stk_words +
-                                         (p.stage ? 2ull * C : 0ull));
+    const RowsFn kfn = rows_fn(im, walk);
+    const uint32_t wpb = kRowsWpb;
+    const size_t lds = ((im.table2.size() + 3) & ~size_t(3)) * 4 +
+                       wpb * (64ull * (im.B + 4) + 256ull * p.stk_words + (walk == WALK_ODOMETER ? 2ull * C : 0ull));
     const uint32_t threads = 64 * wpb;
     // at most 24 waves (3 workgroups of 8) per CU: more waves make the walk phase
     // slower than the extra loads in flight gain (C4 0.426 ms at 3 against
     // 0.456 at 4, C2 0.068 against 0.073: profiles/r03/v06_rows_occupancy_*);
-    // MBRWT_ROWS_WGS_PER_CU overrides (sweeps)
-    const char *occ_e = std::getenv("MBRWT_ROWS_WGS_PER_CU");
-    const int occ_cap = occ_e ? std::max(1, std::atoi(occ_e)) : v5 ? 0 : (int)std::max(1u, 24u / wpb);
+    // MBRWT_ROWS_WGS_PER_CU (read when the image is built) overrides
+    const int occ_cap = im.occ_cap ? (int)im.occ_cap : (int)std::max(1u, 24u / wpb);
     if (c.rb_fn != reinterpret_cast<const void *>(kfn) || c.rb_lds != lds || c.rb_threads != threads ||
         c.rb_cap != occ_cap) {
         if (lds > 65536)
@@ -2255,50 +1539,13 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
                 hipSuccess ||
             per_cu <= 0)
             per_cu = 1;
-        if (occ_cap > 0) per_cu = std::min(per_cu, occ_cap);
+        per_cu = std::min(per_cu, occ_cap);
         c.rb_cap = occ_cap;
         c.rb_fn = reinterpret_cast<const void *>(kfn);
         c.rb_lds = lds;
         c.rb_threads = threads;
         c.rb_blocks = std::max(1, dev_cus) * per_cu;
     }
-    // Split batches (MBRWT_ROWS_SPLIT=k > 1: batches of >= k tiles): the
-    // batch is traversed in two halves and the first half's scan +
-    // compaction run on a side stream while the second half is traversed.
-    // Measured and left off: at C4 the overlapped compaction slows the
-    // second traversal by as much as it hides (step 0.534 vs 0.537 ms,
-    // profiles/r03/v09_split_c4.log); C2 is slower.
-    const char *split_e = std::getenv("MBRWT_ROWS_SPLIT");
-    const uint64_t split_min = split_e ? (uint64_t)std::strtoull(split_e, nullptr, 10) : 0;
-    const bool split = split_min > 1 && nt >= split_min;
-    const uint64_t nt0 = split ? nt / 2 : nt;
-    auto launch = [&](uint64_t tb, uint64_t te) -> int {
-        RowsParams q = p;
-        q.rows = d_rows + tb * 64;
-        q.n = std::min<uint64_t>(n, te * 64) - tb * 64;
-        q.temp = p.temp + tb * region;
-        q.tile_counts = d_tc + tb;
-        q.row_base = tb * 64;
-        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((te - tb + wpb - 1) / wpb, (uint64_t)c.rb_blocks));
-        hipLaunchKernelGGL(kfn, dim3((unsigned)g), dim3(threads), lds, s, q);
-        MBRWT_HIP(hipGetLastError());
-        return MBRWT_OK;
-    };
-    auto compact = [&](uint64_t tb, uint64_t te, bool last, hipStream_t st) -> int {
-        const uint64_t waves = (te - tb + kCompactTpw - 1) / kCompactTpw;
-        hipLaunchKernelGGL(k_compact_tiles, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, p.temp, C, d_tc, d_to,
-                           d_offsets, d_cols, n, tb, te, tb ? d_tc + tb - 1 : (const uint32_t *)nullptr,
-                           tb ? d_to + tb - 1 : (const uint64_t *)nullptr, cap, d_sc,
-                           last ? reinterpret_cast<unsigned long long *>(c.d_scalars) : (unsigned long long *)nullptr);
-        MBRWT_HIP(hipGetLastError());
-        return MBRWT_OK;
-    };
-    if (split && !c.side) {
-        MBRWT_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
-        MBRWT_HIP(hipEventCreateWithFlags(&c.sev_a, hipEventDisableTiming));
-        MBRWT_HIP(hipEventCreateWithFlags(&c.sev_b, hipEventDisableTiming));
-    }
-    if (split && (rc = ensure(c.ws_scan2, scan_bytes))) return rc;
 
     c.rows_sc_dirty = true;  // until k_compact_tiles has run
     hipEvent_t e0 = c.ev0, e1 = c.ev1;
@@ -2314,36 +1561,35 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         ++c.async_used;
     }
     if (c.timing) MBRWT_HIP(hipEventRecord(e0, s));
-    if ((rc = launch(0, nt0))) return rc;
-    if (!split) {
-        if (c.timing) MBRWT_HIP(hipEventRecord(e1, s));
-        MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_to, nt, s));
-        if ((rc = compact(0, nt, true, s))) return rc;
-    } else {
-        MBRWT_HIP(hipEventRecord(c.sev_a, s));
-        if ((rc = launch(nt0, nt))) return rc;
-        if (c.timing) MBRWT_HIP(hipEventRecord(e1, s));
-        MBRWT_HIP(hipStreamWaitEvent(c.side, c.sev_a, 0));
-        MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan2.buf, scan_bytes, it, d_to, nt0, c.side));
-        if ((rc = compact(0, nt0, false, c.side))) return rc;
-        MBRWT_HIP(hipEventRecord(c.sev_b, c.side));
-        MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it + nt0, d_to + nt0, nt - nt0, s));
-        MBRWT_HIP(hipStreamWaitEvent(s, c.sev_b, 0));
-        if ((rc = compact(nt0, nt, true, s))) return rc;
+    {
+        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((nt + wpb - 1) / wpb, (uint64_t)c.rb_blocks));
+        hipLaunchKernelGGL(kfn, dim3((unsigned)g), dim3(threads), lds, s, p);
+        MBRWT_HIP(hipGetLastError());
+    }
+    if (c.timing) MBRWT_HIP(hipEventRecord(e1, s));
+    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_to, nt, s));
+    {
+        CompactParams cp{};
+        cp.temp = p.temp;
+        cp.C = C;
+        cp.tile_counts = d_tc;
+        cp.tile_offsets = d_to;
+        cp.offsets = d_offsets;
+        cp.cols = d_cols;
+        cp.n = n;
+        cp.cap = cap;
+        cp.scalars = d_sc;
+        cp.status = st_blk;
+        cp.rows = d_rows;
+        cp.v = view_of(c);
+        cp.table = im.d_table;
+        const uint64_t waves = (nt + kCompactTpw - 1) / kCompactTpw;
+        hipLaunchKernelGGL(k_compact_tiles, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, cp);
+        MBRWT_HIP(hipGetLastError());
     }
     c.rows_sc_dirty = false;
-    if (d_status) {
-        // no host synchronisation: the rows of direct tiles (their count on
-        // the device) and the call's status, both behind the compaction
-        hipLaunchKernelGGL(k_rows_direct, dim3(64), dim3(256), 0, s, view_of(c), (const uint32_t *)im.d_table, d_rows,
-                           (const uint32_t *)p.ovf_list, (uint64_t)0, (const uint64_t *)d_offsets, d_cols,
-                           reinterpret_cast<unsigned long long *>(c.d_scalars) + 4,
-                           (const unsigned long long *)c.d_scalars, cap,
-                           reinterpret_cast<unsigned long long *>(d_status));
-        MBRWT_HIP(hipGetLastError());
-        return MBRWT_OK;
-    }
-    MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    if (d_status) return MBRWT_OK;  // no host synchronisation: the status lands on the stream
+    MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     MBRWT_HIP(hipStreamSynchronize(s));
     if (c.timing) {
         float ms = 0;
@@ -2351,29 +1597,14 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         c.timing_ms += ms;
         c.timing_launches += 1;
     }
-    const uint64_t total = c.h_scalars[0], ovf = c.h_scalars[1], err = c.h_scalars[2];
-    if (err & 4) {
-        set_error("row-record kernel: a tile ring wait timed out");
-        return MBRWT_ERR_DEVICE;
-    }
-    if (err & 1) {
-        set_error("row out of range");
-        return MBRWT_ERR_RANGE;
-    }
+    const uint64_t total = c.h_scalars[0], st = c.h_scalars[1];
     if (needed) *needed = total;
-    if (total > cap) {
-        set_error("cols_cap too small");
-        return MBRWT_ERR_CAPACITY;
+    switch (st) {
+        case MBRWT_OK: return MBRWT_OK;
+        case MBRWT_ERR_RANGE: set_error("row out of range"); return MBRWT_ERR_RANGE;
+        case MBRWT_ERR_CAPACITY: set_error("cols_cap too small"); return MBRWT_ERR_CAPACITY;
+        default: set_error("row-record walk failed (corrupt image)"); return MBRWT_ERR_DEVICE;
     }
-    if (ovf) {
-        const uint64_t g = std::min<uint64_t>((ovf + 255) / 256, 65536);
-        hipLaunchKernelGGL(k_rows_direct, dim3((unsigned)g), dim3(256), 0, s, view_of(c), (const uint32_t *)im.d_table,
-                           d_rows, (const uint32_t *)p.ovf_list, ovf, (const uint64_t *)d_offsets, d_cols,
-                           reinterpret_cast<unsigned long long *>(c.d_scalars), (const unsigned long long *)nullptr,
-                           (uint64_t)0, (unsigned long long *)nullptr);
-        MBRWT_HIP(hipGetLastError());
-    }
-    return MBRWT_OK;
 }
 
 namespace {
@@ -2469,7 +1700,5 @@ int rows_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap
     MBRWT_HIP(hipStreamSynchronize(s));
     return MBRWT_OK;
 }
-
-const char *rows_kernel_name() { return "k_traverse_rows"; }
 
 }  // namespace mbrwt

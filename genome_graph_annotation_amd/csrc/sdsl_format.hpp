@@ -358,12 +358,15 @@ inline std::vector<uint64_t> get_int_vector64(Reader &r) {
 // rank_level (ones before each level)}.  Level l of the tree holds bit
 // max_level - 1 - l of every symbol, the symbols stably ordered by their top l
 // bits (the wavelet tree's nodes side by side); max_level = bits of
-// max(1, largest symbol).  PARITY UNPINNED like the rest of this file.
+// max(1, largest symbol).  An empty sequence keeps the defaults of a
+// default-constructed wt_int (its constructor returns before max_level is
+// computed): max_level 0, an empty tree and empty level vectors.  PARITY
+// UNPINNED like the rest of this file.
 inline void put_wt_int(Writer &w, const std::vector<uint64_t> &seq) {
     const uint64_t n = seq.size();
     uint64_t mx = 1;
     for (uint64_t x : seq) mx = std::max(mx, x);
-    const uint32_t levels = hi_bit(mx) + 1;
+    const uint32_t levels = n ? hi_bit(mx) + 1 : 0;
     std::vector<uint64_t> sorted(seq);
     std::sort(sorted.begin(), sorted.end());
     const uint64_t sigma = n ? (uint64_t)(std::unique(sorted.begin(), sorted.end()) - sorted.begin()) : 0;
@@ -414,6 +417,7 @@ inline std::vector<uint64_t> get_wt_int(Reader &r) {
     uint32_t levels = 0;
     r.bytes(&levels, 4);
     const std::vector<uint64_t> zero_cnt = get_int_vector64(r), rank_level = get_int_vector64(r);
+    if (levels == 0 && n == 0 && tbits == 0 && zero_cnt.empty() && rank_level.empty()) return {};  // empty wt_int
     if (levels == 0 || levels > 64) throw FormatError("wt_int: bad max_level");
     if (tbits % levels || tbits / levels != n) throw FormatError("wt_int: tree size != size * max_level");
     if (zero_cnt.size() != levels || rank_level.size() != levels) throw FormatError("wt_int: level vectors");

@@ -297,7 +297,7 @@ class DeviceAllGatherV:
         if sl["ev"]:
             sl["ev"]["t0"].record(cur)
         L.check(L.lib().mbrwt_pack_csr_device(offsets.data_ptr(), self.ns[self.rank], cols.data_ptr(),
-                                              d_num_labels.data_ptr(), self.cap, self.bits_c, self.bits_l,
+                                              cols.numel(), d_num_labels.data_ptr(), self.cap, self.bits_c, self.bits_l,
                                               self.lab_off, sl["send"].data_ptr(), self.per, s),
                 "mbrwt_pack_csr_device")
         if sl["ev"]:

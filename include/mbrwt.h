@@ -188,6 +188,9 @@ void mbrwt_destroy(mbrwt_ctx *ctx);
 #define MBRWT_LAYOUT_ROWS 2
 #define MBRWT_LAYOUT_BOTH 3
 int mbrwt_set_build_option(int option, int64_t value);
+/* The calling thread's current value of a build option (so that a caller can
+   restore it after a scoped change). */
+int mbrwt_get_build_option(int option, int64_t *value);
 int mbrwt_layout(const mbrwt_ctx *ctx); /* MBRWT_LAYOUT_NODES / _ROWS / _BOTH of a context */
 /* Row-record image: out[0] block bytes B, [1] rows per block S, [2] block
    bytes, [3] spill bytes, [4] record bytes (counts + masks), [5] spilled rows,
@@ -404,14 +407,17 @@ int mbrwt_unpack_segments_device(const void *d_base, uint32_t nseg, uint64_t seg
    value i at bits [i*bits, (i+1)*bits) of the field, LSB-first)
    with num_labels read from the device (*d_num_labels, e.g. word 0 of the
    status block of mbrwt_get_rows_device_async) and the row counts taken
-   from the CSR offsets (offsets[i+1] - offsets[i]); the label field starts
+   from the CSR offsets (offsets[i+1] - offsets[i]); d_cols holds cols_cap
+   labels: num_labels > cols_cap (the rank's get_rows failed on capacity, its
+   CSR unwritten) writes the header 2^64 - 1 and nothing else, so the unpack
+   flags the exchange; the label field starts
    at byte labels_offset (a multiple of 16, at least
    mbrwt_wire_labels_offset(n_rows, bits_count): every rank of an exchange
    uses the offset of the largest slice) and needs
    ceil(labels_cap / 32) * bits_label words.
    MBRWT_ERR_INVALID when the layout does not fit wire_bytes. */
 uint64_t mbrwt_wire_labels_offset(uint64_t n_rows, uint32_t bits_count);
-int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint32_t *d_cols,
+int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint32_t *d_cols, uint64_t cols_cap,
                           const uint64_t *d_num_labels, uint64_t labels_cap, uint32_t bits_count, uint32_t bits_label,
                           uint64_t labels_offset, void *d_wire, uint64_t wire_bytes, void *stream);
 /* The labels of every segment of an all-gathered buffer of such segments
@@ -430,9 +436,11 @@ int mbrwt_unpack_labels_device(const void *d_base, uint32_t nseg, uint64_t seg_s
                                     k_traverse_fast2 where eligible, else the group kernel), 1 lane-per-row,
                                     2/3/4 group with 1/2/4 children per lane, 5/6 group at 8/6 waves per
                                     SIMD, 10 group + non-temporal reads, 17/18 k_traverse_fast2 plain /
-                                    non-temporal, 19/20 k_traverse_p2w plain / non-temporal (each falls
-                                    back to the next kernel where the tree is not eligible); others
-                                    rejected */
+                                    non-temporal, 19/20 k_traverse_p2w plain / non-temporal, 24..30
+                                    k_traverse_ptw configurations (each falls back to the next kernel where
+                                    the tree is not eligible); others rejected.  Node images only. */
+#define MBRWT_OPT_ROWS_WALK 8  /* row records: 0 default (the odometer walk on uniform trees), 6 the general
+                                   walk (A/B and tests) */
 int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value);
 
 /* Traversal-kernel time accumulated while MBRWT_OPT_TIMING is on (ms, launches); resets the sums. */

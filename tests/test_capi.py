@@ -88,7 +88,7 @@ def test_wire_layout_errors():
     assert L.lib().mbrwt_wire_labels_offset(0, 12) == 16
     assert L.lib().mbrwt_wire_labels_offset(10, 12) == 64  # 8 + one 32-value chunk (48 bytes) -> 64
     # a wire too small for its label capacity, a misaligned label offset
-    assert L.lib().mbrwt_pack_csr_device(None, 0, None, C.c_void_p(16), 1000, 12, 12, 16, C.c_void_p(16), 64,
+    assert L.lib().mbrwt_pack_csr_device(None, 0, None, 0, C.c_void_p(16), 1000, 12, 12, 16, C.c_void_p(16), 64,
                                          None) == L.MBRWT_ERR_INVALID
-    assert L.lib().mbrwt_pack_csr_device(None, 0, None, C.c_void_p(16), 0, 12, 12, 8, C.c_void_p(16), 64,
+    assert L.lib().mbrwt_pack_csr_device(None, 0, None, 0, C.c_void_p(16), 0, 12, 12, 8, C.c_void_p(16), 64,
                                          None) == L.MBRWT_ERR_INVALID

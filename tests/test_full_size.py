@@ -10,6 +10,9 @@ SURVEY §8(d) parity gate).
   position) and restates BRWT::get_row (BRWT.cpp:26-53) with exact inclusive
   ranks; it is checked against the materialised oracle tree in
   tests/test_oracle_stream.py.
+* C4: the 3.7 B x 2,652 Kingsford-shaped Multi-BRWT (BASELINE configs[3],
+  the bench's structure) as row records (the bench's layout), against the
+  same streamed oracle.
 * C5: BinRel-WT(sdsl) 1,000,000,000 x 3,173, d = 3.8 %, 10,000,000 rows
   (seed 43): the rows of the synthetic matrix are row-independent (a counter
   hash per cell), so the oracle evaluates exactly the queried rows; the
@@ -78,6 +81,55 @@ def test_c3_refseq_multibrwt_full_size(oracle_mod):
     assert np.array_equal(off_d, off_o)
     assert np.array_equal(cols_d, cols_o)
     assert 115 < len(cols_o) / batch < 126  # E[L] = 120.6 labels per row at this shape
+
+
+@pytest.mark.timeout(900)
+def test_c4_kingsford_rows_full_size(oracle_mod):
+    """BASELINE configs[3]'s structure on one GPU in the bench's layout: the
+    3.7 B x 2,652 Kingsford-shaped Multi-BRWT (d = 0.3 %, arity 8) as row
+    records, against the streamed oracle -- 2 M uniform random rows, the first
+    and last rows, the rows around every range boundary of the ranged build
+    and around 2^31 / 2^32, then the 16,384 rows of the first 4 M with the
+    most labels (long records: spilled entries and direct tiles) as a batch
+    of their own."""
+    from genome_graph_annotation_amd import BRWTDevice
+
+    n, m, d, arity = 3_700_000_000, 2652, 0.003, 8
+    t0 = time.time()
+    dev = BRWTDevice.synthetic(n, m, d, arity, 42, layout="rows")
+    build_s = time.time() - t0
+    rng = np.random.default_rng(44)
+    edges = [0, n - 1]
+    rng_rows = 2979 * 360360  # rows per range of the ranged build (capi.cpp rows_range_rows)
+    for e in list(range(rng_rows, n, rng_rows)) + [2**31, 2**32 - 1]:
+        edges += list(range(e - 8, min(e + 8, n)))
+    rows = np.concatenate([np.array(edges, dtype=np.uint64), rng.integers(0, n, 2_000_000, dtype=np.uint64)])
+    pool = rng.integers(0, n, 4_000_000, dtype=np.uint64)
+    try:
+        st = dev.rows_stats()
+        assert dev.layout() == "rows" and st["uniform_levels"] == 3
+        off_d, cols_d = dev.get_rows(rows)
+        off_p, _ = dev.get_rows(pool)
+        longest = pool[np.argsort(np.diff(off_p.astype(np.int64)), kind="stable")[-16384:]]
+        off_l, cols_l = dev.get_rows(longest)
+        dev_bytes = dev.device_bytes()
+    finally:
+        dev.close()
+        _release()
+    t0 = time.time()
+    off_o, cols_o = oracle_mod.topdown_get_rows(n, m, d, arity, 42, rows, _threads())
+    off_lo, cols_lo = oracle_mod.topdown_get_rows(n, m, d, arity, 42, longest, _threads())
+    oracle_s = time.time() - t0
+    print(f"C4 {n:,} x {m:,} rows layout: {dev_bytes / 1e9:.1f} GB built in {build_s:.1f} s "
+          f"(B={st['block_bytes']}, S={st['rows_per_block']}, {st['spilled_rows']:,} spilled, "
+          f"{st['long_rows']:,} long); {len(cols_d):,} labels for {len(rows):,} rows; long batch "
+          f"{len(cols_l):,} labels ({np.diff(off_l.astype(np.int64)).min()}+ per row); oracle {oracle_s:.0f} s; "
+          f"CSR hash device {_hash(off_d, cols_d)} oracle {_hash(off_o, cols_o)}")
+    assert np.array_equal(off_d, off_o)
+    assert np.array_equal(cols_d, cols_o)
+    assert np.array_equal(off_l, off_lo)
+    assert np.array_equal(cols_l, cols_lo)
+    assert 7.5 < len(cols_o) / len(rows) < 8.5  # E[L] = 7.96 labels per row at this shape
 
 
 @pytest.mark.timeout(900)

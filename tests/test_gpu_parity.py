@@ -20,11 +20,13 @@ def _dev(tree):
     return BRWTDevice.from_tree(tree.export())
 
 
-def _check_rows(oracle_tree, dev, rows, variants=(0, 1, 2, 4, 5, 10, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30)):
+def _check_rows(oracle_tree, dev, rows, variants=(0, 1, 2, 4, 5, 10, 17, 18, 19, 20, 24, 25, 26, 27, 28, 29, 30)):
     """Every traversal kernel (1 lane-per-row; 2/3/4 group-cooperative with
     1/2/4 children per lane; 0 the default) must
     reproduce the oracle's ordered CSR exactly."""
     from genome_graph_annotation_amd import _lib as L
+    if variants is None:
+        variants = _check_rows.__defaults__[0]
     off_o, cols_o = oracle_tree.get_rows(rows)
     for v in variants:
         dev.set_option(L.MBRWT_OPT_KERNEL, v)
@@ -156,16 +158,23 @@ def test_c1_norepl_arity2(oracle_mod, density):
     _check_rows(t, d, np.random.default_rng(42).integers(0, n, 200_000).astype(np.uint64))
 
 
-def test_c2_kingsford_small_exact(oracle_mod):
+@pytest.mark.parametrize("layout", ["nodes", "rows"])
+def test_c2_kingsford_small_exact(oracle_mod, layout):
     """BASELINE configs[1] (C2): 1M x 2,652, d=0.3%, arity 8, batch 1M --
     the reference's own generator (column-major mt19937, seed 42) and
-    bottom-up builder; every row of the batch compared bit-exactly."""
+    bottom-up builder; every row of the batch compared bit-exactly, on the
+    per-node images (every kernel variant) and on the row records (the
+    bench's layout)."""
     O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
     n, m = 1_000_000, 2652
     t = O.OracleTree.norepl(n, m, 0.003, 42, "basic", 8)
-    d = _dev(t)
+    d = BRWTDevice.from_tree(t.export(), layout=layout)
+    assert d.layout() == layout
     rows = np.random.default_rng(42).integers(0, n, 1_000_000).astype(np.uint64)
-    _check_rows(t, d, rows)
+    _check_rows(t, d, rows, variants=None if layout == "nodes" else (0,))
+    if layout == "rows":
+        assert d.traverse_kernel() == "k_traverse_rows" and d.rows_stats()["uniform_levels"] == 3
 
 
 @pytest.mark.parametrize("n,m,dens,arity", [

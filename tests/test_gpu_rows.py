@@ -123,9 +123,9 @@ def test_random_matrices_rows(oracle_mod, n, m, d, part, arity, relax, layout):
     (20000, 100, 0.05, 8, 2),      # 100 = 12 x 8 + 4: a short last group is still uniform
     (3000, 7, 1.0, 2, 0),          # singleton groups pass through: mixed depths
 ])
-def test_odometer_walk(oracle_mod, n, m, d, arity, levels, monkeypatch):
+def test_odometer_walk(oracle_mod, n, m, d, arity, levels):
     """rows_walk_uni (one lock-step iteration per reached leaf parent) and the
-    general walk (MBRWT_ROWS_WALK=6) return the oracle's CSR on uniform trees;
+    general walk (MBRWT_OPT_ROWS_WALK = 6) return the oracle's CSR on uniform trees;
     non-uniform trees report 0 levels and keep the general walk."""
     O = oracle_mod
     from genome_graph_annotation_amd import BRWTDevice
@@ -139,11 +139,9 @@ def test_odometer_walk(oracle_mod, n, m, d, arity, levels, monkeypatch):
     assert st["uniform_levels"] == levels, (st, int(nc.max()))
     rows = np.concatenate([np.arange(n), rng.integers(0, n, 20000)]).astype(np.uint64)
     off_o, cols_o = t.get_rows(rows)
-    for walk in ("", "6"):
-        if walk:
-            monkeypatch.setenv("MBRWT_ROWS_WALK", walk)
-        else:
-            monkeypatch.delenv("MBRWT_ROWS_WALK", raising=False)
+    from genome_graph_annotation_amd import _lib as L
+    for walk in (0, 6):
+        dev.set_option(L.MBRWT_OPT_ROWS_WALK, walk)
         off_d, cols_d = dev.get_rows(rows)
         np.testing.assert_array_equal(off_d, off_o)
         np.testing.assert_array_equal(cols_d, cols_o)
@@ -287,27 +285,32 @@ def test_errors_and_capacity_rows(oracle_mod):
 
 
 def test_classify_on_rows(oracle_mod):
-    """get_labels / get_top_labels batches (classify) over row records."""
+    """get_labels / get_top_labels batches (classify) over row records, against
+    the reference's semantics applied to the oracle's rows
+    (annotate_static.cpp:71-94, annotate.cpp:57-83)."""
     O = oracle_mod
     from genome_graph_annotation_amd import BRWTDevice
+    from test_gpu_parity import _ref_get_labels, _ref_top_labels
     rng = np.random.default_rng(8)
     n, m = 20000, 300
     dense = rng.random((n, m)) < 0.03
     t = O.OracleTree.from_dense(dense, "basic", 8)
     dev = BRWTDevice.from_tree(t.export(), layout="rows")
-    nodes = BRWTDevice.from_tree(t.export(), layout="nodes")
+    assert dev.layout() == "rows"
     lens = rng.integers(0, 40, 1000)
     roff = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
     rows = rng.integers(0, n, int(roff[-1])).astype(np.uint64)
+    off_o, cols_o = t.get_rows(rows)
     for ratio in (0.0, 0.5, 1.0):
-        a = dev.get_labels_batch(rows, roff, ratio)
-        b = nodes.get_labels_batch(rows, roff, ratio)
-        for x, y in zip(a, b):
+        want = _ref_get_labels(off_o, cols_o, roff, m, ratio)
+        got = dev.get_labels_batch(rows, roff, ratio)
+        for x, y in zip(got, want):
             np.testing.assert_array_equal(x, y)
-    a = dev.get_top_labels_batch(rows, roff, 5)
-    b = nodes.get_top_labels_batch(rows, roff, 5)
-    for x, y in zip(a, b):
-        np.testing.assert_array_equal(x, y)
+    for num_top in (5, 2**64 - 1):
+        want = _ref_top_labels(off_o, cols_o, roff, m, num_top)
+        got = dev.get_top_labels_batch(rows, roff, num_top)
+        for x, y in zip(got, want):
+            np.testing.assert_array_equal(x, y)
 
 
 @pytest.mark.slow

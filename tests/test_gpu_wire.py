@@ -53,7 +53,7 @@ def test_wire_segments_reassemble(oracle_mod, world, n_batch, num_columns):
     s = torch.cuda.current_stream().cuda_stream
     for r, (nr, off, cols, st) in enumerate(sl):
         seg = recv[r * per:(r + 1) * per]
-        L.check(L.lib().mbrwt_pack_csr_device(off.data_ptr(), nr, cols.data_ptr(), st.data_ptr(), cap, bits_c,
+        L.check(L.lib().mbrwt_pack_csr_device(off.data_ptr(), nr, cols.data_ptr(), cols.numel(), st.data_ptr(), cap, bits_c,
                                               bits_l, lab_off, seg.data_ptr(), per, s), "pack")
     N = sum(ns)
     cnt = torch.zeros(max(1, N), dtype=torch.int32, device="cuda")
@@ -80,7 +80,7 @@ def test_wire_segments_reassemble(oracle_mod, world, n_batch, num_columns):
         recv2 = torch.zeros(world * per2, dtype=torch.uint8, device="cuda")
         for r, (nr, off, cols, st) in enumerate(sl):
             seg = recv2[r * per2:(r + 1) * per2]
-            L.check(L.lib().mbrwt_pack_csr_device(off.data_ptr(), nr, cols.data_ptr(), st.data_ptr(), cap2, bits_c,
+            L.check(L.lib().mbrwt_pack_csr_device(off.data_ptr(), nr, cols.data_ptr(), cols.numel(), st.data_ptr(), cap2, bits_c,
                                                   bits_l, lab_off, seg.data_ptr(), per2, s), "pack")
         g2 = torch.full((world * cap2 + 32,), 7, dtype=torch.int32, device="cuda")
         L.check(L.lib().mbrwt_unpack_labels_device(recv2.data_ptr(), world, per2, lab_off, cap2, bits_l,
@@ -88,6 +88,24 @@ def test_wire_segments_reassemble(oracle_mod, world, n_batch, num_columns):
         torch.cuda.synchronize()
         assert status[1].item() == 1
         assert bool((g2 == 7).all())
+    # a rank whose own CSR is smaller than its label count (its get_rows
+    # failed on capacity): flagged through the header, its CSR never read
+    big = max(range(world), key=lambda r: int(sl[r][3][0].item()))
+    nb = int(sl[big][3][0].item())
+    if nb > 1:
+        recv3 = torch.zeros(world * per, dtype=torch.uint8, device="cuda")
+        for r, (nr, off, cols, st) in enumerate(sl):
+            seg = recv3[r * per:(r + 1) * per]
+            ccap = nb - 1 if r == big else cols.numel()
+            L.check(L.lib().mbrwt_pack_csr_device(off.data_ptr(), nr, cols.data_ptr(), ccap, st.data_ptr(), cap,
+                                                  bits_c, bits_l, lab_off, seg.data_ptr(), per, s), "pack")
+        g3 = torch.full((world * cap + 32,), 7, dtype=torch.int32, device="cuda")
+        status.fill_(-1)
+        L.check(L.lib().mbrwt_unpack_labels_device(recv3.data_ptr(), world, per, lab_off, cap, bits_l,
+                                                   g3.data_ptr(), g3.numel(), status.data_ptr(), s), "unpack")
+        torch.cuda.synchronize()
+        assert status[1].item() == 1
+        assert bool((g3 == 7).all())
 
 
 def test_device_allgatherv_one_rank(oracle_mod):

@@ -43,33 +43,18 @@ ASYNC = [False]
 status = torch.zeros(3, dtype=torch.int64, device="cuda")
 
 
-def set_variant(kv):
-    """'' default, 'v1' / 'v2' the first / second row-record kernel, 'diagN'
-    MBRWT_ROWS_DIAG=N, 'async' the timed steps through mbrwt_get_rows_device_async"""
+def set_variant(kv, m=None):
+    """'' default; 'w6' the general walk on a uniform tree (MBRWT_OPT_ROWS_WALK);
+    'async' the timed steps through mbrwt_get_rows_device_async"""
     ASYNC[0] = False
-    os.environ.pop("MBRWT_ROWS_KERNEL", None)
-    os.environ.pop("MBRWT_ROWS_DIAG", None)
-    os.environ.pop("MBRWT_ROWS_WALK", None)
-    os.environ.pop("MBRWT_ROWS_WGS_PER_CU", None)
-    os.environ.pop("MBRWT_ROWS_STAGE", None)
-    os.environ.pop("MBRWT_ROWS_SPLIT", None)
-    for part in kv.split("."):  # e.g. "w2.v2.diag1"
-        if part.startswith("w"):  # w2: the v2 walk
-            os.environ["MBRWT_ROWS_WALK"] = part[1:]
-        elif part in ("v1", "v2", "v3", "v5"):
-            os.environ["MBRWT_ROWS_KERNEL"] = part[1]
-        elif part.startswith("occ"):  # occN: at most N workgroups per CU
-            os.environ["MBRWT_ROWS_WGS_PER_CU"] = part[3:]
-        elif part == "nosplit":
-            os.environ["MBRWT_ROWS_SPLIT"] = "0"
-        elif part == "split":  # two halves, the first half's compaction on a side stream
-            os.environ["MBRWT_ROWS_SPLIT"] = "64"
-        elif part == "stage":
-            os.environ["MBRWT_ROWS_STAGE"] = "1"
+    walk = 0
+    for part in kv.split("."):  # e.g. "w6.async"
+        if part == "w6":
+            walk = 6
         elif part == "async":
             ASYNC[0] = True
-        elif part.startswith("diag"):
-            os.environ["MBRWT_ROWS_DIAG"] = part[4:]
+    if m is not None and m.layout() != "nodes":
+        m.set_option(L.MBRWT_OPT_ROWS_WALK, walk)
 
 
 # config = layout[:B,S][@variant+variant...]: one build, every variant timed on it
@@ -94,7 +79,7 @@ for cfg in a.configs.split(";") if ";" in a.configs else a.configs.split(","):
             need = e.needed
         cols = torch.empty(int(need) + 1024, dtype=torch.int32, device="cuda")
     for kv in (kvs.split("+") if kvs else [""]):
-        set_variant(kv)
+        set_variant(kv, m)
         for _ in range(3):
             nl = m.get_rows_device(rows, off, cols, s)
         torch.cuda.synchronize()
@@ -141,7 +126,7 @@ for cfg in a.configs.split(";") if ";" in a.configs else a.configs.split(","):
                "step_ms": el * 1e3, "rows_per_s": a.batch / el, "labels": int(nl), "csr_hash": hx,
                "same_as_first": hx == ref, "rows_stats": m.rows_stats()}
         print(json.dumps(out), flush=True)
-        if hx != ref and "diag" not in kv:
+        if hx != ref:
             print("MISMATCH", flush=True)
             sys.exit(1)
     set_variant("")
