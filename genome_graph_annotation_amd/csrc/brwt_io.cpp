@@ -19,6 +19,7 @@
 #include <cstring>
 #include <memory>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "mbrwt_internal.hpp"
@@ -422,6 +423,26 @@ int decode_packt(const Tree &t, uint32_t v, std::vector<Bits> &cols) {
     return MBRWT_OK;
 }
 
+// the shape of a context's tree (tree node u = dnode u + 1; the folded
+// root's record keeps no arity: its children are dnode 0's)
+void fill_shape(const Tree &t, mbrwt_tree &out) {
+    const uint32_t N = (uint32_t)t.nodes.size() - 1;
+    out.num_children.resize(N);
+    out.first_child.resize(N);
+    out.leaf_column.assign(N, UINT32_MAX);
+    out.vec_size.assign(N, 0);
+    out.words.resize(N);
+    for (uint32_t u = 0; u < N; ++u) {
+        const DevNode &dn = t.nodes[u + 1];
+        const bool internal = dn.kind != KIND_LEAF;
+        const uint32_t a = dn.kind == KIND_FOLDED ? t.nodes[0].arity : internal ? dn.arity : 0;
+        const uint32_t fc = dn.kind == KIND_FOLDED ? t.nodes[0].first_child : dn.first_child;
+        out.num_children[u] = a;
+        out.first_child[u] = a ? fc - 1 : 0;
+        if (!a) out.leaf_column[u] = t.label_perm.empty() ? dn.label : t.label_perm.at(dn.label);
+    }
+}
+
 int export_tree(const Ctx &c, mbrwt_tree &out) {
     const Tree &t = c.tree;
     out.num_rows = t.num_rows;
@@ -469,23 +490,154 @@ int export_tree(const Ctx &c, mbrwt_tree &out) {
             for (uint32_t k = 0; k < dn.arity; ++k) cols[dn.first_child + k] = std::move(ch[k]);
         }
     }
-    const uint32_t N = D - 1;
-    out.num_children.resize(N);
-    out.first_child.resize(N);
-    out.leaf_column.assign(N, UINT32_MAX);
-    out.vec_size.resize(N);
-    out.words.resize(N);
-    // the folded root's record keeps no arity: its children are dnode 0's
-    for (uint32_t u = 0; u < N; ++u) {
-        const DevNode &dn = t.nodes[u + 1];
-        const bool internal = dn.kind != KIND_LEAF;
-        const uint32_t a = dn.kind == KIND_FOLDED ? t.nodes[0].arity : internal ? dn.arity : 0;
-        const uint32_t fc = dn.kind == KIND_FOLDED ? t.nodes[0].first_child : dn.first_child;
-        out.num_children[u] = a;
-        out.first_child[u] = a ? fc - 1 : 0;
-        if (!a) out.leaf_column[u] = t.label_perm.empty() ? dn.label : t.label_perm.at(dn.label);
+    fill_shape(t, out);
+    for (uint32_t u = 0; u + 1 < D; ++u) {
         out.vec_size[u] = cols[u + 1].n;
         out.words[u] = std::move(cols[u + 1].w);
+    }
+    return MBRWT_OK;
+}
+
+// ---- export of a row-record image (rows.hip, mbrwt_internal.hpp "ROW
+// RECORDS"): a row's record is the children mask of every internal node its
+// descent reaches, in DFS pre-order, and positions in a node ascend with the
+// rows that reach it (rank1 is monotone), so reading the records in row
+// order and appending, at every reached node u, bit c of u's mask to child
+// c's column rebuilds every index column -- the inverse of k_rows_measure /
+// k_rows_write.  A record's label count is 0 exactly when the root's bit is 0
+// (a set index bit always has a set child: BRWTBottomUpBuilder's columns are
+// the OR of their children's, BRWT_builders.cpp:33-50).  Rows are split over
+// host threads; each thread's columns are appended in row order afterwards.
+struct BitAppend {
+    std::vector<uint64_t> w;
+    uint64_t n = 0;
+    void push(uint32_t bit) {
+        if ((n & 63) == 0) w.push_back(0);
+        if (bit) w.back() |= 1ull << (n & 63);
+        ++n;
+    }
+    void append(const BitAppend &o) {  // o's bits after ours
+        if (!o.n) return;
+        const uint64_t at = n;
+        w.resize((at + o.n + 63) / 64, 0);
+        for (size_t i = 0; i < o.w.size(); ++i) {
+            const uint64_t v = o.w[i], pos = at + 64 * i;
+            w[pos >> 6] |= v << (pos & 63);
+            if ((pos & 63) && (pos >> 6) + 1 < w.size()) w[(pos >> 6) + 1] |= v >> (64 - (pos & 63));
+        }
+        n = at + o.n;
+    }
+};
+
+int export_rows(const Ctx &c, mbrwt_tree &out) {
+    const Tree &t = c.tree;
+    const RowsImage &im = c.rows;
+    out.num_rows = t.num_rows;
+    out.num_columns = t.num_columns;
+    if (t.nodes.size() < 2) return MBRWT_OK;
+    const uint32_t D = (uint32_t)t.nodes.size();
+    const uint32_t rootd = t.folded ? 0u : 1u;  // the dnode holding the root's children (arity, first child)
+    const uint64_t R = t.num_rows;
+    std::vector<uint8_t> spill;
+    int rc;
+    if ((rc = copy_down((uint64_t)(uintptr_t)im.spill, im.spill_bytes, spill))) return rc;
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const uint64_t T = R < (1ull << 20) ? 1 : std::min<uint64_t>(hw, (R + (1ull << 20) - 1) >> 20);
+    // thread k: rows [a_k, a_{k+1}), block-aligned
+    std::vector<uint64_t> cut(T + 1);
+    for (uint64_t k = 0; k <= T; ++k) cut[k] = std::min<uint64_t>(R, (R * k / T + im.S - 1) / im.S * im.S);
+    cut[T] = R;
+    std::vector<std::vector<BitAppend>> part(T, std::vector<BitAppend>(D));
+    std::vector<int> prc(T, MBRWT_OK);
+    auto work = [&](uint64_t k) {
+        std::vector<BitAppend> &cols = part[k];
+        std::vector<uint8_t> blk;
+        struct Frame {
+            uint32_t fc;   // first child (dnode)
+            uint32_t rem;  // children still to visit
+        };
+        std::vector<Frame> st;
+        const uint64_t chunk_blocks = std::max<uint64_t>(1, (64ull << 20) / im.B);
+        for (uint64_t b0 = cut[k] / im.S; b0 * im.S < cut[k + 1]; b0 += chunk_blocks) {
+            const uint64_t b1 = std::min<uint64_t>((cut[k + 1] + im.S - 1) / im.S, b0 + chunk_blocks);
+            blk.resize((b1 - b0) * im.B);
+            if (hipMemcpy(blk.data(), im.blocks + b0 * im.B, blk.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+                prc[k] = MBRWT_ERR_DEVICE;
+                return;
+            }
+            for (uint64_t b = b0; b < b1; ++b) {
+                const uint8_t *bp = &blk[(b - b0) * im.B];
+                for (uint32_t tt = 0; tt < im.S; ++tt) {
+                    const uint64_t r = b * im.S + tt;
+                    if (r >= cut[k + 1]) break;
+                    const uint32_t e = bp[tt], o = e & 0x7Fu;
+                    const uint8_t *rec;
+                    uint32_t count;
+                    if (e & 0x80u) {
+                        uint32_t idx = 0;
+                        std::memcpy(&idx, bp + o + 1, 4);
+                        if ((uint64_t)idx * 16 + 8 > spill.size()) {
+                            prc[k] = MBRWT_ERR_INVALID;
+                            return;
+                        }
+                        std::memcpy(&count, &spill[(uint64_t)idx * 16], 4);
+                        rec = &spill[(uint64_t)idx * 16 + 8];
+                    } else {
+                        count = bp[o];
+                        rec = bp + o + 1;
+                    }
+                    cols[1].push(count ? 1u : 0u);
+                    if (!count) continue;
+                    uint32_t pos = 0;
+                    auto visit = [&](uint32_t v) {  // v reached: read its mask, append its children's bits
+                        const DevNode &dn = t.nodes[v];
+                        uint32_t m = rec[pos++];
+                        if (dn.arity > 8) m |= (uint32_t)rec[pos++] << 8;
+                        for (uint32_t ch = 0; ch < dn.arity; ++ch) cols[dn.first_child + ch].push((m >> ch) & 1u);
+                        st.push_back(Frame{dn.first_child, m});
+                    };
+                    st.clear();
+                    visit(rootd);
+                    while (!st.empty()) {
+                        Frame &f = st.back();
+                        if (!f.rem) {
+                            st.pop_back();
+                            continue;
+                        }
+                        const uint32_t ch = (uint32_t)__builtin_ctz(f.rem);
+                        f.rem &= f.rem - 1;
+                        const uint32_t w = f.fc + ch;
+                        if (t.nodes[w].kind != KIND_LEAF) visit(w);
+                    }
+                }
+            }
+        }
+    };
+    if (T == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (uint64_t k = 0; k < T; ++k)
+            th.emplace_back([&, k] {
+                (void)hipSetDevice(c.device);
+                work(k);
+            });
+        for (auto &x : th) x.join();
+    }
+    for (int r : prc)
+        if (r) {
+            set_error("export: row-record image unreadable");
+            return r;
+        }
+    fill_shape(t, out);
+    for (uint32_t u = 0; u + 1 < D; ++u) {
+        BitAppend &acc = part[0][u + 1];
+        for (uint64_t k = 1; k < T; ++k) {
+            acc.append(part[k][u + 1]);
+            part[k][u + 1] = BitAppend();
+        }
+        out.vec_size[u] = acc.n;
+        out.words[u] = std::move(acc.w);
     }
     return MBRWT_OK;
 }
@@ -567,11 +719,14 @@ int mbrwt_tree_export(mbrwt_ctx *ctx, mbrwt_tree **out) {
     try {
         MBRWT_HIP(hipSetDevice(c.device));
         auto t = std::make_unique<mbrwt_tree>();
-        if (c.nodes_freed) {
-            set_error("export needs the node image (context built with layout rows)");
-            return MBRWT_ERR_UNSUPPORTED;
-        }
-        if (c.shards.empty()) {
+        if (c.nodes_freed) {  // row records only: the columns from the records
+            if (!c.rows.ready) {
+                set_error("export: context without an image");
+                return MBRWT_ERR_UNSUPPORTED;
+            }
+            const int rc = export_rows(c, *t);
+            if (rc) return rc;
+        } else if (c.shards.empty()) {
             const int rc = export_tree(c, *t);
             if (rc) return rc;
         } else {

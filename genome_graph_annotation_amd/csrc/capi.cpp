@@ -96,15 +96,17 @@ static void release(Ctx *c) {
 }
 
 static int make_rows(Ctx &c, int layout);
-static int resolve_layout() {
-    const int l = build_layout();
-    return l == LAYOUT_AUTO ? LAYOUT_NODES : l;
-}
+// The layout a create call builds: NODES, ROWS or BOTH as set for the thread
+// (mbrwt_set_build_option / MBRWT_LAYOUT), else AUTO -- row records when the
+// tree is within their limits and the image fits the device, the per-node
+// images otherwise (make_rows, create_rows_ranged).
+static int resolve_layout() { return build_layout(); }
+constexpr int kNoLayoutHook = -1;
 
-// layout_hook: give the finished context the thread's build layout (row
-// records, make_rows); off for the sub-contexts of sharded / ranged builds
+// layout: the finished context's layout (row records, make_rows);
+// kNoLayoutHook for the sub-contexts of sharded / ranged builds
 template <class Build>
-static int create_common(int device, mbrwt_ctx **out, Build &&build, bool layout_hook = true) {
+static int create_common(int device, mbrwt_ctx **out, Build &&build, int layout = resolve_layout()) {
     if (!out) {
         set_error("null output pointer");
         return MBRWT_ERR_INVALID;
@@ -129,7 +131,7 @@ static int create_common(int device, mbrwt_ctx **out, Build &&build, bool layout
     }
     if (!rc) rc = build(*c);
     if (!rc) rc = upload_tables(*c);
-    if (!rc && layout_hook) rc = make_rows(*c, resolve_layout());
+    if (!rc && layout != kNoLayoutHook) rc = make_rows(*c, layout);
     if (rc) {
         release(c);
         return rc;
@@ -145,7 +147,7 @@ static const Ctx *C(const mbrwt_ctx *p) { return reinterpret_cast<const Ctx *>(p
 // [k R, min(n, (k+1) R)), built in row order by build_shard(ctx, a, b).
 template <class BuildShard>
 static int create_sharded(int device, uint64_t num_rows, uint64_t num_columns, uint64_t R, mbrwt_ctx **out,
-                          BuildShard &&build_shard) {
+                          BuildShard &&build_shard, int layout) {
     return create_common(device, out, [&](Ctx &c) {
         c.tree.num_rows = num_rows;
         c.tree.num_columns = num_columns;
@@ -153,7 +155,8 @@ static int create_sharded(int device, uint64_t num_rows, uint64_t num_columns, u
         for (uint64_t a = 0; a < num_rows; a += R) {
             const uint64_t b = std::min(num_rows, a + R);
             mbrwt_ctx *sub = nullptr;
-            const int rc = create_common(device, &sub, [&](Ctx &sc) { return build_shard(sc, a, b); }, false);
+            const int rc =
+                create_common(device, &sub, [&](Ctx &sc) { return build_shard(sc, a, b); }, kNoLayoutHook);
             if (rc) return rc;
             Ctx *sc = C(sub);
             c.shards.push_back(sc);
@@ -162,12 +165,13 @@ static int create_sharded(int device, uint64_t num_rows, uint64_t num_columns, u
             c.tree.num_nodes = sc->tree.num_nodes;
         }
         return MBRWT_OK;
-    });
+    }, layout);
 }
 
 // Row records (rows.hip) of a finished node context -- unsharded, or over
-// its row shards -- for layouts ROWS and BOTH; ROWS then drops the node
-// images (and the shards).
+// its row shards -- for layouts ROWS, BOTH and AUTO; ROWS and AUTO then drop
+// the node images (and the shards).  AUTO keeps the node images instead when
+// the tree is outside the row-record limits or the records do not fit.
 constexpr uint64_t kRowsAlign = 360360;  // a multiple of every S <= 15
 // rows per range of a ranged build: 1,073,512,440 (MBRWT_ROWS_RANGE=<rows>,
 // rounded up to a multiple of kRowsAlign, forces smaller ranges: a test hook)
@@ -189,14 +193,15 @@ static void drop_nodes(Ctx &c) {
 }
 
 static int make_rows(Ctx &c, int layout) {
-    if (layout != LAYOUT_ROWS && layout != LAYOUT_BOTH) return MBRWT_OK;
+    if (layout == LAYOUT_NODES) return MBRWT_OK;
     if (c.nodes_freed) return MBRWT_OK;
     if (c.tree.num_rows == 0) {
+        if (layout == LAYOUT_AUTO) return MBRWT_OK;
         set_error("row records of a matrix without rows");
         return MBRWT_ERR_UNSUPPORTED;
     }
     const bool sharded = !c.shards.empty();
-    RowsBuild *rb = rows_build_begin(c, c.tree.num_rows, sharded ? c.shard_rows : kRowsAlign);
+    RowsBuild *rb = rows_build_begin(c, c.tree.num_rows, sharded ? c.shard_rows : kRowsAlign, layout == LAYOUT_AUTO);
     if (!rb) return MBRWT_ERR_NOMEM;
     int rc = MBRWT_OK;
     if (!sharded) {
@@ -207,35 +212,57 @@ static int make_rows(Ctx &c, int layout) {
             if (!rc) (void)hipSetDevice(c.device);
         }
     }
-    if (rc) {
+    if (!rc) {
+        rc = rows_build_finish(rb);
+    } else {
         rows_build_abort(rb);
-        return rc;
     }
-    if ((rc = rows_build_finish(rb))) return rc;
-    if (layout == LAYOUT_ROWS) drop_nodes(c);
+    if (rc && layout == LAYOUT_AUTO && (rc == MBRWT_ERR_UNSUPPORTED || rc == MBRWT_ERR_NOMEM)) {
+        (void)hipGetLastError();
+        return MBRWT_OK;  // outside the row-record limits or too large: the per-node images answer
+    }
+    if (rc) return rc;
+    if (layout != LAYOUT_BOTH) drop_nodes(c);
     return MBRWT_OK;
 }
 
-// Layout ROWS over more than kRowsRangeRows rows: the node image of one
-// range of rows at a time (build_range(ctx, a, b), an ordinary context over
-// rows [a, b)) is turned into its rows' records and released, so the device
-// holds the records plus ONE range's node image.
+// Row records over many rows: the node image of one range of rows at a time
+// (build_range(ctx, a, b), an ordinary context over rows [a, b)) is turned
+// into its rows' records and released, so the device holds the records plus
+// ONE range's node image.  The first range is small (kRowsAlign x 64 rows);
+// it decides the record layout and measures the node image's bytes per row,
+// from which every later range is sized to the memory left (at most
+// rows_range_rows(); MBRWT_ROWS_RANGE fixes the size: a test hook).
+constexpr uint64_t kRowsFirstRange = 64 * kRowsAlign;
 template <class BuildRange>
-static int create_rows_ranged(int device, uint64_t num_rows, uint64_t num_columns, mbrwt_ctx **out,
+static int create_rows_ranged(int device, uint64_t num_rows, uint64_t num_columns, mbrwt_ctx **out, int layout,
                               BuildRange &&build_range) {
     return create_common(
         device, out,
         [&](Ctx &c) {
             c.tree.num_rows = num_rows;
             c.tree.num_columns = num_columns;
-            const uint64_t R = rows_range_rows();
-            RowsBuild *rb = rows_build_begin(c, num_rows, R);
+            const bool fixed = std::getenv("MBRWT_ROWS_RANGE") != nullptr;
+            uint64_t R = fixed ? rows_range_rows() : std::min(rows_range_rows(), kRowsFirstRange);
+            RowsBuild *rb = rows_build_begin(c, num_rows, kRowsAlign, layout == LAYOUT_AUTO);
             if (!rb) return (int)MBRWT_ERR_NOMEM;
-            for (uint64_t a = 0; a < num_rows; a += R) {
-                const uint64_t b = std::min(num_rows, a + R);
+            for (uint64_t a = 0, b = 0; a < num_rows; a = b) {
+                b = std::min(num_rows, a + R);
                 mbrwt_ctx *sub = nullptr;
-                int rc = create_common(device, &sub, [&](Ctx &sc) { return build_range(sc, a, b); }, false);
+                int rc = create_common(device, &sub, [&](Ctx &sc) { return build_range(sc, a, b); }, kNoLayoutHook);
                 if (!rc) rc = rows_build_range(rb, *C(sub), a);
+                if (!rc && !fixed && a == 0 && b < num_rows) {
+                    // later ranges: what the first range's node image costs per
+                    // row, into the memory its release leaves free
+                    const double per_row = (double)C(sub)->tree.image_bytes / (double)(b - a);
+                    size_t free_b = 0, total_b = 0;
+                    (void)hipMemGetInfo(&free_b, &total_b);
+                    const double avail = (double)free_b + (double)C(sub)->tree.image_bytes - 8.0 * (1ull << 30);
+                    const double fit = per_row > 0 ? avail / (1.3 * per_row) : (double)rows_range_rows();
+                    R = std::max<uint64_t>(kRowsAlign, std::min<uint64_t>(rows_range_rows(),
+                                                                          (uint64_t)std::max(0.0, fit) / kRowsAlign *
+                                                                              kRowsAlign));
+                }
                 if (!rc) {
                     const Tree &st = C(sub)->tree;
                     c.tree.num_relations += st.num_relations;
@@ -260,18 +287,35 @@ static int create_rows_ranged(int device, uint64_t num_rows, uint64_t num_column
             c.nodes_freed = true;
             return (int)MBRWT_OK;
         },
-        false);
+        kNoLayoutHook);
+}
+
+// Layouts ROWS and AUTO over many rows build ranged (ROWS: beyond one range;
+// AUTO: beyond kAutoRangedRows, where the whole node image and the records
+// side by side may not fit).  AUTO falls back to the per-node images when
+// the tree is outside the row-record limits or the records do not fit.
+constexpr uint64_t kAutoRangedRows = 1ull << 27;
+static bool ranged_rows(int layout, uint64_t num_rows) {
+    return (layout == LAYOUT_ROWS && num_rows > rows_range_rows()) ||
+           (layout == LAYOUT_AUTO && num_rows > kAutoRangedRows);
+}
+static bool auto_fallback(int layout, int rc) {
+    if (layout != LAYOUT_AUTO || (rc != MBRWT_ERR_UNSUPPORTED && rc != MBRWT_ERR_NOMEM)) return false;
+    (void)hipGetLastError();
+    return true;
 }
 
 // the synthetic law over row shards: shard k draws node u's masks at the
 // positions after those of shards 0..k-1 (SynthShard, synth.hip)
 static int create_synthetic_any(const mbrwt_synth_desc &desc, const mbrwt_shape_desc *shape, int device,
                                 mbrwt_ctx **out) {
-    if (resolve_layout() == LAYOUT_ROWS && desc.num_rows > rows_range_rows() && desc.num_columns) {
+    int layout = resolve_layout();
+    if (ranged_rows(layout, desc.num_rows) && desc.num_columns) {
         SynthShard st;
         std::vector<uint64_t> lens;
         st.len_out = &lens;
-        return create_rows_ranged(device, desc.num_rows, desc.num_columns, out, [&](Ctx &sc, uint64_t a, uint64_t b) {
+        const int rc =
+            create_rows_ranged(device, desc.num_rows, desc.num_columns, out, layout, [&](Ctx &sc, uint64_t a, uint64_t b) {
             mbrwt_synth_desc d = desc;
             d.num_rows = b - a;
             st.row0 = a;
@@ -281,24 +325,29 @@ static int create_synthetic_any(const mbrwt_synth_desc &desc, const mbrwt_shape_
             for (size_t u = 0; u < lens.size(); ++u) st.pos0[u] += lens[u];
             return (int)MBRWT_OK;
         });
+        if (!auto_fallback(layout, rc)) return rc;
+        layout = LAYOUT_NODES;
     }
     const uint64_t R = desc.num_columns ? shard_rows_for(desc.num_rows) : 0;
     if (!R)
-        return create_common(device, out,
-                             [&](Ctx &c) { return build_synthetic(desc, shape, device, c.tree, c.stream); });
+        return create_common(
+            device, out, [&](Ctx &c) { return build_synthetic(desc, shape, device, c.tree, c.stream); }, layout);
     SynthShard st;
     std::vector<uint64_t> lens;
     st.len_out = &lens;
-    return create_sharded(device, desc.num_rows, desc.num_columns, R, out, [&](Ctx &sc, uint64_t a, uint64_t b) {
-        mbrwt_synth_desc d = desc;
-        d.num_rows = b - a;
-        st.row0 = a;
-        const int rc = build_synthetic(d, shape, device, sc.tree, sc.stream, &st);
-        if (rc) return rc;
-        if (st.pos0.size() < lens.size()) st.pos0.resize(lens.size(), 0);
-        for (size_t u = 0; u < lens.size(); ++u) st.pos0[u] += lens[u];
-        return MBRWT_OK;
-    });
+    return create_sharded(
+        device, desc.num_rows, desc.num_columns, R, out,
+        [&](Ctx &sc, uint64_t a, uint64_t b) {
+            mbrwt_synth_desc d = desc;
+            d.num_rows = b - a;
+            st.row0 = a;
+            const int rc = build_synthetic(d, shape, device, sc.tree, sc.stream, &st);
+            if (rc) return rc;
+            if (st.pos0.size() < lens.size()) st.pos0.resize(lens.size(), 0);
+            for (size_t u = 0; u < lens.size(); ++u) st.pos0[u] += lens[u];
+            return (int)MBRWT_OK;
+        },
+        layout);
 }
 
 }  // namespace mbrwt
@@ -313,22 +362,29 @@ int mbrwt_create(const mbrwt_tree_desc *desc, int device, mbrwt_ctx **out) {
         return MBRWT_ERR_INVALID;
     }
     try {
-        if (resolve_layout() == LAYOUT_ROWS && desc->num_rows > rows_range_rows() && desc->num_nodes)
-            return create_rows_ranged(device, desc->num_rows, desc->num_columns, out,
-                                      [&](Ctx &sc, uint64_t a, uint64_t b) {
-                                          SlicedDesc sd;
-                                          const int rc = slice_desc(*desc, a, b, sd);
-                                          return rc ? rc : build_from_desc(sd.desc, device, sc.tree);
-                                      });
+        int layout = resolve_layout();
+        if (ranged_rows(layout, desc->num_rows) && desc->num_nodes) {
+            const int rc = create_rows_ranged(device, desc->num_rows, desc->num_columns, out, layout,
+                                              [&](Ctx &sc, uint64_t a, uint64_t b) {
+                                                  SlicedDesc sd;
+                                                  const int rc = slice_desc(*desc, a, b, sd);
+                                                  return rc ? rc : build_from_desc(sd.desc, device, sc.tree);
+                                              });
+            if (!auto_fallback(layout, rc)) return rc;
+            layout = LAYOUT_NODES;
+        }
         const uint64_t R = desc->num_nodes ? shard_rows_for(desc->num_rows) : 0;
-        if (R)  // rows >= 2^32: every shard is built from the description's slice
-            return create_sharded(device, desc->num_rows, desc->num_columns, R, out,
-                                  [&](Ctx &sc, uint64_t a, uint64_t b) {
-                                      SlicedDesc sd;
-                                      const int rc = slice_desc(*desc, a, b, sd);
-                                      return rc ? rc : build_from_desc(sd.desc, device, sc.tree);
-                                  });
-        return create_common(device, out, [&](Ctx &c) { return build_from_desc(*desc, device, c.tree); });
+        if (R) {  // rows >= 2^32: every shard is built from the description's slice
+            return create_sharded(
+                device, desc->num_rows, desc->num_columns, R, out,
+                [&](Ctx &sc, uint64_t a, uint64_t b) {
+                    SlicedDesc sd;
+                    const int rc = slice_desc(*desc, a, b, sd);
+                    return rc ? rc : build_from_desc(sd.desc, device, sc.tree);
+                },
+                layout);
+        }
+        return create_common(device, out, [&](Ctx &c) { return build_from_desc(*desc, device, c.tree); }, layout);
     } catch (const std::bad_alloc &) {
         set_error("host allocation failed");
         return MBRWT_ERR_NOMEM;

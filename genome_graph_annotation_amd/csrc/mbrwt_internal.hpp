@@ -379,7 +379,7 @@ struct Ctx {
 // size and rows per block (S must divide `align`: every later range starts at
 // a multiple of it).  finish_rows uploads the table and marks the image ready.
 struct RowsBuild;
-RowsBuild *rows_build_begin(Ctx &top, uint64_t num_rows, uint64_t align);
+RowsBuild *rows_build_begin(Ctx &top, uint64_t num_rows, uint64_t align, bool auto_layout = false);
 int rows_build_range(RowsBuild *rb, Ctx &range, uint64_t row0);
 int rows_build_finish(RowsBuild *rb);  // frees rb
 void rows_build_abort(RowsBuild *rb);

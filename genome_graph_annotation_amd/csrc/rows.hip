@@ -546,6 +546,7 @@ struct RowsBuild {
     Ctx *top = nullptr;
     uint64_t n = 0, align = 1;
     bool decided = false;
+    bool auto_layout = false;  // layout AUTO: decline records that cost more than kAutoMaxCost requests per row
     RowsImage img;
     unsigned long long *d_acc = nullptr;  // [0..3] measure, [4..7] plan
     uint16_t *d_sz = nullptr;
@@ -562,10 +563,11 @@ void free_rows(RowsImage &r) {
     r = RowsImage();
 }
 
-RowsBuild *rows_build_begin(Ctx &top, uint64_t num_rows, uint64_t align) {
+RowsBuild *rows_build_begin(Ctx &top, uint64_t num_rows, uint64_t align, bool auto_layout) {
     RowsBuild *rb = new (std::nothrow) RowsBuild();
     if (!rb) return nullptr;
     rb->top = &top;
+    rb->auto_layout = auto_layout;
     rb->n = num_rows;
     rb->align = std::max<uint64_t>(1, align);
     rb->s = top.stream;
@@ -698,6 +700,14 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         if (tmin == 1e300) {
             set_error("row-record image does not fit the device");
             return MBRWT_ERR_NOMEM;
+        }
+        // layout AUTO keeps the per-node images when the records are long
+        // enough that most rows would take a second (spill) request or the
+        // direct pass -- the dense-row shapes (RefSeq) -- or do not fit
+        constexpr double kAutoMaxCost = 1.25;
+        if (rb.auto_layout && tmin > kAutoMaxCost) {
+            set_error("row records too long for the block layout");
+            return MBRWT_ERR_UNSUPPORTED;
         }
         const Cand *best = nullptr;
         for (const Cand &c : cands)

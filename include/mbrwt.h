@@ -161,15 +161,19 @@ void mbrwt_destroy(mbrwt_ctx *ctx);
  *          and a record walk; the rank1 remaps are resolved at build time.
  *          Trees with arity <= 16, < 2^15 columns, height <= 16.  Built one
  *          range of rows at a time, so rows >= 2^32 need no row shards.
- *          get_column scans the records; mbrwt_tree_export is unsupported.
+ *          get_column scans the records; mbrwt_tree_export rebuilds every
+ *          index column from the records (so BinaryMatrix::serialize works).
  *   BOTH   both images: get_rows / count_labels on the records, the rest on
  *          the node image.
  * The layout is chosen when a context is created: mbrwt_set_build_option
  * (MBRWT_BUILD_LAYOUT, value) sets it for the mbrwt_create* / mbrwt_load calls
  * of the calling thread; MBRWT_LAYOUT_AUTO (the default) takes the
- * environment variable MBRWT_LAYOUT=nodes|rows|both, else NODES.  Layout ROWS
- * on a tree outside its limits -> MBRWT_ERR_UNSUPPORTED.  No reference
- * counterpart (the reference's BRWT has one sdsl layout).
+ * environment variable MBRWT_LAYOUT=nodes|rows|both, else chooses: ROWS when
+ * the tree is within the row-record limits, its records cost at most ~1.25
+ * block requests per row (no dense-row shapes) and the image fits the
+ * device, NODES otherwise.  Layout ROWS on a tree outside its limits ->
+ * MBRWT_ERR_UNSUPPORTED.  No reference counterpart (the reference's BRWT has
+ * one sdsl layout).
  */
 #define MBRWT_BUILD_LAYOUT 1
 /* (MBRWT_BUILD_PARTITIONER, value): the partitioner of the calling thread's

@@ -27,3 +27,13 @@ def oracle_mod():
     import oracle as O
     O.build()
     return O
+
+
+@pytest.fixture
+def nodes_layout():
+    """Pin the calling thread's build layout to the per-node images: the
+    tests of the node kernels, image kinds and row shards.  The library
+    default (AUTO) builds row records wherever they apply."""
+    from genome_graph_annotation_amd.brwt import build_layout
+    with build_layout("nodes"):
+        yield

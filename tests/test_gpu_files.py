@@ -9,7 +9,10 @@ import pytest
 
 from conftest import gpu_available
 
-pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU")]
+# the per-node images (the library default, AUTO, builds row records:
+# tests/test_gpu_rows.py); a test passing layout= explicitly overrides it
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU"),
+              pytest.mark.usefixtures("nodes_layout")]
 
 
 def _same_tree(a, b):
@@ -122,3 +125,73 @@ def test_dump_and_load_answers_like_the_oracle(oracle_mod):
     a, b = syn.get_rows(q), back.get_rows(q)
     np.testing.assert_array_equal(a[0], b[0])
     np.testing.assert_array_equal(a[1], b[1])
+
+
+# ---- row-record contexts (layout rows; the library default AUTO picks them) --
+
+def _rows_cases(O, rng):
+    out = []
+    for n, m, d, part, arity, relax in [(4000, 256, 0.004, "basic", 4, 0), (4000, 64, 0.01, "basic", 8, 0),
+                                        (3000, 2048, 0.04, "basic", 8, 0), (2000, 100, 0.05, "greedy", 2, 0),
+                                        (3000, 200, 0.02, "greedy", 2, 10), (1500, 40, 0.3, "basic", 12, 0),
+                                        (2000, 256, 0.02, "basic", 16, 0), (1000, 7, 1.0, "basic", 2, 0),
+                                        (1000, 9, 0.0, "basic", 3, 0)]:
+        dense = rng.random((n, m)) < d
+        dense[n // 2:n // 2 + 24] = True  # dense rows: spilled entries, records longer than a block
+        out.append((dense, O.OracleTree.from_dense(dense, part, arity, relax)))
+    return out
+
+
+def test_export_rows_layout(oracle_mod):
+    """mbrwt_tree_export of a row-record context (no node image): the index
+    columns rebuilt from the records are the ones the context was built from,
+    for every block shape the builder picks (spills and long rows included)."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    for dense, t in _rows_cases(O, np.random.default_rng(22)):
+        exp = t.export()
+        dev = BRWTDevice.from_tree(exp, layout="rows")
+        assert dev.layout() == "rows"
+        _same_tree(exp, dev.export())
+
+
+def test_export_rows_ranged_and_synthetic(oracle_mod):
+    """Export of a ranged row-record build (several ranges of rows, the
+    synthetic law across them) equals the oracle's tree of the same spec."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    old = os.environ.get("MBRWT_ROWS_RANGE")
+    os.environ["MBRWT_ROWS_RANGE"] = "360360"
+    try:
+        dev = BRWTDevice.synthetic(1_100_000, 700, 0.004, 8, 9, layout="rows")
+    finally:
+        if old is None:
+            del os.environ["MBRWT_ROWS_RANGE"]
+        else:
+            os.environ["MBRWT_ROWS_RANGE"] = old
+    _same_tree(O.OracleTree.topdown(1_100_000, 700, 0.004, 8, 9).export(), dev.export())
+    syn = BRWTDevice.synthetic(300_000, 2652, 0.003, 8, 42, layout="rows")
+    _same_tree(O.OracleTree.topdown(300_000, 2652, 0.003, 8, 42).export(), syn.export())
+
+
+def test_rows_serialize_round_trip(oracle_mod):
+    """BinaryMatrix::serialize of a row-record context (BRWT.cpp:113-128)
+    loads back through mbrwt_load (BRWT.cpp:87-111) -- into the default
+    layout -- and answers like the oracle (test_BRWT.cpp:214-238)."""
+    from genome_graph_annotation_amd import BRWTDevice
+    O = oracle_mod
+    rng = np.random.default_rng(4)
+    for dense, t in _rows_cases(O, rng)[:5]:
+        n, m = dense.shape
+        dev = BRWTDevice.from_tree(t.export(), layout="rows")
+        data = dev.serialize()
+        assert data == BRWTDevice.from_tree(t.export(), layout="nodes").serialize()
+        for layout in ("rows", None):
+            back = BRWTDevice.load(data, layout=layout)
+            rows = np.arange(n, dtype=np.uint64)
+            off_o, cols_o = t.get_rows(rows)
+            off_d, cols_d = back.get_rows(rows)
+            np.testing.assert_array_equal(off_d, off_o)
+            np.testing.assert_array_equal(cols_d, cols_o)
+            for j in sorted({0, m - 1, int(rng.integers(0, m))}):
+                np.testing.assert_array_equal(back.get_column(j), np.asarray(t.get_column(j), dtype=np.uint64))

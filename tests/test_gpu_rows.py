@@ -147,6 +147,36 @@ def test_odometer_walk(oracle_mod, n, m, d, arity, levels):
         np.testing.assert_array_equal(cols_d, cols_o)
 
 
+def test_auto_layout(oracle_mod, monkeypatch):
+    """The library default (MBRWT_LAYOUT_AUTO): row records for every tree
+    within their limits whose records fit one block request per row; the
+    per-node images for a one-column tree, nodes wider than 16 children,
+    records too long for the block layout (dense rows), or MBRWT_LAYOUT=nodes."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    rng = np.random.default_rng(12)
+    sparse = rng.random((5000, 300)) < 0.01
+    for part, arity, relax in [("basic", 8, 0), ("greedy", 2, 10), ("basic", 2, 0)]:
+        t = O.OracleTree.from_dense(sparse, part, arity, relax)
+        d = BRWTDevice.from_tree(t.export())
+        assert d.layout() == "rows" and d.traverse_kernel() == "k_traverse_rows"
+        _check_all(t, d, np.arange(5000, dtype=np.uint64), sparse, columns=False)
+    assert BRWTDevice.synthetic(200_000, 2652, 0.003, 8, 42).layout() == "rows"
+    W = (5000 + 63) // 64
+    words = [np.pad(np.packbits(sparse[:, j], bitorder="little"), (0, 8 * W - (5000 + 7) // 8)).view(np.uint64)
+             for j in range(300)]
+    assert BRWTDevice.from_columns(words, 5000, 8).layout() == "rows"
+    one = O.OracleTree.from_dense(sparse[:, :1], "basic", 2)
+    assert BRWTDevice.from_tree(one.export()).layout() == "nodes"
+    dense = rng.random((3000, 2652)) < 0.3  # ~800 labels per row: long records
+    td = O.OracleTree.from_dense(dense, "basic", 8)
+    dd = BRWTDevice.from_tree(td.export())
+    assert dd.layout() == "nodes"
+    _check_all(td, dd, np.arange(0, 3000, 7, dtype=np.uint64), dense, columns=False)
+    monkeypatch.setenv("MBRWT_LAYOUT", "nodes")
+    assert BRWTDevice.from_tree(O.OracleTree.from_dense(sparse, "basic", 8).export()).layout() == "nodes"
+
+
 def test_arity_limit(oracle_mod):
     """Nodes wider than 16 children stay on the node layout."""
     O = oracle_mod
@@ -265,9 +295,6 @@ def test_errors_and_capacity_rows(oracle_mod):
         d.get_batch([0], [20])
     with pytest.raises(MBRWTError):
         d.get_column(20)
-    with pytest.raises(MBRWTError) as ei:
-        d.export()
-    assert ei.value.status == L.MBRWT_ERR_UNSUPPORTED
     # capacity retry protocol
     rows = np.arange(100, dtype=np.uint64)
     off = np.zeros(101, dtype=np.uint64)

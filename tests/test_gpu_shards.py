@@ -19,7 +19,10 @@ import pytest
 
 from conftest import gpu_available
 
-pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU")]
+# the per-node images (the library default, AUTO, builds row records:
+# tests/test_gpu_rows.py); a test passing layout= explicitly overrides it
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU"),
+              pytest.mark.usefixtures("nodes_layout")]
 
 
 def _env(name, value, fn):
