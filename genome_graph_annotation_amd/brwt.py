@@ -303,6 +303,7 @@ class BRWTDevice:
                 "long_rows", "height")
         d = dict(zip(keys, [int(v) for v in out]))
         d["uniform_levels"] = d["height"] >> 32  # odometer walk when > 0
+        d["variable"] = d["block_bytes"] == 0  # variable-length records (csrc/rows_var.hip)
         d["height"] &= 0xFFFFFFFF
         return d
 

@@ -529,9 +529,175 @@ struct BitAppend {
     }
 };
 
+// Variable-length records (rows_var.hip): a record lists the leaf parents
+// ("units") the row reaches and their masks; every node above a reached unit
+// is reached, and its mask has the bit of each child with a reached unit
+// below.  Those masks are rebuilt per row and then appended exactly as the
+// block records' pre-order masks are.
+int export_var(const Ctx &c, mbrwt_tree &out) {
+    const Tree &t = c.tree;
+    const RowsImage &im = c.rows;
+    const uint32_t D = (uint32_t)t.nodes.size();
+    const uint32_t rootd = t.folded ? 0u : 1u;
+    const uint64_t R = t.num_rows;
+    const uint32_t W = im.var_W;
+    // unit -> dnode, dnode -> (parent, child index)
+    std::vector<uint32_t> unit_dnode(im.var_units.size(), 0), parent(D, UINT32_MAX), cidx(D, 0);
+    for (uint32_t v = 0; v < D; ++v)
+        if (im.var_unit_of[v] != 0xFFFFu) unit_dnode[im.var_unit_of[v]] = v;
+    for (uint32_t v = rootd; v < D; ++v) {
+        const DevNode &dn = t.nodes[v];
+        if (dn.kind == KIND_LEAF || dn.kind == KIND_FOLDED || (v == 0 && !t.folded)) continue;
+        for (uint32_t ch = 0; ch < dn.arity; ++ch) {
+            parent[dn.first_child + ch] = v;
+            cidx[dn.first_child + ch] = ch;
+        }
+    }
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const uint64_t T = R < (1ull << 20) ? 1 : std::min<uint64_t>(hw, (R + (1ull << 20) - 1) >> 20);
+    std::vector<uint64_t> cut(T + 1);
+    for (uint64_t k = 0; k <= T; ++k) cut[k] = std::min<uint64_t>(R, R * k / T / 13 * 13);
+    cut[T] = R;
+    std::vector<std::vector<BitAppend>> part(T, std::vector<BitAppend>(D));
+    std::vector<int> prc(T, MBRWT_OK);
+    auto work = [&](uint64_t k) {
+        std::vector<BitAppend> &cols = part[k];
+        std::vector<uint32_t> mask_of(D, 0), touched;
+        struct Frame {
+            uint32_t fc, rem;
+        };
+        std::vector<Frame> st;
+        const uint64_t g0 = cut[k] / 13, g1 = (cut[k + 1] + 12) / 13;
+        std::vector<uint8_t> lines, recs;
+        for (uint64_t ga = g0; ga < g1;) {
+            const uint64_t gb = std::min<uint64_t>(g1, ga + (1u << 16));
+            lines.resize((gb - ga) * 64);
+            if (hipMemcpy(lines.data(), im.var_lines + ga * 64, lines.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+                prc[k] = MBRWT_ERR_DEVICE;
+                return;
+            }
+            for (uint64_t g = ga; g < gb;) {
+                // a run of lines whose records are contiguous: one copy
+                uint64_t base0 = 0;
+                std::memcpy(&base0, &lines[(g - ga) * 64], 8);
+                uint64_t end = base0, ge = g;
+                while (ge < gb) {
+                    uint64_t b = 0;
+                    uint32_t span = 0;
+                    std::memcpy(&b, &lines[(ge - ga) * 64], 8);
+                    std::memcpy(&span, &lines[(ge - ga) * 64 + 8 + 4 * 13], 4);
+                    if (b != end || (end - base0) + 4ull * span > (64ull << 20)) {
+                        if (ge == g) end = b + 4ull * span, ++ge;  // (a single line always goes)
+                        break;
+                    }
+                    end = b + 4ull * span;
+                    ++ge;
+                }
+                recs.resize(end - base0);
+                if (!recs.empty() &&
+                    hipMemcpy(recs.data(), reinterpret_cast<const void *>(base0), recs.size(), hipMemcpyDeviceToHost) !=
+                        hipSuccess) {
+                    prc[k] = MBRWT_ERR_DEVICE;
+                    return;
+                }
+                for (uint64_t gl = g; gl < ge; ++gl) {
+                    const uint8_t *L = &lines[(gl - ga) * 64];
+                    uint64_t lb = 0;
+                    std::memcpy(&lb, L, 8);
+                    for (uint32_t tt = 0; tt < 13; ++tt) {
+                        const uint64_t r = gl * 13 + tt;
+                        if (r < cut[k] || r >= cut[k + 1]) continue;
+                        uint32_t e = 0;
+                        std::memcpy(&e, L + 8 + 4 * tt, 4);
+                        const uint32_t count = e >> 17;
+                        cols[1].push(count ? 1u : 0u);
+                        if (!count) continue;
+                        const uint8_t *rec = &recs[lb - base0 + 4ull * (e & 0x1FFFFu)];
+                        uint32_t item = 0;
+                        for (uint32_t wi = 0; wi < W; ++wi) {
+                            uint32_t w = 0;
+                            std::memcpy(&w, rec + 4 * wi, 4);
+                            for (; w; w &= w - 1) {
+                                const uint32_t u = wi * 32 + (uint32_t)__builtin_ctz(w);
+                                uint32_t v = unit_dnode[u];
+                                if (!mask_of[v]) touched.push_back(v);
+                                mask_of[v] = rec[4 * W + item++];
+                                while (v != rootd && parent[v] != UINT32_MAX) {
+                                    const uint32_t pv = parent[v], bit = 1u << cidx[v];
+                                    if (!mask_of[pv]) touched.push_back(pv);
+                                    const bool seen = mask_of[pv] != 0;
+                                    mask_of[pv] |= bit;
+                                    if (seen) break;  // its ancestors already have their bits
+                                    v = pv;
+                                }
+                            }
+                        }
+                        // the pre-order visit of the reached nodes (export_rows)
+                        auto visit = [&](uint32_t v) {
+                            const DevNode &dn = t.nodes[v];
+                            const uint32_t m = mask_of[v];
+                            for (uint32_t ch = 0; ch < dn.arity; ++ch) cols[dn.first_child + ch].push((m >> ch) & 1u);
+                            st.push_back(Frame{dn.first_child, m});
+                        };
+                        st.clear();
+                        visit(rootd);
+                        while (!st.empty()) {
+                            Frame &f = st.back();
+                            if (!f.rem) {
+                                st.pop_back();
+                                continue;
+                            }
+                            const uint32_t ch = (uint32_t)__builtin_ctz(f.rem);
+                            f.rem &= f.rem - 1;
+                            const uint32_t w = f.fc + ch;
+                            if (t.nodes[w].kind != KIND_LEAF) visit(w);
+                        }
+                        for (uint32_t v : touched) mask_of[v] = 0;
+                        touched.clear();
+                    }
+                }
+                g = ge;
+            }
+            ga = gb;
+        }
+    };
+    if (T == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (uint64_t k = 0; k < T; ++k)
+            th.emplace_back([&, k] {
+                (void)hipSetDevice(c.device);
+                work(k);
+            });
+        for (auto &x : th) x.join();
+    }
+    for (int r : prc)
+        if (r) {
+            set_error("export: variable-length record image unreadable");
+            return r;
+        }
+    fill_shape(t, out);
+    for (uint32_t u = 0; u + 1 < D; ++u) {
+        BitAppend &acc = part[0][u + 1];
+        for (uint64_t k = 1; k < T; ++k) {
+            acc.append(part[k][u + 1]);
+            part[k][u + 1] = BitAppend();
+        }
+        out.vec_size[u] = acc.n;
+        out.words[u] = std::move(acc.w);
+    }
+    return MBRWT_OK;
+}
+
 int export_rows(const Ctx &c, mbrwt_tree &out) {
     const Tree &t = c.tree;
     const RowsImage &im = c.rows;
+    if (im.var) {
+        out.num_rows = t.num_rows;
+        out.num_columns = t.num_columns;
+        return export_var(c, out);
+    }
     out.num_rows = t.num_rows;
     out.num_columns = t.num_columns;
     if (t.nodes.size() < 2) return MBRWT_OK;

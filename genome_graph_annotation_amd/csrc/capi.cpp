@@ -555,9 +555,9 @@ int mbrwt_rows_stats(const mbrwt_ctx *ctx, uint64_t out[8]) {
         set_error("context has no row records");
         return MBRWT_ERR_UNSUPPORTED;
     }
-    out[0] = r.B;
-    out[1] = r.S;
-    out[2] = r.num_blocks * r.B;
+    out[0] = r.var ? 0 : r.B;  // 0: variable-length records (rows_var.hip)
+    out[1] = r.var ? 13 : r.S;
+    out[2] = r.var ? (C(ctx)->tree.num_rows + 12) / 13 * 64 : r.num_blocks * r.B;
     out[3] = r.spill_bytes;
     out[4] = r.record_bytes;
     out[5] = r.spilled_rows;

@@ -264,6 +264,19 @@ struct RowsImage {
     uint32_t uni = 0;               // K internal levels above leaf parents on every path (rows_walk_uni), else 0
     uint64_t bytes = 0;             // blocks + spill used
     uint32_t occ_cap = 0;           // workgroups per CU of k_traverse_rows (0 = the default; MBRWT_ROWS_WGS_PER_CU)
+    // VARIABLE-LENGTH records (rows_var.hip; dense rows): contiguous records
+    // [unit bitmap][unit masks] addressed by 64-byte directory lines of 13 rows
+    bool var = false;
+    uint32_t var_W = 0;                 // bitmap words (units / 32, rounded up)
+    uint32_t var_G = 0;                 // lanes per row of k_var_decode (0 = from the statistics; MBRWT_VAR_G)
+    std::vector<uint32_t> var_units;    // per unit (leaf parent, DFS order): first column | arity << 16
+    std::vector<uint16_t> var_unit_of;  // per dnode: its unit, or 0xFFFF
+    std::vector<uint32_t> var_anc;      // per unit: its ancestors' dnodes at levels 0..K-1
+    uint8_t *var_lines = nullptr;       // num_rows / 13 lines x 64 bytes
+    std::vector<void *> var_chunks;     // the records, one allocation per range of rows
+    uint32_t *d_var_units = nullptr, *d_var_anc = nullptr;
+    uint16_t *d_unit_of = nullptr;
+    uint64_t var_rec_bytes = 0;
     // build statistics
     uint64_t spilled_rows = 0, long_rows = 0, record_bytes = 0, spill_bytes = 0;
 };
@@ -396,6 +409,22 @@ int rows_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_co
 int rows_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s);
 int rows_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap, uint64_t *rows_needed,
                     hipStream_t s);
+// variable-length records (rows_var.hip)
+struct VarScratch {
+    Workspace units, cnt, off, acc, scan;
+};
+bool var_prepare(const Tree &tree, RowsImage &im);  // the unit tables; false when the tree is not uniform
+int var_measure_range(RowsImage &im, const Ctx &range, VarScratch &ws, uint64_t *rec_bytes, hipStream_t s);
+int var_build_range(RowsImage &im, const Ctx &range, uint64_t row0, VarScratch &ws, hipStream_t s);
+void var_free_scratch(VarScratch &ws);
+int var_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
+                 uint64_t *needed, hipStream_t s, uint64_t *d_status);
+int var_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n, uint8_t *d_out, hipStream_t s);
+// count_labels (d_counts != null) or the V / L accounting (d_counts == null)
+int var_count(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts, uint64_t *visits, uint64_t *labels,
+              hipStream_t s);
+int var_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap, uint64_t *rows_needed,
+                   hipStream_t s);
 
 // status helpers ---------------------------------------------------------
 void set_error(const std::string &msg);

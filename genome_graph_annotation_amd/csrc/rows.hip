@@ -39,6 +39,7 @@
 #include "device_access.hpp"
 #include "mbrwt_internal.hpp"
 #include "pack_block.hpp"
+#include "rows_emit.hpp"
 
 namespace mbrwt {
 
@@ -231,179 +232,6 @@ uint32_t rwt2_uniform_levels(const std::vector<uint32_t> &t2) {
 
 namespace {
 
-// ------------------------------------------------------------------------
-// build: the masks of a row's descent over a node image
-// ------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t rec_mask_bytes(uint32_t arity) { return arity <= 8 ? 1u : 2u; }
-
-constexpr int kEmitFrames = 34;  // PLANE levels on a path (<= 32) + the super-root
-
-// the children bits of PLANE node image `nd` at position j
-__device__ __forceinline__ uint32_t plane_mask(const DevNode &nd, uint32_t j) {
-    const uint64_t blk = nd.base + (uint64_t)(j >> 5) * nd.stride;
-    const uint32_t t = j & 31;
-    uint32_t m = 0;
-    for (uint32_t c = 0; c < nd.arity; ++c) m |= ((gld_at<uint2>(blk + 8u * c).y >> t) & 1u) << c;
-    return m;
-}
-__device__ __forceinline__ uint32_t mask_at(const DevNode &nd, uint32_t j) {
-    if (nd.kind == KIND_MASK8) return gld_at<uint8_t>(nd.base + j);
-    if (nd.kind == KIND_MASK16) return gld_at<uint16_t>(nd.base + 2ull * j);
-    if (nd.kind == KIND_MASK32) return gld_at<uint32_t>(nd.base + 4ull * j);
-    return (uint32_t)gld_at<uint64_t>(nd.base + 8ull * j);  // (arity <= 16 here)
-}
-
-// Row r of a node image: emit(mask, arity) for the children mask of every
-// internal node its descent reaches, in DFS pre-order -- the row's record.
-// Returns the row's labels (set leaves), or ~0u when the descent is deeper
-// than the walker's frames.  Handles every node kind of the images
-// (PLANE, MASK*, PACK, PACK2, PACKT, a folded root).
-template <class Emit>
-__device__ uint32_t emit_row_masks(const DevNode *__restrict__ nodes, bool folded, uint32_t r, Emit emit) {
-    uint32_t fv[kEmitFrames], fj[kEmitFrames], fm[kEmitFrames];
-    int sp = 0;
-    uint32_t leaves = 0;
-    bool bad = false;
-    auto push = [&](uint32_t v, uint32_t j, uint32_t m) {
-        if (sp == kEmitFrames) {
-            bad = true;
-            return;
-        }
-        fv[sp] = v;
-        fj[sp] = j;
-        fm[sp] = m;
-        ++sp;
-    };
-    // internal dnode v at position j of its image (v's index bit is set there)
-    auto visit = [&](uint32_t v, uint32_t j) {
-        const DevNode nd = gld(nodes + v);
-        const uint32_t a = nd.arity;
-        if (nd.kind == KIND_PLANE) {
-            const uint32_t m = plane_mask(nd, j);
-            emit(m, a);
-            push(v, j, m);
-        } else if (nd.kind >= KIND_MASK8 && nd.kind <= KIND_MASK64) {
-            const uint32_t m = mask_at(nd, j);
-            emit(m, a);
-            leaves += (uint32_t)__builtin_popcount(m);
-        } else if (nd.kind == KIND_PACK) {  // children: MASK8 nodes inline
-            PackBlock pb;
-            pb.load(nd.base, j);
-            const uint32_t t = j % kPackSpan;
-            uint32_t m = 0;
-            for (uint32_t k = 0; k < a; ++k) m |= ((pb.bits(k) >> t) & 1u) << k;
-            emit(m, a);
-            uint32_t o = 0;
-            for (uint32_t k = 0; k < a; ++k) {
-                const uint32_t bk = pb.bits(k);
-                if ((bk >> t) & 1u) {
-                    const uint32_t cm = pb.mask(o + (uint32_t)__builtin_popcount(bk & ((1u << t) - 1u)));
-                    emit(cm, gld(nodes + nd.first_child + k).arity);
-                    leaves += (uint32_t)__builtin_popcount(cm);
-                }
-                o += (uint32_t)__builtin_popcount(bk);
-            }
-        } else if (nd.kind == KIND_PACK2) {  // the 3-level subtree inline (level order in the block)
-            Pack2Block pb;
-            pb.load(nd.base, j, nd.stride);
-            const uint32_t s = pb.start(j % nd.stride);
-            const uint32_t m2 = pb.byte(s);
-            emit(m2, a);
-            uint32_t o1 = s + 1, o2 = s + 1 + (uint32_t)__builtin_popcount(m2);
-            for (uint32_t A = 0; A < a; ++A) {
-                if (!((m2 >> A) & 1u)) continue;
-                const DevNode na = gld(nodes + nd.first_child + A);
-                const uint32_t m1 = pb.byte(o1++);
-                emit(m1, na.arity);
-                for (uint32_t x = m1; x; x &= x - 1) {
-                    const DevNode nb = gld(nodes + na.first_child + (uint32_t)__builtin_ctz(x));
-                    const uint32_t lm = pb.byte(o2++);
-                    emit(lm, nb.arity);
-                    leaves += (uint32_t)__builtin_popcount(lm);
-                }
-            }
-        } else if (nd.kind == KIND_PACKT) {  // the whole subtree inline, already DFS pre-order
-            Pack2Block pb;
-            pb.load(nd.base, j, nd.stride);
-            uint32_t o = pb.start(j % nd.stride) + 1;  // (the record's label count)
-            uint32_t m = pb.byte(o++);
-            if (a > 8) m |= pb.byte(o++) << 8;
-            emit(m, a);
-            constexpr int D = (int)kPacktMaxDepth;
-            uint32_t sfc[D], sm[D];
-            int tp = 0;
-            sfc[0] = nd.first_child;
-            sm[0] = m;
-            tp = 1;
-            while (tp) {
-                const int t = tp - 1;
-                if (!sm[t]) {
-                    --tp;
-                    continue;
-                }
-                const uint32_t c = (uint32_t)__builtin_ctz(sm[t]);
-                sm[t] &= sm[t] - 1;
-                const DevNode w = gld(nodes + sfc[t] + c);
-                if (w.kind == KIND_LEAF) {
-                    ++leaves;
-                    continue;
-                }
-                uint32_t mw = pb.byte(o++);
-                if (w.arity > 8) mw |= pb.byte(o++) << 8;
-                emit(mw, w.arity);
-                if (tp == D) {
-                    bad = true;
-                    return;
-                }
-                sfc[tp] = w.first_child;
-                sm[tp] = mw;
-                ++tp;
-            }
-        } else {
-            bad = true;
-        }
-    };
-    const DevNode d0 = gld(nodes);
-    if (folded) {  // dnode 0 holds the root's children over rows
-        const uint32_t m = d0.kind == KIND_PLANE ? plane_mask(d0, r) : mask_at(d0, r);
-        if (!m) return 0;
-        emit(m, d0.arity);
-        if (d0.kind == KIND_PLANE) push(0, r, m);
-        else leaves += (uint32_t)__builtin_popcount(m);
-    } else {  // dnode 0: the root's own column
-        uint32_t bit, jr = 0;
-        if (d0.kind == KIND_PLANE) {
-            const uint2 rb = gld_at<uint2>(d0.base + (uint64_t)(r >> 5) * d0.stride);
-            bit = (rb.y >> (r & 31)) & 1u;
-            jr = rb.x + (uint32_t)__builtin_popcount(rb.y & ((1u << (r & 31)) - 1u));
-        } else {
-            bit = mask_at(d0, r) & 1u;
-        }
-        if (!bit) return 0;
-        if (gld(nodes + d0.first_child).kind == KIND_LEAF) return 1;
-        visit(d0.first_child, jr);
-    }
-    while (sp > 0 && !bad) {
-        const int t = sp - 1;
-        if (!fm[t]) {
-            --sp;
-            continue;
-        }
-        const uint32_t c = (uint32_t)__builtin_ctz(fm[t]);
-        fm[t] &= fm[t] - 1;
-        const DevNode nu = gld(nodes + fv[t]);
-        const uint32_t w = nu.first_child + c;
-        if (gld(nodes + w).kind == KIND_LEAF) {
-            ++leaves;
-            continue;
-        }
-        const uint32_t j = fj[t];
-        const uint2 rb = gld_at<uint2>(nu.base + (uint64_t)(j >> 5) * nu.stride + 8u * c);
-        visit(w, rb.x + (uint32_t)__builtin_popcount(rb.y & ((1u << (j & 31)) - 1u)));
-    }
-    return bad ? ~0u : leaves;
-}
-
 // per row of a range: record size (1 + mask bytes, < 2^15) | 0x8000 when the
 // row has >= 255 labels (its count does not fit the inline byte)
 __global__ __launch_bounds__(256) void k_rows_measure(const DevNode *nodes, uint32_t folded, uint64_t n, uint16_t *sz,
@@ -412,7 +240,7 @@ __global__ __launch_bounds__(256) void k_rows_measure(const DevNode *nodes, uint
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gs) {
         uint32_t b = 1;
-        const uint32_t L = emit_row_masks(nodes, folded != 0, (uint32_t)r, [&](uint32_t, uint32_t a) { b += rec_mask_bytes(a); });
+        const uint32_t L = emit_row_masks(nodes, folded != 0, (uint32_t)r, [&](uint32_t, uint32_t a, uint32_t) { b += rec_mask_bytes(a); });
         if (L == ~0u || b >= 0x8000) {
             ++bad;
             sz[r] = 0x7FFF;
@@ -511,7 +339,7 @@ __global__ __launch_bounds__(256) void k_rows_write(const DevNode *nodes, uint32
                 const uint64_t idx = atomicAdd(spill_used, (unsigned long long)spill_units(s[t]));
                 uint8_t *se = spill + idx * 16;
                 uint32_t w = 8;
-                const uint32_t L = emit_row_masks(nodes, folded != 0, r, [&](uint32_t mk, uint32_t a) {
+                const uint32_t L = emit_row_masks(nodes, folded != 0, r, [&](uint32_t mk, uint32_t a, uint32_t) {
                     se[w++] = (uint8_t)mk;
                     if (a > 8) se[w++] = (uint8_t)(mk >> 8);
                 });
@@ -524,7 +352,7 @@ __global__ __launch_bounds__(256) void k_rows_write(const DevNode *nodes, uint32
             } else {
                 blk[t] = (uint8_t)o;
                 uint32_t w = o + 1;
-                const uint32_t L = emit_row_masks(nodes, folded != 0, r, [&](uint32_t mk, uint32_t a) {
+                const uint32_t L = emit_row_masks(nodes, folded != 0, r, [&](uint32_t mk, uint32_t a, uint32_t) {
                     blk[w++] = (uint8_t)mk;
                     if (a > 8) blk[w++] = (uint8_t)(mk >> 8);
                 });
@@ -547,6 +375,7 @@ struct RowsBuild {
     uint64_t n = 0, align = 1;
     bool decided = false;
     bool auto_layout = false;  // layout AUTO: decline records that cost more than kAutoMaxCost requests per row
+    VarScratch vws;            // variable-length records (rows_var.hip)
     RowsImage img;
     unsigned long long *d_acc = nullptr;  // [0..3] measure, [4..7] plan
     uint16_t *d_sz = nullptr;
@@ -555,6 +384,11 @@ struct RowsBuild {
 };
 
 void free_rows(RowsImage &r) {
+    for (void *p : r.var_chunks) (void)hipFree(p);
+    if (r.var_lines) (void)hipFree(r.var_lines);
+    if (r.d_var_units) (void)hipFree(r.d_var_units);
+    if (r.d_var_anc) (void)hipFree(r.d_var_anc);
+    if (r.d_unit_of) (void)hipFree(r.d_unit_of);
     if (r.blocks) (void)hipFree(r.blocks);
     if (r.spill) (void)hipFree(r.spill);
     if (r.d_spill_used) (void)hipFree(r.d_spill_used);
@@ -584,6 +418,7 @@ void rows_build_abort(RowsBuild *rb) {
     if (!rb) return;
     if (rb->d_acc) (void)hipFree(rb->d_acc);
     if (rb->d_sz) (void)hipFree(rb->d_sz);
+    var_free_scratch(rb->vws);
     free_rows(rb->img);
     delete rb;
 }
@@ -660,7 +495,7 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         set_error("row records: label count differs from the node image");
         return MBRWT_ERR_DEVICE;
     }
-    im.record_bytes += h[1];
+    if (!im.var) im.record_bytes += h[1];
     auto plan = [&](uint32_t B, uint32_t S, unsigned long long out[3]) -> int {
         MBRWT_HIP(hipMemsetAsync(rb.d_acc, 0, 8 * sizeof(unsigned long long), rb.s));
         hipLaunchKernelGGL(k_rows_plan, dim3(build_grid((nr + S - 1) / S)), dim3(256), 0, rb.s, rb.d_sz, nr, B, S,
@@ -697,38 +532,65 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         double tmin = 1e300;
         for (const Cand &c : cands)
             if (c.mem <= budget) tmin = std::min(tmin, c.t);
-        if (tmin == 1e300) {
-            set_error("row-record image does not fit the device");
-            return MBRWT_ERR_NOMEM;
-        }
-        // layout AUTO keeps the per-node images when the records are long
-        // enough that most rows would take a second (spill) request or the
-        // direct pass -- the dense-row shapes (RefSeq) -- or do not fit
+        // the variable-length records (rows_var.hip: uniform trees, ranges
+        // on directory lines): for rows too long for the blocks -- a block
+        // layout costing more than kAutoMaxCost requests per row (most rows
+        // spilled, or records longer than a block) or none that fits.
+        // MBRWT_ROWS_VAR=1 / 0 forces / forbids them (tests, A/B).
         constexpr double kAutoMaxCost = 1.25;
-        if (rb.auto_layout && tmin > kAutoMaxCost) {
-            set_error("row records too long for the block layout");
-            return MBRWT_ERR_UNSUPPORTED;
+        const char *ve = std::getenv("MBRWT_ROWS_VAR");
+        const int force_var = ve && *ve ? std::atoi(ve) : -1;
+        bool var_ok = force_var != 0 && rb.align % 13 == 0 && var_prepare(range.tree, im);
+        double var_mem = 1e300;
+        if (var_ok && (force_var == 1 || tmin > kAutoMaxCost)) {
+            uint64_t vb = 0;
+            const int rc = var_measure_range(im, range, rb.vws, &vb, rb.s);
+            if (rc && rc != MBRWT_ERR_UNSUPPORTED) return rc;
+            var_ok = rc == MBRWT_OK;
+            var_mem = (double)vb * scale * 1.02 + (double)((rb.n + 12) / 13) * 64.0 + 64.0 * (1 + rb.n / rb.align);
         }
-        const Cand *best = nullptr;
-        for (const Cand &c : cands)
-            if (c.mem <= budget && c.t <= tmin * 1.02 && (!best || c.mem < best->mem)) best = &c;
-        im.B = best->B;
-        im.S = best->S;
-        if (const char *e = std::getenv("MBRWT_ROWS_BS")) {  // A/B switch: "B,S"
-            unsigned Bv = 0, Sv = 0;
-            if (std::sscanf(e, "%u,%u", &Bv, &Sv) == 2 && (Bv == 64 || Bv == 128) && Sv >= 1 &&
-                Sv <= (Bv == 64 ? 8u : 15u) && rb.align % Sv == 0) {
-                im.B = Bv;
-                im.S = Sv;
+        if (var_ok && var_mem <= budget && (force_var == 1 || tmin > kAutoMaxCost)) {
+            im.var = true;
+            if (const char *ge = std::getenv("MBRWT_VAR_G")) im.var_G = (uint32_t)std::max(0, std::atoi(ge));
+            if (im.var_G != 0 && im.var_G != 1 && im.var_G != 2 && im.var_G != 4) im.var_G = 0;
+            const uint64_t nlines = (rb.n + 12) / 13;
+            MBRWT_HIP(hipMalloc(&im.var_lines, nlines * 64));
+            MBRWT_HIP(hipMemsetAsync(im.var_lines, 0, nlines * 64, rb.s));
+            rb.decided = true;
+        } else {
+            if (tmin == 1e300) {
+                set_error("row-record image does not fit the device");
+                return MBRWT_ERR_NOMEM;
             }
+            // layout AUTO keeps the per-node images when the records are long
+            // enough that most rows would take a second (spill) request or the
+            // direct pass and no variable-length layout applies
+            if (rb.auto_layout && tmin > kAutoMaxCost) {
+                set_error("row records too long for the block layout");
+                return MBRWT_ERR_UNSUPPORTED;
+            }
+            const Cand *best = nullptr;
+            for (const Cand &c : cands)
+                if (c.mem <= budget && c.t <= tmin * 1.02 && (!best || c.mem < best->mem)) best = &c;
+            im.B = best->B;
+            im.S = best->S;
+            if (const char *e = std::getenv("MBRWT_ROWS_BS")) {  // A/B switch: "B,S"
+                unsigned Bv = 0, Sv = 0;
+                if (std::sscanf(e, "%u,%u", &Bv, &Sv) == 2 && (Bv == 64 || Bv == 128) && Sv >= 1 &&
+                    Sv <= (Bv == 64 ? 8u : 15u) && rb.align % Sv == 0) {
+                    im.B = Bv;
+                    im.S = Sv;
+                }
+            }
+            // row / S = umulhi(row, floor(2^64 / S) + 1), exact for rows < 2^59 and S <= 16
+            im.magic = im.S > 1 ? ((uint64_t)((((unsigned __int128)1) << 64) / im.S) + 1) : 0;
+            im.num_blocks = (rb.n + im.S - 1) / im.S;
+            MBRWT_HIP(hipMalloc(&im.blocks, im.num_blocks * im.B));
+            MBRWT_HIP(hipMemsetAsync(im.blocks, 0, im.num_blocks * im.B, rb.s));
+            rb.decided = true;
         }
-        // row / S = umulhi(row, floor(2^64 / S) + 1), exact for rows < 2^59 and S <= 16
-        im.magic = im.S > 1 ? ((uint64_t)((((unsigned __int128)1) << 64) / im.S) + 1) : 0;
-        im.num_blocks = (rb.n + im.S - 1) / im.S;
-        MBRWT_HIP(hipMalloc(&im.blocks, im.num_blocks * im.B));
-        MBRWT_HIP(hipMemsetAsync(im.blocks, 0, im.num_blocks * im.B, rb.s));
-        rb.decided = true;
     }
+    if (im.var) return var_build_range(im, range, row0, rb.vws, rb.s);
     unsigned long long o[3];
     if (int rc = plan(im.B, im.S, o)) return rc;
     unsigned long long used = 0;
@@ -773,11 +635,23 @@ int rows_build_finish(RowsBuild *rbp) {
         rows_build_abort(rbp);
         return rc;
     }
-    if (!im.spill && ensure_spill(rb, 0)) {
-        rows_build_abort(rbp);
-        return MBRWT_ERR_NOMEM;
+    if (im.var) {
+        if (hipMalloc(&im.d_var_units, im.var_units.size() * 4) != hipSuccess ||
+            hipMemcpy(im.d_var_units, im.var_units.data(), im.var_units.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMalloc(&im.d_var_anc, std::max<size_t>(1, im.var_anc.size()) * 4) != hipSuccess ||
+            hipMemcpy(im.d_var_anc, im.var_anc.data(), im.var_anc.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            rc = hip_fail(hipGetLastError(), "variable-length record tables");
+            rows_build_abort(rbp);
+            return rc;
+        }
+        im.bytes = (rb.n + 12) / 13 * 64 + im.var_rec_bytes;
+    } else {
+        if (!im.spill && ensure_spill(rb, 0)) {
+            rows_build_abort(rbp);
+            return MBRWT_ERR_NOMEM;
+        }
+        im.bytes = im.num_blocks * im.B + im.spill_bytes;
     }
-    im.bytes = im.num_blocks * im.B + im.spill_bytes;
     if (const char *e = std::getenv("MBRWT_ROWS_WGS_PER_CU"))  // occupancy sweeps (read once per image)
         im.occ_cap = (uint32_t)std::max(0, std::atoi(e));
     im.ready = true;
@@ -786,6 +660,7 @@ int rows_build_finish(RowsBuild *rbp) {
     rb.img = RowsImage();  // ownership moved
     if (rb.d_acc) (void)hipFree(rb.d_acc);
     if (rb.d_sz) (void)hipFree(rb.d_sz);
+    var_free_scratch(rb.vws);
     delete rbp;
     return MBRWT_OK;
 }
@@ -1478,6 +1353,7 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         if (needed) *needed = 0;
         return MBRWT_OK;
     }
+    if (im.var) return var_get_rows(c, d_rows, n, d_offsets, d_cols, cap, needed, s, d_status);
     if (n > 0x7FFFFFF0ull) {
         set_error("batch larger than 2^31 rows");
         return MBRWT_ERR_UNSUPPORTED;
@@ -1636,6 +1512,7 @@ static uint64_t simple_grid(uint64_t n) { return std::max<uint64_t>(1, std::min<
 
 int rows_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n, uint8_t *d_out, hipStream_t s) {
     if (n == 0) return MBRWT_OK;
+    if (c.rows.var) return var_get_batch(c, d_rows, d_cols, n, d_out, s);
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
     hipLaunchKernelGGL(k_rows_get, dim3((unsigned)simple_grid(n)), dim3(256), 0, s, view_of(c),
                        (const uint32_t *)c.rows.d_table, d_rows, d_cols, n, c.tree.num_columns, d_out,
@@ -1647,6 +1524,7 @@ int rows_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint6
 }
 
 int rows_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts, hipStream_t s) {
+    if (c.rows.var) return var_count(c, d_rows, n, d_counts, nullptr, nullptr, s);
     if (c.tree.num_columns) MBRWT_HIP(hipMemsetAsync(d_counts, 0, c.tree.num_columns * sizeof(uint64_t), s));
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
     if (n)
@@ -1660,6 +1538,7 @@ int rows_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_co
 }
 
 int rows_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s) {
+    if (c.rows.var) return var_count(c, d_rows, n, nullptr, visits, labels, s);
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
     if (n)
         hipLaunchKernelGGL(k_rows_count<true>, dim3((unsigned)simple_grid(n)), dim3(256), 0, s, view_of(c),
@@ -1676,6 +1555,7 @@ int rows_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits
 
 int rows_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap, uint64_t *rows_needed,
                     hipStream_t s) {
+    if (c.rows.var) return var_get_column(c, column, d_rows, rows_cap, rows_needed, s);
     if (column >= c.tree.num_columns) {
         set_error("column out of range");
         return MBRWT_ERR_RANGE;

@@ -196,7 +196,9 @@ int mbrwt_set_build_option(int option, int64_t value);
    restore it after a scoped change). */
 int mbrwt_get_build_option(int option, int64_t *value);
 int mbrwt_layout(const mbrwt_ctx *ctx); /* MBRWT_LAYOUT_NODES / _ROWS / _BOTH of a context */
-/* Row-record image: out[0] block bytes B, [1] rows per block S, [2] block
+/* Row-record image: out[0] block bytes B (0: the variable-length records of
+   dense rows -- then [1] = 13 rows per directory line, [2] directory bytes),
+   [1] rows per block S, [2] block
    bytes, [3] spill bytes, [4] record bytes (counts + masks), [5] spilled rows,
    [6] rows longer than a block, [7] tree height | K << 32, K = the internal
    levels above the leaf parents when every path has that many (the

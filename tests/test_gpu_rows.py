@@ -170,9 +170,13 @@ def test_auto_layout(oracle_mod, monkeypatch):
     assert BRWTDevice.from_tree(one.export()).layout() == "nodes"
     dense = rng.random((3000, 2652)) < 0.3  # ~800 labels per row: long records
     td = O.OracleTree.from_dense(dense, "basic", 8)
-    dd = BRWTDevice.from_tree(td.export())
-    assert dd.layout() == "nodes"
+    dd = BRWTDevice.from_tree(td.export())  # a uniform tree: variable-length records
+    assert dd.layout() == "rows" and dd.rows_stats()["variable"]
     _check_all(td, dd, np.arange(0, 3000, 7, dtype=np.uint64), dense, columns=False)
+    tg = O.OracleTree.from_dense(dense[:, :600], "greedy", 2, 10)  # long records, not uniform: the node images
+    dg = BRWTDevice.from_tree(tg.export())
+    assert dg.layout() == "nodes"
+    _check_all(tg, dg, np.arange(0, 3000, 7, dtype=np.uint64), dense[:, :600], columns=False)
     monkeypatch.setenv("MBRWT_LAYOUT", "nodes")
     assert BRWTDevice.from_tree(O.OracleTree.from_dense(sparse, "basic", 8).export()).layout() == "nodes"
 
@@ -416,3 +420,81 @@ def test_get_rows_device_async(oracle_mod, layout):
     torch.cuda.synchronize()
     assert st.cpu().tolist() == [len(cols_o), L.MBRWT_OK, 1 << L.MBRWT_OK]
     np.testing.assert_array_equal(ct[:len(cols_o)].cpu().numpy().view(np.uint32), cols_o)
+
+
+# ---- variable-length records (csrc/rows_var.hip; dense rows) ------------------
+
+@pytest.mark.parametrize("n,m,d,arity", [
+    (5000, 3173, 0.038, 8),   # the RefSeq shape (C3), reduced rows
+    (4000, 700, 0.2, 8),
+    (3000, 64, 0.3, 2),       # binary, 5 levels above the leaf parents
+    (3000, 45, 0.5, 3),
+    (2000, 100, 0.05, 8),     # 100 = 12 x 8 + 4: a short last leaf parent
+    (2000, 300, 0.0, 8),      # no labels at all: no records
+    (1000, 2652, 0.003, 8),   # sparse (most rows without a record)
+])
+@pytest.mark.parametrize("G", ["", "1", "2", "4"])
+def test_variable_records(oracle_mod, monkeypatch, n, m, d, arity, G):
+    """The variable-length layout (forced with MBRWT_ROWS_VAR=1; every lane
+    split G) answers every row-record query like the oracle, its V / L
+    accounting equals the node image's, and its export rebuilds the tree."""
+    O = oracle_mod
+    import torch
+    from genome_graph_annotation_amd import BRWTDevice
+    monkeypatch.setenv("MBRWT_ROWS_VAR", "1")
+    if G:
+        monkeypatch.setenv("MBRWT_VAR_G", G)
+    rng = np.random.default_rng(n + m + len(G))
+    dense = rng.random((n, m)) < d
+    dense[n // 3: n // 3 + 70] = rng.random((70, m)) < 0.9  # a run of very long rows: tiles beyond the LDS budget
+    t = O.OracleTree.from_dense(dense, "basic", arity)
+    ex = t.export()
+    dev = BRWTDevice.from_tree(ex, layout="rows")
+    assert dev.layout() == "rows" and dev.rows_stats()["variable"]
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 3000), np.arange(n // 3, n // 3 + 70)]).astype(np.uint64)
+    _check_all(t, dev, rows, dense)
+    np.testing.assert_array_equal(_count_labels(dev, rows), dense[rows.astype(np.int64)].sum(axis=0))
+    rt = torch.from_numpy(rows.view(np.int64)).cuda()
+    nodes = BRWTDevice.from_tree(ex, layout="nodes")
+    assert dev.count_work_device(rt) == nodes.count_work_device(rt)
+    from test_gpu_files import _same_tree
+    _same_tree(ex, dev.export())
+
+
+def test_variable_records_ranged_async_and_errors(oracle_mod, monkeypatch):
+    """Several ranges (one record allocation each), the asynchronous call with
+    its status block, capacity and range errors on the variable layout."""
+    O = oracle_mod
+    import torch
+    from genome_graph_annotation_amd import BRWTDevice, _lib as L
+    monkeypatch.setenv("MBRWT_ROWS_RANGE", "360360")
+    monkeypatch.setenv("MBRWT_ROWS_VAR", "1")
+    n, m, d = 1_100_000, 700, 0.02
+    dev = BRWTDevice.synthetic(n, m, d, 8, 9, layout="rows")
+    assert dev.rows_stats()["variable"]
+    t = O.OracleTree.topdown(n, m, d, 8, 9)
+    rows = np.concatenate([np.arange(360350, 360370), np.arange(720710, 720730), [0, n - 1],
+                           np.random.default_rng(1).integers(0, n, 200_000)]).astype(np.uint64)
+    off_o, cols_o = t.get_rows(rows)
+    off_d, cols_d = dev.get_rows(rows)
+    np.testing.assert_array_equal(off_d, off_o)
+    np.testing.assert_array_equal(cols_d, cols_o)
+    s = torch.cuda.current_stream().cuda_stream
+    rt = torch.from_numpy(rows.view(np.int64)).cuda()
+    ot = torch.empty(len(rows) + 1, dtype=torch.int64, device="cuda")
+    ct = torch.empty(len(cols_o) + 8, dtype=torch.int32, device="cuda")
+    st = torch.zeros(3, dtype=torch.int64, device="cuda")
+    dev.get_rows_device_async(rt, ot, ct, st, s)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [len(cols_o), L.MBRWT_OK, 1 << L.MBRWT_OK]
+    np.testing.assert_array_equal(ct[:len(cols_o)].cpu().numpy().view(np.uint32), cols_o)
+    small = torch.empty(5, dtype=torch.int32, device="cuda")
+    st.zero_()
+    dev.get_rows_device_async(rt, ot, small, st, s)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist()[:2] == [len(cols_o), L.MBRWT_ERR_CAPACITY]
+    with pytest.raises(L.MBRWTError) as ei:
+        dev.get_rows(np.array([0, n], dtype=np.uint64))
+    assert ei.value.status == L.MBRWT_ERR_RANGE
+    for c in (0, 3, m - 1):
+        assert dev.get_column(c).tolist() == t.get_column(c)
