@@ -308,7 +308,9 @@ int mbrwt_unpack_labels_device(const void *d_base, uint32_t nseg, uint64_t seg_s
         return MBRWT_ERR_INVALID;
     }
     const uint64_t bound = std::min<uint64_t>(values_cap, (uint64_t)nseg * labels_cap);
-    const unsigned tiles = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((bound + kUnpackTile - 1) / kUnpackTile, 8192));
+    // one tile per workgroup (no grid-stride rounds: a workgroup's tile is
+    // two dependent memory latencies, so rounds serialise them)
+    const unsigned tiles = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((bound + kUnpackTile - 1) / kUnpackTile, 1u << 20));
     hipLaunchKernelGGL(k_unpack_labels_dev, dim3(tiles), dim3(256), 0,
                        (hipStream_t)stream, reinterpret_cast<const uint8_t *>(d_base), seg_stride, nseg, labels_offset,
                        labels_cap, bits, d_values, values_cap, reinterpret_cast<unsigned long long *>(d_status));

@@ -2126,7 +2126,7 @@ static PtwPick ptw_kernel(const Ctx &c) {
 }
 
 const char *traverse_kernel_name(const Ctx &c) {
-    if (c.rows.ready && c.kernel_variant == 0) return "k_traverse_rows";
+    if (c.rows.ready && c.kernel_variant == 0) return c.rows.var ? "k_var_decode" : "k_traverse_rows";
     if (c.nodes_freed) return "";
     if (ptw_kernel(c).fn) return "k_traverse_ptw";
     if (p2w_kernel(c)) return "k_traverse_p2w";
