@@ -11,15 +11,16 @@ plus (N > 1) the RCCL all-gatherv that reassembles the global CSR on every
 rank (pipelined: step k's exchange overlaps step k+1's traversal).
 
 Prints ONE JSON line (rank 0).
-  roofline  -- the traversal kernel's measured HBM traffic per launch
-               (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, one child pass
-               each over this same workload, at N = 1 before the timed run)
-               / its HIP-event-timed average duration / the 8 TB/s spec
-               (frac); beside it the SURVEY §8(d) algorithmic bytes
-               (64 B x V + 8 + 8 + 4 B x L per row, V and L counted exactly on
-               the device for the batch) as alg_achieved / alg_frac, and the
-               measured ceilings: a streaming read and random 64-byte
-               requests (tools/probe.hip).
+  roofline  -- the dominant kernel's layout-true algorithmic bytes per launch
+               (what its layout must read and write: alg_basis) / its
+               HIP-event-timed average duration (achieved) / the 8 TB/s spec
+               (frac); beside it the measured HBM traffic (rocprofv3 --pmc
+               FETCH_SIZE and WRITE_SIZE, one child pass each over this same
+               workload, at N = 1 before the timed run: traffic,
+               traffic_frac), SURVEY §8(d)'s probe-equivalent bytes
+               (64 B x V + 16 + 4 B x L per row, V and L counted exactly on
+               the device), and the measured ceilings: a streaming read and
+               random 64-byte requests (tools/probe.hip).
   cpu_baseline -- the oracle's restatement of BRWT::get_row on the same
                structure (built on the host from the same spec), on a bounded
                row sample, on the job's host cores and single-threaded.
@@ -54,12 +55,12 @@ FETCH_CALIB = 1.0
 
 
 # BASELINE.json configs: (rows, columns, density, batch, layout).  Row records
-# (layout rows) at the Kingsford shape; the RefSeq shape's records (~180
-# bytes, 120 labels per row) are longer than a block, so it keeps the
-# per-node layout (k_traverse_p2w).
+# (layout rows): fixed blocks at the Kingsford shape (k_traverse_rows); the
+# RefSeq shape's records (~160 bytes, 120 labels per row) are longer than a
+# block, so they take the variable-length records (k_var_decode).
 WORKLOADS = {
     "c4": dict(rows=3_700_000_000, cols=2652, density=0.003, batch=8_000_000, layout="rows"),
-    "c3": dict(rows=1_000_000_000, cols=3173, density=0.038, batch=10_000_000, layout="nodes"),
+    "c3": dict(rows=1_000_000_000, cols=3173, density=0.038, batch=10_000_000, layout="rows"),
     "c2": dict(rows=1_000_000, cols=2652, density=0.003, batch=1_000_000, layout="rows"),
 }
 
@@ -294,7 +295,7 @@ def main():
     traffic = None
     if rank == 0 and world == 1 and a.traffic != "off":
         if a.layout in ("rows", "both") and a.kernel == 0:
-            kernel_re = "k_traverse_rows"
+            kernel_re = "k_traverse_rows|k_var_decode"
         else:
             kernel_re = "k_traverse_(p2w|fast2)" if a.kernel == 0 or 17 <= a.kernel <= 23 else "k_traverse"
         if a.traffic == "live":
@@ -521,7 +522,10 @@ def main():
     # exact work accounting for the algorithmic roofline (untimed diagnostic pass)
     visits, labels = mat.count_work_device(rows_t, sptr)
     assert labels == n_lab, (labels, n_lab)
-    alg_bytes = 64 * visits + 16 * nb + 4 * labels
+    # SURVEY §8(d)'s per-row figure: 64 B per index-bit probe of the
+    # reference recursion (BRWT.cpp:30) + row id + offset + 4 B per label --
+    # "probe-equivalent": the layouts answer a row without those probes
+    probe_bytes = 64 * visits + 16 * nb + 4 * labels
     kern_ms = kern_ms_total / max(1, launches)
     kname = mat.traverse_kernel()
     rstats = mat.rows_stats()
@@ -578,25 +582,54 @@ def main():
                    "nproc": nproc}
         del ref
 
-    # roofline: measured traffic (frac) and the §8(d) algorithmic bytes (alg_frac)
+    # roofline of the dominant kernel: its layout-true algorithmic bytes per
+    # launch (the bytes the layout must move: DESIGN.md §6) / its HIP-event
+    # time (achieved, frac); the measured HBM traffic beside it (traffic,
+    # traffic_frac); SURVEY §8(d)'s probe-equivalent figure labelled as such
     ks = kern_ms / 1e3
+    alg_bytes, alg_basis = None, None
+    if rstats is not None and not rstats.get("variable"):
+        B = rstats["block_bytes"]
+        tiles = (nb + 63) // 64
+        spf = rstats["spilled_rows"] / a.rows
+        # row id + block + spill reload (spilled rows) read; count + u16 label
+        # per label + tile count written into the tile regions
+        alg_bytes = nb * (8 + B + 2) + nb * spf * B + 2 * labels + 4 * tiles
+        alg_basis = (f"k_traverse_rows: per row 8 B id + {B} B block + 2 B count, {B} B per spilled row "
+                     f"({spf:.4f} of rows), 2 B per label (u16 temp), 4 B per 64-row tile")
+    elif rstats is not None:
+        rec = rstats["record_bytes"] / a.rows
+        # loc + count + CSR offset read per row, the record's whole 16-byte
+        # chunks (~ record + 12 B), 4 B per label written into the CSR
+        alg_bytes = nb * (8 + 4 + 8 + rec + 12) + 4 * labels
+        alg_basis = (f"k_var_decode: per row 20 B (locate output, CSR offset) + {rec:.1f} B record + ~12 B "
+                     f"16-byte-chunk rounding; 4 B per label written into the CSR")
     roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": kname, "kernel_ms": kern_ms,
             "step_minus_kernel_ms": elapsed / a.steps * 1e3 - kern_ms if world == 1 else None,
-            "achieved": None, "frac": None, "traffic": None,
-            "alg_bytes_per_launch": alg_bytes, "alg_achieved": alg_bytes / ks / 1e9,
-            "alg_frac": alg_bytes / ks / 1e9 / HBM_PEAK_GBS,
+            "achieved": alg_bytes / ks / 1e9 if alg_bytes else None,
+            "frac": alg_bytes / ks / 1e9 / HBM_PEAK_GBS if alg_bytes else None,
+            "alg_bytes_per_launch": alg_bytes, "alg_basis": alg_basis, "traffic": None,
+            "probe_equivalent": {"bytes_per_launch": probe_bytes, "achieved": probe_bytes / ks / 1e9,
+                                 "frac": probe_bytes / ks / 1e9 / HBM_PEAK_GBS,
+                                 "note": "SURVEY §8(d): 64 B x V + 16 + 4 L per row, V = index-bit probes of the "
+                                         "reference recursion; the row-record layouts issue none of these probes"},
             "visits_per_row": visits / max(1, nb), "labels_per_row": labels / max(1, nb),
             "stream_read_measured": stream_gbs}
     seg = 64
-    if rstats is not None:
+    if rstats is not None and not rstats.get("variable"):
         seg = rstats["block_bytes"]
         roof["row_records"] = dict(rstats, spilled_fraction=rstats["spilled_rows"] / a.rows)
         # one block per row, plus one spill entry per spilled row
         roof["block_requests_per_launch"] = nb * (1.0 + rstats["spilled_rows"] / a.rows)
         roof["block_requests_per_s"] = roof["block_requests_per_launch"] / ks
+    elif rstats is not None:
+        roof["row_records"] = rstats
     if traffic is not None and world == 1:
         tb = traffic["traffic_bytes"]
-        roof.update({"achieved": tb / ks / 1e9, "frac": tb / ks / 1e9 / HBM_PEAK_GBS, "traffic": tb,
+        if alg_bytes is None:  # (node images: the measured bytes stand in)
+            roof.update({"achieved": tb / ks / 1e9, "frac": tb / ks / 1e9 / HBM_PEAK_GBS,
+                         "alg_basis": "measured traffic (node-image kernels)"})
+        roof.update({"traffic_achieved": tb / ks / 1e9, "traffic_frac": tb / ks / 1e9 / HBM_PEAK_GBS, "traffic": tb,
                      "read_bytes": traffic["read_bytes"], "write_bytes": traffic["write_bytes"],
                      "traffic_source": traffic.get("source", "live rocprofv3 --pmc passes of this run") +
                                        f" (sources {traffic['source_hash']})"})
@@ -608,7 +641,7 @@ def main():
         roof["ceiling_random128_per_s"] = rnd.get("seg128_per_s")
         roof["ceiling_sweep_best"] = {k: v for k, v in rnd.items() if k.endswith("_best")}
         ceil = rnd.get(f"seg{seg}_per_s")
-        if rstats is not None and ceil:
+        if rstats is not None and not rstats.get("variable") and ceil:
             roof[f"ceiling_random{seg}_frac"] = roof["block_requests_per_s"] / ceil
         elif traffic is not None and world == 1 and ceil:
             roof["ceiling_random64_frac"] = roof["read_requests_per_s"] / ceil

@@ -230,6 +230,57 @@ uint32_t rwt2_uniform_levels(const std::vector<uint32_t> &t2) {
     return K;
 }
 
+// The PATH TABLE of a uniform tree (rows_walk_path): every leaf parent's
+// first column indexed by the child indices on its path from the root,
+// idx = ((c_0 A_1 + c_1) A_2 + ...) A_{K-1} + c_{K-1}, A_k = the largest
+// arity at level k (level 0 = the root).  Appended to the RWT2 table: t2[3]
+// = its word offset, word 0 = A_1..A_{K-1} (4 bits each), then the u16
+// columns.  The odometer then never reads the table to follow a level: it
+// keeps the path index, and the leaf parent's column is one LDS read.
+// Empty (t2[3] = 0) when the table would exceed kRowsMaxPathEntries.
+constexpr uint32_t kRowsMaxPathEntries = 4096;
+void append_path_table(std::vector<uint32_t> &t2, uint32_t K) {
+    if (!K || t2.size() < 4) return;
+    std::vector<uint32_t> A(K, 0);
+    std::vector<uint32_t> lev{t2[0]};
+    for (uint32_t d = 0; d < K; ++d) {  // A[d] = the largest arity at level d
+        std::vector<uint32_t> next;
+        for (const uint32_t w : lev) {
+            const uint32_t a = (w >> 16) & 0x1Fu, f = w & 0xFFFFu;
+            A[d] = std::max(A[d], a);
+            if (d + 1 < K)
+                for (uint32_t c = 0; c < a; ++c) next.push_back(t2[4 + f + c]);
+        }
+        lev.swap(next);
+    }
+    uint64_t entries = 1;
+    for (uint32_t d = 0; d < K; ++d) entries *= A[d];
+    if (entries > kRowsMaxPathEntries || entries == 0) return;
+    std::vector<uint16_t> col(entries, 0);
+    // depth-first over the paths
+    struct F {
+        uint32_t w, idx, d;
+    };
+    std::vector<F> st{{t2[0], 0, 0}};
+    while (!st.empty()) {
+        const F fr = st.back();
+        st.pop_back();
+        const uint32_t a = (fr.w >> 16) & 0x1Fu, f = fr.w & 0xFFFFu;
+        for (uint32_t c = 0; c < a; ++c) {
+            const uint32_t e = t2[4 + f + c];
+            const uint32_t idx = fr.idx * A[fr.d] + c;
+            if (fr.d + 1 == K) col[idx] = (uint16_t)(e & 0xFFFFu);  // a leaf parent: its first column
+            else st.push_back(F{e, idx, fr.d + 1});
+        }
+    }
+    uint32_t packed = 0;
+    for (uint32_t d = 1; d < K; ++d) packed |= A[d] << (4 * (d - 1));
+    t2[3] = (uint32_t)t2.size();
+    t2.push_back(packed);
+    for (size_t i = 0; i < col.size(); i += 2)
+        t2.push_back((uint32_t)col[i] | (i + 1 < col.size() ? (uint32_t)col[i + 1] << 16 : 0u));
+}
+
 namespace {
 
 // per row of a range: record size (1 + mask bytes, < 2^15) | 0x8000 when the
@@ -474,6 +525,7 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         im.mask1 = ar8(im.table2[0]);
         for (size_t i = 4; i < im.table2.size(); ++i) im.mask1 = im.mask1 && ar8(im.table2[i]);
         im.uni = im.mask1 ? rwt2_uniform_levels(im.table2) : 0u;
+        if (im.uni) append_path_table(im.table2, im.uni);
     }
     if (nr > rb.sz_cap) {
         if (rb.d_sz) MBRWT_HIP(hipFree(rb.d_sz));
@@ -760,6 +812,7 @@ struct RowsParams {
     unsigned long long *scalars;  // the kernel's counters: [2] error flags (bit 0: row out of range)
     unsigned long long *status;   // the call's {needed, status, sticky}: status is reset here
     uint32_t uni;                 // the odometer: the tree's internal levels K (1..5)
+    uint32_t path_walk;           // the odometer over the path table when the tree has one
     uint32_t stk_words;           // per-lane LDS stack slots (general walks)
 };
 
@@ -934,6 +987,66 @@ __device__ __forceinline__ void rows_walk_uni(const AS_LDS uint8_t *pb, uint32_t
     }
 }
 
+// The odometer over the PATH TABLE (append_path_table): the same lock-step
+// iteration per reached leaf parent as rows_walk_uni, but a level keeps the
+// path index of its node instead of its table entry, so refilling a level is
+// register arithmetic (no dependent LDS read per level) and the leaf
+// parent's first column is ONE LDS read; the level refills are selects (at
+// the Kingsford shape nearly every iteration refills the level above the
+// leaf parents in some lane, so branches only added exec-mask work), and a
+// leaf parent's first label is stored unconditionally (1.01 labels per leaf
+// parent at C4), the loop only for the rest.
+template <int K>
+__device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_t o, bool live,
+                                               const AS_LDS uint16_t *ptab, uint32_t A, AS_LDS uint16_t *out,
+                                               uint32_t pos) {
+    const AS_LDS uint8_t *rc = pb + o;  // record cursor
+    uint32_t r[K], idx[K];
+    r[0] = live ? (uint32_t)rc[0] : 0u;
+    idx[0] = 0;
+    ++rc;
+#pragma unroll
+    for (int k = 1; k < K; ++k) r[k] = idx[k] = 0u;
+    uint32_t ob = pos * 2u;  // byte offset of the next label
+    while (true) {
+        uint32_t any = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) any |= r[k];
+        if (!any) break;
+        bool nd[K];  // nd[k]: levels k..K-1 are exhausted
+        nd[K - 1] = r[K - 1] == 0u;
+#pragma unroll
+        for (int k = K - 2; k >= 1; --k) nd[k] = nd[k + 1] && r[k] == 0u;
+#pragma unroll
+        for (int k = 1; k < K; ++k) {
+            const uint32_t c = (uint32_t)__builtin_ctz(r[k - 1]);
+            const uint32_t b = *rc;
+            // the node at level k is child c of the level-(k-1) node: A_{k-1}
+            // (the largest arity at level k-1) scales the parent's index
+            const uint32_t Ak = k >= 2 ? (A >> (4 * (k - 2))) & 0xFu : 0u;  // (wave-uniform)
+            const uint32_t ni = k == 1 ? c : idx[k - 1] * Ak + c;
+            idx[k] = nd[k] ? ni : idx[k];
+            r[k - 1] = nd[k] ? (r[k - 1] & (r[k - 1] - 1u)) : r[k - 1];
+            r[k] = nd[k] ? b : r[k];
+            rc += nd[k] ? 1 : 0;
+        }
+        const uint32_t c = (uint32_t)__builtin_ctz(r[K - 1]);
+        r[K - 1] &= r[K - 1] - 1u;
+        const uint32_t AK = K > 1 ? (A >> (4 * (K - 2))) & 0xFu : 0u;
+        const uint32_t base = ptab[K > 1 ? idx[K - 1] * AK + c : c];  // the leaf parent's first column
+        uint32_t x = *rc;
+        ++rc;
+        *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));
+        ob += 2u;
+        x &= x - 1u;
+        while (x) {
+            *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));
+            ob += 2u;
+            x &= x - 1u;
+        }
+    }
+}
+
 // k_traverse_rows: one wave per tile of 64 query rows (file comment).
 // B: block bytes; WPB: waves per workgroup (the RWT2 table is staged once per
 // workgroup; the grid is persistent); WALK: the walk family.
@@ -947,6 +1060,9 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
     __syncthreads();
     const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows[0]);
     const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows + 4;
+    // the path table of a uniform tree (append_path_table; 0: none)
+    const uint32_t ptw = p.path_walk ? __builtin_amdgcn_readfirstlane(lds_rows[3]) : 0u;
+    const uint32_t pA = ptw ? __builtin_amdgcn_readfirstlane(lds_rows[ptw]) : 0u;
     const uint32_t C = p.C;
     // a row's block at a stride of B + 4 bytes: lanes reading their records
     // at similar offsets hit different LDS banks (a B-byte stride puts every
@@ -1048,12 +1164,23 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
                 // SQ/TA counters showed the texture-address unit as the
                 // busiest unit)
                 AS_LDS uint16_t *stage = (AS_LDS uint16_t *)(wb + 64u * PB + 256u * p.stk_words);
-                switch (p.uni) {
-                    case 1: rows_walk_uni<1>(mine, o, live, root, ent, stage, pos); break;
-                    case 2: rows_walk_uni<2>(mine, o, live, root, ent, stage, pos); break;
-                    case 3: rows_walk_uni<3>(mine, o, live, root, ent, stage, pos); break;
-                    case 4: rows_walk_uni<4>(mine, o, live, root, ent, stage, pos); break;
-                    default: rows_walk_uni<5>(mine, o, live, root, ent, stage, pos); break;
+                if (ptw) {
+                    const AS_LDS uint16_t *ptab = (const AS_LDS uint16_t *)((const AS_LDS uint32_t *)lds_rows + ptw + 1);
+                    switch (p.uni) {
+                        case 1: rows_walk_path<1>(mine, o, live, ptab, pA, stage, pos); break;
+                        case 2: rows_walk_path<2>(mine, o, live, ptab, pA, stage, pos); break;
+                        case 3: rows_walk_path<3>(mine, o, live, ptab, pA, stage, pos); break;
+                        case 4: rows_walk_path<4>(mine, o, live, ptab, pA, stage, pos); break;
+                        default: rows_walk_path<5>(mine, o, live, ptab, pA, stage, pos); break;
+                    }
+                } else {
+                    switch (p.uni) {
+                        case 1: rows_walk_uni<1>(mine, o, live, root, ent, stage, pos); break;
+                        case 2: rows_walk_uni<2>(mine, o, live, root, ent, stage, pos); break;
+                        case 3: rows_walk_uni<3>(mine, o, live, root, ent, stage, pos); break;
+                        case 4: rows_walk_uni<4>(mine, o, live, root, ent, stage, pos); break;
+                        default: rows_walk_uni<5>(mine, o, live, root, ent, stage, pos); break;
+                    }
                 }
                 wave_sync();
                 const uint32_t nbytes = total * 2;
@@ -1339,7 +1466,7 @@ struct MaskTile {
 // (MBRWT_OPT_ROWS_WALK = 6 forces the non-odometer walk: tests)
 static uint32_t rows_walk_of(const Ctx &c) {
     const RowsImage &im = c.rows;
-    if (im.uni && c.rows_walk != 6) return WALK_ODOMETER;
+    if (im.uni && c.rows_walk != 6) return WALK_ODOMETER;  // (7: without the path table)
     return im.mask1 ? WALK_MASK1 : WALK_GENERAL;
 }
 
@@ -1402,6 +1529,7 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     p.scalars = d_sc;
     p.status = st_blk;
     p.uni = im.uni;
+    p.path_walk = c.rows_walk == 7 ? 0u : 1u;  // (7: the r03 odometer, A/B)
     p.stk_words = walk == WALK_ODOMETER ? 0u : rows_stack_words(im);  // (the odometer keeps no stack)
 
     const RowsFn kfn = rows_fn(im, walk);

@@ -124,8 +124,9 @@ def test_random_matrices_rows(oracle_mod, n, m, d, part, arity, relax, layout):
     (3000, 7, 1.0, 2, 0),          # singleton groups pass through: mixed depths
 ])
 def test_odometer_walk(oracle_mod, n, m, d, arity, levels):
-    """rows_walk_uni (one lock-step iteration per reached leaf parent) and the
-    general walk (MBRWT_OPT_ROWS_WALK = 6) return the oracle's CSR on uniform trees;
+    """rows_walk_path / rows_walk_uni (one lock-step iteration per reached leaf
+    parent, with / without the path table) and the general walk
+    (MBRWT_OPT_ROWS_WALK = 6) return the oracle's CSR on uniform trees;
     non-uniform trees report 0 levels and keep the general walk."""
     O = oracle_mod
     from genome_graph_annotation_amd import BRWTDevice
@@ -140,7 +141,7 @@ def test_odometer_walk(oracle_mod, n, m, d, arity, levels):
     rows = np.concatenate([np.arange(n), rng.integers(0, n, 20000)]).astype(np.uint64)
     off_o, cols_o = t.get_rows(rows)
     from genome_graph_annotation_amd import _lib as L
-    for walk in (0, 6):
+    for walk in (0, 6, 7):  # the path-table odometer, the general walk, the r03 odometer
         dev.set_option(L.MBRWT_OPT_ROWS_WALK, walk)
         off_d, cols_d = dev.get_rows(rows)
         np.testing.assert_array_equal(off_d, off_o)

@@ -49,8 +49,8 @@ def set_variant(kv, m=None):
     ASYNC[0] = False
     walk = 0
     for part in kv.split("."):  # e.g. "w6.async"
-        if part == "w6":
-            walk = 6
+        if part in ("w6", "w7"):  # the general walk / the odometer without the path table
+            walk = int(part[1])
         elif part == "async":
             ASYNC[0] = True
     if m is not None and m.layout() != "nodes":
