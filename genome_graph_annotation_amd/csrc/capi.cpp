@@ -290,14 +290,15 @@ static int create_rows_ranged(int device, uint64_t num_rows, uint64_t num_column
         kNoLayoutHook);
 }
 
-// Layouts ROWS and AUTO over many rows build ranged (ROWS: beyond one range;
-// AUTO: beyond kAutoRangedRows, where the whole node image and the records
-// side by side may not fit).  AUTO falls back to the per-node images when
-// the tree is outside the row-record limits or the records do not fit.
+// Layouts ROWS and AUTO over many rows build ranged: beyond kAutoRangedRows
+// the whole node image and the records side by side may not fit (C3: 214 GB
+// of node image + 160 GB of records).  AUTO falls back to the per-node
+// images when the tree is outside the row-record limits or the records do
+// not fit.  (MBRWT_ROWS_RANGE: ranged beyond one such range, a test hook.)
 constexpr uint64_t kAutoRangedRows = 1ull << 27;
 static bool ranged_rows(int layout, uint64_t num_rows) {
-    return (layout == LAYOUT_ROWS && num_rows > rows_range_rows()) ||
-           (layout == LAYOUT_AUTO && num_rows > kAutoRangedRows);
+    return (layout == LAYOUT_ROWS || layout == LAYOUT_AUTO) &&
+           num_rows > std::min<uint64_t>(kAutoRangedRows, rows_range_rows());
 }
 static bool auto_fallback(int layout, int rc) {
     if (layout != LAYOUT_AUTO || (rc != MBRWT_ERR_UNSUPPORTED && rc != MBRWT_ERR_NOMEM)) return false;
