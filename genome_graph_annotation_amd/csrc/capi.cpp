@@ -253,12 +253,15 @@ static int create_rows_ranged(int device, uint64_t num_rows, uint64_t num_column
                 if (!rc) rc = rows_build_range(rb, *C(sub), a);
                 if (!rc && !fixed && a == 0 && b < num_rows) {
                     // later ranges: what the first range's node image costs per
-                    // row, into the memory its release leaves free
+                    // row, into the memory its release leaves free less the
+                    // records the later ranges will still allocate (the
+                    // variable-length records: one allocation per range)
                     const double per_row = (double)C(sub)->tree.image_bytes / (double)(b - a);
                     size_t free_b = 0, total_b = 0;
                     (void)hipMemGetInfo(&free_b, &total_b);
-                    const double avail = (double)free_b + (double)C(sub)->tree.image_bytes - 8.0 * (1ull << 30);
-                    const double fit = per_row > 0 ? avail / (1.3 * per_row) : (double)rows_range_rows();
+                    const double avail = (double)free_b + (double)C(sub)->tree.image_bytes - 8.0 * (1ull << 30) -
+                                         (double)rows_build_pending_bytes(rb, num_rows - b);
+                    const double fit = per_row > 0 ? avail / (1.2 * per_row) : (double)rows_range_rows();
                     R = std::max<uint64_t>(kRowsAlign, std::min<uint64_t>(rows_range_rows(),
                                                                           (uint64_t)std::max(0.0, fit) / kRowsAlign *
                                                                               kRowsAlign));

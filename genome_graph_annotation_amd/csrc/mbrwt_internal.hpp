@@ -395,6 +395,7 @@ struct RowsBuild;
 RowsBuild *rows_build_begin(Ctx &top, uint64_t num_rows, uint64_t align, bool auto_layout = false);
 int rows_build_range(RowsBuild *rb, Ctx &range, uint64_t row0);
 int rows_build_finish(RowsBuild *rb);  // frees rb
+uint64_t rows_build_pending_bytes(const RowsBuild *rb, uint64_t rows);
 void rows_build_abort(RowsBuild *rb);
 void free_rows(RowsImage &r);
 // row-record queries (rows.hip)

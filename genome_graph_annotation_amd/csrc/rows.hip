@@ -427,6 +427,7 @@ struct RowsBuild {
     bool decided = false;
     bool auto_layout = false;  // layout AUTO: decline records that cost more than kAutoMaxCost requests per row
     VarScratch vws;            // variable-length records (rows_var.hip)
+    double var_bytes_per_row = 0;  // their size per row, measured on the first range
     RowsImage img;
     unsigned long long *d_acc = nullptr;  // [0..3] measure, [4..7] plan
     uint16_t *d_sz = nullptr;
@@ -600,6 +601,7 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
             if (rc && rc != MBRWT_ERR_UNSUPPORTED) return rc;
             var_ok = rc == MBRWT_OK;
             var_mem = (double)vb * scale * 1.02 + (double)((rb.n + 12) / 13) * 64.0 + 64.0 * (1 + rb.n / rb.align);
+            rb.var_bytes_per_row = (double)vb / (double)nr;
         }
         if (var_ok && var_mem <= budget && (force_var == 1 || tmin > kAutoMaxCost)) {
             im.var = true;
@@ -667,6 +669,12 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
     MBRWT_HIP(hipGetLastError());
     MBRWT_HIP(hipStreamSynchronize(rb.s));
     return MBRWT_OK;
+}
+
+// device bytes the records of `rows` more rows will still allocate (the
+// variable-length records are allocated per range; blocks up front)
+uint64_t rows_build_pending_bytes(const RowsBuild *rb, uint64_t rows) {
+    return rb && rb->img.var ? (uint64_t)(rb->var_bytes_per_row * 1.02 * (double)rows) + (64ull << 20) : 0;
 }
 
 int rows_build_finish(RowsBuild *rbp) {
@@ -787,6 +795,51 @@ __device__ bool rwt_walk(const uint32_t *ntab, const uint16_t *etab, ByteFn byte
             if (sp == (int)kRowsMaxHeight) return false;
             sf[sp] = first;
             sm[sp] = m;
+            ++sp;
+        }
+        first = nw & 0xFFFFu;
+        m = mw;
+    }
+    return true;
+}
+
+// rwt_walk with its pending frames {first entry | mask << 16} in a per-lane
+// LDS stack (stk[64 k], k < kRowsMaxHeight) instead of registers: the
+// compaction kernel walks direct tiles with it, so its register budget (and
+// occupancy) stays that of its copy loop
+template <class ByteFn, class LeafFn>
+__device__ bool rwt_walk_lds(const uint32_t *ntab, const uint16_t *etab, ByteFn byte, LeafFn leaf,
+                             AS_LDS uint32_t *stk) {
+    uint32_t o = 0;
+    uint32_t nw = ntab[0];
+    uint32_t a = (nw >> 16) & 0xFFu;
+    uint32_t m = byte(o++);
+    if (a > 8) m |= byte(o++) << 8;
+    uint32_t first = nw & 0xFFFFu;
+    uint32_t sp = 0;
+    while (true) {
+        if (!m) {
+            if (!sp) break;
+            --sp;
+            const uint32_t w = stk[64 * sp];
+            first = w & 0xFFFFu;
+            m = w >> 16;
+            continue;
+        }
+        const uint32_t c = (uint32_t)__builtin_ctz(m);
+        m &= m - 1;
+        const uint32_t e = etab[first + c];
+        if (e & 0x8000u) {
+            leaf(e & 0x7FFFu);
+            continue;
+        }
+        nw = ntab[e];
+        a = (nw >> 16) & 0xFFu;
+        uint32_t mw = byte(o++);
+        if (a > 8) mw |= byte(o++) << 8;
+        if (m) {
+            if (sp == kRowsMaxHeight) return false;
+            stk[64 * sp] = first | (m << 16);
             ++sp;
         }
         first = nw & 0xFFFFu;
@@ -1231,6 +1284,7 @@ __device__ __forceinline__ void publish_status(unsigned long long *status, uint6
     atomicOr(&status[2], 1ull << st);
 }
 __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
+    __shared__ uint32_t cstk[4 * 64 * kRowsMaxHeight];  // the direct tiles' walk stacks (one per lane)
     const uint64_t n = p.n;
     const uint64_t ntiles = (n + 63) / 64;
     const uint32_t lane = threadIdx.x & 63;
@@ -1286,13 +1340,13 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
                 const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + p.table[0]);
                 uint32_t *dst = p.cols + rbase;
                 uint32_t j = 0;
-                const bool ok = rwt_walk(
+                const bool ok = rwt_walk_lds(
                     ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
                     [&](uint32_t col) {
                         if (j < count) gst(dst + j, col);
                         ++j;
                     },
-                    [](uint32_t) {});
+                    (AS_LDS uint32_t *)cstk + (threadIdx.x >> 6) * 64 * kRowsMaxHeight + lane);
                 if (!ok || j != count) publish_status(p.status, MBRWT_ERR_DEVICE);
             }
             continue;
