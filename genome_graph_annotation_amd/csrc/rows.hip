@@ -606,7 +606,7 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         if (var_ok && var_mem <= budget && (force_var == 1 || tmin > kAutoMaxCost)) {
             im.var = true;
             if (const char *ge = std::getenv("MBRWT_VAR_G")) im.var_G = (uint32_t)std::max(0, std::atoi(ge));
-            if (im.var_G != 0 && im.var_G != 1 && im.var_G != 2 && im.var_G != 4) im.var_G = 0;
+            if (im.var_G & (im.var_G - 1) || im.var_G > 16) im.var_G = 0;  // (1, 2, 4, 8 or 16)
             const uint64_t nlines = (rb.n + 12) / 13;
             MBRWT_HIP(hipMalloc(&im.var_lines, nlines * 64));
             MBRWT_HIP(hipMemsetAsync(im.var_lines, 0, nlines * 64, rb.s));
@@ -696,7 +696,9 @@ int rows_build_finish(RowsBuild *rbp) {
         return rc;
     }
     if (im.var) {
-        if (hipMalloc(&im.d_var_units, im.var_units.size() * 4) != hipSuccess ||
+        // (+32 zero entries: the decoder's speculative unit reads past the last word)
+        if (hipMalloc(&im.d_var_units, (im.var_units.size() + 32) * 4) != hipSuccess ||
+            hipMemset(im.d_var_units, 0, (im.var_units.size() + 32) * 4) != hipSuccess ||
             hipMemcpy(im.d_var_units, im.var_units.data(), im.var_units.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
             hipMalloc(&im.d_var_anc, std::max<size_t>(1, im.var_anc.size()) * 4) != hipSuccess ||
             hipMemcpy(im.d_var_anc, im.var_anc.data(), im.var_anc.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
@@ -1330,25 +1332,8 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
         const uint64_t rbase = base[k] + (x - cnt[k]);
         if (lane < nr) gst(p.offsets + r0 + lane, rbase);
         if (t == ntiles - 1 && lane == nr - 1) gst(p.offsets + n, base[k] + x);
-        if (tc[k] >> 31) {  // a direct tile: its rows' records walked from global memory
-            if (lane < nr && cnt[k]) {
-                const uint64_t row = gld(p.rows + r0 + lane);
-                uint64_t masks;
-                uint32_t count;
-                rows_locate(p.v, row, masks, count);  // (count = cnt: rows out of range have none)
-                const uint32_t *ntab = p.table + 4;
-                const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + p.table[0]);
-                uint32_t *dst = p.cols + rbase;
-                uint32_t j = 0;
-                const bool ok = rwt_walk_lds(
-                    ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
-                    [&](uint32_t col) {
-                        if (j < count) gst(dst + j, col);
-                        ++j;
-                    },
-                    (AS_LDS uint32_t *)cstk + (threadIdx.x >> 6) * 64 * kRowsMaxHeight + lane);
-                if (!ok || j != count) publish_status(p.status, MBRWT_ERR_DEVICE);
-            }
+        if (tc[k] >> 31) {  // a direct tile: walked below, once the copies' registers are free
+            base[k] = rbase;
             continue;
         }
         const uint32_t tot = tc[k];
@@ -1371,6 +1356,33 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
                 const uint32_t i = i0 + lane + 64 * j;
                 if (i < tot) gst(dst + i, w[j]);
             }
+        }
+    }
+    // direct tiles (rare): one lane per row, the record walked from global
+    // memory straight into the CSR at the row's offset (base[k] now)
+#pragma unroll 1
+    for (uint32_t k = 0; k < kCompactTpw; ++k) {
+        const uint64_t t = t0 + k;
+        if (t >= ntiles || !(tc[k] >> 31)) continue;
+        const uint64_t r0 = t * 64;
+        const uint32_t nr = (uint32_t)(n - r0 < 64 ? n - r0 : 64);
+        if (lane < nr && cnt[k]) {
+            const uint64_t row = gld(p.rows + r0 + lane);
+            uint64_t masks;
+            uint32_t count;
+            rows_locate(p.v, row, masks, count);  // (count = cnt: rows out of range have none)
+            const uint32_t *ntab = p.table + 4;
+            const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + p.table[0]);
+            uint32_t *dst = p.cols + base[k];
+            uint32_t j = 0;
+            const bool ok = rwt_walk_lds(
+                ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
+                [&](uint32_t col) {
+                    if (j < count) gst(dst + j, col);
+                    ++j;
+                },
+                (AS_LDS uint32_t *)cstk + (threadIdx.x >> 6) * 64 * kRowsMaxHeight + lane);
+            if (!ok || j != count) publish_status(p.status, MBRWT_ERR_DEVICE);
         }
     }
 }

@@ -321,6 +321,10 @@ __device__ __forceinline__ void var_locate(const VarView &v, uint64_t r, uint64_
 // one lane's labels of a record: the bitmap words [w0, w1) (items_before
 // units and labels_before labels precede them in the row), emit(k, label)
 // for its k-th label.  Word(i) / Byte(i) read the record.
+// (The refill of an exhausted mask runs in ~88 % of the iterations at the
+// RefSeq shape -- 1.13 labels per reached unit -- so it is computed
+// unconditionally and selected, rather than branched over; only the step
+// to the next bitmap word, rare, is a branch.)
 template <class Word, class Byte, class Base, class Emit>
 __device__ __forceinline__ void var_lane_labels(Word word, Byte byte, uint32_t W, uint32_t w0, uint32_t nitems0,
                                                 uint32_t nlab, Base ubase, Emit emit) {
@@ -329,16 +333,37 @@ __device__ __forceinline__ void var_lane_labels(Word word, Byte byte, uint32_t W
     uint32_t cur = 4 * W + nitems0;  // the next mask byte
     uint32_t m = 0, base = 0;
     for (uint32_t k = 0; k < nlab; ++k) {
-        if (m == 0) {
-            while (w == 0) w = word(++wi);
-            const uint32_t u = wi * 32 + (uint32_t)__builtin_ctz(w);
-            w &= w - 1;
-            base = ubase(u);
-            m = byte(cur++);
+        const bool rf = m == 0;
+        if (rf && w == 0) {
+            do {
+                w = word(++wi);
+            } while (w == 0);
         }
+        const uint32_t u = wi * 32 + (uint32_t)__builtin_ctz(w | (rf ? 0u : 0x80000000u));
+        const uint32_t nb = ubase(u), nm = byte(cur);
+        base = rf ? nb : base;
+        m = rf ? nm : m;
+        w = rf ? (w & (w - 1)) : w;
+        cur += rf ? 1u : 0u;
         emit(k, base + (uint32_t)__builtin_ctz(m));
         m &= m - 1;
     }
+}
+
+// the labels of `items` consecutive unit masks starting at mask byte `b0`
+// (aligned 32-bit reads, the partial words masked)
+template <class Word>
+__device__ __forceinline__ uint32_t var_mask_labels(Word word, uint32_t byte0, uint32_t items) {
+    if (!items) return 0;
+    const uint32_t b1 = byte0 + items;
+    uint32_t labs = 0;
+    for (uint32_t wb = byte0 & ~3u; wb < b1; wb += 4) {
+        uint32_t v = word(wb >> 2);
+        if (wb < byte0) v &= ~0u << (8 * (byte0 - wb));
+        if (wb + 4 > b1) v &= ~0u >> (8 * (wb + 4 - b1));
+        labs += (uint32_t)__builtin_popcount(v);
+    }
+    return labs;
 }
 
 struct VarParams {
@@ -409,8 +434,9 @@ __global__ __launch_bounds__(64 * WPB) void k_var_decode(VarParams p) {
     if (total_all > p.cap) return;
     AS_LDS uint16_t *ubase = (AS_LDS uint16_t *)lds_var;
     for (uint32_t i = threadIdx.x; i < p.U; i += blockDim.x) ubase[i] = (uint16_t)(gld(p.units + i) & 0xFFFFu);
+    // (speculative reads may index up to 31 entries past the last unit)
     __syncthreads();
-    const uint32_t ub_words = (p.U * 2 + 15) / 16 * 4;  // (16-byte aligned)
+    const uint32_t ub_words = ((p.U + 32) * 2 + 15) / 16 * 4;  // (16-byte aligned; 32 entries of slack)
     const uint32_t per_wave = p.CR + p.CR / 16 + 2 * p.CS;
     AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_var + ub_words) + wv * per_wave;
     AS_LDS uint8_t *rec = wb;                                   // CR bytes of 16-byte chunks
@@ -487,8 +513,7 @@ __global__ __launch_bounds__(64 * WPB) void k_var_decode(VarParams p) {
             if (q >= d) ib += y;
         }
         ib -= items;
-        uint32_t labs = 0;
-        for (uint32_t i = 0; i < items; ++i) labs += (uint32_t)__builtin_popcount(fits ? byte_l(4 * W + ib + i) : byte_g(4 * W + ib + i));
+        const uint32_t labs = fits ? var_mask_labels(word_l, 4 * W + ib, items) : var_mask_labels(word_g, 4 * W + ib, items);
         uint32_t lb = labs;
 #pragma unroll
         for (uint32_t d = 1; d < (uint32_t)G; d <<= 1) {
@@ -634,7 +659,11 @@ struct U32ToU64v {
 using VarFn = void (*)(VarParams);
 constexpr uint32_t kVarWpb = 4;
 VarFn var_fn(uint32_t G) {
-    return G == 1 ? k_var_decode<1, kVarWpb> : G == 2 ? k_var_decode<2, kVarWpb> : k_var_decode<4, kVarWpb>;
+    return G == 1    ? k_var_decode<1, kVarWpb>
+           : G == 2  ? k_var_decode<2, kVarWpb>
+           : G == 4  ? k_var_decode<4, kVarWpb>
+           : G == 8  ? k_var_decode<8, kVarWpb>
+                     : k_var_decode<16, kVarWpb>;
 }
 
 uint64_t simple_grid(uint64_t n) { return std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 65536)); }
@@ -701,7 +730,7 @@ int var_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
     p.scalars = d_sc;
     p.status = st_blk;
     const VarFn kfn = var_fn(G);
-    const size_t lds = (p.U * 2 + 15) / 16 * 16 + kVarWpb * (size_t)(CR + CR / 16 + 2 * CS);
+    const size_t lds = ((p.U + 32) * 2 + 15) / 16 * 16 + kVarWpb * (size_t)(CR + CR / 16 + 2 * CS);
     const uint32_t threads = 64 * kVarWpb;
     if (c.rb_fn != reinterpret_cast<const void *>(kfn) || c.rb_lds != lds || c.rb_threads != threads) {
         if (lds > 65536)

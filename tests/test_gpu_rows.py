@@ -434,7 +434,7 @@ def test_get_rows_device_async(oracle_mod, layout):
     (2000, 300, 0.0, 8),      # no labels at all: no records
     (1000, 2652, 0.003, 8),   # sparse (most rows without a record)
 ])
-@pytest.mark.parametrize("G", ["", "1", "2", "4"])
+@pytest.mark.parametrize("G", ["", "1", "2", "4", "8", "16"])
 def test_variable_records(oracle_mod, monkeypatch, n, m, d, arity, G):
     """The variable-length layout (forced with MBRWT_ROWS_VAR=1; every lane
     split G) answers every row-record query like the oracle, its V / L
