@@ -903,7 +903,7 @@ static int apply_option(Ctx &c, int option, int64_t value) {
         c.slot_labels = (uint32_t)value;
         return MBRWT_OK;
     case MBRWT_OPT_ROWS_WALK:
-        if (value != 0 && value != 6 && value != 7) return MBRWT_ERR_INVALID;
+        if (value != 0 && value != 3 && value != 4 && value != 6 && value != 7) return MBRWT_ERR_INVALID;
         c.rows_walk = (int)value;
         return MBRWT_OK;
     case MBRWT_OPT_KERNEL:

@@ -562,7 +562,13 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         // (measured ceilings), a record longer than a block a
         // direct-pass row (x50) -- among the images that fit the device,
         // then the smallest within 2 % of that
-        constexpr double kCost128 = 1.05;  // random 128-byte reads: 52.6 vs 53.7 G/s (profiles/r03/v01_probe_sweep.json)
+        // a 128-byte block costs more than its request (random 128-byte reads
+        // run at 52.6 vs 53.7 G/s, profiles/r03/v01_probe_sweep.json): its
+        // LDS slots halve the traversal's resident waves -- the greedy +
+        // relax shape at 3.7 B rows took 0.859 ms with 128-byte blocks of 3
+        // rows against 0.522 ms with 64-byte blocks of one row
+        // (profiles/r04/v09_tree_odometer/)
+        constexpr double kCost128 = 1.6;
         size_t free_b = 0, total_b = 0;
         MBRWT_HIP(hipMemGetInfo(&free_b, &total_b));
         const double budget = (double)free_b - 4.0 * (1ull << 30);
@@ -851,7 +857,7 @@ __device__ bool rwt_walk_lds(const uint32_t *ntab, const uint16_t *etab, ByteFn 
 }
 
 // walk families of k_traverse_rows (RowsImage::walk)
-enum : uint32_t { WALK_GENERAL = 0, WALK_MASK1 = 1, WALK_ODOMETER = 2 };
+enum : uint32_t { WALK_GENERAL = 0, WALK_MASK1 = 1, WALK_ODOMETER = 2, WALK_TREE_ODOMETER = 3 };
 
 struct RowsParams {
     const uint64_t *rows;
@@ -869,6 +875,8 @@ struct RowsParams {
     uint32_t uni;                 // the odometer: the tree's internal levels K (1..5)
     uint32_t path_walk;           // the odometer over the path table when the tree has one
     uint32_t stk_words;           // per-lane LDS stack slots (general walks)
+    uint32_t frames;              // the tree odometer: internal levels on the longest path (1..kRowsOdoLevels)
+    uint32_t mask1;               // every mask one byte
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -1102,6 +1110,93 @@ __device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_
     }
 }
 
+// The odometer for ANY tree shape (r04; the greedy + relax trees of the
+// reference's production build: leaf parents at different depths, leaf
+// parents whose columns are not consecutive -- walked as internal nodes with
+// leaf children -- and masks of up to 16 bits).  As in rows_walk_uni one
+// lock-step iteration reaches the row's next TERMINAL in pre-order (a leaf
+// parent with consecutive columns, or a leaf): the deepest level with a
+// remaining child takes it, and while that child is internal the walk
+// descends in the same iteration, each level reading its node's mask as the
+// record's next byte(s) -- BRWT::get_row's pre-order (BRWT.cpp:43-51), the
+// record format unchanged.  Levels are unrolled and predicated: a level no
+// lane of the wave needs costs a skipped branch.  State: 2 KM registers.
+constexpr uint32_t kRowsOdoLevels = 8;
+template <int KM, bool M1>
+__device__ __forceinline__ void rows_walk_tree(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
+                                               const AS_LDS uint32_t *ent, AS_LDS uint16_t *out, uint32_t pos) {
+    const AS_LDS uint8_t *rc = pb + o;  // record cursor
+    // a node's mask of arity a (<= 16) at the cursor; its width in bytes
+    auto mask_at = [&](uint32_t a) -> uint32_t {
+        uint32_t m = rc[0];
+        if (!M1) m |= (uint32_t)rc[1] << 8;
+        return m & ((1u << a) - 1u);
+    };
+    auto width = [](uint32_t a) -> uint32_t { return (M1 || a <= 8) ? 1u : 2u; };
+    uint32_t ob = pos * 2u;  // byte offset of the next label
+    auto emit = [&](uint32_t base, uint32_t x) {
+        *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));
+        ob += 2u;
+        x &= x - 1u;
+        while (x) {
+            *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));
+            ob += 2u;
+            x &= x - 1u;
+        }
+    };
+    const uint32_t ra = (root >> 16) & 0x1Fu;
+    if ((root >> 30) == 3u) {  // a one-level tree: the root is a leaf parent
+        if (live) {
+            const uint32_t x = mask_at(ra);
+            if (x) emit(root & 0xFFFFu, x);
+        }
+        return;
+    }
+    uint32_t r[KM], f[KM];
+    r[0] = live ? mask_at(ra) : 0u;
+    f[0] = root & 0xFFFFu;
+    rc += width(ra);
+#pragma unroll
+    for (int k = 1; k < KM; ++k) r[k] = f[k] = 0u;
+    while (true) {
+        uint32_t nz = 0;
+#pragma unroll
+        for (int k = 0; k < KM; ++k) nz |= (r[k] != 0u ? 1u : 0u) << k;
+        if (!nz) break;
+        const uint32_t ks = 31u - (uint32_t)__builtin_clz(nz);  // the deepest level with a child left
+        bool go = true;
+        uint32_t term = 0;
+#pragma unroll
+        for (int k = 0; k < KM; ++k) {
+            if (go && (uint32_t)k >= ks) {
+                const uint32_t c = (uint32_t)__builtin_ctz(r[k]);
+                r[k] &= r[k] - 1u;
+                const uint32_t e = ent[f[k] + c];
+                if ((int32_t)e >= 0) {  // an internal child: its mask, one level down
+                    const uint32_t a = (e >> 16) & 0x1Fu;
+                    const uint32_t m = mask_at(a);
+                    rc += width(a);
+                    if (k + 1 < KM) {
+                        r[k + 1] = m;
+                        f[k + 1] = e & 0xFFFFu;
+                    }
+                } else {
+                    term = e;
+                    go = false;
+                }
+            }
+        }
+        // the terminal: a leaf parent (its set children) or a leaf (its column)
+        uint32_t x = 1u;
+        if ((term >> 30) == 3u) {
+            const uint32_t a = (term >> 16) & 0x1Fu;
+            x = mask_at(a);
+            rc += width(a);
+        }
+        emit(term & 0xFFFFu, x);
+    }
+}
+
 // k_traverse_rows: one wave per tile of 64 query rows (file comment).
 // B: block bytes; WPB: waves per workgroup (the RWT2 table is staged once per
 // workgroup; the grid is persistent); WALK: the walk family.
@@ -1124,7 +1219,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
     // other lane in the same bank)
     constexpr uint32_t PB = B + 4;
     AS_LDS uint8_t *wb = (AS_LDS uint8_t *)(lds_rows + ((p.table_words + 3) & ~3u)) +
-                         wv * (64u * PB + 256u * p.stk_words + (WALK == WALK_ODOMETER ? 2u * C : 0u));
+                         wv * (64u * PB + 256u * p.stk_words + (WALK >= WALK_ODOMETER ? 2u * C : 0u));
     AS_LDS uint8_t *mine = wb + lane * PB;
     AS_LDS uint32_t *stk = (AS_LDS uint32_t *)(wb + 64u * PB) + lane;
     constexpr uint32_t LPB = B / 16, RPI = 64 / LPB;
@@ -1212,14 +1307,33 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
         if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
         if (!direct) {
             const bool live = valid && cnt > 0;
-            if constexpr (WALK == WALK_ODOMETER) {
+            if constexpr (WALK == WALK_ODOMETER || WALK == WALK_TREE_ODOMETER) {
                 // the odometer into the wave's LDS label stage, then the
                 // tile's labels as 16-byte vector stores (a few wide stores
                 // instead of one scattered 2-byte store per label: the r03
                 // SQ/TA counters showed the texture-address unit as the
                 // busiest unit)
                 AS_LDS uint16_t *stage = (AS_LDS uint16_t *)(wb + 64u * PB + 256u * p.stk_words);
-                if (ptw) {
+                if constexpr (WALK == WALK_TREE_ODOMETER) {
+#define MBRWT_TREE_CASE(K)                                                        \
+    case K:                                                                       \
+        if (p.mask1)                                                              \
+            rows_walk_tree<K, true>(mine, o, live, root, ent, stage, pos);        \
+        else                                                                      \
+            rows_walk_tree<K, false>(mine, o, live, root, ent, stage, pos);       \
+        break;
+                    switch (p.frames) {
+                        MBRWT_TREE_CASE(1)
+                        MBRWT_TREE_CASE(2)
+                        MBRWT_TREE_CASE(3)
+                        MBRWT_TREE_CASE(4)
+                        MBRWT_TREE_CASE(5)
+                        MBRWT_TREE_CASE(6)
+                        MBRWT_TREE_CASE(7)
+                        default: rows_walk_tree<8, false>(mine, o, live, root, ent, stage, pos); break;
+                    }
+#undef MBRWT_TREE_CASE
+                } else if (ptw) {
                     const AS_LDS uint16_t *ptab = (const AS_LDS uint16_t *)((const AS_LDS uint32_t *)lds_rows + ptw + 1);
                     switch (p.uni) {
                         case 1: rows_walk_path<1>(mine, o, live, ptab, pA, stage, pos); break;
@@ -1497,8 +1611,9 @@ using RowsFn = void (*)(RowsParams);
 constexpr uint32_t kRowsWpb = 8;
 template <int B, bool NT>
 RowsFn rows_fn_b(uint32_t walk) {
-    return walk == WALK_ODOMETER ? k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER>
-           : walk == WALK_MASK1  ? k_traverse_rows<B, kRowsWpb, NT, WALK_MASK1>
+    return walk == WALK_ODOMETER        ? k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER>
+           : walk == WALK_TREE_ODOMETER ? k_traverse_rows<B, kRowsWpb, NT, WALK_TREE_ODOMETER>
+           : walk == WALK_MASK1         ? k_traverse_rows<B, kRowsWpb, NT, WALK_MASK1>
                                  : k_traverse_rows<B, kRowsWpb, NT, WALK_GENERAL>;
 }
 RowsFn rows_fn(const RowsImage &im, uint32_t walk) {
@@ -1532,7 +1647,12 @@ struct MaskTile {
 // (MBRWT_OPT_ROWS_WALK = 6 forces the non-odometer walk: tests)
 static uint32_t rows_walk_of(const Ctx &c) {
     const RowsImage &im = c.rows;
-    if (im.uni && c.rows_walk != 6) return WALK_ODOMETER;  // (7: without the path table)
+    if (im.uni && c.rows_walk != 6 && c.rows_walk != 4 && c.rows_walk != 3)
+        return WALK_ODOMETER;  // (7: without the path table)
+    // (A/B: 6 = rows_walk6 where every mask is one byte, 4 = rows_walk4)
+    if (c.rows_walk == 6 && im.mask1) return WALK_MASK1;
+    if (c.rows_walk == 4) return WALK_GENERAL;
+    if (im.frames >= 1 && im.frames <= kRowsOdoLevels) return WALK_TREE_ODOMETER;
     return im.mask1 ? WALK_MASK1 : WALK_GENERAL;
 }
 
@@ -1596,12 +1716,14 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     p.status = st_blk;
     p.uni = im.uni;
     p.path_walk = c.rows_walk == 7 ? 0u : 1u;  // (7: the r03 odometer, A/B)
-    p.stk_words = walk == WALK_ODOMETER ? 0u : rows_stack_words(im);  // (the odometer keeps no stack)
+    p.stk_words = walk >= WALK_ODOMETER ? 0u : rows_stack_words(im);  // (the odometers keep no stack)
+    p.frames = im.frames;
+    p.mask1 = im.mask1 ? 1u : 0u;
 
     const RowsFn kfn = rows_fn(im, walk);
     const uint32_t wpb = kRowsWpb;
     const size_t lds = ((im.table2.size() + 3) & ~size_t(3)) * 4 +
-                       wpb * (64ull * (im.B + 4) + 256ull * p.stk_words + (walk == WALK_ODOMETER ? 2ull * C : 0ull));
+                       wpb * (64ull * (im.B + 4) + 256ull * p.stk_words + (walk >= WALK_ODOMETER ? 2ull * C : 0ull));
     const uint32_t threads = 64 * wpb;
     // at most 24 waves (3 workgroups of 8) per CU: more waves make the walk phase
     // slower than the extra loads in flight gain (C4 0.426 ms at 3 against

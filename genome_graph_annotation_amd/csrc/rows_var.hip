@@ -318,19 +318,16 @@ __device__ __forceinline__ void var_locate(const VarView &v, uint64_t r, uint64_
     addr = base + 4ull * o0;
 }
 
-// one lane's labels of a record: the bitmap words [w0, w1) (items_before
-// units and labels_before labels precede them in the row), emit(k, label)
-// for its k-th label.  Word(i) / Byte(i) read the record.
+// one lane's labels of a record: from bitmap word wi (its bits below the
+// lane's first unit already cleared: w) and mask byte `cur` on, nlab labels;
+// emit(k, label) for its k-th label.  Word(i) / Byte(i) read the record.
 // (The refill of an exhausted mask runs in ~88 % of the iterations at the
 // RefSeq shape -- 1.13 labels per reached unit -- so it is computed
 // unconditionally and selected, rather than branched over; only the step
 // to the next bitmap word, rare, is a branch.)
 template <class Word, class Byte, class Base, class Emit>
-__device__ __forceinline__ void var_lane_labels(Word word, Byte byte, uint32_t W, uint32_t w0, uint32_t nitems0,
+__device__ __forceinline__ void var_lane_labels(Word word, Byte byte, uint32_t wi, uint32_t w, uint32_t cur,
                                                 uint32_t nlab, Base ubase, Emit emit) {
-    uint32_t wi = w0;
-    uint32_t w = nlab ? word(wi) : 0u;
-    uint32_t cur = 4 * W + nitems0;  // the next mask byte
     uint32_t m = 0, base = 0;
     for (uint32_t k = 0; k < nlab; ++k) {
         const bool rf = m == 0;
@@ -496,24 +493,58 @@ __global__ __launch_bounds__(64 * WPB) void k_var_decode(VarParams p) {
             }
             var_wave_sync();
         }
-        // this lane's share of the row: units in words [w0, w1)
+        // this lane's share of the row: an equal share of its units (mask
+        // bytes), found from the units in words [w0, w1) of every lane
         const AS_LDS uint8_t *rl = rec + 16 * cs_row + (uint32_t)(addr & 15);
         auto word_l = [&](uint32_t i) -> uint32_t { return *(const AS_LDS uint32_t *)(rl + 4 * i); };
         auto byte_l = [&](uint32_t i) -> uint32_t { return rl[i]; };
         auto word_g = [&](uint32_t i) -> uint32_t { return gld_at<uint32_t>(addr + 4ull * i); };
         auto byte_g = [&](uint32_t i) -> uint32_t { return gld_at<uint8_t>(addr + i); };
+        auto word_a = [&](uint32_t i) -> uint32_t { return fits ? word_l(i) : word_g(i); };
         uint32_t items = 0;
         if (count)
-            for (uint32_t i = w0; i < w1; ++i) items += (uint32_t)__builtin_popcount(fits ? word_l(i) : word_g(i));
-        // units and labels of the lanes before this one in the row
-        uint32_t ib = items;
+            for (uint32_t i = w0; i < w1; ++i) items += (uint32_t)__builtin_popcount(word_a(i));
+        uint32_t wi = 0, wv0 = 0, j0 = 0, nunits = 0;
+        if constexpr (G == 1) {
+            wi = 0;
+            wv0 = count ? word_a(0) : 0u;
+            nunits = items;
+        } else {
+            // units of the word ranges before this lane's (inclusive scan - own)
+            uint32_t ie = items;
 #pragma unroll
-        for (uint32_t d = 1; d < (uint32_t)G; d <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)ib, d, 64);
-            if (q >= d) ib += y;
+            for (uint32_t d = 1; d < (uint32_t)G; d <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)ie, d, 64);
+                if (q >= d) ie += y;
+            }
+            const uint32_t NB = (uint32_t)__shfl((int)ie, (int)(rr * G + G - 1), 64);  // the row's units
+            j0 = q * NB / G;
+            nunits = (q + 1) * NB / G - j0;
+            // the word range holding unit j0: after every range ending at or before it
+            uint32_t qs = 0, before = 0;
+#pragma unroll
+            for (uint32_t g = 0; g < (uint32_t)G; ++g) {
+                const uint32_t e = (uint32_t)__shfl((int)ie, (int)(rr * G + g), 64);
+                if (e <= j0) {
+                    qs = g + 1;
+                    before = e;
+                }
+            }
+            // unit j0 is unit k of that range: scan its words, then select
+            uint32_t k = j0 - before;
+            wi = qs * Wq;
+            if (nunits) {
+                uint32_t w = word_a(wi);
+                for (uint32_t c = (uint32_t)__builtin_popcount(w); k >= c; c = (uint32_t)__builtin_popcount(w)) {
+                    k -= c;
+                    w = word_a(++wi);
+                }
+                // clear the k lowest set bits
+                for (; k; --k) w &= w - 1u;
+                wv0 = w;
+            }
         }
-        ib -= items;
-        const uint32_t labs = fits ? var_mask_labels(word_l, 4 * W + ib, items) : var_mask_labels(word_g, 4 * W + ib, items);
+        const uint32_t labs = fits ? var_mask_labels(word_l, 4 * W + j0, nunits) : var_mask_labels(word_g, 4 * W + j0, nunits);
         uint32_t lb = labs;
 #pragma unroll
         for (uint32_t d = 1; d < (uint32_t)G; d <<= 1) {
@@ -523,7 +554,7 @@ __global__ __launch_bounds__(64 * WPB) void k_var_decode(VarParams p) {
         lb -= labs;
         const uint32_t pos = (uint32_t)(roff - tbase) + lb;  // the lane's first label in the tile
         if (fits) {
-            var_lane_labels(word_l, byte_l, W, w0, ib, labs, [&](uint32_t u) -> uint32_t { return ubase[u]; },
+            var_lane_labels(word_l, byte_l, wi, wv0, 4 * W + j0, labs, [&](uint32_t u) -> uint32_t { return ubase[u]; },
                             [&](uint32_t k, uint32_t lab) { stage[pos + k] = (uint16_t)lab; });
             var_wave_sync();
             // the tile's labels: contiguous in the CSR, 4 per lane and store
@@ -541,7 +572,7 @@ __global__ __launch_bounds__(64 * WPB) void k_var_decode(VarParams p) {
             // a tile beyond the LDS budget: records read and labels stored
             // straight from / to global memory
             uint32_t *dst = p.cols + tbase + pos;
-            var_lane_labels(word_g, byte_g, W, w0, ib, labs, [&](uint32_t u) -> uint32_t { return ubase[u]; },
+            var_lane_labels(word_g, byte_g, wi, wv0, 4 * W + j0, labs, [&](uint32_t u) -> uint32_t { return ubase[u]; },
                             [&](uint32_t k, uint32_t lab) { gst(dst + k, lab); });
         }
     }
@@ -556,7 +587,8 @@ __device__ __forceinline__ void var_row(const VarView &v, const uint32_t *units,
     var_locate(v, row, addr, len, count);
     if (!count) return;
     var_lane_labels([&](uint32_t i) -> uint32_t { return gld_at<uint32_t>(addr + 4ull * i); },
-                    [&](uint32_t i) -> uint32_t { return gld_at<uint8_t>(addr + i); }, v.W, 0u, 0u, count,
+                    [&](uint32_t i) -> uint32_t { return gld_at<uint8_t>(addr + i); }, 0u,
+                    gld_at<uint32_t>(addr), 4 * v.W, count,
                     [&](uint32_t u) -> uint32_t { return gld(units + u) & 0xFFFFu; },
                     [&](uint32_t, uint32_t lab) { leaf(lab); });
 }

@@ -446,8 +446,9 @@ int mbrwt_unpack_labels_device(const void *d_base, uint32_t nseg, uint64_t seg_s
                                     k_traverse_ptw configurations (each falls back to the next kernel where
                                     the tree is not eligible); others rejected.  Node images only. */
 #define MBRWT_OPT_ROWS_WALK 8  /* row records: 0 default (the odometer walk over the path table on uniform
-                                   trees), 6 the general walk, 7 the odometer without the path table (A/B and
-                                   tests) */
+                                   trees, the tree odometer on every other shape of <= 8 internal levels),
+                                   3 the tree odometer, 4 the stack walk, 6 the stack walk of one-byte masks,
+                                   7 the odometer without the path table (A/B and tests) */
 int mbrwt_set_option(mbrwt_ctx *ctx, int option, int64_t value);
 
 /* Traversal-kernel time accumulated while MBRWT_OPT_TIMING is on (ms, launches); resets the sums. */

@@ -141,7 +141,39 @@ def test_odometer_walk(oracle_mod, n, m, d, arity, levels):
     rows = np.concatenate([np.arange(n), rng.integers(0, n, 20000)]).astype(np.uint64)
     off_o, cols_o = t.get_rows(rows)
     from genome_graph_annotation_amd import _lib as L
-    for walk in (0, 6, 7):  # the path-table odometer, the general walk, the r03 odometer
+    # the path-table odometer, the tree odometer, the stack walks, the r03 odometer
+    for walk in (0, 3, 4, 6, 7):
+        dev.set_option(L.MBRWT_OPT_ROWS_WALK, walk)
+        off_d, cols_d = dev.get_rows(rows)
+        np.testing.assert_array_equal(off_d, off_o)
+        np.testing.assert_array_equal(cols_d, cols_o)
+
+
+@pytest.mark.parametrize("n,m,d,part,arity,relax", [
+    (20000, 600, 0.01, "greedy", 2, 10),   # the reference's production shape (convert.sh:24): mixed depths
+    (20000, 300, 0.05, "greedy", 2, 4),
+    (20000, 256, 0.02, "greedy", 2, 0),    # binary greedy: 8+ internal levels
+    (20000, 512, 0.02, "basic", 2, 0),     # binary, 9 internal levels: beyond the tree odometer
+    (20000, 300, 0.02, "basic", 16, 0),    # two-byte masks
+    (20000, 250, 0.05, "basic", 12, 0),    # arity 12: two-byte masks, mixed depths
+    (4000, 300, 0.4, "greedy", 2, 10),     # long records: spills and the direct pass
+    (3000, 7, 1.0, "basic", 2, 0),         # singleton groups pass through
+])
+def test_tree_odometer(oracle_mod, n, m, d, part, arity, relax):
+    """rows_walk_tree (the default on non-uniform trees: one lock-step
+    iteration per reached leaf parent or leaf, leaf parents at any depth,
+    non-consecutive leaf parents walked as internal nodes, masks up to 16
+    bits) returns the oracle's CSR, as do the stack walks it replaced."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    from genome_graph_annotation_amd import _lib as L
+    rng = np.random.default_rng(n + m + arity)
+    dense = rng.random((n, m)) < d
+    t = O.OracleTree.from_dense(dense, part, arity, relax)
+    dev = BRWTDevice.from_tree(t.export(), layout="rows")
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 20000)]).astype(np.uint64)
+    off_o, cols_o = t.get_rows(rows)
+    for walk in (0, 3, 4, 6):
         dev.set_option(L.MBRWT_OPT_ROWS_WALK, walk)
         off_d, cols_d = dev.get_rows(rows)
         np.testing.assert_array_equal(off_d, off_o)

@@ -41,7 +41,11 @@ def measure(dev, rows_np, ref, variants, reps):
     visits, labels = dev.count_work_device(rows_t, s)
     out = {}
     for v in variants:
-        dev.set_option(L.MBRWT_OPT_KERNEL, v)
+        if isinstance(v, str):  # "wN": row records with MBRWT_OPT_ROWS_WALK = N
+            dev.set_option(L.MBRWT_OPT_KERNEL, 0)
+            dev.set_option(L.MBRWT_OPT_ROWS_WALK, int(v[1:]))
+        else:
+            dev.set_option(L.MBRWT_OPT_KERNEL, v)
         name = dev.traverse_kernel()
         nl = dev.get_rows_device(rows_t, off_t, cols_t, s)
         torch.cuda.synchronize()
@@ -68,6 +72,8 @@ def measure(dev, rows_np, ref, variants, reps):
         log(f"variant {v} ({name}): kernel {ms / k:.3f} ms, step {wall * 1e3:.3f} ms, "
             f"{n / wall / 1e9:.2f} G rows/s, bit-exact {exact}")
     dev.set_option(L.MBRWT_OPT_KERNEL, 0)
+    if dev.layout() != "nodes":
+        dev.set_option(L.MBRWT_OPT_ROWS_WALK, 0)
     return {"visits_per_row": visits / n, "labels_per_row": labels / n, "variants": out}
 
 
@@ -86,17 +92,27 @@ def main():
     ap.add_argument("--scaled-batch", type=int, default=8_000_000)
     ap.add_argument("--skip-small", action="store_true", help="only the scaled shape")
     ap.add_argument("--shapes", default="greedy+relax,basic arity 8", help="comma-separated subset of the shapes")
+    ap.add_argument("--shape-npz", default="",
+                    help="the greedy + relax tree shape of the C2 build (num_children / first_child / "
+                         "leaf_column, BFS) from a file written by --save-shape: skips the oracle's greedy build "
+                         "(~2.5 min) and measures only the scaled shape")
+    ap.add_argument("--save-shape", default="", help="write the greedy + relax shape of the C2 build to this .npz")
     ap.add_argument("--layout", default="nodes", choices=["nodes", "rows", "both"],
                     help="device layout (include/mbrwt.h MBRWT_BUILD_LAYOUT)")
     a = ap.parse_args()
     import oracle as O
     from genome_graph_annotation_amd import BRWTDevice
 
-    variants = [int(x) for x in a.variants.split(",")]
+    variants = [x if x.startswith("w") else int(x) for x in a.variants.split(",")]
     rows_np = np.random.default_rng(42).integers(0, a.rows, a.batch, dtype=np.uint64)
     res = {}
     shapes = {}
     want = set(a.shapes.split(","))
+    if a.shape_npz:
+        z = np.load(a.shape_npz)
+        shapes["greedy+relax"] = ({"num_children": z["num_children"], "first_child": z["first_child"],
+                                   "leaf_column": z["leaf_column"]}, 0.0)
+        want = set()
     for shape, part, arity, relax in [("greedy+relax", "greedy", 2, a.relax), ("basic arity 8", "basic", 8, 0)]:
         if shape not in want:
             continue
@@ -104,6 +120,10 @@ def main():
             t0 = time.time()
             t = O.OracleTree.norepl(a.rows, a.cols, a.density, 42, part, arity, relax)
             shapes[shape] = (t.export(), time.time() - t0)
+            if a.save_shape and shape == "greedy+relax":
+                ex = shapes[shape][0]
+                np.savez(a.save_shape, num_children=ex["num_children"], first_child=ex["first_child"],
+                         leaf_column=ex["leaf_column"])
             del t
             continue
         t0 = time.time()
