@@ -123,12 +123,15 @@ bool build_rwt_table(const Tree &tree, std::vector<uint32_t> &table, uint32_t &h
 }
 
 // RWT2 table (k_traverse_rows): one u32 ENTRY per child of every internal
-// node that is not a leaf parent with consecutive columns ("LP" nodes, whose
-// labels are base column + bit: no entries, no frame), u32 words
+// node that is not a leaf parent ("LP" nodes, whose labels are base column +
+// bit, or entry bit of a column list: no entries, no frame), u32 words
 //   [0] the root's entry, [1] nE, [2] frames (non-LP internal levels on a
-//   path), [3] 0, nE entries; an entry is
+//   path), [3] 0 (or the path table's offset, append_path_table), nE
+//   entries, then the column lists (u16) of the leaf parents whose columns
+//   are not consecutive (the greedy partitioner's groups); an entry is
 //     leaf      0x80000000 | column
 //     LP node   0xC0000000 | arity << 16 | first column
+//     LP list   0xE0000000 | arity << 16 | first u16 of its column list
 //     internal  arity << 16 | first entry of its children
 // so the walk reads ONE table word per visited child.
 bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &t2, uint32_t &frames) {
@@ -140,22 +143,30 @@ bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &t2, uint32_t &fra
     const uint32_t root = folded ? 0u : 1u;
     if (N[root].kind == KIND_LEAF || N[root].arity == 0) return false;
     auto column_of = [&](const DevNode &d) { return tree.label_perm.empty() ? d.label : tree.label_perm[d.label]; };
-    auto is_lp = [&](uint32_t v, uint32_t &base) {
+    // a leaf parent: base = its first column (consecutive: cons) 
+    auto is_lp2 = [&](uint32_t v, uint32_t &base, bool &cons) {
         const DevNode &d = N[v];
+        cons = true;
         for (uint32_t c = 0; c < d.arity; ++c) {
             const DevNode &w = N[d.first_child + c];
             if (w.kind != KIND_LEAF) return false;
             if (c == 0) base = column_of(w);
-            else if (column_of(w) != base + c) return false;
+            else if (column_of(w) != base + c) cons = false;
         }
-        return true;
+        return d.arity > 0;
     };
+    auto is_lp = [&](uint32_t v, uint32_t &base) {
+        bool cons;
+        return is_lp2(v, base, cons);
+    };
+    std::vector<uint16_t> lists;  // the column lists of non-consecutive leaf parents
     // non-LP internal nodes in BFS order, each with its first entry
     std::vector<uint32_t> order{root}, depth{1}, first;
     uint32_t nE = 0;
     std::vector<uint32_t> first_of(N.size(), 0);
     uint32_t rb = 0;
-    const bool root_lp = is_lp(root, rb);
+    bool root_cons = false;
+    const bool root_lp = is_lp2(root, rb, root_cons) && root_cons;  // (a listed root: an internal node)
     if (!root_lp) {
         for (size_t h = 0; h < order.size(); ++h) {
             const uint32_t v = order[h];
@@ -186,9 +197,20 @@ bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &t2, uint32_t &fra
         }
         if (d.arity == 0 || d.arity > kRowsMaxArity) return false;
         uint32_t b;
-        if (is_lp(w, b)) {
-            if (b + d.arity > 0x8000) return false;
-            out = 0xC0000000u | ((uint32_t)d.arity << 16) | b;
+        bool cons;
+        if (is_lp2(w, b, cons)) {
+            if (cons) {
+                if (b + d.arity > 0x8000) return false;
+                out = 0xC0000000u | ((uint32_t)d.arity << 16) | b;
+                return true;
+            }
+            if (lists.size() + d.arity > 0x10000) return false;
+            out = 0xE0000000u | ((uint32_t)d.arity << 16) | (uint32_t)lists.size();
+            for (uint32_t c = 0; c < d.arity; ++c) {
+                const uint32_t col = column_of(N[d.first_child + c]);
+                if (col >= 0x8000) return false;
+                lists.push_back((uint16_t)col);
+            }
             return true;
         }
         out = ((uint32_t)d.arity << 16) | first_of[w];
@@ -204,7 +226,9 @@ bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &t2, uint32_t &fra
             for (uint32_t c = 0; c < d.arity; ++c)
                 if (!entry(d.first_child + c, t2[4 + first_of[v] + c])) return false;
         }
-    return true;
+    for (size_t i = 0; i < lists.size(); i += 2)
+        t2.push_back((uint32_t)lists[i] | (i + 1 < lists.size() ? (uint32_t)lists[i + 1] << 16 : 0u));
+    return t2.size() <= kRowsMaxTableWords;
 }
 
 // K when every root-to-leaf path of the RWT2 table crosses exactly K internal
@@ -221,7 +245,7 @@ uint32_t rwt2_uniform_levels(const std::vector<uint32_t> &t2) {
             for (uint32_t c = 0; c < a; ++c) {
                 if (4 + (size_t)f + c >= t2.size()) return 0;
                 const uint32_t e = t2[4 + f + c];
-                if ((e >> 30) != (d == K ? 3u : 0u)) return 0;  // leaf parents exactly at depth K + 1
+                if ((e >> 29) != (d == K ? 6u : 0u)) return 0;  // consecutive leaf parents exactly at depth K + 1
                 if (d < K) next.push_back(e);
             }
         }
@@ -524,7 +548,7 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         // or leaf-parent entry of arity <= 8
         auto ar8 = [](uint32_t e) { return (e >> 30) == 2u || ((e >> 16) & 0x1Fu) <= 8; };
         im.mask1 = ar8(im.table2[0]);
-        for (size_t i = 4; i < im.table2.size(); ++i) im.mask1 = im.mask1 && ar8(im.table2[i]);
+        for (size_t i = 4; i < 4 + (size_t)im.table2[1]; ++i) im.mask1 = im.mask1 && ar8(im.table2[i]);
         im.uni = im.mask1 ? rwt2_uniform_levels(im.table2) : 0u;
         if (im.uni) append_path_table(im.table2, im.uni);
     }
@@ -896,9 +920,16 @@ __device__ __forceinline__ void st16(uint16_t *base, uint32_t idx, uint32_t v) {
 // frames in a per-lane LDS stack (one write / one read per push / pop), one
 // emission loop for leaves and leaf parents, mask bytes read as two bytes
 // masked by the arity.
+// a terminal entry's label for bit `bit` of its mask: a leaf's column (bit
+// 0), a leaf parent's first column + bit, or entry `bit` of its column list
+__device__ __forceinline__ uint32_t term_label(uint32_t e, const AS_LDS uint16_t *lst, uint32_t bit) {
+    const uint32_t i = (e & 0xFFFFu) + bit;
+    return ((e >> 29) & 1u) ? (uint32_t)lst[i] : i;
+}
+
 __device__ __forceinline__ void rows_walk4(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
-                                           const AS_LDS uint32_t *ent, AS_LDS uint32_t *stk, uint16_t *out,
-                                           uint32_t pos) {
+                                           const AS_LDS uint32_t *ent, const AS_LDS uint16_t *lst,
+                                           AS_LDS uint32_t *stk, uint16_t *out, uint32_t pos) {
     const uint32_t ra = (root >> 16) & 0x1Fu;
     const uint32_t rm = ((uint32_t)pb[o] | ((uint32_t)pb[o + 1] << 8)) & ((1u << ra) - 1u);
     o += ra > 8 ? 2u : 1u;
@@ -920,7 +951,7 @@ __device__ __forceinline__ void rows_walk4(const AS_LDS uint8_t *pb, uint32_t o,
         const bool inner = act && (e >> 31) == 0u;
         uint32_t x = (act && (e >> 31)) ? (a ? mw : 1u) : 0u;  // a leaf: its column; a leaf parent: its set children
         const uint32_t base = e & 0xFFFFu;
-        for (; x; x &= x - 1) st16(out, pos++, base + (uint32_t)__builtin_ctz(x));
+        for (; x; x &= x - 1) st16(out, pos++, term_label(e, lst, (uint32_t)__builtin_ctz(x)));
         if (inner && m) {
             stk[sp * 64] = f | (m << 16);
             ++sp;
@@ -946,8 +977,8 @@ __device__ __forceinline__ void rows_walk4(const AS_LDS uint8_t *pb, uint32_t o,
 // exec-masked branches.  Labels are stored one by one into the tile's temp
 // region (global u16).
 __device__ __forceinline__ void rows_walk6(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
-                                           const AS_LDS uint32_t *ent, AS_LDS uint32_t *stk, AS_GLOBAL uint16_t *out,
-                                           uint32_t pos) {
+                                           const AS_LDS uint32_t *ent, const AS_LDS uint16_t *lst,
+                                           AS_LDS uint32_t *stk, AS_GLOBAL uint16_t *out, uint32_t pos) {
     const AS_LDS uint8_t *rc = pb + o;  // record cursor
     const uint32_t rm = rc[0];
     ++rc;
@@ -969,9 +1000,8 @@ __device__ __forceinline__ void rows_walk6(const AS_LDS uint8_t *pb, uint32_t o,
             const bool lp = (e >> 30) & 1u;
             uint32_t x = lp ? mw : 1u;
             rc += lp ? 1 : 0;
-            const uint32_t base = e & 0xFFFFu;
             do {
-                *(AS_GLOBAL uint16_t *)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));
+                *(AS_GLOBAL uint16_t *)((uintptr_t)out + ob) = (uint16_t)term_label(e, lst, (uint32_t)__builtin_ctz(x));
                 ob += 2u;
                 x &= x - 1u;
             } while (x);
@@ -1124,22 +1154,23 @@ __device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_
 constexpr uint32_t kRowsOdoLevels = 8;
 template <int KM, bool M1>
 __device__ __forceinline__ void rows_walk_tree(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
-                                               const AS_LDS uint32_t *ent, AS_LDS uint16_t *out, uint32_t pos) {
+                                               const AS_LDS uint32_t *ent, const AS_LDS uint16_t *lst,
+                                               AS_LDS uint16_t *out, uint32_t pos) {
     const AS_LDS uint8_t *rc = pb + o;  // record cursor
     // a node's mask of arity a (<= 16) at the cursor; its width in bytes
     auto mask_at = [&](uint32_t a) -> uint32_t {
         uint32_t m = rc[0];
-        if (!M1) m |= (uint32_t)rc[1] << 8;
+        if (!M1 && a > 8) m |= (uint32_t)rc[1] << 8;  // (rare: a branch, not a read in every lane)
         return m & ((1u << a) - 1u);
     };
     auto width = [](uint32_t a) -> uint32_t { return (M1 || a <= 8) ? 1u : 2u; };
     uint32_t ob = pos * 2u;  // byte offset of the next label
-    auto emit = [&](uint32_t base, uint32_t x) {
-        *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));
+    auto emit = [&](uint32_t e, uint32_t x) {
+        *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)term_label(e, lst, (uint32_t)__builtin_ctz(x));
         ob += 2u;
         x &= x - 1u;
         while (x) {
-            *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));
+            *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)term_label(e, lst, (uint32_t)__builtin_ctz(x));
             ob += 2u;
             x &= x - 1u;
         }
@@ -1148,7 +1179,7 @@ __device__ __forceinline__ void rows_walk_tree(const AS_LDS uint8_t *pb, uint32_
     if ((root >> 30) == 3u) {  // a one-level tree: the root is a leaf parent
         if (live) {
             const uint32_t x = mask_at(ra);
-            if (x) emit(root & 0xFFFFu, x);
+            if (x) emit(root, x);
         }
         return;
     }
@@ -1193,7 +1224,7 @@ __device__ __forceinline__ void rows_walk_tree(const AS_LDS uint8_t *pb, uint32_
             x = mask_at(a);
             rc += width(a);
         }
-        emit(term & 0xFFFFu, x);
+        emit(term, x);
     }
 }
 
@@ -1210,6 +1241,8 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
     __syncthreads();
     const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows[0]);
     const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows + 4;
+    // the leaf parents' column lists after the entries
+    const AS_LDS uint16_t *lst = (const AS_LDS uint16_t *)(ent + __builtin_amdgcn_readfirstlane(lds_rows[1]));
     // the path table of a uniform tree (append_path_table; 0: none)
     const uint32_t ptw = p.path_walk ? __builtin_amdgcn_readfirstlane(lds_rows[3]) : 0u;
     const uint32_t pA = ptw ? __builtin_amdgcn_readfirstlane(lds_rows[ptw]) : 0u;
@@ -1300,13 +1333,15 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
         }
         const uint32_t total = __builtin_amdgcn_readlane(x, 63);
         const uint32_t pos = x - cnt;
-        // a tile whose labels exceed its region, or holding a record longer
-        // than a block, is walked by k_compact_tiles from global memory
-        const bool direct = total > C || __any(lng);
+        // a tile whose labels exceed its region is walked by k_compact_tiles
+        // from global memory; so is a record longer than a block (its count
+        // flagged with bit 15; its labels' places in the tile are kept)
+        const bool direct = total > C;
+        const bool has_long = __any(lng);
         uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
-        if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)cnt);
+        if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)(cnt | (lng ? 0x8000u : 0u)));
         if (!direct) {
-            const bool live = valid && cnt > 0;
+            const bool live = valid && cnt > 0 && !lng;
             if constexpr (WALK == WALK_ODOMETER || WALK == WALK_TREE_ODOMETER) {
                 // the odometer into the wave's LDS label stage, then the
                 // tile's labels as 16-byte vector stores (a few wide stores
@@ -1318,9 +1353,9 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
 #define MBRWT_TREE_CASE(K)                                                        \
     case K:                                                                       \
         if (p.mask1)                                                              \
-            rows_walk_tree<K, true>(mine, o, live, root, ent, stage, pos);        \
+            rows_walk_tree<K, true>(mine, o, live, root, ent, lst, stage, pos);        \
         else                                                                      \
-            rows_walk_tree<K, false>(mine, o, live, root, ent, stage, pos);       \
+            rows_walk_tree<K, false>(mine, o, live, root, ent, lst, stage, pos);       \
         break;
                     switch (p.frames) {
                         MBRWT_TREE_CASE(1)
@@ -1330,7 +1365,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
                         MBRWT_TREE_CASE(5)
                         MBRWT_TREE_CASE(6)
                         MBRWT_TREE_CASE(7)
-                        default: rows_walk_tree<8, false>(mine, o, live, root, ent, stage, pos); break;
+                        default: rows_walk_tree<8, false>(mine, o, live, root, ent, lst, stage, pos); break;
                     }
 #undef MBRWT_TREE_CASE
                 } else if (ptw) {
@@ -1357,13 +1392,13 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
                     gst(reinterpret_cast<u32x4_t *>(treg + 128 + q2),
                         *(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2));
             } else if constexpr (WALK == WALK_MASK1) {
-                rows_walk6(mine, o, live, root, ent, stk, (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128),
-                           pos);
+                rows_walk6(mine, o, live, root, ent, lst, stk,
+                           (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128), pos);
             } else {
-                rows_walk4(mine, o, live, root, ent, stk, reinterpret_cast<uint16_t *>(treg + 128), pos);
+                rows_walk4(mine, o, live, root, ent, lst, stk, reinterpret_cast<uint16_t *>(treg + 128), pos);
             }
         }
-        if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u));
+        if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u) | (has_long ? 0x40000000u : 0u));
         wave_sync();  // the slots are reused
     }
 }
@@ -1404,7 +1439,7 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
     const uint64_t n = p.n;
     const uint64_t ntiles = (n + 63) / 64;
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t total = gld(p.tile_offsets + ntiles - 1) + (gld(p.tile_counts + ntiles - 1) & 0x7FFFFFFFu);
+    const uint64_t total = gld(p.tile_offsets + ntiles - 1) + (gld(p.tile_counts + ntiles - 1) & 0x3FFFFFFFu);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const uint64_t err = p.scalars[2];
         p.scalars[2] = 0;
@@ -1426,7 +1461,7 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
         const uint64_t r0 = t * 64;
         tc[k] = in ? gld(p.tile_counts + t) : 0x80000000u;
         base[k] = in ? gld(p.tile_offsets + t) : 0;
-        cnt[k] = (in && r0 + lane < n) ? (uint32_t)gld(reinterpret_cast<const uint16_t *>(treg) + lane) : 0u;
+        cnt[k] = (in && r0 + lane < n) ? (uint32_t)gld(reinterpret_cast<const uint16_t *>(treg) + lane) : 0u;  // (bit 15: long)
         const uint16_t *lab = reinterpret_cast<const uint16_t *>(treg + 128);
 #pragma unroll
         for (uint32_t j = 0; j < 8; ++j) v[k][j] = gld(lab + lane + 64 * j);  // (C >= 1024: inside the region)
@@ -1437,21 +1472,21 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
         if (t >= ntiles) break;
         const uint64_t r0 = t * 64;
         const uint32_t nr = (uint32_t)(n - r0 < 64 ? n - r0 : 64);
-        uint32_t x = cnt[k];
+        const uint32_t c = cnt[k] & 0x7FFFu;
+        uint32_t x = c;
 #pragma unroll
         for (uint32_t d = 1; d < 64; d <<= 1) {
             const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
             if (lane >= d) x += y;
         }
-        const uint64_t rbase = base[k] + (x - cnt[k]);
+        const uint64_t rbase = base[k] + (x - c);
         if (lane < nr) gst(p.offsets + r0 + lane, rbase);
         if (t == ntiles - 1 && lane == nr - 1) gst(p.offsets + n, base[k] + x);
-        if (tc[k] >> 31) {  // a direct tile: walked below, once the copies' registers are free
-            base[k] = rbase;
-            continue;
-        }
-        const uint32_t tot = tc[k];
-        uint32_t *dst = p.cols + base[k];
+        const uint32_t tot = tc[k] & 0x3FFFFFFFu;
+        const uint64_t tb = base[k];
+        base[k] = rbase;  // (the walks below: each row's own offset)
+        if (tc[k] >> 31) continue;  // a direct tile: walked below, once the copies' registers are free
+        uint32_t *dst = p.cols + tb;
 #pragma unroll
         for (uint32_t j = 0; j < 8; ++j) {
             const uint32_t i = lane + 64 * j;
@@ -1472,15 +1507,19 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
             }
         }
     }
-    // direct tiles (rare): one lane per row, the record walked from global
-    // memory straight into the CSR at the row's offset (base[k] now)
+    // direct tiles and records longer than a block (rare): one lane per row,
+    // the record walked from global memory straight into the CSR at the
+    // row's offset (base[k] now) -- over the places the copy above filled
+    // for a long record, hence the fence
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 #pragma unroll 1
     for (uint32_t k = 0; k < kCompactTpw; ++k) {
         const uint64_t t = t0 + k;
-        if (t >= ntiles || !(tc[k] >> 31)) continue;
+        if (t >= ntiles || !(tc[k] >> 30)) continue;
         const uint64_t r0 = t * 64;
         const uint32_t nr = (uint32_t)(n - r0 < 64 ? n - r0 : 64);
-        if (lane < nr && cnt[k]) {
+        const bool walk = (tc[k] >> 31) ? (cnt[k] & 0x7FFFu) != 0 : (cnt[k] >> 15) != 0;
+        if (lane < nr && walk) {
             const uint64_t row = gld(p.rows + r0 + lane);
             uint64_t masks;
             uint32_t count;
@@ -1637,7 +1676,7 @@ uint32_t rows_tile_labels(const Ctx &c) {
 }
 
 struct MaskTile {
-    __host__ __device__ __forceinline__ uint64_t operator()(const uint32_t &x) const { return x & 0x7FFFFFFFu; }
+    __host__ __device__ __forceinline__ uint64_t operator()(const uint32_t &x) const { return x & 0x3FFFFFFFu; }
 };
 
 }  // namespace
