@@ -836,12 +836,12 @@ __device__ bool rwt_walk(const uint32_t *ntab, const uint16_t *etab, ByteFn byte
 }
 
 // rwt_walk with its pending frames {first entry | mask << 16} in a per-lane
-// LDS stack (stk[64 k], k < kRowsMaxHeight) instead of registers: the
-// compaction kernel walks direct tiles with it, so its register budget (and
-// occupancy) stays that of its copy loop
+// LDS stack (stk[64 k], k < lim <= kRowsMaxHeight: the tree's height) instead
+// of registers: the compaction kernel walks direct tiles with it, so its
+// register budget (and occupancy) stays that of its copy loop
 template <class ByteFn, class LeafFn>
 __device__ bool rwt_walk_lds(const uint32_t *ntab, const uint16_t *etab, ByteFn byte, LeafFn leaf,
-                             AS_LDS uint32_t *stk) {
+                             AS_LDS uint32_t *stk, uint32_t lim) {
     uint32_t o = 0;
     uint32_t nw = ntab[0];
     uint32_t a = (nw >> 16) & 0xFFu;
@@ -870,7 +870,7 @@ __device__ bool rwt_walk_lds(const uint32_t *ntab, const uint16_t *etab, ByteFn 
         uint32_t mw = byte(o++);
         if (a > 8) mw |= byte(o++) << 8;
         if (m) {
-            if (sp == kRowsMaxHeight) return false;
+            if (sp == lim) return false;
             stk[64 * sp] = first | (m << 16);
             ++sp;
         }
@@ -1429,13 +1429,14 @@ struct CompactParams {
     const uint64_t *rows;         // the batch (direct tiles)
     RowsView v;
     const uint32_t *table;        // RWT (direct tiles)
+    uint32_t stk_lim;             // walk stack frames (the tree's height; dynamic LDS)
 };
 __device__ __forceinline__ void publish_status(unsigned long long *status, uint64_t st) {
     atomicMax(&status[1], (unsigned long long)st);
     atomicOr(&status[2], 1ull << st);
 }
 __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
-    __shared__ uint32_t cstk[4 * 64 * kRowsMaxHeight];  // the direct tiles' walk stacks (one per lane)
+    extern __shared__ uint32_t cstk[];  // the direct walks' stacks: 4 x 64 x stk_lim words (one per lane)
     const uint64_t n = p.n;
     const uint64_t ntiles = (n + 63) / 64;
     const uint32_t lane = threadIdx.x & 63;
@@ -1534,7 +1535,7 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
                     if (j < count) gst(dst + j, col);
                     ++j;
                 },
-                (AS_LDS uint32_t *)cstk + (threadIdx.x >> 6) * 64 * kRowsMaxHeight + lane);
+                (AS_LDS uint32_t *)cstk + (threadIdx.x >> 6) * 64 * p.stk_lim + lane, p.stk_lim);
             if (!ok || j != count) publish_status(p.status, MBRWT_ERR_DEVICE);
         }
     }
@@ -1825,7 +1826,9 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         cp.v = view_of(c);
         cp.table = im.d_table;
         const uint64_t waves = (nt + kCompactTpw - 1) / kCompactTpw;
-        hipLaunchKernelGGL(k_compact_tiles, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, cp);
+        cp.stk_lim = std::max(1u, std::min(im.height, kRowsMaxHeight));
+        hipLaunchKernelGGL(k_compact_tiles, dim3((unsigned)((waves + 3) / 4)), dim3(256),
+                           (size_t)256 * cp.stk_lim * 4, s, cp);
         MBRWT_HIP(hipGetLastError());
     }
     c.rows_sc_dirty = false;

@@ -9,3 +9,5 @@ timeout -k 10 200 python -u tools/rows_ab.py $C4 > gpurun_out/r4l/c4_cur1.log 2>
 MBRWT_LIB=tools/_ab/libmbrwt_6bf1e26.so timeout -k 10 200 python -u tools/rows_ab.py $C4 > gpurun_out/r4l/c4_6bf1e26.log 2>&1 || exit 1
 MBRWT_LIB=tools/_ab/libmbrwt_02ea363.so timeout -k 10 200 python -u tools/rows_ab.py $C4 > gpurun_out/r4l/c4_02ea363.log 2>&1 || exit 1
 timeout -k 10 200 python -u tools/rows_ab.py $C4 > gpurun_out/r4l/c4_cur2.log 2>&1 || exit 1
+# batch k+1's traversal on a second context and stream while batch k's output pass runs
+timeout -k 10 400 python -u tools/overlap_ab.py --steps 40 > gpurun_out/r4l/overlap.log 2>&1 || exit 1
