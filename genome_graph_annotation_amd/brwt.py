@@ -259,6 +259,14 @@ class BRWTDevice:
         """BRWT::serialize (BRWT.cpp:113-128) of this matrix."""
         return serialize_tree(self.export())
 
+    def clone(self) -> "BRWTDevice":
+        """A second query context over the same device image
+        (mbrwt_ctx_clone): its own workspaces, so its queries may run
+        concurrently with this one's on another stream or thread."""
+        h = C.c_void_p()
+        L.check(L.lib().mbrwt_ctx_clone(self._h, C.byref(h)), "mbrwt_ctx_clone")
+        return BRWTDevice(h.value)
+
     def close(self):
         if getattr(self, "_h", None):
             L.lib().mbrwt_destroy(self._h)

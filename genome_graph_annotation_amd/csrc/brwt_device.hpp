@@ -179,6 +179,19 @@ class BRWTDevice : public BinaryMatrix {
         return build_bottom_up(columns, num_rows, 2, device, relax_max_arity);
     }
 
+    // a query handle over the same device image (mbrwt_ctx_clone): one per
+    // server worker thread, so their get_rows calls do not serialise on a
+    // shared workspace (the reference shares its annotator by reference
+    // across the server's thread pool)
+    BRWTDevice clone() const {
+        if (!ctx_) return BRWTDevice(device_);
+        BRWTDevice m(device_);
+        mbrwt_ctx *c = nullptr;
+        check_status(mbrwt_ctx_clone(ctx_.get(), &c), "mbrwt_ctx_clone");
+        m.ctx_.reset(c, Deleter());
+        return m;
+    }
+
     // BRWTOptimizer::relax(brwt, max_arity) of an exported tree
     // (`annograph relax_brwt`, main.cpp:746)
     static BRWTDevice relaxed(const mbrwt_tree_desc &desc, uint64_t max_arity, int device = 0) {

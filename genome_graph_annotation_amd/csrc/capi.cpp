@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 
@@ -20,6 +21,8 @@ int hip_fail(hipError_t e, const char *what) {
     (void)hipGetLastError();  // clear the sticky non-fatal error
     return (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) ? MBRWT_ERR_NOMEM : MBRWT_ERR_DEVICE;
 }
+
+static int init_query_state(Ctx &c);
 
 static int upload_tables(Ctx &c) {
     Tree &t = c.tree;
@@ -57,6 +60,11 @@ static int upload_tables(Ctx &c) {
         MBRWT_HIP(hipMalloc(&c.d_col_leaf, t.col_leaf.size() * 4));
         MBRWT_HIP(hipMemcpy(c.d_col_leaf, t.col_leaf.data(), t.col_leaf.size() * 4, hipMemcpyHostToDevice));
     }
+    return init_query_state(c);
+}
+
+// the per-context query state: status scalars, timing events, workspace fence
+static int init_query_state(Ctx &c) {
     MBRWT_HIP(hipHostMalloc(reinterpret_cast<void **>(&c.h_scalars), 8 * sizeof(uint64_t), hipHostMallocDefault));
     MBRWT_HIP(hipMalloc(&c.d_scalars, 8 * sizeof(uint64_t)));
     MBRWT_HIP(hipEventCreate(&c.ev0));
@@ -65,23 +73,34 @@ static int upload_tables(Ctx &c) {
     return MBRWT_OK;
 }
 
+static std::mutex g_clone_mu;  // Ctx::clones / Ctx::released of every image owner
+
 static void release(Ctx *c) {
     if (!c) return;
+    if (!c->image_owner) {
+        std::lock_guard<std::mutex> lk(g_clone_mu);
+        if (c->clones > 0) {  // freed with its last clone
+            c->released = true;
+            return;
+        }
+    }
     for (Ctx *sc : c->shards) release(sc);
     (void)hipSetDevice(c->device);
-    free_tree(c->tree);
-    free_rows(c->rows);
+    if (!c->image_owner) {  // the image: only its owner frees it
+        free_tree(c->tree);
+        free_rows(c->rows);
+        if (c->d_nodes) (void)hipFree(c->d_nodes);
+        if (c->d_cnodes) (void)hipFree(c->d_cnodes);
+        if (c->d_p2w) (void)hipFree(c->d_p2w);
+        if (c->d_ptw) (void)hipFree(c->d_ptw);
+        if (c->d_label_map) (void)hipFree(c->d_label_map);
+        if (c->d_col_path) (void)hipFree(c->d_col_path);
+        if (c->d_col_leaf) (void)hipFree(c->d_col_leaf);
+    }
     for (Workspace *w : {&c->ws_temp, &c->ws_counts, &c->ws_ovf, &c->ws_scan, &c->ws_rows, &c->ws_out, &c->ws_sort,
                          &c->ws_cls_off, &c->ws_cls_cols, &c->ws_sh_keys, &c->ws_sh_local, &c->ws_sh_cnt,
                          &c->ws_sh_sort, &c->ws_sh_tmp})
         if (w->buf) (void)hipFree(w->buf);
-    if (c->d_nodes) (void)hipFree(c->d_nodes);
-    if (c->d_cnodes) (void)hipFree(c->d_cnodes);
-    if (c->d_p2w) (void)hipFree(c->d_p2w);
-    if (c->d_ptw) (void)hipFree(c->d_ptw);
-    if (c->d_label_map) (void)hipFree(c->d_label_map);
-    if (c->d_col_path) (void)hipFree(c->d_col_path);
-    if (c->d_col_leaf) (void)hipFree(c->d_col_leaf);
     if (c->d_scalars) (void)hipFree(c->d_scalars);
     if (c->h_scalars) (void)hipHostFree(c->h_scalars);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -92,7 +111,56 @@ static void release(Ctx *c) {
     }
     destroy_fence(c->fence);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    Ctx *owner = c->image_owner;
     delete c;
+    if (owner) {
+        bool last;
+        {
+            std::lock_guard<std::mutex> lk(g_clone_mu);
+            last = --owner->clones == 0 && owner->released;
+        }
+        if (last) release(owner);
+    }
+}
+
+// a query context over src's image (mbrwt_ctx_clone)
+static int clone_ctx(Ctx *src, Ctx **out) {
+    *out = nullptr;
+    Ctx *c = new (std::nothrow) Ctx();
+    if (!c) return MBRWT_ERR_NOMEM;
+    c->device = src->device;
+    c->tree = src->tree;
+    c->d_nodes = src->d_nodes;
+    c->d_cnodes = src->d_cnodes;
+    c->d_p2w = src->d_p2w;
+    c->d_ptw = src->d_ptw;
+    c->d_label_map = src->d_label_map;
+    c->d_col_path = src->d_col_path;
+    c->d_col_leaf = src->d_col_leaf;
+    c->rows = src->rows;
+    c->nodes_freed = src->nodes_freed;
+    c->shard_rows = src->shard_rows;
+    Ctx *owner = src->image_owner ? src->image_owner : src;
+    c->image_owner = owner;
+    {
+        std::lock_guard<std::mutex> lk(g_clone_mu);
+        ++owner->clones;
+    }
+    int rc = MBRWT_OK;
+    if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+        rc = hip_fail(hipGetLastError(), "stream creation");
+    if (!rc) rc = init_query_state(*c);
+    for (size_t i = 0; !rc && i < src->shards.size(); ++i) {
+        Ctx *sc = nullptr;
+        rc = clone_ctx(src->shards[i], &sc);
+        if (!rc) c->shards.push_back(sc);
+    }
+    if (rc) {
+        release(c);
+        return rc;
+    }
+    *out = c;
+    return MBRWT_OK;
 }
 
 static int make_rows(Ctx &c, int layout);
@@ -516,6 +584,17 @@ int mbrwt_create_relaxed(const mbrwt_tree_desc *desc, uint64_t max_arity, int de
 }
 
 void mbrwt_destroy(mbrwt_ctx *ctx) { release(C(ctx)); }
+
+int mbrwt_ctx_clone(mbrwt_ctx *src, mbrwt_ctx **out) {
+    if (!src || !out) {
+        set_error("null context or output pointer");
+        return MBRWT_ERR_INVALID;
+    }
+    Ctx *c = nullptr;
+    const int rc = clone_ctx(C(src), &c);
+    *out = reinterpret_cast<mbrwt_ctx *>(c);
+    return rc;
+}
 
 uint64_t mbrwt_num_rows(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.num_rows : 0; }
 uint64_t mbrwt_num_columns(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.num_columns : 0; }

@@ -384,6 +384,14 @@ struct Ctx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> async_ev;  // timing of asynchronous calls
     size_t async_used = 0;
     uint64_t rows_sc_at = 0;     // their byte offset in ws_counts
+
+    // mbrwt_ctx_clone: a clone shares image_owner's device image (tree
+    // images, tables, row records) and owns only its query state; the owner
+    // counts its live clones and, destroyed while any is alive, is freed
+    // with the last one (both under the clone mutex, capi.cpp)
+    Ctx *image_owner = nullptr;
+    int clones = 0;
+    bool released = false;
 };
 
 // row-record image construction (rows.hip): records of the rows [row0, row0 +

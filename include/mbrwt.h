@@ -151,6 +151,17 @@ int mbrwt_create_relaxed(const mbrwt_tree_desc *desc, uint64_t max_arity, int de
 
 void mbrwt_destroy(mbrwt_ctx *ctx);
 
+/* A second query context over the SAME device image (no copy): its own
+ * workspaces, status block, events and host-buffer stream, so queries on a
+ * context and on its clones may run concurrently on different streams (or
+ * host threads) -- the reference's server answers concurrent requests from
+ * one annotator (cli/server.cpp); calls on ONE context are ordered on its
+ * workspace fence.  Options start at their defaults.  Destroying the source
+ * while clones are alive defers the image's release to the last clone.
+ * Sharded contexts clone their shards.  Replaces nothing in the reference:
+ * its annotator is shared by reference across its worker threads. */
+int mbrwt_ctx_clone(mbrwt_ctx *src, mbrwt_ctx **out);
+
 /* ---- device layout ------------------------------------------------------
  * Two layouts of the same tree:
  *   NODES  per-node, sibling-interleaved index columns with ranks; get_row is

@@ -77,6 +77,25 @@ static void grid(int kind, uint64_t relax) {
     }
 }
 
+// a clone (mbrwt_ctx_clone) answers like its source, before and after the
+// source is destroyed (device backend only; the oracle has no clones)
+TEST(BRWT, CloneAnswersLikeSource) {
+    if (!g_device) return;
+    for (int kind = 0; kind < 3; ++kind) {
+        const uint64_t n = 19;
+        Columns cols(13, std::vector<bool>(n));
+        for (size_t j = 0; j < cols.size(); ++j)
+            for (uint64_t i = 0; i < n; ++i) cols[j][i] = kind == 0 ? false : kind == 1 ? true : ((i + 2 * j) % 2) != 0;
+        auto src = std::make_shared<mbrwt_host::BRWTDevice>(
+            to_device(OracleMatrix(build_oracle(cols, n, 0, 2, 0))));
+        mbrwt_host::BRWTDevice cl = src->clone();
+        test_brwt(cl, cols, n);
+        src.reset();  // the image lives on in the clone
+        test_brwt(cl, cols, n);
+        test_brwt(cl.clone(), cols, n);
+    }
+}
+
 TEST(BRWT, EmptyConstructor) {  // test_BRWT.cpp:15-25
     auto m = build({}, 0);
     EXPECT_EQ(0u, m->num_columns());

@@ -531,3 +531,51 @@ def test_variable_records_ranged_async_and_errors(oracle_mod, monkeypatch):
     assert ei.value.status == L.MBRWT_ERR_RANGE
     for c in (0, 3, m - 1):
         assert dev.get_column(c).tolist() == t.get_column(c)
+
+
+@pytest.mark.parametrize("layout", ["rows", "nodes"])
+def test_clone_concurrent_streams(oracle_mod, layout):
+    """mbrwt_ctx_clone: a second query context over the same image answers
+    like the oracle while the source's queries run on another stream (their
+    workspaces are separate), and outlives the source (the image is freed
+    with the last clone)."""
+    O = oracle_mod
+    import torch
+    from genome_graph_annotation_amd import BRWTDevice
+    n, m = 200_000, 2652
+    src = BRWTDevice.synthetic(n, m, 0.003, 8, 7, layout=layout)
+    cl = src.clone()
+    assert cl.layout() == src.layout() and cl.num_rows() == n and cl.device_bytes() == src.device_bytes()
+    t = O.OracleTree.topdown(n, m, 0.003, 8, 7)
+    rng = np.random.default_rng(3)
+    batches = [rng.integers(0, n, 50_000, dtype=np.uint64) for _ in range(2)]
+    want = [t.get_rows(b) for b in batches]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for j in range(2):
+        rt = torch.from_numpy(batches[j].view(np.int64)).cuda()
+        outs.append((rt, torch.empty(len(batches[j]) + 1, dtype=torch.int64, device="cuda"),
+                     torch.empty(len(want[j][1]) + 64, dtype=torch.int32, device="cuda"),
+                     torch.zeros(3, dtype=torch.int64, device="cuda")))
+    torch.cuda.synchronize()
+    for _ in range(8):  # interleaved on two streams, no host synchronisation
+        for j, ctx in enumerate((src, cl)):
+            rt, off, cols, st = outs[j]
+            ctx.get_rows_device_async(rt, off, cols, st, streams[j].cuda_stream)
+    torch.cuda.synchronize()
+    for j in range(2):
+        rt, off, cols, st = outs[j]
+        assert st.cpu().tolist()[1:] == [0, 1]
+        np.testing.assert_array_equal(off.cpu().numpy().view(np.uint64), want[j][0])
+        np.testing.assert_array_equal(cols[:len(want[j][1])].cpu().numpy().view(np.uint32), want[j][1])
+    src.close()  # the clone keeps the image
+    off_d, cols_d = cl.get_rows(batches[0])
+    np.testing.assert_array_equal(off_d, want[0][0])
+    np.testing.assert_array_equal(cols_d, want[0][1])
+    c2 = cl.clone()  # a clone of a clone shares the same image
+    off_d, cols_d = c2.get_rows(batches[1])
+    np.testing.assert_array_equal(cols_d, want[1][1])
+    cl.close()
+    off_d, cols_d = c2.get_rows(batches[1])
+    np.testing.assert_array_equal(cols_d, want[1][1])
+    c2.close()

@@ -1,7 +1,8 @@
 """overlap_ab.py -- does batch k+1's traversal overlap batch k's output pass?
-Two row-record images of the same synthetic structure (two contexts, each
-with its own workspaces), each driven on its own stream; batches alternate
-between them (async get_rows).  Compared with one context on one stream.
+One row-record image and a clone of its context (mbrwt_ctx_clone: the same
+image, separate workspaces), each driven on its own stream; batches
+alternate between them (async get_rows).  Compared with one context on one
+stream.
 Experiment tool (not the bench); every batch's CSR hash is checked equal.
 
     python tools/overlap_ab.py --rows 3700000000 --batch 8000000 --steps 40
@@ -30,8 +31,7 @@ a = ap.parse_args()
 rows_np = np.random.default_rng(42).integers(0, a.rows, a.batch, dtype=np.uint64)
 rows = torch.from_numpy(rows_np.view(np.int64)).cuda()
 mats = [BRWTDevice.synthetic(a.rows, a.cols, a.density, 8, 42)]
-torch.cuda.synchronize()
-mats.append(BRWTDevice.synthetic(a.rows, a.cols, a.density, 8, 42))
+mats.append(mats[0].clone())  # the same image, its own workspaces (mbrwt_ctx_clone)
 torch.cuda.synchronize()
 streams = [torch.cuda.Stream(), torch.cuda.Stream()]
 need = mats[0].get_rows_device(rows, torch.empty(a.batch + 1, dtype=torch.int64, device="cuda"),
