@@ -96,6 +96,10 @@ def parse():
     ap.add_argument("--check-rows", type=int, default=0,
                     help="rows checked element-wise against the oracle (0 = the whole global batch)")
     ap.add_argument("--kernel", type=int, default=0, help="MBRWT_OPT_KERNEL variant (0 = library default)")
+    ap.add_argument("--query-streams", type=int, default=1, choices=[1, 2],
+                    help="N = 1: consecutive batches alternate between the context and a clone of it "
+                         "(mbrwt_ctx_clone: the same image, separate workspaces) on two streams, so batch "
+                         "k+1's traversal may overlap batch k's output pass")
     ap.add_argument("--sync", action="store_true",
                     help="N = 1: time the synchronous mbrwt_get_rows_device (default: the asynchronous call, "
                          "status checked after the timed region)")
@@ -381,6 +385,17 @@ def main():
     # sticky status bits -- is read once after the timed region)
     use_async = (world == 1 or wire is not None) and not a.sync
     status_t = torch.zeros(3, dtype=torch.int64, device=dev_t)
+    # N = 1 with two query streams: batch i runs on query context i mod 2 (the
+    # context, or a clone over the same image) on its own stream, into its
+    # own output buffers and status block
+    Q = a.query_streams if (world == 1 and use_async) else 1
+    qmats, qstreams, qstatus = [mat], [sptr], [status_t]
+    if Q == 2:
+        qmats.append(mat.clone())
+        side = torch.cuda.Stream(dev_t)
+        qstreams.append(side.cuda_stream)
+        qstatus.append(torch.zeros(3, dtype=torch.int64, device=dev_t))
+        bufs.append((torch.empty_like(off_t), torch.empty_like(cols_t)))
 
     def step():
         i = state["i"]
@@ -388,7 +403,8 @@ def main():
         state["i"] += 1
         h0 = time.perf_counter()
         if use_async:
-            mat.get_rows_device_async(rows_ts[i % K], o, cb, status_t, sptr)
+            q = i % Q
+            qmats[q].get_rows_device_async(rows_ts[i % K], o, cb, qstatus[q], qstreams[q])
             if state["timed"]:
                 state["get_rows_host"].append((time.perf_counter() - h0) * 1e3)
             if wire is not None:
@@ -425,8 +441,9 @@ def main():
     torch.cuda.synchronize()
     if wire is not None:
         wire.last_phases = []
-    mat.take_timing()
-    mat.set_option(L.MBRWT_OPT_TIMING, 1)
+    for qm in qmats:
+        qm.take_timing()
+        qm.set_option(L.MBRWT_OPT_TIMING, 1)
     state["timed"] = True
     if world > 1:
         dist.barrier()
@@ -441,13 +458,19 @@ def main():
     elapsed = time.perf_counter() - t0
     state["timed"] = False
     if use_async:
-        need_l, st_l, sticky = status_t.cpu().tolist()
-        if sticky != 1 << L.MBRWT_OK:
-            raise RuntimeError(f"asynchronous get_rows reported status bits {sticky:#x} (last status {st_l})")
-        n_lab = int(need_l)
+        for q, st in enumerate(qstatus):
+            need_l, st_l, sticky = st.cpu().tolist()
+            if sticky != 1 << L.MBRWT_OK:
+                raise RuntimeError(f"asynchronous get_rows reported status bits {sticky:#x} (last status {st_l})")
+            if q == (state["i"] - 1) % Q:  # the last step's context
+                n_lab = int(need_l)
     log(f"timed {a.steps} steps: {elapsed / a.steps * 1e3:.3f} ms/step")
-    mat.set_option(L.MBRWT_OPT_TIMING, 0)
-    kern_ms_total, launches = mat.take_timing()
+    kern_ms_total, launches = 0.0, 0
+    for qm in qmats:
+        qm.set_option(L.MBRWT_OPT_TIMING, 0)
+        km, kl = qm.take_timing()
+        kern_ms_total += km
+        launches += kl
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -681,6 +704,7 @@ def main():
             "num_rows": a.rows, "num_columns": a.cols, "density": a.density, "arity": a.arity,
             "global_batch": G, "batch_per_gpu": nb, "batches": K, "layout": a.layout,
             "api": "mbrwt_get_rows_device_async" if use_async else "mbrwt_get_rows_device",
+            "query_streams": Q,
             "parallelism": f"batch-sharded x{world}, tree replicated" + ("" if world == 1 or a.no_gather
                                                                          else ", all-gatherv over " + ("RCCL" if a.dist_backend == "nccl" else a.dist_backend)
                                                                          + (" (device-sized wire, no host sync)" if wire is not None else " (host-sized)")),

@@ -12,3 +12,5 @@ MBRWT_LIB=tools/_ab/libmbrwt_6bf1e26.so timeout -k 10 200 python -u tools/rows_a
 MBRWT_LIB=tools/_ab/libmbrwt_02ea363.so timeout -k 10 200 python -u tools/rows_ab.py $C4 > gpurun_out/r4l/c4_02ea363.log 2>&1 || exit 1
 timeout -k 10 200 python -u tools/rows_ab.py $C4 > gpurun_out/r4l/c4_cur2.log 2>&1 || exit 1
 timeout -k 10 300 python -u tools/overlap_ab.py --steps 40 > gpurun_out/r4l/overlap.log 2>&1 || exit 1
+timeout -k 10 300 python -u bench.py --no-cpu --traffic off --steps 30 --query-streams 2 > gpurun_out/r4l/bench_q2.log 2>&1 || exit 1
+timeout -k 10 300 python -u bench.py --no-cpu --traffic off --steps 30 --query-streams 1 > gpurun_out/r4l/bench_q1.log 2>&1 || exit 1
