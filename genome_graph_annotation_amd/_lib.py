@@ -223,7 +223,10 @@ def lib():
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                 "(there is no CPU fallback)")
         L = C.CDLL(LIB_PATH)
+        older = bool(os.environ.get("MBRWT_LIB"))  # an A/B build of an earlier commit may lack newer entry points
         for name, (res, args) in SIGNATURES.items():
+            if older and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

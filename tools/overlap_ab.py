@@ -33,7 +33,10 @@ rows = torch.from_numpy(rows_np.view(np.int64)).cuda()
 mats = [BRWTDevice.synthetic(a.rows, a.cols, a.density, 8, 42)]
 mats.append(mats[0].clone())  # the same image, its own workspaces (mbrwt_ctx_clone)
 torch.cuda.synchronize()
-streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+pool = [torch.cuda.Stream(), torch.cuda.Stream()]
+null = torch.cuda.default_stream()
+STREAMS = {"pool": pool, "null+pool": [null, pool[1]]}
+streams = pool
 need = mats[0].get_rows_device(rows, torch.empty(a.batch + 1, dtype=torch.int64, device="cuda"),
                                torch.empty(80_000_000, dtype=torch.int32, device="cuda"),
                                torch.cuda.current_stream().cuda_stream)
@@ -58,17 +61,19 @@ def digest(j):
     return h.hexdigest()
 
 
-out = {"rows": a.rows, "batch": a.batch, "steps": a.steps, "device_gb_each": mats[0].device_bytes() / 1e9}
-for mode in ("single", "dual", "single", "dual"):
-    dual = mode == "dual"
-    run(6, dual)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(a.steps, dual)
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / a.steps * 1e3
-    out.setdefault(mode, []).append({"ms_per_step": ms, "rows_per_s": a.batch / ms * 1e3})
-    print(f"{mode}: {ms:.4f} ms/step, {a.batch / ms / 1e6:.2f} G rows/s", file=sys.stderr, flush=True)
+out = {"rows": a.rows, "batch": a.batch, "steps": a.steps, "device_gb": mats[0].device_bytes() / 1e9}
+for sk in ("pool", "null+pool", "pool", "null+pool"):
+    streams = STREAMS[sk]
+    for mode in ("single", "dual"):
+        dual = mode == "dual"
+        run(6, dual)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(a.steps, dual)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / a.steps * 1e3
+        out.setdefault(f"{mode}/{sk}", []).append({"ms_per_step": ms, "rows_per_s": a.batch / ms * 1e3})
+        print(f"{mode} on {sk}: {ms:.4f} ms/step, {a.batch / ms / 1e6:.2f} G rows/s", file=sys.stderr, flush=True)
 hs = [digest(0), digest(1)]
 out["hashes"] = hs
 out["same"] = hs[0] == hs[1]
