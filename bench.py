@@ -96,10 +96,11 @@ def parse():
     ap.add_argument("--check-rows", type=int, default=0,
                     help="rows checked element-wise against the oracle (0 = the whole global batch)")
     ap.add_argument("--kernel", type=int, default=0, help="MBRWT_OPT_KERNEL variant (0 = library default)")
-    ap.add_argument("--query-streams", type=int, default=1, choices=[1, 2],
+    ap.add_argument("--query-streams", type=int, default=2, choices=[1, 2],
                     help="N = 1: consecutive batches alternate between the context and a clone of it "
-                         "(mbrwt_ctx_clone: the same image, separate workspaces) on two streams, so batch "
-                         "k+1's traversal may overlap batch k's output pass")
+                         "(mbrwt_ctx_clone: the same image, separate workspaces) on the default stream and "
+                         "a second stream, so batch k+1's traversal overlaps batch k's output pass "
+                         "(DESIGN.md §6); 1 = one context, one stream")
     ap.add_argument("--sync", action="store_true",
                     help="N = 1: time the synchronous mbrwt_get_rows_device (default: the asynchronous call, "
                          "status checked after the timed region)")

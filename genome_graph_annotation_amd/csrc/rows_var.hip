@@ -414,8 +414,11 @@ __device__ __forceinline__ void var_publish(unsigned long long *status, uint64_t
 
 // k_var_decode: R = 64 / G rows per tile (one wave), G lanes per row; the
 // grid is persistent, WPB waves per workgroup share the unit table in LDS.
+// (G >= 8: tiles of <= 8 rows need < 6 KB of LDS per wave, so 24 waves per
+// CU fit when the registers do: 6 waves per SIMD requested, 79 VGPRs, no
+// scratch; G <= 4 is bound by LDS at 16 waves per CU anyway.)
 template <int G, int WPB>
-__global__ __launch_bounds__(64 * WPB) void k_var_decode(VarParams p) {
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(G >= 8 ? 6 : 1))) void k_var_decode(VarParams p) {
     constexpr uint32_t R = 64 / G;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_var[];
     const uint32_t lane = threadIdx.x & 63;
