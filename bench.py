@@ -537,6 +537,27 @@ def main():
         del g_off, g_cols, glob_off, glob_cols
         state["global"] = None
 
+    # two query streams: the traversal's HIP-event time above includes the
+    # other stream's compaction running beside it; the same kernel timed
+    # alone (one context, one stream, untimed for `value`) is reported
+    # beside the roofline as `isolated`
+    iso = None
+    if Q == 2:
+        for _ in range(3):
+            mat.get_rows_device_async(rows_ts[0], off_t, cols_t, status_t, sptr)
+        torch.cuda.synchronize()
+        mat.take_timing()
+        mat.set_option(L.MBRWT_OPT_TIMING, 1)
+        iso_steps = 20
+        t1 = time.perf_counter()
+        for i in range(iso_steps):
+            mat.get_rows_device_async(rows_ts[i % K], off_t, cols_t, status_t, sptr)
+        torch.cuda.synchronize()
+        iso_wall = (time.perf_counter() - t1) / iso_steps * 1e3
+        mat.set_option(L.MBRWT_OPT_TIMING, 0)
+        ikm, ikl = mat.take_timing()
+        iso = {"kernel_ms": ikm / max(1, ikl), "ms_per_step": iso_wall, "steps": iso_steps}
+
     # measured ceilings of this GPU (streaming read; random 64-/128-B requests)
     stream_gbs = rnd = None
     if rank == 0 and not a.no_probe:
@@ -652,6 +673,16 @@ def main():
                                          "reference recursion; the row-record layouts issue none of these probes"},
             "visits_per_row": visits / max(1, nb), "labels_per_row": labels / max(1, nb),
             "stream_read_measured": stream_gbs}
+    if iso is not None:
+        iks = iso["kernel_ms"] / 1e3
+        iso.update({"achieved": alg_bytes / iks / 1e9 if alg_bytes else None,
+                    "frac": alg_bytes / iks / 1e9 / HBM_PEAK_GBS if alg_bytes else None,
+                    "step_minus_kernel_ms": iso["ms_per_step"] - iso["kernel_ms"],
+                    "note": "the same kernel with one context on one stream (no other batch beside it), "
+                            "20 untimed-for-value steps after the timed region; kernel_ms / achieved / frac "
+                            "above are over the timed region, where batch k+1's traversal runs beside batch "
+                            "k's compaction on a second query stream"})
+        roof["isolated"] = iso
     seg = 64
     if rstats is not None and not rstats.get("variable"):
         seg = rstats["block_bytes"]
@@ -680,8 +711,12 @@ def main():
         ceil = rnd.get(f"seg{seg}_per_s")
         if rstats is not None and not rstats.get("variable") and ceil:
             roof[f"ceiling_random{seg}_frac"] = roof["block_requests_per_s"] / ceil
+            if iso is not None:
+                iso[f"ceiling_random{seg}_frac"] = roof["block_requests_per_launch"] / (iso["kernel_ms"] / 1e3) / ceil
         elif traffic is not None and world == 1 and ceil:
             roof["ceiling_random64_frac"] = roof["read_requests_per_s"] / ceil
+            if iso is not None:
+                iso["ceiling_random64_frac"] = roof["read_requests_per_launch"] / (iso["kernel_ms"] / 1e3) / ceil
 
     value = G * a.steps / elapsed
     line = {

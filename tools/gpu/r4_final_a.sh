@@ -12,3 +12,4 @@ for c in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum; do
   timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "k_traverse_rows|k_compact_tiles" -d gpurun_out/r4fa/pmc_$c -o run --output-format csv -- python bench.py --no-cpu --traffic off --steps 5 > gpurun_out/r4fa/pmc_$c.log 2>&1 || exit 1
 done
 timeout -k 10 200 python -u tools/bench_wire.py > gpurun_out/r4fa/bench_wire.log 2>&1 || exit 1
+timeout -k 10 400 python -u bench.py --workload c3 --no-cpu > gpurun_out/r4fa/bench_c3_q2.log 2>&1 || exit 1
