@@ -131,6 +131,8 @@ SIGNATURES = {
                                         C.c_uint32, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]),
     "mbrwt_unpack_labels_device": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32,
                                              C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
+    "mbrwt_unpack_offsets_device": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64, u64p, C.c_uint32, C.c_void_p,
+                                              C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p]),
     "mbrwt_destroy": (None, [C.c_void_p]),
     "mbrwt_ctx_clone": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
     "mbrwt_set_build_option": (C.c_int, [C.c_int, C.c_int64]),

@@ -2,6 +2,8 @@
 // exchange (genome_graph_annotation_amd/dist.py): n values < 2^bits become
 // ceil(n * bits / 32) u32 words, value i at bits [i*bits, (i+1)*bits),
 // LSB-first.  One pass each way; the unpacking writes the int32 CSR directly.
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 
 #include "device_access.hpp"
@@ -199,6 +201,152 @@ __global__ __launch_bounds__(256) void k_unpack_labels_dev(const uint8_t *__rest
     }
 }
 
+// row i's count from the wire: its segment by the row prefix (an unrolled
+// count over at most kWireScanSegs boundaries, read from a small device
+// table: the functor is copied into every scan thread, so it stays a few
+// words -- a table inside it went to scratch), then its `bits`-bit field at
+// byte 8 of the segment (the scan's input iterator)
+constexpr uint32_t kWireScanSegs = 8;
+struct WireCount {
+    const uint8_t *base;
+    const uint64_t *first;  // kWireScanSegs + 1 row prefixes (device)
+    uint64_t stride;
+    uint32_t nseg, bits;
+    __host__ __device__ __forceinline__ uint64_t operator()(const uint64_t &i) const {
+        uint32_t sg = 0;
+        uint64_t f = 0;
+#pragma unroll
+        for (uint32_t k = 1; k < kWireScanSegs; ++k) {
+            const uint64_t fk = first[k];
+            const bool past = k < nseg && i >= fk;
+            sg += past ? 1u : 0u;
+            f = past ? fk : f;
+        }
+        if (i >= first[nseg]) return 0;
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(base + sg * stride + 8);
+        const uint64_t pos = (i - f) * bits;
+        const uint64_t k = pos >> 5;
+        const uint32_t off = (uint32_t)(pos & 31);
+        uint32_t x = w[k] >> off;
+        if (off + bits > 32) x |= w[k + 1] << (32 - off);
+        return bits == 32 ? x : (x & ((1u << bits) - 1u));
+    }
+};
+struct WireFirst {
+    uint64_t v[kWireScanSegs + 1];
+};
+__global__ void k_wire_first(WireFirst f, uint64_t *out) {
+    if (threadIdx.x <= kWireScanSegs) out[threadIdx.x] = f.v[threadIdx.x];
+}
+
+// labels of <= 12 bits (every BASELINE shape: < 4,096 columns): thread t of
+// a workgroup takes labels 8 t .. 8 t + 7 of each of the workgroup's R tiles
+// of 2,048 -- one 16-byte load covers their <= 96 bits (plus the offset
+// into the first word), two 16-byte stores write them; every load of the
+// workgroup is issued before its first store (the headers' latency is paid
+// once per R tiles, not per tile), no LDS stage.  A group of 8 that crosses
+// a segment boundary takes the label-by-label path.
+constexpr uint32_t kUnpackTiles12 = 4;
+__global__ __launch_bounds__(256) void k_unpack_labels12(const uint8_t *__restrict__ base, uint64_t stride,
+                                                         uint32_t nseg, uint64_t lab_off, uint64_t cap,
+                                                         uint32_t bits, uint32_t *__restrict__ out,
+                                                         uint64_t out_cap, unsigned long long *status) {
+    __shared__ uint64_t first[kMaxSegs + 1];
+    __shared__ uint32_t bad;
+    if (threadIdx.x < 64) {  // the headers, one lane each, then a wave scan
+        const uint32_t r = threadIdx.x;
+        uint64_t L = 0;
+        if (r < nseg) {
+            const uint32_t *h = reinterpret_cast<const uint32_t *>(base + r * stride);
+            L = (uint64_t)gld(h) | ((uint64_t)gld(h + 1) << 32);
+        }
+        const bool over = L > cap;
+        const uint64_t Lc = L < cap ? L : cap;
+        uint64_t x = Lc;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(x, d, 64);
+            if (r >= d) x += y;
+        }
+        if (r < nseg) first[r + 1] = x;
+        if (r == 0) first[0] = 0;
+        const uint64_t tot = __shfl(x, 63, 64);
+        const bool any_over = __any(over);
+        if (r == 0) {
+            bad = (any_over || tot > out_cap) ? 1u : 0u;
+            if (blockIdx.x == 0) {
+                status[0] = tot;
+                status[1] = bad;
+            }
+        }
+    }
+    __syncthreads();
+    if (bad) return;
+    const uint64_t N = first[nseg];
+    const uint32_t mask = (1u << bits) - 1u;
+    auto seg_of = [&](uint64_t i) {
+        uint32_t lo = 0, hi = nseg;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (first[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+        return lo;
+    };
+    u32x4_t v[kUnpackTiles12];
+    uint32_t sh[kUnpackTiles12];
+    bool fast[kUnpackTiles12];
+    const uint64_t seg_words = (cap + 31) / 32 * bits;  // a segment's label words (whole 32-value chunks)
+    const uint64_t g0 = (uint64_t)blockIdx.x * kUnpackTiles12 * kUnpackTile;
+#pragma unroll
+    for (uint32_t r = 0; r < kUnpackTiles12; ++r) {
+        const uint64_t i = g0 + (uint64_t)r * kUnpackTile + 8 * threadIdx.x;
+        fast[r] = false;
+        sh[r] = 0;
+        if (i >= N) continue;
+        const uint32_t sg = seg_of(i);
+        if (i + 8 > first[sg + 1]) continue;  // (crosses a segment's end, or the batch's: slow path)
+        const uint64_t pos = (i - first[sg]) * bits;
+        if ((pos >> 5) + 4 > seg_words) continue;  // (the 4 words must lie in the segment's label words)
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(base + sg * stride + lab_off) + (pos >> 5);
+        sh[r] = (uint32_t)(pos & 31);
+        v[r] = u32x4_t{gld(w), gld(w + 1), gld(w + 2), gld(w + 3)};
+        fast[r] = true;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kUnpackTiles12; ++r) {
+        const uint64_t i = g0 + (uint64_t)r * kUnpackTile + 8 * threadIdx.x;
+        if (i >= N) continue;
+        if (fast[r]) {
+            const uint64_t lo = (uint64_t)v[r].x | ((uint64_t)v[r].y << 32);
+            const uint64_t hi = (uint64_t)v[r].z | ((uint64_t)v[r].w << 32);
+            // bits [sh, sh + 8 bits) of the 128-bit value hi:lo
+            uint32_t lab[8];
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t b = sh[r] + j * bits;  // < 128
+                const uint64_t a = b < 64 ? (lo >> b) | (b ? hi << (64 - b) : 0) : hi >> (b - 64);
+                lab[j] = (uint32_t)a & mask;
+            }
+            u32x4_t o0{lab[0], lab[1], lab[2], lab[3]}, o1{lab[4], lab[5], lab[6], lab[7]};
+            *(AS_GLOBAL u32x4_t *)(uintptr_t)(out + i) = o0;
+            *(AS_GLOBAL u32x4_t *)(uintptr_t)(out + i + 4) = o1;
+        } else {
+            const uint64_t e = i + 8 < N ? i + 8 : N;
+            for (uint64_t k = i; k < e; ++k) {
+                const uint32_t sg = seg_of(k);
+                const uint32_t *wd = reinterpret_cast<const uint32_t *>(base + sg * stride + lab_off);
+                const uint64_t pos = (k - first[sg]) * bits;
+                const uint64_t w = pos >> 5;
+                const uint32_t off = (uint32_t)(pos & 31);
+                uint32_t x = gld(wd + w) >> off;
+                if (off + bits > 32) x |= gld(wd + w + 1) << (32 - off);
+                gst(out + k, x & mask);
+            }
+        }
+    }
+}
+
 unsigned grid_of(uint64_t n) { return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 16384)); }
 
 }  // namespace
@@ -299,6 +447,45 @@ int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint
     return MBRWT_OK;
 }
 
+int mbrwt_unpack_offsets_device(const void *d_base, uint32_t nseg, uint64_t seg_stride, const uint64_t *counts,
+                                uint32_t bits, uint64_t *d_offsets, void *d_temp, uint64_t *temp_bytes,
+                                void *stream) {
+    if (bits < 1 || bits > 32 || !d_base || !counts || !temp_bytes || nseg < 1 || seg_stride % 4 ||
+        (d_temp && !d_offsets)) {
+        set_error("invalid argument");
+        return MBRWT_ERR_INVALID;
+    }
+    if (nseg > kWireScanSegs) {
+        set_error("more than 8 segments: unpack the counts (mbrwt_unpack_segments_device) and scan them");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
+    WireFirst wf{};
+    for (uint32_t r = 0; r < nseg; ++r) wf.v[r + 1] = wf.v[r] + counts[r];
+    for (uint32_t r = nseg + 1; r <= kWireScanSegs; ++r) wf.v[r] = wf.v[nseg];
+    const uint64_t N = wf.v[nseg];
+    // scratch: the row prefixes (128 bytes), then the scan's own
+    uint64_t *d_first = reinterpret_cast<uint64_t *>(d_temp);
+    WireCount wc{reinterpret_cast<const uint8_t *>(d_base), d_first, seg_stride, nseg, bits};
+    hipcub::CountingInputIterator<uint64_t> idx(0);
+    hipcub::TransformInputIterator<uint64_t, WireCount, hipcub::CountingInputIterator<uint64_t>> it(idx, wc);
+    size_t need = 0;
+    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need, it, d_offsets, N + 1, (hipStream_t)stream));
+    if (!d_temp) {
+        *temp_bytes = need + 128;
+        return MBRWT_OK;
+    }
+    if (*temp_bytes < need + 128) {
+        set_error("scratch smaller than the size the scan needs");
+        return MBRWT_ERR_INVALID;
+    }
+    hipLaunchKernelGGL(k_wire_first, dim3(1), dim3(64), 0, (hipStream_t)stream, wf, d_first);
+    MBRWT_HIP(hipGetLastError());
+    size_t have = (size_t)*temp_bytes - 128;
+    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(reinterpret_cast<uint8_t *>(d_temp) + 128, have, it, d_offsets, N + 1,
+                                               (hipStream_t)stream));
+    return MBRWT_OK;
+}
+
 int mbrwt_unpack_labels_device(const void *d_base, uint32_t nseg, uint64_t seg_stride, uint64_t labels_offset,
                                uint64_t labels_cap, uint32_t bits, uint32_t *d_values, uint64_t values_cap,
                                uint64_t *d_status, void *stream) {
@@ -308,6 +495,20 @@ int mbrwt_unpack_labels_device(const void *d_base, uint32_t nseg, uint64_t seg_s
         return MBRWT_ERR_INVALID;
     }
     const uint64_t bound = std::min<uint64_t>(values_cap, (uint64_t)nseg * labels_cap);
+    if (bits <= 12 && (reinterpret_cast<uintptr_t>(d_values) & 15) == 0) {
+        // (16-byte stores at label 8 t: the output must be 16-byte aligned)
+        const uint64_t per = (uint64_t)kUnpackTiles12 * kUnpackTile;
+        const unsigned wgs = (unsigned)std::max<uint64_t>(1, (bound + per - 1) / per);
+        if ((bound + per - 1) / per > (1u << 24)) {
+            set_error("batch too large for the unpack grid");
+            return MBRWT_ERR_UNSUPPORTED;
+        }
+        hipLaunchKernelGGL(k_unpack_labels12, dim3(wgs), dim3(256), 0, (hipStream_t)stream,
+                           reinterpret_cast<const uint8_t *>(d_base), seg_stride, nseg, labels_offset, labels_cap, bits,
+                           d_values, values_cap, reinterpret_cast<unsigned long long *>(d_status));
+        MBRWT_HIP(hipGetLastError());
+        return MBRWT_OK;
+    }
     // one tile per workgroup (no grid-stride rounds: a workgroup's tile is
     // two dependent memory latencies, so rounds serialise them)
     const unsigned tiles = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((bound + kUnpackTile - 1) / kUnpackTile, 1u << 20));

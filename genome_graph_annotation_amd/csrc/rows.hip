@@ -1649,17 +1649,29 @@ RowsView view_of(const Ctx &c) {
 
 using RowsFn = void (*)(RowsParams);
 constexpr uint32_t kRowsWpb = 8;
+// the tree odometer's wide workgroups: a large walk table (the greedy +
+// relax shape's 8.8 KB, staged once per workgroup) leaves room for only two
+// 8-wave workgroups per CU (16 waves); two of 11 waves fit (22)
+constexpr uint32_t kRowsWpbWide = 11;
 template <int B, bool NT>
-RowsFn rows_fn_b(uint32_t walk) {
+RowsFn rows_fn_b(uint32_t walk, uint32_t wpb) {
+    if (wpb == kRowsWpbWide) return k_traverse_rows<B, kRowsWpbWide, NT, WALK_TREE_ODOMETER>;
     return walk == WALK_ODOMETER        ? k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER>
            : walk == WALK_TREE_ODOMETER ? k_traverse_rows<B, kRowsWpb, NT, WALK_TREE_ODOMETER>
            : walk == WALK_MASK1         ? k_traverse_rows<B, kRowsWpb, NT, WALK_MASK1>
                                  : k_traverse_rows<B, kRowsWpb, NT, WALK_GENERAL>;
 }
-RowsFn rows_fn(const RowsImage &im, uint32_t walk) {
+RowsFn rows_fn(const RowsImage &im, uint32_t walk, uint32_t wpb) {
     const bool nt = im.bytes > (1ull << 30);  // non-temporal block reads for images beyond the caches
-    if (im.B == 64) return nt ? rows_fn_b<64, true>(walk) : rows_fn_b<64, false>(walk);
-    return nt ? rows_fn_b<128, true>(walk) : rows_fn_b<128, false>(walk);
+    if (im.B == 64) return nt ? rows_fn_b<64, true>(walk, wpb) : rows_fn_b<64, false>(walk, wpb);
+    return nt ? rows_fn_b<128, true>(walk, wpb) : rows_fn_b<128, false>(walk, wpb);
+}
+// resident waves per CU with workgroups of w waves: the LDS (160 KiB per CU:
+// the table once per workgroup + per_wave bytes per wave) within the 24-wave cap
+uint32_t rows_waves_per_cu(size_t table_bytes, size_t per_wave, uint32_t w) {
+    const size_t lds = table_bytes + w * per_wave;
+    const uint32_t wgs = std::min<uint32_t>((uint32_t)((160u << 10) / std::max<size_t>(1, lds)), 24u / w);
+    return wgs * w;
 }
 // per-lane stack slots of the general walks: the current frame is held in
 // registers and only a descent pushes, so at most frames - 1 are pending.
@@ -1760,10 +1772,15 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     p.frames = im.frames;
     p.mask1 = im.mask1 ? 1u : 0u;
 
-    const RowsFn kfn = rows_fn(im, walk);
-    const uint32_t wpb = kRowsWpb;
-    const size_t lds = ((im.table2.size() + 3) & ~size_t(3)) * 4 +
-                       wpb * (64ull * (im.B + 4) + 256ull * p.stk_words + (walk >= WALK_ODOMETER ? 2ull * C : 0ull));
+    const size_t table_bytes = ((im.table2.size() + 3) & ~size_t(3)) * 4;
+    const size_t per_wave = 64ull * (im.B + 4) + 256ull * p.stk_words + (walk >= WALK_ODOMETER ? 2ull * C : 0ull);
+    const uint32_t wpb = (walk == WALK_TREE_ODOMETER && !im.occ_cap &&
+                          rows_waves_per_cu(table_bytes, per_wave, kRowsWpbWide) >
+                              rows_waves_per_cu(table_bytes, per_wave, kRowsWpb))
+                             ? kRowsWpbWide
+                             : kRowsWpb;
+    const RowsFn kfn = rows_fn(im, walk, wpb);
+    const size_t lds = table_bytes + wpb * per_wave;
     const uint32_t threads = 64 * wpb;
     // at most 24 waves (3 workgroups of 8) per CU: more waves make the walk phase
     // slower than the extra loads in flight gain (C4 0.426 ms at 3 against

@@ -268,13 +268,25 @@ class DeviceAllGatherV:
         self.timing = timing
         N = sum(self.ns)
         self.N = N
+        # the global offsets straight from the packed counts: one scan whose
+        # input unpacks them (mbrwt_unpack_offsets_device), its scratch sized
+        # once (every unpack runs on the one side stream, so one scratch)
+        import ctypes as C
+        self._counts = (C.c_uint64 * self.world)(*self.ns)
+        self.fused_offsets = self.world <= 8  # (beyond one node: counts unpacked, then scanned)
+        tb = C.c_uint64(0)
+        if self.fused_offsets:
+            L.check(L.lib().mbrwt_unpack_offsets_device(C.c_void_p(16), self.world, self.per, self._counts,
+                                                        self.bits_c, None, None, C.byref(tb), None),
+                    "mbrwt_unpack_offsets_device")
+        self.scan_tmp = torch.empty(max(16, int(tb.value)), dtype=torch.uint8, device=device)
         self.slots = []
         for _ in range(slots):
             self.slots.append({
                 "send": torch.empty(self.per, dtype=torch.uint8, device=device),
                 "recv": torch.empty(self.world * self.per, dtype=torch.uint8, device=device),
-                "cnt": torch.empty(max(1, N), dtype=torch.int32, device=device),
                 "off": torch.zeros(N + 1, dtype=torch.int64, device=device),
+                "cnt": None if self.fused_offsets else torch.empty(max(1, N), dtype=torch.int32, device=device),
                 "cols": torch.empty(max(1, self.world * self.cap) + 32, dtype=torch.int32, device=device),
                 "status": torch.zeros(2, dtype=torch.int64, device=device),
                 "done": torch.cuda.Event(),
@@ -313,17 +325,23 @@ class DeviceAllGatherV:
                 sl["ev"]["gathered"].record(self.side)
             ss = self.side.cuda_stream
             import ctypes as C
-            arr = (C.c_uint64 * self.world)(*self.ns)
             base = sl["recv"].data_ptr()
-            # row counts (static per rank) at byte 8 of every segment, then the
-            # labels with their device-side prefix, then the global offsets
-            L.check(L.lib().mbrwt_unpack_segments_device(base + 8, self.world, self.per, arr, self.bits_c,
-                                                         sl["cnt"].data_ptr(), ss), "mbrwt_unpack_segments_device")
+            # the labels with their device-side prefix, then the global offsets
+            # from the row counts (static per rank) at byte 8 of every segment
             L.check(L.lib().mbrwt_unpack_labels_device(base, self.world, self.per, self.lab_off, self.cap,
                                                        self.bits_l, sl["cols"].data_ptr(), sl["cols"].numel(),
                                                        sl["status"].data_ptr(), ss), "mbrwt_unpack_labels_device")
-            if self.N:
-                torch.cumsum(sl["cnt"][:self.N], 0, dtype=torch.int64, out=sl["off"][1:])
+            if self.fused_offsets:
+                tb = C.c_uint64(self.scan_tmp.numel())
+                L.check(L.lib().mbrwt_unpack_offsets_device(base, self.world, self.per, self._counts, self.bits_c,
+                                                            sl["off"].data_ptr(), self.scan_tmp.data_ptr(),
+                                                            C.byref(tb), ss), "mbrwt_unpack_offsets_device")
+            else:
+                L.check(L.lib().mbrwt_unpack_segments_device(base + 8, self.world, self.per, self._counts,
+                                                             self.bits_c, sl["cnt"].data_ptr(), ss),
+                        "mbrwt_unpack_segments_device")
+                if self.N:
+                    torch.cumsum(sl["cnt"][:self.N], 0, dtype=torch.int64, out=sl["off"][1:])
             if sl["ev"]:
                 sl["ev"]["done"].record(self.side)
             sl["done"].record(self.side)

@@ -447,6 +447,18 @@ int mbrwt_unpack_labels_device(const void *d_base, uint32_t nseg, uint64_t seg_s
                                uint64_t labels_cap, uint32_t bits, uint32_t *d_values, uint64_t values_cap,
                                uint64_t *d_status, void *stream);
 
+/* The global CSR offsets of an all-gathered wire straight from its packed
+   row counts (r04): d_offsets[0 .. N] = the exclusive prefix of every
+   segment's counts (segment r: counts[r] values of `bits` bits each at byte
+   8 of d_base + r * seg_stride, the layout mbrwt_pack_csr_device writes),
+   N = sum(counts) -- one scan whose input iterator unpacks the counts, no
+   int32 count array in between.  d_temp == NULL: *temp_bytes receives the
+   scratch size the call needs and nothing runs.  At most 8 segments (one
+   node); MBRWT_ERR_UNSUPPORTED beyond (unpack the counts and scan them). */
+int mbrwt_unpack_offsets_device(const void *d_base, uint32_t nseg, uint64_t seg_stride, const uint64_t *counts,
+                                uint32_t bits, uint64_t *d_offsets, void *d_temp, uint64_t *temp_bytes,
+                                void *stream);
+
 #define MBRWT_OPT_TIMING 1       /* 1: time the traversal kernel with HIP events */
 #define MBRWT_OPT_SLOT_LABELS 2  /* per-row label slots of the fast path (0 = auto) */
 #define MBRWT_OPT_KERNEL 4       /* traversal kernel (A/B measurement): 0 default (k_traverse_p2w, else
