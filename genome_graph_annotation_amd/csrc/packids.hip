@@ -2,8 +2,6 @@
 // exchange (genome_graph_annotation_amd/dist.py): n values < 2^bits become
 // ceil(n * bits / 32) u32 words, value i at bits [i*bits, (i+1)*bits),
 // LSB-first.  One pass each way; the unpacking writes the int32 CSR directly.
-#include <hipcub/hipcub.hpp>
-
 #include <algorithm>
 
 #include "device_access.hpp"
@@ -201,42 +199,131 @@ __global__ __launch_bounds__(256) void k_unpack_labels_dev(const uint8_t *__rest
     }
 }
 
-// row i's count from the wire: its segment by the row prefix (an unrolled
-// count over at most kWireScanSegs boundaries, read from a small device
-// table: the functor is copied into every scan thread, so it stays a few
-// words -- a table inside it went to scratch), then its `bits`-bit field at
-// byte 8 of the segment (the scan's input iterator)
+// The global offsets from the wire's packed row counts (at byte 8 of every
+// segment): three passes over blocks of kOffRows rows -- per-block sums,
+// one workgroup scanning the sums, then each block's counts re-read and
+// scanned in LDS with the block's prefix added, written as coalesced u64s.
+// (A hipcub scan over an iterator unpacking the counts took 87 us for 8 M
+// rows: its per-item loads do not coalesce.)
 constexpr uint32_t kWireScanSegs = 8;
-struct WireCount {
-    const uint8_t *base;
-    const uint64_t *first;  // kWireScanSegs + 1 row prefixes (device)
-    uint64_t stride;
-    uint32_t nseg, bits;
-    __host__ __device__ __forceinline__ uint64_t operator()(const uint64_t &i) const {
-        uint32_t sg = 0;
-        uint64_t f = 0;
-#pragma unroll
-        for (uint32_t k = 1; k < kWireScanSegs; ++k) {
-            const uint64_t fk = first[k];
-            const bool past = k < nseg && i >= fk;
-            sg += past ? 1u : 0u;
-            f = past ? fk : f;
-        }
-        if (i >= first[nseg]) return 0;
-        const uint32_t *w = reinterpret_cast<const uint32_t *>(base + sg * stride + 8);
-        const uint64_t pos = (i - f) * bits;
-        const uint64_t k = pos >> 5;
-        const uint32_t off = (uint32_t)(pos & 31);
-        uint32_t x = w[k] >> off;
-        if (off + bits > 32) x |= w[k + 1] << (32 - off);
-        return bits == 32 ? x : (x & ((1u << bits) - 1u));
-    }
-};
+constexpr uint32_t kOffRows = 2048;  // rows per block: 8 per thread
 struct WireFirst {
     uint64_t v[kWireScanSegs + 1];
 };
-__global__ void k_wire_first(WireFirst f, uint64_t *out) {
-    if (threadIdx.x <= kWireScanSegs) out[threadIdx.x] = f.v[threadIdx.x];
+struct WireCounts {
+    const uint8_t *base;
+    uint64_t stride;
+    uint32_t nseg, bits;
+    WireFirst f;
+};
+// row i's count (i < N); first[] in LDS
+__device__ __forceinline__ uint32_t wire_count(const WireCounts &w, const uint64_t *first, uint64_t i) {
+    uint32_t sg = 0;
+#pragma unroll
+    for (uint32_t k = 1; k < kWireScanSegs; ++k) sg += (k < w.nseg && i >= first[k]) ? 1u : 0u;
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(w.base + sg * w.stride + 8);
+    const uint64_t pos = (i - first[sg]) * w.bits;
+    const uint64_t k = pos >> 5;
+    const uint32_t off = (uint32_t)(pos & 31);
+    uint32_t x = gld(p + k) >> off;
+    if (off + w.bits > 32) x |= gld(p + k + 1) << (32 - off);
+    return w.bits == 32 ? x : (x & ((1u << w.bits) - 1u));
+}
+__device__ __forceinline__ uint64_t block_sum256(uint64_t v, uint64_t *red) {
+#pragma unroll
+    for (uint32_t d = 32; d > 0; d >>= 1) v += __shfl_down(v, d, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const uint64_t t = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    return t;
+}
+__global__ __launch_bounds__(256) void k_off_sums(WireCounts w, uint64_t *sums) {
+    __shared__ uint64_t first[kWireScanSegs + 1];
+    __shared__ uint64_t red[4];
+    if (threadIdx.x <= kWireScanSegs) first[threadIdx.x] = w.f.v[threadIdx.x];
+    __syncthreads();
+    const uint64_t N = first[w.nseg];
+    const uint64_t i0 = (uint64_t)blockIdx.x * kOffRows + 8 * threadIdx.x;  // (blocked: 16.5 vs 22 us striped)
+    uint64_t s = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j)
+        if (i0 + j < N) s += wire_count(w, first, i0 + j);
+    const uint64_t t = block_sum256(s, red);
+    if (threadIdx.x == 0) sums[blockIdx.x] = t;
+}
+// one workgroup: exclusive scan of the block sums in place, in chunks of 1,024
+__global__ __launch_bounds__(1024) void k_off_scan_sums(uint64_t *sums, uint64_t nblk) {
+    __shared__ uint64_t wsum[16];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint64_t c0 = 0; c0 < nblk; c0 += 1024) {
+        const uint64_t i = c0 + threadIdx.x;
+        const uint64_t v = i < nblk ? sums[i] : 0;
+        uint64_t x = v;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) wsum[wv] = x;
+        __syncthreads();
+        uint64_t before = carry;
+        for (uint32_t k = 0; k < wv; ++k) before += wsum[k];
+        if (i < nblk) sums[i] = before + x - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = before + x;
+        __syncthreads();
+    }
+}
+// counts loaded and offsets stored row-striped (row base + t + 256 j:
+// coalesced), scanned blocked (thread t: rows 8 t .. 8 t + 7) through LDS
+__global__ __launch_bounds__(256) void k_off_write(WireCounts w, const uint64_t *sums, uint64_t *offsets) {
+    __shared__ uint64_t first[kWireScanSegs + 1];
+    __shared__ uint64_t wsum[4];
+    __shared__ uint32_t lc[kOffRows];  // counts, then block-relative inclusive prefixes (< 2^32: 2,048 rows)
+    if (threadIdx.x <= kWireScanSegs) first[threadIdx.x] = w.f.v[threadIdx.x];
+    __syncthreads();
+    const uint64_t N = first[w.nseg];
+    const uint64_t rb = (uint64_t)blockIdx.x * kOffRows;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        const uint64_t i = rb + threadIdx.x + 256 * j;
+        lc[threadIdx.x + 256 * j] = i < N ? wire_count(w, first, i) : 0u;
+    }
+    __syncthreads();
+    uint32_t c[8], s = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        c[j] = lc[8 * threadIdx.x + j];
+        s += c[j];
+    }
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t x = s;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t run = x - s;
+    for (uint32_t k = 0; k < wv; ++k) run += (uint32_t)wsum[k];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        run += c[j];
+        lc[8 * threadIdx.x + j] = run;
+    }
+    __syncthreads();
+    const uint64_t base = sums[blockIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x == 0) offsets[0] = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        const uint32_t r = threadIdx.x + 256 * j;
+        if (rb + r < N) offsets[rb + r + 1] = base + lc[r];
+    }
 }
 
 // labels of <= 12 bits (every BASELINE shape: < 4,096 columns): thread t of
@@ -459,30 +546,37 @@ int mbrwt_unpack_offsets_device(const void *d_base, uint32_t nseg, uint64_t seg_
         set_error("more than 8 segments: unpack the counts (mbrwt_unpack_segments_device) and scan them");
         return MBRWT_ERR_UNSUPPORTED;
     }
-    WireFirst wf{};
-    for (uint32_t r = 0; r < nseg; ++r) wf.v[r + 1] = wf.v[r] + counts[r];
-    for (uint32_t r = nseg + 1; r <= kWireScanSegs; ++r) wf.v[r] = wf.v[nseg];
-    const uint64_t N = wf.v[nseg];
-    // scratch: the row prefixes (128 bytes), then the scan's own
-    uint64_t *d_first = reinterpret_cast<uint64_t *>(d_temp);
-    WireCount wc{reinterpret_cast<const uint8_t *>(d_base), d_first, seg_stride, nseg, bits};
-    hipcub::CountingInputIterator<uint64_t> idx(0);
-    hipcub::TransformInputIterator<uint64_t, WireCount, hipcub::CountingInputIterator<uint64_t>> it(idx, wc);
-    size_t need = 0;
-    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need, it, d_offsets, N + 1, (hipStream_t)stream));
+    WireCounts wc{reinterpret_cast<const uint8_t *>(d_base), seg_stride, nseg, bits, WireFirst{}};
+    for (uint32_t r = 0; r < nseg; ++r) wc.f.v[r + 1] = wc.f.v[r] + counts[r];
+    for (uint32_t r = nseg + 1; r <= kWireScanSegs; ++r) wc.f.v[r] = wc.f.v[nseg];
+    const uint64_t N = wc.f.v[nseg];
+    const uint64_t nblk = (N + kOffRows - 1) / kOffRows;
+    // scratch: the block sums
+    const uint64_t need = std::max<uint64_t>(1, nblk) * 8;
     if (!d_temp) {
-        *temp_bytes = need + 128;
+        *temp_bytes = need;
         return MBRWT_OK;
     }
-    if (*temp_bytes < need + 128) {
+    if (*temp_bytes < need) {
         set_error("scratch smaller than the size the scan needs");
         return MBRWT_ERR_INVALID;
     }
-    hipLaunchKernelGGL(k_wire_first, dim3(1), dim3(64), 0, (hipStream_t)stream, wf, d_first);
+    if (nblk > 0x7FFFFFFFull) {
+        set_error("too many rows");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
+    const hipStream_t s = (hipStream_t)stream;
+    if (!N) {
+        MBRWT_HIP(hipMemsetAsync(d_offsets, 0, 8, s));
+        return MBRWT_OK;
+    }
+    uint64_t *sums = reinterpret_cast<uint64_t *>(d_temp);
+    hipLaunchKernelGGL(k_off_sums, dim3((unsigned)nblk), dim3(256), 0, s, wc, sums);
     MBRWT_HIP(hipGetLastError());
-    size_t have = (size_t)*temp_bytes - 128;
-    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(reinterpret_cast<uint8_t *>(d_temp) + 128, have, it, d_offsets, N + 1,
-                                               (hipStream_t)stream));
+    hipLaunchKernelGGL(k_off_scan_sums, dim3(1), dim3(1024), 0, s, sums, nblk);
+    MBRWT_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_off_write, dim3((unsigned)nblk), dim3(256), 0, s, wc, (const uint64_t *)sums, d_offsets);
+    MBRWT_HIP(hipGetLastError());
     return MBRWT_OK;
 }
 

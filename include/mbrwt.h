@@ -451,8 +451,9 @@ int mbrwt_unpack_labels_device(const void *d_base, uint32_t nseg, uint64_t seg_s
    row counts (r04): d_offsets[0 .. N] = the exclusive prefix of every
    segment's counts (segment r: counts[r] values of `bits` bits each at byte
    8 of d_base + r * seg_stride, the layout mbrwt_pack_csr_device writes),
-   N = sum(counts) -- one scan whose input iterator unpacks the counts, no
-   int32 count array in between.  d_temp == NULL: *temp_bytes receives the
+   N = sum(counts) -- block sums, one workgroup's scan of them, then every
+   block's counts re-read and scanned in LDS (no int32 count array in
+   between).  d_temp == NULL: *temp_bytes receives the
    scratch size the call needs and nothing runs.  At most 8 segments (one
    node); MBRWT_ERR_UNSUPPORTED beyond (unpack the counts and scan them). */
 int mbrwt_unpack_offsets_device(const void *d_base, uint32_t nseg, uint64_t seg_stride, const uint64_t *counts,
