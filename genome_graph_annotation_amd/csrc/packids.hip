@@ -115,6 +115,65 @@ __global__ __launch_bounds__(256) void k_pack_csr(const uint64_t *__restrict__ o
     }
 }
 
+// k_pack_csr for 12-bit counts and labels (every BASELINE shape: < 4,096
+// columns): thread t packs values 8 t .. 8 t + 7 of a field into its words
+// 3 t .. 3 t + 2 (8 x 12 bits = 3 words exactly) -- 16-byte loads of the
+// labels (or of the offsets), three word stores; a thread whose 8 values run
+// past the field's end packs them one by one.  Threads [0, cnt_threads) pack
+// the counts, the rest the labels.
+__global__ __launch_bounds__(256) void k_pack_csr12(const uint64_t *__restrict__ offsets, uint64_t n_rows,
+                                                    const uint32_t *__restrict__ cols, uint64_t cols_cap,
+                                                    const uint64_t *__restrict__ num_labels, uint64_t cap,
+                                                    uint32_t *__restrict__ wire, uint64_t lab_word0,
+                                                    uint64_t cnt_threads, uint64_t lab_threads) {
+    const uint64_t L = gld(num_labels);
+    const bool lost = L > cols_cap;
+    const uint64_t nl = lost ? 0 : L < cap ? L : cap;
+    const uint64_t hdr = lost ? ~0ull : L;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        gst(wire, (uint32_t)hdr);
+        gst(wire + 1, (uint32_t)(hdr >> 32));
+    }
+    if (lost) return;
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= cnt_threads + lab_threads) return;
+    const bool lab = g >= cnt_threads;
+    const uint64_t t = lab ? g - cnt_threads : g;
+    const uint64_t n = lab ? nl : n_rows;
+    const uint64_t i0 = 8 * t;
+    if (i0 >= n) return;  // (the words past the field's values stay zero: memset)
+    uint32_t v[8];
+    if (i0 + 8 <= n) {
+        if (lab) {
+            const u32x4_t a = *(const AS_GLOBAL u32x4_t *)(uintptr_t)(cols + i0);
+            const u32x4_t b = *(const AS_GLOBAL u32x4_t *)(uintptr_t)(cols + i0 + 4);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+            v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        } else {
+            uint64_t o[9];
+#pragma unroll
+            for (uint32_t j = 0; j < 9; ++j) o[j] = gld(offsets + i0 + j);
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j) v[j] = (uint32_t)(o[j + 1] - o[j]);
+        }
+    } else {
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint64_t i = i0 + j;
+            v[j] = i < n ? (lab ? gld(cols + i) : (uint32_t)(gld(offsets + i + 1) - gld(offsets + i))) : 0u;
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) v[j] &= 0xFFFu;
+    const uint32_t w0 = v[0] | (v[1] << 12) | (v[2] << 24);
+    const uint32_t w1 = (v[2] >> 8) | (v[3] << 4) | (v[4] << 16) | (v[5] << 28);
+    const uint32_t w2 = (v[5] >> 4) | (v[6] << 8) | (v[7] << 20);
+    uint32_t *dst = wire + (lab ? lab_word0 : 2) + 3 * t;
+    gst(dst, w0);
+    gst(dst + 1, w1);
+    gst(dst + 2, w2);
+}
+
 // the labels of every segment, the segments' sizes from their headers.
 // A workgroup writes global labels [2048 g, 2048 g + 2048): when they lie in
 // one segment (nearly always), their packed bits are staged in LDS by
@@ -525,6 +584,19 @@ int mbrwt_pack_csr_device(const uint64_t *d_offsets, uint64_t n_rows, const uint
     if (8 + cnt_chunks * bits_count * 4 > lab_off || lab_off + lab_chunks * bits_label * 4 > wire_bytes) {
         set_error("wire segment too small for whole 32-value chunks");
         return MBRWT_ERR_INVALID;
+    }
+    if (bits_count == 12 && bits_label == 12 && (reinterpret_cast<uintptr_t>(d_cols) & 15) == 0 && lab_off % 4 == 0) {
+        // (16-byte label loads at value 8 t: the CSR must be 16-byte aligned)
+        const uint64_t ct = (n_rows + 7) / 8, lt = (labels_cap + 7) / 8;
+        const uint64_t th = std::max<uint64_t>(1, ct + lt);
+        if ((th + 255) / 256 > 0x7FFFFFFFull) {
+            set_error("batch too large for the pack grid");
+            return MBRWT_ERR_UNSUPPORTED;
+        }
+        hipLaunchKernelGGL(k_pack_csr12, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, d_offsets, n_rows, d_cols,
+                           cols_cap, d_num_labels, labels_cap, reinterpret_cast<uint32_t *>(d_wire), lab_off / 4, ct, lt);
+        MBRWT_HIP(hipGetLastError());
+        return MBRWT_OK;
     }
     const uint64_t cnt_words = (n_rows * bits_count + 31) / 32, lab_words_used = (labels_cap * bits_label + 31) / 32;
     hipLaunchKernelGGL(k_pack_csr, dim3(grid_of(std::max<uint64_t>(1, cnt_words + lab_words_used))), dim3(256), 0, s,

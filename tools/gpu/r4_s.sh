@@ -1,5 +1,5 @@
-# r04 step S: the device wire's offsets by a three-pass scan of the packed
-# counts: wire + 2-rank tests, the wire micro-benchmark and its kernel trace
+# r04 step S: the device wire: three-pass offsets scan, register-based 12-bit
+# pack and unpack: wire + 2-rank tests, the wire micro-benchmark and its kernel trace
 set -o pipefail
 mkdir -p gpurun_out/r4s
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
