@@ -101,6 +101,9 @@ def parse():
                          "(mbrwt_ctx_clone: the same image, separate workspaces) on the default stream and "
                          "a second stream, so batch k+1's traversal overlaps batch k's output pass "
                          "(DESIGN.md §6); 1 = one context, one stream")
+    ap.add_argument("--kernel-timing", choices=["all", "first", "off"], default="all",
+                    help="HIP events around the dominant kernel in the timed region: every query context, the "
+                         "first only, or none (diagnosis: the events' own cost)")
     ap.add_argument("--sync", action="store_true",
                     help="N = 1: time the synchronous mbrwt_get_rows_device (default: the asynchronous call, "
                          "status checked after the timed region)")
@@ -442,9 +445,10 @@ def main():
     torch.cuda.synchronize()
     if wire is not None:
         wire.last_phases = []
-    for qm in qmats:
+    for qi, qm in enumerate(qmats):
         qm.take_timing()
-        qm.set_option(L.MBRWT_OPT_TIMING, 1)
+        if a.kernel_timing == "all" or (a.kernel_timing == "first" and qi == 0):
+            qm.set_option(L.MBRWT_OPT_TIMING, 1)
     state["timed"] = True
     if world > 1:
         dist.barrier()
@@ -572,6 +576,8 @@ def main():
     # "probe-equivalent": the layouts answer a row without those probes
     probe_bytes = 64 * visits + 16 * nb + 4 * labels
     kern_ms = kern_ms_total / max(1, launches)
+    if launches == 0 and iso is not None:  # (--kernel-timing off: the isolated pass's time stands in)
+        kern_ms = iso["kernel_ms"]
     kname = mat.traverse_kernel()
     rstats = mat.rows_stats()
 

@@ -32,23 +32,27 @@ rows_np = np.random.default_rng(42).integers(0, a.rows, a.batch, dtype=np.uint64
 rows = torch.from_numpy(rows_np.view(np.int64)).cuda()
 mats = [BRWTDevice.synthetic(a.rows, a.cols, a.density, 8, 42)]
 mats.append(mats[0].clone())  # the same image, its own workspaces (mbrwt_ctx_clone)
+mats.append(mats[0].clone())
 torch.cuda.synchronize()
 pool = [torch.cuda.Stream(), torch.cuda.Stream()]
 null = torch.cuda.default_stream()
-STREAMS = {"pool": pool, "null+pool": [null, pool[1]]}
+hi = torch.cuda.Stream(priority=-1)
+STREAMS = {"pool": pool, "null+pool": [null, pool[1]], "null+hi": [null, hi], "null+pool+hi": [null, pool[1], hi],
+           "null+pool+pool": [null, pool[0], pool[1]]}
 streams = pool
 need = mats[0].get_rows_device(rows, torch.empty(a.batch + 1, dtype=torch.int64, device="cuda"),
                                torch.empty(80_000_000, dtype=torch.int32, device="cuda"),
                                torch.cuda.current_stream().cuda_stream)
 bufs = [(torch.empty(a.batch + 1, dtype=torch.int64, device="cuda"),
          torch.empty(int(need) + 1024, dtype=torch.int32, device="cuda"),
-         torch.zeros(3, dtype=torch.int64, device="cuda")) for _ in range(2)]
+         torch.zeros(3, dtype=torch.int64, device="cuda")) for _ in range(3)]
 torch.cuda.synchronize()
 
 
 def run(k, dual):
+    q = len(streams) if dual else 1
     for i in range(k):
-        j = i % 2 if dual else 0
+        j = i % q
         off, cols, st = bufs[j]
         mats[j].get_rows_device_async(rows, off, cols, st, streams[j].cuda_stream)
 
@@ -62,7 +66,7 @@ def digest(j):
 
 
 out = {"rows": a.rows, "batch": a.batch, "steps": a.steps, "device_gb": mats[0].device_bytes() / 1e9}
-for sk in ("pool", "null+pool", "pool", "null+pool"):
+for sk in ("pool", "null+pool", "null+hi", "null+pool+hi", "null+pool+pool", "null+pool"):
     streams = STREAMS[sk]
     for mode in ("single", "dual"):
         dual = mode == "dual"
