@@ -68,8 +68,10 @@ WORKLOADS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    # (a step is ~0.36 ms: 50 timed steps after 10 warm-up steps keep the
+    # timed region clear of the first steps' ramp, profiles/r04/v13_query_streams/)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c4",
                     help="BASELINE config preset (c4 = configs[3], the driver's default; c3 = configs[2]; "
                          "c2 = configs[1]); --rows/--cols/--density/--batch/--layout override it")
