@@ -38,7 +38,8 @@ def _slices(O, n_batch, world, num_columns, seed=5):
     return t, rows, out
 
 
-@pytest.mark.parametrize("world,n_batch,num_columns", [(3, 30_001, 2652), (4, 3, 2652), (2, 10_000, None)])
+@pytest.mark.parametrize("world,n_batch,num_columns", [(3, 30_001, 2652), (4, 3, 2652), (2, 10_000, None),
+                                                     (8, 40_003, 2652), (5, 20_001, 5000)])
 def test_wire_segments_reassemble(oracle_mod, world, n_batch, num_columns):
     import torch
     from genome_graph_annotation_amd import _lib as L
@@ -72,6 +73,20 @@ def test_wire_segments_reassemble(oracle_mod, world, n_batch, num_columns):
     g_off = np.concatenate([[0], np.cumsum(cnt[:N].cpu().numpy().astype(np.uint64))]).astype(np.uint64)
     np.testing.assert_array_equal(g_off, off_o)
     np.testing.assert_array_equal(g_cols[:tot].cpu().numpy().view(np.uint32), cols_o)
+    # the global offsets straight from the packed counts (r04: three-pass scan)
+    tb = C.c_uint64(0)
+    L.check(L.lib().mbrwt_unpack_offsets_device(recv.data_ptr(), world, per, arr, bits_c, None, None, C.byref(tb), s),
+            "offsets scratch")
+    tmp = torch.zeros(max(16, int(tb.value)), dtype=torch.uint8, device="cuda")
+    off_d = torch.full((N + 1,), -1, dtype=torch.int64, device="cuda")
+    L.check(L.lib().mbrwt_unpack_offsets_device(recv.data_ptr(), world, per, arr, bits_c, off_d.data_ptr(),
+                                                tmp.data_ptr(), C.byref(tb), s), "offsets")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(off_d.cpu().numpy().view(np.uint64), off_o)
+    if world <= 8:  # (nine segments: beyond one node, the call declines)
+        arr9 = (C.c_uint64 * 9)(*([1] * 9))
+        assert L.lib().mbrwt_unpack_offsets_device(recv.data_ptr(), 9, per, arr9, bits_c, None, None,
+                                                   C.byref(tb), s) == L.MBRWT_ERR_UNSUPPORTED
     # a label capacity below a slice's count: flagged, nothing written
     small = min(int(x[3][0].item()) for x in sl if x[0] > 0)
     if small > 1:
