@@ -28,6 +28,9 @@ MBRWT_OPT_ROWS_WALK = 8
 
 MBRWT_BUILD_LAYOUT = 1
 MBRWT_BUILD_PARTITIONER = 2
+MBRWT_BUILD_ROWS_FOOTPRINT = 3
+MBRWT_ROWS_FAST = 0
+MBRWT_ROWS_COMPACT = 1
 MBRWT_PARTITIONER_BASIC = 0
 MBRWT_PARTITIONER_GREEDY = 1
 PARTITIONERS = {"basic": MBRWT_PARTITIONER_BASIC, "greedy": MBRWT_PARTITIONER_GREEDY}

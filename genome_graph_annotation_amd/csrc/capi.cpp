@@ -608,6 +608,10 @@ int mbrwt_set_build_option(int option, int64_t value) {
         set_build_partitioner((int)value);
         return MBRWT_OK;
     }
+    if (option == MBRWT_BUILD_ROWS_FOOTPRINT && (value == MBRWT_ROWS_FAST || value == MBRWT_ROWS_COMPACT)) {
+        set_rows_footprint((int)value);
+        return MBRWT_OK;
+    }
     if (option != MBRWT_BUILD_LAYOUT || value < MBRWT_LAYOUT_AUTO || value > MBRWT_LAYOUT_BOTH) {
         set_error("unknown build option or value");
         return MBRWT_ERR_INVALID;
@@ -617,11 +621,14 @@ int mbrwt_set_build_option(int option, int64_t value) {
 }
 
 int mbrwt_get_build_option(int option, int64_t *value) {
-    if (!value || (option != MBRWT_BUILD_LAYOUT && option != MBRWT_BUILD_PARTITIONER)) {
+    if (!value || (option != MBRWT_BUILD_LAYOUT && option != MBRWT_BUILD_PARTITIONER &&
+                   option != MBRWT_BUILD_ROWS_FOOTPRINT)) {
         set_error("unknown build option or null output");
         return MBRWT_ERR_INVALID;
     }
-    *value = option == MBRWT_BUILD_LAYOUT ? thread_build_layout() : build_partitioner();
+    *value = option == MBRWT_BUILD_LAYOUT        ? thread_build_layout()
+             : option == MBRWT_BUILD_PARTITIONER ? build_partitioner()
+                                                 : rows_footprint();
     return MBRWT_OK;
 }
 

@@ -289,6 +289,8 @@ uint32_t rwt2_uniform_levels(const std::vector<uint32_t> &table2);
 int build_layout();
 void set_build_layout(int layout);
 int thread_build_layout();  // the value set for the calling thread (AUTO when unset)
+void set_rows_footprint(int v);  // MBRWT_BUILD_ROWS_FOOTPRINT of the calling thread
+int rows_footprint();
 
 // Cross-stream ordering of a context's workspaces.  A *_device call returns
 // with work still queued on the caller's stream that reads the context's

@@ -60,6 +60,9 @@ int build_layout() {
 
 void set_build_layout(int layout) { g_build_layout = layout; }
 int thread_build_layout() { return g_build_layout; }
+static thread_local int g_rows_footprint = 0;  // MBRWT_ROWS_FAST
+void set_rows_footprint(int v) { g_rows_footprint = v; }
+int rows_footprint() { return g_rows_footprint; }
 
 // ------------------------------------------------------------------------
 // RWT table
@@ -450,6 +453,7 @@ struct RowsBuild {
     uint64_t n = 0, align = 1;
     bool decided = false;
     bool auto_layout = false;  // layout AUTO: decline records that cost more than kAutoMaxCost requests per row
+    int footprint = 0;         // MBRWT_BUILD_ROWS_FOOTPRINT of the creating thread
     VarScratch vws;            // variable-length records (rows_var.hip)
     double var_bytes_per_row = 0;  // their size per row, measured on the first range
     RowsImage img;
@@ -478,6 +482,7 @@ RowsBuild *rows_build_begin(Ctx &top, uint64_t num_rows, uint64_t align, bool au
     if (!rb) return nullptr;
     rb->top = &top;
     rb->auto_layout = auto_layout;
+    rb->footprint = g_rows_footprint;
     rb->n = num_rows;
     rb->align = std::max<uint64_t>(1, align);
     rb->s = top.stream;
@@ -653,9 +658,15 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
                 set_error("row records too long for the block layout");
                 return MBRWT_ERR_UNSUPPORTED;
             }
+            // FAST: the smallest within 2 % of the fewest modelled requests;
+            // COMPACT (MBRWT_BUILD_ROWS_FOOTPRINT): within 30 % -- the model
+            // prices a spilled row as a whole request, while on walk-bound
+            // shapes its reload overlaps other waves' walks (greedy + relax,
+            // 20 % of rows spilled: +2 % kernel time)
+            const double tol = rb.footprint == 1 ? 1.30 : 1.02;
             const Cand *best = nullptr;
             for (const Cand &c : cands)
-                if (c.mem <= budget && c.t <= tmin * 1.02 && (!best || c.mem < best->mem)) best = &c;
+                if (c.mem <= budget && c.t <= tmin * tol && (!best || c.mem < best->mem)) best = &c;
             im.B = best->B;
             im.S = best->S;
             if (const char *e = std::getenv("MBRWT_ROWS_BS")) {  // A/B switch: "B,S"

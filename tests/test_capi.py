@@ -40,6 +40,36 @@ def test_status_strings_and_options():
         assert getattr(L, name) == int(val), name
 
 
+def test_build_options_thread_local():
+    """mbrwt_set/get_build_option: layout, partitioner and row-record
+    footprint per calling thread; unknown options or values rejected; the
+    Python scope restores the caller's value."""
+    import ctypes as C
+    import threading
+    from genome_graph_annotation_amd import _lib as L
+    from genome_graph_annotation_amd.brwt import build_option
+    lib = L.lib()
+
+    def get(opt):
+        v = C.c_int64(-1)
+        assert lib.mbrwt_get_build_option(opt, C.byref(v)) == L.MBRWT_OK
+        return v.value
+
+    assert get(L.MBRWT_BUILD_ROWS_FOOTPRINT) == L.MBRWT_ROWS_FAST
+    with build_option(L.MBRWT_BUILD_ROWS_FOOTPRINT, L.MBRWT_ROWS_COMPACT):
+        assert get(L.MBRWT_BUILD_ROWS_FOOTPRINT) == L.MBRWT_ROWS_COMPACT
+        seen = []
+        th = threading.Thread(target=lambda: seen.append(get(L.MBRWT_BUILD_ROWS_FOOTPRINT)))
+        th.start()
+        th.join()
+        assert seen == [L.MBRWT_ROWS_FAST]  # (thread-local)
+    assert get(L.MBRWT_BUILD_ROWS_FOOTPRINT) == L.MBRWT_ROWS_FAST
+    assert lib.mbrwt_set_build_option(L.MBRWT_BUILD_ROWS_FOOTPRINT, 2) == L.MBRWT_ERR_INVALID
+    assert lib.mbrwt_set_build_option(99, 0) == L.MBRWT_ERR_INVALID
+    v = C.c_int64(0)
+    assert lib.mbrwt_get_build_option(99, C.byref(v)) == L.MBRWT_ERR_INVALID
+
+
 def test_null_arguments_fail_cleanly():
     from genome_graph_annotation_amd import _lib as L
     lib = L.lib()

@@ -579,3 +579,29 @@ def test_clone_concurrent_streams(oracle_mod, layout):
     off_d, cols_d = c2.get_rows(batches[1])
     np.testing.assert_array_equal(cols_d, want[1][1])
     c2.close()
+
+
+def test_rows_compact_footprint(oracle_mod):
+    """MBRWT_BUILD_ROWS_FOOTPRINT = MBRWT_ROWS_COMPACT: the greedy + relax
+    shape's records in a smaller (or equal) image than the default's, every
+    row like the oracle."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice, _lib as L
+    from genome_graph_annotation_amd.brwt import build_option
+    rng = np.random.default_rng(17)
+    n, m = 30_000, 600
+    dense = rng.random((n, m)) < 0.012
+    t = O.OracleTree.from_dense(dense, "greedy", 2, 10)
+    ex = t.export()
+    fast = BRWTDevice.from_tree(ex, layout="rows")
+    with build_option(L.MBRWT_BUILD_ROWS_FOOTPRINT, L.MBRWT_ROWS_COMPACT):
+        comp = BRWTDevice.from_tree(ex, layout="rows")
+    assert comp.device_bytes() <= fast.device_bytes()
+    sf, sc = fast.rows_stats(), comp.rows_stats()
+    assert sc["block_bytes"] / sc["rows_per_block"] <= sf["block_bytes"] / sf["rows_per_block"]
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 20_000)]).astype(np.uint64)
+    off_o, cols_o = t.get_rows(rows)
+    for d in (fast, comp):
+        off_d, cols_d = d.get_rows(rows)
+        np.testing.assert_array_equal(off_d, off_o)
+        np.testing.assert_array_equal(cols_d, cols_o)

@@ -97,6 +97,9 @@ def main():
                          "leaf_column, BFS) from a file written by --save-shape: skips the oracle's greedy build "
                          "(~2.5 min) and measures only the scaled shape")
     ap.add_argument("--save-shape", default="", help="write the greedy + relax shape of the C2 build to this .npz")
+    ap.add_argument("--compact", action="store_true",
+                    help="row records built with MBRWT_BUILD_ROWS_FOOTPRINT = MBRWT_ROWS_COMPACT (the smallest image "
+                         "within 30 %% of the fewest modelled requests per row)")
     ap.add_argument("--layout", default="nodes", choices=["nodes", "rows", "both"],
                     help="device layout (include/mbrwt.h MBRWT_BUILD_LAYOUT)")
     a = ap.parse_args()
@@ -147,7 +150,11 @@ def main():
             keep = {k: exp[k] for k in ("num_children", "first_child", "leaf_column")}
             nc = np.asarray(keep["num_children"])
             t0 = time.time()
-            dev = BRWTDevice.synthetic_shaped(a.scaled_rows, keep, a.density, 42, layout=a.layout)
+            from genome_graph_annotation_amd import _lib as LB
+            from genome_graph_annotation_amd.brwt import build_option
+            with build_option(LB.MBRWT_BUILD_ROWS_FOOTPRINT,
+                              LB.MBRWT_ROWS_COMPACT if a.compact else LB.MBRWT_ROWS_FAST):
+                dev = BRWTDevice.synthetic_shaped(a.scaled_rows, keep, a.density, 42, layout=a.layout)
             torch.cuda.synchronize()
             gen_s = time.time() - t0
             t0 = time.time()
