@@ -367,14 +367,14 @@ def main():
     wire = None
     if world > 1 and not a.no_gather and not a.host_sizes:
         # the device-sized all-gatherv: every rank's wire segment holds up to
-        # labels_cap labels, agreed once here (max over ranks and batches)
-        cap_t = torch.tensor([int(need * 1.02) + 1024], dtype=torch.int64, device=dev_t)
-        dist.all_reduce(cap_t, op=dist.ReduceOp.MAX)
+        # labels_cap labels -- this rank's sizing (max over its batches); the
+        # constructor agrees on the largest over the ranks and checks that
+        # every rank passed the same slices (dist._agree_wire)
         rows_per_rank = [shard_bounds(G, world, r)[1] - shard_bounds(G, world, r)[0] for r in range(world)]
         # 3 slots: up to 2 exchanges in flight behind the current step, so
         # step k's pack + all-gather (RCCL stream) and step k-1's unpack (side
         # stream) overlap instead of chaining through the main stream
-        wire = DeviceAllGatherV(rows_per_rank, int(cap_t.item()), a.cols, dev_t, timing=True, slots=3)
+        wire = DeviceAllGatherV(rows_per_rank, int(need * 1.02) + 1024, a.cols, dev_t, timing=True, slots=3)
 
     # N > 1: steps are pipelined -- batch k's all-gatherv (RCCL stream) runs
     # while batch k+1 is traversed, so the outputs are double-buffered; drain()

@@ -1239,6 +1239,13 @@ __device__ __forceinline__ void rows_walk_tree(const AS_LDS uint8_t *pb, uint32_
     }
 }
 
+#if defined(MBRWT_AB_STAMPS)
+// A/B diagnostics (tools/ build only, never the release library): per wave,
+// shader-clock cycles spent in each phase of the tile loop
+constexpr uint32_t kAbStampWaves = 16384, kAbStampWords = 8;
+__device__ unsigned long long g_ab_stamps[kAbStampWaves * kAbStampWords];
+#endif
+
 // k_traverse_rows: one wave per tile of 64 query rows (file comment).
 // B: block bytes; WPB: waves per workgroup (the RWT2 table is staged once per
 // workgroup; the grid is persistent); WALK: the walk family.
@@ -1273,7 +1280,22 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
     uint64_t t = (uint64_t)blockIdx.x * WPB + wv;
     uint64_t row_n = 0;  // the row of this lane in the wave's next tile
     if (t < ntiles && t * 64 + lane < p.n) row_n = gld(p.rows + t * 64 + lane);
+#if defined(MBRWT_AB_STAMPS)
+    uint64_t ab_ph[5] = {0, 0, 0, 0, 0}, ab_tiles = 0, ab_t0 = __builtin_amdgcn_s_memtime();
+    uint64_t ab_last = ab_t0;
+#define AB_STAMP(k)                                               \
+    do {                                                          \
+        const uint64_t ab_now = __builtin_amdgcn_s_memtime();     \
+        ab_ph[k] += ab_now - ab_last;                             \
+        ab_last = ab_now;                                         \
+    } while (0)
+#else
+#define AB_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
     for (; t < ntiles; t += tstride) {
+        AB_STAMP(4);
         const uint64_t r0 = t * 64;
         const uint32_t nr = (uint32_t)(p.n - r0 < 64 ? p.n - r0 : 64);
         const uint64_t row = row_n;
@@ -1283,7 +1305,12 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
         if (lane < nr && !valid) atomicOr(&p.scalars[2], 1ull);
         const uint64_t b = valid ? rows_block(row, S, p.magic) : 0;
         const uint32_t sub = (uint32_t)(row - b * S);
+#if defined(MBRWT_AB_HOT)
+        // (timing only: every block read from a 256 KiB window, cache-resident)
+        const uint64_t addr = p.blocks + (b & 4095u) * B;
+#else
         const uint64_t addr = p.blocks + b * B;
+#endif
         // the 64 blocks as coalesced quarters: load k brings rows RPI k ..
         // RPI k + RPI - 1, lane L its 16 bytes L % LPB
         u32x4_t q[LPB];
@@ -1303,6 +1330,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
             d[3] = q[k].w;
         }
         wave_sync();
+        AB_STAMP(0);
         uint32_t cnt = 0, o = 0;
         bool spl = false;
         if (valid) {
@@ -1351,8 +1379,13 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
         const bool has_long = __any(lng);
         uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
         if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)(cnt | (lng ? 0x8000u : 0u)));
+        AB_STAMP(1);
         if (!direct) {
+#if defined(MBRWT_AB_NOWALK)
+            const bool live = false;  // (timing only: no walk)
+#else
             const bool live = valid && cnt > 0 && !lng;
+#endif
             if constexpr (WALK == WALK_ODOMETER || WALK == WALK_TREE_ODOMETER) {
                 // the odometer into the wave's LDS label stage, then the
                 // tile's labels as 16-byte vector stores (a few wide stores
@@ -1398,6 +1431,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
                     }
                 }
                 wave_sync();
+                AB_STAMP(2);
                 const uint32_t nbytes = total * 2;
                 for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
                     gst(reinterpret_cast<u32x4_t *>(treg + 128 + q2),
@@ -1411,7 +1445,20 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
         }
         if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u) | (has_long ? 0x40000000u : 0u));
         wave_sync();  // the slots are reused
+        AB_STAMP(3);
+#if defined(MBRWT_AB_STAMPS)
+        ++ab_tiles;
+#endif
     }
+#if defined(MBRWT_AB_STAMPS)
+    AB_STAMP(4);
+    const uint32_t gw = blockIdx.x * WPB + wv;
+    if (lane < kAbStampWords && gw < kAbStampWaves) {
+        uint64_t v = lane < 5 ? ab_ph[lane] : lane == 5 ? ab_tiles : lane == 6 ? ab_last - ab_t0 : 1;
+        gst(reinterpret_cast<unsigned long long *>(g_ab_stamps) + gw * kAbStampWords + lane, (unsigned long long)v);
+    }
+#endif
+#undef AB_STAMP
 }
 
 // tile regions -> CSR: one wave per TPW consecutive tiles (every load of
@@ -1886,6 +1933,20 @@ __global__ void k_set_status(unsigned long long *status, uint64_t need, uint64_t
     status[2] |= 1ull << st;
 }
 }  // namespace
+
+#if defined(MBRWT_AB_STAMPS)
+// A/B diagnostics: the per-wave phase cycles of the last k_traverse_rows
+// launch (waves x 8 words: load, parse + scan, walk, output, loop, tiles,
+// total, written) -- then cleared
+extern "C" int mbrwt_ab_stamps(uint64_t *out, uint64_t words) {
+    const uint64_t n = std::min<uint64_t>(words, (uint64_t)kAbStampWaves * kAbStampWords);
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ab_stamps), n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+    static const std::vector<unsigned long long> zero((size_t)kAbStampWaves * kAbStampWords, 0ull);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_ab_stamps), zero.data(), zero.size() * 8, 0, hipMemcpyHostToDevice) != hipSuccess)
+        return 1;
+    return 0;
+}
+#endif
 
 int rows_set_status(uint64_t *d_status, uint64_t need, int rc, hipStream_t s) {
     hipLaunchKernelGGL(k_set_status, dim3(1), dim3(1), 0, s, reinterpret_cast<unsigned long long *>(d_status), need,

@@ -246,9 +246,16 @@ class DeviceAllGatherV:
     label count above labels_cap sets status[1]; the caller reads the status
     after its timed region.  GPU tensors and RCCL (or gloo) only.
 
-    rows_per_rank: every rank's slice length (host ints, the same on every
-    rank); labels_cap: the per-rank label capacity (the same on every rank);
-    slots: output double-buffering for pipelined steps."""
+    rows_per_rank: every rank's slice length (host ints; every rank must pass
+    the same list); labels_cap: this rank's label capacity -- the ranks AGREE
+    on the largest one here, so callers may pass their own sizing; slots:
+    output double-buffering for pipelined steps.
+
+    The wire segments of all ranks must have one size, or the all-gather
+    mismatches (gloo aborts, RCCL hangs or reads past a segment), so the
+    constructor is collective: it agrees on labels_cap (MAX over the group)
+    and checks that every rank passed the same rows_per_rank and
+    num_columns, raising the same ValueError on every rank otherwise."""
 
     def __init__(self, rows_per_rank, labels_cap, num_columns, device, group=None, timing=False, slots=2):
         from . import _lib as L
@@ -256,9 +263,10 @@ class DeviceAllGatherV:
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        assert len(rows_per_rank) == self.world
+        if len(rows_per_rank) != self.world:
+            raise ValueError(f"rows_per_rank has {len(rows_per_rank)} entries for a group of {self.world} ranks")
         self.ns = [int(x) for x in rows_per_rank]
-        self.cap = int(labels_cap)
+        self.cap = _agree_wire(self.ns, int(labels_cap), int(num_columns), group, device)
         self.bits_l, self.bits_c = wire_bits(num_columns)
         n_max = max(self.ns)
         self.lab_off = int(L.lib().mbrwt_wire_labels_offset(n_max, self.bits_c))
@@ -374,6 +382,28 @@ class DeviceAllGatherV:
 
 
 _SIDE = {}
+
+
+def _agree_wire(ns, labels_cap, num_columns, group, device):
+    """Collective precondition of the fixed-size wire: every rank's segment
+    layout is a function of (rows_per_rank, labels_cap, num_columns), so all
+    three must be equal on every rank.  Returns the group's largest
+    labels_cap; raises ValueError on EVERY rank (they all see the same
+    reduced values) when rows_per_rank or num_columns differ."""
+    v = [labels_cap, num_columns, len(ns)] + list(ns)
+    on = device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    mx = torch.tensor(v, dtype=torch.int64, device=on)
+    mn = -mx  # MIN as the MAX of the negation: one reduction op for both backends
+    both = torch.cat([mx, mn])
+    dist.all_reduce(both, op=dist.ReduceOp.MAX, group=group)
+    both = both.cpu().tolist()
+    hi, lo = both[:len(v)], [-x for x in both[len(v):]]
+    if hi[1:] != lo[1:]:
+        what = "num_columns" if hi[1] != lo[1] else "rows_per_rank"
+        raise ValueError(f"DeviceAllGatherV: the ranks passed different {what} "
+                         f"(max {hi[1] if what == 'num_columns' else hi[3:]}, "
+                         f"min {lo[1] if what == 'num_columns' else lo[3:]}); the wire segments would differ")
+    return int(hi[0])
 
 
 def _side_stream(dev):

@@ -143,3 +143,49 @@ def test_pipelined_allgatherv_start_finish():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(ok and n == 4 for _, ok, n in res)
+
+
+def _agree_worker(rank, world, port, q, mismatch):
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from genome_graph_annotation_amd.dist import _agree_wire
+        ns = [5, 4, 4][:world]
+        if mismatch == "rows" and rank == 1:
+            ns = [4, 5, 4][:world]
+        m = 2652 + (1 if mismatch == "cols" and rank == world - 1 else 0)
+        try:
+            cap = _agree_wire(ns, 1000 + 24 * rank, m, None, torch.device("cpu"))
+            q.put((rank, "ok", cap))
+        except ValueError as e:
+            q.put((rank, "error", str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,mismatch", [(2, None), (3, None), (2, "rows"), (3, "cols")])
+def test_device_wire_agrees_on_layout(world, mismatch):
+    """DeviceAllGatherV's collective precondition (the r4c
+    gloo abort): ranks that pass different label capacities agree on the
+    largest; ranks that pass different slices or column counts all raise the
+    same ValueError before any wire collective (the exchange itself with
+    per-rank capacities: tests/test_gpu_dist.py)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, world, port, q, mismatch)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    res = sorted(q.get(timeout=5) for _ in range(world))
+    assert [r[0] for r in res] == list(range(world))
+    if mismatch is None:
+        assert all(r[1] == "ok" and r[2] == 1000 + 24 * (world - 1) for r in res), res
+    else:
+        assert all(r[1] == "error" for r in res), res
+        assert len({r[2] for r in res}) == 1, res  # the same message on every rank
+        assert ("rows_per_rank" if mismatch == "rows" else "num_columns") in res[0][2]
+    assert all(p.exitcode == 0 for p in procs)

@@ -50,9 +50,13 @@ def _rank(rank, world, port, q):
         nb = hi - lo
         globals_np = [np.random.default_rng(500 + k).integers(0, n, G, dtype=np.uint64) for k in range(K)]
         rows_ts = [torch.from_numpy(np.ascontiguousarray(g[lo:hi]).view(np.int64)).to(dev_t) for g in globals_np]
-        cap = int((G + world - 1) // world * 8 * 1.3) + 1024  # (every rank's wire has the same size)
+        # each rank sizes its own capacity from its own slice (they differ:
+        # r4c's gloo abort); DeviceAllGatherV agrees on the largest itself
+        cap = int(nb * 8 * 1.3) + 1024 + 24 * rank
         rows_per_rank = [shard_bounds(G, world, r)[1] - shard_bounds(G, world, r)[0] for r in range(world)]
         wire = DeviceAllGatherV(rows_per_rank, cap, m, dev_t, slots=3)
+        assert wire.cap == int(max(shard_bounds(G, world, r)[1] - shard_bounds(G, world, r)[0]
+                                   for r in range(world)) * 8 * 1.3) + 1024 + 24 * (world - 1) or world == 1
         bufs = [(torch.empty(nb + 1, dtype=torch.int64, device=dev_t), torch.empty(cap, dtype=torch.int32, device=dev_t))
                 for _ in range(2)]
         status = torch.zeros(3, dtype=torch.int64, device=dev_t)
