@@ -115,6 +115,7 @@ def parse():
                          "same kernel sources, or none")
     ap.add_argument("--traffic-out", default="", help="write the live traffic summary (JSON) here")
     ap.add_argument("--no-probe", action="store_true", help="skip the measured ceilings")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host buffers) leg")
     ap.add_argument("--pmc-pass", action="store_true", help=argparse.SUPPRESS)  # child under rocprofv3
     a = ap.parse_args()
     w = WORKLOADS[a.workload]
@@ -283,6 +284,74 @@ def probe_ceilings(dev_t, stream_ptr, free_bytes, struct_bytes=64 << 30):
         del buf
     torch.cuda.empty_cache()
     return stream_gbs, rnd
+
+
+def pcie_rates(dev_t, mib=256):
+    """Pinned H2D / D2H GB/s of this box (torch copies of `mib` MiB, best of 3):
+    the PCIe bound of the end-to-end leg."""
+    nb = mib << 20
+    d = torch.empty(nb, dtype=torch.uint8, device=dev_t)
+    h = torch.empty(nb, dtype=torch.uint8).pin_memory()
+    out = {}
+    for name, fn in (("h2d", lambda: d.copy_(h, non_blocking=True)), ("d2h", lambda: h.copy_(d, non_blocking=True))):
+        fn()
+        torch.cuda.synchronize()
+        best = 0.0
+        for _ in range(3):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            best = max(best, nb / (time.perf_counter() - t0) / 1e9)
+        out[name + "_GBs"] = best
+    del d, h
+    return out
+
+
+def end_to_end(mat, rows_np, n_labels, dev_t, ref_hash, reps=3):
+    """The drop-in path (SURVEY §8(d) 'also'): host row ids -> host CSR through
+    mbrwt_get_rows (csrc/hostpipe.cpp: chunks of 2^20 rows, upload / query /
+    download overlapped), on the bench's own batch, with caller buffers that
+    are pageable (numpy: staged through pinned slots) and page-locked (torch
+    pin_memory: DMA straight into them).  Best of `reps` calls after one
+    warm-up; the CSR is hashed against the device-resident result."""
+    import ctypes as C
+    from genome_graph_annotation_amd import _lib as L
+    n = len(rows_np)
+    lib = L.lib()
+    rates = pcie_rates(dev_t)
+    bytes_in, bytes_out = 8 * n, 8 * (n + 1) + 4 * n_labels
+    bound_s = max(bytes_in / (rates["h2d_GBs"] * 1e9), bytes_out / (rates["d2h_GBs"] * 1e9))
+    out = {"rows": n, "labels": n_labels, "bytes_in": bytes_in, "bytes_out": bytes_out, "pcie": rates,
+           "pcie_bound_ms": bound_s * 1e3, "pcie_bound_rows_per_s": n / bound_s}
+    kinds = {
+        "pageable": (rows_np, np.empty(n + 1, dtype=np.uint64), np.empty(n_labels, dtype=np.uint32)),
+        "pinned": (torch.from_numpy(rows_np.view(np.int64)).pin_memory(),
+                   torch.empty(n + 1, dtype=torch.int64).pin_memory(),
+                   torch.empty(max(1, n_labels), dtype=torch.int32).pin_memory()),
+    }
+    for kind, (r, o, c) in kinds.items():
+        def ptr(x, t):
+            return C.cast(C.c_void_p(x.data_ptr() if kind == "pinned" else x.ctypes.data), C.POINTER(t))
+        need = C.c_uint64(0)
+        times = []
+        for i in range(reps + 1):
+            t0 = time.perf_counter()
+            st = lib.mbrwt_get_rows(mat._h, ptr(r, C.c_uint64), n, ptr(o, C.c_uint64), ptr(c, C.c_uint32), n_labels,
+                                    C.byref(need))
+            dt = time.perf_counter() - t0
+            if st != L.MBRWT_OK or need.value != n_labels:
+                raise RuntimeError(f"end-to-end mbrwt_get_rows ({kind}): status {st}, labels {need.value}")
+            if i:
+                times.append(dt)
+        oh = o.numpy().view(np.uint64) if kind == "pinned" else o
+        ch = c.numpy().view(np.uint32)[:n_labels] if kind == "pinned" else c
+        best = min(times)
+        h = csr_hash(oh, ch)
+        out[kind] = {"ms": best * 1e3, "rows_per_s": n / best, "d2h_GBs": bytes_out / best / 1e9,
+                     "vs_pcie_bound": best / bound_s, "csr_hash": h, "bit_exact_vs_device": h == ref_hash,
+                     "ms_all": [t * 1e3 for t in times]}
+    del kinds
+    return out
 
 
 def main():
@@ -578,7 +647,13 @@ def main():
     # "probe-equivalent": the layouts answer a row without those probes
     probe_bytes = 64 * visits + 16 * nb + 4 * labels
     kern_ms = kern_ms_total / max(1, launches)
-    if launches == 0 and iso is not None:  # (--kernel-timing off: the isolated pass's time stands in)
+    # the roofline's kernel time must fit inside the step:
+    # with two query streams the HIP events around one traversal also span
+    # the other stream's compaction running beside it, so the kernel timed
+    # alone on one stream (the isolated pass) is the roofline's time and the
+    # overlapped event time is reported beside it
+    kern_ms_overlapped = kern_ms if Q == 2 else None
+    if iso is not None:
         kern_ms = iso["kernel_ms"]
     kname = mat.traverse_kernel()
     rstats = mat.rows_stats()
@@ -648,6 +723,16 @@ def main():
                    "nproc": nproc}
         del ref
 
+    # the drop-in path end to end (host ids -> host CSR), N = 1, rank 0
+    e2e = None
+    if rank == 0 and world == 1 and have_global and not a.no_e2e:
+        dev_hash = csr_hash(off_h, cols_h)
+        e2e = end_to_end(mat, np.ascontiguousarray(rows_global[:chk]), int(off_h[-1]), dev_t, dev_hash)
+        e2e["scope"] = (f"the bench's batch {last_k} ({chk:,} rows) through mbrwt_get_rows; csr_hash compared with the "
+                        f"device-resident CSR of the same batch (itself checked against the oracle: parity)")
+        log(f"end-to-end: pageable {e2e['pageable']['ms']:.2f} ms, pinned {e2e['pinned']['ms']:.2f} ms, "
+            f"PCIe bound {e2e['pcie_bound_ms']:.2f} ms")
+
     # roofline of the dominant kernel: its layout-true algorithmic bytes per
     # launch (the bytes the layout must move: DESIGN.md §6) / its HIP-event
     # time (achieved, frac); the measured HBM traffic beside it (traffic,
@@ -671,7 +756,13 @@ def main():
         alg_basis = (f"k_var_decode: per row 20 B (locate output, CSR offset) + {rec:.1f} B record + ~12 B "
                      f"16-byte-chunk rounding; 4 B per label written into the CSR")
     roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": kname, "kernel_ms": kern_ms,
+            "kernel_ms_basis": ("HIP events around the kernel on its own stream, one context, no other batch beside "
+                                "it (the isolated pass after the timed region)" if iso is not None else
+                                "HIP events around the kernel in the timed region"),
+            "kernel_ms_overlapped": kern_ms_overlapped,
             "step_minus_kernel_ms": elapsed / a.steps * 1e3 - kern_ms if world == 1 else None,
+            "step_implied_frac": (alg_bytes / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS
+                                  if alg_bytes and world == 1 else None),
             "achieved": alg_bytes / ks / 1e9 if alg_bytes else None,
             "frac": alg_bytes / ks / 1e9 / HBM_PEAK_GBS if alg_bytes else None,
             "alg_bytes_per_launch": alg_bytes, "alg_basis": alg_basis, "traffic": None,
@@ -683,13 +774,11 @@ def main():
             "stream_read_measured": stream_gbs}
     if iso is not None:
         iks = iso["kernel_ms"] / 1e3
-        iso.update({"achieved": alg_bytes / iks / 1e9 if alg_bytes else None,
-                    "frac": alg_bytes / iks / 1e9 / HBM_PEAK_GBS if alg_bytes else None,
-                    "step_minus_kernel_ms": iso["ms_per_step"] - iso["kernel_ms"],
-                    "note": "the same kernel with one context on one stream (no other batch beside it), "
-                            "20 untimed-for-value steps after the timed region; kernel_ms / achieved / frac "
-                            "above are over the timed region, where batch k+1's traversal runs beside batch "
-                            "k's compaction on a second query stream"})
+        iso.update({"step_minus_kernel_ms": iso["ms_per_step"] - iso["kernel_ms"],
+                    "note": "the kernel with one context on one stream (no other batch beside it), 20 "
+                            "untimed-for-value steps after the timed region: roofline.kernel_ms / achieved / frac "
+                            "are computed from this time; kernel_ms_overlapped is the HIP-event time in the timed "
+                            "region, where batch k+1's traversal runs beside batch k's compaction"})
         roof["isolated"] = iso
     seg = 64
     if rstats is not None and not rstats.get("variable"):
@@ -757,6 +846,7 @@ def main():
         },
         "roofline": roof,
         "phases": phases,
+        "end_to_end": e2e,
         "cpu_baseline": cpu,
         "reassembly": reassembly,
         "parity": parity,

@@ -101,6 +101,7 @@ static void release(Ctx *c) {
                          &c->ws_cls_off, &c->ws_cls_cols, &c->ws_sh_keys, &c->ws_sh_local, &c->ws_sh_cnt,
                          &c->ws_sh_sort, &c->ws_sh_tmp})
         if (w->buf) (void)hipFree(w->buf);
+    free_host_pipe(c->pipe);
     if (c->d_scalars) (void)hipFree(c->d_scalars);
     if (c->h_scalars) (void)hipHostFree(c->h_scalars);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -713,24 +714,8 @@ int mbrwt_get_rows(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n, uint64_t *o
     WsFence fence_(c.fence, c.stream);
     try {
         MBRWT_HIP(hipSetDevice(c.device));
-        int rc;
-        if ((rc = ensure(c.ws_rows, (n + 1) * sizeof(uint64_t) * 2))) return rc;
-        uint64_t *d_rows = reinterpret_cast<uint64_t *>(c.ws_rows.buf);
-        uint64_t *d_off = d_rows + n;
-        if (n) MBRWT_HIP(hipMemcpyAsync(d_rows, rows, n * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
-        uint64_t needed = 0;
-        // size the output buffer from a first pass over the batch, then fill
-        uint64_t cap = cols_cap;
-        if ((rc = ensure(c.ws_out, std::max<uint64_t>(cap, 1) * sizeof(uint32_t)))) return rc;
-        rc = run_get_rows(c, d_rows, n, d_off, reinterpret_cast<uint32_t *>(c.ws_out.buf), cols ? cap : 0, &needed,
-                          c.stream);
-        if (cols_needed) *cols_needed = needed;
-        if (rc) return rc;
-        MBRWT_HIP(hipMemcpyAsync(offsets, d_off, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-        if (needed)
-            MBRWT_HIP(hipMemcpyAsync(cols, c.ws_out.buf, needed * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
-        MBRWT_HIP(hipStreamSynchronize(c.stream));
-        return MBRWT_OK;
+        // chunks of the batch pipelined over PCIe (hostpipe.cpp)
+        return host_get_rows(c, rows, n, offsets, cols, cols ? cols_cap : 0, cols_needed);
     } catch (...) {
         set_error("unexpected exception in mbrwt_get_rows");
         return MBRWT_ERR_INVALID;

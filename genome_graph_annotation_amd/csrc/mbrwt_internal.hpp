@@ -330,6 +330,9 @@ inline void destroy_fence(WsFenceState &st) {
     st.live = false;
 }
 
+struct HostPipe;  // hostpipe.cpp: the chunked host-buffer get_rows
+void free_host_pipe(HostPipe *p);
+
 struct Ctx {
     int device = 0;
     Tree tree;
@@ -350,6 +353,7 @@ struct Ctx {
     Workspace ws_cls_off, ws_cls_cols;  // get_labels batch: the rows' CSR
     uint64_t *h_scalars = nullptr;      // pinned: [0] total, [1] overflow count, [2] error
     uint64_t *d_scalars = nullptr;      // device twin
+    HostPipe *pipe = nullptr;           // streams, slots and staging of mbrwt_get_rows (lazily created)
 
     // options
     bool timing = false;
@@ -426,6 +430,8 @@ struct VarScratch {
 };
 bool var_prepare(const Tree &tree, RowsImage &im);  // the unit tables; false when the tree is not uniform
 int var_measure_range(RowsImage &im, const Ctx &range, VarScratch &ws, uint64_t *rec_bytes, hipStream_t s);
+// the decode's LDS holds a mean tile of such rows beside the tree's unit table
+bool var_lds_fits(const RowsImage &im, double labels_per_row, double record_bytes_per_row);
 int var_build_range(RowsImage &im, const Ctx &range, uint64_t row0, VarScratch &ws, hipStream_t s);
 void var_free_scratch(VarScratch &ws);
 int var_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
@@ -532,6 +538,9 @@ inline bool packt_enabled() {
 int run_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap, uint64_t *rows_needed,
                    hipStream_t s);
 const char *traverse_kernel_name(const Ctx &c);  // the kernel mbrwt_get_rows* launches
+// mbrwt_get_rows: host row ids -> host CSR, chunked and pipelined (hostpipe.cpp)
+int host_get_rows(Ctx &c, const uint64_t *rows, uint64_t n, uint64_t *offsets, uint32_t *cols, uint64_t cols_cap,
+                  uint64_t *cols_needed);
 int run_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
                  uint64_t *needed, hipStream_t s);
 int run_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n, uint8_t *d_out, hipStream_t s);

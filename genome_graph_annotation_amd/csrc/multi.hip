@@ -184,6 +184,17 @@ int run_slices(mbrwt_multi &m, const uint64_t *rows, bool rows_on_host, uint64_t
     return MBRWT_OK;
 }
 
+// the caller thread's build options (include/mbrwt.h mbrwt_set_build_option:
+// thread-local), captured once and applied in every replica's worker thread
+struct BuildOptions {
+    int layout = build_layout(), footprint = rows_footprint(), partitioner = build_partitioner();
+    void apply() const {
+        set_build_layout(layout);
+        set_rows_footprint(footprint);
+        set_build_partitioner(partitioner);
+    }
+};
+
 }  // namespace
 
 extern "C" {
@@ -193,9 +204,9 @@ int mbrwt_multi_create(const mbrwt_tree_desc *desc, const int *devices, int n, m
         set_error("null tree description");
         return MBRWT_ERR_INVALID;
     }
-    const int layout = build_layout();  // the caller thread's layout, for every replica
+    const BuildOptions opt;  // the caller thread's options, for every replica
     return create_multi(devices, n, out, [&](int d, mbrwt_ctx **c) {
-        set_build_layout(layout);
+        opt.apply();
         return mbrwt_create(desc, d, c);
     });
 }
@@ -205,9 +216,9 @@ int mbrwt_multi_create_synthetic(const mbrwt_synth_desc *desc, const int *device
         set_error("null synthetic description");
         return MBRWT_ERR_INVALID;
     }
-    const int layout = build_layout();
+    const BuildOptions opt;
     return create_multi(devices, n, out, [&](int d, mbrwt_ctx **c) {
-        set_build_layout(layout);
+        opt.apply();
         return mbrwt_create_synthetic(desc, d, c);
     });
 }

@@ -337,6 +337,10 @@ __global__ __launch_bounds__(1024) void k_off_scan_sums(uint64_t *sums, uint64_t
         __syncthreads();
     }
 }
+// k_off_write's block-relative prefixes are u32: 2,048 counts of at most
+// 2^21 - 1 each cannot wrap (mbrwt_unpack_offsets_device rejects wider counts)
+constexpr uint32_t kOffMaxBits = 21;
+static_assert(((uint64_t)kOffRows << kOffMaxBits) <= (1ull << 32), "block prefix must fit u32");
 // counts loaded and offsets stored row-striped (row base + t + 256 j:
 // coalesced), scanned blocked (thread t: rows 8 t .. 8 t + 7) through LDS
 __global__ __launch_bounds__(256) void k_off_write(WireCounts w, const uint64_t *sums, uint64_t *offsets) {
@@ -616,6 +620,10 @@ int mbrwt_unpack_offsets_device(const void *d_base, uint32_t nseg, uint64_t seg_
     }
     if (nseg > kWireScanSegs) {
         set_error("more than 8 segments: unpack the counts (mbrwt_unpack_segments_device) and scan them");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
+    if (bits > kOffMaxBits) {  // k_off_write scans a block's 2,048 counts in u32
+        set_error("row counts wider than 21 bits: unpack the counts (mbrwt_unpack_segments_device) and scan them");
         return MBRWT_ERR_UNSUPPORTED;
     }
     WireCounts wc{reinterpret_cast<const uint8_t *>(d_base), seg_stride, nseg, bits, WireFirst{}};

@@ -40,6 +40,7 @@
 #include "mbrwt_internal.hpp"
 #include "pack_block.hpp"
 #include "rows_emit.hpp"
+#include "wave_scan.hpp"
 
 namespace mbrwt {
 
@@ -637,6 +638,13 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
             var_ok = rc == MBRWT_OK;
             var_mem = (double)vb * scale * 1.02 + (double)((rb.n + 12) / 13) * 64.0 + 64.0 * (1 + rb.n / rb.align);
             rb.var_bytes_per_row = (double)vb / (double)nr;
+            // a unit table so large that the decode's LDS cannot hold a mean
+            // tile beside it: AUTO keeps the other layouts (forced: allowed,
+            // every such tile then takes the decode's global path)
+            if (var_ok && force_var != 1 &&
+                !var_lds_fits(im, (double)range.tree.num_relations / std::max<double>(1.0, (double)range.tree.num_rows),
+                              rb.var_bytes_per_row))
+                var_ok = false;
         }
         if (var_ok && var_mem <= budget && (force_var == 1 || tmin > kAutoMaxCost)) {
             im.var = true;
@@ -912,6 +920,7 @@ struct RowsParams {
     uint32_t stk_words;           // per-lane LDS stack slots (general walks)
     uint32_t frames;              // the tree odometer: internal levels on the longest path (1..kRowsOdoLevels)
     uint32_t mask1;               // every mask one byte
+    unsigned long long *claims;   // kRowsClaimCounters tile counters, kRowsClaimStride apart (zeroed between calls)
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -1246,6 +1255,83 @@ constexpr uint32_t kAbStampWaves = 16384, kAbStampWords = 8;
 __device__ unsigned long long g_ab_stamps[kAbStampWaves * kAbStampWords];
 #endif
 
+// The tile order of k_traverse_rows (r05).  A static assignment (tile gw +
+// k NW for wave gw of NW) gives every wave the same number of tiles, but not
+// the same time: waves of one SIMD are issued by age, so the youngest waves
+// of the persistent grid are the slowest (per-wave phase stamps at C4: wave
+// lifetimes 334k..608k cycles around a mean of 468k, profiles/r05), and the
+// kernel lasts as long as its slowest wave.  So each wave takes its first
+// kRowsStaticNum/Den of a fair share statically and then claims chunks of
+// kRowsClaim tiles from kRowsClaimCounters counters, each over its own range
+// of the remaining tiles (a wave starts at counter blockIdx % 8 -- one XCD's
+// workgroups under round-robin placement, a speed hint only -- and moves to
+// the next counter when its range is exhausted).  The claim for the next
+// chunk is issued one chunk ahead, so its return is hidden behind a tile.
+// Every tile is taken exactly once: the static tiles are disjoint, and a
+// counter hands out each chunk of its range once.
+constexpr uint32_t kRowsClaimCounters = 8, kRowsClaimStride = 16;  // (u64 words: a 128-byte line each)
+constexpr uint32_t kRowsClaim = 2, kRowsStaticNum = 1, kRowsStaticDen = 2;
+struct TileSeq {
+    uint64_t ntiles, NW, S0, dyn0, ndyn;
+    uint64_t gw, k;
+    uint64_t cs, ce;       // the current claimed chunk [cs, ce)
+    uint32_t px, probes;   // the counter of the pending claim; counters found exhausted
+    uint32_t pend;         // the pending claim (lane 0's atomic return)
+    bool has_pend;
+    unsigned long long *claims;
+    __device__ __forceinline__ uint64_t lo(uint32_t x) const { return dyn0 + ndyn * x / kRowsClaimCounters; }
+    __device__ __forceinline__ void claim(uint32_t lane) {
+        uint32_t v = 0;
+        if (lane == 0) v = (uint32_t)atomicAdd(claims + (uint64_t)px * kRowsClaimStride, 1ull);
+        pend = v;
+        has_pend = true;
+    }
+    __device__ __forceinline__ void init(uint64_t n_tiles, uint64_t nw, uint64_t wave, uint32_t home,
+                                         unsigned long long *c) {
+        ntiles = n_tiles;
+        NW = nw;
+        gw = wave;
+        k = 0;
+#if defined(MBRWT_AB_CLAIMS)
+        S0 = ntiles / NW * kRowsStaticNum / kRowsStaticDen;  // (A/B: claimed tail)
+#else
+        S0 = (ntiles + NW - 1) / NW;  // the static order only
+#endif
+        dyn0 = S0 * NW < ntiles ? S0 * NW : ntiles;
+        ndyn = ntiles - dyn0;
+        cs = ce = 0;
+        px = home % kRowsClaimCounters;
+        probes = 0;
+        pend = 0;
+        has_pend = false;
+        claims = c;
+    }
+    // the wave's next tile (wave-uniform), ntiles when there is none
+    __device__ __forceinline__ uint64_t next(uint32_t lane) {
+        if (k < S0) {
+            const uint64_t t = gw + k * NW;
+            ++k;
+            if (t < ntiles) return t;
+        }
+        if (cs < ce) return cs++;
+        while (ndyn && probes < kRowsClaimCounters) {
+            if (!has_pend) claim(lane);
+            const uint64_t v = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
+            has_pend = false;
+            const uint64_t start = lo(px) + v * kRowsClaim, hi = lo(px + 1);
+            if (start < hi) {
+                cs = start;
+                ce = start + kRowsClaim < hi ? start + kRowsClaim : hi;
+                claim(lane);  // the next chunk, one chunk ahead
+                return cs++;
+            }
+            px = (px + 1) % kRowsClaimCounters;
+            ++probes;
+        }
+        return ntiles;
+    }
+};
+
 // k_traverse_rows: one wave per tile of 64 query rows (file comment).
 // B: block bytes; WPB: waves per workgroup (the RWT2 table is staged once per
 // workgroup; the grid is persistent); WALK: the walk family.
@@ -1254,6 +1340,18 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows[];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if defined(MBRWT_AB_PRIO)
+    // (A/B: the later-dispatched workgroups of the persistent grid lose issue
+    // arbitration by age; raise their priority)
+    if (blockIdx.x >= gridDim.x / 3 * 2) __builtin_amdgcn_s_setprio(2);
+    else if (blockIdx.x >= gridDim.x / 3) __builtin_amdgcn_s_setprio(1);
+#endif
+    const uint64_t ntiles = (p.n + 63) / 64;
+    TileSeq seq;
+    seq.init(ntiles, (uint64_t)gridDim.x * WPB, (uint64_t)blockIdx.x * WPB + wv, blockIdx.x, p.claims);
+    uint64_t t = seq.next(lane);
+    uint64_t row_n = 0;  // the row of this lane in the wave's next tile (its load overlaps the table's)
+    if (t < ntiles && t * 64 + lane < p.n) row_n = gld(p.rows + t * 64 + lane);
     for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_rows[i] = gld(p.table + i);
     if (blockIdx.x == 0 && threadIdx.x == 0) p.status[1] = MBRWT_OK;  // k_compact_tiles raises it
     __syncthreads();
@@ -1274,12 +1372,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
     AS_LDS uint8_t *mine = wb + lane * PB;
     AS_LDS uint32_t *stk = (AS_LDS uint32_t *)(wb + 64u * PB) + lane;
     constexpr uint32_t LPB = B / 16, RPI = 64 / LPB;
-    const uint64_t ntiles = (p.n + 63) / 64;
-    const uint64_t tstride = (uint64_t)gridDim.x * WPB;
     const uint32_t S = p.S;
-    uint64_t t = (uint64_t)blockIdx.x * WPB + wv;
-    uint64_t row_n = 0;  // the row of this lane in the wave's next tile
-    if (t < ntiles && t * 64 + lane < p.n) row_n = gld(p.rows + t * 64 + lane);
 #if defined(MBRWT_AB_STAMPS)
     uint64_t ab_ph[5] = {0, 0, 0, 0, 0}, ab_tiles = 0, ab_t0 = __builtin_amdgcn_s_memtime();
     uint64_t ab_last = ab_t0;
@@ -1294,12 +1387,15 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
     do {            \
     } while (0)
 #endif
-    for (; t < ntiles; t += tstride) {
+#if defined(MBRWT_AB_GATHER)
+    uint32_t ab_acc = 0;
+#endif
+    for (uint64_t tn; t < ntiles; t = tn) {
         AB_STAMP(4);
         const uint64_t r0 = t * 64;
         const uint32_t nr = (uint32_t)(p.n - r0 < 64 ? p.n - r0 : 64);
         const uint64_t row = row_n;
-        const uint64_t tn = t + tstride;
+        tn = seq.next(lane);
         if (tn < ntiles && tn * 64 + lane < p.n) row_n = gld(p.rows + tn * 64 + lane);
         const bool valid = lane < nr && row < p.num_rows;
         if (lane < nr && !valid) atomicOr(&p.scalars[2], 1ull);
@@ -1321,6 +1417,12 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
             const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(addr >> 32), src, 64);
             q[k] = gld_at_nt<u32x4_t, NT>((((uint64_t)hi << 32) | lo) + 16u * (lane % LPB));
         }
+#if defined(MBRWT_AB_GATHER)
+        // (timing only: the block loads into registers, no LDS, nothing else)
+#pragma unroll
+        for (uint32_t k = 0; k < LPB; ++k) ab_acc ^= q[k].x ^ q[k].y ^ q[k].z ^ q[k].w;
+        continue;
+#endif
 #pragma unroll
         for (uint32_t k = 0; k < LPB; ++k) {
             AS_LDS uint32_t *d = (AS_LDS uint32_t *)(wb + (RPI * k + lane / LPB) * PB + 16u * (lane % LPB));
@@ -1331,6 +1433,9 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
         }
         wave_sync();
         AB_STAMP(0);
+#if defined(MBRWT_AB_LOADONLY)
+        continue;  // (timing only: the block loads and their LDS staging, nothing else)
+#endif
         uint32_t cnt = 0, o = 0;
         bool spl = false;
         if (valid) {
@@ -1364,12 +1469,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
                 o = 8;
             }
         }
-        uint32_t x = cnt;
-#pragma unroll
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-            if (lane >= d) x += y;
-        }
+        const uint32_t x = wave_incl_sum(cnt);
         const uint32_t total = __builtin_amdgcn_readlane(x, 63);
         const uint32_t pos = x - cnt;
         // a tile whose labels exceed its region is walked by k_compact_tiles
@@ -1378,7 +1478,9 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
         const bool direct = total > C;
         const bool has_long = __any(lng);
         uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
+#if !defined(MBRWT_AB_NOSTORE)
         if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)(cnt | (lng ? 0x8000u : 0u)));
+#endif
         AB_STAMP(1);
         if (!direct) {
 #if defined(MBRWT_AB_NOWALK)
@@ -1433,9 +1535,13 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
                 wave_sync();
                 AB_STAMP(2);
                 const uint32_t nbytes = total * 2;
+#if !defined(MBRWT_AB_NOSTORE)
                 for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
                     gst(reinterpret_cast<u32x4_t *>(treg + 128 + q2),
                         *(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2));
+#else
+                (void)nbytes;  // (timing only: no temp-region stores)
+#endif
             } else if constexpr (WALK == WALK_MASK1) {
                 rows_walk6(mine, o, live, root, ent, lst, stk,
                            (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128), pos);
@@ -1450,6 +1556,9 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
         ++ab_tiles;
 #endif
     }
+#if defined(MBRWT_AB_GATHER)
+    if (ab_acc == 0x9E3779B9u) p.scalars[3] = ab_acc;  // (keeps the loads alive)
+#endif
 #if defined(MBRWT_AB_STAMPS)
     AB_STAMP(4);
     const uint32_t gw = blockIdx.x * WPB + wv;
@@ -1484,6 +1593,7 @@ struct CompactParams {
     uint64_t n, cap;
     unsigned long long *scalars;  // the traversal's counters ([2] error flags)
     unsigned long long *status;   // {total, status, sticky}
+    unsigned long long *claims;   // the traversal's tile counters (cleared here)
     const uint64_t *rows;         // the batch (direct tiles)
     RowsView v;
     const uint32_t *table;        // RWT (direct tiles)
@@ -1499,6 +1609,8 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
     const uint64_t ntiles = (n + 63) / 64;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t total = gld(p.tile_offsets + ntiles - 1) + (gld(p.tile_counts + ntiles - 1) & 0x3FFFFFFFu);
+    if (blockIdx.x == 0 && threadIdx.x < kRowsClaimCounters)  // the traversal's tile counters, for the next call
+        p.claims[threadIdx.x * kRowsClaimStride] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const uint64_t err = p.scalars[2];
         p.scalars[2] = 0;
@@ -1532,12 +1644,7 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
         const uint64_t r0 = t * 64;
         const uint32_t nr = (uint32_t)(n - r0 < 64 ? n - r0 : 64);
         const uint32_t c = cnt[k] & 0x7FFFu;
-        uint32_t x = c;
-#pragma unroll
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-            if (lane >= d) x += y;
-        }
+        const uint32_t x = wave_incl_sum(c);
         const uint64_t rbase = base[k] + (x - c);
         if (lane < nr) gst(p.offsets + r0 + lane, rbase);
         if (t == ntiles - 1 && lane == nr - 1) gst(p.offsets + n, base[k] + x);
@@ -1720,7 +1827,11 @@ RowsFn rows_fn_b(uint32_t walk, uint32_t wpb) {
                                  : k_traverse_rows<B, kRowsWpb, NT, WALK_GENERAL>;
 }
 RowsFn rows_fn(const RowsImage &im, uint32_t walk, uint32_t wpb) {
+#if defined(MBRWT_AB_NT0)
+    const bool nt = false;  // (A/B: plain block reads)
+#else
     const bool nt = im.bytes > (1ull << 30);  // non-temporal block reads for images beyond the caches
+#endif
     if (im.B == 64) return nt ? rows_fn_b<64, true>(walk, wpb) : rows_fn_b<64, false>(walk, wpb);
     return nt ? rows_fn_b<128, true>(walk, wpb) : rows_fn_b<128, false>(walk, wpb);
 }
@@ -1788,13 +1899,18 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     // counts workspace: nt+1 tile counts | (8-byte aligned) nt+1 tile offsets
     const uint64_t to_off = ((nt + 1) * sizeof(uint32_t) + 7) / 8 * 8;
     if ((rc = ensure(c.ws_temp, nt * region))) return rc;
-    // [tile counts | tile offsets | the kernel's own counters (4 x u64)]
+    // [tile counts | tile offsets | the kernel's own counters (4 x u64) |
+    // (128-byte aligned) the tile claim counters, a line each]
     const uint64_t sc_off = to_off + (nt + 1) * sizeof(uint64_t);
-    const bool fresh = c.ws_counts.bytes < sc_off + 32;
-    if ((rc = ensure(c.ws_counts, sc_off + 32))) return rc;
+    const uint64_t cl_off = (sc_off + 32 + 127) / 128 * 128;
+    const uint64_t sc_bytes = cl_off + kRowsClaimCounters * kRowsClaimStride * 8 - sc_off;
+    const bool fresh = c.ws_counts.bytes < sc_off + sc_bytes;
+    if ((rc = ensure(c.ws_counts, sc_off + sc_bytes))) return rc;
     unsigned long long *d_sc = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + sc_off);
+    unsigned long long *d_claims =
+        reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + cl_off);
     if (fresh || c.rows_sc_dirty || c.rows_sc_at != sc_off) {  // the counters are cleared by k_compact_tiles
-        MBRWT_HIP(hipMemsetAsync(d_sc, 0, 32, s));
+        MBRWT_HIP(hipMemsetAsync(d_sc, 0, sc_bytes, s));
         c.rows_sc_dirty = false;
         c.rows_sc_at = sc_off;
     }
@@ -1829,6 +1945,7 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     p.stk_words = walk >= WALK_ODOMETER ? 0u : rows_stack_words(im);  // (the odometers keep no stack)
     p.frames = im.frames;
     p.mask1 = im.mask1 ? 1u : 0u;
+    p.claims = d_claims;
 
     const size_t table_bytes = ((im.table2.size() + 3) & ~size_t(3)) * 4;
     const size_t per_wave = 64ull * (im.B + 4) + 256ull * p.stk_words + (walk >= WALK_ODOMETER ? 2ull * C : 0ull);
@@ -1879,7 +1996,12 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     }
     if (c.timing) MBRWT_HIP(hipEventRecord(e0, s));
     {
+#if defined(MBRWT_AB_TPW)
+        // (A/B: a grid of ceil(tiles / (wpb x TPW)) workgroups, TPW tiles per wave)
+        const uint64_t g = std::max<uint64_t>(1, (nt + (uint64_t)wpb * MBRWT_AB_TPW - 1) / ((uint64_t)wpb * MBRWT_AB_TPW));
+#else
         const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((nt + wpb - 1) / wpb, (uint64_t)c.rb_blocks));
+#endif
         hipLaunchKernelGGL(kfn, dim3((unsigned)g), dim3(threads), lds, s, p);
         MBRWT_HIP(hipGetLastError());
     }
@@ -1897,6 +2019,7 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         cp.cap = cap;
         cp.scalars = d_sc;
         cp.status = st_blk;
+        cp.claims = d_claims;
         cp.rows = d_rows;
         cp.v = view_of(c);
         cp.table = im.d_table;

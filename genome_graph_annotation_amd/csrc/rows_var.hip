@@ -706,18 +706,53 @@ uint64_t simple_grid(uint64_t n) { return std::max<uint64_t>(1, std::min<uint64_
 }  // namespace
 
 // lanes per row and the per-wave LDS budget from the image's statistics
-static void var_geometry(const Ctx &c, uint32_t &G, uint32_t &CR, uint32_t &CS) {
-    const RowsImage &im = c.rows;
-    const double rows = std::max<double>(1.0, (double)c.tree.num_rows);
-    const double lab = (double)c.tree.num_relations / rows, rec = (double)im.var_rec_bytes / rows;
-    G = im.var_G ? im.var_G : lab >= 48.0 ? 4u : lab >= 12.0 ? 2u : 1u;
-    const double R = 64.0 / G;
+// (labels and record bytes per row), within the workgroup's LDS: the unit
+// table (u16 per unit) is staged once per workgroup, so a tree with many
+// units leaves less for the kWpb waves' record / owner / stage areas, which
+// are then scaled down (tiles beyond them take the global path; at worst
+// CR = CS = 0 and every non-empty tile does).  lds_ok: a mean tile still fits
+// (the build declines the variable-length records otherwise).
+constexpr size_t kVarLdsMax = 160u << 10;  // gfx950: LDS per CU, all of it one workgroup's at most
+struct VarGeom {
+    uint32_t G, CR, CS;
+    bool lds_ok;
+};
+static VarGeom var_geometry_of(uint32_t var_G, uint32_t U, double lab, double rec) {
+    VarGeom g{};
+    g.G = var_G ? var_G : lab >= 48.0 ? 4u : lab >= 12.0 ? 2u : 1u;
+    const double R = 64.0 / g.G;
     // a tile's records (whole 16-byte chunks: + 16 per row) and labels with
     // ~6 standard deviations of room; larger tiles take the global path
     const double cr = R * (rec + 16.0) + 6.0 * std::sqrt(R) * (rec * 0.25 + 16.0) + 256.0;
     const double cs = R * lab + 6.0 * std::sqrt(R * lab + 1.0) * 2.0 + 64.0;
-    CR = (uint32_t)std::min(32768.0, std::ceil(cr / 256.0) * 256.0);
-    CS = (uint32_t)std::min(16384.0, std::ceil(cs / 64.0) * 64.0);
+    g.CR = (uint32_t)std::min(32768.0, std::ceil(cr / 256.0) * 256.0);
+    g.CS = (uint32_t)std::min(16384.0, std::ceil(cs / 64.0) * 64.0);
+    const size_t ub = ((size_t)(U + 32) * 2 + 15) / 16 * 16;
+    const size_t avail = ub < kVarLdsMax ? (kVarLdsMax - ub) / kVarWpb : 0;
+    auto need = [&]() { return (size_t)g.CR + g.CR / 16 + 2ull * g.CS; };
+    if (need() > avail) {
+        const double f = (double)avail / (double)need();
+        g.CR = (uint32_t)(std::floor(g.CR * f / 256.0) * 256.0);
+        g.CS = (uint32_t)(std::floor(g.CS * f / 64.0) * 64.0);
+        while (need() > avail && (g.CR || g.CS)) {
+            if (g.CR) g.CR -= 256;
+            if (need() > avail && g.CS) g.CS -= 64;
+        }
+    }
+    g.lds_ok = g.CR >= R * (rec + 16.0) && g.CS >= R * lab;
+    return g;
+}
+static void var_geometry(const Ctx &c, uint32_t &G, uint32_t &CR, uint32_t &CS) {
+    const RowsImage &im = c.rows;
+    const double rows = std::max<double>(1.0, (double)c.tree.num_rows);
+    const VarGeom g = var_geometry_of(im.var_G, (uint32_t)im.var_units.size(), (double)c.tree.num_relations / rows,
+                                      (double)im.var_rec_bytes / rows);
+    G = g.G;
+    CR = g.CR;
+    CS = g.CS;
+}
+bool var_lds_fits(const RowsImage &im, double labels_per_row, double record_bytes_per_row) {
+    return var_geometry_of(im.var_G, (uint32_t)im.var_units.size(), labels_per_row, record_bytes_per_row).lds_ok;
 }
 
 int var_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,

@@ -281,7 +281,8 @@ class DeviceAllGatherV:
         # once (every unpack runs on the one side stream, so one scratch)
         import ctypes as C
         self._counts = (C.c_uint64 * self.world)(*self.ns)
-        self.fused_offsets = self.world <= 8  # (beyond one node: counts unpacked, then scanned)
+        # (beyond one node, or counts wider than 21 bits: counts unpacked, then scanned)
+        self.fused_offsets = self.world <= 8 and self.bits_c <= 21
         tb = C.c_uint64(0)
         if self.fused_offsets:
             L.check(L.lib().mbrwt_unpack_offsets_device(C.c_void_p(16), self.world, self.per, self._counts,

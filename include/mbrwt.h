@@ -302,8 +302,13 @@ uint64_t mbrwt_num_shards(const mbrwt_ctx *ctx);
  * Batched BRWT::get_row over rows[0..n): CSR result with offsets[0..n]
  * (n+1 entries, offsets[0] = 0) and cols[offsets[i]..offsets[i+1]) = row i's
  * column ids in the reference's order.  If the total exceeds cols_cap,
- * returns MBRWT_ERR_CAPACITY with *cols_needed set and cols untouched (retry
- * protocol).  cols_needed may be NULL.  Host buffers.
+ * returns MBRWT_ERR_CAPACITY with *cols_needed set to the total (retry
+ * protocol); offsets and cols are then unspecified (a prefix of the CSR
+ * may have been written).  cols_needed may be NULL.  Host buffers: the
+ * batch is cut into chunks of 2^20 rows whose upload, query and download
+ * overlap (r05, hostpipe.cpp); page-locked buffers (hipHostMalloc,
+ * hipHostRegister) are read and written by DMA directly, pageable ones are
+ * staged through the context's pinned buffers by a pool of host threads.
  */
 int mbrwt_get_rows(mbrwt_ctx *ctx, const uint64_t *rows, uint64_t n, uint64_t *offsets, uint32_t *cols,
                    uint64_t cols_cap, uint64_t *cols_needed);
@@ -464,7 +469,8 @@ int mbrwt_unpack_labels_device(const void *d_base, uint32_t nseg, uint64_t seg_s
    block's counts re-read and scanned in LDS (no int32 count array in
    between).  d_temp == NULL: *temp_bytes receives the
    scratch size the call needs and nothing runs.  At most 8 segments (one
-   node); MBRWT_ERR_UNSUPPORTED beyond (unpack the counts and scan them). */
+   node) and counts of at most 21 bits (tables below 2^21 columns);
+   MBRWT_ERR_UNSUPPORTED beyond (unpack the counts and scan them). */
 int mbrwt_unpack_offsets_device(const void *d_base, uint32_t nseg, uint64_t seg_stride, const uint64_t *counts,
                                 uint32_t bits, uint64_t *d_offsets, void *d_temp, uint64_t *temp_bytes,
                                 void *stream);

@@ -55,8 +55,7 @@ def _rank(rank, world, port, q):
         cap = int(nb * 8 * 1.3) + 1024 + 24 * rank
         rows_per_rank = [shard_bounds(G, world, r)[1] - shard_bounds(G, world, r)[0] for r in range(world)]
         wire = DeviceAllGatherV(rows_per_rank, cap, m, dev_t, slots=3)
-        assert wire.cap == int(max(shard_bounds(G, world, r)[1] - shard_bounds(G, world, r)[0]
-                                   for r in range(world)) * 8 * 1.3) + 1024 + 24 * (world - 1) or world == 1
+        assert wire.cap == max(int(rows_per_rank[r] * 8 * 1.3) + 1024 + 24 * r for r in range(world))
         bufs = [(torch.empty(nb + 1, dtype=torch.int64, device=dev_t), torch.empty(cap, dtype=torch.int32, device=dev_t))
                 for _ in range(2)]
         status = torch.zeros(3, dtype=torch.int64, device=dev_t)

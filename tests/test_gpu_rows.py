@@ -494,6 +494,32 @@ def test_variable_records(oracle_mod, monkeypatch, n, m, d, arity, G):
     _same_tree(ex, dev.export())
 
 
+@pytest.mark.parametrize("force", ["1", ""])
+def test_variable_records_wide_units(oracle_mod, monkeypatch, force):
+    """Rows of ~1,230 labels (4,096 columns, arity 4, 1,024 units, d = 0.3):
+    the decode's full-size per-wave budget (record chunks, owners, label stage)
+    for 4 waves plus the unit table would need ~245 KB of LDS (ADVICE r04;
+    the RWT table's 8,192 words bound the unit table itself to a few KB).  The budget is scaled to the workgroup's LDS;
+    forced, the variable-length records answer through the global path;
+    under AUTO the build declines them (a mean tile no longer fits) and the
+    rows stay queryable on the other layouts."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    if force:
+        monkeypatch.setenv("MBRWT_ROWS_VAR", force)
+    n, m, d = 1500, 4096, 0.3
+    rng = np.random.default_rng(77)
+    dense = rng.random((n, m)) < d
+    t = O.OracleTree.from_dense(dense, "basic", 4)
+    dev = BRWTDevice.from_tree(t.export(), layout=None)
+    assert bool(force) == bool((dev.rows_stats() or {}).get("variable")), dev.rows_stats()
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 500)]).astype(np.uint64)
+    off_o, cols_o = t.get_rows(rows)
+    off_d, cols_d = dev.get_rows(rows)
+    np.testing.assert_array_equal(off_d, off_o)
+    np.testing.assert_array_equal(cols_d, cols_o)
+
+
 def test_variable_records_ranged_async_and_errors(oracle_mod, monkeypatch):
     """Several ranges (one record allocation each), the asynchronous call with
     its status block, capacity and range errors on the variable layout."""

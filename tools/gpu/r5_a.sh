@@ -15,3 +15,4 @@ i=0
 for P in "$A" "$B" "$C"; do i=$((i+1))
 timeout -s KILL 240 rocprofv3 --pmc $P --kernel-include-regex k_traverse_rows -d $O/sq$i -o run --output-format csv -- python tools/trav_ab.py --steps 3 --warmup 2 --tag sq$i > $O/sq$i.log 2>&1 || exit 1
 done
+timeout -k 10 120 python -u tools/pcie_probe.py > $O/pcie_probe.log 2>&1 || exit 1

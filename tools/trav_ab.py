@@ -36,7 +36,8 @@ ap.add_argument("--warmup", type=int, default=5)
 ap.add_argument("--seed", type=int, default=42)
 ap.add_argument("--shape", default="", help="npz (num_children/first_child/leaf_column): synthetic_shaped")
 ap.add_argument("--tag", default="")
-ap.add_argument("--check", action="store_true", help="compare the CSR with the release library's (same process)")
+ap.add_argument("--stamps-out", default="", help="save the per-wave stamp words (npy) here")
+ap.add_argument("--probe", action="store_true", help="also measure the random-request ceiling (tools/probe.hip)")
 a = ap.parse_args()
 
 dev = torch.device("cuda:0")
@@ -78,6 +79,8 @@ if hasattr(lib, "mbrwt_ab_stamps"):
     torch.cuda.synchronize()
     lib.mbrwt_ab_stamps(buf.ctypes.data, words)
     w = buf.reshape(-1, 8)
+    if a.stamps_out:
+        np.save(a.stamps_out, w)
     w = w[w[:, 7] == 1]
     names = ["load", "parse_scan", "walk", "output", "loop"]
     tot = w[:, 6].astype(np.float64)
@@ -88,4 +91,12 @@ if hasattr(lib, "mbrwt_ab_stamps"):
                      "share": {n: v / max(1.0, all_c) for n, v in ph.items()},
                      "wave_cycles_mean": float(tot.mean()), "wave_cycles_max": float(tot.max()),
                      "wave_cycles_min": float(tot.min())}
+if a.probe:
+    # the request ceiling on this box beside the structure: random 64-byte
+    # segments over a buffer of the image's size (tools/probe.hip)
+    sys.path.insert(0, ROOT)
+    import bench
+    free, _ = torch.cuda.mem_get_info(dev)
+    sg, rnd = bench.probe_ceilings(dev, s, free, mat.device_bytes())
+    out["probe"] = {"stream_read_GBs": sg, "random": rnd}
 print(json.dumps(out), flush=True)
