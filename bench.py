@@ -449,9 +449,6 @@ def main():
     # while batch k+1 is traversed, so the outputs are double-buffered; drain()
     # completes the last exchange inside the timed region
     gather = world > 1 and not a.no_gather
-    bufs = [(off_t, cols_t)]
-    if gather:
-        bufs.append((torch.empty_like(off_t), torch.empty_like(cols_t)))
     state = {"i": 0, "pending": None, "inflight": [], "global": None, "timed": False, "exchanges": [],
              "get_rows_host": []}
 
@@ -460,16 +457,22 @@ def main():
     # sticky status bits -- is read once after the timed region)
     use_async = (world == 1 or wire is not None) and not a.sync
     status_t = torch.zeros(3, dtype=torch.int64, device=dev_t)
-    # N = 1 with two query streams: batch i runs on query context i mod 2 (the
-    # context, or a clone over the same image) on its own stream, into its
-    # own output buffers and status block
-    Q = a.query_streams if (world == 1 and use_async) else 1
-    qmats, qstreams, qstatus = [mat], [sptr], [status_t]
+    # two query streams (N = 1 and, since r05, N > 1): batch i runs on query
+    # context i mod 2 (the context, or a clone over the same image) on its own
+    # stream, into its own output buffers and status block, so batch i+1's
+    # traversal runs beside batch i's compaction (and, at N > 1, beside its
+    # pack; the all-gather and the unpack run on RCCL's and a side stream)
+    Q = a.query_streams if use_async else 1
+    qmats, qstreams, qstatus = [mat], [stream], [status_t]
     if Q == 2:
         qmats.append(mat.clone())
-        side = torch.cuda.Stream(dev_t)
-        qstreams.append(side.cuda_stream)
+        qstreams.append(torch.cuda.Stream(dev_t))
         qstatus.append(torch.zeros(3, dtype=torch.int64, device=dev_t))
+    # outputs: step i writes bufs[i mod len]; with two buffers a buffer's next
+    # writer is two steps later on the SAME stream, behind this step's readers
+    # (its compaction, its pack) -- double-buffered whenever steps overlap
+    bufs = [(off_t, cols_t)]
+    if gather or Q == 2:
         bufs.append((torch.empty_like(off_t), torch.empty_like(cols_t)))
 
     def step():
@@ -479,17 +482,18 @@ def main():
         h0 = time.perf_counter()
         if use_async:
             q = i % Q
-            qmats[q].get_rows_device_async(rows_ts[i % K], o, cb, qstatus[q], qstreams[q])
-            if state["timed"]:
-                state["get_rows_host"].append((time.perf_counter() - h0) * 1e3)
-            if wire is not None:
-                # no host synchronisation: the label count travels from the
-                # status block on the device into the wire header
-                # finish the oldest exchange only when its slot comes round
-                # again (it then gates this step's pack on its unpack)
-                if len(state["inflight"]) == len(wire.slots) - 1:
-                    state["global"] = wire.finish(state["inflight"].pop(0))
-                state["inflight"].append(wire.start(o, cb, status_t))
+            with torch.cuda.stream(qstreams[q]):
+                qmats[q].get_rows_device_async(rows_ts[i % K], o, cb, qstatus[q], qstreams[q].cuda_stream)
+                if state["timed"]:
+                    state["get_rows_host"].append((time.perf_counter() - h0) * 1e3)
+                if wire is not None:
+                    # no host synchronisation: the label count travels from the
+                    # status block on the device into the wire header; the
+                    # pack runs on this query's stream.  The oldest exchange is
+                    # finished only when its slot comes round again
+                    if len(state["inflight"]) == len(wire.slots) - 1:
+                        state["global"] = wire.finish(state["inflight"].pop(0))
+                    state["inflight"].append(wire.start(o, cb, qstatus[q]))
             return None
         n_lab = mat.get_rows_device(rows_ts[i % K], o, cb, sptr)
         if state["timed"]:

@@ -29,6 +29,18 @@ MBRWT_OPT_ROWS_WALK = 8
 MBRWT_BUILD_LAYOUT = 1
 MBRWT_BUILD_PARTITIONER = 2
 MBRWT_BUILD_ROWS_FOOTPRINT = 3
+MBRWT_BUILD_ROWS_VAR = 4
+MBRWT_BUILD_VAR_LANES = 5
+MBRWT_BUILD_ROWS_BLOCK = 6
+MBRWT_BUILD_ROWS_RANGE = 7
+MBRWT_BUILD_NODE_KINDS = 8
+MBRWT_BUILD_SHARD_ROWS = 9
+MBRWT_BUILD_ROWS_WGS_PER_CU = 10
+MBRWT_KIND_FOLD_ROOT = 1
+MBRWT_KIND_PACK = 2
+MBRWT_KIND_PACK2 = 4
+MBRWT_KIND_PACKT = 8
+MBRWT_KIND_ALL = 15
 MBRWT_ROWS_FAST = 0
 MBRWT_ROWS_COMPACT = 1
 MBRWT_PARTITIONER_BASIC = 0

@@ -242,13 +242,11 @@ static int create_sharded(int device, uint64_t num_rows, uint64_t num_columns, u
 // the node images (and the shards).  AUTO keeps the node images instead when
 // the tree is outside the row-record limits or the records do not fit.
 constexpr uint64_t kRowsAlign = 360360;  // a multiple of every S <= 15
-// rows per range of a ranged build: 1,073,512,440 (MBRWT_ROWS_RANGE=<rows>,
-// rounded up to a multiple of kRowsAlign, forces smaller ranges: a test hook)
+// rows per range of a ranged build: 1,073,512,440 (the build option
+// MBRWT_BUILD_ROWS_RANGE, rounded up to a multiple of kRowsAlign, forces
+// smaller ranges: a test hook)
 static uint64_t rows_range_rows() {
-    if (const char *e = std::getenv("MBRWT_ROWS_RANGE")) {
-        const unsigned long long v = std::strtoull(e, nullptr, 10);
-        if (v) return (v + kRowsAlign - 1) / kRowsAlign * kRowsAlign;
-    }
+    if (const uint64_t v = build_tuning().rows_range) return (v + kRowsAlign - 1) / kRowsAlign * kRowsAlign;
     return 2979ull * kRowsAlign;
 }
 
@@ -311,7 +309,7 @@ static int create_rows_ranged(int device, uint64_t num_rows, uint64_t num_column
         [&](Ctx &c) {
             c.tree.num_rows = num_rows;
             c.tree.num_columns = num_columns;
-            const bool fixed = std::getenv("MBRWT_ROWS_RANGE") != nullptr;
+            const bool fixed = build_tuning().rows_range != 0;
             uint64_t R = fixed ? rows_range_rows() : std::min(rows_range_rows(), kRowsFirstRange);
             RowsBuild *rb = rows_build_begin(c, num_rows, kRowsAlign, layout == LAYOUT_AUTO);
             if (!rb) return (int)MBRWT_ERR_NOMEM;
@@ -604,6 +602,45 @@ uint64_t mbrwt_num_nodes(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.num_n
 uint64_t mbrwt_device_bytes(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->tree.image_bytes + C(ctx)->rows.bytes : 0; }
 
 int mbrwt_set_build_option(int option, int64_t value) {
+    BuildTuning &t = build_tuning();
+    switch (option) {
+    case MBRWT_BUILD_ROWS_VAR:
+        if (value < -1 || value > 1) break;
+        t.rows_var = (int)value;
+        return MBRWT_OK;
+    case MBRWT_BUILD_VAR_LANES:
+        if (value < 0 || value > 16 || (value & (value - 1))) break;
+        t.var_lanes = (uint32_t)value;
+        return MBRWT_OK;
+    case MBRWT_BUILD_ROWS_BLOCK: {
+        const int64_t Bv = value >> 8, Sv = value & 0xFF;
+        if (value != 0 && !((Bv == 64 && Sv >= 1 && Sv <= 8) || (Bv == 128 && Sv >= 1 && Sv <= 15))) break;
+        t.rows_block = (uint32_t)value;
+        return MBRWT_OK;
+    }
+    case MBRWT_BUILD_ROWS_RANGE:
+        if (value < 0) break;
+        t.rows_range = (uint64_t)value;
+        return MBRWT_OK;
+    case MBRWT_BUILD_NODE_KINDS:
+        if (value < 0 || value > MBRWT_KIND_ALL) break;
+        t.node_kinds = (uint32_t)value;
+        return MBRWT_OK;
+    case MBRWT_BUILD_SHARD_ROWS:
+        if (value < 0) break;
+        t.shard_rows = (uint64_t)value;
+        return MBRWT_OK;
+    case MBRWT_BUILD_ROWS_WGS_PER_CU:
+        if (value < 0 || value > 32) break;
+        t.rows_wgs_per_cu = (uint32_t)value;
+        return MBRWT_OK;
+    default:
+        break;
+    }
+    if (option >= MBRWT_BUILD_ROWS_VAR && option <= MBRWT_BUILD_ROWS_WGS_PER_CU) {
+        set_error("build option value out of range");
+        return MBRWT_ERR_INVALID;
+    }
     if (option == MBRWT_BUILD_PARTITIONER &&
         (value == MBRWT_PARTITIONER_BASIC || value == MBRWT_PARTITIONER_GREEDY)) {
         set_build_partitioner((int)value);
@@ -622,14 +659,23 @@ int mbrwt_set_build_option(int option, int64_t value) {
 }
 
 int mbrwt_get_build_option(int option, int64_t *value) {
-    if (!value || (option != MBRWT_BUILD_LAYOUT && option != MBRWT_BUILD_PARTITIONER &&
-                   option != MBRWT_BUILD_ROWS_FOOTPRINT)) {
+    if (!value || option < MBRWT_BUILD_LAYOUT || option > MBRWT_BUILD_ROWS_WGS_PER_CU) {
         set_error("unknown build option or null output");
         return MBRWT_ERR_INVALID;
     }
-    *value = option == MBRWT_BUILD_LAYOUT        ? thread_build_layout()
-             : option == MBRWT_BUILD_PARTITIONER ? build_partitioner()
-                                                 : rows_footprint();
+    const BuildTuning &t = build_tuning();
+    switch (option) {
+    case MBRWT_BUILD_LAYOUT: *value = thread_build_layout(); break;
+    case MBRWT_BUILD_PARTITIONER: *value = build_partitioner(); break;
+    case MBRWT_BUILD_ROWS_FOOTPRINT: *value = rows_footprint(); break;
+    case MBRWT_BUILD_ROWS_VAR: *value = t.rows_var; break;
+    case MBRWT_BUILD_VAR_LANES: *value = t.var_lanes; break;
+    case MBRWT_BUILD_ROWS_BLOCK: *value = t.rows_block; break;
+    case MBRWT_BUILD_ROWS_RANGE: *value = (int64_t)t.rows_range; break;
+    case MBRWT_BUILD_NODE_KINDS: *value = t.node_kinds; break;
+    case MBRWT_BUILD_SHARD_ROWS: *value = (int64_t)t.shard_rows; break;
+    default: *value = t.rows_wgs_per_cu; break;
+    }
     return MBRWT_OK;
 }
 

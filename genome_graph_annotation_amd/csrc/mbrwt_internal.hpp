@@ -511,27 +511,24 @@ void build_p2w_table(Tree &tree);
 // the PTW table of k_traverse_ptw (empty when the tree has another shape)
 void build_ptw_table(Tree &tree);
 
-// root folding is on unless MBRWT_FOLD_ROOT=0 (A/B measurement switch)
-inline bool fold_root_enabled() {
-    const char *e = std::getenv("MBRWT_FOLD_ROOT");
-    return !(e && e[0] == '0');
-}
-// KIND_PACK nodes are built unless MBRWT_PACK=0 (A/B measurement switch)
-inline bool pack_enabled() {
-    const char *e = std::getenv("MBRWT_PACK");
-    return !(e && e[0] == '0');
-}
-// KIND_PACK2 nodes are built unless MBRWT_PACK2=0 or MBRWT_PACK=0
-inline bool pack2_enabled() {
-    const char *e = std::getenv("MBRWT_PACK2");
-    return pack_enabled() && !(e && e[0] == '0');
-}
+// the calling thread's tuning / test build options (include/mbrwt.h
+// MBRWT_BUILD_ROWS_VAR .. MBRWT_BUILD_ROWS_WGS_PER_CU; every default automatic)
+struct BuildTuning {
+    int rows_var = -1;           // -1 auto, 0 never, 1 always
+    uint32_t var_lanes = 0;      // 0 auto
+    uint32_t rows_block = 0;     // 0 auto, else B << 8 | S
+    uint64_t rows_range = 0;     // 0 auto
+    uint32_t node_kinds = 15;    // MBRWT_KIND_* bits
+    uint64_t shard_rows = 0;     // 0: the default shard size
+    uint32_t rows_wgs_per_cu = 0;
+};
+BuildTuning &build_tuning();
+void set_build_tuning(const BuildTuning &t);
 
-// KIND_PACKT nodes are built unless MBRWT_PACKT=0 or MBRWT_PACK=0
-inline bool packt_enabled() {
-    const char *e = std::getenv("MBRWT_PACKT");
-    return pack_enabled() && !(e && e[0] == '0');
-}
+inline bool fold_root_enabled() { return (build_tuning().node_kinds & 1u) != 0; }
+inline bool pack_enabled() { return (build_tuning().node_kinds & 2u) != 0; }
+inline bool pack2_enabled() { return pack_enabled() && (build_tuning().node_kinds & 4u) != 0; }
+inline bool packt_enabled() { return pack_enabled() && (build_tuning().node_kinds & 8u) != 0; }
 
 // queries (query.hip)
 // column query (column.hip): ascending rows of `column` into d_rows (u64)

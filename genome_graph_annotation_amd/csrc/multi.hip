@@ -188,10 +188,12 @@ int run_slices(mbrwt_multi &m, const uint64_t *rows, bool rows_on_host, uint64_t
 // thread-local), captured once and applied in every replica's worker thread
 struct BuildOptions {
     int layout = build_layout(), footprint = rows_footprint(), partitioner = build_partitioner();
+    BuildTuning tuning = build_tuning();
     void apply() const {
         set_build_layout(layout);
         set_rows_footprint(footprint);
         set_build_partitioner(partitioner);
+        set_build_tuning(tuning);
     }
 };
 

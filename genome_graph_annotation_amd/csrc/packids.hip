@@ -337,16 +337,14 @@ __global__ __launch_bounds__(1024) void k_off_scan_sums(uint64_t *sums, uint64_t
         __syncthreads();
     }
 }
-// k_off_write's block-relative prefixes are u32: 2,048 counts of at most
-// 2^21 - 1 each cannot wrap (mbrwt_unpack_offsets_device rejects wider counts)
-constexpr uint32_t kOffMaxBits = 21;
-static_assert(((uint64_t)kOffRows << kOffMaxBits) <= (1ull << 32), "block prefix must fit u32");
 // counts loaded and offsets stored row-striped (row base + t + 256 j:
 // coalesced), scanned blocked (thread t: rows 8 t .. 8 t + 7) through LDS
 __global__ __launch_bounds__(256) void k_off_write(WireCounts w, const uint64_t *sums, uint64_t *offsets) {
     __shared__ uint64_t first[kWireScanSegs + 1];
     __shared__ uint64_t wsum[4];
-    __shared__ uint32_t lc[kOffRows];  // counts, then block-relative inclusive prefixes (< 2^32: 2,048 rows)
+    // counts, then block-relative inclusive prefixes: u64, as k_off_sums' block
+    // sums -- 2,048 counts of up to 32 bits can pass 2^32
+    __shared__ uint64_t lc[kOffRows];
     if (threadIdx.x <= kWireScanSegs) first[threadIdx.x] = w.f.v[threadIdx.x];
     __syncthreads();
     const uint64_t N = first[w.nseg];
@@ -357,23 +355,23 @@ __global__ __launch_bounds__(256) void k_off_write(WireCounts w, const uint64_t 
         lc[threadIdx.x + 256 * j] = i < N ? wire_count(w, first, i) : 0u;
     }
     __syncthreads();
-    uint32_t c[8], s = 0;
+    uint64_t c[8], s = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j) {
         c[j] = lc[8 * threadIdx.x + j];
         s += c[j];
     }
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t x = s;
+    uint64_t x = s;
 #pragma unroll
     for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        const uint64_t y = __shfl_up(x, d, 64);
         if (lane >= d) x += y;
     }
     if (lane == 63) wsum[wv] = x;
     __syncthreads();
-    uint32_t run = x - s;
-    for (uint32_t k = 0; k < wv; ++k) run += (uint32_t)wsum[k];
+    uint64_t run = x - s;
+    for (uint32_t k = 0; k < wv; ++k) run += wsum[k];
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j) {
         run += c[j];
@@ -620,10 +618,6 @@ int mbrwt_unpack_offsets_device(const void *d_base, uint32_t nseg, uint64_t seg_
     }
     if (nseg > kWireScanSegs) {
         set_error("more than 8 segments: unpack the counts (mbrwt_unpack_segments_device) and scan them");
-        return MBRWT_ERR_UNSUPPORTED;
-    }
-    if (bits > kOffMaxBits) {  // k_off_write scans a block's 2,048 counts in u32
-        set_error("row counts wider than 21 bits: unpack the counts (mbrwt_unpack_segments_device) and scan them");
         return MBRWT_ERR_UNSUPPORTED;
     }
     WireCounts wc{reinterpret_cast<const uint8_t *>(d_base), seg_stride, nseg, bits, WireFirst{}};

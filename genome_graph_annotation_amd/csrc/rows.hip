@@ -47,17 +47,12 @@ namespace mbrwt {
 // ------------------------------------------------------------------------
 // layout selection
 // ------------------------------------------------------------------------
-static thread_local int g_build_layout = LAYOUT_AUTO;  // AUTO: MBRWT_LAYOUT, else the automatic choice
+static thread_local int g_build_layout = LAYOUT_AUTO;  // AUTO: the automatic choice
+static thread_local BuildTuning g_build_tuning;        // MBRWT_BUILD_ROWS_VAR .. _ROWS_WGS_PER_CU
+BuildTuning &build_tuning() { return g_build_tuning; }
+void set_build_tuning(const BuildTuning &t) { g_build_tuning = t; }
 
-int build_layout() {
-    if (g_build_layout != LAYOUT_AUTO) return g_build_layout;
-    const char *e = std::getenv("MBRWT_LAYOUT");
-    if (!e || !*e) return LAYOUT_AUTO;
-    if (!std::strcmp(e, "nodes")) return LAYOUT_NODES;
-    if (!std::strcmp(e, "rows")) return LAYOUT_ROWS;
-    if (!std::strcmp(e, "both")) return LAYOUT_BOTH;
-    return LAYOUT_AUTO;
-}
+int build_layout() { return g_build_layout; }
 
 void set_build_layout(int layout) { g_build_layout = layout; }
 int thread_build_layout() { return g_build_layout; }
@@ -625,10 +620,9 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         // on directory lines): for rows too long for the blocks -- a block
         // layout costing more than kAutoMaxCost requests per row (most rows
         // spilled, or records longer than a block) or none that fits.
-        // MBRWT_ROWS_VAR=1 / 0 forces / forbids them (tests, A/B).
+        // The build option MBRWT_BUILD_ROWS_VAR = 1 / 0 forces / forbids them.
         constexpr double kAutoMaxCost = 1.25;
-        const char *ve = std::getenv("MBRWT_ROWS_VAR");
-        const int force_var = ve && *ve ? std::atoi(ve) : -1;
+        const int force_var = build_tuning().rows_var;
         bool var_ok = force_var != 0 && rb.align % 13 == 0 && var_prepare(range.tree, im);
         double var_mem = 1e300;
         if (var_ok && (force_var == 1 || tmin > kAutoMaxCost)) {
@@ -648,7 +642,7 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         }
         if (var_ok && var_mem <= budget && (force_var == 1 || tmin > kAutoMaxCost)) {
             im.var = true;
-            if (const char *ge = std::getenv("MBRWT_VAR_G")) im.var_G = (uint32_t)std::max(0, std::atoi(ge));
+            im.var_G = build_tuning().var_lanes;
             if (im.var_G & (im.var_G - 1) || im.var_G > 16) im.var_G = 0;  // (1, 2, 4, 8 or 16)
             const uint64_t nlines = (rb.n + 12) / 13;
             MBRWT_HIP(hipMalloc(&im.var_lines, nlines * 64));
@@ -677,10 +671,9 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
                 if (c.mem <= budget && c.t <= tmin * tol && (!best || c.mem < best->mem)) best = &c;
             im.B = best->B;
             im.S = best->S;
-            if (const char *e = std::getenv("MBRWT_ROWS_BS")) {  // A/B switch: "B,S"
-                unsigned Bv = 0, Sv = 0;
-                if (std::sscanf(e, "%u,%u", &Bv, &Sv) == 2 && (Bv == 64 || Bv == 128) && Sv >= 1 &&
-                    Sv <= (Bv == 64 ? 8u : 15u) && rb.align % Sv == 0) {
+            if (const uint32_t bs = build_tuning().rows_block) {  // MBRWT_BUILD_ROWS_BLOCK: B << 8 | S
+                const uint32_t Bv = bs >> 8, Sv = bs & 0xFFu;
+                if ((Bv == 64 || Bv == 128) && Sv >= 1 && Sv <= (Bv == 64 ? 8u : 15u) && rb.align % Sv == 0) {
                     im.B = Bv;
                     im.S = Sv;
                 }
@@ -763,8 +756,7 @@ int rows_build_finish(RowsBuild *rbp) {
         }
         im.bytes = im.num_blocks * im.B + im.spill_bytes;
     }
-    if (const char *e = std::getenv("MBRWT_ROWS_WGS_PER_CU"))  // occupancy sweeps (read once per image)
-        im.occ_cap = (uint32_t)std::max(0, std::atoi(e));
+    im.occ_cap = build_tuning().rows_wgs_per_cu;  // (MBRWT_BUILD_ROWS_WGS_PER_CU: occupancy sweeps)
     im.ready = true;
     free_rows(rb.top->rows);
     rb.top->rows = im;
@@ -920,7 +912,6 @@ struct RowsParams {
     uint32_t stk_words;           // per-lane LDS stack slots (general walks)
     uint32_t frames;              // the tree odometer: internal levels on the longest path (1..kRowsOdoLevels)
     uint32_t mask1;               // every mask one byte
-    unsigned long long *claims;   // kRowsClaimCounters tile counters, kRowsClaimStride apart (zeroed between calls)
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -1255,82 +1246,20 @@ constexpr uint32_t kAbStampWaves = 16384, kAbStampWords = 8;
 __device__ unsigned long long g_ab_stamps[kAbStampWaves * kAbStampWords];
 #endif
 
-// The tile order of k_traverse_rows (r05).  A static assignment (tile gw +
-// k NW for wave gw of NW) gives every wave the same number of tiles, but not
-// the same time: waves of one SIMD are issued by age, so the youngest waves
-// of the persistent grid are the slowest (per-wave phase stamps at C4: wave
-// lifetimes 334k..608k cycles around a mean of 468k, profiles/r05), and the
-// kernel lasts as long as its slowest wave.  So each wave takes its first
-// kRowsStaticNum/Den of a fair share statically and then claims chunks of
-// kRowsClaim tiles from kRowsClaimCounters counters, each over its own range
-// of the remaining tiles (a wave starts at counter blockIdx % 8 -- one XCD's
-// workgroups under round-robin placement, a speed hint only -- and moves to
-// the next counter when its range is exhausted).  The claim for the next
-// chunk is issued one chunk ahead, so its return is hidden behind a tile.
-// Every tile is taken exactly once: the static tiles are disjoint, and a
-// counter hands out each chunk of its range once.
-constexpr uint32_t kRowsClaimCounters = 8, kRowsClaimStride = 16;  // (u64 words: a 128-byte line each)
-constexpr uint32_t kRowsClaim = 2, kRowsStaticNum = 1, kRowsStaticDen = 2;
-struct TileSeq {
-    uint64_t ntiles, NW, S0, dyn0, ndyn;
-    uint64_t gw, k;
-    uint64_t cs, ce;       // the current claimed chunk [cs, ce)
-    uint32_t px, probes;   // the counter of the pending claim; counters found exhausted
-    uint32_t pend;         // the pending claim (lane 0's atomic return)
-    bool has_pend;
-    unsigned long long *claims;
-    __device__ __forceinline__ uint64_t lo(uint32_t x) const { return dyn0 + ndyn * x / kRowsClaimCounters; }
-    __device__ __forceinline__ void claim(uint32_t lane) {
-        uint32_t v = 0;
-        if (lane == 0) v = (uint32_t)atomicAdd(claims + (uint64_t)px * kRowsClaimStride, 1ull);
-        pend = v;
-        has_pend = true;
-    }
-    __device__ __forceinline__ void init(uint64_t n_tiles, uint64_t nw, uint64_t wave, uint32_t home,
-                                         unsigned long long *c) {
-        ntiles = n_tiles;
-        NW = nw;
-        gw = wave;
-        k = 0;
-#if defined(MBRWT_AB_CLAIMS)
-        S0 = ntiles / NW * kRowsStaticNum / kRowsStaticDen;  // (A/B: claimed tail)
-#else
-        S0 = (ntiles + NW - 1) / NW;  // the static order only
-#endif
-        dyn0 = S0 * NW < ntiles ? S0 * NW : ntiles;
-        ndyn = ntiles - dyn0;
-        cs = ce = 0;
-        px = home % kRowsClaimCounters;
-        probes = 0;
-        pend = 0;
-        has_pend = false;
-        claims = c;
-    }
-    // the wave's next tile (wave-uniform), ntiles when there is none
-    __device__ __forceinline__ uint64_t next(uint32_t lane) {
-        if (k < S0) {
-            const uint64_t t = gw + k * NW;
-            ++k;
-            if (t < ntiles) return t;
-        }
-        if (cs < ce) return cs++;
-        while (ndyn && probes < kRowsClaimCounters) {
-            if (!has_pend) claim(lane);
-            const uint64_t v = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
-            has_pend = false;
-            const uint64_t start = lo(px) + v * kRowsClaim, hi = lo(px + 1);
-            if (start < hi) {
-                cs = start;
-                ce = start + kRowsClaim < hi ? start + kRowsClaim : hi;
-                claim(lane);  // the next chunk, one chunk ahead
-                return cs++;
-            }
-            px = (px + 1) % kRowsClaimCounters;
-            ++probes;
-        }
-        return ntiles;
-    }
-};
+// Tiles per wave (r05).  A persistent grid (every wave a fixed share of the
+// tiles) lasts as long as its slowest wave, and its waves are not equally
+// fast: the workgroups dispatched last lose issue arbitration by age (per-wave
+// phase stamps at C4: the third workgroup of each CU took 27.5k cycles per
+// tile against 22.3k for the first, lifetimes 396k..623k cycles around a mean
+// of 507k; profiles/r05/v03_balance).  A grid of one tile per wave lets the
+// dispatcher refill each CU as its waves finish: 0.263-0.271 ms against
+// 0.280-0.284 ms per 8 M rows on the same boxes.  Rejected (same boxes):
+// claiming the second half of the tiles from per-XCD atomic counters (0.316:
+// the claims' returns sit in the waves' vmcnt queue ahead of their block
+// loads), s_setprio for the later workgroups (0.2855), and requesting the
+// next tile's blocks before walking this one (register prefetch with the
+// spill reloads issued first: 0.2865 persistent, 0.2775 at 4 tiles per wave).
+constexpr uint32_t kRowsTilesPerWave = 1;
 
 // k_traverse_rows: one wave per tile of 64 query rows (file comment).
 // B: block bytes; WPB: waves per workgroup (the RWT2 table is staged once per
@@ -1340,16 +1269,9 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows[];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if defined(MBRWT_AB_PRIO)
-    // (A/B: the later-dispatched workgroups of the persistent grid lose issue
-    // arbitration by age; raise their priority)
-    if (blockIdx.x >= gridDim.x / 3 * 2) __builtin_amdgcn_s_setprio(2);
-    else if (blockIdx.x >= gridDim.x / 3) __builtin_amdgcn_s_setprio(1);
-#endif
     const uint64_t ntiles = (p.n + 63) / 64;
-    TileSeq seq;
-    seq.init(ntiles, (uint64_t)gridDim.x * WPB, (uint64_t)blockIdx.x * WPB + wv, blockIdx.x, p.claims);
-    uint64_t t = seq.next(lane);
+    const uint64_t tstride = (uint64_t)gridDim.x * WPB;  // (one tile per wave unless the grid is capped)
+    uint64_t t = (uint64_t)blockIdx.x * WPB + wv;
     uint64_t row_n = 0;  // the row of this lane in the wave's next tile (its load overlaps the table's)
     if (t < ntiles && t * 64 + lane < p.n) row_n = gld(p.rows + t * 64 + lane);
     for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_rows[i] = gld(p.table + i);
@@ -1390,33 +1312,38 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
 #if defined(MBRWT_AB_GATHER)
     uint32_t ab_acc = 0;
 #endif
-    for (uint64_t tn; t < ntiles; t = tn) {
-        AB_STAMP(4);
-        const uint64_t r0 = t * 64;
-        const uint32_t nr = (uint32_t)(p.n - r0 < 64 ? p.n - r0 : 64);
-        const uint64_t row = row_n;
-        tn = seq.next(lane);
-        if (tn < ntiles && tn * 64 + lane < p.n) row_n = gld(p.rows + tn * 64 + lane);
-        const bool valid = lane < nr && row < p.num_rows;
-        if (lane < nr && !valid) atomicOr(&p.scalars[2], 1ull);
-        const uint64_t b = valid ? rows_block(row, S, p.magic) : 0;
-        const uint32_t sub = (uint32_t)(row - b * S);
-#if defined(MBRWT_AB_HOT)
-        // (timing only: every block read from a 256 KiB window, cache-resident)
-        const uint64_t addr = p.blocks + (b & 4095u) * B;
-#else
-        const uint64_t addr = p.blocks + b * B;
-#endif
-        // the 64 blocks as coalesced quarters: load k brings rows RPI k ..
-        // RPI k + RPI - 1, lane L its 16 bytes L % LPB
-        u32x4_t q[LPB];
+    // a tile's 64 blocks as coalesced quarters: load k brings rows RPI k ..
+    // RPI k + RPI - 1, lane L its 16 bytes L % LPB (row addresses by __shfl)
+    auto issue_blocks = [&](uint64_t addr, u32x4_t (&qq)[LPB]) {
 #pragma unroll
         for (uint32_t k = 0; k < LPB; ++k) {
             const int src = (int)(RPI * k + lane / LPB);
             const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)addr, src, 64);
             const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(addr >> 32), src, 64);
-            q[k] = gld_at_nt<u32x4_t, NT>((((uint64_t)hi << 32) | lo) + 16u * (lane % LPB));
+            qq[k] = gld_at_nt<u32x4_t, NT>((((uint64_t)hi << 32) | lo) + 16u * (lane % LPB));
         }
+    };
+    auto block_of = [&](uint64_t row, bool ok) -> uint64_t { return ok ? rows_block(row, S, p.magic) : 0; };
+    auto addr_of = [&](uint64_t b) -> uint64_t {
+#if defined(MBRWT_AB_HOT)
+        return p.blocks + (b & 4095u) * B;  // (timing only: a 256 KiB window, cache-resident)
+#else
+        return p.blocks + b * B;
+#endif
+    };
+    u32x4_t q[LPB];
+    for (uint64_t tn; t < ntiles; t = tn) {
+        AB_STAMP(4);
+        const uint64_t r0 = t * 64;
+        const uint32_t nr = (uint32_t)(p.n - r0 < 64 ? p.n - r0 : 64);
+        const uint64_t row = row_n;
+        tn = t + tstride;
+        if (tn < ntiles && tn * 64 + lane < p.n) row_n = gld(p.rows + tn * 64 + lane);
+        const bool valid = lane < nr && row < p.num_rows;
+        if (lane < nr && !valid) atomicOr(&p.scalars[2], 1ull);
+        const uint64_t b = block_of(row, valid);
+        const uint32_t sub = (uint32_t)(row - b * S);
+        issue_blocks(addr_of(b), q);
 #if defined(MBRWT_AB_GATHER)
         // (timing only: the block loads into registers, no LDS, nothing else)
 #pragma unroll
@@ -1446,28 +1373,29 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
             ++o;
         }
         bool lng = false;
-        if (__any(spl)) {
-            // spilled rows: the entry (<= B bytes of it) replaces the block in
-            // the lane's own slot; masks from byte 8
-            if (spl) {
-                const uint32_t idx = (uint32_t)mine[o] | ((uint32_t)mine[o + 1] << 8) | ((uint32_t)mine[o + 2] << 16) |
-                                     ((uint32_t)mine[o + 3] << 24);
-                const uint64_t sa = p.spill + (uint64_t)idx * 16;
-                u32x4_t sq[LPB];
+        // spilled rows: the entry (<= B bytes of it) replaces the block in
+        // the lane's own slot; masks from byte 8
+        const bool any_spl = __any(spl);
+        u32x4_t sq[LPB];
+        if (any_spl && spl) {
+            const uint32_t idx = (uint32_t)mine[o] | ((uint32_t)mine[o + 1] << 8) | ((uint32_t)mine[o + 2] << 16) |
+                                 ((uint32_t)mine[o + 3] << 24);
+            const uint64_t sa = p.spill + (uint64_t)idx * 16;
 #pragma unroll
-                for (uint32_t k = 0; k < LPB; ++k) sq[k] = gld_at<u32x4_t>(sa + 16u * k);
+            for (uint32_t k = 0; k < LPB; ++k) sq[k] = gld_at<u32x4_t>(sa + 16u * k);
+        }
+        if (any_spl && spl) {
 #pragma unroll
-                for (uint32_t k = 0; k < LPB; ++k) {
-                    AS_LDS uint32_t *d = (AS_LDS uint32_t *)mine + 4 * k;
-                    d[0] = sq[k].x;
-                    d[1] = sq[k].y;
-                    d[2] = sq[k].z;
-                    d[3] = sq[k].w;
-                }
-                cnt = sq[0].x;
-                lng = 8 + sq[0].y > B;
-                o = 8;
+            for (uint32_t k = 0; k < LPB; ++k) {
+                AS_LDS uint32_t *d = (AS_LDS uint32_t *)mine + 4 * k;
+                d[0] = sq[k].x;
+                d[1] = sq[k].y;
+                d[2] = sq[k].z;
+                d[3] = sq[k].w;
             }
+            cnt = sq[0].x;
+            lng = 8 + sq[0].y > B;
+            o = 8;
         }
         const uint32_t x = wave_incl_sum(cnt);
         const uint32_t total = __builtin_amdgcn_readlane(x, 63);
@@ -1593,7 +1521,6 @@ struct CompactParams {
     uint64_t n, cap;
     unsigned long long *scalars;  // the traversal's counters ([2] error flags)
     unsigned long long *status;   // {total, status, sticky}
-    unsigned long long *claims;   // the traversal's tile counters (cleared here)
     const uint64_t *rows;         // the batch (direct tiles)
     RowsView v;
     const uint32_t *table;        // RWT (direct tiles)
@@ -1609,8 +1536,6 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
     const uint64_t ntiles = (n + 63) / 64;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t total = gld(p.tile_offsets + ntiles - 1) + (gld(p.tile_counts + ntiles - 1) & 0x3FFFFFFFu);
-    if (blockIdx.x == 0 && threadIdx.x < kRowsClaimCounters)  // the traversal's tile counters, for the next call
-        p.claims[threadIdx.x * kRowsClaimStride] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const uint64_t err = p.scalars[2];
         p.scalars[2] = 0;
@@ -1899,18 +1824,13 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     // counts workspace: nt+1 tile counts | (8-byte aligned) nt+1 tile offsets
     const uint64_t to_off = ((nt + 1) * sizeof(uint32_t) + 7) / 8 * 8;
     if ((rc = ensure(c.ws_temp, nt * region))) return rc;
-    // [tile counts | tile offsets | the kernel's own counters (4 x u64) |
-    // (128-byte aligned) the tile claim counters, a line each]
+    // [tile counts | tile offsets | the kernel's own counters (4 x u64)]
     const uint64_t sc_off = to_off + (nt + 1) * sizeof(uint64_t);
-    const uint64_t cl_off = (sc_off + 32 + 127) / 128 * 128;
-    const uint64_t sc_bytes = cl_off + kRowsClaimCounters * kRowsClaimStride * 8 - sc_off;
-    const bool fresh = c.ws_counts.bytes < sc_off + sc_bytes;
-    if ((rc = ensure(c.ws_counts, sc_off + sc_bytes))) return rc;
+    const bool fresh = c.ws_counts.bytes < sc_off + 32;
+    if ((rc = ensure(c.ws_counts, sc_off + 32))) return rc;
     unsigned long long *d_sc = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + sc_off);
-    unsigned long long *d_claims =
-        reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + cl_off);
     if (fresh || c.rows_sc_dirty || c.rows_sc_at != sc_off) {  // the counters are cleared by k_compact_tiles
-        MBRWT_HIP(hipMemsetAsync(d_sc, 0, sc_bytes, s));
+        MBRWT_HIP(hipMemsetAsync(d_sc, 0, 32, s));
         c.rows_sc_dirty = false;
         c.rows_sc_at = sc_off;
     }
@@ -1945,7 +1865,6 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     p.stk_words = walk >= WALK_ODOMETER ? 0u : rows_stack_words(im);  // (the odometers keep no stack)
     p.frames = im.frames;
     p.mask1 = im.mask1 ? 1u : 0u;
-    p.claims = d_claims;
 
     const size_t table_bytes = ((im.table2.size() + 3) & ~size_t(3)) * 4;
     const size_t per_wave = 64ull * (im.B + 4) + 256ull * p.stk_words + (walk >= WALK_ODOMETER ? 2ull * C : 0ull);
@@ -1960,7 +1879,7 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     // at most 24 waves (3 workgroups of 8) per CU: more waves make the walk phase
     // slower than the extra loads in flight gain (C4 0.426 ms at 3 against
     // 0.456 at 4, C2 0.068 against 0.073: profiles/r03/v06_rows_occupancy_*);
-    // MBRWT_ROWS_WGS_PER_CU (read when the image is built) overrides
+    // MBRWT_BUILD_ROWS_WGS_PER_CU (when the image is built) overrides
     const int occ_cap = im.occ_cap ? (int)im.occ_cap : (int)std::max(1u, 24u / wpb);
     if (c.rb_fn != reinterpret_cast<const void *>(kfn) || c.rb_lds != lds || c.rb_threads != threads ||
         c.rb_cap != occ_cap) {
@@ -1996,11 +1915,13 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     }
     if (c.timing) MBRWT_HIP(hipEventRecord(e0, s));
     {
-#if defined(MBRWT_AB_TPW)
-        // (A/B: a grid of ceil(tiles / (wpb x TPW)) workgroups, TPW tiles per wave)
-        const uint64_t g = std::max<uint64_t>(1, (nt + (uint64_t)wpb * MBRWT_AB_TPW - 1) / ((uint64_t)wpb * MBRWT_AB_TPW));
-#else
+#if defined(MBRWT_AB_PERSISTENT)
+        // (A/B: the r04 persistent grid, the resident workgroups only)
         const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((nt + wpb - 1) / wpb, (uint64_t)c.rb_blocks));
+#else
+        // kRowsTilesPerWave tiles per wave; the dispatcher refills each CU
+        const uint64_t per_wg = (uint64_t)wpb * kRowsTilesPerWave;
+        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((nt + per_wg - 1) / per_wg, 1ull << 30));
 #endif
         hipLaunchKernelGGL(kfn, dim3((unsigned)g), dim3(threads), lds, s, p);
         MBRWT_HIP(hipGetLastError());
@@ -2019,7 +1940,6 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         cp.cap = cap;
         cp.scalars = d_sc;
         cp.status = st_blk;
-        cp.claims = d_claims;
         cp.rows = d_rows;
         cp.v = view_of(c);
         cp.table = im.d_table;

@@ -23,12 +23,9 @@
 namespace mbrwt {
 
 uint64_t shard_rows_for(uint64_t num_rows) {
-    // MBRWT_SHARD_ROWS: test hook (small shards exercise the routing on
+    // MBRWT_BUILD_SHARD_ROWS: test hook (small shards exercise the routing on
     // oracle-sized trees); otherwise shards only when one image cannot hold the rows
-    if (const char *e = std::getenv("MBRWT_SHARD_ROWS")) {
-        const uint64_t v = std::strtoull(e, nullptr, 10);
-        if (v > 0 && v < num_rows) return std::min<uint64_t>(v, kShardRowsMax);
-    }
+    if (const uint64_t v = build_tuning().shard_rows; v > 0 && v < num_rows) return std::min<uint64_t>(v, kShardRowsMax);
     return num_rows > kMaxRows ? kShardRowsMax : 0;
 }
 

@@ -281,8 +281,7 @@ class DeviceAllGatherV:
         # once (every unpack runs on the one side stream, so one scratch)
         import ctypes as C
         self._counts = (C.c_uint64 * self.world)(*self.ns)
-        # (beyond one node, or counts wider than 21 bits: counts unpacked, then scanned)
-        self.fused_offsets = self.world <= 8 and self.bits_c <= 21
+        self.fused_offsets = self.world <= 8  # (beyond one node: counts unpacked, then scanned)
         tb = C.c_uint64(0)
         if self.fused_offsets:
             L.check(L.lib().mbrwt_unpack_offsets_device(C.c_void_p(16), self.world, self.per, self._counts,
@@ -315,6 +314,12 @@ class DeviceAllGatherV:
         self.k += 1
         cur = torch.cuda.current_stream(self.device)
         s = cur.cuda_stream
+        if sl.get("used"):
+            # the slot's previous exchange (queued from any stream: callers may
+            # alternate query streams) has read its send buffer and written its
+            # outputs before this one packs
+            cur.wait_event(sl["done"])
+        sl["used"] = True
         if sl["ev"]:
             sl["ev"]["t0"].record(cur)
         L.check(L.lib().mbrwt_pack_csr_device(offsets.data_ptr(), self.ns[self.rank], cols.data_ptr(),

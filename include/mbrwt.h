@@ -178,8 +178,7 @@ int mbrwt_ctx_clone(mbrwt_ctx *src, mbrwt_ctx **out);
  *          the node image.
  * The layout is chosen when a context is created: mbrwt_set_build_option
  * (MBRWT_BUILD_LAYOUT, value) sets it for the mbrwt_create* / mbrwt_load calls
- * of the calling thread; MBRWT_LAYOUT_AUTO (the default) takes the
- * environment variable MBRWT_LAYOUT=nodes|rows|both, else chooses: ROWS when
+ * of the calling thread; MBRWT_LAYOUT_AUTO (the default) chooses: ROWS when
  * the tree is within the row-record limits, its records cost at most ~1.25
  * block requests per row (no dense-row shapes) and the image fits the
  * device, NODES otherwise.  Layout ROWS on a tree outside its limits ->
@@ -211,6 +210,36 @@ int mbrwt_ctx_clone(mbrwt_ctx *src, mbrwt_ctx **out);
 #define MBRWT_LAYOUT_NODES 1
 #define MBRWT_LAYOUT_ROWS 2
 #define MBRWT_LAYOUT_BOTH 3
+/* Tuning and test options of the calling thread's builds (r05: these were
+   environment variables read by the library; they are now explicit, scoped
+   like the options above).  Every default is the automatic choice.
+   MBRWT_BUILD_ROWS_VAR       -1 auto, 0 never, 1 always the variable-length
+                              records of dense rows (uniform trees)
+   MBRWT_BUILD_VAR_LANES      lanes per row of their decode (0 auto; 1..16, a
+                              power of two)
+   MBRWT_BUILD_ROWS_BLOCK     row-record blocks: 0 auto, else B << 8 | S (B 64 or
+                              128 bytes, S rows per block)
+   MBRWT_BUILD_ROWS_RANGE     rows per range of a ranged row-record build (0
+                              auto; a multiple of 360,360)
+   MBRWT_BUILD_NODE_KINDS     node-image kinds built (bit mask, default all):
+                              MBRWT_KIND_FOLD_ROOT | _PACK | _PACK2 | _PACKT;
+                              PACK2 / PACKT also need PACK
+   MBRWT_BUILD_SHARD_ROWS     rows per row shard (0: 2^31; small values force
+                              shards on small trees -- a test hook)
+   MBRWT_BUILD_ROWS_WGS_PER_CU  resident workgroups per CU of the row-record
+                              traversal (0 auto; occupancy sweeps) */
+#define MBRWT_BUILD_ROWS_VAR 4
+#define MBRWT_BUILD_VAR_LANES 5
+#define MBRWT_BUILD_ROWS_BLOCK 6
+#define MBRWT_BUILD_ROWS_RANGE 7
+#define MBRWT_BUILD_NODE_KINDS 8
+#define MBRWT_BUILD_SHARD_ROWS 9
+#define MBRWT_BUILD_ROWS_WGS_PER_CU 10
+#define MBRWT_KIND_FOLD_ROOT 1
+#define MBRWT_KIND_PACK 2
+#define MBRWT_KIND_PACK2 4
+#define MBRWT_KIND_PACKT 8
+#define MBRWT_KIND_ALL 15
 int mbrwt_set_build_option(int option, int64_t value);
 /* The calling thread's current value of a build option (so that a caller can
    restore it after a scoped change). */
@@ -292,8 +321,8 @@ int mbrwt_device(const mbrwt_ctx *ctx);
  * (mbrwt_create, mbrwt_load, mbrwt_create_synthetic[_shaped]) holds row
  * shards of 2^31 rows -- each the BRWT restricted to its row range -- and
  * routes every query's rows to them; results are those of the whole matrix.
- * mbrwt_num_shards = 1 for an ordinary context.  (MBRWT_SHARD_ROWS=<rows> in
- * the environment at creation forces smaller shards: a test hook.)
+ * mbrwt_num_shards = 1 for an ordinary context.  (The build option
+ * MBRWT_BUILD_SHARD_ROWS forces smaller shards: a test hook.)
  */
 uint64_t mbrwt_num_shards(const mbrwt_ctx *ctx);
 
@@ -469,8 +498,7 @@ int mbrwt_unpack_labels_device(const void *d_base, uint32_t nseg, uint64_t seg_s
    block's counts re-read and scanned in LDS (no int32 count array in
    between).  d_temp == NULL: *temp_bytes receives the
    scratch size the call needs and nothing runs.  At most 8 segments (one
-   node) and counts of at most 21 bits (tables below 2^21 columns);
-   MBRWT_ERR_UNSUPPORTED beyond (unpack the counts and scan them). */
+   node); MBRWT_ERR_UNSUPPORTED beyond (unpack the counts and scan them). */
 int mbrwt_unpack_offsets_device(const void *d_base, uint32_t nseg, uint64_t seg_stride, const uint64_t *counts,
                                 uint32_t bits, uint64_t *d_offsets, void *d_temp, uint64_t *temp_bytes,
                                 void *stream);

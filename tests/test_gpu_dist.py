@@ -2,8 +2,9 @@
 traverses its contiguous slice of each global batch with the asynchronous
 get_rows (row records, the library default), and dist.DeviceAllGatherV
 reassembles the global CSR pipelined over 3 wire slots (up to two exchanges
-in flight behind the current step, no host synchronisation per step) -- the
-exact call pattern of bench.py at N > 1.  The process group is gloo (two
+in flight behind the current step, no host synchronisation per step), the
+batches alternating between two query contexts on two streams -- the exact
+call pattern of bench.py at N > 1.  The process group is gloo (two
 processes sharing one GPU cannot form an RCCL group); on the 8-GPU node the
 same code runs over RCCL.  Every reassembled batch is checked against the
 oracle."""
@@ -58,24 +59,29 @@ def _rank(rank, world, port, q):
         assert wire.cap == max(int(rows_per_rank[r] * 8 * 1.3) + 1024 + 24 * r for r in range(world))
         bufs = [(torch.empty(nb + 1, dtype=torch.int64, device=dev_t), torch.empty(cap, dtype=torch.int32, device=dev_t))
                 for _ in range(2)]
-        status = torch.zeros(3, dtype=torch.int64, device=dev_t)
-        s = torch.cuda.current_stream(dev_t).cuda_stream
+        # bench.py's N > 1 step since r05: two query contexts (the context and
+        # a clone over the same image) on two streams, alternating batches
+        mats = [mat, mat.clone()]
+        streams = [torch.cuda.current_stream(dev_t), torch.cuda.Stream(dev_t)]
+        status = [torch.zeros(3, dtype=torch.int64, device=dev_t) for _ in range(2)]
         inflight, done = [], []
         for i in range(K):
             o, cb = bufs[i % 2]
-            mat.get_rows_device_async(rows_ts[i], o, cb, status, s)
-            if len(inflight) == len(wire.slots) - 1:
-                k, sl = inflight.pop(0)
-                g_off, g_cols, g_st = wire.finish(sl)
-                done.append((k, g_off.clone(), g_cols.clone(), g_st.clone()))
-            inflight.append((i, wire.start(o, cb, status)))
+            qi = i % 2
+            with torch.cuda.stream(streams[qi]):
+                mats[qi].get_rows_device_async(rows_ts[i], o, cb, status[qi], streams[qi].cuda_stream)
+                if len(inflight) == len(wire.slots) - 1:
+                    k, sl = inflight.pop(0)
+                    g_off, g_cols, g_st = wire.finish(sl)
+                    done.append((k, g_off.clone(), g_cols.clone(), g_st.clone()))
+                inflight.append((i, wire.start(o, cb, status[qi])))
         while inflight:
             k, sl = inflight.pop(0)
             g_off, g_cols, g_st = wire.finish(sl)
             done.append((k, g_off.clone(), g_cols.clone(), g_st.clone()))
         torch.cuda.synchronize()
-        need, st, sticky = status.cpu().tolist()
-        ok = sticky == 1  # every asynchronous get_rows returned MBRWT_OK
+        # every asynchronous get_rows on both contexts returned MBRWT_OK
+        ok = all(st.cpu().tolist()[2] == 1 for st in status)
         t = O.OracleTree.topdown(n, m, d, 8, 31)
         for k, g_off, g_cols, g_st in done:
             tot, bad = g_st.cpu().tolist()

@@ -21,15 +21,9 @@ def _same_tree(a, b):
 
 
 def _env(name, value, fn):
-    old = os.environ.get(name)
-    os.environ[name] = value
-    try:
-        return fn()
-    finally:
-        if old is None:
-            del os.environ[name]
-        else:
-            os.environ[name] = old
+    """fn() under the build option that replaced the r04 switch `name`."""
+    from conftest import with_build
+    return with_build(name, value, fn)
 
 
 @pytest.mark.parametrize("layout", [{}, {"MBRWT_PACK2": "0"}, {"MBRWT_PACK": "0"}, {"MBRWT_FOLD_ROOT": "0"},
@@ -160,15 +154,7 @@ def test_export_rows_ranged_and_synthetic(oracle_mod):
     synthetic law across them) equals the oracle's tree of the same spec."""
     from genome_graph_annotation_amd import BRWTDevice
     O = oracle_mod
-    old = os.environ.get("MBRWT_ROWS_RANGE")
-    os.environ["MBRWT_ROWS_RANGE"] = "360360"
-    try:
-        dev = BRWTDevice.synthetic(1_100_000, 700, 0.004, 8, 9, layout="rows")
-    finally:
-        if old is None:
-            del os.environ["MBRWT_ROWS_RANGE"]
-        else:
-            os.environ["MBRWT_ROWS_RANGE"] = old
+    dev = _env("MBRWT_ROWS_RANGE", "360360", lambda: BRWTDevice.synthetic(1_100_000, 700, 0.004, 8, 9, layout="rows"))
     _same_tree(O.OracleTree.topdown(1_100_000, 700, 0.004, 8, 9).export(), dev.export())
     syn = BRWTDevice.synthetic(300_000, 2652, 0.003, 8, 42, layout="rows")
     _same_tree(O.OracleTree.topdown(300_000, 2652, 0.003, 8, 42).export(), syn.export())

@@ -308,22 +308,15 @@ def test_get_column_synthetic_and_errors(oracle_mod):
 # ---- KIND_PACK layout (mbrwt_internal.hpp) vs the plain PLANE + MASK8 layout ----
 
 def _with_env(name, value, fn):
-    import os
-    old = os.environ.get(name)
-    os.environ[name] = value
-    try:
-        return fn()
-    finally:
-        if old is None:
-            del os.environ[name]
-        else:
-            os.environ[name] = old
+    """fn() under the build option that replaced the r04 switch `name`."""
+    from conftest import with_build
+    return with_build(name, value, fn)
 
 
 @pytest.fixture
-def no_packt(monkeypatch):
+def no_packt(build_env):
     """The PACK / PACK2 layout tests measure those layouts: no KIND_PACKT."""
-    monkeypatch.setenv("MBRWT_PACKT", "0")
+    build_env("MBRWT_PACKT", "0")
 
 
 def _agree(oracle_tree, devs, rows, cols, m):

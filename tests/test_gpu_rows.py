@@ -180,7 +180,7 @@ def test_tree_odometer(oracle_mod, n, m, d, part, arity, relax):
         np.testing.assert_array_equal(cols_d, cols_o)
 
 
-def test_auto_layout(oracle_mod, monkeypatch):
+def test_auto_layout(oracle_mod, build_env):
     """The library default (MBRWT_LAYOUT_AUTO): row records for every tree
     within their limits whose records fit one block request per row; the
     per-node images for a one-column tree, nodes wider than 16 children,
@@ -210,7 +210,7 @@ def test_auto_layout(oracle_mod, monkeypatch):
     dg = BRWTDevice.from_tree(tg.export())
     assert dg.layout() == "nodes"
     _check_all(tg, dg, np.arange(0, 3000, 7, dtype=np.uint64), dense, columns=False)
-    monkeypatch.setenv("MBRWT_LAYOUT", "nodes")
+    build_env("MBRWT_LAYOUT", "nodes")
     assert BRWTDevice.from_tree(O.OracleTree.from_dense(sparse, "basic", 8).export()).layout() == "nodes"
 
 
@@ -227,12 +227,12 @@ def test_arity_limit(oracle_mod):
 
 
 @pytest.mark.parametrize("bs", ["64,1", "64,2", "64,3", "64,5", "64,8", "128,1", "128,3", "128,7", "128,15"])
-def test_every_block_shape(oracle_mod, bs, monkeypatch):
+def test_every_block_shape(oracle_mod, bs, build_env):
     """Every (block bytes, rows per block) the builder may pick -- spills,
     long records and the direct pass included -- answers like the oracle."""
     O = oracle_mod
     from genome_graph_annotation_amd import BRWTDevice
-    monkeypatch.setenv("MBRWT_ROWS_BS", bs)
+    build_env("MBRWT_ROWS_BS", bs)
     rng = np.random.default_rng(5)
     n, m = 30000, 300
     # rows of very different lengths: most sparse, some dense (long records)
@@ -294,12 +294,12 @@ def test_greedy_relax_shape_rows(oracle_mod):
     np.testing.assert_array_equal(cols_d, cols_o)
 
 
-def test_ranged_build(oracle_mod, monkeypatch):
+def test_ranged_build(oracle_mod, build_env):
     """Layout rows built one range of rows at a time (synthetic law across
     the ranges, and a tree description sliced per range)."""
     O = oracle_mod
     from genome_graph_annotation_amd import BRWTDevice
-    monkeypatch.setenv("MBRWT_ROWS_RANGE", "360360")
+    build_env("MBRWT_ROWS_RANGE", "360360")
     n, m, d = 1_500_000, 700, 0.004
     dev = BRWTDevice.synthetic(n, m, d, 8, 9, layout="rows")
     t = O.OracleTree.topdown(n, m, d, 8, 9)
@@ -467,16 +467,16 @@ def test_get_rows_device_async(oracle_mod, layout):
     (1000, 2652, 0.003, 8),   # sparse (most rows without a record)
 ])
 @pytest.mark.parametrize("G", ["", "1", "2", "4", "8", "16"])
-def test_variable_records(oracle_mod, monkeypatch, n, m, d, arity, G):
+def test_variable_records(oracle_mod, build_env, n, m, d, arity, G):
     """The variable-length layout (forced with MBRWT_ROWS_VAR=1; every lane
     split G) answers every row-record query like the oracle, its V / L
     accounting equals the node image's, and its export rebuilds the tree."""
     O = oracle_mod
     import torch
     from genome_graph_annotation_amd import BRWTDevice
-    monkeypatch.setenv("MBRWT_ROWS_VAR", "1")
+    build_env("MBRWT_ROWS_VAR", "1")
     if G:
-        monkeypatch.setenv("MBRWT_VAR_G", G)
+        build_env("MBRWT_VAR_G", G)
     rng = np.random.default_rng(n + m + len(G))
     dense = rng.random((n, m)) < d
     dense[n // 3: n // 3 + 70] = rng.random((70, m)) < 0.9  # a run of very long rows: tiles beyond the LDS budget
@@ -495,7 +495,7 @@ def test_variable_records(oracle_mod, monkeypatch, n, m, d, arity, G):
 
 
 @pytest.mark.parametrize("force", ["1", ""])
-def test_variable_records_wide_units(oracle_mod, monkeypatch, force):
+def test_variable_records_wide_units(oracle_mod, build_env, force):
     """Rows of ~1,230 labels (4,096 columns, arity 4, 1,024 units, d = 0.3):
     the decode's full-size per-wave budget (record chunks, owners, label stage)
     for 4 waves plus the unit table would need ~245 KB of LDS (ADVICE r04;
@@ -506,7 +506,7 @@ def test_variable_records_wide_units(oracle_mod, monkeypatch, force):
     O = oracle_mod
     from genome_graph_annotation_amd import BRWTDevice
     if force:
-        monkeypatch.setenv("MBRWT_ROWS_VAR", force)
+        build_env("MBRWT_ROWS_VAR", force)
     n, m, d = 1500, 4096, 0.3
     rng = np.random.default_rng(77)
     dense = rng.random((n, m)) < d
@@ -520,14 +520,14 @@ def test_variable_records_wide_units(oracle_mod, monkeypatch, force):
     np.testing.assert_array_equal(cols_d, cols_o)
 
 
-def test_variable_records_ranged_async_and_errors(oracle_mod, monkeypatch):
+def test_variable_records_ranged_async_and_errors(oracle_mod, build_env):
     """Several ranges (one record allocation each), the asynchronous call with
     its status block, capacity and range errors on the variable layout."""
     O = oracle_mod
     import torch
     from genome_graph_annotation_amd import BRWTDevice, _lib as L
-    monkeypatch.setenv("MBRWT_ROWS_RANGE", "360360")
-    monkeypatch.setenv("MBRWT_ROWS_VAR", "1")
+    build_env("MBRWT_ROWS_RANGE", "360360")
+    build_env("MBRWT_ROWS_VAR", "1")
     n, m, d = 1_100_000, 700, 0.02
     dev = BRWTDevice.synthetic(n, m, d, 8, 9, layout="rows")
     assert dev.rows_stats()["variable"]

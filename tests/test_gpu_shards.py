@@ -26,15 +26,9 @@ pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="n
 
 
 def _env(name, value, fn):
-    old = os.environ.get(name)
-    os.environ[name] = value
-    try:
-        return fn()
-    finally:
-        if old is None:
-            del os.environ[name]
-        else:
-            os.environ[name] = old
+    """fn() under the build option that replaced the r04 switch `name`."""
+    from conftest import with_build
+    return with_build(name, value, fn)
 
 
 def _same_tree(a, b):

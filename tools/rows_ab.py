@@ -17,6 +17,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from genome_graph_annotation_amd import BRWTDevice, _lib as L  # noqa: E402
+from genome_graph_annotation_amd.brwt import build_option  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=3_700_000_000)
@@ -61,16 +62,17 @@ def set_variant(kv, m=None):
 for cfg in a.configs.split(";") if ";" in a.configs else a.configs.split(","):
     cfg_k, _, kvs = cfg.partition("@")
     layout, _, bs = cfg_k.partition(":")
-    if bs:
-        os.environ["MBRWT_ROWS_BS"] = bs
-    else:
-        os.environ.pop("MBRWT_ROWS_BS", None)
+    block = 0
+    if bs:  # row-record blocks "B,S" (build option MBRWT_BUILD_ROWS_BLOCK)
+        b_, s_ = (int(x) for x in bs.split(","))
+        block = b_ << 8 | s_
     set_variant("")
     t0 = time.time()
-    if shape is not None:
-        m = BRWTDevice.synthetic_shaped(a.rows, shape, a.density, a.seed, layout=layout)
-    else:
-        m = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, layout=layout)
+    with build_option(L.MBRWT_BUILD_ROWS_BLOCK, block):
+        if shape is not None:
+            m = BRWTDevice.synthetic_shaped(a.rows, shape, a.density, a.seed, layout=layout)
+        else:
+            m = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, layout=layout)
     build_s = time.time() - t0
     if cols is None:
         try:

@@ -11,6 +11,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from genome_graph_annotation_amd import BRWTDevice, _lib as L  # noqa: E402
+from genome_graph_annotation_amd.brwt import build_option  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=3_700_000_000)
@@ -26,9 +27,10 @@ a = ap.parse_args()
 ap2 = a
 mats = {}
 for fold in a.fold.split(","):
-    os.environ["MBRWT_FOLD_ROOT"] = fold
     t0 = time.time()
-    mats[fold] = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, 42)
+    kinds = L.MBRWT_KIND_ALL if fold != "0" else L.MBRWT_KIND_ALL & ~L.MBRWT_KIND_FOLD_ROOT
+    with build_option(L.MBRWT_BUILD_NODE_KINDS, kinds):
+        mats[fold] = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, 42)
     print(f"built fold={fold} {mats[fold].device_bytes() / 1e9:.1f} GB in {time.time() - t0:.1f}s", flush=True)
 m = next(iter(mats.values()))
 rows_np = np.random.default_rng(42).integers(0, a.rows, a.batch, dtype=np.uint64)
