@@ -268,6 +268,7 @@ struct RowsImage {
     // [unit bitmap][unit masks] addressed by 64-byte directory lines of 13 rows
     bool var = false;
     uint32_t var_W = 0;                 // bitmap words (units / 32, rounded up)
+    uint32_t var_ustride = 0;           // unit u's first column = u * var_ustride for every unit (0: use the table)
     uint32_t var_G = 0;                 // lanes per row of k_var_decode (0 = from the statistics; MBRWT_VAR_G)
     std::vector<uint32_t> var_units;    // per unit (leaf parent, DFS order): first column | arity << 16
     std::vector<uint16_t> var_unit_of;  // per dnode: its unit, or 0xFFFF

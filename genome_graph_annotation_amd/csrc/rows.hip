@@ -660,12 +660,18 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
                 set_error("row records too long for the block layout");
                 return MBRWT_ERR_UNSUPPORTED;
             }
-            // FAST: the smallest within 2 % of the fewest modelled requests;
-            // COMPACT (MBRWT_BUILD_ROWS_FOOTPRINT): within 30 % -- the model
-            // prices a spilled row as a whole request, while on walk-bound
-            // shapes its reload overlaps other waves' walks (greedy + relax,
-            // 20 % of rows spilled: +2 % kernel time)
-            const double tol = rb.footprint == 1 ? 1.30 : 1.02;
+            // The smallest image within `tol` of the fewest modelled requests.
+            // The model prices a spilled row as a whole second request, which
+            // holds on the odometer's uniform trees (request-bound: C4 with
+            // three rows per block, 0.321 against 0.268 ms, profiles/r05), so
+            // there FAST keeps within 2 %.  Under the tree odometer (greedy +
+            // relax, non-uniform) the reloads overlap the other waves' walks
+            // (20 % of the rows spilled: +2 % kernel time, profiles/r04/v15_*),
+            // so from r05 such trees take the COMPACT tolerance (30 %) by
+            // default: two rows per block, 158.9 GB instead of 236.9 GB at
+            // 3.7 B rows.  MBRWT_BUILD_ROWS_FOOTPRINT = COMPACT takes 30 % always.
+            const bool compact = rb.footprint == 1 || !im.uni;
+            const double tol = compact ? 1.30 : 1.02;
             const Cand *best = nullptr;
             for (const Cand &c : cands)
                 if (c.mem <= budget && c.t <= tmin * tol && (!best || c.mem < best->mem)) best = &c;
@@ -1915,14 +1921,16 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     }
     if (c.timing) MBRWT_HIP(hipEventRecord(e0, s));
     {
-#if defined(MBRWT_AB_PERSISTENT)
-        // (A/B: the r04 persistent grid, the resident workgroups only)
-        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((nt + wpb - 1) / wpb, (uint64_t)c.rb_blocks));
-#else
-        // kRowsTilesPerWave tiles per wave; the dispatcher refills each CU
+        // the odometer: kRowsTilesPerWave tiles per wave, the dispatcher
+        // refilling each CU; the other walks keep the persistent grid (the
+        // tree odometer's table -- 8.8 KB at the greedy + relax shape -- is
+        // staged once per workgroup: one tile per wave took 0.518 against
+        // 0.458 ms there, profiles/r05)
+        const bool persistent = walk != WALK_ODOMETER;
         const uint64_t per_wg = (uint64_t)wpb * kRowsTilesPerWave;
-        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((nt + per_wg - 1) / per_wg, 1ull << 30));
-#endif
+        const uint64_t g = persistent
+                               ? std::max<uint64_t>(1, std::min<uint64_t>((nt + wpb - 1) / wpb, (uint64_t)c.rb_blocks))
+                               : std::max<uint64_t>(1, std::min<uint64_t>((nt + per_wg - 1) / per_wg, 1ull << 30));
         hipLaunchKernelGGL(kfn, dim3((unsigned)g), dim3(threads), lds, s, p);
         MBRWT_HIP(hipGetLastError());
     }
