@@ -1387,6 +1387,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
             const uint32_t idx = (uint32_t)mine[o] | ((uint32_t)mine[o + 1] << 8) | ((uint32_t)mine[o + 2] << 16) |
                                  ((uint32_t)mine[o + 3] << 24);
             const uint64_t sa = p.spill + (uint64_t)idx * 16;
+            *(AS_LDS uint32_t *)(mine + B) = idx;  // (the slot's pad word: a long record's copy below)
 #pragma unroll
             for (uint32_t k = 0; k < LPB; ++k) sq[k] = gld_at<u32x4_t>(sa + 16u * k);
         }
@@ -1410,6 +1411,34 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
         // from global memory; so is a record longer than a block (its count
         // flagged with bit 15; its labels' places in the tile are kept)
         const bool direct = total > C;
+        // the lane's record in LDS: its block slot, or (r05) for a record
+        // longer than a block, a copy of its whole spill entry in the free tail
+        // of the wave's label stage (the tile's labels take its first 2 total
+        // bytes), so the odometers walk it here instead of k_compact_tiles
+        // walking it byte by byte from global memory (the greedy + relax
+        // shape: 0.13 % of rows, 8 % of tiles; its compaction took 266 us of
+        // a 0.76 ms step, profiles/r05)
+        const AS_LDS uint8_t *rec = mine;
+        if constexpr (WALK == WALK_ODOMETER || WALK == WALK_TREE_ODOMETER) {
+            if (!direct && __any(lng)) {
+                // each long row's entry (16-byte chunks) below the previous
+                // one's from the stage's end; all of them, or none
+                // (the entry's mask bytes and index from the lane's slot)
+                const uint32_t need = lng ? ((8u + *(const AS_LDS uint32_t *)(mine + 4) + 15u) & ~15u) : 0u;
+                const uint32_t incl = wave_incl_sum(need);
+                if (2u * total + __builtin_amdgcn_readlane(incl, 63) <= 2u * C) {
+                    AS_LDS uint8_t *stg = wb + 64u * PB + 256u * p.stk_words + 2u * C - incl;
+                    if (lng) {
+                        const uint64_t sa = p.spill + (uint64_t)*(const AS_LDS uint32_t *)(mine + B) * 16;
+#pragma unroll 1
+                        for (uint32_t b = 0; b < need; b += 16u) *(AS_LDS u32x4_t *)(stg + b) = gld_at<u32x4_t>(sa + b);
+                        rec = stg;  // masks from byte 8, as in a spilled row's slot
+                        lng = false;
+                    }
+                    wave_sync();
+                }
+            }
+        }
         const bool has_long = __any(lng);
         uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
 #if !defined(MBRWT_AB_NOSTORE)
@@ -1433,9 +1462,9 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
 #define MBRWT_TREE_CASE(K)                                                        \
     case K:                                                                       \
         if (p.mask1)                                                              \
-            rows_walk_tree<K, true>(mine, o, live, root, ent, lst, stage, pos);        \
+            rows_walk_tree<K, true>(rec, o, live, root, ent, lst, stage, pos);         \
         else                                                                      \
-            rows_walk_tree<K, false>(mine, o, live, root, ent, lst, stage, pos);       \
+            rows_walk_tree<K, false>(rec, o, live, root, ent, lst, stage, pos);        \
         break;
                     switch (p.frames) {
                         MBRWT_TREE_CASE(1)
@@ -1445,25 +1474,25 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
                         MBRWT_TREE_CASE(5)
                         MBRWT_TREE_CASE(6)
                         MBRWT_TREE_CASE(7)
-                        default: rows_walk_tree<8, false>(mine, o, live, root, ent, lst, stage, pos); break;
+                        default: rows_walk_tree<8, false>(rec, o, live, root, ent, lst, stage, pos); break;
                     }
 #undef MBRWT_TREE_CASE
                 } else if (ptw) {
                     const AS_LDS uint16_t *ptab = (const AS_LDS uint16_t *)((const AS_LDS uint32_t *)lds_rows + ptw + 1);
                     switch (p.uni) {
-                        case 1: rows_walk_path<1>(mine, o, live, ptab, pA, stage, pos); break;
-                        case 2: rows_walk_path<2>(mine, o, live, ptab, pA, stage, pos); break;
-                        case 3: rows_walk_path<3>(mine, o, live, ptab, pA, stage, pos); break;
-                        case 4: rows_walk_path<4>(mine, o, live, ptab, pA, stage, pos); break;
-                        default: rows_walk_path<5>(mine, o, live, ptab, pA, stage, pos); break;
+                        case 1: rows_walk_path<1>(rec, o, live, ptab, pA, stage, pos); break;
+                        case 2: rows_walk_path<2>(rec, o, live, ptab, pA, stage, pos); break;
+                        case 3: rows_walk_path<3>(rec, o, live, ptab, pA, stage, pos); break;
+                        case 4: rows_walk_path<4>(rec, o, live, ptab, pA, stage, pos); break;
+                        default: rows_walk_path<5>(rec, o, live, ptab, pA, stage, pos); break;
                     }
                 } else {
                     switch (p.uni) {
-                        case 1: rows_walk_uni<1>(mine, o, live, root, ent, stage, pos); break;
-                        case 2: rows_walk_uni<2>(mine, o, live, root, ent, stage, pos); break;
-                        case 3: rows_walk_uni<3>(mine, o, live, root, ent, stage, pos); break;
-                        case 4: rows_walk_uni<4>(mine, o, live, root, ent, stage, pos); break;
-                        default: rows_walk_uni<5>(mine, o, live, root, ent, stage, pos); break;
+                        case 1: rows_walk_uni<1>(rec, o, live, root, ent, stage, pos); break;
+                        case 2: rows_walk_uni<2>(rec, o, live, root, ent, stage, pos); break;
+                        case 3: rows_walk_uni<3>(rec, o, live, root, ent, stage, pos); break;
+                        case 4: rows_walk_uni<4>(rec, o, live, root, ent, stage, pos); break;
+                        default: rows_walk_uni<5>(rec, o, live, root, ent, stage, pos); break;
                     }
                 }
                 wave_sync();
