@@ -1026,6 +1026,20 @@ static int apply_option(Ctx &c, int option, int64_t value) {
     case MBRWT_OPT_KERNEL:
         if (!(value >= 0 && value <= 6) && value != 10 && !(value >= 17 && value <= 20) && !(value >= 24 && value <= 30))
             return MBRWT_ERR_INVALID;
+#if !defined(MBRWT_AB_VARIANTS)
+        // the release library dispatches the default families only: 0, and 1
+        // (the lane-per-row general kernel); the measured A/B variants are an
+        // A/B build (tools/ab_build.sh NAME -DMBRWT_AB_VARIANTS csrc/query.hip
+        // csrc/capi.cpp)
+        if (value > 1) {
+            set_error("kernel variant is an A/B build option (-DMBRWT_AB_VARIANTS)");
+            return MBRWT_ERR_UNSUPPORTED;
+        }
+#endif
+        if (value != 0 && c.nodes_freed) {  // (a variant would fail at query time)
+            set_error("kernel variants run on the node image: build with layout NODES or BOTH");
+            return MBRWT_ERR_UNSUPPORTED;
+        }
         c.kernel_variant = (int)value;
         return MBRWT_OK;
     default:

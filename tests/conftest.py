@@ -83,3 +83,16 @@ def build_env():
             opt, v = _build_option_of(name, value)
             stack.enter_context(build_option(opt, v))
         yield set_
+
+
+def kernel_variants(dev, variants):
+    """The MBRWT_OPT_KERNEL values of `variants` this library accepts on dev:
+    the release build dispatches 0 and 1 only (the measured A/B variants are
+    an A/B build, -DMBRWT_AB_VARIANTS); restores variant 0."""
+    from genome_graph_annotation_amd import _lib as L
+    ok = []
+    for v in variants:
+        if L.lib().mbrwt_set_option(dev._h, L.MBRWT_OPT_KERNEL, int(v)) == L.MBRWT_OK:
+            ok.append(v)
+    L.lib().mbrwt_set_option(dev._h, L.MBRWT_OPT_KERNEL, 0)
+    return ok

@@ -30,8 +30,9 @@ def _check_rows(oracle_tree, dev, rows, variants=(0, 1, 2, 4, 5, 10, 17, 18, 19,
     from genome_graph_annotation_amd import _lib as L
     if variants is None:
         variants = _check_rows.__defaults__[0]
+    from conftest import kernel_variants
     off_o, cols_o = oracle_tree.get_rows(rows)
-    for v in variants:
+    for v in kernel_variants(dev, variants):
         dev.set_option(L.MBRWT_OPT_KERNEL, v)
         off_d, cols_d = dev.get_rows(rows)
         np.testing.assert_array_equal(off_d, off_o)
@@ -222,7 +223,8 @@ def test_device_api_and_accounting(oracle_mod):
     np.testing.assert_array_equal(ot.cpu().numpy().view(np.uint64), off_o)
     np.testing.assert_array_equal(ct[:got].cpu().numpy().view(np.uint32), cols_o)
     from genome_graph_annotation_amd import _lib as L
-    for variant in (0, 1, 2, 4):
+    from conftest import kernel_variants
+    for variant in kernel_variants(d, (0, 1, 2, 4)):
         d.set_option(L.MBRWT_OPT_KERNEL, variant)
         # V and L accounting used by the roofline (DESIGN.md "Measurement")
         v, lab = d.count_work_device(rt, s.cuda_stream)

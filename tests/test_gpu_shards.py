@@ -45,7 +45,8 @@ def _check_all(O, t, dev, rng, n, m):
     rows = np.concatenate([np.arange(n), rng.integers(0, n, 3 * n), [n - 1, 0, n - 1]]).astype(np.uint64)
     rng.shuffle(rows)
     off_o, cols_o = t.get_rows(rows)
-    for v in (0, 1, 5, 10):
+    from conftest import kernel_variants
+    for v in kernel_variants(dev, (0, 1, 5, 10)):
         dev.set_option(L.MBRWT_OPT_KERNEL, v)
         off_d, cols_d = dev.get_rows(rows)
         np.testing.assert_array_equal(off_d, off_o)
