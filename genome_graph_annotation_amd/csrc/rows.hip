@@ -1134,7 +1134,13 @@ __device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_
             // the node at level k is child c of the level-(k-1) node: A_{k-1}
             // (the largest arity at level k-1) scales the parent's index
             const uint32_t Ak = k >= 2 ? (A >> (4 * (k - 2))) & 0xFu : 0u;  // (wave-uniform)
+            // (24-bit multiplies: v_mad_u32_u24 issues at full rate, the
+            // 32-bit v_mad_u64_u32 the compiler picks otherwise does not)
+#if defined(MBRWT_AB_MUL32)
             const uint32_t ni = k == 1 ? c : idx[k - 1] * Ak + c;
+#else
+            const uint32_t ni = k == 1 ? c : __umul24(idx[k - 1], Ak) + c;
+#endif
             idx[k] = nd[k] ? ni : idx[k];
             r[k - 1] = nd[k] ? (r[k - 1] & (r[k - 1] - 1u)) : r[k - 1];
             r[k] = nd[k] ? b : r[k];
@@ -1143,7 +1149,11 @@ __device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_
         const uint32_t c = (uint32_t)__builtin_ctz(r[K - 1]);
         r[K - 1] &= r[K - 1] - 1u;
         const uint32_t AK = K > 1 ? (A >> (4 * (K - 2))) & 0xFu : 0u;
-        const uint32_t base = ptab[K > 1 ? idx[K - 1] * AK + c : c];  // the leaf parent's first column
+#if defined(MBRWT_AB_MUL32)
+        const uint32_t base = ptab[K > 1 ? idx[K - 1] * AK + c : c];
+#else
+        const uint32_t base = ptab[K > 1 ? __umul24(idx[K - 1], AK) + c : c];  // the leaf parent's first column
+#endif
         uint32_t x = *rc;
         ++rc;
         *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));

@@ -573,7 +573,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(G >= 8
             // (r05: mask bytes read as words and labels stored in pairs halved
             // the LDS bank-conflict cycles, 218 M -> 108 M per 10 M rows, but
             // added 17 % VALU: 2.46 against 2.22 ms; profiles/r05/v06_*)
-            if (us)
+            if (us && !(us & (us - 1))) {  // (a shift: v_mul_lo_u32 issues at a quarter rate)
+                const uint32_t sh = (uint32_t)__builtin_ctz(us);
+                var_lane_labels(word_l, byte_l, wi, wv0, 4 * W + j0, labs, [&](uint32_t u) -> uint32_t { return u << sh; },
+                                [&](uint32_t k, uint32_t lab) { stage[pos + k] = (uint16_t)lab; });
+            } else if (us)
                 var_lane_labels(word_l, byte_l, wi, wv0, 4 * W + j0, labs, [&](uint32_t u) -> uint32_t { return u * us; },
                                 [&](uint32_t k, uint32_t lab) { stage[pos + k] = (uint16_t)lab; });
             else
