@@ -36,6 +36,7 @@ MBRWT_BUILD_ROWS_RANGE = 7
 MBRWT_BUILD_NODE_KINDS = 8
 MBRWT_BUILD_SHARD_ROWS = 9
 MBRWT_BUILD_ROWS_WGS_PER_CU = 10
+MBRWT_BUILD_ROWS_CLASSES = 11
 MBRWT_KIND_FOLD_ROOT = 1
 MBRWT_KIND_PACK = 2
 MBRWT_KIND_PACK2 = 4
@@ -164,6 +165,7 @@ SIGNATURES = {
                                               C.c_uint64, u64p, C.c_void_p]),
     "mbrwt_layout": (C.c_int, [C.c_void_p]),
     "mbrwt_rows_stats": (C.c_int, [C.c_void_p, u64p]),
+    "mbrwt_rows_classes": (C.c_int, [C.c_void_p, u64p]),
     "mbrwt_tree_parse": (C.c_int, [u8p, C.c_uint64, u64p, C.POINTER(C.c_void_p)]),
     "mbrwt_tree_serialize": (C.c_int, [C.POINTER(TreeDesc), u8p, C.c_uint64, u64p]),
     "mbrwt_tree_export": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),

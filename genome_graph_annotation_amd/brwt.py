@@ -313,6 +313,10 @@ class BRWTDevice:
         d["uniform_levels"] = d["height"] >> 32  # odometer walk when > 0
         d["variable"] = d["block_bytes"] == 0  # variable-length records (csrc/rows_var.hip)
         d["height"] &= 0xFFFFFFFF
+        cl = (C.c_uint64 * 4)()
+        if L.lib().mbrwt_rows_classes(self._h, cl) == L.MBRWT_OK:
+            # record classes (csrc/rows_class.hip): 0 = none
+            d["classes"], d["class_bits"], d["class_index_bytes"], d["class_sample_distinct"] = (int(v) for v in cl)
         return d
 
     # -- host-buffer queries --------------------------------------------------

@@ -707,6 +707,11 @@ int export_rows(const Ctx &c, mbrwt_tree &out) {
     std::vector<uint8_t> spill;
     int rc;
     if ((rc = copy_down((uint64_t)(uintptr_t)im.spill, im.spill_bytes, spill))) return rc;
+    std::vector<uint8_t> dict, cidx;  // record classes: the dictionary blocks and the class index
+    if (im.classes) {
+        if ((rc = copy_down((uint64_t)(uintptr_t)im.blocks, im.num_blocks * im.B, dict))) return rc;
+        if ((rc = copy_down((uint64_t)(uintptr_t)im.classes, im.class_index_bytes, cidx))) return rc;
+    }
     const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     const uint64_t T = R < (1ull << 20) ? 1 : std::min<uint64_t>(hw, (R + (1ull << 20) - 1) >> 20);
     // thread k: rows [a_k, a_{k+1}), block-aligned
@@ -723,6 +728,60 @@ int export_rows(const Ctx &c, mbrwt_tree &out) {
             uint32_t rem;  // children still to visit
         };
         std::vector<Frame> st;
+        // one row's record (entry tt of block bp) -> its bits of every index column
+        auto row_bits = [&](const uint8_t *bp, uint32_t tt) -> bool {
+            const uint32_t e = bp[tt], o = e & 0x7Fu;
+            const uint8_t *rec;
+            uint32_t count;
+            if (e & 0x80u) {
+                uint32_t idx = 0;
+                std::memcpy(&idx, bp + o + 1, 4);
+                if ((uint64_t)idx * 16 + 8 > spill.size()) return false;
+                std::memcpy(&count, &spill[(uint64_t)idx * 16], 4);
+                rec = &spill[(uint64_t)idx * 16 + 8];
+            } else {
+                count = bp[o];
+                rec = bp + o + 1;
+            }
+            cols[1].push(count ? 1u : 0u);
+            if (!count) return true;
+            uint32_t pos = 0;
+            auto visit = [&](uint32_t v) {  // v reached: read its mask, append its children's bits
+                const DevNode &dn = t.nodes[v];
+                uint32_t m = rec[pos++];
+                if (dn.arity > 8) m |= (uint32_t)rec[pos++] << 8;
+                for (uint32_t ch = 0; ch < dn.arity; ++ch) cols[dn.first_child + ch].push((m >> ch) & 1u);
+                st.push_back(Frame{dn.first_child, m});
+            };
+            st.clear();
+            visit(rootd);
+            while (!st.empty()) {
+                Frame &f = st.back();
+                if (!f.rem) {
+                    st.pop_back();
+                    continue;
+                }
+                const uint32_t ch = (uint32_t)__builtin_ctz(f.rem);
+                f.rem &= f.rem - 1;
+                const uint32_t w = f.fc + ch;
+                if (t.nodes[w].kind != KIND_LEAF) visit(w);
+            }
+            return true;
+        };
+        if (im.classes) {  // record classes: row r's record is block class(r) of the dictionary
+            const uint32_t w = im.class_bits;
+            for (uint64_t r = cut[k]; r < cut[k + 1]; ++r) {
+                const uint64_t bit = r * w;
+                uint64_t x = 0;
+                std::memcpy(&x, &cidx[(bit >> 5) * 4], 8);
+                const uint64_t cls = (x >> (bit & 31)) & ((1ull << w) - 1);
+                if (cls >= im.num_classes || !row_bits(&dict[cls * im.B], 0)) {
+                    prc[k] = MBRWT_ERR_INVALID;
+                    return;
+                }
+            }
+            return;
+        }
         const uint64_t chunk_blocks = std::max<uint64_t>(1, (64ull << 20) / im.B);
         for (uint64_t b0 = cut[k] / im.S; b0 * im.S < cut[k + 1]; b0 += chunk_blocks) {
             const uint64_t b1 = std::min<uint64_t>((cut[k + 1] + im.S - 1) / im.S, b0 + chunk_blocks);
@@ -736,44 +795,9 @@ int export_rows(const Ctx &c, mbrwt_tree &out) {
                 for (uint32_t tt = 0; tt < im.S; ++tt) {
                     const uint64_t r = b * im.S + tt;
                     if (r >= cut[k + 1]) break;
-                    const uint32_t e = bp[tt], o = e & 0x7Fu;
-                    const uint8_t *rec;
-                    uint32_t count;
-                    if (e & 0x80u) {
-                        uint32_t idx = 0;
-                        std::memcpy(&idx, bp + o + 1, 4);
-                        if ((uint64_t)idx * 16 + 8 > spill.size()) {
-                            prc[k] = MBRWT_ERR_INVALID;
-                            return;
-                        }
-                        std::memcpy(&count, &spill[(uint64_t)idx * 16], 4);
-                        rec = &spill[(uint64_t)idx * 16 + 8];
-                    } else {
-                        count = bp[o];
-                        rec = bp + o + 1;
-                    }
-                    cols[1].push(count ? 1u : 0u);
-                    if (!count) continue;
-                    uint32_t pos = 0;
-                    auto visit = [&](uint32_t v) {  // v reached: read its mask, append its children's bits
-                        const DevNode &dn = t.nodes[v];
-                        uint32_t m = rec[pos++];
-                        if (dn.arity > 8) m |= (uint32_t)rec[pos++] << 8;
-                        for (uint32_t ch = 0; ch < dn.arity; ++ch) cols[dn.first_child + ch].push((m >> ch) & 1u);
-                        st.push_back(Frame{dn.first_child, m});
-                    };
-                    st.clear();
-                    visit(rootd);
-                    while (!st.empty()) {
-                        Frame &f = st.back();
-                        if (!f.rem) {
-                            st.pop_back();
-                            continue;
-                        }
-                        const uint32_t ch = (uint32_t)__builtin_ctz(f.rem);
-                        f.rem &= f.rem - 1;
-                        const uint32_t w = f.fc + ch;
-                        if (t.nodes[w].kind != KIND_LEAF) visit(w);
+                    if (!row_bits(bp, tt)) {
+                        prc[k] = MBRWT_ERR_INVALID;
+                        return;
                     }
                 }
             }

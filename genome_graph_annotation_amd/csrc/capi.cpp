@@ -98,7 +98,7 @@ static void release(Ctx *c) {
         if (c->d_col_leaf) (void)hipFree(c->d_col_leaf);
     }
     for (Workspace *w : {&c->ws_temp, &c->ws_counts, &c->ws_ovf, &c->ws_scan, &c->ws_rows, &c->ws_out, &c->ws_sort,
-                         &c->ws_cls_off, &c->ws_cls_cols, &c->ws_sh_keys, &c->ws_sh_local, &c->ws_sh_cnt,
+                         &c->ws_cls_off, &c->ws_cls_cols, &c->ws_class, &c->ws_sh_keys, &c->ws_sh_local, &c->ws_sh_cnt,
                          &c->ws_sh_sort, &c->ws_sh_tmp})
         if (w->buf) (void)hipFree(w->buf);
     free_host_pipe(c->pipe);
@@ -634,10 +634,14 @@ int mbrwt_set_build_option(int option, int64_t value) {
         if (value < 0 || value > 32) break;
         t.rows_wgs_per_cu = (uint32_t)value;
         return MBRWT_OK;
+    case MBRWT_BUILD_ROWS_CLASSES:
+        if (value < -1 || value > 1) break;
+        t.rows_classes = (int)value;
+        return MBRWT_OK;
     default:
         break;
     }
-    if (option >= MBRWT_BUILD_ROWS_VAR && option <= MBRWT_BUILD_ROWS_WGS_PER_CU) {
+    if (option >= MBRWT_BUILD_ROWS_VAR && option <= MBRWT_BUILD_ROWS_CLASSES) {
         set_error("build option value out of range");
         return MBRWT_ERR_INVALID;
     }
@@ -659,7 +663,7 @@ int mbrwt_set_build_option(int option, int64_t value) {
 }
 
 int mbrwt_get_build_option(int option, int64_t *value) {
-    if (!value || option < MBRWT_BUILD_LAYOUT || option > MBRWT_BUILD_ROWS_WGS_PER_CU) {
+    if (!value || option < MBRWT_BUILD_LAYOUT || option > MBRWT_BUILD_ROWS_CLASSES) {
         set_error("unknown build option or null output");
         return MBRWT_ERR_INVALID;
     }
@@ -674,7 +678,8 @@ int mbrwt_get_build_option(int option, int64_t *value) {
     case MBRWT_BUILD_ROWS_RANGE: *value = (int64_t)t.rows_range; break;
     case MBRWT_BUILD_NODE_KINDS: *value = t.node_kinds; break;
     case MBRWT_BUILD_SHARD_ROWS: *value = (int64_t)t.shard_rows; break;
-    default: *value = t.rows_wgs_per_cu; break;
+    case MBRWT_BUILD_ROWS_WGS_PER_CU: *value = t.rows_wgs_per_cu; break;
+    default: *value = t.rows_classes; break;
     }
     return MBRWT_OK;
 }
@@ -700,6 +705,19 @@ int mbrwt_rows_stats(const mbrwt_ctx *ctx, uint64_t out[8]) {
     out[5] = r.spilled_rows;
     out[6] = r.long_rows;
     out[7] = r.height | (uint64_t)r.uni << 32;
+    return MBRWT_OK;
+}
+int mbrwt_rows_classes(const mbrwt_ctx *ctx, uint64_t out[4]) {
+    if (!ctx || !out) return MBRWT_ERR_INVALID;
+    const RowsImage &r = C(ctx)->rows;
+    if (!r.ready) {
+        set_error("context has no row records");
+        return MBRWT_ERR_UNSUPPORTED;
+    }
+    out[0] = r.num_classes;
+    out[1] = r.class_bits;
+    out[2] = r.class_index_bytes;
+    out[3] = r.class_sample_distinct;
     return MBRWT_OK;
 }
 int mbrwt_device(const mbrwt_ctx *ctx) { return ctx ? C(ctx)->device : -1; }

@@ -278,6 +278,12 @@ struct RowsImage {
     uint32_t *d_var_units = nullptr, *d_var_anc = nullptr;
     uint16_t *d_unit_of = nullptr;
     uint64_t var_rec_bytes = 0;
+    // RECORD CLASSES (rows_class.hip; block layout only): the blocks hold one
+    // record per distinct record (S = 1) and classes[] maps row r to its
+    // record, class_bits bits per row packed LSB-first in u32 words
+    uint32_t *classes = nullptr;
+    uint32_t class_bits = 0;
+    uint64_t num_classes = 0, class_index_bytes = 0, class_sample_distinct = 0;
     // build statistics
     uint64_t spilled_rows = 0, long_rows = 0, record_bytes = 0, spill_bytes = 0;
 };
@@ -352,6 +358,7 @@ struct Ctx {
     // once warmed up)
     Workspace ws_temp, ws_counts, ws_ovf, ws_scan, ws_rows, ws_out, ws_sort;
     Workspace ws_cls_off, ws_cls_cols;  // get_labels batch: the rows' CSR
+    Workspace ws_class;                 // record classes: the batch's classes (rows_class.hip)
     uint64_t *h_scalars = nullptr;      // pinned: [0] total, [1] overflow count, [2] error
     uint64_t *d_scalars = nullptr;      // device twin
     HostPipe *pipe = nullptr;           // streams, slots and staging of mbrwt_get_rows (lazily created)
@@ -425,6 +432,13 @@ int rows_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_co
 int rows_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s);
 int rows_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap, uint64_t *rows_needed,
                     hipStream_t s);
+// record classes (rows_class.hip): build them over a finished block image of
+// n rows (mode -1 auto, 0 never, 1 whenever exact and room), map a batch's
+// rows to their classes (into ws_class), get_column over the classes
+int rows_classes_build(RowsImage &im, uint64_t n, int mode, uint64_t *sample_distinct, hipStream_t s);
+int rows_class_map(Ctx &c, const uint64_t *d_rows, uint64_t n, const uint64_t **mapped, hipStream_t s);
+int rows_class_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap, uint64_t *rows_needed,
+                          hipStream_t s);
 // variable-length records (rows_var.hip)
 struct VarScratch {
     Workspace units, cnt, off, acc, scan;
@@ -513,7 +527,7 @@ void build_p2w_table(Tree &tree);
 void build_ptw_table(Tree &tree);
 
 // the calling thread's tuning / test build options (include/mbrwt.h
-// MBRWT_BUILD_ROWS_VAR .. MBRWT_BUILD_ROWS_WGS_PER_CU; every default automatic)
+// MBRWT_BUILD_ROWS_VAR .. MBRWT_BUILD_ROWS_CLASSES; every default automatic)
 struct BuildTuning {
     int rows_var = -1;           // -1 auto, 0 never, 1 always
     uint32_t var_lanes = 0;      // 0 auto
@@ -522,6 +536,7 @@ struct BuildTuning {
     uint32_t node_kinds = 15;    // MBRWT_KIND_* bits
     uint64_t shard_rows = 0;     // 0: the default shard size
     uint32_t rows_wgs_per_cu = 0;
+    int rows_classes = -1;       // record classes: -1 auto, 0 never, 1 whenever exact
 };
 BuildTuning &build_tuning();
 void set_build_tuning(const BuildTuning &t);

@@ -40,6 +40,7 @@
 #include "mbrwt_internal.hpp"
 #include "pack_block.hpp"
 #include "rows_emit.hpp"
+#include "rows_record.hpp"
 #include "wave_scan.hpp"
 
 namespace mbrwt {
@@ -470,6 +471,7 @@ void free_rows(RowsImage &r) {
     if (r.d_spill_used) (void)hipFree(r.d_spill_used);
     if (r.d_table) (void)hipFree(r.d_table);
     if (r.d_table2) (void)hipFree(r.d_table2);
+    if (r.classes) (void)hipFree(r.classes);
     r = RowsImage();
 }
 
@@ -762,6 +764,13 @@ int rows_build_finish(RowsBuild *rbp) {
         }
         im.bytes = im.num_blocks * im.B + im.spill_bytes;
     }
+    if (!im.var) {  // record classes where rows repeat few distinct records (rows_class.hip)
+        rc = rows_classes_build(im, rb.n, build_tuning().rows_classes, &im.class_sample_distinct, rb.s);
+        if (rc) {
+            rows_build_abort(rbp);
+            return rc;
+        }
+    }
     im.occ_cap = build_tuning().rows_wgs_per_cu;  // (MBRWT_BUILD_ROWS_WGS_PER_CU: occupancy sweeps)
     im.ready = true;
     free_rows(rb.top->rows);
@@ -779,78 +788,6 @@ int rows_build_finish(RowsBuild *rbp) {
 // queries
 // ------------------------------------------------------------------------
 namespace {
-
-struct RowsView {
-    uint64_t blocks, spill, magic, num_rows;
-    uint32_t B, S;
-};
-__device__ __forceinline__ uint64_t rows_block(uint64_t r, uint32_t S, uint64_t magic) {
-    return S == 1 ? r : __umul64hi(r, magic);
-}
-// the record of row r (< num_rows): address of its first mask byte, label count
-__device__ __forceinline__ void rows_locate(const RowsView &v, uint64_t r, uint64_t &masks, uint32_t &count) {
-    const uint64_t b = rows_block(r, v.S, v.magic);
-    const uint32_t t = (uint32_t)(r - b * v.S);
-    const uint64_t blk = v.blocks + b * v.B;
-    const uint32_t e = gld_at<uint8_t>(blk + t);
-    const uint32_t o = e & 0x7Fu;
-    if (e & 0x80u) {
-        uint32_t idx = 0;
-        for (uint32_t k = 0; k < 4; ++k) idx |= (uint32_t)gld_at<uint8_t>(blk + o + 1 + k) << (8 * k);
-        const uint64_t se = v.spill + (uint64_t)idx * 16;
-        count = gld_at<uint32_t>(se);
-        masks = se + 8;
-    } else {
-        count = gld_at<uint8_t>(blk + o);
-        masks = blk + o + 1;
-    }
-}
-
-// DFS walk of a record (masks from byte 0 of `byte`) over the RWT table:
-// leaf(column) per set leaf in pre-order (BRWT.cpp:45-51), inner(arity) per
-// mask read (the root's included).  One lane; false past kRowsMaxHeight.
-template <class ByteFn, class LeafFn, class InnerFn>
-__device__ bool rwt_walk(const uint32_t *ntab, const uint16_t *etab, ByteFn byte, LeafFn leaf, InnerFn inner) {
-    uint32_t o = 0;
-    uint32_t nw = ntab[0];
-    uint32_t a = (nw >> 16) & 0xFFu;
-    uint32_t m = byte(o++);
-    if (a > 8) m |= byte(o++) << 8;
-    inner(a);
-    uint32_t first = nw & 0xFFFFu;
-    uint32_t sf[kRowsMaxHeight], sm[kRowsMaxHeight];
-    int sp = 0;
-    while (true) {
-        if (!m) {
-            if (!sp) break;
-            --sp;
-            first = sf[sp];
-            m = sm[sp];
-            continue;
-        }
-        const uint32_t c = (uint32_t)__builtin_ctz(m);
-        m &= m - 1;
-        const uint32_t e = etab[first + c];
-        if (e & 0x8000u) {
-            leaf(e & 0x7FFFu);
-            continue;
-        }
-        nw = ntab[e];
-        a = (nw >> 16) & 0xFFu;
-        uint32_t mw = byte(o++);
-        if (a > 8) mw |= byte(o++) << 8;
-        inner(a);
-        if (m) {
-            if (sp == (int)kRowsMaxHeight) return false;
-            sf[sp] = first;
-            sm[sp] = m;
-            ++sp;
-        }
-        first = nw & 0xFFFFu;
-        m = mw;
-    }
-    return true;
-}
 
 // rwt_walk with its pending frames {first entry | mask << 16} in a per-lane
 // LDS stack (stk[64 k], k < lim <= kRowsMaxHeight: the tree's height) instead
@@ -1776,7 +1713,7 @@ RowsView view_of(const Ctx &c) {
     v.blocks = (uint64_t)(uintptr_t)c.rows.blocks;
     v.spill = (uint64_t)(uintptr_t)c.rows.spill;
     v.magic = c.rows.magic;
-    v.num_rows = c.tree.num_rows;
+    v.num_rows = c.rows.classes ? c.rows.num_classes : c.tree.num_rows;  // (classes: the dictionary's records)
     v.B = c.rows.B;
     v.S = c.rows.S;
     return v;
@@ -1863,6 +1800,11 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         return MBRWT_ERR_UNSUPPORTED;
     }
     int rc;
+    if (im.classes) {  // record classes: the batch's classes are the dictionary's rows
+        const uint64_t *mapped = nullptr;
+        if ((rc = rows_class_map(c, d_rows, n, &mapped, s))) return rc;
+        d_rows = mapped;
+    }
     const uint32_t C = rows_tile_labels(c);
     const uint64_t nt = (n + 63) / 64;
     const uint64_t region = 128 + 2ull * C;
@@ -1893,7 +1835,7 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     RowsParams p{};
     p.rows = d_rows;
     p.n = n;
-    p.num_rows = c.tree.num_rows;
+    p.num_rows = im.classes ? im.num_classes : c.tree.num_rows;
     p.blocks = (uint64_t)(uintptr_t)im.blocks;
     p.spill = (uint64_t)(uintptr_t)im.spill;
     p.magic = im.magic;
@@ -2050,6 +1992,8 @@ static uint64_t simple_grid(uint64_t n) { return std::max<uint64_t>(1, std::min<
 int rows_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint64_t n, uint8_t *d_out, hipStream_t s) {
     if (n == 0) return MBRWT_OK;
     if (c.rows.var) return var_get_batch(c, d_rows, d_cols, n, d_out, s);
+    if (c.rows.classes)
+        if (int rc = rows_class_map(c, d_rows, n, &d_rows, s)) return rc;
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
     hipLaunchKernelGGL(k_rows_get, dim3((unsigned)simple_grid(n)), dim3(256), 0, s, view_of(c),
                        (const uint32_t *)c.rows.d_table, d_rows, d_cols, n, c.tree.num_columns, d_out,
@@ -2062,6 +2006,8 @@ int rows_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint6
 
 int rows_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_counts, hipStream_t s) {
     if (c.rows.var) return var_count(c, d_rows, n, d_counts, nullptr, nullptr, s);
+    if (c.rows.classes)
+        if (int rc = rows_class_map(c, d_rows, n, &d_rows, s)) return rc;
     if (c.tree.num_columns) MBRWT_HIP(hipMemsetAsync(d_counts, 0, c.tree.num_columns * sizeof(uint64_t), s));
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
     if (n)
@@ -2076,6 +2022,8 @@ int rows_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_co
 
 int rows_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s) {
     if (c.rows.var) return var_count(c, d_rows, n, nullptr, visits, labels, s);
+    if (c.rows.classes)
+        if (int rc = rows_class_map(c, d_rows, n, &d_rows, s)) return rc;
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
     if (n)
         hipLaunchKernelGGL(k_rows_count<true>, dim3((unsigned)simple_grid(n)), dim3(256), 0, s, view_of(c),
@@ -2097,6 +2045,7 @@ int rows_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap
         set_error("column out of range");
         return MBRWT_ERR_RANGE;
     }
+    if (c.rows.classes) return rows_class_get_column(c, column, d_rows, rows_cap, rows_needed, s);
     const uint64_t n = c.tree.num_rows;
     const RowHasColumn f{view_of(c), c.rows.d_table, (uint32_t)column};
     hipcub::CountingInputIterator<uint64_t> rows_it(0);

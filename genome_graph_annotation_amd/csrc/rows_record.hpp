@@ -1,0 +1,88 @@
+// rows_record.hpp -- reading one row record of the block layout (rows.hip):
+// the block / spill addressing and the single-lane DFS walk of a record over
+// the RWT table.  Shared by the row-record kernels (rows.hip) and the record
+// classes (rows_class.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device_access.hpp"
+#include "mbrwt_internal.hpp"
+
+namespace mbrwt {
+
+struct RowsView {
+    uint64_t blocks, spill, magic, num_rows;
+    uint32_t B, S;
+};
+__device__ __forceinline__ uint64_t rows_block(uint64_t r, uint32_t S, uint64_t magic) {
+    return S == 1 ? r : __umul64hi(r, magic);
+}
+// the record of row r (< num_rows): address of its first mask byte, label count
+__device__ __forceinline__ void rows_locate(const RowsView &v, uint64_t r, uint64_t &masks, uint32_t &count) {
+    const uint64_t b = rows_block(r, v.S, v.magic);
+    const uint32_t t = (uint32_t)(r - b * v.S);
+    const uint64_t blk = v.blocks + b * v.B;
+    const uint32_t e = gld_at<uint8_t>(blk + t);
+    const uint32_t o = e & 0x7Fu;
+    if (e & 0x80u) {
+        uint32_t idx = 0;
+        for (uint32_t k = 0; k < 4; ++k) idx |= (uint32_t)gld_at<uint8_t>(blk + o + 1 + k) << (8 * k);
+        const uint64_t se = v.spill + (uint64_t)idx * 16;
+        count = gld_at<uint32_t>(se);
+        masks = se + 8;
+    } else {
+        count = gld_at<uint8_t>(blk + o);
+        masks = blk + o + 1;
+    }
+}
+
+// DFS walk of a record (masks from byte 0 of `byte`) over the RWT table:
+// leaf(column) per set leaf in pre-order (BRWT.cpp:45-51), inner(arity) per
+// mask read (the root's included).  One lane; false past kRowsMaxHeight.
+template <class ByteFn, class LeafFn, class InnerFn>
+__device__ bool rwt_walk(const uint32_t *ntab, const uint16_t *etab, ByteFn byte, LeafFn leaf, InnerFn inner) {
+    uint32_t o = 0;
+    uint32_t nw = ntab[0];
+    uint32_t a = (nw >> 16) & 0xFFu;
+    uint32_t m = byte(o++);
+    if (a > 8) m |= byte(o++) << 8;
+    inner(a);
+    uint32_t first = nw & 0xFFFFu;
+    uint32_t sf[kRowsMaxHeight], sm[kRowsMaxHeight];
+    int sp = 0;
+    while (true) {
+        if (!m) {
+            if (!sp) break;
+            --sp;
+            first = sf[sp];
+            m = sm[sp];
+            continue;
+        }
+        const uint32_t c = (uint32_t)__builtin_ctz(m);
+        m &= m - 1;
+        const uint32_t e = etab[first + c];
+        if (e & 0x8000u) {
+            leaf(e & 0x7FFFu);
+            continue;
+        }
+        nw = ntab[e];
+        a = (nw >> 16) & 0xFFu;
+        uint32_t mw = byte(o++);
+        if (a > 8) mw |= byte(o++) << 8;
+        inner(a);
+        if (m) {
+            if (sp == (int)kRowsMaxHeight) return false;
+            sf[sp] = first;
+            sm[sp] = m;
+            ++sp;
+        }
+        first = nw & 0xFFFFu;
+        m = mw;
+    }
+    return true;
+}
+
+}  // namespace mbrwt

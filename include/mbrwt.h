@@ -227,7 +227,17 @@ int mbrwt_ctx_clone(mbrwt_ctx *src, mbrwt_ctx **out);
    MBRWT_BUILD_SHARD_ROWS     rows per row shard (0: 2^31; small values force
                               shards on small trees -- a test hook)
    MBRWT_BUILD_ROWS_WGS_PER_CU  resident workgroups per CU of the row-record
-                              traversal (0 auto; occupancy sweeps) */
+                              traversal (0 auto; occupancy sweeps)
+   MBRWT_BUILD_ROWS_CLASSES   RECORD CLASSES of the block layout:
+                              one copy of every distinct row record plus a
+                              class index of ceil(log2 classes) bits per row,
+                              for data whose rows repeat few label sets.
+                              -1 auto (default: built when a tenth of a
+                              2^20-row sample repeats a record, kept when
+                              there are at most half as many classes as rows
+                              and they at least halve the image), 0 never,
+                              1 whenever they fit (always exact: every row's
+                              record is compared with its class's) */
 #define MBRWT_BUILD_ROWS_VAR 4
 #define MBRWT_BUILD_VAR_LANES 5
 #define MBRWT_BUILD_ROWS_BLOCK 6
@@ -235,6 +245,7 @@ int mbrwt_ctx_clone(mbrwt_ctx *src, mbrwt_ctx **out);
 #define MBRWT_BUILD_NODE_KINDS 8
 #define MBRWT_BUILD_SHARD_ROWS 9
 #define MBRWT_BUILD_ROWS_WGS_PER_CU 10
+#define MBRWT_BUILD_ROWS_CLASSES 11
 #define MBRWT_KIND_FOLD_ROOT 1
 #define MBRWT_KIND_PACK 2
 #define MBRWT_KIND_PACK2 4
@@ -254,6 +265,12 @@ int mbrwt_layout(const mbrwt_ctx *ctx); /* MBRWT_LAYOUT_NODES / _ROWS / _BOTH of
    odometer walk of csrc/rows.hip), else 0.  MBRWT_ERR_UNSUPPORTED without
    row records. */
 int mbrwt_rows_stats(const mbrwt_ctx *ctx, uint64_t out[8]);
+/* Record classes of a row-record image: out[0] classes (0: none -- then the
+   blocks hold one record per row), [1] class index bits per row, [2] class
+   index bytes, [3] distinct records in the layout-AUTO sample (0: not
+   sampled).  With classes, mbrwt_rows_stats describes the dictionary (one
+   record per class, S = 1).  MBRWT_ERR_UNSUPPORTED without row records. */
+int mbrwt_rows_classes(const mbrwt_ctx *ctx, uint64_t out[4]);
 
 /* ---- multi-device (one process, N GPUs) --------------------------------
  * A replica of the tree on every device of `devices` (n entries; a device
