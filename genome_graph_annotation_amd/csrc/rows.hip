@@ -855,6 +855,8 @@ struct RowsParams {
     uint32_t stk_words;           // per-lane LDS stack slots (general walks)
     uint32_t frames;              // the tree odometer: internal levels on the longest path (1..kRowsOdoLevels)
     uint32_t mask1;               // every mask one byte
+    const uint32_t *classes;      // record classes: the packed class index (null: none; rows_class.hip)
+    uint32_t class_bits;
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -1294,8 +1296,12 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
         if (tn < ntiles && tn * 64 + lane < p.n) row_n = gld(p.rows + tn * 64 + lane);
         const bool valid = lane < nr && row < p.num_rows;
         if (lane < nr && !valid) atomicOr(&p.scalars[2], 1ull);
-        const uint64_t b = block_of(row, valid);
-        const uint32_t sub = (uint32_t)(row - b * S);
+        // record classes: the row's class is its record's row in the
+        // dictionary (S = 1); the class index is the random HBM read, the
+        // dictionary's blocks mostly cache hits
+        const uint64_t rec_row = (p.classes && valid) ? class_field(p.classes, p.class_bits, row) : row;
+        const uint64_t b = block_of(rec_row, valid);
+        const uint32_t sub = (uint32_t)(rec_row - b * S);
         issue_blocks(addr_of(b), q);
 #if defined(MBRWT_AB_GATHER)
         // (timing only: the block loads into registers, no LDS, nothing else)
@@ -1504,6 +1510,8 @@ struct CompactParams {
     unsigned long long *scalars;  // the traversal's counters ([2] error flags)
     unsigned long long *status;   // {total, status, sticky}
     const uint64_t *rows;         // the batch (direct tiles)
+    const uint32_t *classes;      // record classes (null: none)
+    uint32_t class_bits;
     RowsView v;
     const uint32_t *table;        // RWT (direct tiles)
     uint32_t stk_lim;             // walk stack frames (the tree's height; dynamic LDS)
@@ -1593,7 +1601,8 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
         const uint32_t nr = (uint32_t)(n - r0 < 64 ? n - r0 : 64);
         const bool walk = (tc[k] >> 31) ? (cnt[k] & 0x7FFFu) != 0 : (cnt[k] >> 15) != 0;
         if (lane < nr && walk) {
-            const uint64_t row = gld(p.rows + r0 + lane);
+            uint64_t row = gld(p.rows + r0 + lane);
+            if (p.classes) row = class_field(p.classes, p.class_bits, row);
             uint64_t masks;
             uint32_t count;
             rows_locate(p.v, row, masks, count);  // (count = cnt: rows out of range have none)
@@ -1800,11 +1809,6 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         return MBRWT_ERR_UNSUPPORTED;
     }
     int rc;
-    if (im.classes) {  // record classes: the batch's classes are the dictionary's rows
-        const uint64_t *mapped = nullptr;
-        if ((rc = rows_class_map(c, d_rows, n, &mapped, s))) return rc;
-        d_rows = mapped;
-    }
     const uint32_t C = rows_tile_labels(c);
     const uint64_t nt = (n + 63) / 64;
     const uint64_t region = 128 + 2ull * C;
@@ -1835,7 +1839,9 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     RowsParams p{};
     p.rows = d_rows;
     p.n = n;
-    p.num_rows = im.classes ? im.num_classes : c.tree.num_rows;
+    p.num_rows = c.tree.num_rows;  // (record classes: mapped inside the traversal)
+    p.classes = im.classes;
+    p.class_bits = im.class_bits;
     p.blocks = (uint64_t)(uintptr_t)im.blocks;
     p.spill = (uint64_t)(uintptr_t)im.spill;
     p.magic = im.magic;
@@ -1930,6 +1936,8 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         cp.scalars = d_sc;
         cp.status = st_blk;
         cp.rows = d_rows;
+        cp.classes = im.classes;
+        cp.class_bits = im.class_bits;
         cp.v = view_of(c);
         cp.table = im.d_table;
         const uint64_t waves = (nt + kCompactTpw - 1) / kCompactTpw;

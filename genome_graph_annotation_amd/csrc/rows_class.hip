@@ -186,13 +186,6 @@ __global__ __launch_bounds__(256) void k_class_write(RowsView v, const uint32_t 
     }
 }
 
-__device__ __forceinline__ uint64_t class_field(const uint32_t *index, uint32_t w, uint64_t r) {
-    const uint64_t bit = r * w;
-    const uint64_t word = bit >> 5;
-    const uint64_t x = (uint64_t)gld(index + word) | (uint64_t)gld(index + word + 1) << 32;
-    return (x >> (bit & 31)) & ((1ull << w) - 1);
-}
-
 // the batch's row ids -> their classes (rows out of range -> D, which the
 // dictionary kernels report as out of range)
 __global__ __launch_bounds__(256) void k_class_map(const uint64_t *rows, uint64_t n, uint64_t num_rows,

@@ -85,4 +85,13 @@ __device__ bool rwt_walk(const uint32_t *ntab, const uint16_t *etab, ByteFn byte
     return true;
 }
 
+// record classes (rows_class.hip): row r's class, bits [r w, r w + w) of the
+// packed index (one dword-aligned 8-byte load; the index has a pad word)
+__device__ __forceinline__ uint64_t class_field(const uint32_t *index, uint32_t w, uint64_t r) {
+    typedef uint64_t u64a4 __attribute__((aligned(4)));
+    const uint64_t bit = r * w;
+    const uint64_t x = *(const AS_GLOBAL u64a4 *)(uintptr_t)(index + (bit >> 5));
+    return (x >> (bit & 31)) & ((1ull << w) - 1);
+}
+
 }  // namespace mbrwt

@@ -123,7 +123,7 @@ def uniform_columns(n, m, d, unique, seed):
     freq = m // unique
     src = np.repeat(np.arange(unique), freq)
     src = src[torch.randperm(len(src), generator=torch.Generator().manual_seed(seed)).numpy()]
-    return [gen[s] for s in src], unique * freq
+    return [gen[s] for s in src], n
 
 
 def weighted_freqs(n, unique):
