@@ -166,7 +166,7 @@ static int clone_ctx(Ctx *src, Ctx **out) {
 
 static int make_rows(Ctx &c, int layout);
 // The layout a create call builds: NODES, ROWS or BOTH as set for the thread
-// (mbrwt_set_build_option / MBRWT_LAYOUT), else AUTO -- row records when the
+// (mbrwt_set_build_option), else AUTO -- row records when the
 // tree is within their limits and the image fits the device, the per-node
 // images otherwise (make_rows, create_rows_ranged).
 static int resolve_layout() { return build_layout(); }
@@ -299,7 +299,7 @@ static int make_rows(Ctx &c, int layout) {
 // ONE range's node image.  The first range is small (kRowsAlign x 64 rows);
 // it decides the record layout and measures the node image's bytes per row,
 // from which every later range is sized to the memory left (at most
-// rows_range_rows(); MBRWT_ROWS_RANGE fixes the size: a test hook).
+// rows_range_rows(); MBRWT_BUILD_ROWS_RANGE fixes the size: a test hook).
 constexpr uint64_t kRowsFirstRange = 64 * kRowsAlign;
 template <class BuildRange>
 static int create_rows_ranged(int device, uint64_t num_rows, uint64_t num_columns, mbrwt_ctx **out, int layout,
@@ -364,7 +364,7 @@ static int create_rows_ranged(int device, uint64_t num_rows, uint64_t num_column
 // the whole node image and the records side by side may not fit (C3: 214 GB
 // of node image + 160 GB of records).  AUTO falls back to the per-node
 // images when the tree is outside the row-record limits or the records do
-// not fit.  (MBRWT_ROWS_RANGE: ranged beyond one such range, a test hook.)
+// not fit.  (MBRWT_BUILD_ROWS_RANGE: ranged beyond one such range, a test hook.)
 constexpr uint64_t kAutoRangedRows = 1ull << 27;
 static bool ranged_rows(int layout, uint64_t num_rows) {
     return (layout == LAYOUT_ROWS || layout == LAYOUT_AUTO) &&

@@ -263,13 +263,13 @@ struct RowsImage {
     bool mask1 = false;             // every internal node (leaf parents too) has arity <= 8: one-byte masks
     uint32_t uni = 0;               // K internal levels above leaf parents on every path (rows_walk_uni), else 0
     uint64_t bytes = 0;             // blocks + spill used
-    uint32_t occ_cap = 0;           // workgroups per CU of k_traverse_rows (0 = the default; MBRWT_ROWS_WGS_PER_CU)
+    uint32_t occ_cap = 0;           // workgroups per CU of k_traverse_rows (0 = the default; MBRWT_BUILD_ROWS_WGS_PER_CU)
     // VARIABLE-LENGTH records (rows_var.hip; dense rows): contiguous records
     // [unit bitmap][unit masks] addressed by 64-byte directory lines of 13 rows
     bool var = false;
     uint32_t var_W = 0;                 // bitmap words (units / 32, rounded up)
     uint32_t var_ustride = 0;           // unit u's first column = u * var_ustride for every unit (0: use the table)
-    uint32_t var_G = 0;                 // lanes per row of k_var_decode (0 = from the statistics; MBRWT_VAR_G)
+    uint32_t var_G = 0;                 // lanes per row of k_var_decode (0 = from the statistics; MBRWT_BUILD_VAR_LANES)
     std::vector<uint32_t> var_units;    // per unit (leaf parent, DFS order): first column | arity << 16
     std::vector<uint16_t> var_unit_of;  // per dnode: its unit, or 0xFFFF
     std::vector<uint32_t> var_anc;      // per unit: its ancestors' dnodes at levels 0..K-1
@@ -292,7 +292,7 @@ struct RowsImage {
 bool build_rwt_table(const Tree &tree, std::vector<uint32_t> &table, uint32_t &height);
 bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &table2, uint32_t &frames);
 uint32_t rwt2_uniform_levels(const std::vector<uint32_t> &table2);
-// the thread's build layout (mbrwt_set_build_option, else MBRWT_LAYOUT)
+// the thread's build layout (mbrwt_set_build_option; AUTO when unset)
 int build_layout();
 void set_build_layout(int layout);
 int thread_build_layout();  // the value set for the calling thread (AUTO when unset)

@@ -724,7 +724,7 @@ __device__ __forceinline__ uint32_t quad_exclusive_sum(uint32_t v, uint32_t c, u
 //   PACK  -- the same block read gives the children bits AND their MASK8
 //            masks; the block is staged in LDS and each lane picks the masks
 //            of its two children: a level costs no second dependent read;
-//   PLANE with FLAG_MASK_CHILDREN (MBRWT_PACK=0 trees) -- block read, then
+//   PLANE with FLAG_MASK_CHILDREN (node kinds without MBRWT_KIND_PACK) -- block read, then
 //            the (independent) mask reads of the set MASK8 children;
 //   MASK8 -- leaf labels from one byte (only as the root's child).
 // Labels are staged in LDS (32 per row) and flushed as 16-byte vectors when
