@@ -589,8 +589,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(G >= 8
             uint32_t *dst = p.cols + tbase;
             for (uint32_t i = 4 * lane; i < ttot; i += 256) {
                 if (i + 4 <= ttot) {
-                    const uint32_t a = stage[i], b = stage[i + 1], c = stage[i + 2], d = stage[i + 3];
-                    *(AS_GLOBAL u32x4_t *)(uintptr_t)(dst + i) = u32x4_t{a, b, c, d};
+                    // one 8-byte LDS read per 4 labels (r05: the same LDS instruction
+                    // count and conflicts as four u16 reads -- the compiler merged
+                    // those already -- 2.150 vs 2.155 ms, profiles/r05/v11_*)
+                    const uint64_t w4 = *(const AS_LDS uint64_t *)(stage + i);
+                    const uint32_t lo = (uint32_t)w4, hi = (uint32_t)(w4 >> 32);
+                    *(AS_GLOBAL u32x4_t *)(uintptr_t)(dst + i) = u32x4_t{lo & 0xFFFFu, lo >> 16, hi & 0xFFFFu, hi >> 16};
                 } else {
                     for (uint32_t j = i; j < ttot; ++j) gst(dst + j, (uint32_t)stage[j]);
                 }
