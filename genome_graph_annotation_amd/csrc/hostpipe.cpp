@@ -207,15 +207,11 @@ static int pipe_init(Ctx &c) {
         MBRWT_HIP(hipEventRecord(s.ev_in, p->s_in));
         MBRWT_HIP(hipEventRecord(s.ev_q, p->s_in));
     }
-    // copy threads beside the caller: host memcpy, not PCIe, bounds a pageable
-    // caller's 0.38 GB per 8 M C4 rows (one thread moves ~6 GB/s)
-#if defined(MBRWT_AB_POOL)
-    constexpr unsigned kPoolMax = MBRWT_AB_POOL;
-#else
-    constexpr unsigned kPoolMax = 15;
-#endif
+    // copy threads beside the caller (r05: 15 instead of 7 changed nothing
+    // measurable on the same box -- the pageable leg varies more between
+    // boxes and runs than with the pool: profiles/r05/v13_copy_pool/)
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    p->pool = new CopyPool(std::min(kPoolMax, hw > 1 ? hw - 1 : 0u));
+    p->pool = new CopyPool(std::min(7u, hw > 1 ? hw / 2 : 0u));
     return MBRWT_OK;
 }
 
