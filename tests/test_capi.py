@@ -68,6 +68,16 @@ def test_build_options_thread_local():
     assert lib.mbrwt_set_build_option(99, 0) == L.MBRWT_ERR_INVALID
     v = C.c_int64(0)
     assert lib.mbrwt_get_build_option(99, C.byref(v)) == L.MBRWT_ERR_INVALID
+    # record classes (csrc/rows_class.hip): -1 auto (default), 0 never, 1 always
+    assert get(L.MBRWT_BUILD_ROWS_CLASSES) == -1
+    for val in (0, 1, -1):
+        with build_option(L.MBRWT_BUILD_ROWS_CLASSES, val):
+            assert get(L.MBRWT_BUILD_ROWS_CLASSES) == val
+    for bad in (2, -2):
+        assert lib.mbrwt_set_build_option(L.MBRWT_BUILD_ROWS_CLASSES, bad) == L.MBRWT_ERR_INVALID
+    assert get(L.MBRWT_BUILD_ROWS_CLASSES) == -1
+    out = (C.c_uint64 * 4)()
+    assert lib.mbrwt_rows_classes(None, out) == L.MBRWT_ERR_INVALID
 
 
 def test_null_arguments_fail_cleanly():
