@@ -281,6 +281,7 @@ void append_path_table(std::vector<uint32_t> &t2, uint32_t K) {
     for (uint32_t d = 0; d < K; ++d) entries *= A[d];
     if (entries > kRowsMaxPathEntries || entries == 0) return;
     std::vector<uint16_t> col(entries, 0);
+    std::vector<uint8_t> set(entries, 0);
     // depth-first over the paths
     struct F {
         uint32_t w, idx, d;
@@ -293,12 +294,27 @@ void append_path_table(std::vector<uint32_t> &t2, uint32_t K) {
         for (uint32_t c = 0; c < a; ++c) {
             const uint32_t e = t2[4 + f + c];
             const uint32_t idx = fr.idx * A[fr.d] + c;
-            if (fr.d + 1 == K) col[idx] = (uint16_t)(e & 0xFFFFu);  // a leaf parent: its first column
+            if (fr.d + 1 == K) {  // a leaf parent: its first column
+                col[idx] = (uint16_t)(e & 0xFFFFu);
+                set[idx] = 1;
+            }
             else st.push_back(F{e, idx, fr.d + 1});
         }
     }
     uint32_t packed = 0;
     for (uint32_t d = 1; d < K; ++d) packed |= A[d] << (4 * (d - 1));
+    // a LINEAR path table (every leaf parent's first column = its path index
+    // << s: the basic partitioner's trees, whose only incomplete nodes are the
+    // last of their level -- C2-C4 with s = 3) is flagged in bit 31, s in bits
+    // 24..28: the walk then computes the column instead of reading it
+    for (uint32_t sh = 0; sh < 16; ++sh) {
+        bool lin = true;
+        for (uint64_t i = 0; i < entries && lin; ++i) lin = !set[i] || col[i] == (uint32_t)(i << sh);
+        if (lin) {
+            packed |= 0x80000000u | sh << 24;
+            break;
+        }
+    }
     t2[3] = (uint32_t)t2.size();
     t2.push_back(packed);
     for (size_t i = 0; i < col.size(); i += 2)
@@ -1045,7 +1061,20 @@ __device__ __forceinline__ void rows_walk_uni(const AS_LDS uint8_t *pb, uint32_t
 // leaf parents in some lane, so branches only added exec-mask work), and a
 // leaf parent's first label is stored unconditionally (1.01 labels per leaf
 // parent at C4), the loop only for the rest.
-template <int K>
+// a * b + c in one full-rate v_mad_u32_u24 (a, b < 2^24; b wave-uniform):
+// the compiler folds __umul24(a, b) + c into the quarter-rate 64-bit
+// v_mad_u64_u32, so the instruction is named here
+__device__ __forceinline__ uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(MBRWT_AB_NOASM24)
+    return __umul24(a, b) + c;
+#else
+    uint32_t r;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+    return r;
+#endif
+}
+
+template <int K, bool LIN>
 __device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_t o, bool live,
                                                const AS_LDS uint16_t *ptab, uint32_t A, AS_LDS uint16_t *out,
                                                uint32_t pos) {
@@ -1078,7 +1107,7 @@ __device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_
 #if defined(MBRWT_AB_MUL32)
             const uint32_t ni = k == 1 ? c : idx[k - 1] * Ak + c;
 #else
-            const uint32_t ni = k == 1 ? c : __umul24(idx[k - 1], Ak) + c;
+            const uint32_t ni = k == 1 ? c : mad_u24(idx[k - 1], Ak, c);
 #endif
             idx[k] = nd[k] ? ni : idx[k];
             r[k - 1] = nd[k] ? (r[k - 1] & (r[k - 1] - 1u)) : r[k - 1];
@@ -1091,7 +1120,10 @@ __device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_
 #if defined(MBRWT_AB_MUL32)
         const uint32_t base = ptab[K > 1 ? idx[K - 1] * AK + c : c];
 #else
-        const uint32_t base = ptab[K > 1 ? __umul24(idx[K - 1], AK) + c : c];  // the leaf parent's first column
+        const uint32_t pidx = K > 1 ? mad_u24(idx[K - 1], AK, c) : c;
+        // the leaf parent's first column: computed on a linear path table (no
+        // LDS round trip per iteration), else read
+        const uint32_t base = LIN ? pidx << ((A >> 24) & 0x1Fu) : (uint32_t)ptab[pidx];
 #endif
         uint32_t x = *rc;
         ++rc;
@@ -1432,13 +1464,27 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
 #undef MBRWT_TREE_CASE
                 } else if (ptw) {
                     const AS_LDS uint16_t *ptab = (const AS_LDS uint16_t *)((const AS_LDS uint32_t *)lds_rows + ptw + 1);
+#if defined(MBRWT_AB_NOLIN)
+                    const bool lin = false;  // (A/B: always read the path table)
+#else
+                    const bool lin = (pA >> 31) != 0u;
+#endif
+#define MBRWT_PATH_CASE(K)                                                      \
+    case K:                                                                     \
+        if (lin)                                                                \
+            rows_walk_path<K, true>(rec, o, live, ptab, pA, stage, pos);        \
+        else                                                                    \
+            rows_walk_path<K, false>(rec, o, live, ptab, pA, stage, pos);       \
+        break;
                     switch (p.uni) {
-                        case 1: rows_walk_path<1>(rec, o, live, ptab, pA, stage, pos); break;
-                        case 2: rows_walk_path<2>(rec, o, live, ptab, pA, stage, pos); break;
-                        case 3: rows_walk_path<3>(rec, o, live, ptab, pA, stage, pos); break;
-                        case 4: rows_walk_path<4>(rec, o, live, ptab, pA, stage, pos); break;
-                        default: rows_walk_path<5>(rec, o, live, ptab, pA, stage, pos); break;
+                        MBRWT_PATH_CASE(1)
+                        MBRWT_PATH_CASE(2)
+                        MBRWT_PATH_CASE(3)
+                        MBRWT_PATH_CASE(4)
+                        default:
+                        MBRWT_PATH_CASE(5)
                     }
+#undef MBRWT_PATH_CASE
                 } else {
                     switch (p.uni) {
                         case 1: rows_walk_uni<1>(rec, o, live, root, ent, stage, pos); break;
