@@ -38,10 +38,14 @@ ap.add_argument("--shape", default="", help="npz (num_children/first_child/leaf_
 ap.add_argument("--tag", default="")
 ap.add_argument("--stamps-out", default="", help="save the per-wave stamp words (npy) here")
 ap.add_argument("--probe", action="store_true", help="also measure the random-request ceiling (tools/probe.hip)")
+ap.add_argument("--var-lanes", type=int, default=0, help="MBRWT_BUILD_VAR_LANES of the build (0: auto)")
 a = ap.parse_args()
 
 dev = torch.device("cuda:0")
 t0 = time.time()
+from genome_graph_annotation_amd.brwt import build_option  # noqa: E402
+_lanes = build_option(L.MBRWT_BUILD_VAR_LANES, a.var_lanes)
+_lanes.__enter__()
 if a.shape:
     mat = BRWTDevice.synthetic_shaped(a.rows, dict(np.load(a.shape)), a.density, a.seed, device=0, layout="rows")
 else:
