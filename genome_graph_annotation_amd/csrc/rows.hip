@@ -1913,7 +1913,11 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
                              ? kRowsWpbWide
                              : kRowsWpb;
     const RowsFn kfn = rows_fn(im, walk, wpb);
+#if defined(MBRWT_AB_LDS_PAD)
+    const size_t lds = table_bytes + wpb * per_wave + MBRWT_AB_LDS_PAD;  // (A/B: fewer resident workgroups)
+#else
     const size_t lds = table_bytes + wpb * per_wave;
+#endif
     const uint32_t threads = 64 * wpb;
     // at most 24 waves (3 workgroups of 8) per CU: more waves make the walk phase
     // slower than the extra loads in flight gain (C4 0.426 ms at 3 against

@@ -39,6 +39,7 @@ ap.add_argument("--tag", default="")
 ap.add_argument("--stamps-out", default="", help="save the per-wave stamp words (npy) here")
 ap.add_argument("--probe", action="store_true", help="also measure the random-request ceiling (tools/probe.hip)")
 ap.add_argument("--var-lanes", type=int, default=0, help="MBRWT_BUILD_VAR_LANES of the build (0: auto)")
+ap.add_argument("--wgs-per-cu", type=int, default=0, help="MBRWT_BUILD_ROWS_WGS_PER_CU of the build (0: auto)")
 a = ap.parse_args()
 
 dev = torch.device("cuda:0")
@@ -46,6 +47,8 @@ t0 = time.time()
 from genome_graph_annotation_amd.brwt import build_option  # noqa: E402
 _lanes = build_option(L.MBRWT_BUILD_VAR_LANES, a.var_lanes)
 _lanes.__enter__()
+_wgs = build_option(L.MBRWT_BUILD_ROWS_WGS_PER_CU, a.wgs_per_cu)
+_wgs.__enter__()
 if a.shape:
     mat = BRWTDevice.synthetic_shaped(a.rows, dict(np.load(a.shape)), a.density, a.seed, device=0, layout="rows")
 else:
