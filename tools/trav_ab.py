@@ -40,6 +40,7 @@ ap.add_argument("--stamps-out", default="", help="save the per-wave stamp words 
 ap.add_argument("--probe", action="store_true", help="also measure the random-request ceiling (tools/probe.hip)")
 ap.add_argument("--var-lanes", type=int, default=0, help="MBRWT_BUILD_VAR_LANES of the build (0: auto)")
 ap.add_argument("--wgs-per-cu", type=int, default=0, help="MBRWT_BUILD_ROWS_WGS_PER_CU of the build (0: auto)")
+ap.add_argument("--rows-block", default="", help="B,S: MBRWT_BUILD_ROWS_BLOCK of the build (default: auto)")
 a = ap.parse_args()
 
 dev = torch.device("cuda:0")
@@ -49,6 +50,10 @@ _lanes = build_option(L.MBRWT_BUILD_VAR_LANES, a.var_lanes)
 _lanes.__enter__()
 _wgs = build_option(L.MBRWT_BUILD_ROWS_WGS_PER_CU, a.wgs_per_cu)
 _wgs.__enter__()
+if a.rows_block:
+    _bb, _ss = (int(x) for x in a.rows_block.split(","))
+    _blk = build_option(L.MBRWT_BUILD_ROWS_BLOCK, _bb << 8 | _ss)  # (kept referenced: scoped to the script)
+    _blk.__enter__()
 if a.shape:
     mat = BRWTDevice.synthetic_shaped(a.rows, dict(np.load(a.shape)), a.density, a.seed, device=0, layout="rows")
 else:
