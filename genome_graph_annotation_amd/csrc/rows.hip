@@ -1427,7 +1427,18 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
         const bool has_long = __any(lng);
         uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
 #if !defined(MBRWT_AB_NOSTORE)
+#if !defined(MBRWT_AB_PLAINSTORE)
+        // (non-temporal: the temp region is read once, by k_compact_tiles;
+        // the stores then disturb the random block reads less -- C4 kernel
+        // 0.262 -> 0.255 ms, step 0.348 -> 0.333 ms; the same hint on the
+        // compaction's CSR stores made the two-stream step slower again,
+        // 0.344 ms: profiles/r05/v21_temp_stores)
+        if (lane < nr)
+            __builtin_nontemporal_store((uint16_t)(cnt | (lng ? 0x8000u : 0u)),
+                                        (AS_GLOBAL uint16_t *)(uintptr_t)(reinterpret_cast<uint16_t *>(treg) + lane));
+#else
         if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)(cnt | (lng ? 0x8000u : 0u)));
+#endif
 #endif
         AB_STAMP(1);
         if (!direct) {
@@ -1496,11 +1507,18 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
                 }
                 wave_sync();
                 AB_STAMP(2);
+                // (r05: rounding the copy up to whole 128-byte lines helped plain
+                // stores by 1.5 % and non-temporal ones not at all: not kept)
                 const uint32_t nbytes = total * 2;
 #if !defined(MBRWT_AB_NOSTORE)
                 for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
+#if !defined(MBRWT_AB_PLAINSTORE)
+                    __builtin_nontemporal_store(*(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2),
+                                                (AS_GLOBAL u32x4_t *)(uintptr_t)(treg + 128 + q2));
+#else
                     gst(reinterpret_cast<u32x4_t *>(treg + 128 + q2),
                         *(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2));
+#endif
 #else
                 (void)nbytes;  // (timing only: no temp-region stores)
 #endif
