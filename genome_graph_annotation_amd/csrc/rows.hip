@@ -850,6 +850,18 @@ __device__ bool rwt_walk_lds(const uint32_t *ntab, const uint16_t *etab, ByteFn 
     return true;
 }
 
+// (A/B: non-temporal loads of the data read once -- row ids, spill entries,
+// the temp region in the compaction)
+#if defined(MBRWT_AB_NTLOADS)
+constexpr bool kAbNtLoads = true;
+#else
+constexpr bool kAbNtLoads = false;
+#endif
+template <class T>
+__device__ __forceinline__ T ab_ld(const T *p) {
+    return gld_at_nt<T, kAbNtLoads>((uint64_t)(uintptr_t)p);
+}
+
 // walk families of k_traverse_rows (RowsImage::walk)
 enum : uint32_t { WALK_GENERAL = 0, WALK_MASK1 = 1, WALK_ODOMETER = 2, WALK_TREE_ODOMETER = 3 };
 
@@ -1260,7 +1272,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
     const uint64_t tstride = (uint64_t)gridDim.x * WPB;  // (one tile per wave unless the grid is capped)
     uint64_t t = (uint64_t)blockIdx.x * WPB + wv;
     uint64_t row_n = 0;  // the row of this lane in the wave's next tile (its load overlaps the table's)
-    if (t < ntiles && t * 64 + lane < p.n) row_n = gld(p.rows + t * 64 + lane);
+    if (t < ntiles && t * 64 + lane < p.n) row_n = ab_ld(p.rows + t * 64 + lane);
     for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_rows[i] = gld(p.table + i);
     if (blockIdx.x == 0 && threadIdx.x == 0) p.status[1] = MBRWT_OK;  // k_compact_tiles raises it
     __syncthreads();
@@ -1325,7 +1337,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
         const uint32_t nr = (uint32_t)(p.n - r0 < 64 ? p.n - r0 : 64);
         const uint64_t row = row_n;
         tn = t + tstride;
-        if (tn < ntiles && tn * 64 + lane < p.n) row_n = gld(p.rows + tn * 64 + lane);
+        if (tn < ntiles && tn * 64 + lane < p.n) row_n = ab_ld(p.rows + tn * 64 + lane);
         const bool valid = lane < nr && row < p.num_rows;
         if (lane < nr && !valid) atomicOr(&p.scalars[2], 1ull);
         // record classes: the row's class is its record's row in the
@@ -1374,7 +1386,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
             const uint64_t sa = p.spill + (uint64_t)idx * 16;
             *(AS_LDS uint32_t *)(mine + B) = idx;  // (the slot's pad word: a long record's copy below)
 #pragma unroll
-            for (uint32_t k = 0; k < LPB; ++k) sq[k] = gld_at<u32x4_t>(sa + 16u * k);
+            for (uint32_t k = 0; k < LPB; ++k) sq[k] = gld_at_nt<u32x4_t, kAbNtLoads>(sa + 16u * k);
         }
         if (any_spl && spl) {
 #pragma unroll
@@ -1611,10 +1623,10 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
         const uint64_t r0 = t * 64;
         tc[k] = in ? gld(p.tile_counts + t) : 0x80000000u;
         base[k] = in ? gld(p.tile_offsets + t) : 0;
-        cnt[k] = (in && r0 + lane < n) ? (uint32_t)gld(reinterpret_cast<const uint16_t *>(treg) + lane) : 0u;  // (bit 15: long)
+        cnt[k] = (in && r0 + lane < n) ? (uint32_t)ab_ld(reinterpret_cast<const uint16_t *>(treg) + lane) : 0u;  // (bit 15: long)
         const uint16_t *lab = reinterpret_cast<const uint16_t *>(treg + 128);
 #pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) v[k][j] = gld(lab + lane + 64 * j);  // (C >= 1024: inside the region)
+        for (uint32_t j = 0; j < 8; ++j) v[k][j] = ab_ld(lab + lane + 64 * j);  // (C >= 1024: inside the region)
     }
 #pragma unroll
     for (uint32_t k = 0; k < kCompactTpw; ++k) {
@@ -1643,7 +1655,7 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
 #pragma unroll
             for (uint32_t j = 0; j < 8; ++j) {
                 const uint32_t i = i0 + lane + 64 * j;
-                w[j] = i < tot ? (uint32_t)gld(lab + i) : 0u;
+                w[j] = i < tot ? (uint32_t)ab_ld(lab + i) : 0u;
             }
 #pragma unroll
             for (uint32_t j = 0; j < 8; ++j) {

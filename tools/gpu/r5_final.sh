@@ -2,7 +2,7 @@
 # bench C4 (live PMC, ceilings, CPU baseline, end-to-end, whole-batch parity)
 # and its kernel trace; heartbeat per minute
 set -o pipefail
-O=gpurun_out/r5final; mkdir -p $O
+O=gpurun_out/r5final2; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 ( for i in $(seq 1 25); do sleep 60; echo "heartbeat $i $(date +%T)" >> $O/heartbeat.log; done ) &
 HB=$!
