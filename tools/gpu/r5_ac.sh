@@ -1,7 +1,7 @@
 # r05 step AC: the slow full-size cases and the greedy + relax shape at 3.7 B
 # rows (whole batch against the streamed shaped oracle) on the final sources
 set -o pipefail
-O=gpurun_out/r5ac; mkdir -p $O
+O=gpurun_out/r5ac2; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 ( for i in $(seq 1 20); do sleep 60; echo "heartbeat $i $(date +%T)" >> $O/heartbeat.log; done ) &
 HB=$!
