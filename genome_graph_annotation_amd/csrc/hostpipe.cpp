@@ -244,6 +244,20 @@ int host_get_rows(Ctx &c, const uint64_t *rows, uint64_t n, uint64_t *offsets, u
     if ((rc = pipe_init(c))) return rc;
     HostPipe &P = *c.pipe;
     const hipStream_t sq = c.stream;
+    // every way out waits for the chunks already queued: an error return
+    // (NOMEM growing a slot, a failed HIP call) must not leave H2D copies,
+    // queries or D2H copies into the caller's page-locked buffers running
+    // after the call has returned; on success the streams are
+    // idle by then and the waits return at once
+    struct Quiesce {
+        HostPipe &P;
+        hipStream_t sq;
+        ~Quiesce() {
+            (void)hipStreamSynchronize(P.s_in);
+            (void)hipStreamSynchronize(sq);
+            (void)hipStreamSynchronize(P.s_out);
+        }
+    } quiesce{P, sq};
     const bool pin_rows = is_pinned(rows), pin_off = is_pinned(offsets), pin_cols = cols && is_pinned(cols);
     const uint64_t nch = n ? (n + kChunkRows - 1) / kChunkRows : 1;
     const double mean = c.tree.num_rows ? (double)c.tree.num_relations / (double)c.tree.num_rows : 0.0;
@@ -256,6 +270,10 @@ int host_get_rows(Ctx &c, const uint64_t *rows, uint64_t n, uint64_t *offsets, u
     // step 1: chunk i's row ids to the device, its query queued
     auto issue = [&](uint64_t i) -> int {
         HostPipe::Slot &s = slot_of(i);
+        if (c.test_fail_chunk >= 0 && i == (uint64_t)c.test_fail_chunk) {  // (test hook: an injected NOMEM)
+            set_error("injected failure (MBRWT_OPT_TEST_FAIL_CHUNK)");
+            return MBRWT_ERR_NOMEM;
+        }
         s.row0 = i * kChunkRows;
         s.n = std::min<uint64_t>(kChunkRows, n - s.row0);
         const uint64_t lcap = (uint64_t)((double)s.n * mean * 1.25) + 65536;

@@ -1954,20 +1954,6 @@ Trav pick_traverse(const Ctx &c) {
     const int v = (c.kernel_variant == 0 || c.kernel_variant >= 11) ? 5 : c.kernel_variant;  // 17/18: fast2 only
     const int cpl = v == 2 ? 1 : (v == 4 || v == 6) ? 4 : 2;
     const int wpe = (v == 5 || v == 10) ? 8 : v == 6 ? 6 : 1;  // (v == 10 past depth 8 runs as 5)
-#if defined(MBRWT_AB_VARIANTS)
-    if (v == 10 && depth <= 8) {  // variant 5 with non-temporal block/mask reads
-        const uint32_t need = (max_arity + 1) / 2;
-        uint32_t G = 1;
-        while (G < need) G <<= 1;
-        t.G = G;
-        if (depth <= 4) t.group_fn = max_arity <= 32 ? (GroupFn)k_traverse_group<4, 2, uint32_t, MODE, 8, true>
-                                                     : (GroupFn)k_traverse_group<4, 2, uint64_t, MODE, 8, true>;
-        else if (depth <= 8) t.group_fn = max_arity <= 32 ? (GroupFn)k_traverse_group<8, 2, uint32_t, MODE, 8, true>
-                                                          : (GroupFn)k_traverse_group<8, 2, uint64_t, MODE, 8, true>;
-        t.fn = reinterpret_cast<const void *>(t.group_fn);
-        return t;
-    }
-#endif
     const uint32_t need = (max_arity + cpl - 1) / cpl;
     uint32_t G = 1;
     while (G < need) G <<= 1;
@@ -1980,12 +1966,6 @@ Trav pick_traverse(const Ctx &c) {
         return t;                                                                                  \
     }
 #define PICKD(CPLV, W) PICKG(4, CPLV, W) PICKG(8, CPLV, W) PICKG(16, CPLV, W) PICKG(32, CPLV, W)
-#if defined(MBRWT_AB_VARIANTS)
-    PICKD(1, 1)
-    PICKD(2, 1)
-    PICKD(4, 1)
-    PICKD(4, 6)
-#endif
     PICKD(2, 8)
 #undef PICKD
 #undef PICKG
@@ -2072,10 +2052,6 @@ static P2wFn p2w_kernel(const Ctx &c) {
     if (c.tree.p2w_table.empty() || !c.d_p2w || !(kv == 0 || kv == 19 || kv == 20)) return nullptr;
     const bool big = c.tree.image_bytes > (1ull << 30);
     switch (kv) {
-#if defined(MBRWT_AB_VARIANTS)
-    case 19: return k_traverse_p2w<false>;
-    case 20: return k_traverse_p2w<true>;
-#endif
     default:  // u16 temp labels when they fit (p2w_label16)
         if (c.tree.num_columns <= 0x10000u) return big ? k_traverse_p2w<true, uint16_t> : k_traverse_p2w<false, uint16_t>;
         return big ? k_traverse_p2w<true> : k_traverse_p2w<false>;
@@ -2108,15 +2084,8 @@ struct PtwPick {
 };
 template <bool NT, bool WIDE, int MAXD>
 static P2wFn ptw_fn(uint32_t wpb) {
-#if defined(MBRWT_AB_VARIANTS)
-    return wpb == 16  ? k_traverse_ptw<NT, WIDE, MAXD, 16>
-           : wpb == 8 ? k_traverse_ptw<NT, WIDE, MAXD, 8>
-           : wpb == 7 ? k_traverse_ptw<NT, WIDE, MAXD, 7, 256, uint16_t>
-                      : k_traverse_ptw<NT, WIDE, MAXD, 4>;
-#else
-    (void)wpb;  // (the release library: the default 7-wave kernel only)
+    (void)wpb;  // (the default 7-wave kernel only; the r02 wave-count variants were retired)
     return k_traverse_ptw<NT, WIDE, MAXD, 7, 256, uint16_t>;
-#endif
 }
 static PtwPick ptw_kernel(const Ctx &c) {
     PtwPick r;

@@ -642,6 +642,11 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         constexpr double kAutoMaxCost = 1.25;
         const int force_var = build_tuning().rows_var;
         bool var_ok = force_var != 0 && rb.align % 13 == 0 && var_prepare(range.tree, im);
+        // the lanes per row the decode will run with (the build option, else
+        // automatic): the LDS gate below must judge that geometry
+        uint32_t var_G = build_tuning().var_lanes;
+        if (var_G & (var_G - 1) || var_G > 16) var_G = 0;  // (1, 2, 4, 8 or 16; 0: automatic)
+        im.var_G = var_G;
         double var_mem = 1e300;
         if (var_ok && (force_var == 1 || tmin > kAutoMaxCost)) {
             uint64_t vb = 0;
@@ -660,8 +665,7 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         }
         if (var_ok && var_mem <= budget && (force_var == 1 || tmin > kAutoMaxCost)) {
             im.var = true;
-            im.var_G = build_tuning().var_lanes;
-            if (im.var_G & (im.var_G - 1) || im.var_G > 16) im.var_G = 0;  // (1, 2, 4, 8 or 16)
+            im.var_G = var_G;
             const uint64_t nlines = (rb.n + 12) / 13;
             MBRWT_HIP(hipMalloc(&im.var_lines, nlines * 64));
             MBRWT_HIP(hipMemsetAsync(im.var_lines, 0, nlines * 64, rb.s));
@@ -850,18 +854,6 @@ __device__ bool rwt_walk_lds(const uint32_t *ntab, const uint16_t *etab, ByteFn 
     return true;
 }
 
-// (A/B: non-temporal loads of the data read once -- row ids, spill entries,
-// the temp region in the compaction)
-#if defined(MBRWT_AB_NTLOADS)
-constexpr bool kAbNtLoads = true;
-#else
-constexpr bool kAbNtLoads = false;
-#endif
-template <class T>
-__device__ __forceinline__ T ab_ld(const T *p) {
-    return gld_at_nt<T, kAbNtLoads>((uint64_t)(uintptr_t)p);
-}
-
 // walk families of k_traverse_rows (RowsImage::walk)
 enum : uint32_t { WALK_GENERAL = 0, WALK_MASK1 = 1, WALK_ODOMETER = 2, WALK_TREE_ODOMETER = 3 };
 
@@ -885,6 +877,16 @@ struct RowsParams {
     uint32_t mask1;               // every mask one byte
     const uint32_t *classes;      // record classes: the packed class index (null: none; rows_class.hip)
     uint32_t class_bits;
+    // the one-pass form (FUSED): the tiles' look-back descriptors, the call's
+    // epoch, the caller's CSR and capacity, the RWT table and its frames
+    // limit (global walks)
+    uint64_t *desc;
+    uint32_t epoch;
+    uint64_t *offsets;
+    uint32_t *cols;
+    uint64_t cap;
+    const uint32_t *rwt;
+    uint32_t stk_lim;
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -1077,13 +1079,9 @@ __device__ __forceinline__ void rows_walk_uni(const AS_LDS uint8_t *pb, uint32_t
 // the compiler folds __umul24(a, b) + c into the quarter-rate 64-bit
 // v_mad_u64_u32, so the instruction is named here
 __device__ __forceinline__ uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) {
-#if defined(MBRWT_AB_NOASM24)
-    return __umul24(a, b) + c;
-#else
     uint32_t r;
     asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
     return r;
-#endif
 }
 
 template <int K, bool LIN>
@@ -1116,11 +1114,7 @@ __device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_
             const uint32_t Ak = k >= 2 ? (A >> (4 * (k - 2))) & 0xFu : 0u;  // (wave-uniform)
             // (24-bit multiplies: v_mad_u32_u24 issues at full rate, the
             // 32-bit v_mad_u64_u32 the compiler picks otherwise does not)
-#if defined(MBRWT_AB_MUL32)
-            const uint32_t ni = k == 1 ? c : idx[k - 1] * Ak + c;
-#else
             const uint32_t ni = k == 1 ? c : mad_u24(idx[k - 1], Ak, c);
-#endif
             idx[k] = nd[k] ? ni : idx[k];
             r[k - 1] = nd[k] ? (r[k - 1] & (r[k - 1] - 1u)) : r[k - 1];
             r[k] = nd[k] ? b : r[k];
@@ -1129,14 +1123,10 @@ __device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_
         const uint32_t c = (uint32_t)__builtin_ctz(r[K - 1]);
         r[K - 1] &= r[K - 1] - 1u;
         const uint32_t AK = K > 1 ? (A >> (4 * (K - 2))) & 0xFu : 0u;
-#if defined(MBRWT_AB_MUL32)
-        const uint32_t base = ptab[K > 1 ? idx[K - 1] * AK + c : c];
-#else
         const uint32_t pidx = K > 1 ? mad_u24(idx[K - 1], AK, c) : c;
         // the leaf parent's first column: computed on a linear path table (no
         // LDS round trip per iteration), else read
         const uint32_t base = LIN ? pidx << ((A >> 24) & 0x1Fu) : (uint32_t)ptab[pidx];
-#endif
         uint32_t x = *rc;
         ++rc;
         *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));
@@ -1238,13 +1228,6 @@ __device__ __forceinline__ void rows_walk_tree(const AS_LDS uint8_t *pb, uint32_
     }
 }
 
-#if defined(MBRWT_AB_STAMPS)
-// A/B diagnostics (tools/ build only, never the release library): per wave,
-// shader-clock cycles spent in each phase of the tile loop
-constexpr uint32_t kAbStampWaves = 16384, kAbStampWords = 8;
-__device__ unsigned long long g_ab_stamps[kAbStampWaves * kAbStampWords];
-#endif
-
 // Tiles per wave (r05).  A persistent grid (every wave a fixed share of the
 // tiles) lasts as long as its slowest wave, and its waves are not equally
 // fast: the workgroups dispatched last lose issue arbitration by age (per-wave
@@ -1258,24 +1241,172 @@ __device__ unsigned long long g_ab_stamps[kAbStampWaves * kAbStampWords];
 // loads), s_setprio for the later workgroups (0.2855), and requesting the
 // next tile's blocks before walking this one (register prefetch with the
 // spill reloads issued first: 0.2865 persistent, 0.2775 at 4 tiles per wave).
+// (The r05 A/B variants of this kernel -- phase stamps, gather-only, no-walk,
+// no-store, cache-resident blocks -- were retired in r06; their results are
+// in profiles/r05 and DESIGN.md §16.)
 constexpr uint32_t kRowsTilesPerWave = 1;
+
+// ---- the one-pass form (r06, FUSED) ---------------------------------------
+// Each tile writes its rows' offsets and labels straight into the caller's
+// CSR.  Its place there -- the labels of all tiles before it -- comes from a
+// decoupled look-back over per-tile DESCRIPTORS, one 8-byte granule per tile
+// {epoch:16 | flag:2 | error bits:2 | value:44}, stored and loaded with
+// agent-scope relaxed atomics (sc1: past the per-XCD L2s; the granule is the
+// whole message, so no fence orders it, MI355X_MICROARCH.md "R2"):
+//   * A (aggregate): the tile's label total, published as soon as its blocks
+//     are read (before its walk; before it waits on anything);
+//   * P (prefix): the inclusive label prefix, published once the tile knows
+//     its own.
+// After its walk a tile reads the 64 descriptors before it (one 512-byte
+// load): the nearest P plus the A totals after it is its exclusive prefix;
+// with no P among them it moves 64 tiles further back.  A tile only ever
+// waits for a predecessor's A, which that predecessor publishes before it
+// waits on anyone, so the waves progress whenever the waves they wait on
+// have been dispatched (in-order dispatch makes that always true); a bounded
+// spin turns anything else into MBRWT_ERR_DEVICE instead of a hang.  The
+// error bits (bit 0: a row out of range, bit 1: a record that does not walk)
+// travel with the totals, so the last tile publishes the call's status.
+// Replaces the temp region, the tile scan and k_compact_tiles (C4: 143 MB of
+// u16 labels written and read back, two more launches per batch).  Epochs
+// tell this call's descriptors from an earlier call's (the array is cleared
+// when the 16-bit epoch wraps).
+enum : uint32_t { DESC_A = 1, DESC_P = 2 };
+constexpr uint32_t kDescValueBits = 44;
+constexpr uint32_t kLookbackSpins = 1u << 22;  // (about a second of 1-2 us polls)
+__device__ __forceinline__ uint64_t desc_pack(uint32_t epoch, uint32_t flag, uint32_t err, uint64_t v) {
+    return ((uint64_t)epoch << 48) | ((uint64_t)flag << 46) | ((uint64_t)err << kDescValueBits) | v;
+}
+__device__ __forceinline__ void desc_store(uint64_t *d, uint64_t v) {
+    __hip_atomic_store((AS_GLOBAL uint64_t *)(uintptr_t)d, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t desc_load(const uint64_t *d) {
+    return __hip_atomic_load((AS_GLOBAL uint64_t *)(uintptr_t)d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the sum over the wave of one value < 2^44 per lane (two 22-bit halves
+// through the DPP scan: 64 x 2^22 fits 32 bits)
+__device__ __forceinline__ uint64_t wave_sum44(uint64_t v) {
+    const uint32_t lo = wave_incl_sum((uint32_t)v & 0x3FFFFFu);
+    const uint32_t hi = wave_incl_sum((uint32_t)(v >> 22));
+    return ((uint64_t)__builtin_amdgcn_readlane(hi, 63) << 22) + (uint64_t)__builtin_amdgcn_readlane(lo, 63);
+}
+// the exclusive label prefix of descriptor t > 0 (the scan wave's
+// workgroup); ORs the error bits of the ones before it into errs (every lane
+// active).  (r06: letting every look-back also publish P for the A granules
+// of its window -- "helping" -- made the kernel slower, 0.71 against 0.46 ms
+// at C4: the extra 8-byte write-through stores congest the memory system,
+// profiles/r06/v01_one_pass)
+__device__ __forceinline__ uint64_t rows_lookback(uint64_t *desc, uint64_t t, uint32_t epoch, uint32_t lane,
+                                                  uint32_t &errs) {
+    constexpr uint64_t kVal = (1ull << kDescValueBits) - 1ull;
+    uint64_t ex = 0;
+    int64_t j0 = (int64_t)t - 1;
+    for (uint32_t spins = 0;;) {
+        const int64_t j = j0 - (int64_t)lane;
+        // (before tile 0: a P of prefix 0)
+        const uint64_t d = j >= 0 ? desc_load(desc + j) : desc_pack(epoch, DESC_P, 0, 0);
+        const uint32_t f = (uint32_t)(d >> 48) == epoch ? (uint32_t)(d >> 46) & 3u : 0u;
+        const uint64_t pm = __ballot(f == DESC_P), okm = __ballot(f != 0u);
+        const uint32_t lp = pm ? (uint32_t)__builtin_ctzll(pm) : 63u;  // the nearest P (or the whole window)
+        const uint64_t need = lp == 63u ? ~0ull : (2ull << lp) - 1ull;
+        if ((okm & need) != need) {  // a tile up to it has published nothing yet
+            if (++spins >= kLookbackSpins) {
+                errs |= 2u;
+                return ex;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        const bool in = lane <= lp;
+        ex += wave_sum44(in ? d & kVal : 0ull);
+        errs |= (__ballot(in && ((d >> kDescValueBits) & 1ull)) ? 1u : 0u) |
+                (__ballot(in && ((d >> (kDescValueBits + 1)) & 1ull)) ? 2u : 0u);
+        if (pm) return ex;
+        j0 -= 64;
+    }
+}
+// a row's labels by the one-lane walk of its record in global memory (a tile
+// with more labels than its LDS stage, a record longer than the stage's
+// copy): counts them and, with dst, stores them there (u32); false when the
+// record does not walk to its count (a corrupt image).  The pending frames
+// live in the wave's block slots (free once the records are walked).
+template <int B>
+__device__ __forceinline__ bool rows_walk_global(const RowsParams &p, uint64_t rec_row, uint32_t *dst,
+                                                 AS_LDS uint32_t *stk) {
+    RowsView v;
+    v.blocks = p.blocks;
+    v.spill = p.spill;
+    v.magic = p.magic;
+    v.num_rows = 0;
+    v.B = B;
+    v.S = p.S;
+    uint64_t masks;
+    uint32_t count;
+    rows_locate(v, rec_row, masks, count);
+    const uint32_t *ntab = p.rwt + 4;
+    const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + gld(p.rwt));
+    uint32_t j = 0;
+    const bool ok = rwt_walk_lds(
+        ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
+        [&](uint32_t col) {
+            if (dst && j < count) __builtin_nontemporal_store(col, (AS_GLOBAL uint32_t *)(uintptr_t)(dst + j));
+            ++j;
+        },
+        stk, p.stk_lim);
+    return ok && j == count;
+}
 
 // k_traverse_rows: one wave per tile of 64 query rows (file comment).
 // B: block bytes; WPB: waves per workgroup (the RWT2 table is staged once per
-// workgroup; the grid is persistent); WALK: the walk family.
-template <int B, int WPB, bool NT, uint32_t WALK>
-__global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
+// workgroup); WALK: the walk family; FUSED: the one-pass form above (the
+// odometers only), else the tile's labels go to its temp region for
+// k_compact_tiles.
+template <int B, int WPB, bool NT, uint32_t WALK, bool FUSED>
+__global__ __launch_bounds__(64 * (WPB + (FUSED ? 1 : 0))) void k_traverse_rows(RowsParams p) {
+    static_assert(!FUSED || WALK == WALK_ODOMETER || WALK == WALK_TREE_ODOMETER, "one pass: the odometers only");
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows[];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t ntiles = (p.n + 63) / 64;
     const uint64_t tstride = (uint64_t)gridDim.x * WPB;  // (one tile per wave unless the grid is capped)
     uint64_t t = (uint64_t)blockIdx.x * WPB + wv;
+    // FUSED: the workgroup's look-back state (the scan wave below)
+    __shared__ uint32_t s_tot[WPB];  // tile totals
+    __shared__ uint32_t s_err, s_arrive, s_ready, s_errs;
+    __shared__ uint64_t s_base;
+    if (FUSED && threadIdx.x == 0) {
+        s_err = 0;
+        s_arrive = 0;
+        s_ready = 0;
+    }
     uint64_t row_n = 0;  // the row of this lane in the wave's next tile (its load overlaps the table's)
-    if (t < ntiles && t * 64 + lane < p.n) row_n = ab_ld(p.rows + t * 64 + lane);
+    if (t < ntiles && t * 64 + lane < p.n && wv < WPB) row_n = gld(p.rows + t * 64 + lane);
     for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_rows[i] = gld(p.table + i);
-    if (blockIdx.x == 0 && threadIdx.x == 0) p.status[1] = MBRWT_OK;  // k_compact_tiles raises it
+    if (!FUSED && blockIdx.x == 0 && threadIdx.x == 0) p.status[1] = MBRWT_OK;  // k_compact_tiles raises it
     __syncthreads();
+    if constexpr (FUSED) {
+        if (wv == WPB) {  // the scan wave: the workgroup's place in the CSR
+            const uint64_t b = blockIdx.x, t0 = b * WPB;
+            if (t0 >= ntiles) return;
+            const uint32_t nwv = (uint32_t)(ntiles - t0 < WPB ? ntiles - t0 : WPB);
+            while (__hip_atomic_load(&s_arrive, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < nwv)
+                __builtin_amdgcn_s_sleep(1);
+            const uint32_t wtot = __builtin_amdgcn_readlane(wave_incl_sum(lane < nwv ? s_tot[lane] : 0u), 63);
+            const uint32_t werr = s_err;
+            uint32_t errs = 0;
+            uint64_t ex = 0;
+            desc_store(p.desc + b, desc_pack(p.epoch, b == 0 ? DESC_P : DESC_A, werr, wtot));
+            if (b > 0) {
+                ex = rows_lookback(p.desc, b, p.epoch, lane, errs);
+                desc_store(p.desc + b, desc_pack(p.epoch, DESC_P, errs | werr, ex + wtot));
+            }
+            if (lane == 0) {
+                s_base = ex;
+                s_errs = errs | werr;
+                __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            return;
+        }
+    }
     const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows[0]);
     const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows + 4;
     // the leaf parents' column lists after the entries
@@ -1294,23 +1425,6 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
     AS_LDS uint32_t *stk = (AS_LDS uint32_t *)(wb + 64u * PB) + lane;
     constexpr uint32_t LPB = B / 16, RPI = 64 / LPB;
     const uint32_t S = p.S;
-#if defined(MBRWT_AB_STAMPS)
-    uint64_t ab_ph[5] = {0, 0, 0, 0, 0}, ab_tiles = 0, ab_t0 = __builtin_amdgcn_s_memtime();
-    uint64_t ab_last = ab_t0;
-#define AB_STAMP(k)                                               \
-    do {                                                          \
-        const uint64_t ab_now = __builtin_amdgcn_s_memtime();     \
-        ab_ph[k] += ab_now - ab_last;                             \
-        ab_last = ab_now;                                         \
-    } while (0)
-#else
-#define AB_STAMP(k) \
-    do {            \
-    } while (0)
-#endif
-#if defined(MBRWT_AB_GATHER)
-    uint32_t ab_acc = 0;
-#endif
     // a tile's 64 blocks as coalesced quarters: load k brings rows RPI k ..
     // RPI k + RPI - 1, lane L its 16 bytes L % LPB (row addresses by __shfl)
     auto issue_blocks = [&](uint64_t addr, u32x4_t (&qq)[LPB]) {
@@ -1323,36 +1437,22 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
         }
     };
     auto block_of = [&](uint64_t row, bool ok) -> uint64_t { return ok ? rows_block(row, S, p.magic) : 0; };
-    auto addr_of = [&](uint64_t b) -> uint64_t {
-#if defined(MBRWT_AB_HOT)
-        return p.blocks + (b & 4095u) * B;  // (timing only: a 256 KiB window, cache-resident)
-#else
-        return p.blocks + b * B;
-#endif
-    };
     u32x4_t q[LPB];
     for (uint64_t tn; t < ntiles; t = tn) {
-        AB_STAMP(4);
         const uint64_t r0 = t * 64;
         const uint32_t nr = (uint32_t)(p.n - r0 < 64 ? p.n - r0 : 64);
         const uint64_t row = row_n;
         tn = t + tstride;
-        if (tn < ntiles && tn * 64 + lane < p.n) row_n = ab_ld(p.rows + tn * 64 + lane);
+        if (tn < ntiles && tn * 64 + lane < p.n) row_n = gld(p.rows + tn * 64 + lane);
         const bool valid = lane < nr && row < p.num_rows;
-        if (lane < nr && !valid) atomicOr(&p.scalars[2], 1ull);
+        if (!FUSED && lane < nr && !valid) atomicOr(&p.scalars[2], 1ull);
         // record classes: the row's class is its record's row in the
         // dictionary (S = 1); the class index is the random HBM read, the
         // dictionary's blocks mostly cache hits
         const uint64_t rec_row = (p.classes && valid) ? class_field(p.classes, p.class_bits, row) : row;
         const uint64_t b = block_of(rec_row, valid);
         const uint32_t sub = (uint32_t)(rec_row - b * S);
-        issue_blocks(addr_of(b), q);
-#if defined(MBRWT_AB_GATHER)
-        // (timing only: the block loads into registers, no LDS, nothing else)
-#pragma unroll
-        for (uint32_t k = 0; k < LPB; ++k) ab_acc ^= q[k].x ^ q[k].y ^ q[k].z ^ q[k].w;
-        continue;
-#endif
+        issue_blocks(p.blocks + b * B, q);
 #pragma unroll
         for (uint32_t k = 0; k < LPB; ++k) {
             AS_LDS uint32_t *d = (AS_LDS uint32_t *)(wb + (RPI * k + lane / LPB) * PB + 16u * (lane % LPB));
@@ -1362,10 +1462,6 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
             d[3] = q[k].w;
         }
         wave_sync();
-        AB_STAMP(0);
-#if defined(MBRWT_AB_LOADONLY)
-        continue;  // (timing only: the block loads and their LDS staging, nothing else)
-#endif
         uint32_t cnt = 0, o = 0;
         bool spl = false;
         if (valid) {
@@ -1386,7 +1482,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
             const uint64_t sa = p.spill + (uint64_t)idx * 16;
             *(AS_LDS uint32_t *)(mine + B) = idx;  // (the slot's pad word: a long record's copy below)
 #pragma unroll
-            for (uint32_t k = 0; k < LPB; ++k) sq[k] = gld_at_nt<u32x4_t, kAbNtLoads>(sa + 16u * k);
+            for (uint32_t k = 0; k < LPB; ++k) sq[k] = gld_at<u32x4_t>(sa + 16u * k);
         }
         if (any_spl && spl) {
 #pragma unroll
@@ -1404,18 +1500,20 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
         const uint32_t x = wave_incl_sum(cnt);
         const uint32_t total = __builtin_amdgcn_readlane(x, 63);
         const uint32_t pos = x - cnt;
-        // a tile whose labels exceed its region is walked by k_compact_tiles
-        // from global memory; so is a record longer than a block (its count
-        // flagged with bit 15; its labels' places in the tile are kept)
+        // a tile whose labels exceed its region (its LDS stage) is walked from
+        // global memory -- by k_compact_tiles, or (FUSED) by the tile's own
+        // lanes; so is a record longer than a block (its count flagged with
+        // bit 15; its labels' places in the tile are kept)
         const bool direct = total > C;
         // the lane's record in LDS: its block slot, or (r05) for a record
         // longer than a block, a copy of its whole spill entry in the free tail
         // of the wave's label stage (the tile's labels take its first 2 total
-        // bytes), so the odometers walk it here instead of k_compact_tiles
-        // walking it byte by byte from global memory (the greedy + relax
-        // shape: 0.13 % of rows, 8 % of tiles; its compaction took 266 us of
-        // a 0.76 ms step, profiles/r05)
+        // bytes), so the odometers walk it here instead of walking it byte by
+        // byte from global memory (the greedy + relax shape: 0.13 % of rows,
+        // 8 % of tiles; their global walks took 266 us of a 0.76 ms step,
+        // profiles/r05)
         const AS_LDS uint8_t *rec = mine;
+        AS_LDS uint16_t *stage = (AS_LDS uint16_t *)(wb + 64u * PB + 256u * p.stk_words);
         if constexpr (WALK == WALK_ODOMETER || WALK == WALK_TREE_ODOMETER) {
             if (!direct && __any(lng)) {
                 // each long row's entry (16-byte chunks) below the previous
@@ -1424,7 +1522,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
                 const uint32_t need = lng ? ((8u + *(const AS_LDS uint32_t *)(mine + 4) + 15u) & ~15u) : 0u;
                 const uint32_t incl = wave_incl_sum(need);
                 if (2u * total + __builtin_amdgcn_readlane(incl, 63) <= 2u * C) {
-                    AS_LDS uint8_t *stg = wb + 64u * PB + 256u * p.stk_words + 2u * C - incl;
+                    AS_LDS uint8_t *stg = (AS_LDS uint8_t *)stage + 2u * C - incl;
                     if (lng) {
                         const uint64_t sa = p.spill + (uint64_t)*(const AS_LDS uint32_t *)(mine + B) * 16;
 #pragma unroll 1
@@ -1437,42 +1535,49 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
             }
         }
         const bool has_long = __any(lng);
-        uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
-#if !defined(MBRWT_AB_NOSTORE)
-#if !defined(MBRWT_AB_PLAINSTORE)
-        // (non-temporal: the temp region is read once, by k_compact_tiles;
-        // the stores then disturb the random block reads less -- C4 kernel
-        // 0.262 -> 0.255 ms, step 0.348 -> 0.333 ms; the same hint on the
-        // compaction's CSR stores made the two-stream step slower again,
-        // 0.344 ms: profiles/r05/v21_temp_stores)
-        if (lane < nr)
-            __builtin_nontemporal_store((uint16_t)(cnt | (lng ? 0x8000u : 0u)),
-                                        (AS_GLOBAL uint16_t *)(uintptr_t)(reinterpret_cast<uint16_t *>(treg) + lane));
-#else
-        if (lane < nr) gst(reinterpret_cast<uint16_t *>(treg) + lane, (uint16_t)(cnt | (lng ? 0x8000u : 0u)));
-#endif
-#endif
-        AB_STAMP(1);
+        uint8_t *treg = FUSED ? nullptr : p.temp + t * (uint64_t)(128 + 2 * C);
+        // FUSED: rows walked from global memory (a direct tile's rows, long
+        // records) are walked once before the tile's total is published, so a
+        // record that does not walk raises the error bit that travels with it
+        const bool gw = direct ? (valid && cnt > 0) : lng;
+        const bool any_gw = FUSED && __any(gw);
+        uint32_t err = 0;
+        // FUSED: a tile hands its total to the scan wave (LDS)
+        auto hand_in = [&]() {
+            if (lane == 0) {
+                s_tot[wv] = total;
+                if (err) __hip_atomic_fetch_or(&s_err, err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&s_arrive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        };
+        if constexpr (FUSED) {
+            err = __any(lane < nr && !valid) ? 1u : 0u;
+            if (!any_gw) hand_in();
+        } else {
+            // (non-temporal: the temp region is read once, by k_compact_tiles;
+            // the stores then disturb the random block reads less -- C4 kernel
+            // 0.262 -> 0.255 ms, step 0.348 -> 0.333 ms; the same hint on the
+            // compaction's CSR stores made the two-stream step slower again,
+            // 0.344 ms: profiles/r05/v21_temp_stores)
+            if (lane < nr)
+                __builtin_nontemporal_store((uint16_t)(cnt | (lng ? 0x8000u : 0u)),
+                                            (AS_GLOBAL uint16_t *)(uintptr_t)(reinterpret_cast<uint16_t *>(treg) + lane));
+        }
         if (!direct) {
-#if defined(MBRWT_AB_NOWALK)
-            const bool live = false;  // (timing only: no walk)
-#else
             const bool live = valid && cnt > 0 && !lng;
-#endif
             if constexpr (WALK == WALK_ODOMETER || WALK == WALK_TREE_ODOMETER) {
                 // the odometer into the wave's LDS label stage, then the
                 // tile's labels as 16-byte vector stores (a few wide stores
                 // instead of one scattered 2-byte store per label: the r03
                 // SQ/TA counters showed the texture-address unit as the
                 // busiest unit)
-                AS_LDS uint16_t *stage = (AS_LDS uint16_t *)(wb + 64u * PB + 256u * p.stk_words);
                 if constexpr (WALK == WALK_TREE_ODOMETER) {
 #define MBRWT_TREE_CASE(K)                                                        \
     case K:                                                                       \
         if (p.mask1)                                                              \
-            rows_walk_tree<K, true>(rec, o, live, root, ent, lst, stage, pos);         \
+            rows_walk_tree<K, true>(rec, o, live, root, ent, lst, stage, pos);    \
         else                                                                      \
-            rows_walk_tree<K, false>(rec, o, live, root, ent, lst, stage, pos);        \
+            rows_walk_tree<K, false>(rec, o, live, root, ent, lst, stage, pos);   \
         break;
                     switch (p.frames) {
                         MBRWT_TREE_CASE(1)
@@ -1487,11 +1592,7 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
 #undef MBRWT_TREE_CASE
                 } else if (ptw) {
                     const AS_LDS uint16_t *ptab = (const AS_LDS uint16_t *)((const AS_LDS uint32_t *)lds_rows + ptw + 1);
-#if defined(MBRWT_AB_NOLIN)
-                    const bool lin = false;  // (A/B: always read the path table)
-#else
                     const bool lin = (pA >> 31) != 0u;
-#endif
 #define MBRWT_PATH_CASE(K)                                                      \
     case K:                                                                     \
         if (lin)                                                                \
@@ -1518,22 +1619,14 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
                     }
                 }
                 wave_sync();
-                AB_STAMP(2);
-                // (r05: rounding the copy up to whole 128-byte lines helped plain
-                // stores by 1.5 % and non-temporal ones not at all: not kept)
-                const uint32_t nbytes = total * 2;
-#if !defined(MBRWT_AB_NOSTORE)
-                for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
-#if !defined(MBRWT_AB_PLAINSTORE)
-                    __builtin_nontemporal_store(*(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2),
-                                                (AS_GLOBAL u32x4_t *)(uintptr_t)(treg + 128 + q2));
-#else
-                    gst(reinterpret_cast<u32x4_t *>(treg + 128 + q2),
-                        *(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2));
-#endif
-#else
-                (void)nbytes;  // (timing only: no temp-region stores)
-#endif
+                if constexpr (!FUSED) {
+                    // (r05: rounding the copy up to whole 128-byte lines helped
+                    // plain stores by 1.5 % and non-temporal ones not at all)
+                    const uint32_t nbytes = total * 2;
+                    for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
+                        __builtin_nontemporal_store(*(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2),
+                                                    (AS_GLOBAL u32x4_t *)(uintptr_t)(treg + 128 + q2));
+                }
             } else if constexpr (WALK == WALK_MASK1) {
                 rows_walk6(mine, o, live, root, ent, lst, stk,
                            (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128), pos);
@@ -1541,25 +1634,74 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
                 rows_walk4(mine, o, live, root, ent, lst, stk, reinterpret_cast<uint16_t *>(treg + 128), pos);
             }
         }
-        if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u) | (has_long ? 0x40000000u : 0u));
+        if constexpr (FUSED) {
+            // the block slots hold the global walks' frames from here on
+            AS_LDS uint32_t *gstk = (AS_LDS uint32_t *)wb + lane;
+            if (any_gw) {
+                wave_sync();
+                const bool ok = !gw || rows_walk_global<B>(p, rec_row, nullptr, gstk);
+                err |= __any(!ok) ? 2u : 0u;
+                hand_in();
+            }
+            // the workgroup's prefix from the scan wave, then this tile's
+            while (__hip_atomic_load(&s_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+                __builtin_amdgcn_s_sleep(1);
+            uint64_t ex = s_base;
+            for (uint32_t w = 0; w < wv; ++w) ex += s_tot[w];
+            const uint32_t errs = s_errs;
+            const uint64_t tot = ex + total;
+            if (lane < nr)
+                __builtin_nontemporal_store(ex + pos, (AS_GLOBAL uint64_t *)(uintptr_t)(p.offsets + r0 + lane));
+            if (t == ntiles - 1 && lane == 0) {  // the batch's end: its total and the call's status
+                gst(p.offsets + p.n, tot);
+                const uint64_t st = (errs & 2u)   ? MBRWT_ERR_DEVICE
+                                    : (errs & 1u) ? MBRWT_ERR_RANGE
+                                    : tot > p.cap ? MBRWT_ERR_CAPACITY
+                                                  : MBRWT_OK;
+                p.status[0] = tot;
+                p.status[1] = st;
+                atomicOr(&p.status[2], 1ull << st);
+            }
+            if (tot <= p.cap) {
+                if (!direct) {
+                    // u16 stage -> u32 labels at ex: whole 16-byte stores on
+                    // 16-byte boundaries of the CSR (lead = ex mod 4 labels
+                    // before the first boundary), single stores at the ends
+                    uint32_t *dst = p.cols + (ex & ~3ull);
+                    const uint32_t lead = (uint32_t)ex & 3u, span = total + lead;
+                    for (uint32_t i4 = lane * 4; i4 < span; i4 += 256) {
+                        const int32_t l0 = (int32_t)i4 - (int32_t)lead;
+                        uint32_t v[4];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const int32_t li = l0 + k;
+                            v[k] = (li >= 0 && li < (int32_t)total) ? (uint32_t)stage[li] : 0u;
+                        }
+                        if (l0 >= 0 && l0 + 4 <= (int32_t)total) {
+                            __builtin_nontemporal_store(u32x4_t{v[0], v[1], v[2], v[3]},
+                                                        (AS_GLOBAL u32x4_t *)(uintptr_t)(dst + i4));
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                const int32_t li = l0 + k;
+                                if (li >= 0 && li < (int32_t)total)
+                                    __builtin_nontemporal_store(v[k], (AS_GLOBAL uint32_t *)(uintptr_t)(dst + i4 + k));
+                            }
+                        }
+                    }
+                }
+                if (any_gw) {
+                    // (a long record's labels overwrite the places the copy
+                    // above filled for it: other lanes' stores, hence the fence)
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (gw) (void)rows_walk_global<B>(p, rec_row, p.cols + ex + pos, gstk);
+                }
+            }
+        } else {
+            if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u) | (has_long ? 0x40000000u : 0u));
+        }
         wave_sync();  // the slots are reused
-        AB_STAMP(3);
-#if defined(MBRWT_AB_STAMPS)
-        ++ab_tiles;
-#endif
     }
-#if defined(MBRWT_AB_GATHER)
-    if (ab_acc == 0x9E3779B9u) p.scalars[3] = ab_acc;  // (keeps the loads alive)
-#endif
-#if defined(MBRWT_AB_STAMPS)
-    AB_STAMP(4);
-    const uint32_t gw = blockIdx.x * WPB + wv;
-    if (lane < kAbStampWords && gw < kAbStampWaves) {
-        uint64_t v = lane < 5 ? ab_ph[lane] : lane == 5 ? ab_tiles : lane == 6 ? ab_last - ab_t0 : 1;
-        gst(reinterpret_cast<unsigned long long *>(g_ab_stamps) + gw * kAbStampWords + lane, (unsigned long long)v);
-    }
-#endif
-#undef AB_STAMP
 }
 
 // tile regions -> CSR: one wave per TPW consecutive tiles (every load of
@@ -1623,10 +1765,10 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
         const uint64_t r0 = t * 64;
         tc[k] = in ? gld(p.tile_counts + t) : 0x80000000u;
         base[k] = in ? gld(p.tile_offsets + t) : 0;
-        cnt[k] = (in && r0 + lane < n) ? (uint32_t)ab_ld(reinterpret_cast<const uint16_t *>(treg) + lane) : 0u;  // (bit 15: long)
+        cnt[k] = (in && r0 + lane < n) ? (uint32_t)gld(reinterpret_cast<const uint16_t *>(treg) + lane) : 0u;  // (bit 15: long)
         const uint16_t *lab = reinterpret_cast<const uint16_t *>(treg + 128);
 #pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) v[k][j] = ab_ld(lab + lane + 64 * j);  // (C >= 1024: inside the region)
+        for (uint32_t j = 0; j < 8; ++j) v[k][j] = gld(lab + lane + 64 * j);  // (C >= 1024: inside the region)
     }
 #pragma unroll
     for (uint32_t k = 0; k < kCompactTpw; ++k) {
@@ -1655,7 +1797,7 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
 #pragma unroll
             for (uint32_t j = 0; j < 8; ++j) {
                 const uint32_t i = i0 + lane + 64 * j;
-                w[j] = i < tot ? (uint32_t)ab_ld(lab + i) : 0u;
+                w[j] = i < tot ? (uint32_t)gld(lab + i) : 0u;
             }
 #pragma unroll
             for (uint32_t j = 0; j < 8; ++j) {
@@ -1811,21 +1953,22 @@ constexpr uint32_t kRowsWpb = 8;
 // 8-wave workgroups per CU (16 waves); two of 11 waves fit (22)
 constexpr uint32_t kRowsWpbWide = 11;
 template <int B, bool NT>
-RowsFn rows_fn_b(uint32_t walk, uint32_t wpb) {
-    if (wpb == kRowsWpbWide) return k_traverse_rows<B, kRowsWpbWide, NT, WALK_TREE_ODOMETER>;
-    return walk == WALK_ODOMETER        ? k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER>
-           : walk == WALK_TREE_ODOMETER ? k_traverse_rows<B, kRowsWpb, NT, WALK_TREE_ODOMETER>
-           : walk == WALK_MASK1         ? k_traverse_rows<B, kRowsWpb, NT, WALK_MASK1>
-                                 : k_traverse_rows<B, kRowsWpb, NT, WALK_GENERAL>;
+RowsFn rows_fn_b(uint32_t walk, uint32_t wpb, bool fused) {
+    if (fused) {
+        if (walk == WALK_ODOMETER) return k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER, true>;
+        if (wpb == kRowsWpbWide) return k_traverse_rows<B, kRowsWpbWide, NT, WALK_TREE_ODOMETER, true>;
+        return k_traverse_rows<B, kRowsWpb, NT, WALK_TREE_ODOMETER, true>;
+    }
+    if (wpb == kRowsWpbWide) return k_traverse_rows<B, kRowsWpbWide, NT, WALK_TREE_ODOMETER, false>;
+    return walk == WALK_ODOMETER        ? k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER, false>
+           : walk == WALK_TREE_ODOMETER ? k_traverse_rows<B, kRowsWpb, NT, WALK_TREE_ODOMETER, false>
+           : walk == WALK_MASK1         ? k_traverse_rows<B, kRowsWpb, NT, WALK_MASK1, false>
+                                        : k_traverse_rows<B, kRowsWpb, NT, WALK_GENERAL, false>;
 }
-RowsFn rows_fn(const RowsImage &im, uint32_t walk, uint32_t wpb) {
-#if defined(MBRWT_AB_NT0)
-    const bool nt = false;  // (A/B: plain block reads)
-#else
+RowsFn rows_fn(const RowsImage &im, uint32_t walk, uint32_t wpb, bool fused) {
     const bool nt = im.bytes > (1ull << 30);  // non-temporal block reads for images beyond the caches
-#endif
-    if (im.B == 64) return nt ? rows_fn_b<64, true>(walk, wpb) : rows_fn_b<64, false>(walk, wpb);
-    return nt ? rows_fn_b<128, true>(walk, wpb) : rows_fn_b<128, false>(walk, wpb);
+    if (im.B == 64) return nt ? rows_fn_b<64, true>(walk, wpb, fused) : rows_fn_b<64, false>(walk, wpb, fused);
+    return nt ? rows_fn_b<128, true>(walk, wpb, fused) : rows_fn_b<128, false>(walk, wpb, fused);
 }
 // resident waves per CU with workgroups of w waves: the LDS (160 KiB per CU:
 // the table once per workgroup + per_wave bytes per wave) within the 24-wave cap
@@ -1869,6 +2012,17 @@ static uint32_t rows_walk_of(const Ctx &c) {
     return im.mask1 ? WALK_MASK1 : WALK_GENERAL;
 }
 
+// the one-pass traversal (FUSED, r06) for this context's get_rows: the
+// odometer walks on block records; the global walks' frames fit the wave's
+// block slots
+bool rows_one_pass(const Ctx &c) {
+    const RowsImage &im = c.rows;
+    if (!im.ready || im.var || !c.rows_fused || !im.d_table) return false;
+    const uint32_t walk = rows_walk_of(c);
+    const uint32_t stk_lim = std::max(1u, std::min(im.height, kRowsMaxHeight));
+    return (walk == WALK_ODOMETER || walk == WALK_TREE_ODOMETER) && 256u * stk_lim <= 64u * (im.B + 4);
+}
+
 int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
                   uint64_t *needed, hipStream_t s, uint64_t *d_status) {
     const RowsImage &im = c.rows;
@@ -1888,30 +2042,47 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     const uint32_t C = rows_tile_labels(c);
     const uint64_t nt = (n + 63) / 64;
     const uint64_t region = 128 + 2ull * C;
-    // counts workspace: nt+1 tile counts | (8-byte aligned) nt+1 tile offsets
-    const uint64_t to_off = ((nt + 1) * sizeof(uint32_t) + 7) / 8 * 8;
-    if ((rc = ensure(c.ws_temp, nt * region))) return rc;
-    // [tile counts | tile offsets | the kernel's own counters (4 x u64)]
-    const uint64_t sc_off = to_off + (nt + 1) * sizeof(uint64_t);
-    const bool fresh = c.ws_counts.bytes < sc_off + 32;
-    if ((rc = ensure(c.ws_counts, sc_off + 32))) return rc;
-    unsigned long long *d_sc = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + sc_off);
-    if (fresh || c.rows_sc_dirty || c.rows_sc_at != sc_off) {  // the counters are cleared by k_compact_tiles
-        MBRWT_HIP(hipMemsetAsync(d_sc, 0, 32, s));
-        c.rows_sc_dirty = false;
-        c.rows_sc_at = sc_off;
-    }
-    uint32_t *d_tc = reinterpret_cast<uint32_t *>(c.ws_counts.buf);
-    uint64_t *d_to = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + to_off);
-    hipcub::TransformInputIterator<uint64_t, MaskTile, const uint32_t *> it(d_tc, MaskTile());
+    const uint32_t walk = rows_walk_of(c);
+    const uint32_t stk_lim = std::max(1u, std::min(im.height, kRowsMaxHeight));
+    const bool fused = rows_one_pass(c);
+    uint32_t *d_tc = nullptr;
+    uint64_t *d_to = nullptr;
+    unsigned long long *d_sc = nullptr;
     size_t scan_bytes = 0;
-    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, it, d_to, nt, s));
-    if ((rc = ensure(c.ws_scan, scan_bytes))) return rc;
+    if (fused) {
+        // look-back descriptors: cleared when (re)allocated and when the
+        // 16-bit epoch wraps, so no earlier call's granule carries this epoch
+        const size_t had = c.ws_desc.bytes;
+        if ((rc = ensure(c.ws_desc, (nt + 1) * sizeof(uint64_t)))) return rc;
+        if (c.ws_desc.bytes != had || c.desc_epoch >= 0xFFFFu) {
+            MBRWT_HIP(hipMemsetAsync(c.ws_desc.buf, 0, c.ws_desc.bytes, s));
+            c.desc_epoch = 0;
+        }
+        ++c.desc_epoch;
+    } else {
+        // counts workspace: nt+1 tile counts | (8-byte aligned) nt+1 tile offsets
+        const uint64_t to_off = ((nt + 1) * sizeof(uint32_t) + 7) / 8 * 8;
+        if ((rc = ensure(c.ws_temp, nt * region))) return rc;
+        // [tile counts | tile offsets | the kernel's own counters (4 x u64)]
+        const uint64_t sc_off = to_off + (nt + 1) * sizeof(uint64_t);
+        const bool fresh = c.ws_counts.bytes < sc_off + 32;
+        if ((rc = ensure(c.ws_counts, sc_off + 32))) return rc;
+        d_sc = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + sc_off);
+        if (fresh || c.rows_sc_dirty || c.rows_sc_at != sc_off) {  // the counters are cleared by k_compact_tiles
+            MBRWT_HIP(hipMemsetAsync(d_sc, 0, 32, s));
+            c.rows_sc_dirty = false;
+            c.rows_sc_at = sc_off;
+        }
+        d_tc = reinterpret_cast<uint32_t *>(c.ws_counts.buf);
+        d_to = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + to_off);
+        hipcub::TransformInputIterator<uint64_t, MaskTile, const uint32_t *> it(d_tc, MaskTile());
+        MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, it, d_to, nt, s));
+        if ((rc = ensure(c.ws_scan, scan_bytes))) return rc;
+    }
     // the call's status block: the caller's (asynchronous) or the context's
     unsigned long long *st_blk =
         reinterpret_cast<unsigned long long *>(d_status ? d_status : c.d_scalars);
 
-    const uint32_t walk = rows_walk_of(c);
     RowsParams p{};
     p.rows = d_rows;
     p.n = n;
@@ -1925,10 +2096,17 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     p.table_words = (uint32_t)im.table2.size();
     p.table = im.d_table2;
     p.C = C;
-    p.temp = reinterpret_cast<uint8_t *>(c.ws_temp.buf);
+    p.temp = fused ? nullptr : reinterpret_cast<uint8_t *>(c.ws_temp.buf);
     p.tile_counts = d_tc;
     p.scalars = d_sc;
     p.status = st_blk;
+    p.desc = fused ? reinterpret_cast<uint64_t *>(c.ws_desc.buf) : nullptr;
+    p.epoch = c.desc_epoch;
+    p.offsets = d_offsets;
+    p.cols = d_cols;
+    p.cap = cap;
+    p.rwt = im.d_table;
+    p.stk_lim = stk_lim;
     p.uni = im.uni;
     p.path_walk = c.rows_walk == 7 ? 0u : 1u;  // (7: the r03 odometer, A/B)
     p.stk_words = walk >= WALK_ODOMETER ? 0u : rows_stack_words(im);  // (the odometers keep no stack)
@@ -1942,13 +2120,9 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
                               rows_waves_per_cu(table_bytes, per_wave, kRowsWpb))
                              ? kRowsWpbWide
                              : kRowsWpb;
-    const RowsFn kfn = rows_fn(im, walk, wpb);
-#if defined(MBRWT_AB_LDS_PAD)
-    const size_t lds = table_bytes + wpb * per_wave + MBRWT_AB_LDS_PAD;  // (A/B: fewer resident workgroups)
-#else
+    const RowsFn kfn = rows_fn(im, walk, wpb, fused);
     const size_t lds = table_bytes + wpb * per_wave;
-#endif
-    const uint32_t threads = 64 * wpb;
+    const uint32_t threads = 64 * (wpb + (fused ? 1u : 0u));  // (FUSED: + the scan wave)
     // at most 24 waves (3 workgroups of 8) per CU: more waves make the walk phase
     // slower than the extra loads in flight gain (C4 0.426 ms at 3 against
     // 0.456 at 4, C2 0.068 against 0.073: profiles/r03/v06_rows_occupancy_*);
@@ -1973,7 +2147,7 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         c.rb_blocks = std::max(1, dev_cus) * per_cu;
     }
 
-    c.rows_sc_dirty = true;  // until k_compact_tiles has run
+    if (!fused) c.rows_sc_dirty = true;  // until k_compact_tiles has run
     hipEvent_t e0 = c.ev0, e1 = c.ev1;
     if (c.timing && d_status) {  // asynchronous calls: one event pair per call, summed by mbrwt_take_timing
         if (c.async_ev.size() <= c.async_used) {
@@ -1993,7 +2167,9 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         // tree odometer's table -- 8.8 KB at the greedy + relax shape -- is
         // staged once per workgroup: one tile per wave took 0.518 against
         // 0.458 ms there, profiles/r05)
-        const bool persistent = walk != WALK_ODOMETER;
+        // (the one-pass form never runs persistent: a wave waits on the tiles
+        // before its own, so every wave must be dispatchable in tile order)
+        const bool persistent = walk != WALK_ODOMETER && !fused;
         const uint64_t per_wg = (uint64_t)wpb * kRowsTilesPerWave;
         const uint64_t g = persistent
                                ? std::max<uint64_t>(1, std::min<uint64_t>((nt + wpb - 1) / wpb, (uint64_t)c.rb_blocks))
@@ -2002,8 +2178,9 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         MBRWT_HIP(hipGetLastError());
     }
     if (c.timing) MBRWT_HIP(hipEventRecord(e1, s));
-    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_to, nt, s));
-    {
+    if (!fused) {
+        hipcub::TransformInputIterator<uint64_t, MaskTile, const uint32_t *> it(d_tc, MaskTile());
+        MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_to, nt, s));
         CompactParams cp{};
         cp.temp = p.temp;
         cp.C = C;
@@ -2021,12 +2198,12 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         cp.v = view_of(c);
         cp.table = im.d_table;
         const uint64_t waves = (nt + kCompactTpw - 1) / kCompactTpw;
-        cp.stk_lim = std::max(1u, std::min(im.height, kRowsMaxHeight));
+        cp.stk_lim = stk_lim;
         hipLaunchKernelGGL(k_compact_tiles, dim3((unsigned)((waves + 3) / 4)), dim3(256),
                            (size_t)256 * cp.stk_lim * 4, s, cp);
         MBRWT_HIP(hipGetLastError());
+        c.rows_sc_dirty = false;
     }
-    c.rows_sc_dirty = false;
     if (d_status) return MBRWT_OK;  // no host synchronisation: the status lands on the stream
     MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     MBRWT_HIP(hipStreamSynchronize(s));
@@ -2053,20 +2230,6 @@ __global__ void k_set_status(unsigned long long *status, uint64_t need, uint64_t
     status[2] |= 1ull << st;
 }
 }  // namespace
-
-#if defined(MBRWT_AB_STAMPS)
-// A/B diagnostics: the per-wave phase cycles of the last k_traverse_rows
-// launch (waves x 8 words: load, parse + scan, walk, output, loop, tiles,
-// total, written) -- then cleared
-extern "C" int mbrwt_ab_stamps(uint64_t *out, uint64_t words) {
-    const uint64_t n = std::min<uint64_t>(words, (uint64_t)kAbStampWaves * kAbStampWords);
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ab_stamps), n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-    static const std::vector<unsigned long long> zero((size_t)kAbStampWaves * kAbStampWords, 0ull);
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_ab_stamps), zero.data(), zero.size() * 8, 0, hipMemcpyHostToDevice) != hipSuccess)
-        return 1;
-    return 0;
-}
-#endif
 
 int rows_set_status(uint64_t *d_status, uint64_t need, int rc, hipStream_t s) {
     hipLaunchKernelGGL(k_set_status, dim3(1), dim3(1), 0, s, reinterpret_cast<unsigned long long *>(d_status), need,

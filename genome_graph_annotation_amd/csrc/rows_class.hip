@@ -245,10 +245,17 @@ struct Scratch {
     ~Scratch() {
         for (void *x : p) (void)hipFree(x);
     }
+    // null when the device has no room -- a tolerated failure (the caller
+    // keeps the block image), so HIP's sticky last error is cleared: the
+    // next MBRWT_HIP(hipGetLastError()) of the same create call must not
+    // fail the whole build with it
     template <class T>
     T *get(uint64_t count) {
         void *x = nullptr;
-        if (hipMalloc(&x, std::max<uint64_t>(1, count) * sizeof(T)) != hipSuccess) return nullptr;
+        if (hipMalloc(&x, std::max<uint64_t>(1, count) * sizeof(T)) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
         p.push_back(x);
         return static_cast<T *>(x);
     }
@@ -292,10 +299,23 @@ int rows_classes_build(RowsImage &im, uint64_t n, int mode, uint64_t *sample_dis
         if (distinct * 10 > m * 9) return MBRWT_OK;
     }
 
-    // every row: (hash, row) sorted by hash; 32 bytes a row of scratch
+    // every row: (hash, row) sorted by hash -- four u64 arrays of n, the
+    // sort's and the scan's temporary storage (hipcub's own figures), and the
+    // class index at its widest (u32 per row); the build is skipped without
+    // that much free memory, not failed
+    size_t tb = 0, qb = 0;
+    {
+        hipcub::CountingInputIterator<uint64_t> it0(0);
+        hipcub::TransformInputIterator<uint64_t, HeadFlag, hipcub::CountingInputIterator<uint64_t>> h0(
+            it0, HeadFlag{nullptr});
+        MBRWT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (uint64_t *)nullptr, (uint64_t *)nullptr,
+                                                     (uint64_t *)nullptr, (uint64_t *)nullptr, n, 0, 64, s));
+        MBRWT_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, qb, h0, (uint64_t *)nullptr, n, s));
+    }
     size_t free_b = 0, total_b = 0;
     MBRWT_HIP(hipMemGetInfo(&free_b, &total_b));
-    if ((double)n * 34.0 + (256ull << 20) > (double)free_b) return MBRWT_OK;
+    const double need_b = 32.0 * (double)n + (double)std::max(tb, qb) + 4.0 * (double)n + (double)(256ull << 20);
+    if (need_b > (double)free_b) return MBRWT_OK;
     uint64_t *keys_in = sc.get<uint64_t>(n), *vals_in = sc.get<uint64_t>(n);
     uint64_t *keys = sc.get<uint64_t>(n), *rows = sc.get<uint64_t>(n);
     if (!keys_in || !vals_in || !keys || !rows) return MBRWT_OK;
@@ -304,9 +324,6 @@ int rows_classes_build(RowsImage &im, uint64_t n, int mode, uint64_t *sample_dis
     MBRWT_HIP(hipGetLastError());
     hipcub::CountingInputIterator<uint64_t> it(0);
     hipcub::TransformInputIterator<uint64_t, HeadFlag, hipcub::CountingInputIterator<uint64_t>> heads(it, HeadFlag{keys});
-    size_t tb = 0, qb = 0;
-    MBRWT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys_in, keys, vals_in, rows, n, 0, 64, s));
-    MBRWT_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, qb, heads, keys_in, n, s));
     void *tmp = sc.get<uint8_t>(std::max(tb, qb));
     if (!tmp) return MBRWT_OK;
     MBRWT_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys_in, keys, vals_in, rows, n, 0, 64, s));
@@ -323,7 +340,10 @@ int rows_classes_build(RowsImage &im, uint64_t n, int mode, uint64_t *sample_dis
     while (w < 32 && (1ull << w) < D) ++w;
     const uint64_t index_words = (n * w + 31) / 32 + 2;  // (+2: class_field reads the next word)
     uint32_t *index = nullptr;
-    if (hipMalloc(&index, index_words * 4) != hipSuccess) return MBRWT_OK;
+    if (hipMalloc(&index, index_words * 4) != hipSuccess) {
+        (void)hipGetLastError();  // (tolerated: keep the block image)
+        return MBRWT_OK;
+    }
     MBRWT_HIP(hipMemsetAsync(index, 0, index_words * 4, s));
     hipLaunchKernelGGL(k_class_assign, dim3((unsigned)grid_of(n)), dim3(256), 0, s, v, im.d_table, rows, cid1, rep, n,
                        w, index, d_err);
@@ -345,6 +365,7 @@ int rows_classes_build(RowsImage &im, uint64_t n, int mode, uint64_t *sample_dis
     uint8_t *dblocks = nullptr, *dspill = nullptr;
     const uint64_t spill_cap = spill_bytes + kClassB + 256;
     if (hipMalloc(&dblocks, D * kClassB) != hipSuccess || hipMalloc(&dspill, spill_cap) != hipSuccess) {
+        (void)hipGetLastError();  // (tolerated: keep the block image)
         if (dblocks) (void)hipFree(dblocks);
         (void)hipFree(index);
         return MBRWT_OK;

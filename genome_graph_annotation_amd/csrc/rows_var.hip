@@ -826,11 +826,7 @@ int var_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets
     p.U = (uint32_t)im.var_units.size();
     p.CR = CR;
     p.CS = CS;
-#if defined(MBRWT_AB_NO_USTRIDE)
-    p.ustride = 0;  // (A/B: the unit table)
-#else
     p.ustride = im.var_ustride;
-#endif
     p.scalars = d_sc;
     p.status = st_blk;
     const VarFn kfn = var_fn(G);

@@ -263,9 +263,9 @@ class DeviceAllGatherV:
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        if len(rows_per_rank) != self.world:
-            raise ValueError(f"rows_per_rank has {len(rows_per_rank)} entries for a group of {self.world} ranks")
         self.ns = [int(x) for x in rows_per_rank]
+        # (the entry count is checked inside the collective: a local raise
+        # here would leave the other ranks blocked in its all-reduce)
         self.cap = _agree_wire(self.ns, int(labels_cap), int(num_columns), group, device)
         self.bits_l, self.bits_c = wire_bits(num_columns)
         n_max = max(self.ns)
@@ -396,8 +396,18 @@ def _agree_wire(ns, labels_cap, num_columns, group, device):
     three must be equal on every rank.  Returns the group's largest
     labels_cap; raises ValueError on EVERY rank (they all see the same
     reduced values) when rows_per_rank or num_columns differ."""
-    v = [labels_cap, num_columns, len(ns)] + list(ns)
     on = device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    world = dist.get_world_size(group)
+    # first the entry counts, in a reduction of fixed size (ranks with lists
+    # of different lengths would otherwise enter all-reduces of different
+    # sizes: RCCL hangs, gloo times out), so every rank raises alike (ADVICE r05)
+    k = torch.tensor([len(ns), -len(ns)], dtype=torch.int64, device=on)
+    dist.all_reduce(k, op=dist.ReduceOp.MAX, group=group)
+    k_hi, k_lo = int(k[0].item()), -int(k[1].item())
+    if k_hi != k_lo or k_hi != world:
+        raise ValueError(f"DeviceAllGatherV: rows_per_rank has {k_lo}..{k_hi} entries over the ranks "
+                         f"for a group of {world} ranks")
+    v = [labels_cap, num_columns, len(ns)] + list(ns)
     mx = torch.tensor(v, dtype=torch.int64, device=on)
     mn = -mx  # MIN as the MAX of the negation: one reduction op for both backends
     both = torch.cat([mx, mn])

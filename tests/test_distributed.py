@@ -155,6 +155,8 @@ def _agree_worker(rank, world, port, q, mismatch):
         ns = [5, 4, 4][:world]
         if mismatch == "rows" and rank == 1:
             ns = [4, 5, 4][:world]
+        if mismatch == "length" and rank == 0:
+            ns = ns + [4]  # (one entry too many on one rank only)
         m = 2652 + (1 if mismatch == "cols" and rank == world - 1 else 0)
         try:
             cap = _agree_wire(ns, 1000 + 24 * rank, m, None, torch.device("cpu"))
@@ -165,7 +167,8 @@ def _agree_worker(rank, world, port, q, mismatch):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mismatch", [(2, None), (3, None), (2, "rows"), (3, "cols")])
+@pytest.mark.parametrize("world,mismatch", [(2, None), (3, None), (2, "rows"), (3, "cols"), (2, "length"),
+                                           (3, "length")])
 def test_device_wire_agrees_on_layout(world, mismatch):
     """DeviceAllGatherV's collective precondition (the r4c
     gloo abort): ranks that pass different label capacities agree on the
@@ -187,5 +190,5 @@ def test_device_wire_agrees_on_layout(world, mismatch):
     else:
         assert all(r[1] == "error" for r in res), res
         assert len({r[2] for r in res}) == 1, res  # the same message on every rank
-        assert ("rows_per_rank" if mismatch == "rows" else "num_columns") in res[0][2]
+        assert ("num_columns" if mismatch == "cols" else "rows_per_rank") in res[0][2]
     assert all(p.exitcode == 0 for p in procs)

@@ -102,3 +102,33 @@ def test_host_pipeline_dense_chunks(oracle_mod):
     off_d, cols_d = dev.get_rows(q)
     np.testing.assert_array_equal(off_d, off_o)
     np.testing.assert_array_equal(cols_d, cols_o)
+
+
+@pytest.mark.parametrize("fail_at", [1, 3])
+def test_host_pipeline_error_drains_inflight_copies(c2, fail_at):
+    """An error return in the middle of a batch (an injected NOMEM when chunk
+    `fail_at` is issued, MBRWT_OPT_TEST_FAIL_CHUNK) comes back only after the
+    chunks already queued have finished: nothing lands in the caller's
+    page-locked buffers after the call returned, and the context
+    answers correctly afterwards."""
+    import time
+    import torch
+    from genome_graph_annotation_amd import _lib as L
+    dev, ref, n = c2
+    q = np.random.default_rng(9).integers(0, n, 5 * (1 << 20) + 77, dtype=np.uint64)
+    rows = torch.from_numpy(q.view(np.int64)).pin_memory()
+    offsets = torch.zeros(len(q) + 1, dtype=torch.int64).pin_memory()
+    cols = torch.zeros(len(q) * 12, dtype=torch.int32).pin_memory()
+    dev.set_option(L.MBRWT_OPT_TEST_FAIL_CHUNK, fail_at)
+    try:
+        st, _ = _call(dev, rows, offsets, cols, cols.numel())
+    finally:
+        dev.set_option(L.MBRWT_OPT_TEST_FAIL_CHUNK, -1)
+    assert st == L.MBRWT_ERR_NOMEM
+    snap_o, snap_c = offsets.clone(), cols.clone()
+    time.sleep(0.3)  # (a DMA still running would change the buffers now)
+    assert torch.equal(offsets, snap_o) and torch.equal(cols, snap_c)
+    off_o, cols_o = ref.get_rows(q[:300_000])
+    off_d, cols_d = dev.get_rows(q[:300_000])
+    np.testing.assert_array_equal(off_d, off_o)
+    np.testing.assert_array_equal(cols_d, cols_o)

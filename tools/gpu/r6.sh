@@ -1,0 +1,27 @@
+# r06 GPU steps (run from the repo root:
+#   /usr/local/graft/bin/gpurun --timeout 900 -- bash tools/gpu/r6.sh STAGE)
+# Every GPU step has its own time limit, steps chain with &&, a heartbeat
+# file shows progress.  Outputs: gpurun_out/r6_STAGE/ (copied to profiles/r06/).
+set -o pipefail
+STAGE="$1"
+O=gpurun_out/r6_$STAGE; mkdir -p $O
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+( for i in $(seq 1 30); do sleep 60; echo "heartbeat $i $(date +%T)" >> $O/heartbeat.log; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+PYT="python -u -m pytest -v --timeout 300 --timeout-method thread"
+B="python -u bench.py --no-e2e --no-probe --traffic off"
+case "$STAGE" in
+onepass)  # the one-pass traversal: row-record tests, then a same-box A/B against the two-kernel path
+  timeout -k 10 700 $PYT tests/test_gpu_rows.py -k "one_pass or odometer or tree_odometer or errors or async or clone or synthetic_c2 or greedy_relax" > $O/pytest_rows.log 2>&1 &&
+  timeout -k 10 300 $B --rows-fused 1 > $O/bench_fused_parity.log 2>&1 &&
+  timeout -k 10 120 $B --no-cpu --rows-fused 0 > $O/bench_twokernel_1.log 2>&1 &&
+  timeout -k 10 120 $B --no-cpu --rows-fused 1 > $O/bench_fused_1.log 2>&1 &&
+  timeout -k 10 120 $B --no-cpu --rows-fused 0 > $O/bench_twokernel_2.log 2>&1 &&
+  timeout -k 10 120 $B --no-cpu --rows-fused 1 > $O/bench_fused_2.log 2>&1
+  ;;
+rows)  # the row-record GPU tests (one-pass option included) + host pipeline + classes
+  timeout -k 10 700 $PYT tests/test_gpu_rows.py tests/test_gpu_hostpipe.py tests/test_gpu_classes.py > $O/pytest_rows.log 2>&1
+  ;;
+*) echo "unknown stage $STAGE"; exit 2 ;;
+esac
