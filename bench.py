@@ -98,8 +98,6 @@ def parse():
     ap.add_argument("--check-rows", type=int, default=0,
                     help="rows checked element-wise against the oracle (0 = the whole global batch)")
     ap.add_argument("--kernel", type=int, default=0, help="MBRWT_OPT_KERNEL variant (0 = library default)")
-    ap.add_argument("--rows-fused", type=int, default=0, choices=[0, 1],
-                    help="row records: 0 traversal + scan + compaction (library default), 1 the one-pass traversal")
     ap.add_argument("--query-streams", type=int, default=2, choices=[1, 2],
                     help="N = 1: consecutive batches alternate between the context and a clone of it "
                          "(mbrwt_ctx_clone: the same image, separate workspaces) on the default stream and "
@@ -145,8 +143,7 @@ def kernel_source_hash():
 
 def workload_args(a):
     return ["--rows", str(a.rows), "--cols", str(a.cols), "--density", repr(a.density), "--arity", str(a.arity),
-            "--batch", str(a.batch), "--seed", str(a.seed), "--kernel", str(a.kernel), "--layout", a.layout,
-            "--rows-fused", str(a.rows_fused)]
+            "--batch", str(a.batch), "--seed", str(a.seed), "--kernel", str(a.kernel), "--layout", a.layout]
 
 
 def pmc_pass(a):
@@ -157,8 +154,6 @@ def pmc_pass(a):
     mat = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, device=0, layout=a.layout)
     if a.kernel:
         mat.set_option(L.MBRWT_OPT_KERNEL, a.kernel)
-    if a.layout in ("rows", "both"):
-        mat.set_option(L.MBRWT_OPT_ROWS_FUSED, a.rows_fused)
     rows_np = np.random.default_rng(a.seed).integers(0, a.rows, a.batch, dtype=np.uint64)
     rows_t = torch.from_numpy(rows_np.view(np.int64)).cuda()
     off_t = torch.empty(a.batch + 1, dtype=torch.int64, device="cuda")
@@ -189,7 +184,7 @@ def live_traffic(a, kernel_re):
     two dispatches are warm-up."""
     out = {"counters": {}, "source_hash": kernel_source_hash(), "kernel_regex": kernel_re,
            "config": {"rows": a.rows, "cols": a.cols, "density": a.density, "arity": a.arity, "batch": a.batch,
-                      "kernel": a.kernel, "layout": a.layout, "rows_fused": a.rows_fused}}
+                      "kernel": a.kernel, "layout": a.layout}}
     env = dict(os.environ, TMPDIR="/tmp")
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="bench_pmc_", dir="/tmp")
@@ -224,7 +219,7 @@ def committed_traffic(a, kernel_re):
     """A committed live-traffic summary (profiles/*/traffic_*.json) of this
     workload measured on the CURRENT kernel sources, or None."""
     want_cfg = {"rows": a.rows, "cols": a.cols, "density": a.density, "arity": a.arity, "batch": a.batch,
-                "kernel": a.kernel, "layout": a.layout, "rows_fused": a.rows_fused}
+                "kernel": a.kernel, "layout": a.layout}
     h = kernel_source_hash()
     hit = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic_*.json"))):
@@ -413,9 +408,6 @@ def main():
         f"{mat.rows_stats()})")
     if a.kernel:
         mat.set_option(L.MBRWT_OPT_KERNEL, a.kernel)
-    if a.layout in ("rows", "both"):
-        mat.set_option(L.MBRWT_OPT_ROWS_FUSED, a.rows_fused)
-    one_pass = mat.rows_one_pass()
 
     # K distinct global batches (batch k: seed + k; batch 0 is the r01/r02
     # batch) and this rank's contiguous slice of each; timed step i queries
@@ -474,8 +466,6 @@ def main():
     qmats, qstreams, qstatus = [mat], [stream], [status_t]
     if Q == 2:
         qmats.append(mat.clone())
-        if a.layout in ("rows", "both"):
-            qmats[-1].set_option(L.MBRWT_OPT_ROWS_FUSED, a.rows_fused)
         qstreams.append(torch.cuda.Stream(dev_t))
         qstatus.append(torch.zeros(3, dtype=torch.int64, device=dev_t))
     # outputs: step i writes bufs[i mod len]; with two buffers a buffer's next
@@ -791,18 +781,7 @@ def main():
     # traffic_frac); SURVEY §8(d)'s probe-equivalent figure labelled as such
     ks = kern_ms / 1e3
     alg_bytes, alg_basis = None, None
-    if rstats is not None and not rstats.get("variable") and one_pass:
-        B = rstats["block_bytes"]
-        tiles = (nb + 63) // 64
-        spf = rstats["spilled_rows"] / a.rows
-        # row id + block + spill reload (spilled rows) read; the CSR (u64
-        # offset per row, u32 per label) written; per 64-row tile two 8-byte
-        # descriptor stores and one 512-byte look-back window read
-        alg_bytes = nb * (8 + B + 8) + nb * spf * B + 4 * labels + (16 + 512) * tiles
-        alg_basis = (f"k_traverse_rows (one pass): per row 8 B id + {B} B block + 8 B CSR offset, {B} B per "
-                     f"spilled row ({spf:.4f} of rows), 4 B per label (CSR), per 64-row tile 16 B descriptors "
-                     f"written + 512 B look-back read")
-    elif rstats is not None and not rstats.get("variable"):
+    if rstats is not None and not rstats.get("variable"):
         B = rstats["block_bytes"]
         tiles = (nb + 63) // 64
         spf = rstats["spilled_rows"] / a.rows
@@ -901,7 +880,6 @@ def main():
             "global_batch": G, "batch_per_gpu": nb, "batches": K, "layout": a.layout,
             "api": "mbrwt_get_rows_device_async" if use_async else "mbrwt_get_rows_device",
             "query_streams": Q,
-            "rows_one_pass": one_pass,
             "parallelism": f"batch-sharded x{world}, tree replicated" + ("" if world == 1 or a.no_gather
                                                                          else ", all-gatherv over " + ("RCCL" if a.dist_backend == "nccl" else a.dist_backend)
                                                                          + (" (device-sized wire, no host sync)" if wire is not None else " (host-sized)")),

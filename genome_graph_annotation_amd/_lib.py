@@ -26,7 +26,6 @@ MBRWT_OPT_SLOT_LABELS = 2
 MBRWT_OPT_KERNEL = 4
 MBRWT_OPT_ROWS_WALK = 8
 MBRWT_OPT_TEST_FAIL_CHUNK = 32  # test hook (host-buffer path)
-MBRWT_OPT_ROWS_FUSED = 16  # 1: the one-pass traversal (default), 0: traversal + scan + compaction
 
 MBRWT_BUILD_LAYOUT = 1
 MBRWT_BUILD_PARTITIONER = 2
@@ -197,7 +196,6 @@ SIGNATURES = {
     "mbrwt_strerror": (C.c_char_p, [C.c_int]),
     "mbrwt_last_error_message": (C.c_char_p, []),
     "mbrwt_traverse_kernel": (C.c_char_p, [C.c_void_p]),
-    "mbrwt_rows_one_pass": (C.c_int, [C.c_void_p]),
     # include/mbrwt_wt.h (BinRel-WT)
     "mbrwt_wt_create": (C.c_int, [C.POINTER(BinRelDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "mbrwt_wt_create_synthetic": (C.c_int, [C.POINTER(BinRelSynthDesc), C.c_int, C.POINTER(C.c_void_p)]),

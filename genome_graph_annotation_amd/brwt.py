@@ -464,10 +464,6 @@ class BRWTDevice:
     def set_option(self, option, value):
         L.check(L.lib().mbrwt_set_option(self._h, option, int(value)), "mbrwt_set_option")
 
-    def rows_one_pass(self) -> bool:
-        """get_rows runs the one-pass row-record traversal (mbrwt_rows_one_pass)."""
-        return bool(L.lib().mbrwt_rows_one_pass(self._h))
-
     def traverse_kernel(self) -> str:
         """Name of the traversal kernel get_rows launches (diagnostics)."""
         return (L.lib().mbrwt_traverse_kernel(self._h) or b"").decode()

@@ -99,7 +99,7 @@ static void release(Ctx *c) {
     }
     for (Workspace *w : {&c->ws_temp, &c->ws_counts, &c->ws_ovf, &c->ws_scan, &c->ws_rows, &c->ws_out, &c->ws_sort,
                          &c->ws_cls_off, &c->ws_cls_cols, &c->ws_class, &c->ws_sh_keys, &c->ws_sh_local, &c->ws_sh_cnt,
-                         &c->ws_sh_sort, &c->ws_sh_tmp, &c->ws_desc})
+                         &c->ws_sh_sort, &c->ws_sh_tmp})
         if (w->buf) (void)hipFree(w->buf);
     free_host_pipe(c->pipe);
     if (c->d_scalars) (void)hipFree(c->d_scalars);
@@ -707,11 +707,6 @@ int mbrwt_rows_stats(const mbrwt_ctx *ctx, uint64_t out[8]) {
     out[7] = r.height | (uint64_t)r.uni << 32;
     return MBRWT_OK;
 }
-int mbrwt_rows_one_pass(const mbrwt_ctx *ctx) {
-    if (!ctx) return 0;
-    const Ctx &c = *C(ctx);
-    return rows_one_pass(c.shards.empty() ? c : *c.shards[0]) ? 1 : 0;
-}
 int mbrwt_rows_classes(const mbrwt_ctx *ctx, uint64_t out[4]) {
     if (!ctx || !out) return MBRWT_ERR_INVALID;
     const RowsImage &r = C(ctx)->rows;
@@ -1048,10 +1043,6 @@ static int apply_option(Ctx &c, int option, int64_t value) {
         return MBRWT_OK;
     case MBRWT_OPT_TEST_FAIL_CHUNK:
         c.test_fail_chunk = value < 0 ? -1 : value;
-        return MBRWT_OK;
-    case MBRWT_OPT_ROWS_FUSED:
-        if (value != 0 && value != 1) return MBRWT_ERR_INVALID;
-        c.rows_fused = (int)value;
         return MBRWT_OK;
     case MBRWT_OPT_KERNEL:
         if (!(value >= 0 && value <= 6) && value != 10 && !(value >= 17 && value <= 20) && !(value >= 24 && value <= 30))

@@ -368,10 +368,7 @@ struct Ctx {
     uint32_t slot_labels = 0;           // 0 = auto
     int kernel_variant = 0;             // MBRWT_OPT_KERNEL (0 = default = 5)
     int rows_walk = 0;                  // MBRWT_OPT_ROWS_WALK (6: the non-odometer walk on uniform trees)
-    int rows_fused = 0;                 // MBRWT_OPT_ROWS_FUSED (1: the one-pass row-record traversal)
     int64_t test_fail_chunk = -1;       // MBRWT_OPT_TEST_FAIL_CHUNK (test hook: host_get_rows fails at that chunk)
-    Workspace ws_desc;                  // the one-pass traversal's look-back descriptors (rows.hip)
-    uint32_t desc_epoch = 0;            // their epoch of the last call (16 bits; 0 = cleared)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double timing_ms = 0;
     uint64_t timing_launches = 0;
@@ -427,7 +424,6 @@ void free_rows(RowsImage &r);
 // row-record queries (rows.hip)
 // d_status != null: asynchronous (no host synchronisation; the call's
 // {labels needed, status, sticky status bits} land in d_status on the stream)
-bool rows_one_pass(const Ctx &c);  // get_rows runs the one-pass traversal (rows.hip)
 int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
                   uint64_t *needed, hipStream_t s, uint64_t *d_status = nullptr);
 // {need, rc, sticky |= 1 << rc} into a caller's status block on the stream

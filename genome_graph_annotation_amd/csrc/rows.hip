@@ -877,16 +877,6 @@ struct RowsParams {
     uint32_t mask1;               // every mask one byte
     const uint32_t *classes;      // record classes: the packed class index (null: none; rows_class.hip)
     uint32_t class_bits;
-    // the one-pass form (FUSED): the tiles' look-back descriptors, the call's
-    // epoch, the caller's CSR and capacity, the RWT table and its frames
-    // limit (global walks)
-    uint64_t *desc;
-    uint32_t epoch;
-    uint64_t *offsets;
-    uint32_t *cols;
-    uint64_t cap;
-    const uint32_t *rwt;
-    uint32_t stk_lim;
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -1246,167 +1236,24 @@ __device__ __forceinline__ void rows_walk_tree(const AS_LDS uint8_t *pb, uint32_
 // in profiles/r05 and DESIGN.md §16.)
 constexpr uint32_t kRowsTilesPerWave = 1;
 
-// ---- the one-pass form (r06, FUSED) ---------------------------------------
-// Each tile writes its rows' offsets and labels straight into the caller's
-// CSR.  Its place there -- the labels of all tiles before it -- comes from a
-// decoupled look-back over per-tile DESCRIPTORS, one 8-byte granule per tile
-// {epoch:16 | flag:2 | error bits:2 | value:44}, stored and loaded with
-// agent-scope relaxed atomics (sc1: past the per-XCD L2s; the granule is the
-// whole message, so no fence orders it, MI355X_MICROARCH.md "R2"):
-//   * A (aggregate): the tile's label total, published as soon as its blocks
-//     are read (before its walk; before it waits on anything);
-//   * P (prefix): the inclusive label prefix, published once the tile knows
-//     its own.
-// After its walk a tile reads the 64 descriptors before it (one 512-byte
-// load): the nearest P plus the A totals after it is its exclusive prefix;
-// with no P among them it moves 64 tiles further back.  A tile only ever
-// waits for a predecessor's A, which that predecessor publishes before it
-// waits on anyone, so the waves progress whenever the waves they wait on
-// have been dispatched (in-order dispatch makes that always true); a bounded
-// spin turns anything else into MBRWT_ERR_DEVICE instead of a hang.  The
-// error bits (bit 0: a row out of range, bit 1: a record that does not walk)
-// travel with the totals, so the last tile publishes the call's status.
-// Replaces the temp region, the tile scan and k_compact_tiles (C4: 143 MB of
-// u16 labels written and read back, two more launches per batch).  Epochs
-// tell this call's descriptors from an earlier call's (the array is cleared
-// when the 16-bit epoch wraps).
-enum : uint32_t { DESC_A = 1, DESC_P = 2 };
-constexpr uint32_t kDescValueBits = 44;
-constexpr uint32_t kLookbackSpins = 1u << 22;  // (about a second of 1-2 us polls)
-__device__ __forceinline__ uint64_t desc_pack(uint32_t epoch, uint32_t flag, uint32_t err, uint64_t v) {
-    return ((uint64_t)epoch << 48) | ((uint64_t)flag << 46) | ((uint64_t)err << kDescValueBits) | v;
-}
-__device__ __forceinline__ void desc_store(uint64_t *d, uint64_t v) {
-    __hip_atomic_store((AS_GLOBAL uint64_t *)(uintptr_t)d, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t desc_load(const uint64_t *d) {
-    return __hip_atomic_load((AS_GLOBAL uint64_t *)(uintptr_t)d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// the sum over the wave of one value < 2^44 per lane (two 22-bit halves
-// through the DPP scan: 64 x 2^22 fits 32 bits)
-__device__ __forceinline__ uint64_t wave_sum44(uint64_t v) {
-    const uint32_t lo = wave_incl_sum((uint32_t)v & 0x3FFFFFu);
-    const uint32_t hi = wave_incl_sum((uint32_t)(v >> 22));
-    return ((uint64_t)__builtin_amdgcn_readlane(hi, 63) << 22) + (uint64_t)__builtin_amdgcn_readlane(lo, 63);
-}
-// the exclusive label prefix of descriptor t > 0 (the scan wave's
-// workgroup); ORs the error bits of the ones before it into errs (every lane
-// active).  (r06: letting every look-back also publish P for the A granules
-// of its window -- "helping" -- made the kernel slower, 0.71 against 0.46 ms
-// at C4: the extra 8-byte write-through stores congest the memory system,
-// profiles/r06/v01_one_pass)
-__device__ __forceinline__ uint64_t rows_lookback(uint64_t *desc, uint64_t t, uint32_t epoch, uint32_t lane,
-                                                  uint32_t &errs) {
-    constexpr uint64_t kVal = (1ull << kDescValueBits) - 1ull;
-    uint64_t ex = 0;
-    int64_t j0 = (int64_t)t - 1;
-    for (uint32_t spins = 0;;) {
-        const int64_t j = j0 - (int64_t)lane;
-        // (before tile 0: a P of prefix 0)
-        const uint64_t d = j >= 0 ? desc_load(desc + j) : desc_pack(epoch, DESC_P, 0, 0);
-        const uint32_t f = (uint32_t)(d >> 48) == epoch ? (uint32_t)(d >> 46) & 3u : 0u;
-        const uint64_t pm = __ballot(f == DESC_P), okm = __ballot(f != 0u);
-        const uint32_t lp = pm ? (uint32_t)__builtin_ctzll(pm) : 63u;  // the nearest P (or the whole window)
-        const uint64_t need = lp == 63u ? ~0ull : (2ull << lp) - 1ull;
-        if ((okm & need) != need) {  // a tile up to it has published nothing yet
-            if (++spins >= kLookbackSpins) {
-                errs |= 2u;
-                return ex;
-            }
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-        }
-        const bool in = lane <= lp;
-        ex += wave_sum44(in ? d & kVal : 0ull);
-        errs |= (__ballot(in && ((d >> kDescValueBits) & 1ull)) ? 1u : 0u) |
-                (__ballot(in && ((d >> (kDescValueBits + 1)) & 1ull)) ? 2u : 0u);
-        if (pm) return ex;
-        j0 -= 64;
-    }
-}
-// a row's labels by the one-lane walk of its record in global memory (a tile
-// with more labels than its LDS stage, a record longer than the stage's
-// copy): counts them and, with dst, stores them there (u32); false when the
-// record does not walk to its count (a corrupt image).  The pending frames
-// live in the wave's block slots (free once the records are walked).
-template <int B>
-__device__ __forceinline__ bool rows_walk_global(const RowsParams &p, uint64_t rec_row, uint32_t *dst,
-                                                 AS_LDS uint32_t *stk) {
-    RowsView v;
-    v.blocks = p.blocks;
-    v.spill = p.spill;
-    v.magic = p.magic;
-    v.num_rows = 0;
-    v.B = B;
-    v.S = p.S;
-    uint64_t masks;
-    uint32_t count;
-    rows_locate(v, rec_row, masks, count);
-    const uint32_t *ntab = p.rwt + 4;
-    const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + gld(p.rwt));
-    uint32_t j = 0;
-    const bool ok = rwt_walk_lds(
-        ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
-        [&](uint32_t col) {
-            if (dst && j < count) __builtin_nontemporal_store(col, (AS_GLOBAL uint32_t *)(uintptr_t)(dst + j));
-            ++j;
-        },
-        stk, p.stk_lim);
-    return ok && j == count;
-}
-
 // k_traverse_rows: one wave per tile of 64 query rows (file comment).
 // B: block bytes; WPB: waves per workgroup (the RWT2 table is staged once per
-// workgroup); WALK: the walk family; FUSED: the one-pass form above (the
-// odometers only), else the tile's labels go to its temp region for
-// k_compact_tiles.
-template <int B, int WPB, bool NT, uint32_t WALK, bool FUSED>
-__global__ __launch_bounds__(64 * (WPB + (FUSED ? 1 : 0))) void k_traverse_rows(RowsParams p) {
-    static_assert(!FUSED || WALK == WALK_ODOMETER || WALK == WALK_TREE_ODOMETER, "one pass: the odometers only");
+// workgroup); WALK: the walk family.  (r06: a one-pass form that wrote the
+// CSR itself, its place found by a decoupled look-back, measured 0.44-0.48
+// against 0.33 ms per C4 step and was retired: profiles/r06/v01_one_pass.)
+template <int B, int WPB, bool NT, uint32_t WALK>
+__global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows[];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t ntiles = (p.n + 63) / 64;
     const uint64_t tstride = (uint64_t)gridDim.x * WPB;  // (one tile per wave unless the grid is capped)
     uint64_t t = (uint64_t)blockIdx.x * WPB + wv;
-    // FUSED: the workgroup's look-back state (the scan wave below)
-    __shared__ uint32_t s_tot[WPB];  // tile totals
-    __shared__ uint32_t s_err, s_arrive, s_ready, s_errs;
-    __shared__ uint64_t s_base;
-    if (FUSED && threadIdx.x == 0) {
-        s_err = 0;
-        s_arrive = 0;
-        s_ready = 0;
-    }
     uint64_t row_n = 0;  // the row of this lane in the wave's next tile (its load overlaps the table's)
-    if (t < ntiles && t * 64 + lane < p.n && wv < WPB) row_n = gld(p.rows + t * 64 + lane);
+    if (t < ntiles && t * 64 + lane < p.n) row_n = gld(p.rows + t * 64 + lane);
     for (uint32_t i = threadIdx.x; i < p.table_words; i += blockDim.x) lds_rows[i] = gld(p.table + i);
-    if (!FUSED && blockIdx.x == 0 && threadIdx.x == 0) p.status[1] = MBRWT_OK;  // k_compact_tiles raises it
+    if (blockIdx.x == 0 && threadIdx.x == 0) p.status[1] = MBRWT_OK;  // k_compact_tiles raises it
     __syncthreads();
-    if constexpr (FUSED) {
-        if (wv == WPB) {  // the scan wave: the workgroup's place in the CSR
-            const uint64_t b = blockIdx.x, t0 = b * WPB;
-            if (t0 >= ntiles) return;
-            const uint32_t nwv = (uint32_t)(ntiles - t0 < WPB ? ntiles - t0 : WPB);
-            while (__hip_atomic_load(&s_arrive, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < nwv)
-                __builtin_amdgcn_s_sleep(1);
-            const uint32_t wtot = __builtin_amdgcn_readlane(wave_incl_sum(lane < nwv ? s_tot[lane] : 0u), 63);
-            const uint32_t werr = s_err;
-            uint32_t errs = 0;
-            uint64_t ex = 0;
-            desc_store(p.desc + b, desc_pack(p.epoch, b == 0 ? DESC_P : DESC_A, werr, wtot));
-            if (b > 0) {
-                ex = rows_lookback(p.desc, b, p.epoch, lane, errs);
-                desc_store(p.desc + b, desc_pack(p.epoch, DESC_P, errs | werr, ex + wtot));
-            }
-            if (lane == 0) {
-                s_base = ex;
-                s_errs = errs | werr;
-                __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            return;
-        }
-    }
     const uint32_t root = __builtin_amdgcn_readfirstlane(lds_rows[0]);
     const AS_LDS uint32_t *ent = (const AS_LDS uint32_t *)lds_rows + 4;
     // the leaf parents' column lists after the entries
@@ -1445,7 +1292,7 @@ __global__ __launch_bounds__(64 * (WPB + (FUSED ? 1 : 0))) void k_traverse_rows(
         tn = t + tstride;
         if (tn < ntiles && tn * 64 + lane < p.n) row_n = gld(p.rows + tn * 64 + lane);
         const bool valid = lane < nr && row < p.num_rows;
-        if (!FUSED && lane < nr && !valid) atomicOr(&p.scalars[2], 1ull);
+        if (lane < nr && !valid) atomicOr(&p.scalars[2], 1ull);
         // record classes: the row's class is its record's row in the
         // dictionary (S = 1); the class index is the random HBM read, the
         // dictionary's blocks mostly cache hits
@@ -1500,17 +1347,16 @@ __global__ __launch_bounds__(64 * (WPB + (FUSED ? 1 : 0))) void k_traverse_rows(
         const uint32_t x = wave_incl_sum(cnt);
         const uint32_t total = __builtin_amdgcn_readlane(x, 63);
         const uint32_t pos = x - cnt;
-        // a tile whose labels exceed its region (its LDS stage) is walked from
-        // global memory -- by k_compact_tiles, or (FUSED) by the tile's own
-        // lanes; so is a record longer than a block (its count flagged with
-        // bit 15; its labels' places in the tile are kept)
+        // a tile whose labels exceed its region is walked by k_compact_tiles
+        // from global memory; so is a record longer than a block (its count
+        // flagged with bit 15; its labels' places in the tile are kept)
         const bool direct = total > C;
         // the lane's record in LDS: its block slot, or (r05) for a record
         // longer than a block, a copy of its whole spill entry in the free tail
         // of the wave's label stage (the tile's labels take its first 2 total
         // bytes), so the odometers walk it here instead of walking it byte by
         // byte from global memory (the greedy + relax shape: 0.13 % of rows,
-        // 8 % of tiles; their global walks took 266 us of a 0.76 ms step,
+        // 8 % of tiles; its compaction took 266 us of a 0.76 ms step,
         // profiles/r05)
         const AS_LDS uint8_t *rec = mine;
         AS_LDS uint16_t *stage = (AS_LDS uint16_t *)(wb + 64u * PB + 256u * p.stk_words);
@@ -1535,34 +1381,15 @@ __global__ __launch_bounds__(64 * (WPB + (FUSED ? 1 : 0))) void k_traverse_rows(
             }
         }
         const bool has_long = __any(lng);
-        uint8_t *treg = FUSED ? nullptr : p.temp + t * (uint64_t)(128 + 2 * C);
-        // FUSED: rows walked from global memory (a direct tile's rows, long
-        // records) are walked once before the tile's total is published, so a
-        // record that does not walk raises the error bit that travels with it
-        const bool gw = direct ? (valid && cnt > 0) : lng;
-        const bool any_gw = FUSED && __any(gw);
-        uint32_t err = 0;
-        // FUSED: a tile hands its total to the scan wave (LDS)
-        auto hand_in = [&]() {
-            if (lane == 0) {
-                s_tot[wv] = total;
-                if (err) __hip_atomic_fetch_or(&s_err, err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_add(&s_arrive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        };
-        if constexpr (FUSED) {
-            err = __any(lane < nr && !valid) ? 1u : 0u;
-            if (!any_gw) hand_in();
-        } else {
-            // (non-temporal: the temp region is read once, by k_compact_tiles;
-            // the stores then disturb the random block reads less -- C4 kernel
-            // 0.262 -> 0.255 ms, step 0.348 -> 0.333 ms; the same hint on the
-            // compaction's CSR stores made the two-stream step slower again,
-            // 0.344 ms: profiles/r05/v21_temp_stores)
-            if (lane < nr)
-                __builtin_nontemporal_store((uint16_t)(cnt | (lng ? 0x8000u : 0u)),
-                                            (AS_GLOBAL uint16_t *)(uintptr_t)(reinterpret_cast<uint16_t *>(treg) + lane));
-        }
+        uint8_t *treg = p.temp + t * (uint64_t)(128 + 2 * C);
+        // (non-temporal: the temp region is read once, by k_compact_tiles;
+        // the stores then disturb the random block reads less -- C4 kernel
+        // 0.262 -> 0.255 ms, step 0.348 -> 0.333 ms; the same hint on the
+        // compaction's CSR stores made the two-stream step slower again,
+        // 0.344 ms: profiles/r05/v21_temp_stores)
+        if (lane < nr)
+            __builtin_nontemporal_store((uint16_t)(cnt | (lng ? 0x8000u : 0u)),
+                                        (AS_GLOBAL uint16_t *)(uintptr_t)(reinterpret_cast<uint16_t *>(treg) + lane));
         if (!direct) {
             const bool live = valid && cnt > 0 && !lng;
             if constexpr (WALK == WALK_ODOMETER || WALK == WALK_TREE_ODOMETER) {
@@ -1619,14 +1446,12 @@ __global__ __launch_bounds__(64 * (WPB + (FUSED ? 1 : 0))) void k_traverse_rows(
                     }
                 }
                 wave_sync();
-                if constexpr (!FUSED) {
-                    // (r05: rounding the copy up to whole 128-byte lines helped
-                    // plain stores by 1.5 % and non-temporal ones not at all)
-                    const uint32_t nbytes = total * 2;
-                    for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
-                        __builtin_nontemporal_store(*(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2),
-                                                    (AS_GLOBAL u32x4_t *)(uintptr_t)(treg + 128 + q2));
-                }
+                // (r05: rounding the copy up to whole 128-byte lines helped
+                // plain stores by 1.5 % and non-temporal ones not at all)
+                const uint32_t nbytes = total * 2;
+                for (uint32_t q2 = lane * 16; q2 < nbytes; q2 += 1024)
+                    __builtin_nontemporal_store(*(const AS_LDS u32x4_t *)((const AS_LDS uint8_t *)stage + q2),
+                                                (AS_GLOBAL u32x4_t *)(uintptr_t)(treg + 128 + q2));
             } else if constexpr (WALK == WALK_MASK1) {
                 rows_walk6(mine, o, live, root, ent, lst, stk,
                            (AS_GLOBAL uint16_t *)reinterpret_cast<uint16_t *>(treg + 128), pos);
@@ -1634,72 +1459,7 @@ __global__ __launch_bounds__(64 * (WPB + (FUSED ? 1 : 0))) void k_traverse_rows(
                 rows_walk4(mine, o, live, root, ent, lst, stk, reinterpret_cast<uint16_t *>(treg + 128), pos);
             }
         }
-        if constexpr (FUSED) {
-            // the block slots hold the global walks' frames from here on
-            AS_LDS uint32_t *gstk = (AS_LDS uint32_t *)wb + lane;
-            if (any_gw) {
-                wave_sync();
-                const bool ok = !gw || rows_walk_global<B>(p, rec_row, nullptr, gstk);
-                err |= __any(!ok) ? 2u : 0u;
-                hand_in();
-            }
-            // the workgroup's prefix from the scan wave, then this tile's
-            while (__hip_atomic_load(&s_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
-                __builtin_amdgcn_s_sleep(1);
-            uint64_t ex = s_base;
-            for (uint32_t w = 0; w < wv; ++w) ex += s_tot[w];
-            const uint32_t errs = s_errs;
-            const uint64_t tot = ex + total;
-            if (lane < nr)
-                __builtin_nontemporal_store(ex + pos, (AS_GLOBAL uint64_t *)(uintptr_t)(p.offsets + r0 + lane));
-            if (t == ntiles - 1 && lane == 0) {  // the batch's end: its total and the call's status
-                gst(p.offsets + p.n, tot);
-                const uint64_t st = (errs & 2u)   ? MBRWT_ERR_DEVICE
-                                    : (errs & 1u) ? MBRWT_ERR_RANGE
-                                    : tot > p.cap ? MBRWT_ERR_CAPACITY
-                                                  : MBRWT_OK;
-                p.status[0] = tot;
-                p.status[1] = st;
-                atomicOr(&p.status[2], 1ull << st);
-            }
-            if (tot <= p.cap) {
-                if (!direct) {
-                    // u16 stage -> u32 labels at ex: whole 16-byte stores on
-                    // 16-byte boundaries of the CSR (lead = ex mod 4 labels
-                    // before the first boundary), single stores at the ends
-                    uint32_t *dst = p.cols + (ex & ~3ull);
-                    const uint32_t lead = (uint32_t)ex & 3u, span = total + lead;
-                    for (uint32_t i4 = lane * 4; i4 < span; i4 += 256) {
-                        const int32_t l0 = (int32_t)i4 - (int32_t)lead;
-                        uint32_t v[4];
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            const int32_t li = l0 + k;
-                            v[k] = (li >= 0 && li < (int32_t)total) ? (uint32_t)stage[li] : 0u;
-                        }
-                        if (l0 >= 0 && l0 + 4 <= (int32_t)total) {
-                            __builtin_nontemporal_store(u32x4_t{v[0], v[1], v[2], v[3]},
-                                                        (AS_GLOBAL u32x4_t *)(uintptr_t)(dst + i4));
-                        } else {
-#pragma unroll
-                            for (int k = 0; k < 4; ++k) {
-                                const int32_t li = l0 + k;
-                                if (li >= 0 && li < (int32_t)total)
-                                    __builtin_nontemporal_store(v[k], (AS_GLOBAL uint32_t *)(uintptr_t)(dst + i4 + k));
-                            }
-                        }
-                    }
-                }
-                if (any_gw) {
-                    // (a long record's labels overwrite the places the copy
-                    // above filled for it: other lanes' stores, hence the fence)
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    if (gw) (void)rows_walk_global<B>(p, rec_row, p.cols + ex + pos, gstk);
-                }
-            }
-        } else {
-            if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u) | (has_long ? 0x40000000u : 0u));
-        }
+        if (lane == 0) gst(p.tile_counts + t, total | (direct ? 0x80000000u : 0u) | (has_long ? 0x40000000u : 0u));
         wave_sync();  // the slots are reused
     }
 }
@@ -1953,22 +1713,17 @@ constexpr uint32_t kRowsWpb = 8;
 // 8-wave workgroups per CU (16 waves); two of 11 waves fit (22)
 constexpr uint32_t kRowsWpbWide = 11;
 template <int B, bool NT>
-RowsFn rows_fn_b(uint32_t walk, uint32_t wpb, bool fused) {
-    if (fused) {
-        if (walk == WALK_ODOMETER) return k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER, true>;
-        if (wpb == kRowsWpbWide) return k_traverse_rows<B, kRowsWpbWide, NT, WALK_TREE_ODOMETER, true>;
-        return k_traverse_rows<B, kRowsWpb, NT, WALK_TREE_ODOMETER, true>;
-    }
-    if (wpb == kRowsWpbWide) return k_traverse_rows<B, kRowsWpbWide, NT, WALK_TREE_ODOMETER, false>;
-    return walk == WALK_ODOMETER        ? k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER, false>
-           : walk == WALK_TREE_ODOMETER ? k_traverse_rows<B, kRowsWpb, NT, WALK_TREE_ODOMETER, false>
-           : walk == WALK_MASK1         ? k_traverse_rows<B, kRowsWpb, NT, WALK_MASK1, false>
-                                        : k_traverse_rows<B, kRowsWpb, NT, WALK_GENERAL, false>;
+RowsFn rows_fn_b(uint32_t walk, uint32_t wpb) {
+    if (wpb == kRowsWpbWide) return k_traverse_rows<B, kRowsWpbWide, NT, WALK_TREE_ODOMETER>;
+    return walk == WALK_ODOMETER        ? k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER>
+           : walk == WALK_TREE_ODOMETER ? k_traverse_rows<B, kRowsWpb, NT, WALK_TREE_ODOMETER>
+           : walk == WALK_MASK1         ? k_traverse_rows<B, kRowsWpb, NT, WALK_MASK1>
+                                        : k_traverse_rows<B, kRowsWpb, NT, WALK_GENERAL>;
 }
-RowsFn rows_fn(const RowsImage &im, uint32_t walk, uint32_t wpb, bool fused) {
+RowsFn rows_fn(const RowsImage &im, uint32_t walk, uint32_t wpb) {
     const bool nt = im.bytes > (1ull << 30);  // non-temporal block reads for images beyond the caches
-    if (im.B == 64) return nt ? rows_fn_b<64, true>(walk, wpb, fused) : rows_fn_b<64, false>(walk, wpb, fused);
-    return nt ? rows_fn_b<128, true>(walk, wpb, fused) : rows_fn_b<128, false>(walk, wpb, fused);
+    if (im.B == 64) return nt ? rows_fn_b<64, true>(walk, wpb) : rows_fn_b<64, false>(walk, wpb);
+    return nt ? rows_fn_b<128, true>(walk, wpb) : rows_fn_b<128, false>(walk, wpb);
 }
 // resident waves per CU with workgroups of w waves: the LDS (160 KiB per CU:
 // the table once per workgroup + per_wave bytes per wave) within the 24-wave cap
@@ -2012,17 +1767,6 @@ static uint32_t rows_walk_of(const Ctx &c) {
     return im.mask1 ? WALK_MASK1 : WALK_GENERAL;
 }
 
-// the one-pass traversal (FUSED, r06) for this context's get_rows: the
-// odometer walks on block records; the global walks' frames fit the wave's
-// block slots
-bool rows_one_pass(const Ctx &c) {
-    const RowsImage &im = c.rows;
-    if (!im.ready || im.var || !c.rows_fused || !im.d_table) return false;
-    const uint32_t walk = rows_walk_of(c);
-    const uint32_t stk_lim = std::max(1u, std::min(im.height, kRowsMaxHeight));
-    return (walk == WALK_ODOMETER || walk == WALK_TREE_ODOMETER) && 256u * stk_lim <= 64u * (im.B + 4);
-}
-
 int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offsets, uint32_t *d_cols, uint64_t cap,
                   uint64_t *needed, hipStream_t s, uint64_t *d_status) {
     const RowsImage &im = c.rows;
@@ -2044,41 +1788,25 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     const uint64_t region = 128 + 2ull * C;
     const uint32_t walk = rows_walk_of(c);
     const uint32_t stk_lim = std::max(1u, std::min(im.height, kRowsMaxHeight));
-    const bool fused = rows_one_pass(c);
-    uint32_t *d_tc = nullptr;
-    uint64_t *d_to = nullptr;
-    unsigned long long *d_sc = nullptr;
-    size_t scan_bytes = 0;
-    if (fused) {
-        // look-back descriptors: cleared when (re)allocated and when the
-        // 16-bit epoch wraps, so no earlier call's granule carries this epoch
-        const size_t had = c.ws_desc.bytes;
-        if ((rc = ensure(c.ws_desc, (nt + 1) * sizeof(uint64_t)))) return rc;
-        if (c.ws_desc.bytes != had || c.desc_epoch >= 0xFFFFu) {
-            MBRWT_HIP(hipMemsetAsync(c.ws_desc.buf, 0, c.ws_desc.bytes, s));
-            c.desc_epoch = 0;
-        }
-        ++c.desc_epoch;
-    } else {
-        // counts workspace: nt+1 tile counts | (8-byte aligned) nt+1 tile offsets
-        const uint64_t to_off = ((nt + 1) * sizeof(uint32_t) + 7) / 8 * 8;
-        if ((rc = ensure(c.ws_temp, nt * region))) return rc;
-        // [tile counts | tile offsets | the kernel's own counters (4 x u64)]
-        const uint64_t sc_off = to_off + (nt + 1) * sizeof(uint64_t);
-        const bool fresh = c.ws_counts.bytes < sc_off + 32;
-        if ((rc = ensure(c.ws_counts, sc_off + 32))) return rc;
-        d_sc = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + sc_off);
-        if (fresh || c.rows_sc_dirty || c.rows_sc_at != sc_off) {  // the counters are cleared by k_compact_tiles
-            MBRWT_HIP(hipMemsetAsync(d_sc, 0, 32, s));
-            c.rows_sc_dirty = false;
-            c.rows_sc_at = sc_off;
-        }
-        d_tc = reinterpret_cast<uint32_t *>(c.ws_counts.buf);
-        d_to = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + to_off);
-        hipcub::TransformInputIterator<uint64_t, MaskTile, const uint32_t *> it(d_tc, MaskTile());
-        MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, it, d_to, nt, s));
-        if ((rc = ensure(c.ws_scan, scan_bytes))) return rc;
+    // counts workspace: nt+1 tile counts | (8-byte aligned) nt+1 tile offsets
+    const uint64_t to_off = ((nt + 1) * sizeof(uint32_t) + 7) / 8 * 8;
+    if ((rc = ensure(c.ws_temp, nt * region))) return rc;
+    // [tile counts | tile offsets | the kernel's own counters (4 x u64)]
+    const uint64_t sc_off = to_off + (nt + 1) * sizeof(uint64_t);
+    const bool fresh = c.ws_counts.bytes < sc_off + 32;
+    if ((rc = ensure(c.ws_counts, sc_off + 32))) return rc;
+    unsigned long long *d_sc = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + sc_off);
+    if (fresh || c.rows_sc_dirty || c.rows_sc_at != sc_off) {  // the counters are cleared by k_compact_tiles
+        MBRWT_HIP(hipMemsetAsync(d_sc, 0, 32, s));
+        c.rows_sc_dirty = false;
+        c.rows_sc_at = sc_off;
     }
+    uint32_t *d_tc = reinterpret_cast<uint32_t *>(c.ws_counts.buf);
+    uint64_t *d_to = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(c.ws_counts.buf) + to_off);
+    hipcub::TransformInputIterator<uint64_t, MaskTile, const uint32_t *> it(d_tc, MaskTile());
+    size_t scan_bytes = 0;
+    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, it, d_to, nt, s));
+    if ((rc = ensure(c.ws_scan, scan_bytes))) return rc;
     // the call's status block: the caller's (asynchronous) or the context's
     unsigned long long *st_blk =
         reinterpret_cast<unsigned long long *>(d_status ? d_status : c.d_scalars);
@@ -2096,17 +1824,10 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     p.table_words = (uint32_t)im.table2.size();
     p.table = im.d_table2;
     p.C = C;
-    p.temp = fused ? nullptr : reinterpret_cast<uint8_t *>(c.ws_temp.buf);
+    p.temp = reinterpret_cast<uint8_t *>(c.ws_temp.buf);
     p.tile_counts = d_tc;
     p.scalars = d_sc;
     p.status = st_blk;
-    p.desc = fused ? reinterpret_cast<uint64_t *>(c.ws_desc.buf) : nullptr;
-    p.epoch = c.desc_epoch;
-    p.offsets = d_offsets;
-    p.cols = d_cols;
-    p.cap = cap;
-    p.rwt = im.d_table;
-    p.stk_lim = stk_lim;
     p.uni = im.uni;
     p.path_walk = c.rows_walk == 7 ? 0u : 1u;  // (7: the r03 odometer, A/B)
     p.stk_words = walk >= WALK_ODOMETER ? 0u : rows_stack_words(im);  // (the odometers keep no stack)
@@ -2120,9 +1841,9 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
                               rows_waves_per_cu(table_bytes, per_wave, kRowsWpb))
                              ? kRowsWpbWide
                              : kRowsWpb;
-    const RowsFn kfn = rows_fn(im, walk, wpb, fused);
+    const RowsFn kfn = rows_fn(im, walk, wpb);
     const size_t lds = table_bytes + wpb * per_wave;
-    const uint32_t threads = 64 * (wpb + (fused ? 1u : 0u));  // (FUSED: + the scan wave)
+    const uint32_t threads = 64 * wpb;
     // at most 24 waves (3 workgroups of 8) per CU: more waves make the walk phase
     // slower than the extra loads in flight gain (C4 0.426 ms at 3 against
     // 0.456 at 4, C2 0.068 against 0.073: profiles/r03/v06_rows_occupancy_*);
@@ -2147,7 +1868,7 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         c.rb_blocks = std::max(1, dev_cus) * per_cu;
     }
 
-    if (!fused) c.rows_sc_dirty = true;  // until k_compact_tiles has run
+    c.rows_sc_dirty = true;  // until k_compact_tiles has run
     hipEvent_t e0 = c.ev0, e1 = c.ev1;
     if (c.timing && d_status) {  // asynchronous calls: one event pair per call, summed by mbrwt_take_timing
         if (c.async_ev.size() <= c.async_used) {
@@ -2167,9 +1888,7 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         // tree odometer's table -- 8.8 KB at the greedy + relax shape -- is
         // staged once per workgroup: one tile per wave took 0.518 against
         // 0.458 ms there, profiles/r05)
-        // (the one-pass form never runs persistent: a wave waits on the tiles
-        // before its own, so every wave must be dispatchable in tile order)
-        const bool persistent = walk != WALK_ODOMETER && !fused;
+        const bool persistent = walk != WALK_ODOMETER;
         const uint64_t per_wg = (uint64_t)wpb * kRowsTilesPerWave;
         const uint64_t g = persistent
                                ? std::max<uint64_t>(1, std::min<uint64_t>((nt + wpb - 1) / wpb, (uint64_t)c.rb_blocks))
@@ -2178,9 +1897,8 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         MBRWT_HIP(hipGetLastError());
     }
     if (c.timing) MBRWT_HIP(hipEventRecord(e1, s));
-    if (!fused) {
-        hipcub::TransformInputIterator<uint64_t, MaskTile, const uint32_t *> it(d_tc, MaskTile());
-        MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_to, nt, s));
+    MBRWT_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_scan.buf, scan_bytes, it, d_to, nt, s));
+    {
         CompactParams cp{};
         cp.temp = p.temp;
         cp.C = C;

@@ -271,10 +271,6 @@ int mbrwt_rows_stats(const mbrwt_ctx *ctx, uint64_t out[8]);
    sampled).  With classes, mbrwt_rows_stats describes the dictionary (one
    record per class, S = 1).  MBRWT_ERR_UNSUPPORTED without row records. */
 int mbrwt_rows_classes(const mbrwt_ctx *ctx, uint64_t out[4]);
-/* 1 when get_rows on this context runs the one-pass row-record traversal
-   (MBRWT_OPT_ROWS_FUSED, csrc/rows.hip: each tile places its labels in the
-   CSR by a decoupled look-back), else 0 (two kernels, or another layout). */
-int mbrwt_rows_one_pass(const mbrwt_ctx *ctx);
 
 /* ---- multi-device (one process, N GPUs) --------------------------------
  * A replica of the tree on every device of `devices` (n entries; a device
@@ -379,9 +375,7 @@ int mbrwt_get_rows_device(mbrwt_ctx *ctx, const uint64_t *d_rows, uint64_t n, ui
  * (device memory, 3 uint64) holds {labels needed, MBRWT_* status of the
  * call, sticky bits |= 1 << status} -- the caller clears word 2 and checks
  * it after synchronising.  Over cols_cap the status is MBRWT_ERR_CAPACITY
- * and no label is written past cols_cap (offsets and a prefix of the labels
- * may be: the one-pass row-record traversal writes each tile's labels once
- * their place is known); out-of-range rows give
+ * and no label is written past cols_cap (offsets may be); out-of-range rows give
  * MBRWT_ERR_RANGE.  The return value reports only argument and launch errors.
  * On a per-node image the call runs the synchronous path (one host sync)
  * and then writes the same status block.
@@ -539,10 +533,6 @@ int mbrwt_unpack_offsets_device(const void *d_base, uint32_t nseg, uint64_t seg_
                                    trees, the tree odometer on every other shape of <= 8 internal levels),
                                    3 the tree odometer, 4 the stack walk, 6 the stack walk of one-byte masks,
                                    7 the odometer without the path table (A/B and tests) */
-#define MBRWT_OPT_ROWS_FUSED 16 /* row records, odometer walks: 1 the one-pass traversal that writes the CSR
-                                   itself (workgroup prefixes by a decoupled look-back, r06: measured slower,
-                                   profiles/r06/v01_one_pass); 0 default -- traversal into temp regions +
-                                   tile scan + compaction */
 #define MBRWT_OPT_TEST_FAIL_CHUNK 32 /* test hook: mbrwt_get_rows (host buffers) fails with MBRWT_ERR_NOMEM
                                         when it reaches chunk `value` of the batch (-1: never) -- the error
                                         path's drain of the chunks already in flight is tested with it */

@@ -141,16 +141,12 @@ def test_odometer_walk(oracle_mod, n, m, d, arity, levels):
     rows = np.concatenate([np.arange(n), rng.integers(0, n, 20000)]).astype(np.uint64)
     off_o, cols_o = t.get_rows(rows)
     from genome_graph_annotation_amd import _lib as L
-    # the path-table odometer, the tree odometer, the stack walks, the r03
-    # odometer; the odometers both in one pass (look-back) and as traversal +
-    # compaction
+    # the path-table odometer, the tree odometer, the stack walks, the r03 odometer
     for walk in (0, 3, 4, 6, 7):
-        for fused in (1, 0):
-            dev.set_option(L.MBRWT_OPT_ROWS_WALK, walk)
-            dev.set_option(L.MBRWT_OPT_ROWS_FUSED, fused)
-            off_d, cols_d = dev.get_rows(rows)
-            np.testing.assert_array_equal(off_d, off_o)
-            np.testing.assert_array_equal(cols_d, cols_o)
+        dev.set_option(L.MBRWT_OPT_ROWS_WALK, walk)
+        off_d, cols_d = dev.get_rows(rows)
+        np.testing.assert_array_equal(off_d, off_o)
+        np.testing.assert_array_equal(cols_d, cols_o)
 
 
 @pytest.mark.parametrize("n,m,d,part,arity,relax", [
@@ -178,12 +174,10 @@ def test_tree_odometer(oracle_mod, n, m, d, part, arity, relax):
     rows = np.concatenate([np.arange(n), rng.integers(0, n, 20000)]).astype(np.uint64)
     off_o, cols_o = t.get_rows(rows)
     for walk in (0, 3, 4, 6):
-        for fused in (1, 0):
-            dev.set_option(L.MBRWT_OPT_ROWS_WALK, walk)
-            dev.set_option(L.MBRWT_OPT_ROWS_FUSED, fused)
-            off_d, cols_d = dev.get_rows(rows)
-            np.testing.assert_array_equal(off_d, off_o)
-            np.testing.assert_array_equal(cols_d, cols_o)
+        dev.set_option(L.MBRWT_OPT_ROWS_WALK, walk)
+        off_d, cols_d = dev.get_rows(rows)
+        np.testing.assert_array_equal(off_d, off_o)
+        np.testing.assert_array_equal(cols_d, cols_o)
 
 
 def test_auto_layout(oracle_mod, build_env):
@@ -355,14 +349,14 @@ def test_errors_and_capacity_rows(oracle_mod):
 
 
 @pytest.mark.parametrize("shape", ["uniform", "greedy", "long"])
-def test_one_pass_lookback(oracle_mod, shape):
-    """The one-pass traversal (r06: each tile places its labels in the CSR by a
-    decoupled look-back over the tiles before it): the same CSR as the oracle
-    and as the two-kernel path on batches of 1 .. 32k tiles (look-back chains
-    many windows long), the capacity boundary (cap = total is enough, total - 1
-    reports MBRWT_ERR_CAPACITY and writes nothing past the capacity), range
-    errors anywhere in the batch, and consecutive asynchronous calls (the
-    descriptors' epochs) through one status block."""
+def test_async_capacity_boundary_and_batches(oracle_mod, shape):
+    """The asynchronous row-record call on batches of 1 .. 31k tiles (uniform,
+    greedy + relax, and long records: direct tiles, spills): the oracle's
+    CSR; the capacity boundary (cap = total is enough, total - 1 reports
+    MBRWT_ERR_CAPACITY and writes nothing past the capacity); a row out of
+    range in the middle of the batch; many calls back to back through one
+    status block.  (r06: also the one-pass traversal's test while it existed,
+    profiles/r06/v01_one_pass.)"""
     O = oracle_mod
     import torch
     from genome_graph_annotation_amd import BRWTDevice, _lib as L
@@ -383,38 +377,33 @@ def test_one_pass_lookback(oracle_mod, shape):
         off_o, cols_o = t.get_rows(rows)
         tot = len(cols_o)
         rt = torch.from_numpy(rows.view(np.int64)).cuda()
-        for fused in (1, 0):
-            dev.set_option(L.MBRWT_OPT_ROWS_FUSED, fused)
-            ot = torch.empty(k + 1, dtype=torch.int64, device="cuda")
-            ct = torch.full((tot + 64,), -1, dtype=torch.int32, device="cuda")
-            for cap in (tot, max(0, tot - 1)):
-                st.zero_()
-                ct.fill_(-1)
-                dev.get_rows_device_async(rt, ot, ct[:cap], st, s)
-                torch.cuda.synchronize()
-                need, status, sticky = st.cpu().tolist()
-                assert need == tot
-                if cap >= tot:
-                    assert status == L.MBRWT_OK and sticky == 1 << L.MBRWT_OK
-                    np.testing.assert_array_equal(ot.cpu().numpy().view(np.uint64), off_o)
-                    np.testing.assert_array_equal(ct[:tot].cpu().numpy().view(np.uint32), cols_o)
-                else:
-                    assert status == L.MBRWT_ERR_CAPACITY and sticky == 1 << L.MBRWT_ERR_CAPACITY
-                assert (ct[cap:] == -1).all(), "a label written past the capacity"
+        ot = torch.empty(k + 1, dtype=torch.int64, device="cuda")
+        ct = torch.full((tot + 64,), -1, dtype=torch.int32, device="cuda")
+        for cap in (tot, max(0, tot - 1)):
+            st.zero_()
+            ct.fill_(-1)
+            dev.get_rows_device_async(rt, ot, ct[:cap], st, s)
+            torch.cuda.synchronize()
+            need, status, sticky = st.cpu().tolist()
+            assert need == tot
+            if cap >= tot:
+                assert status == L.MBRWT_OK and sticky == 1 << L.MBRWT_OK
+                np.testing.assert_array_equal(ot.cpu().numpy().view(np.uint64), off_o)
+                np.testing.assert_array_equal(ct[:tot].cpu().numpy().view(np.uint32), cols_o)
+            else:
+                assert status == L.MBRWT_ERR_CAPACITY and sticky == 1 << L.MBRWT_ERR_CAPACITY
+            assert (ct[cap:] == -1).all(), "a label written past the capacity"
         # a row out of range in the middle of the batch
         if k > 64:
             bad = rows.copy()
             bad[k // 2] = n
             bt = torch.from_numpy(bad.view(np.int64)).cuda()
-            for fused in (1, 0):
-                dev.set_option(L.MBRWT_OPT_ROWS_FUSED, fused)
-                st.zero_()
-                ct = torch.empty(tot + 64, dtype=torch.int32, device="cuda")
-                dev.get_rows_device_async(bt, ot, ct, st, s)
-                torch.cuda.synchronize()
-                assert st.cpu().tolist()[1] == L.MBRWT_ERR_RANGE
-    dev.set_option(L.MBRWT_OPT_ROWS_FUSED, 1)
-    # many asynchronous calls back to back on one context (epochs 1, 2, ...)
+            st.zero_()
+            ct = torch.empty(tot + 64, dtype=torch.int32, device="cuda")
+            dev.get_rows_device_async(bt, ot, ct, st, s)
+            torch.cuda.synchronize()
+            assert st.cpu().tolist()[1] == L.MBRWT_ERR_RANGE
+    # many asynchronous calls back to back on one context
     rows = rng.integers(0, n, 100_000).astype(np.uint64)
     off_o, cols_o = t.get_rows(rows)
     rt = torch.from_numpy(rows.view(np.int64)).cuda()
