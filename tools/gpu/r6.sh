@@ -20,8 +20,13 @@ onepass)  # the one-pass traversal: row-record tests, then a same-box A/B agains
   timeout -k 10 120 $B --no-cpu --rows-fused 0 > $O/bench_twokernel_2.log 2>&1 &&
   timeout -k 10 120 $B --no-cpu --rows-fused 1 > $O/bench_fused_2.log 2>&1
   ;;
-rows)  # the row-record GPU tests (one-pass option included) + host pipeline + classes
+rows)  # the row-record GPU tests + host pipeline + classes
   timeout -k 10 700 $PYT tests/test_gpu_rows.py tests/test_gpu_hostpipe.py tests/test_gpu_classes.py > $O/pytest_rows.log 2>&1
+  ;;
+trace)  # C4 bench (live PMC, ceilings) and the kernel trace of its two-stream timed region
+  timeout -k 10 400 python -u bench.py --no-cpu --no-e2e --traffic-out $O/traffic_c4.json > $O/bench_c4.log 2>&1 &&
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_c4 -o run --output-format csv -- python -u bench.py --no-cpu --no-e2e --no-probe --traffic off --steps 50 > $O/bench_c4_under_rocprof.log 2>&1 &&
+  python tools/trace_overlap.py $(find $O/prof_c4 -name "*kernel_trace.csv" | head -1) > $O/overlap.json 2>&1
   ;;
 *) echo "unknown stage $STAGE"; exit 2 ;;
 esac
