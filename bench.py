@@ -98,6 +98,9 @@ def parse():
     ap.add_argument("--check-rows", type=int, default=0,
                     help="rows checked element-wise against the oracle (0 = the whole global batch)")
     ap.add_argument("--kernel", type=int, default=0, help="MBRWT_OPT_KERNEL variant (0 = library default)")
+    ap.add_argument("--rows-code", type=int, default=0, choices=[0, 1],
+                    help="row-record masks: 0 bytes (library default), 1 nibble codes (MBRWT_BUILD_ROWS_CODE: the "
+                         "compact image, DESIGN §4g)")
     ap.add_argument("--query-streams", type=int, default=2, choices=[1, 2],
                     help="N = 1: consecutive batches alternate between the context and a clone of it "
                          "(mbrwt_ctx_clone: the same image, separate workspaces) on the default stream and "
@@ -143,15 +146,18 @@ def kernel_source_hash():
 
 def workload_args(a):
     return ["--rows", str(a.rows), "--cols", str(a.cols), "--density", repr(a.density), "--arity", str(a.arity),
-            "--batch", str(a.batch), "--seed", str(a.seed), "--kernel", str(a.kernel), "--layout", a.layout]
+            "--batch", str(a.batch), "--seed", str(a.seed), "--kernel", str(a.kernel), "--layout", a.layout,
+            "--rows-code", str(a.rows_code)]
 
 
 def pmc_pass(a):
     """Child under rocprofv3 --pmc: the structure and the rank-0 batch of an
     N = 1 run, 2 warm-up + 3 counted launches of the traversal."""
     from genome_graph_annotation_amd import BRWTDevice, _lib as L
+    from genome_graph_annotation_amd.brwt import build_option
     torch.cuda.set_device(0)
-    mat = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, device=0, layout=a.layout)
+    with build_option(L.MBRWT_BUILD_ROWS_CODE, a.rows_code):
+        mat = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, device=0, layout=a.layout)
     if a.kernel:
         mat.set_option(L.MBRWT_OPT_KERNEL, a.kernel)
     rows_np = np.random.default_rng(a.seed).integers(0, a.rows, a.batch, dtype=np.uint64)
@@ -184,7 +190,7 @@ def live_traffic(a, kernel_re):
     two dispatches are warm-up."""
     out = {"counters": {}, "source_hash": kernel_source_hash(), "kernel_regex": kernel_re,
            "config": {"rows": a.rows, "cols": a.cols, "density": a.density, "arity": a.arity, "batch": a.batch,
-                      "kernel": a.kernel, "layout": a.layout}}
+                      "kernel": a.kernel, "layout": a.layout, "rows_code": a.rows_code}}
     env = dict(os.environ, TMPDIR="/tmp")
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="bench_pmc_", dir="/tmp")
@@ -219,7 +225,7 @@ def committed_traffic(a, kernel_re):
     """A committed live-traffic summary (profiles/*/traffic_*.json) of this
     workload measured on the CURRENT kernel sources, or None."""
     want_cfg = {"rows": a.rows, "cols": a.cols, "density": a.density, "arity": a.arity, "batch": a.batch,
-                "kernel": a.kernel, "layout": a.layout}
+                "kernel": a.kernel, "layout": a.layout, "rows_code": a.rows_code}
     h = kernel_source_hash()
     hit = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic_*.json"))):
@@ -366,6 +372,7 @@ def main():
     local = local % max(1, ndev)  # (rehearsal only: several ranks may share one GPU under gloo)
 
     from genome_graph_annotation_amd import BRWTDevice, _lib as L
+    from genome_graph_annotation_amd.brwt import build_option
     from genome_graph_annotation_amd.dist import AllGatherV, DeviceAllGatherV, shard_bounds
 
     # roofline traffic first: the PMC child passes need the GPU's memory for
@@ -401,7 +408,8 @@ def main():
 
     dev_t = torch.device("cuda", local)
     t0 = time.time()
-    mat = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, device=local, layout=a.layout)
+    with build_option(L.MBRWT_BUILD_ROWS_CODE, a.rows_code):
+        mat = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, device=local, layout=a.layout)
     setup_s = time.time() - t0
     struct_bytes = mat.device_bytes()
     log(f"device structure built in {setup_s:.1f} s ({mat.device_bytes() / 1e9:.1f} GB, layout {mat.layout()}, "
@@ -843,6 +851,19 @@ def main():
         req = traffic["read_bytes"] / 64.0  # FETCH_SIZE in 64-byte units (calibrated on random 64-B segments)
         roof["read_requests_per_launch"] = req
         roof["read_requests_per_s"] = req / ks
+    # first-class keys: the physical read fraction, and how
+    # close the block requests run to the measured random-request ceiling --
+    # the binding limit of this layout: one random request per row caps the
+    # read fraction at ceiling x segment / peak (about 0.38-0.39 at 64 B)
+    if traffic is not None and world == 1:
+        roof["read_frac"] = traffic["read_bytes"] / ks / 1e9 / HBM_PEAK_GBS
+    if rnd is not None and rnd.get(f"seg{seg}_per_s"):
+        ceil = rnd[f"seg{seg}_per_s"]
+        roof["read_frac_cap_by_request_ceiling"] = ceil * seg / 1e9 / HBM_PEAK_GBS
+        if "block_requests_per_launch" in roof:
+            roof["request_ceiling_frac"] = roof["block_requests_per_launch"] / ks / ceil
+        elif "read_requests_per_launch" in roof:
+            roof["request_ceiling_frac"] = roof["read_requests_per_launch"] / ks / ceil
     if rnd is not None:
         roof["ceiling_random64_per_s"] = rnd.get("seg64_per_s")
         roof["ceiling_random128_per_s"] = rnd.get("seg128_per_s")
@@ -880,6 +901,7 @@ def main():
             "global_batch": G, "batch_per_gpu": nb, "batches": K, "layout": a.layout,
             "api": "mbrwt_get_rows_device_async" if use_async else "mbrwt_get_rows_device",
             "query_streams": Q,
+            "rows_code": "nibble" if a.rows_code else "byte",
             "parallelism": f"batch-sharded x{world}, tree replicated" + ("" if world == 1 or a.no_gather
                                                                          else ", all-gatherv over " + ("RCCL" if a.dist_backend == "nccl" else a.dist_backend)
                                                                          + (" (device-sized wire, no host sync)" if wire is not None else " (host-sized)")),

@@ -38,6 +38,7 @@ MBRWT_BUILD_NODE_KINDS = 8
 MBRWT_BUILD_SHARD_ROWS = 9
 MBRWT_BUILD_ROWS_WGS_PER_CU = 10
 MBRWT_BUILD_ROWS_CLASSES = 11
+MBRWT_BUILD_ROWS_CODE = 12
 MBRWT_KIND_FOLD_ROOT = 1
 MBRWT_KIND_PACK = 2
 MBRWT_KIND_PACK2 = 4

@@ -310,7 +310,8 @@ class BRWTDevice:
         keys = ("block_bytes", "rows_per_block", "blocks_bytes", "spill_bytes", "record_bytes", "spilled_rows",
                 "long_rows", "height")
         d = dict(zip(keys, [int(v) for v in out]))
-        d["uniform_levels"] = d["height"] >> 32  # odometer walk when > 0
+        d["uniform_levels"] = (d["height"] >> 32) & 0xFF  # odometer walk when > 0
+        d["nibble_codes"] = bool((d["height"] >> 40) & 1)  # masks as nibble codes (MBRWT_BUILD_ROWS_CODE)
         d["variable"] = d["block_bytes"] == 0  # variable-length records (csrc/rows_var.hip)
         d["height"] &= 0xFFFFFFFF
         cl = (C.c_uint64 * 4)()

@@ -745,11 +745,24 @@ int export_rows(const Ctx &c, mbrwt_tree &out) {
             }
             cols[1].push(count ? 1u : 0u);
             if (!count) return true;
-            uint32_t pos = 0;
+            uint32_t pos = 0;  // (bytes; nibbles for nibble-coded masks, rows_record.hpp RecMasks)
+            auto nibble = [&](uint32_t k) { return (uint32_t)(rec[k >> 1] >> ((k & 1u) * 4u)) & 15u; };
             auto visit = [&](uint32_t v) {  // v reached: read its mask, append its children's bits
                 const DevNode &dn = t.nodes[v];
-                uint32_t m = rec[pos++];
-                if (dn.arity > 8) m |= (uint32_t)rec[pos++] << 8;
+                uint32_t m;
+                if (im.nib) {
+                    const uint32_t c = nibble(pos);
+                    if (c < 8) {
+                        m = 1u << c;
+                        pos += 1;
+                    } else {
+                        m = nibble(pos + 1) | nibble(pos + 2) << 4;
+                        pos += 3;
+                    }
+                } else {
+                    m = rec[pos++];
+                    if (dn.arity > 8) m |= (uint32_t)rec[pos++] << 8;
+                }
                 for (uint32_t ch = 0; ch < dn.arity; ++ch) cols[dn.first_child + ch].push((m >> ch) & 1u);
                 st.push_back(Frame{dn.first_child, m});
             };

@@ -638,10 +638,14 @@ int mbrwt_set_build_option(int option, int64_t value) {
         if (value < -1 || value > 1) break;
         t.rows_classes = (int)value;
         return MBRWT_OK;
+    case MBRWT_BUILD_ROWS_CODE:
+        if (value < 0 || value > 1) break;
+        t.rows_code = (int)value;
+        return MBRWT_OK;
     default:
         break;
     }
-    if (option >= MBRWT_BUILD_ROWS_VAR && option <= MBRWT_BUILD_ROWS_CLASSES) {
+    if (option >= MBRWT_BUILD_ROWS_VAR && option <= MBRWT_BUILD_ROWS_CODE) {
         set_error("build option value out of range");
         return MBRWT_ERR_INVALID;
     }
@@ -663,7 +667,7 @@ int mbrwt_set_build_option(int option, int64_t value) {
 }
 
 int mbrwt_get_build_option(int option, int64_t *value) {
-    if (!value || option < MBRWT_BUILD_LAYOUT || option > MBRWT_BUILD_ROWS_CLASSES) {
+    if (!value || option < MBRWT_BUILD_LAYOUT || option > MBRWT_BUILD_ROWS_CODE) {
         set_error("unknown build option or null output");
         return MBRWT_ERR_INVALID;
     }
@@ -679,7 +683,8 @@ int mbrwt_get_build_option(int option, int64_t *value) {
     case MBRWT_BUILD_NODE_KINDS: *value = t.node_kinds; break;
     case MBRWT_BUILD_SHARD_ROWS: *value = (int64_t)t.shard_rows; break;
     case MBRWT_BUILD_ROWS_WGS_PER_CU: *value = t.rows_wgs_per_cu; break;
-    default: *value = t.rows_classes; break;
+    case MBRWT_BUILD_ROWS_CLASSES: *value = t.rows_classes; break;
+    default: *value = t.rows_code; break;
     }
     return MBRWT_OK;
 }
@@ -704,7 +709,7 @@ int mbrwt_rows_stats(const mbrwt_ctx *ctx, uint64_t out[8]) {
     out[4] = r.record_bytes;
     out[5] = r.spilled_rows;
     out[6] = r.long_rows;
-    out[7] = r.height | (uint64_t)r.uni << 32;
+    out[7] = r.height | (uint64_t)r.uni << 32 | (uint64_t)(r.nib ? 1 : 0) << 40;
     return MBRWT_OK;
 }
 int mbrwt_rows_classes(const mbrwt_ctx *ctx, uint64_t out[4]) {

@@ -261,6 +261,7 @@ struct RowsImage {
     uint32_t *d_table2 = nullptr;
     uint32_t frames = 0;            // its stack levels
     bool mask1 = false;             // every internal node (leaf parents too) has arity <= 8: one-byte masks
+    bool nib = false;               // masks as nibble codes (rows_record.hpp RecMasks; MBRWT_BUILD_ROWS_CODE)
     uint32_t uni = 0;               // K internal levels above leaf parents on every path (rows_walk_uni), else 0
     uint64_t bytes = 0;             // blocks + spill used
     uint32_t occ_cap = 0;           // workgroups per CU of k_traverse_rows (0 = the default; MBRWT_BUILD_ROWS_WGS_PER_CU)
@@ -538,6 +539,7 @@ struct BuildTuning {
     uint64_t shard_rows = 0;     // 0: the default shard size
     uint32_t rows_wgs_per_cu = 0;
     int rows_classes = -1;       // record classes: -1 auto, 0 never, 1 whenever exact
+    int rows_code = 0;           // record masks: 0 bytes, 1 nibble codes (uniform trees of arity <= 8)
 };
 BuildTuning &build_tuning();
 void set_build_tuning(const BuildTuning &t);

@@ -325,13 +325,20 @@ namespace {
 
 // per row of a range: record size (1 + mask bytes, < 2^15) | 0x8000 when the
 // row has >= 255 labels (its count does not fit the inline byte)
+// (nib: the masks as nibble codes, rows_record.hpp RecMasks)
 __global__ __launch_bounds__(256) void k_rows_measure(const DevNode *nodes, uint32_t folded, uint64_t n, uint16_t *sz,
-                                                      unsigned long long *acc) {
-    unsigned long long lab = 0, bytes = 0, bad = 0;
+                                                      unsigned long long *acc, uint32_t nib) {
+    unsigned long long lab = 0, bytes = 0, bad = 0, bytes1 = 0;
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gs) {
-        uint32_t b = 1;
-        const uint32_t L = emit_row_masks(nodes, folded != 0, (uint32_t)r, [&](uint32_t, uint32_t a, uint32_t) { b += rec_mask_bytes(a); });
+        uint32_t b = 1, nn = 0, b1 = 1;
+        const uint32_t L = emit_row_masks(nodes, folded != 0, (uint32_t)r, [&](uint32_t mk, uint32_t a, uint32_t) {
+            if (nib) nn += nib_codes(mk);
+            else b += rec_mask_bytes(a);
+            b1 += rec_mask_bytes(a);
+        });
+        b += (nn + 1) / 2;
+        bytes1 += b1;
         if (L == ~0u || b >= 0x8000) {
             ++bad;
             sz[r] = 0x7FFF;
@@ -345,11 +352,13 @@ __global__ __launch_bounds__(256) void k_rows_measure(const DevNode *nodes, uint
         lab += __shfl_down(lab, off);
         bytes += __shfl_down(bytes, off);
         bad += __shfl_down(bad, off);
+        bytes1 += __shfl_down(bytes1, off);
     }
     if ((threadIdx.x & 63) == 0) {
         if (lab) atomicAdd(acc + 0, lab);
         if (bytes) atomicAdd(acc + 1, bytes);
         if (bad) atomicAdd(acc + 2, bad);
+        if (bytes1) atomicAdd(acc + 3, bytes1);  // (the byte-coded size, beside a nibble measure)
     }
 }
 
@@ -411,10 +420,37 @@ __global__ __launch_bounds__(256) void k_rows_plan(const uint16_t *sz, uint64_t 
     }
 }
 
+// the masks of row r written from byte p on (bytes, or nibble codes); the
+// bytes written
+__device__ __forceinline__ uint32_t write_row_masks(const DevNode *nodes, bool folded, uint32_t r, uint8_t *p,
+                                                    uint32_t nib, uint32_t &labels) {
+    uint32_t w = 0;
+    auto put = [&](uint32_t v) {  // nibble w: byte w / 2, low half first
+        if (w & 1u) p[w >> 1] |= (uint8_t)(v << 4);
+        else p[w >> 1] = (uint8_t)v;
+        ++w;
+    };
+    labels = emit_row_masks(nodes, folded, r, [&](uint32_t mk, uint32_t a, uint32_t) {
+        if (nib) {
+            if (nib_codes(mk) == 1u) {
+                put((uint32_t)__builtin_ctz(mk));
+            } else {
+                put(8u);
+                put(mk & 15u);
+                put((mk >> 4) & 15u);
+            }
+        } else {
+            p[w++] = (uint8_t)mk;
+            if (a > 8) p[w++] = (uint8_t)(mk >> 8);
+        }
+    });
+    return nib ? (w + 1) / 2 : w;
+}
+
 // one thread per block of the range: header, inline records, spill entries
 __global__ __launch_bounds__(256) void k_rows_write(const DevNode *nodes, uint32_t folded, uint64_t nr_range,
                                                     const uint16_t *sz, uint32_t B, uint32_t S, uint8_t *blocks,
-                                                    uint8_t *spill, unsigned long long *spill_used) {
+                                                    uint8_t *spill, unsigned long long *spill_used, uint32_t nib) {
     const uint64_t nb = (nr_range + S - 1) / S;
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gs) {
@@ -429,26 +465,20 @@ __global__ __launch_bounds__(256) void k_rows_write(const DevNode *nodes, uint32
             if ((m >> t) & 1u) {
                 const uint64_t idx = atomicAdd(spill_used, (unsigned long long)spill_units(s[t]));
                 uint8_t *se = spill + idx * 16;
-                uint32_t w = 8;
-                const uint32_t L = emit_row_masks(nodes, folded != 0, r, [&](uint32_t mk, uint32_t a, uint32_t) {
-                    se[w++] = (uint8_t)mk;
-                    if (a > 8) se[w++] = (uint8_t)(mk >> 8);
-                });
+                uint32_t L = 0;
+                const uint32_t w = write_row_masks(nodes, folded != 0, r, se + 8, nib, L);
                 *reinterpret_cast<uint32_t *>(se) = L;
-                *reinterpret_cast<uint32_t *>(se + 4) = w - 8;
+                *reinterpret_cast<uint32_t *>(se + 4) = w;
                 blk[t] = (uint8_t)(o | 0x80u);
                 blk[o] = (uint8_t)std::min<uint32_t>(L, 255);
                 for (uint32_t k = 0; k < 4; ++k) blk[o + 1 + k] = (uint8_t)(idx >> (8 * k));
                 o += 5;
             } else {
                 blk[t] = (uint8_t)o;
-                uint32_t w = o + 1;
-                const uint32_t L = emit_row_masks(nodes, folded != 0, r, [&](uint32_t mk, uint32_t a, uint32_t) {
-                    blk[w++] = (uint8_t)mk;
-                    if (a > 8) blk[w++] = (uint8_t)(mk >> 8);
-                });
+                uint32_t L = 0;
+                const uint32_t w = write_row_masks(nodes, folded != 0, r, blk + o + 1, nib, L);
                 blk[o] = (uint8_t)L;
-                o = w;
+                o += 1 + w;
             }
         }
     }
@@ -570,6 +600,10 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         for (size_t i = 4; i < 4 + (size_t)im.table2[1]; ++i) im.mask1 = im.mask1 && ar8(im.table2[i]);
         im.uni = im.mask1 ? rwt2_uniform_levels(im.table2) : 0u;
         if (im.uni) append_path_table(im.table2, im.uni);
+        // nibble-coded masks (MBRWT_BUILD_ROWS_CODE = 1, r06): read by the
+        // path-table odometer and the one-lane walks, so uniform trees of
+        // one-byte masks with a path table only (the others keep bytes)
+        im.nib = build_tuning().rows_code == 1 && im.uni && im.table2.size() > 3 && im.table2[3] != 0;
     }
     if (nr > rb.sz_cap) {
         if (rb.d_sz) MBRWT_HIP(hipFree(rb.d_sz));
@@ -578,11 +612,20 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         rb.sz_cap = nr;
     }
     unsigned long long h[8];
-    MBRWT_HIP(hipMemsetAsync(rb.d_acc, 0, 8 * sizeof(unsigned long long), rb.s));
-    hipLaunchKernelGGL(k_rows_measure, dim3(build_grid(nr)), dim3(256), 0, rb.s, range.d_nodes,
-                       range.tree.folded ? 1u : 0u, nr, rb.d_sz, rb.d_acc);
-    MBRWT_HIP(hipGetLastError());
-    if (int rc = read_acc(rb, h, 3)) return rc;
+    auto measure = [&]() -> int {
+        MBRWT_HIP(hipMemsetAsync(rb.d_acc, 0, 8 * sizeof(unsigned long long), rb.s));
+        hipLaunchKernelGGL(k_rows_measure, dim3(build_grid(nr)), dim3(256), 0, rb.s, range.d_nodes,
+                           range.tree.folded ? 1u : 0u, nr, rb.d_sz, rb.d_acc, im.nib ? 1u : 0u);
+        MBRWT_HIP(hipGetLastError());
+        return read_acc(rb, h, 4);
+    };
+    if (int rc = measure()) return rc;
+    // nibble codes that do not shrink the first range's records (dense rows:
+    // most masks hold several bits) give way to bytes for the whole image
+    if (im.nib && !rb.decided && h[2] == 0 && h[1] >= h[3]) {
+        im.nib = false;
+        if (int rc = measure()) return rc;
+    }
     if (h[2]) {
         set_error("row record deeper than the build walker supports");
         return MBRWT_ERR_UNSUPPORTED;
@@ -735,7 +778,7 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
     im.spill_bytes += o[1] * 16;
     hipLaunchKernelGGL(k_rows_write, dim3(build_grid((nr + im.S - 1) / im.S)), dim3(256), 0, rb.s, range.d_nodes,
                        range.tree.folded ? 1u : 0u, nr, rb.d_sz, im.B, im.S, im.blocks + (row0 / im.S) * im.B,
-                       im.spill, im.d_spill_used);
+                       im.spill, im.d_spill_used, im.nib ? 1u : 0u);
     MBRWT_HIP(hipGetLastError());
     MBRWT_HIP(hipStreamSynchronize(rb.s));
     return MBRWT_OK;
@@ -813,14 +856,12 @@ namespace {
 // LDS stack (stk[64 k], k < lim <= kRowsMaxHeight: the tree's height) instead
 // of registers: the compaction kernel walks direct tiles with it, so its
 // register budget (and occupancy) stays that of its copy loop
-template <class ByteFn, class LeafFn>
-__device__ bool rwt_walk_lds(const uint32_t *ntab, const uint16_t *etab, ByteFn byte, LeafFn leaf,
+template <class MaskFn, class LeafFn>
+__device__ bool rwt_walk_lds(const uint32_t *ntab, const uint16_t *etab, MaskFn mask, LeafFn leaf,
                              AS_LDS uint32_t *stk, uint32_t lim) {
-    uint32_t o = 0;
     uint32_t nw = ntab[0];
     uint32_t a = (nw >> 16) & 0xFFu;
-    uint32_t m = byte(o++);
-    if (a > 8) m |= byte(o++) << 8;
+    uint32_t m = mask(a);
     uint32_t first = nw & 0xFFFFu;
     uint32_t sp = 0;
     while (true) {
@@ -841,8 +882,7 @@ __device__ bool rwt_walk_lds(const uint32_t *ntab, const uint16_t *etab, ByteFn 
         }
         nw = ntab[e];
         a = (nw >> 16) & 0xFFu;
-        uint32_t mw = byte(o++);
-        if (a > 8) mw |= byte(o++) << 8;
+        const uint32_t mw = mask(a);
         if (m) {
             if (sp == lim) return false;
             stk[64 * sp] = first | (m << 16);
@@ -1074,15 +1114,38 @@ __device__ __forceinline__ uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) 
     return r;
 }
 
-template <int K, bool LIN>
+// a record's next mask at cursor c (bytes: byte c; nibble codes, r06:
+// nibble c, rows_record.hpp RecMasks) and the cursor's advance.  The nibble
+// form reads the two bytes the code can span (LDS: a read past the record
+// stays inside the wave's slots)
+struct MaskAt {
+    uint32_t m, adv;
+};
+template <bool NIB>
+__device__ __forceinline__ MaskAt rec_mask_at(const AS_LDS uint8_t *rec, uint32_t c) {
+    if constexpr (!NIB) {
+        return MaskAt{(uint32_t)rec[c], 1u};
+    } else {
+        const uint32_t i = c >> 1;
+        const uint32_t w = ((uint32_t)rec[i] | ((uint32_t)rec[i + 1] << 8)) >> ((c & 1u) * 4u);
+        const uint32_t v = w & 15u;
+        return v < 8u ? MaskAt{1u << v, 1u} : MaskAt{(w >> 4) & 0xFFu, 3u};
+    }
+}
+
+template <int K, bool LIN, bool NIB>
 __device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_t o, bool live,
                                                const AS_LDS uint16_t *ptab, uint32_t A, AS_LDS uint16_t *out,
                                                uint32_t pos) {
-    const AS_LDS uint8_t *rc = pb + o;  // record cursor
+    const AS_LDS uint8_t *rec = pb + o;  // the record's masks
+    uint32_t rc = 0;                     // cursor (bytes or nibbles)
     uint32_t r[K], idx[K];
-    r[0] = live ? (uint32_t)rc[0] : 0u;
+    {
+        const MaskAt m0 = rec_mask_at<NIB>(rec, 0);
+        r[0] = live ? m0.m : 0u;
+        rc = m0.adv;
+    }
     idx[0] = 0;
-    ++rc;
 #pragma unroll
     for (int k = 1; k < K; ++k) r[k] = idx[k] = 0u;
     uint32_t ob = pos * 2u;  // byte offset of the next label
@@ -1098,7 +1161,8 @@ __device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_
 #pragma unroll
         for (int k = 1; k < K; ++k) {
             const uint32_t c = (uint32_t)__builtin_ctz(r[k - 1]);
-            const uint32_t b = *rc;
+            const MaskAt bm = rec_mask_at<NIB>(rec, rc);
+            const uint32_t b = bm.m;
             // the node at level k is child c of the level-(k-1) node: A_{k-1}
             // (the largest arity at level k-1) scales the parent's index
             const uint32_t Ak = k >= 2 ? (A >> (4 * (k - 2))) & 0xFu : 0u;  // (wave-uniform)
@@ -1108,7 +1172,7 @@ __device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_
             idx[k] = nd[k] ? ni : idx[k];
             r[k - 1] = nd[k] ? (r[k - 1] & (r[k - 1] - 1u)) : r[k - 1];
             r[k] = nd[k] ? b : r[k];
-            rc += nd[k] ? 1 : 0;
+            rc += nd[k] ? bm.adv : 0u;
         }
         const uint32_t c = (uint32_t)__builtin_ctz(r[K - 1]);
         r[K - 1] &= r[K - 1] - 1u;
@@ -1117,8 +1181,9 @@ __device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_
         // the leaf parent's first column: computed on a linear path table (no
         // LDS round trip per iteration), else read
         const uint32_t base = LIN ? pidx << ((A >> 24) & 0x1Fu) : (uint32_t)ptab[pidx];
-        uint32_t x = *rc;
-        ++rc;
+        const MaskAt xm = rec_mask_at<NIB>(rec, rc);
+        uint32_t x = xm.m;
+        rc += xm.adv;
         *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)(base + (uint32_t)__builtin_ctz(x));
         ob += 2u;
         x &= x - 1u;
@@ -1241,7 +1306,7 @@ constexpr uint32_t kRowsTilesPerWave = 1;
 // workgroup); WALK: the walk family.  (r06: a one-pass form that wrote the
 // CSR itself, its place found by a decoupled look-back, measured 0.44-0.48
 // against 0.33 ms per C4 step and was retired: profiles/r06/v01_one_pass.)
-template <int B, int WPB, bool NT, uint32_t WALK>
+template <int B, int WPB, bool NT, uint32_t WALK, bool NIB = false>
 __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows[];
     const uint32_t lane = threadIdx.x & 63;
@@ -1423,9 +1488,9 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
 #define MBRWT_PATH_CASE(K)                                                      \
     case K:                                                                     \
         if (lin)                                                                \
-            rows_walk_path<K, true>(rec, o, live, ptab, pA, stage, pos);        \
+            rows_walk_path<K, true, NIB>(rec, o, live, ptab, pA, stage, pos);   \
         else                                                                    \
-            rows_walk_path<K, false>(rec, o, live, ptab, pA, stage, pos);       \
+            rows_walk_path<K, false, NIB>(rec, o, live, ptab, pA, stage, pos);  \
         break;
                     switch (p.uni) {
                         MBRWT_PATH_CASE(1)
@@ -1589,7 +1654,7 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
             uint32_t *dst = p.cols + base[k];
             uint32_t j = 0;
             const bool ok = rwt_walk_lds(
-                ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
+                ntab, etab, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, p.v.nib),
                 [&](uint32_t col) {
                     if (j < count) gst(dst + j, col);
                     ++j;
@@ -1620,7 +1685,7 @@ __global__ __launch_bounds__(256) void k_rows_get(RowsView v, const uint32_t *ta
         uint32_t hit = 0;
         if (count)
             (void)rwt_walk(
-                ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
+                ntab, etab, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
                 [&](uint32_t c) { hit |= c == col; }, [](uint32_t) {});
         gst(out + i, (uint8_t)hit);
     }
@@ -1649,7 +1714,7 @@ __global__ __launch_bounds__(256) void k_rows_count(RowsView v, const uint32_t *
         vis += 1;
         if (!count) continue;
         (void)rwt_walk(
-            ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
+            ntab, etab, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
             [&](uint32_t c) {
                 if constexpr (WORK) ++lab;
                 else atomicAdd(counts + c, 1ull);
@@ -1685,7 +1750,7 @@ struct RowHasColumn {
         const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + table[0]);
         bool hit = false;
         (void)rwt_walk(
-            ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
+            ntab, etab, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
             [&](uint32_t c) { hit |= c == col; }, [](uint32_t) {});
         return hit;
     }
@@ -1703,6 +1768,7 @@ RowsView view_of(const Ctx &c) {
     v.num_rows = c.rows.classes ? c.rows.num_classes : c.tree.num_rows;  // (classes: the dictionary's records)
     v.B = c.rows.B;
     v.S = c.rows.S;
+    v.nib = c.rows.nib ? 1u : 0u;
     return v;
 }
 
@@ -1713,7 +1779,8 @@ constexpr uint32_t kRowsWpb = 8;
 // 8-wave workgroups per CU (16 waves); two of 11 waves fit (22)
 constexpr uint32_t kRowsWpbWide = 11;
 template <int B, bool NT>
-RowsFn rows_fn_b(uint32_t walk, uint32_t wpb) {
+RowsFn rows_fn_b(uint32_t walk, uint32_t wpb, bool nib) {
+    if (nib) return k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER, true>;  // (nibble codes: the path odometer)
     if (wpb == kRowsWpbWide) return k_traverse_rows<B, kRowsWpbWide, NT, WALK_TREE_ODOMETER>;
     return walk == WALK_ODOMETER        ? k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER>
            : walk == WALK_TREE_ODOMETER ? k_traverse_rows<B, kRowsWpb, NT, WALK_TREE_ODOMETER>
@@ -1722,8 +1789,8 @@ RowsFn rows_fn_b(uint32_t walk, uint32_t wpb) {
 }
 RowsFn rows_fn(const RowsImage &im, uint32_t walk, uint32_t wpb) {
     const bool nt = im.bytes > (1ull << 30);  // non-temporal block reads for images beyond the caches
-    if (im.B == 64) return nt ? rows_fn_b<64, true>(walk, wpb) : rows_fn_b<64, false>(walk, wpb);
-    return nt ? rows_fn_b<128, true>(walk, wpb) : rows_fn_b<128, false>(walk, wpb);
+    if (im.B == 64) return nt ? rows_fn_b<64, true>(walk, wpb, im.nib) : rows_fn_b<64, false>(walk, wpb, im.nib);
+    return nt ? rows_fn_b<128, true>(walk, wpb, im.nib) : rows_fn_b<128, false>(walk, wpb, im.nib);
 }
 // resident waves per CU with workgroups of w waves: the LDS (160 KiB per CU:
 // the table once per workgroup + per_wave bytes per wave) within the 24-wave cap
@@ -1758,6 +1825,7 @@ struct MaskTile {
 // (MBRWT_OPT_ROWS_WALK = 6 forces the non-odometer walk: tests)
 static uint32_t rows_walk_of(const Ctx &c) {
     const RowsImage &im = c.rows;
+    if (im.nib) return WALK_ODOMETER;  // (nibble codes: only the path odometer reads them)
     if (im.uni && c.rows_walk != 6 && c.rows_walk != 4 && c.rows_walk != 3)
         return WALK_ODOMETER;  // (7: without the path table)
     // (A/B: 6 = rows_walk6 where every mask is one byte, 4 = rows_walk4)
@@ -1829,7 +1897,7 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     p.scalars = d_sc;
     p.status = st_blk;
     p.uni = im.uni;
-    p.path_walk = c.rows_walk == 7 ? 0u : 1u;  // (7: the r03 odometer, A/B)
+    p.path_walk = (c.rows_walk == 7 && !im.nib) ? 0u : 1u;  // (7: the r03 odometer, A/B)
     p.stk_words = walk >= WALK_ODOMETER ? 0u : rows_stack_words(im);  // (the odometers keep no stack)
     p.frames = im.frames;
     p.mask1 = im.mask1 ? 1u : 0u;

@@ -64,10 +64,12 @@ __device__ bool record_of(const RowsView &v, const uint32_t *table, uint64_t r, 
     const uint64_t m = rr.masks;
     const bool ok = rwt_walk(
         ntab, etab,
-        [&](uint32_t o) {
-            hi = o + 1;
-            return (uint32_t)gld_at<uint8_t>(m + o);
-        },
+        rec_masks(
+            [&](uint32_t o) {
+                hi = o + 1 > hi ? o + 1 : hi;
+                return (uint32_t)gld_at<uint8_t>(m + o);
+            },
+            v.nib),
         [](uint32_t) {}, [](uint32_t) {});
     rr.len = hi;
     return ok;
@@ -210,7 +212,7 @@ __global__ __launch_bounds__(256) void k_class_has(RowsView v, const uint32_t *t
         bool hit = false;
         if (count)
             (void)rwt_walk(
-                ntab, etab, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); },
+                ntab, etab, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
                 [&](uint32_t c) { hit |= c == col; }, [](uint32_t) {});
         gst(has + k, (uint8_t)(hit ? 1 : 0));
     }
@@ -236,6 +238,7 @@ RowsView block_view(const RowsImage &im, uint64_t records) {
     v.num_rows = records;
     v.B = im.B;
     v.S = im.S;
+    v.nib = im.nib ? 1u : 0u;
     return v;
 }
 
@@ -264,7 +267,9 @@ struct Scratch {
 }  // namespace
 
 int rows_classes_build(RowsImage &im, uint64_t n, int mode, uint64_t *sample_distinct, hipStream_t s) {
-    if (mode == 0 || im.var || !im.blocks || !im.d_table || n < 2 || n > (1ull << 32)) return MBRWT_OK;
+    // (nibble-coded records: no classes -- a compact image of rows that do not
+    // repeat; the two compressions answer different data)
+    if (mode == 0 || im.var || im.nib || !im.blocks || !im.d_table || n < 2 || n > (1ull << 32)) return MBRWT_OK;
     const RowsView v = block_view(im, n);
     Scratch sc;
     unsigned long long *d_err = sc.get<unsigned long long>(4);

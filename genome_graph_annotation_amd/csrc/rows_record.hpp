@@ -16,6 +16,7 @@ namespace mbrwt {
 struct RowsView {
     uint64_t blocks, spill, magic, num_rows;
     uint32_t B, S;
+    uint32_t nib;  // masks stored as nibble codes (RowsImage::nib)
 };
 __device__ __forceinline__ uint64_t rows_block(uint64_t r, uint32_t S, uint64_t magic) {
     return S == 1 ? r : __umul64hi(r, magic);
@@ -39,16 +40,50 @@ __device__ __forceinline__ void rows_locate(const RowsView &v, uint64_t r, uint6
     }
 }
 
-// DFS walk of a record (masks from byte 0 of `byte`) over the RWT table:
+// The masks of a record, one per call (mask(arity)), from the record's
+// bytes byte(k): one byte per mask (two for arity > 8), or (RowsImage::nib,
+// r06) NIBBLE CODES for arity <= 8 -- a mask with one bit set is the nibble
+// of its bit's index (0..7), any other mask the nibble 8 and its two halves,
+// low first; nibble k is in byte k / 2, low half first.  At the Kingsford
+// shape most masks of a row's descent hold one bit (the leaf parents' and
+// most of the level above), so a record takes 15.2 instead of 21.3 bytes.
+template <class ByteFn>
+struct RecMasks {
+    ByteFn byte;
+    uint32_t nib;
+    uint32_t c;
+    __device__ __forceinline__ uint32_t nibble(uint32_t k) { return (byte(k >> 1) >> ((k & 1u) * 4u)) & 15u; }
+    __device__ __forceinline__ uint32_t operator()(uint32_t a) {
+        if (!nib) {
+            uint32_t m = byte(c++);
+            if (a > 8) m |= byte(c++) << 8;
+            return m;
+        }
+        const uint32_t v = nibble(c);
+        if (v < 8) {
+            c += 1;
+            return 1u << v;
+        }
+        const uint32_t m = nibble(c + 1) | nibble(c + 2) << 4;
+        c += 3;
+        return m;
+    }
+};
+template <class ByteFn>
+__device__ __forceinline__ RecMasks<ByteFn> rec_masks(ByteFn byte, uint32_t nib) {
+    return RecMasks<ByteFn>{byte, nib, 0u};
+}
+// the nibbles one mask (arity <= 8, non-zero) takes as a nibble code
+__host__ __device__ __forceinline__ uint32_t nib_codes(uint32_t m) { return (m && !(m & (m - 1))) ? 1u : 3u; }
+
+// DFS walk of a record (its masks from `mask`, a RecMasks) over the RWT table:
 // leaf(column) per set leaf in pre-order (BRWT.cpp:45-51), inner(arity) per
 // mask read (the root's included).  One lane; false past kRowsMaxHeight.
-template <class ByteFn, class LeafFn, class InnerFn>
-__device__ bool rwt_walk(const uint32_t *ntab, const uint16_t *etab, ByteFn byte, LeafFn leaf, InnerFn inner) {
-    uint32_t o = 0;
+template <class MaskFn, class LeafFn, class InnerFn>
+__device__ bool rwt_walk(const uint32_t *ntab, const uint16_t *etab, MaskFn mask, LeafFn leaf, InnerFn inner) {
     uint32_t nw = ntab[0];
     uint32_t a = (nw >> 16) & 0xFFu;
-    uint32_t m = byte(o++);
-    if (a > 8) m |= byte(o++) << 8;
+    uint32_t m = mask(a);
     inner(a);
     uint32_t first = nw & 0xFFFFu;
     uint32_t sf[kRowsMaxHeight], sm[kRowsMaxHeight];
@@ -70,8 +105,7 @@ __device__ bool rwt_walk(const uint32_t *ntab, const uint16_t *etab, ByteFn byte
         }
         nw = ntab[e];
         a = (nw >> 16) & 0xFFu;
-        uint32_t mw = byte(o++);
-        if (a > 8) mw |= byte(o++) << 8;
+        const uint32_t mw = mask(a);
         inner(a);
         if (m) {
             if (sp == (int)kRowsMaxHeight) return false;

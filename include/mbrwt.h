@@ -237,7 +237,15 @@ int mbrwt_ctx_clone(mbrwt_ctx *src, mbrwt_ctx **out);
                               there are at most half as many classes as rows
                               and they at least halve the image), 0 never,
                               1 whenever they fit (always exact: every row's
-                              record is compared with its class's) */
+                              record is compared with its class's)
+   MBRWT_BUILD_ROWS_CODE      how a row record stores its masks:
+                              0 (default) one byte per mask, 1 NIBBLE CODES
+                              -- a mask with one bit set as that bit's index
+                              in 4 bits, any other as 12 bits -- for uniform
+                              trees of arity <= 8 (the basic partitioner's:
+                              C2-C4; other trees keep bytes): 15.2 instead of
+                              21.3 bytes per Kingsford-shape record, three
+                              rows per 64-byte block */
 #define MBRWT_BUILD_ROWS_VAR 4
 #define MBRWT_BUILD_VAR_LANES 5
 #define MBRWT_BUILD_ROWS_BLOCK 6
@@ -246,6 +254,7 @@ int mbrwt_ctx_clone(mbrwt_ctx *src, mbrwt_ctx **out);
 #define MBRWT_BUILD_SHARD_ROWS 9
 #define MBRWT_BUILD_ROWS_WGS_PER_CU 10
 #define MBRWT_BUILD_ROWS_CLASSES 11
+#define MBRWT_BUILD_ROWS_CODE 12
 #define MBRWT_KIND_FOLD_ROOT 1
 #define MBRWT_KIND_PACK 2
 #define MBRWT_KIND_PACK2 4

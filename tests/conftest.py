@@ -60,7 +60,7 @@ def _build_option_of(name, value):
         return L.MBRWT_BUILD_LAYOUT, L.LAYOUTS[value]
     table = {"MBRWT_ROWS_VAR": L.MBRWT_BUILD_ROWS_VAR, "MBRWT_VAR_G": L.MBRWT_BUILD_VAR_LANES,
              "MBRWT_ROWS_RANGE": L.MBRWT_BUILD_ROWS_RANGE, "MBRWT_SHARD_ROWS": L.MBRWT_BUILD_SHARD_ROWS,
-             "MBRWT_ROWS_WGS_PER_CU": L.MBRWT_BUILD_ROWS_WGS_PER_CU}
+             "MBRWT_ROWS_WGS_PER_CU": L.MBRWT_BUILD_ROWS_WGS_PER_CU, "MBRWT_ROWS_CODE": L.MBRWT_BUILD_ROWS_CODE}
     return table[name], int(value)
 
 

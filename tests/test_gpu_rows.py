@@ -418,6 +418,86 @@ def test_async_capacity_boundary_and_batches(oracle_mod, shape):
     np.testing.assert_array_equal(ct[:len(cols_o)].cpu().numpy().view(np.uint32), cols_o)
 
 
+# ---- nibble-coded masks (r06, MBRWT_BUILD_ROWS_CODE = 1) ------------
+
+@pytest.mark.parametrize("n,m,d,arity", [
+    (20000, 2652, 0.003, 8),   # the Kingsford shape (C2-C4)
+    (20000, 512, 0.02, 8),
+    (5000, 2652, 0.3, 8),      # dense rows: multi-bit masks, spills, long records, direct tiles
+    (20000, 64, 0.05, 2),      # binary, 5 internal levels
+    (20000, 100, 0.05, 8),     # a short last group
+    (20000, 9, 0.2, 3),        # the root's children are leaf parents
+    (3000, 40, 0.0, 8),        # rows without labels
+])
+def test_nibble_codes(oracle_mod, build_env, n, m, d, arity):
+    """Row records whose masks are nibble codes: every query (ordered CSR,
+    point queries, columns, count_labels, the V/L accounting, the async call)
+    against the oracle and against the byte-coded image of the same tree,
+    and the image exported back into the reference's index columns."""
+    O = oracle_mod
+    import torch
+    from genome_graph_annotation_amd import BRWTDevice, _lib as L
+    rng = np.random.default_rng(n + m + arity)
+    dense = rng.random((n, m)) < d
+    t = O.OracleTree.from_dense(dense, "basic", arity)
+    ex = t.export()
+    plain = BRWTDevice.from_tree(ex, layout="rows")
+    build_env("MBRWT_ROWS_CODE", 1)
+    dev = BRWTDevice.from_tree(ex, layout="rows")
+    st, sp = dev.rows_stats(), plain.rows_stats()
+    assert not sp["nibble_codes"] and (sp["uniform_levels"] > 0 or not st["nibble_codes"]), (st, sp)
+    # nibble codes where they shrink the records (bytes kept otherwise: dense rows)
+    assert st["record_bytes"] <= sp["record_bytes"], (st, sp)
+    assert st["nibble_codes"] == (st["record_bytes"] < sp["record_bytes"]), (st, sp)
+    if (m, d) == (2652, 0.003):
+        assert st["nibble_codes"] and st["record_bytes"] < 0.8 * sp["record_bytes"], (st, sp)
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 20000)]).astype(np.uint64)
+    off_o, cols_o = _check_all(t, dev, rows, dense)
+    np.testing.assert_array_equal(_count_labels(dev, rows), _count_labels(plain, rows))
+    rt = torch.from_numpy(rows.view(np.int64)).cuda()
+    assert dev.count_work_device(rt) == plain.count_work_device(rt)
+    # the asynchronous call
+    s = torch.cuda.current_stream().cuda_stream
+    stt = torch.zeros(3, dtype=torch.int64, device="cuda")
+    ot = torch.empty(len(rows) + 1, dtype=torch.int64, device="cuda")
+    ct = torch.empty(len(cols_o) + 1, dtype=torch.int32, device="cuda")
+    dev.get_rows_device_async(rt, ot, ct, stt, s)
+    torch.cuda.synchronize()
+    assert stt.cpu().tolist() == [len(cols_o), L.MBRWT_OK, 1 << L.MBRWT_OK]
+    np.testing.assert_array_equal(ot.cpu().numpy().view(np.uint64), off_o)
+    # the reference's index columns read back from the nibble-coded records
+    back = dev.export()
+    for k in ("num_children", "first_child", "leaf_column"):
+        np.testing.assert_array_equal(np.asarray(back[k]), np.asarray(ex[k]))
+    again = BRWTDevice.from_tree(back, layout="rows")
+    off_a, cols_a = again.get_rows(rows)
+    np.testing.assert_array_equal(off_a, off_o)
+    np.testing.assert_array_equal(cols_a, cols_o)
+
+
+def test_nibble_codes_kingsford_synthetic(oracle_mod, build_env):
+    """The C2 shape generated on the device with nibble-coded records: the
+    whole batch against the oracle's independent generator, three rows per
+    64-byte block, and the image at most 0.75x the byte-coded one."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    n, m, d = 1_000_000, 2652, 0.003
+    plain = BRWTDevice.synthetic(n, m, d, 8, 42, layout="rows")
+    build_env("MBRWT_ROWS_CODE", 1)
+    dev = BRWTDevice.synthetic(n, m, d, 8, 42, layout="rows")
+    st = dev.rows_stats()
+    assert st["nibble_codes"] and st["block_bytes"] == 64 and st["rows_per_block"] >= 3, st
+    assert dev.device_bytes() <= 0.75 * plain.device_bytes(), (dev.device_bytes(), plain.device_bytes())
+    t = O.OracleTree.topdown(n, m, d, 8, 42)
+    rows = np.random.default_rng(42).integers(0, n, 300_000).astype(np.uint64)
+    off_o, cols_o = t.get_rows(rows)
+    off_d, cols_d = dev.get_rows(rows)
+    np.testing.assert_array_equal(off_d, off_o)
+    np.testing.assert_array_equal(cols_d, cols_o)
+    for c in (0, 1, 1000, m - 1):
+        assert dev.get_column(c).tolist() == t.get_column(c)
+
+
 def test_classify_on_rows(oracle_mod):
     """get_labels / get_top_labels batches (classify) over row records, against
     the reference's semantics applied to the oracle's rows

@@ -100,6 +100,9 @@ def main():
     ap.add_argument("--compact", action="store_true",
                     help="row records built with MBRWT_BUILD_ROWS_FOOTPRINT = MBRWT_ROWS_COMPACT (the smallest image "
                          "within 30 %% of the fewest modelled requests per row)")
+    ap.add_argument("--blocks", default="",
+                    help="scaled shape: comma-separated row-record block shapes 'B:S' to build and measure one after "
+                         "the other (MBRWT_BUILD_ROWS_BLOCK; '' = the automatic choice only, 'auto' names it)")
     ap.add_argument("--layout", default="nodes", choices=["nodes", "rows", "both"],
                     help="device layout (include/mbrwt.h MBRWT_BUILD_LAYOUT)")
     a = ap.parse_args()
@@ -149,25 +152,32 @@ def main():
         for shape, (exp, build_s) in shapes.items():
             keep = {k: exp[k] for k in ("num_children", "first_child", "leaf_column")}
             nc = np.asarray(keep["num_children"])
-            t0 = time.time()
             from genome_graph_annotation_amd import _lib as LB
             from genome_graph_annotation_amd.brwt import build_option
-            with build_option(LB.MBRWT_BUILD_ROWS_FOOTPRINT,
-                              LB.MBRWT_ROWS_COMPACT if a.compact else LB.MBRWT_ROWS_FAST):
-                dev = BRWTDevice.synthetic_shaped(a.scaled_rows, keep, a.density, 42, layout=a.layout)
-            torch.cuda.synchronize()
-            gen_s = time.time() - t0
-            t0 = time.time()
-            ref = O.topdown_get_rows_shaped(a.scaled_rows, keep, a.density, 42, srows)
-            log(f"scaled {shape}: {a.scaled_rows:,} rows, {len(nc)} nodes, max arity {int(nc.max())}, device "
-                f"{dev.device_bytes() / 1e9:.2f} GB (generated in {gen_s:.1f} s), kernel {dev.traverse_kernel()}, "
-                f"streamed oracle {time.time() - t0:.0f} s")
-            r = measure(dev, srows, ref, variants, a.reps)
-            r.update({"layout": dev.layout(), "rows_stats": dev.rows_stats(), "nodes": len(nc), "max_arity": int(nc.max()), "device_bytes": int(dev.device_bytes()),
-                      "generate_s": gen_s, "rows": a.scaled_rows, "batch": a.scaled_batch,
-                      "num_relations": int(dev.num_relations())})
-            res[f"scaled {shape}"] = r
-            del dev
+            ref = None
+            for blk in (a.blocks.split(",") if a.blocks else ["auto"]):
+                t0 = time.time()
+                bs = 0 if blk == "auto" else (int(blk.split(":")[0]) << 8) | int(blk.split(":")[1])
+                with build_option(LB.MBRWT_BUILD_ROWS_FOOTPRINT,
+                                  LB.MBRWT_ROWS_COMPACT if a.compact else LB.MBRWT_ROWS_FAST), \
+                        build_option(LB.MBRWT_BUILD_ROWS_BLOCK, bs):
+                    dev = BRWTDevice.synthetic_shaped(a.scaled_rows, keep, a.density, 42, layout=a.layout)
+                torch.cuda.synchronize()
+                gen_s = time.time() - t0
+                t0 = time.time()
+                if ref is None:
+                    ref = O.topdown_get_rows_shaped(a.scaled_rows, keep, a.density, 42, srows)
+                log(f"scaled {shape} (blocks {blk}): {a.scaled_rows:,} rows, {len(nc)} nodes, max arity "
+                    f"{int(nc.max())}, device {dev.device_bytes() / 1e9:.2f} GB (generated in {gen_s:.1f} s), "
+                    f"kernel {dev.traverse_kernel()}, rows_stats {dev.rows_stats()}")
+                r = measure(dev, srows, ref, variants, a.reps)
+                r.update({"layout": dev.layout(), "rows_stats": dev.rows_stats(), "nodes": len(nc),
+                          "max_arity": int(nc.max()), "device_bytes": int(dev.device_bytes()),
+                          "generate_s": gen_s, "rows": a.scaled_rows, "batch": a.scaled_batch,
+                          "num_relations": int(dev.num_relations()), "blocks": blk})
+                res[f"scaled {shape}" + ("" if blk == "auto" else f" blocks {blk}")] = r
+                del dev
+                torch.cuda.empty_cache()
     print(json.dumps({"workload": f"C2 columns {a.rows:,} x {a.cols:,} d={a.density} (mt19937 seed 42), batch "
                                   f"{a.batch:,} uniform rows (seed 42)", "shapes": res}), flush=True)
 

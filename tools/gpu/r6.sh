@@ -1,16 +1,17 @@
 # r06 GPU steps (run from the repo root:
-#   /usr/local/graft/bin/gpurun --timeout 900 -- bash tools/gpu/r6.sh STAGE)
+#   /usr/local/graft/bin/gpurun --timeout 900 -- bash tools/gpu/r6.sh STAGE [STAGE ...])
 # Every GPU step has its own time limit, steps chain with &&, a heartbeat
 # file shows progress.  Outputs: gpurun_out/r6_STAGE/ (copied to profiles/r06/).
 set -o pipefail
-STAGE="$1"
-O=gpurun_out/r6_$STAGE; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-( for i in $(seq 1 30); do sleep 60; echo "heartbeat $i $(date +%T)" >> $O/heartbeat.log; done ) &
+mkdir -p gpurun_out
+( for i in $(seq 1 30); do sleep 60; echo "heartbeat $i $(date +%T)" >> gpurun_out/r6_heartbeat.log; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 PYT="python -u -m pytest -v --timeout 300 --timeout-method thread"
 B="python -u bench.py --no-e2e --no-probe --traffic off"
+for STAGE in "$@"; do
+O=gpurun_out/r6_$STAGE; mkdir -p $O
 case "$STAGE" in
 onepass)  # the one-pass traversal: row-record tests, then a same-box A/B against the two-kernel path
   timeout -k 10 700 $PYT tests/test_gpu_rows.py -k "one_pass or odometer or tree_odometer or errors or async or clone or synthetic_c2 or greedy_relax" > $O/pytest_rows.log 2>&1 &&
@@ -28,5 +29,15 @@ trace)  # C4 bench (live PMC, ceilings) and the kernel trace of its two-stream t
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_c4 -o run --output-format csv -- python -u bench.py --no-cpu --no-e2e --no-probe --traffic off --steps 50 > $O/bench_c4_under_rocprof.log 2>&1 &&
   python tools/trace_overlap.py $(find $O/prof_c4 -name "*kernel_trace.csv" | head -1) > $O/overlap.json 2>&1
   ;;
+greedy)  # the greedy + relax shape at 3.7 B rows: the automatic block shape and the alternatives
+  timeout -k 10 900 python -u tools/bench_greedy.py --shape-npz tools/data/greedy_relax10_c2_shape.npz --scaled-rows 3700000000 --layout rows --variants 0 --reps 10 --skip-small --blocks auto,128:3,64:1 > $O/greedy_blocks.log 2>&1
+  ;;
+nib)  # nibble-coded records: the row-record tests, C4 with nibble codes (parity) and bytes (A/B)
+  timeout -k 10 700 $PYT tests/test_gpu_rows.py tests/test_gpu_classes.py tests/test_gpu_files.py > $O/pytest_rows.log 2>&1 &&
+  timeout -k 10 400 python -u bench.py --no-e2e --traffic off --rows-code 1 > $O/bench_c4_nib.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --rows-code 0 > $O/bench_c4_byte.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --rows-code 1 > $O/bench_c4_nib2.log 2>&1
+  ;;
 *) echo "unknown stage $STAGE"; exit 2 ;;
-esac
+esac || exit $?
+done
