@@ -38,6 +38,12 @@ nib)  # nibble-coded records: the row-record tests, C4 with nibble codes (parity
   timeout -k 10 200 $B --no-cpu --rows-code 0 > $O/bench_c4_byte.log 2>&1 &&
   timeout -k 10 200 $B --no-cpu --rows-code 1 > $O/bench_c4_nib2.log 2>&1
   ;;
+nib2)  # nibble decode with one 4-byte LDS read: the nibble tests, C4 nibble (parity) / byte A/B
+  timeout -k 10 700 $PYT tests/test_gpu_rows.py -k "nibble or odometer or async or errors" > $O/pytest_rows.log 2>&1 &&
+  timeout -k 10 400 python -u bench.py --no-e2e --traffic off --rows-code 1 > $O/bench_c4_nib.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --rows-code 0 > $O/bench_c4_byte.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --rows-code 1 > $O/bench_c4_nib2.log 2>&1
+  ;;
 *) echo "unknown stage $STAGE"; exit 2 ;;
 esac || exit $?
 done
