@@ -101,6 +101,9 @@ def parse():
     ap.add_argument("--rows-code", type=int, default=0, choices=[0, 1],
                     help="row-record masks: 0 bytes (library default), 1 nibble codes (MBRWT_BUILD_ROWS_CODE: the "
                          "compact image, DESIGN §4g)")
+    ap.add_argument("--compact-cus", type=int, default=0,
+                    help="row records: run each query stream's compaction on a stream masked to K of every 32 "
+                         "CUs (MBRWT_OPT_COMPACT_CUS, VERDICT r05 #1a; 0 = the library default, same stream)")
     ap.add_argument("--query-streams", type=int, default=2, choices=[1, 2],
                     help="N = 1: consecutive batches alternate between the context and a clone of it "
                          "(mbrwt_ctx_clone: the same image, separate workspaces) on the default stream and "
@@ -476,6 +479,9 @@ def main():
         qmats.append(mat.clone())
         qstreams.append(torch.cuda.Stream(dev_t))
         qstatus.append(torch.zeros(3, dtype=torch.int64, device=dev_t))
+    if a.compact_cus:
+        for qm in qmats:
+            qm.set_option(L.MBRWT_OPT_COMPACT_CUS, a.compact_cus)
     # outputs: step i writes bufs[i mod len]; with two buffers a buffer's next
     # writer is two steps later on the SAME stream, behind this step's readers
     # (its compaction, its pack) -- double-buffered whenever steps overlap
@@ -902,6 +908,7 @@ def main():
             "api": "mbrwt_get_rows_device_async" if use_async else "mbrwt_get_rows_device",
             "query_streams": Q,
             "rows_code": "nibble" if a.rows_code else "byte",
+            **({"compact_cus_of_32": a.compact_cus} if a.compact_cus else {}),
             "parallelism": f"batch-sharded x{world}, tree replicated" + ("" if world == 1 or a.no_gather
                                                                          else ", all-gatherv over " + ("RCCL" if a.dist_backend == "nccl" else a.dist_backend)
                                                                          + (" (device-sized wire, no host sync)" if wire is not None else " (host-sized)")),

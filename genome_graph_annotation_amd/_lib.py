@@ -26,6 +26,7 @@ MBRWT_OPT_SLOT_LABELS = 2
 MBRWT_OPT_KERNEL = 4
 MBRWT_OPT_ROWS_WALK = 8
 MBRWT_OPT_TEST_FAIL_CHUNK = 32  # test hook (host-buffer path)
+MBRWT_OPT_COMPACT_CUS = 64  # row records: compaction on a CU-masked stream (measurement)
 
 MBRWT_BUILD_LAYOUT = 1
 MBRWT_BUILD_PARTITIONER = 2

@@ -647,7 +647,7 @@ int export_var(const Ctx &c, mbrwt_tree &out) {
                                 st.pop_back();
                                 continue;
                             }
-                            const uint32_t ch = (uint32_t)__builtin_ctz(f.rem);
+                            const uint32_t ch = (uint32_t)__builtin_ctzll(f.rem);
                             f.rem &= f.rem - 1;
                             const uint32_t w = f.fc + ch;
                             if (t.nodes[w].kind != KIND_LEAF) visit(w);
@@ -725,7 +725,7 @@ int export_rows(const Ctx &c, mbrwt_tree &out) {
         std::vector<uint8_t> blk;
         struct Frame {
             uint32_t fc;   // first child (dnode)
-            uint32_t rem;  // children still to visit
+            uint64_t rem;  // children still to visit
         };
         std::vector<Frame> st;
         // one row's record (entry tt of block bp) -> its bits of every index column
@@ -749,7 +749,7 @@ int export_rows(const Ctx &c, mbrwt_tree &out) {
             auto nibble = [&](uint32_t k) { return (uint32_t)(rec[k >> 1] >> ((k & 1u) * 4u)) & 15u; };
             auto visit = [&](uint32_t v) {  // v reached: read its mask, append its children's bits
                 const DevNode &dn = t.nodes[v];
-                uint32_t m;
+                uint64_t m;
                 if (im.nib) {
                     const uint32_t c = nibble(pos);
                     if (c < 8) {
@@ -759,9 +759,9 @@ int export_rows(const Ctx &c, mbrwt_tree &out) {
                         m = nibble(pos + 1) | nibble(pos + 2) << 4;
                         pos += 3;
                     }
-                } else {
+                } else {  // one byte per 8 children (arity <= 64)
                     m = rec[pos++];
-                    if (dn.arity > 8) m |= (uint32_t)rec[pos++] << 8;
+                    for (uint32_t k = 8; k < dn.arity; k += 8) m |= (uint64_t)rec[pos++] << k;
                 }
                 for (uint32_t ch = 0; ch < dn.arity; ++ch) cols[dn.first_child + ch].push((m >> ch) & 1u);
                 st.push_back(Frame{dn.first_child, m});
@@ -774,7 +774,7 @@ int export_rows(const Ctx &c, mbrwt_tree &out) {
                     st.pop_back();
                     continue;
                 }
-                const uint32_t ch = (uint32_t)__builtin_ctz(f.rem);
+                const uint32_t ch = (uint32_t)__builtin_ctzll(f.rem);
                 f.rem &= f.rem - 1;
                 const uint32_t w = f.fc + ch;
                 if (t.nodes[w].kind != KIND_LEAF) visit(w);

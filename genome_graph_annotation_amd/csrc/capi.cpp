@@ -106,6 +106,9 @@ static void release(Ctx *c) {
     if (c->h_scalars) (void)hipHostFree(c->h_scalars);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev_trav) (void)hipEventDestroy(c->ev_trav);
+    if (c->ev_comp) (void)hipEventDestroy(c->ev_comp);
+    if (c->s_compact) (void)hipStreamDestroy(c->s_compact);
     for (auto &pr : c->async_ev) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -1049,6 +1052,30 @@ static int apply_option(Ctx &c, int option, int64_t value) {
     case MBRWT_OPT_TEST_FAIL_CHUNK:
         c.test_fail_chunk = value < 0 ? -1 : value;
         return MBRWT_OK;
+    case MBRWT_OPT_COMPACT_CUS: {
+        if (value < 0 || value > 31) return MBRWT_ERR_INVALID;
+        if ((uint32_t)value == c.compact_cus) return MBRWT_OK;
+        MBRWT_HIP(hipSetDevice(c.device));
+        if (c.s_compact) {
+            MBRWT_HIP(hipStreamSynchronize(c.s_compact));
+            MBRWT_HIP(hipStreamDestroy(c.s_compact));
+            c.s_compact = nullptr;
+        }
+        c.compact_cus = 0;
+        if (value == 0) return MBRWT_OK;
+        // CU k is in the mask when k % 32 < value: the same share of every
+        // XCD whether the logical CU ids run across the XCDs or within them
+        int cus = 0;
+        MBRWT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device));
+        std::vector<uint32_t> mask((std::max(cus, 1) + 31) / 32, 0u);
+        for (int k = 0; k < cus; ++k)
+            if ((uint32_t)(k % 32) < (uint32_t)value) mask[k / 32] |= 1u << (k % 32);
+        MBRWT_HIP(hipExtStreamCreateWithCUMask(&c.s_compact, (uint32_t)mask.size(), mask.data()));
+        if (!c.ev_trav) MBRWT_HIP(hipEventCreateWithFlags(&c.ev_trav, hipEventDisableTiming));
+        if (!c.ev_comp) MBRWT_HIP(hipEventCreateWithFlags(&c.ev_comp, hipEventDisableTiming));
+        c.compact_cus = (uint32_t)value;
+        return MBRWT_OK;
+    }
     case MBRWT_OPT_KERNEL:
         if (!(value >= 0 && value <= 6) && value != 10 && !(value >= 17 && value <= 20) && !(value >= 24 && value <= 30))
             return MBRWT_ERR_INVALID;

@@ -237,12 +237,14 @@ struct Workspace {
 //     spilled entry [u8 min(count, 255)][u32 LE spill offset in 16-byte units]
 //   spill entry (16-byte aligned): [u32 count][u32 mask bytes][masks]
 // An empty row (no label) is the one-byte entry [0].
-// RWT table (the walk's tree, staged in LDS): u32 words
+// RWT table (the one-lane walks' tree, read from global memory): u32 words
 //   [0] nI internal nodes, [1] nE entries, [2] height (internal levels), [3] 0,
-//   nI x {first entry [0:16) | arity [16:24)}      (local index 0 = the BRWT root)
-//   nE u16 entries: bit 15 = leaf + global column in bits 0..14, else the local index
-constexpr uint32_t kRowsMaxArity = 16;
+//   nI x {first entry [0:24) | arity [24:32)}      (local index 0 = the BRWT root;
+//        r06: 24-bit first entries -- 2^16 columns need more than 2^16 entries)
+//   nE u32 entries: bit 31 = leaf + global column in bits 0..30, else the local index
+constexpr uint32_t kRowsMaxArity = 64;  // (r06: 16 before; masks of up to 8 bytes)
 constexpr uint32_t kRowsMaxHeight = 16;
+constexpr uint32_t kRowsOdoLevels = 8;  // internal levels the tree odometer walks (rows.hip rows_walk_tree)
 constexpr uint32_t kRowsMaxTableWords = 8192;
 enum : int { LAYOUT_AUTO = 0, LAYOUT_NODES = 1, LAYOUT_ROWS = 2, LAYOUT_BOTH = 3 };
 struct RowsImage {
@@ -262,6 +264,7 @@ struct RowsImage {
     uint32_t frames = 0;            // its stack levels
     bool mask1 = false;             // every internal node (leaf parents too) has arity <= 8: one-byte masks
     bool nib = false;               // masks as nibble codes (rows_record.hpp RecMasks; MBRWT_BUILD_ROWS_CODE)
+    uint32_t max_arity = 0;         // the widest internal node (masks of (arity + 7) / 8 bytes; r06: up to 64)
     uint32_t uni = 0;               // K internal levels above leaf parents on every path (rows_walk_uni), else 0
     uint64_t bytes = 0;             // blocks + spill used
     uint32_t occ_cap = 0;           // workgroups per CU of k_traverse_rows (0 = the default; MBRWT_BUILD_ROWS_WGS_PER_CU)
@@ -290,7 +293,7 @@ struct RowsImage {
 };
 // the RWT table of a finished node tree; false (and an empty table) when the
 // shape is outside the row-record kernels' limits
-bool build_rwt_table(const Tree &tree, std::vector<uint32_t> &table, uint32_t &height);
+bool build_rwt_table(const Tree &tree, std::vector<uint32_t> &table, uint32_t &height, uint32_t &max_arity);
 bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &table2, uint32_t &frames);
 uint32_t rwt2_uniform_levels(const std::vector<uint32_t> &table2);
 // the thread's build layout (mbrwt_set_build_option; AUTO when unset)
@@ -371,6 +374,12 @@ struct Ctx {
     int rows_walk = 0;                  // MBRWT_OPT_ROWS_WALK (6: the non-odometer walk on uniform trees)
     int64_t test_fail_chunk = -1;       // MBRWT_OPT_TEST_FAIL_CHUNK (test hook: host_get_rows fails at that chunk)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // MBRWT_OPT_COMPACT_CUS (r06, VERDICT r05 #1a): k_compact_tiles on a
+    // stream masked to compact_cus of every 32 CUs, ordered after the
+    // traversal and before the caller's stream by two events
+    uint32_t compact_cus = 0;
+    hipStream_t s_compact = nullptr;
+    hipEvent_t ev_trav = nullptr, ev_comp = nullptr;
     double timing_ms = 0;
     uint64_t timing_launches = 0;
     int grid_cache = 0;

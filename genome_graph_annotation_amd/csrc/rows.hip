@@ -32,6 +32,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -64,9 +65,10 @@ int rows_footprint() { return g_rows_footprint; }
 // ------------------------------------------------------------------------
 // RWT table
 // ------------------------------------------------------------------------
-bool build_rwt_table(const Tree &tree, std::vector<uint32_t> &table, uint32_t &height) {
+bool build_rwt_table(const Tree &tree, std::vector<uint32_t> &table, uint32_t &height, uint32_t &max_arity) {
     table.clear();
     height = 0;
+    max_arity = 0;
     const auto &N = tree.nodes;
     if (N.size() < 2) return false;
     // the logical root: the folded root's children hang off dnode 0
@@ -82,6 +84,7 @@ bool build_rwt_table(const Tree &tree, std::vector<uint32_t> &table, uint32_t &h
         const DevNode &v = N[inner[h]];
         height = std::max(height, level[h]);
         if (v.arity == 0 || v.arity > kRowsMaxArity) return false;
+        max_arity = std::max<uint32_t>(max_arity, v.arity);
         for (uint32_t c = 0; c < v.arity; ++c) {
             const uint32_t w = v.first_child + c;
             if (w >= N.size()) return false;
@@ -94,31 +97,33 @@ bool build_rwt_table(const Tree &tree, std::vector<uint32_t> &table, uint32_t &h
     }
     if (height > kRowsMaxHeight || inner.size() >= 0x8000) return false;
     std::vector<uint32_t> nodew(inner.size());
-    std::vector<uint16_t> ent;
+    std::vector<uint32_t> ent;  // (r06: u32 entries -- columns up to 2^16; u16 with 15-bit columns before)
     for (size_t i = 0; i < inner.size(); ++i) {
         const DevNode &v = N[inner[i]];
-        if (ent.size() + v.arity > 0xFFFF) return false;
-        nodew[i] = (uint32_t)ent.size() | ((uint32_t)v.arity << 16);
+        if (ent.size() + v.arity > 0xFFFFFF) return false;
+        nodew[i] = (uint32_t)ent.size() | ((uint32_t)v.arity << 24);
         for (uint32_t c = 0; c < v.arity; ++c) {
             const DevNode &w = N[v.first_child + c];
             if (w.kind == KIND_LEAF) {
                 const uint32_t col = column_of(w);
-                if (col >= 0x8000) return false;
-                ent.push_back((uint16_t)(0x8000u | col));
+                if (col >= 0x10000) return false;  // (the label stage and temp regions hold u16 labels)
+                ent.push_back(0x80000000u | col);
             } else {
-                ent.push_back((uint16_t)local[v.first_child + c]);
+                ent.push_back(local[v.first_child + c]);
             }
         }
     }
     const size_t nI = inner.size(), nE = ent.size();
-    const size_t words = 4 + nI + (nE + 1) / 2;
-    if (words > kRowsMaxTableWords) return false;
+    const size_t words = 4 + nI + nE;
+    // (the RWT table stays in global memory -- the one-lane walks read it
+    // there -- so only the LDS-staged RWT2 table has kRowsMaxTableWords)
+    if (words > (1u << 22)) return false;
     table.assign(words, 0);
     table[0] = (uint32_t)nI;
     table[1] = (uint32_t)nE;
     table[2] = height;
     std::memcpy(&table[4], nodew.data(), nI * 4);
-    std::memcpy(&table[4 + nI], ent.data(), nE * 2);
+    std::memcpy(&table[4 + nI], ent.data(), nE * 4);
     return true;
 }
 
@@ -191,7 +196,7 @@ bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &t2, uint32_t &fra
         const DevNode &d = N[w];
         if (d.kind == KIND_LEAF) {
             const uint32_t col = column_of(d);
-            if (col >= 0x8000) return false;
+            if (col >= 0x10000) return false;
             out = 0x80000000u | col;
             return true;
         }
@@ -200,7 +205,7 @@ bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &t2, uint32_t &fra
         bool cons;
         if (is_lp2(w, b, cons)) {
             if (cons) {
-                if (b + d.arity > 0x8000) return false;
+                if (b + d.arity > 0x10000) return false;
                 out = 0xC0000000u | ((uint32_t)d.arity << 16) | b;
                 return true;
             }
@@ -208,7 +213,7 @@ bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &t2, uint32_t &fra
             out = 0xE0000000u | ((uint32_t)d.arity << 16) | (uint32_t)lists.size();
             for (uint32_t c = 0; c < d.arity; ++c) {
                 const uint32_t col = column_of(N[d.first_child + c]);
-                if (col >= 0x8000) return false;
+                if (col >= 0x10000) return false;
                 lists.push_back((uint16_t)col);
             }
             return true;
@@ -241,7 +246,7 @@ uint32_t rwt2_uniform_levels(const std::vector<uint32_t> &t2) {
     for (uint32_t d = 1; d <= K; ++d) {
         std::vector<uint32_t> next;
         for (const uint32_t w : lev) {
-            const uint32_t a = (w >> 16) & 0x1Fu, f = w & 0xFFFFu;
+            const uint32_t a = (w >> 16) & 0x7Fu, f = w & 0xFFFFu;
             for (uint32_t c = 0; c < a; ++c) {
                 if (4 + (size_t)f + c >= t2.size()) return 0;
                 const uint32_t e = t2[4 + f + c];
@@ -270,7 +275,7 @@ void append_path_table(std::vector<uint32_t> &t2, uint32_t K) {
     for (uint32_t d = 0; d < K; ++d) {  // A[d] = the largest arity at level d
         std::vector<uint32_t> next;
         for (const uint32_t w : lev) {
-            const uint32_t a = (w >> 16) & 0x1Fu, f = w & 0xFFFFu;
+            const uint32_t a = (w >> 16) & 0x7Fu, f = w & 0xFFFFu;
             A[d] = std::max(A[d], a);
             if (d + 1 < K)
                 for (uint32_t c = 0; c < a; ++c) next.push_back(t2[4 + f + c]);
@@ -290,7 +295,7 @@ void append_path_table(std::vector<uint32_t> &t2, uint32_t K) {
     while (!st.empty()) {
         const F fr = st.back();
         st.pop_back();
-        const uint32_t a = (fr.w >> 16) & 0x1Fu, f = fr.w & 0xFFFFu;
+        const uint32_t a = (fr.w >> 16) & 0x7Fu, f = fr.w & 0xFFFFu;
         for (uint32_t c = 0; c < a; ++c) {
             const uint32_t e = t2[4 + f + c];
             const uint32_t idx = fr.idx * A[fr.d] + c;
@@ -332,8 +337,8 @@ __global__ __launch_bounds__(256) void k_rows_measure(const DevNode *nodes, uint
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gs) {
         uint32_t b = 1, nn = 0, b1 = 1;
-        const uint32_t L = emit_row_masks(nodes, folded != 0, (uint32_t)r, [&](uint32_t mk, uint32_t a, uint32_t) {
-            if (nib) nn += nib_codes(mk);
+        const uint32_t L = emit_row_masks(nodes, folded != 0, (uint32_t)r, [&](uint64_t mk, uint32_t a, uint32_t) {
+            if (nib) nn += nib_codes((uint32_t)mk);
             else b += rec_mask_bytes(a);
             b1 += rec_mask_bytes(a);
         });
@@ -430,18 +435,17 @@ __device__ __forceinline__ uint32_t write_row_masks(const DevNode *nodes, bool f
         else p[w >> 1] = (uint8_t)v;
         ++w;
     };
-    labels = emit_row_masks(nodes, folded, r, [&](uint32_t mk, uint32_t a, uint32_t) {
-        if (nib) {
-            if (nib_codes(mk) == 1u) {
-                put((uint32_t)__builtin_ctz(mk));
+    labels = emit_row_masks(nodes, folded, r, [&](uint64_t mk, uint32_t a, uint32_t) {
+        if (nib) {  // (arity <= 8)
+            if (nib_codes((uint32_t)mk) == 1u) {
+                put((uint32_t)__builtin_ctzll(mk));
             } else {
                 put(8u);
-                put(mk & 15u);
-                put((mk >> 4) & 15u);
+                put((uint32_t)mk & 15u);
+                put((uint32_t)(mk >> 4) & 15u);
             }
-        } else {
-            p[w++] = (uint8_t)mk;
-            if (a > 8) p[w++] = (uint8_t)(mk >> 8);
+        } else {  // one byte per 8 children, little-endian
+            for (uint32_t k = 0; k < a; k += 8) p[w++] = (uint8_t)(mk >> k);
         }
     });
     return nib ? (w + 1) / 2 : w;
@@ -588,18 +592,28 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         return MBRWT_ERR_INVALID;
     }
     if (im.table.empty()) {
-        if (!build_rwt_table(range.tree, im.table, im.height) || !build_rwt2_table(range.tree, im.table2, im.frames)) {
+        if (!build_rwt_table(range.tree, im.table, im.height, im.max_arity) || !build_rwt2_table(range.tree, im.table2, im.frames)) {
             im.table.clear();
-            set_error("tree shape outside the row-record limits (arity <= 16, columns < 2^15, height <= 16)");
+            set_error("tree shape outside the row-record limits (arity <= 64, columns < 2^16, height <= 16, a walk table of <= 8192 words)");
             return MBRWT_ERR_UNSUPPORTED;
         }
         // one-byte masks everywhere (rows_walk6): the root and every internal
         // or leaf-parent entry of arity <= 8
-        auto ar8 = [](uint32_t e) { return (e >> 30) == 2u || ((e >> 16) & 0x1Fu) <= 8; };
+        auto ar8 = [](uint32_t e) { return (e >> 30) == 2u || ((e >> 16) & 0x7Fu) <= 8; };
         im.mask1 = ar8(im.table2[0]);
         for (size_t i = 4; i < 4 + (size_t)im.table2[1]; ++i) im.mask1 = im.mask1 && ar8(im.table2[i]);
         im.uni = im.mask1 ? rwt2_uniform_levels(im.table2) : 0u;
         if (im.uni) append_path_table(im.table2, im.uni);
+        // masks wider than 16 bits (r06: arity up to 64) are read by the tree
+        // odometer and the one-lane walks only: such a tree needs the tree
+        // odometer's depth
+        // (im.max_arity: over the nodes the walk reaches -- record-only
+        // dnodes such as PACKT_IN carry other arities)
+        if (im.max_arity > 16 && im.frames > kRowsOdoLevels) {
+            im.table.clear();
+            set_error("row records: a node wider than 16 children in a tree deeper than the tree odometer (8 levels)");
+            return MBRWT_ERR_UNSUPPORTED;
+        }
         // nibble-coded masks (MBRWT_BUILD_ROWS_CODE = 1, r06): read by the
         // path-table odometer and the one-lane walks, so uniform trees of
         // one-byte masks with a path table only (the others keep bytes)
@@ -852,46 +866,56 @@ int rows_build_finish(RowsBuild *rbp) {
 // ------------------------------------------------------------------------
 namespace {
 
-// rwt_walk with its pending frames {first entry | mask << 16} in a per-lane
-// LDS stack (stk[64 k], k < lim <= kRowsMaxHeight: the tree's height) instead
+// rwt_walk with its pending frames {first entry, mask} in a per-lane LDS
+// stack (stk[128 k], stk[128 k + 64], k < lim <= kRowsMaxHeight: the tree's
+// height) instead
 // of registers: the compaction kernel walks direct tiles with it, so its
 // register budget (and occupancy) stays that of its copy loop
 template <class MaskFn, class LeafFn>
-__device__ bool rwt_walk_lds(const uint32_t *ntab, const uint16_t *etab, MaskFn mask, LeafFn leaf,
-                             AS_LDS uint32_t *stk, uint32_t lim) {
+__device__ bool rwt_walk_lds(const uint32_t *table, MaskFn mask, LeafFn leaf, AS_LDS uint32_t *stk, uint32_t lim) {
+    const uint32_t nI = table[0], nE = table[1];
+    const uint32_t *ntab = table + 4;
+    const uint32_t *etab = ntab + nI;
     uint32_t nw = ntab[0];
-    uint32_t a = (nw >> 16) & 0xFFu;
-    uint32_t m = mask(a);
-    uint32_t first = nw & 0xFFFFu;
+    uint32_t a = nw >> 24;
+    uint32_t m = (uint32_t)mask(a);  // (arity <= 16 here: wide trees take rwt_walk)
+    uint32_t first = nw & 0xFFFFFFu;
     uint32_t sp = 0;
+    bool ok = true;
     while (true) {
         if (!m) {
             if (!sp) break;
             --sp;
-            const uint32_t w = stk[64 * sp];
-            first = w & 0xFFFFu;
-            m = w >> 16;
+            first = stk[128 * sp];
+            m = stk[128 * sp + 64];
             continue;
         }
         const uint32_t c = (uint32_t)__builtin_ctz(m);
         m &= m - 1;
+        if (first + c >= nE) {
+            ok = false;
+            break;
+        }
         const uint32_t e = etab[first + c];
-        if (e & 0x8000u) {
-            leaf(e & 0x7FFFu);
+        if (e & 0x80000000u) {
+            leaf(e & 0x7FFFFFFFu);
             continue;
         }
-        nw = ntab[e];
-        a = (nw >> 16) & 0xFFu;
-        const uint32_t mw = mask(a);
-        if (m) {
-            if (sp == lim) return false;
-            stk[64 * sp] = first | (m << 16);
+        if (e >= nI || (m && sp == lim)) {
+            ok = false;
+            break;
+        }
+        if (m) {  // (the push before the child's mask read: rwt_walk)
+            stk[128 * sp] = first;
+            stk[128 * sp + 64] = m;
             ++sp;
         }
-        first = nw & 0xFFFFu;
-        m = mw;
+        nw = ntab[e];
+        a = nw >> 24;
+        m = (uint32_t)mask(a);
+        first = nw & 0xFFFFFFu;
     }
-    return true;
+    return ok;
 }
 
 // walk families of k_traverse_rows (RowsImage::walk)
@@ -946,7 +970,7 @@ __device__ __forceinline__ uint32_t term_label(uint32_t e, const AS_LDS uint16_t
 __device__ __forceinline__ void rows_walk4(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
                                            const AS_LDS uint32_t *ent, const AS_LDS uint16_t *lst,
                                            AS_LDS uint32_t *stk, uint16_t *out, uint32_t pos) {
-    const uint32_t ra = (root >> 16) & 0x1Fu;
+    const uint32_t ra = (root >> 16) & 0x7Fu;
     const uint32_t rm = ((uint32_t)pb[o] | ((uint32_t)pb[o + 1] << 8)) & ((1u << ra) - 1u);
     o += ra > 8 ? 2u : 1u;
     if ((root >> 30) == 3u) {  // a one-level tree: the root is a leaf parent
@@ -961,7 +985,7 @@ __device__ __forceinline__ void rows_walk4(const AS_LDS uint8_t *pb, uint32_t o,
         const uint32_t c = (uint32_t)__builtin_ctz(m | 0x10000u);
         m &= m - 1;
         const uint32_t e = ent[act ? f + c : 0u];
-        const uint32_t a = act ? (e >> 16) & 0x1Fu : 0u;  // leaf: 0
+        const uint32_t a = act ? (e >> 16) & 0x7Fu : 0u;  // leaf: 0
         const uint32_t mw = ((uint32_t)pb[o] | ((uint32_t)pb[o + 1] << 8)) & ((1u << a) - 1u);
         o += a ? (a > 8 ? 2u : 1u) : 0u;
         const bool inner = act && (e >> 31) == 0u;
@@ -1178,7 +1202,7 @@ __device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_
         }
         const uint32_t c = (uint32_t)__builtin_ctz(r[K - 1]);
         r[K - 1] &= r[K - 1] - 1u;
-        const uint32_t AK = K > 1 ? (A >> (4 * (K - 2))) & 0xFu : 0u;
+        const uint32_t AK = K > 1 ? (A >> (4 * (K > 1 ? K - 2 : 0))) & 0xFu : 0u;
         const uint32_t pidx = K > 1 ? mad_u24(idx[K - 1], AK, c) : c;
         // the leaf parent's first column: computed on a linear path table (no
         // LDS round trip per iteration), else read
@@ -1208,48 +1232,60 @@ __device__ __forceinline__ void rows_walk_path(const AS_LDS uint8_t *pb, uint32_
 // record's next byte(s) -- BRWT::get_row's pre-order (BRWT.cpp:43-51), the
 // record format unchanged.  Levels are unrolled and predicated: a level no
 // lane of the wave needs costs a skipped branch.  State: 2 KM registers.
-constexpr uint32_t kRowsOdoLevels = 8;
-template <int KM, bool M1>
+template <int KM, bool M1, bool WIDE = false>
 __device__ __forceinline__ void rows_walk_tree(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t root,
                                                const AS_LDS uint32_t *ent, const AS_LDS uint16_t *lst,
                                                AS_LDS uint16_t *out, uint32_t pos) {
+    // masks: one byte (M1), up to two (arity <= 16), or (WIDE, r06) up to
+    // eight -- arity <= 64, one byte per 8 children
+    using MT = typename std::conditional<WIDE, uint64_t, uint32_t>::type;
     const AS_LDS uint8_t *rc = pb + o;  // record cursor
-    // a node's mask of arity a (<= 16) at the cursor; its width in bytes
-    auto mask_at = [&](uint32_t a) -> uint32_t {
-        uint32_t m = rc[0];
-        if (!M1 && a > 8) m |= (uint32_t)rc[1] << 8;  // (rare: a branch, not a read in every lane)
-        return m & ((1u << a) - 1u);
+    // a node's mask of arity a at the cursor; its width in bytes
+    auto mask_at = [&](uint32_t a) -> MT {
+        MT m = rc[0];
+        if constexpr (WIDE) {
+            for (uint32_t k = 8; k < a; k += 8) m |= (MT)rc[k >> 3] << k;  // (rare: a loop, not reads in every lane)
+            return a >= 64 ? m : (m & (((MT)1 << a) - 1u));
+        } else {
+            if (!M1 && a > 8) m |= (uint32_t)rc[1] << 8;  // (rare: a branch, not a read in every lane)
+            return m & ((1u << a) - 1u);
+        }
     };
-    auto width = [](uint32_t a) -> uint32_t { return (M1 || a <= 8) ? 1u : 2u; };
+    auto width = [](uint32_t a) -> uint32_t { return WIDE ? (a + 7u) >> 3 : (M1 || a <= 8) ? 1u : 2u; };
     uint32_t ob = pos * 2u;  // byte offset of the next label
-    auto emit = [&](uint32_t e, uint32_t x) {
-        *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)term_label(e, lst, (uint32_t)__builtin_ctz(x));
+    auto ctz = [](MT x) -> uint32_t { return WIDE ? (uint32_t)__builtin_ctzll((uint64_t)x) : (uint32_t)__builtin_ctz((uint32_t)x); };
+    auto emit = [&](uint32_t e, MT x) {
+        *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)term_label(e, lst, ctz(x));
         ob += 2u;
         x &= x - 1u;
         while (x) {
-            *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)term_label(e, lst, (uint32_t)__builtin_ctz(x));
+            *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)term_label(e, lst, ctz(x));
             ob += 2u;
             x &= x - 1u;
         }
     };
-    const uint32_t ra = (root >> 16) & 0x1Fu;
+    const uint32_t ra = (root >> 16) & 0x7Fu;
     if ((root >> 30) == 3u) {  // a one-level tree: the root is a leaf parent
         if (live) {
-            const uint32_t x = mask_at(ra);
+            const MT x = mask_at(ra);
             if (x) emit(root, x);
         }
         return;
     }
-    uint32_t r[KM], f[KM];
-    r[0] = live ? mask_at(ra) : 0u;
+    MT r[KM];
+    uint32_t f[KM];
+    r[0] = live ? mask_at(ra) : (MT)0;
     f[0] = root & 0xFFFFu;
     rc += width(ra);
 #pragma unroll
-    for (int k = 1; k < KM; ++k) r[k] = f[k] = 0u;
+    for (int k = 1; k < KM; ++k) {
+        r[k] = 0;
+        f[k] = 0u;
+    }
     while (true) {
         uint32_t nz = 0;
 #pragma unroll
-        for (int k = 0; k < KM; ++k) nz |= (r[k] != 0u ? 1u : 0u) << k;
+        for (int k = 0; k < KM; ++k) nz |= (r[k] != 0 ? 1u : 0u) << k;
         if (!nz) break;
         const uint32_t ks = 31u - (uint32_t)__builtin_clz(nz);  // the deepest level with a child left
         bool go = true;
@@ -1257,12 +1293,12 @@ __device__ __forceinline__ void rows_walk_tree(const AS_LDS uint8_t *pb, uint32_
 #pragma unroll
         for (int k = 0; k < KM; ++k) {
             if (go && (uint32_t)k >= ks) {
-                const uint32_t c = (uint32_t)__builtin_ctz(r[k]);
+                const uint32_t c = ctz(r[k]);
                 r[k] &= r[k] - 1u;
                 const uint32_t e = ent[f[k] + c];
                 if ((int32_t)e >= 0) {  // an internal child: its mask, one level down
-                    const uint32_t a = (e >> 16) & 0x1Fu;
-                    const uint32_t m = mask_at(a);
+                    const uint32_t a = (e >> 16) & 0x7Fu;
+                    const MT m = mask_at(a);
                     rc += width(a);
                     if (k + 1 < KM) {
                         r[k + 1] = m;
@@ -1275,9 +1311,9 @@ __device__ __forceinline__ void rows_walk_tree(const AS_LDS uint8_t *pb, uint32_
             }
         }
         // the terminal: a leaf parent (its set children) or a leaf (its column)
-        uint32_t x = 1u;
+        MT x = 1u;
         if ((term >> 30) == 3u) {
-            const uint32_t a = (term >> 16) & 0x1Fu;
+            const uint32_t a = (term >> 16) & 0x7Fu;
             x = mask_at(a);
             rc += width(a);
         }
@@ -1308,8 +1344,12 @@ constexpr uint32_t kRowsTilesPerWave = 1;
 // workgroup); WALK: the walk family.  (r06: a one-pass form that wrote the
 // CSR itself, its place found by a decoupled look-back, measured 0.44-0.48
 // against 0.33 ms per C4 step and was retired: profiles/r06/v01_one_pass.)
-template <int B, int WPB, bool NT, uint32_t WALK, bool NIB = false>
+// VAR: the record variant -- 0 byte masks, VAR_NIB nibble codes (the path
+// odometer), VAR_WIDE masks of up to 64 bits (the tree odometer, r06)
+enum : uint32_t { VAR_BYTE = 0, VAR_NIB = 1, VAR_WIDE = 2 };
+template <int B, int WPB, bool NT, uint32_t WALK, uint32_t VAR = VAR_BYTE>
 __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
+    constexpr bool NIB = VAR == VAR_NIB;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_rows[];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1466,12 +1506,14 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
                 // SQ/TA counters showed the texture-address unit as the
                 // busiest unit)
                 if constexpr (WALK == WALK_TREE_ODOMETER) {
-#define MBRWT_TREE_CASE(K)                                                        \
-    case K:                                                                       \
-        if (p.mask1)                                                              \
-            rows_walk_tree<K, true>(rec, o, live, root, ent, lst, stage, pos);    \
-        else                                                                      \
-            rows_walk_tree<K, false>(rec, o, live, root, ent, lst, stage, pos);   \
+#define MBRWT_TREE_CASE(K)                                                              \
+    case K:                                                                             \
+        if constexpr (VAR == VAR_WIDE)                                                  \
+            rows_walk_tree<K, false, true>(rec, o, live, root, ent, lst, stage, pos);   \
+        else if (p.mask1)                                                               \
+            rows_walk_tree<K, true>(rec, o, live, root, ent, lst, stage, pos);          \
+        else                                                                            \
+            rows_walk_tree<K, false>(rec, o, live, root, ent, lst, stage, pos);         \
         break;
                     switch (p.frames) {
                         MBRWT_TREE_CASE(1)
@@ -1481,7 +1523,12 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
                         MBRWT_TREE_CASE(5)
                         MBRWT_TREE_CASE(6)
                         MBRWT_TREE_CASE(7)
-                        default: rows_walk_tree<8, false>(rec, o, live, root, ent, lst, stage, pos); break;
+                        default:
+                            if constexpr (VAR == VAR_WIDE)
+                                rows_walk_tree<8, false, true>(rec, o, live, root, ent, lst, stage, pos);
+                            else
+                                rows_walk_tree<8, false>(rec, o, live, root, ent, lst, stage, pos);
+                            break;
                     }
 #undef MBRWT_TREE_CASE
                 } else if (ptw) {
@@ -1565,8 +1612,9 @@ __device__ __forceinline__ void publish_status(unsigned long long *status, uint6
     atomicMax(&status[1], (unsigned long long)st);
     atomicOr(&status[2], 1ull << st);
 }
+template <bool WIDE>
 __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
-    extern __shared__ uint32_t cstk[];  // the direct walks' stacks: 4 x 64 x stk_lim words (one per lane)
+    extern __shared__ uint32_t cstk[];  // the direct walks' stacks: 4 x 128 x stk_lim words (two per lane and frame)
     const uint64_t n = p.n;
     const uint64_t ntiles = (n + 63) / 64;
     const uint32_t lane = threadIdx.x & 63;
@@ -1651,17 +1699,18 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
             uint64_t masks;
             uint32_t count;
             rows_locate(p.v, row, masks, count);  // (count = cnt: rows out of range have none)
-            const uint32_t *ntab = p.table + 4;
-            const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + p.table[0]);
             uint32_t *dst = p.cols + base[k];
             uint32_t j = 0;
-            const bool ok = rwt_walk_lds(
-                ntab, etab, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, p.v.nib),
-                [&](uint32_t col) {
-                    if (j < count) gst(dst + j, col);
-                    ++j;
-                },
-                (AS_LDS uint32_t *)cstk + (threadIdx.x >> 6) * 64 * p.stk_lim + lane, p.stk_lim);
+            auto put = [&](uint32_t col) {
+                if (j < count) gst(dst + j, col);
+                ++j;
+            };
+            const auto mk = rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, p.v.nib);
+            // (masks beyond 16 bits: the frames in registers, not packed in LDS)
+            const bool ok = WIDE ? rwt_walk(p.table, mk, put, [](uint32_t) {})
+                                 : rwt_walk_lds(p.table, mk, put,
+                                                (AS_LDS uint32_t *)cstk + (threadIdx.x >> 6) * 128 * p.stk_lim + lane,
+                                                p.stk_lim);
             if (!ok || j != count) publish_status(p.status, MBRWT_ERR_DEVICE);
         }
     }
@@ -1671,8 +1720,6 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
 __global__ __launch_bounds__(256) void k_rows_get(RowsView v, const uint32_t *table, const uint64_t *rows,
                                                   const uint64_t *qcols, uint64_t n, uint64_t num_cols, uint8_t *out,
                                                   unsigned long long *scalars) {
-    const uint32_t *ntab = table + 4;
-    const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + table[0]);
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
         const uint64_t row = gld(rows + i), col = gld(qcols + i);
@@ -1687,7 +1734,7 @@ __global__ __launch_bounds__(256) void k_rows_get(RowsView v, const uint32_t *ta
         uint32_t hit = 0;
         if (count)
             (void)rwt_walk(
-                ntab, etab, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
+                table, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
                 [&](uint32_t c) { hit |= c == col; }, [](uint32_t) {});
         gst(out + i, (uint8_t)hit);
     }
@@ -1700,8 +1747,6 @@ template <bool WORK>
 __global__ __launch_bounds__(256) void k_rows_count(RowsView v, const uint32_t *table, const uint64_t *rows,
                                                     uint64_t n, unsigned long long *counts,
                                                     unsigned long long *scalars) {
-    const uint32_t *ntab = table + 4;
-    const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + table[0]);
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     unsigned long long vis = 0, lab = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
@@ -1716,7 +1761,7 @@ __global__ __launch_bounds__(256) void k_rows_count(RowsView v, const uint32_t *
         vis += 1;
         if (!count) continue;
         (void)rwt_walk(
-            ntab, etab, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
+            table, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
             [&](uint32_t c) {
                 if constexpr (WORK) ++lab;
                 else atomicAdd(counts + c, 1ull);
@@ -1748,11 +1793,9 @@ struct RowHasColumn {
         uint32_t count;
         rows_locate(v, row, masks, count);
         if (!count) return false;
-        const uint32_t *ntab = table + 4;
-        const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + table[0]);
         bool hit = false;
         (void)rwt_walk(
-            ntab, etab, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
+            table, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
             [&](uint32_t c) { hit |= c == col; }, [](uint32_t) {});
         return hit;
     }
@@ -1781,8 +1824,11 @@ constexpr uint32_t kRowsWpb = 8;
 // 8-wave workgroups per CU (16 waves); two of 11 waves fit (22)
 constexpr uint32_t kRowsWpbWide = 11;
 template <int B, bool NT>
-RowsFn rows_fn_b(uint32_t walk, uint32_t wpb, bool nib) {
-    if (nib) return k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER, true>;  // (nibble codes: the path odometer)
+RowsFn rows_fn_b(uint32_t walk, uint32_t wpb, bool nib, bool wide) {
+    if (nib) return k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER, VAR_NIB>;  // (nibble codes: the path odometer)
+    if (wide)  // (masks beyond 16 bits: the tree odometer)
+        return wpb == kRowsWpbWide ? k_traverse_rows<B, kRowsWpbWide, NT, WALK_TREE_ODOMETER, VAR_WIDE>
+                                   : k_traverse_rows<B, kRowsWpb, NT, WALK_TREE_ODOMETER, VAR_WIDE>;
     if (wpb == kRowsWpbWide) return k_traverse_rows<B, kRowsWpbWide, NT, WALK_TREE_ODOMETER>;
     return walk == WALK_ODOMETER        ? k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER>
            : walk == WALK_TREE_ODOMETER ? k_traverse_rows<B, kRowsWpb, NT, WALK_TREE_ODOMETER>
@@ -1791,8 +1837,10 @@ RowsFn rows_fn_b(uint32_t walk, uint32_t wpb, bool nib) {
 }
 RowsFn rows_fn(const RowsImage &im, uint32_t walk, uint32_t wpb) {
     const bool nt = im.bytes > (1ull << 30);  // non-temporal block reads for images beyond the caches
-    if (im.B == 64) return nt ? rows_fn_b<64, true>(walk, wpb, im.nib) : rows_fn_b<64, false>(walk, wpb, im.nib);
-    return nt ? rows_fn_b<128, true>(walk, wpb, im.nib) : rows_fn_b<128, false>(walk, wpb, im.nib);
+    const bool wide = im.max_arity > 16;
+    if (im.B == 64)
+        return nt ? rows_fn_b<64, true>(walk, wpb, im.nib, wide) : rows_fn_b<64, false>(walk, wpb, im.nib, wide);
+    return nt ? rows_fn_b<128, true>(walk, wpb, im.nib, wide) : rows_fn_b<128, false>(walk, wpb, im.nib, wide);
 }
 // resident waves per CU with workgroups of w waves: the LDS (160 KiB per CU:
 // the table once per workgroup + per_wave bytes per wave) within the 24-wave cap
@@ -1827,7 +1875,8 @@ struct MaskTile {
 // (MBRWT_OPT_ROWS_WALK = 6 forces the non-odometer walk: tests)
 static uint32_t rows_walk_of(const Ctx &c) {
     const RowsImage &im = c.rows;
-    if (im.nib) return WALK_ODOMETER;  // (nibble codes: only the path odometer reads them)
+    if (im.nib) return WALK_ODOMETER;       // (nibble codes: only the path odometer reads them)
+    if (im.max_arity > 16) return WALK_TREE_ODOMETER;  // (masks beyond 16 bits: the tree odometer only)
     if (im.uni && c.rows_walk != 6 && c.rows_walk != 4 && c.rows_walk != 3)
         return WALK_ODOMETER;  // (7: without the path table)
     // (A/B: 6 = rows_walk6 where every mask is one byte, 4 = rows_walk4)
@@ -1987,9 +2036,23 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         cp.table = im.d_table;
         const uint64_t waves = (nt + kCompactTpw - 1) / kCompactTpw;
         cp.stk_lim = stk_lim;
-        hipLaunchKernelGGL(k_compact_tiles, dim3((unsigned)((waves + 3) / 4)), dim3(256),
-                           (size_t)256 * cp.stk_lim * 4, s, cp);
+        // (MBRWT_OPT_COMPACT_CUS: on the CU-masked stream, between two events)
+        hipStream_t sc = s;
+        if (c.compact_cus && c.s_compact) {
+            MBRWT_HIP(hipEventRecord(c.ev_trav, s));
+            MBRWT_HIP(hipStreamWaitEvent(c.s_compact, c.ev_trav, 0));
+            sc = c.s_compact;
+        }
+        if (im.max_arity > 16)
+            hipLaunchKernelGGL(k_compact_tiles<true>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, sc, cp);
+        else
+            hipLaunchKernelGGL(k_compact_tiles<false>, dim3((unsigned)((waves + 3) / 4)), dim3(256),
+                               (size_t)256 * cp.stk_lim * 8, sc, cp);
         MBRWT_HIP(hipGetLastError());
+        if (sc != s) {
+            MBRWT_HIP(hipEventRecord(c.ev_comp, sc));
+            MBRWT_HIP(hipStreamWaitEvent(s, c.ev_comp, 0));
+        }
         c.rows_sc_dirty = false;
     }
     if (d_status) return MBRWT_OK;  // no host synchronisation: the status lands on the stream

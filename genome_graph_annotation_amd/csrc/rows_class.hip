@@ -58,12 +58,10 @@ __device__ bool record_of(const RowsView &v, const uint32_t *table, uint64_t r, 
     rows_locate(v, r, rr.masks, rr.count);
     rr.len = 0;
     if (!rr.count) return true;
-    const uint32_t *ntab = table + 4;
-    const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + table[0]);
     uint32_t hi = 0;
     const uint64_t m = rr.masks;
     const bool ok = rwt_walk(
-        ntab, etab,
+        table,
         rec_masks(
             [&](uint32_t o) {
                 hi = o + 1 > hi ? o + 1 : hi;
@@ -202,8 +200,6 @@ __global__ __launch_bounds__(256) void k_class_map(const uint64_t *rows, uint64_
 // get_column: which classes hold the column (one byte per class)
 __global__ __launch_bounds__(256) void k_class_has(RowsView v, const uint32_t *table, uint64_t D, uint32_t col,
                                                    uint8_t *has) {
-    const uint32_t *ntab = table + 4;
-    const uint16_t *etab = reinterpret_cast<const uint16_t *>(ntab + table[0]);
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < D; k += gs) {
         uint64_t masks;
@@ -212,7 +208,7 @@ __global__ __launch_bounds__(256) void k_class_has(RowsView v, const uint32_t *t
         bool hit = false;
         if (count)
             (void)rwt_walk(
-                ntab, etab, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
+                table, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
                 [&](uint32_t c) { hit |= c == col; }, [](uint32_t) {});
         gst(has + k, (uint8_t)(hit ? 1 : 0));
     }

@@ -13,37 +13,39 @@ namespace {
 // ------------------------------------------------------------------------
 // build: the masks of a row's descent over a node image
 // ------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t rec_mask_bytes(uint32_t arity) { return arity <= 8 ? 1u : 2u; }
+// one byte per 8 children (r06: arity up to 64; one or two bytes up to 16)
+__device__ __forceinline__ uint32_t rec_mask_bytes(uint32_t arity) { return (arity + 7u) >> 3; }
 
 constexpr int kEmitFrames = 34;  // PLANE levels on a path (<= 32) + the super-root
 
-// the children bits of PLANE node image `nd` at position j
-__device__ __forceinline__ uint32_t plane_mask(const DevNode &nd, uint32_t j) {
+// the children bits of PLANE node image `nd` at position j (arity <= 64)
+__device__ __forceinline__ uint64_t plane_mask(const DevNode &nd, uint32_t j) {
     const uint64_t blk = nd.base + (uint64_t)(j >> 5) * nd.stride;
     const uint32_t t = j & 31;
-    uint32_t m = 0;
-    for (uint32_t c = 0; c < nd.arity; ++c) m |= ((gld_at<uint2>(blk + 8u * c).y >> t) & 1u) << c;
+    uint64_t m = 0;
+    for (uint32_t c = 0; c < nd.arity; ++c) m |= (uint64_t)((gld_at<uint2>(blk + 8u * c).y >> t) & 1u) << c;
     return m;
 }
-__device__ __forceinline__ uint32_t mask_at(const DevNode &nd, uint32_t j) {
+__device__ __forceinline__ uint64_t mask_at(const DevNode &nd, uint32_t j) {
     if (nd.kind == KIND_MASK8) return gld_at<uint8_t>(nd.base + j);
     if (nd.kind == KIND_MASK16) return gld_at<uint16_t>(nd.base + 2ull * j);
     if (nd.kind == KIND_MASK32) return gld_at<uint32_t>(nd.base + 4ull * j);
-    return (uint32_t)gld_at<uint64_t>(nd.base + 8ull * j);  // (arity <= 16 here)
+    return gld_at<uint64_t>(nd.base + 8ull * j);
 }
 
-// Row r of a node image: emit(mask, arity, dnode) for the children mask of
+// Row r of a node image: emit(mask (u64), arity, dnode) for the children mask of
 // every internal node its descent reaches, in DFS pre-order -- the row's record.
 // Returns the row's labels (set leaves), or ~0u when the descent is deeper
 // than the walker's frames.  Handles every node kind of the images
 // (PLANE, MASK*, PACK, PACK2, PACKT, a folded root).
 template <class Emit>
 __device__ uint32_t emit_row_masks(const DevNode *__restrict__ nodes, bool folded, uint32_t r, Emit emit) {
-    uint32_t fv[kEmitFrames], fj[kEmitFrames], fm[kEmitFrames];
+    uint32_t fv[kEmitFrames], fj[kEmitFrames];
+    uint64_t fm[kEmitFrames];
     int sp = 0;
     uint32_t leaves = 0;
     bool bad = false;
-    auto push = [&](uint32_t v, uint32_t j, uint32_t m) {
+    auto push = [&](uint32_t v, uint32_t j, uint64_t m) {
         if (sp == kEmitFrames) {
             bad = true;
             return;
@@ -58,13 +60,13 @@ __device__ uint32_t emit_row_masks(const DevNode *__restrict__ nodes, bool folde
         const DevNode nd = gld(nodes + v);
         const uint32_t a = nd.arity;
         if (nd.kind == KIND_PLANE) {
-            const uint32_t m = plane_mask(nd, j);
+            const uint64_t m = plane_mask(nd, j);
             emit(m, a, v);
             push(v, j, m);
         } else if (nd.kind >= KIND_MASK8 && nd.kind <= KIND_MASK64) {
-            const uint32_t m = mask_at(nd, j);
+            const uint64_t m = mask_at(nd, j);
             emit(m, a, v);
-            leaves += (uint32_t)__builtin_popcount(m);
+            leaves += (uint32_t)__builtin_popcountll(m);
         } else if (nd.kind == KIND_PACK) {  // children: MASK8 nodes inline
             PackBlock pb;
             pb.load(nd.base, j);
@@ -146,11 +148,11 @@ __device__ uint32_t emit_row_masks(const DevNode *__restrict__ nodes, bool folde
     };
     const DevNode d0 = gld(nodes);
     if (folded) {  // dnode 0 holds the root's children over rows
-        const uint32_t m = d0.kind == KIND_PLANE ? plane_mask(d0, r) : mask_at(d0, r);
+        const uint64_t m = d0.kind == KIND_PLANE ? plane_mask(d0, r) : mask_at(d0, r);
         if (!m) return 0;
         emit(m, d0.arity, 0u);
         if (d0.kind == KIND_PLANE) push(0, r, m);
-        else leaves += (uint32_t)__builtin_popcount(m);
+        else leaves += (uint32_t)__builtin_popcountll(m);
     } else {  // dnode 0: the root's own column
         uint32_t bit, jr = 0;
         if (d0.kind == KIND_PLANE) {
@@ -170,7 +172,7 @@ __device__ uint32_t emit_row_masks(const DevNode *__restrict__ nodes, bool folde
             --sp;
             continue;
         }
-        const uint32_t c = (uint32_t)__builtin_ctz(fm[t]);
+        const uint32_t c = (uint32_t)__builtin_ctzll(fm[t]);
         fm[t] &= fm[t] - 1;
         const DevNode nu = gld(nodes + fv[t]);
         const uint32_t w = nu.first_child + c;

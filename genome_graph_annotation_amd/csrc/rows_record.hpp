@@ -53,10 +53,10 @@ struct RecMasks {
     uint32_t nib;
     uint32_t c;
     __device__ __forceinline__ uint32_t nibble(uint32_t k) { return (byte(k >> 1) >> ((k & 1u) * 4u)) & 15u; }
-    __device__ __forceinline__ uint32_t operator()(uint32_t a) {
-        if (!nib) {
-            uint32_t m = byte(c++);
-            if (a > 8) m |= byte(c++) << 8;
+    __device__ __forceinline__ uint64_t operator()(uint32_t a) {
+        if (!nib) {  // one byte per 8 children, little-endian (arity <= 64)
+            uint64_t m = byte(c++);
+            for (uint32_t k = 8; k < a; k += 8) m |= (uint64_t)byte(c++) << k;
             return m;
         }
         const uint32_t v = nibble(c);
@@ -76,18 +76,29 @@ __device__ __forceinline__ RecMasks<ByteFn> rec_masks(ByteFn byte, uint32_t nib)
 // the nibbles one mask (arity <= 8, non-zero) takes as a nibble code
 __host__ __device__ __forceinline__ uint32_t nib_codes(uint32_t m) { return (m && !(m & (m - 1))) ? 1u : 3u; }
 
-// DFS walk of a record (its masks from `mask`, a RecMasks) over the RWT table:
-// leaf(column) per set leaf in pre-order (BRWT.cpp:45-51), inner(arity) per
-// mask read (the root's included).  One lane; false past kRowsMaxHeight.
+// DFS walk of a record (its masks from `mask`, a RecMasks) over the RWT table
+// `table` (mbrwt_internal.hpp): leaf(column) per set leaf in pre-order
+// (BRWT.cpp:45-51), inner(arity) per mask read (the root's included).  One
+// lane; false past kRowsMaxHeight pending frames, or when a mask names a
+// child the table does not have (a corrupt record: an error, not a read past
+// the table).  A descent pushes the parent's remaining children BEFORE it
+// reads the child's mask, so no mask value lives across the push (r06: the
+// other order, with an early return between, was miscompiled in the LDS
+// variant below -- the child's mask replaced by the parent's).
 template <class MaskFn, class LeafFn, class InnerFn>
-__device__ bool rwt_walk(const uint32_t *ntab, const uint16_t *etab, MaskFn mask, LeafFn leaf, InnerFn inner) {
+__device__ bool rwt_walk(const uint32_t *table, MaskFn mask, LeafFn leaf, InnerFn inner) {
+    const uint32_t nI = table[0], nE = table[1];
+    const uint32_t *ntab = table + 4;
+    const uint32_t *etab = ntab + nI;
     uint32_t nw = ntab[0];
-    uint32_t a = (nw >> 16) & 0xFFu;
-    uint32_t m = mask(a);
+    uint32_t a = nw >> 24;
+    uint64_t m = mask(a);
     inner(a);
-    uint32_t first = nw & 0xFFFFu;
-    uint32_t sf[kRowsMaxHeight], sm[kRowsMaxHeight];
+    uint32_t first = nw & 0xFFFFFFu;
+    uint32_t sf[kRowsMaxHeight];
+    uint64_t sm[kRowsMaxHeight];
     int sp = 0;
+    bool ok = true;
     while (true) {
         if (!m) {
             if (!sp) break;
@@ -96,27 +107,33 @@ __device__ bool rwt_walk(const uint32_t *ntab, const uint16_t *etab, MaskFn mask
             m = sm[sp];
             continue;
         }
-        const uint32_t c = (uint32_t)__builtin_ctz(m);
+        const uint32_t c = (uint32_t)__builtin_ctzll(m);
         m &= m - 1;
+        if (first + c >= nE) {
+            ok = false;
+            break;
+        }
         const uint32_t e = etab[first + c];
-        if (e & 0x8000u) {
-            leaf(e & 0x7FFFu);
+        if (e & 0x80000000u) {
+            leaf(e & 0x7FFFFFFFu);
             continue;
         }
-        nw = ntab[e];
-        a = (nw >> 16) & 0xFFu;
-        const uint32_t mw = mask(a);
-        inner(a);
+        if (e >= nI || (m && sp == (int)kRowsMaxHeight)) {
+            ok = false;
+            break;
+        }
         if (m) {
-            if (sp == (int)kRowsMaxHeight) return false;
             sf[sp] = first;
             sm[sp] = m;
             ++sp;
         }
-        first = nw & 0xFFFFu;
-        m = mw;
+        nw = ntab[e];
+        a = nw >> 24;
+        m = mask(a);
+        inner(a);
+        first = nw & 0xFFFFFFu;
     }
-    return true;
+    return ok;
 }
 
 // record classes (rows_class.hip): row r's class, bits [r w, r w + w) of the

@@ -170,7 +170,9 @@ int mbrwt_ctx_clone(mbrwt_ctx *src, mbrwt_ctx **out);
  *          descent -- the children mask of every internal node it reaches, in
  *          DFS pre-order -- stored with the row), so get_row is one block read
  *          and a record walk; the rank1 remaps are resolved at build time.
- *          Trees with arity <= 16, < 2^15 columns, height <= 16.  Built one
+ *          Trees with arity <= 64 (r06; 16 before: nodes wider than 16
+ *          need a tree of at most 8 internal levels), < 2^16 columns (2^15
+ *          before), height <= 16.  Built one
  *          range of rows at a time, so rows >= 2^32 need no row shards.
  *          get_column scans the records; mbrwt_tree_export rebuilds every
  *          index column from the records (so BinaryMatrix::serialize works).
@@ -542,6 +544,10 @@ int mbrwt_unpack_offsets_device(const void *d_base, uint32_t nseg, uint64_t seg_
                                    trees, the tree odometer on every other shape of <= 8 internal levels),
                                    3 the tree odometer, 4 the stack walk, 6 the stack walk of one-byte masks,
                                    7 the odometer without the path table (A/B and tests) */
+#define MBRWT_OPT_COMPACT_CUS 64 /* row records (r06, measurement): 0 default; k in 1..31 runs the
+                                    compaction of get_rows_device on a stream masked to k of every 32 CUs
+                                    (hipExtStreamCreateWithCUMask), after the traversal and before the
+                                    caller's stream by two events */
 #define MBRWT_OPT_TEST_FAIL_CHUNK 32 /* test hook: mbrwt_get_rows (host buffers) fails with MBRWT_ERR_NOMEM
                                         when it reaches chunk `value` of the batch (-1: never) -- the error
                                         path's drain of the chunks already in flight is tested with it */

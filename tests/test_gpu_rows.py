@@ -72,9 +72,9 @@ def test_reference_grids_rows(oracle_mod, kind, build):
             dense = _dense_grid(kind, n, m)
             t = O.OracleTree.from_dense(dense, part, arity, relax)
             ex = t.export()
-            if m == 1 or int(ex["num_children"].max()) > 16:
-                # a leaf root, or a node wider than 16 (relax without an
-                # arity bound): outside the row-record layout
+            if m == 1:
+                # a leaf root: outside the row-record layout (r06: nodes up to
+                # 64 children wide -- relax without an arity bound -- are in)
                 with pytest.raises(MBRWTError) as ei:
                     BRWTDevice.from_tree(ex, layout="rows")
                 assert ei.value.status == L.MBRWT_ERR_UNSUPPORTED
@@ -183,7 +183,7 @@ def test_tree_odometer(oracle_mod, n, m, d, part, arity, relax):
 def test_auto_layout(oracle_mod, build_env):
     """The library default (MBRWT_LAYOUT_AUTO): row records for every tree
     within their limits whose records fit one block request per row; the
-    per-node images for a one-column tree, nodes wider than 16 children,
+    per-node images for a one-column tree, nodes wider than 64 children,
     records too long for the block layout (dense rows), or MBRWT_LAYOUT=nodes."""
     O = oracle_mod
     from genome_graph_annotation_amd import BRWTDevice
@@ -214,16 +214,130 @@ def test_auto_layout(oracle_mod, build_env):
     assert BRWTDevice.from_tree(O.OracleTree.from_dense(sparse, "basic", 8).export()).layout() == "nodes"
 
 
-def test_arity_limit(oracle_mod):
-    """Nodes wider than 16 children stay on the node layout."""
+@pytest.mark.parametrize("n,m,d,part,arity,relax,max_arity", [
+    (500, 64, 0.1, "basic", 33, 0, 33),                # one node of 33 children above one of 31
+    (500, 64, 0.1, "basic", 64, 0, 64),                # one level: the root holds 64 leaves
+    (5000, 200, 0.05, "greedy", 2, 2**64 - 1, 25),     # relax without an arity bound
+    (5000, 300, 0.1, "greedy", 2, 2**64 - 1, 37),      # (test_BRWT_optimizer.cpp:102-163)
+    (4000, 400, 0.05, "greedy", 2, 2**64 - 1, 50),
+])
+def test_wide_nodes_rows(oracle_mod, n, m, d, part, arity, relax, max_arity):
+    """Row records over nodes up to 64 children wide (r06; 16 before): masks
+    of up to eight bytes, walked by the tree odometer and the one-lane walks;
+    the library default (AUTO) takes them; every query and the export back
+    into index columns against the oracle."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    rng = np.random.default_rng(n + m)
+    dense = rng.random((n, m)) < d
+    t = O.OracleTree.from_dense(dense, part, arity, relax)
+    ex = t.export()
+    assert int(np.asarray(ex["num_children"]).max()) == max_arity
+    dev = BRWTDevice.from_tree(ex)
+    assert dev.layout() == "rows" and dev.traverse_kernel() == "k_traverse_rows"
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 20000)]).astype(np.uint64)
+    _check_all(t, dev, rows, dense)
+    np.testing.assert_array_equal(_count_labels(dev, rows), dense[rows.astype(np.int64)].sum(axis=0))
+    back = dev.export()
+    for k in ("num_children", "first_child", "leaf_column"):
+        np.testing.assert_array_equal(np.asarray(back[k]), np.asarray(ex[k]))
+
+
+@pytest.mark.parametrize("n,m,d,part,arity,relax", [
+    (20000, 2652, 0.003, "basic", 8, 0),     # the Kingsford shape
+    (4000, 300, 0.4, "greedy", 2, 10),       # dense rows: direct tiles and long records in the compaction
+])
+def test_compact_cus_option(oracle_mod, n, m, d, part, arity, relax):
+    """MBRWT_OPT_COMPACT_CUS (r06): the compaction on a CU-masked stream
+    between two events returns the same CSR, on a context and its clone,
+    through the host and the device entry points; out-of-range values are
+    rejected."""
+    import torch
     O = oracle_mod
     from genome_graph_annotation_amd import BRWTDevice, MBRWTError, _lib as L
-    dense = np.random.default_rng(1).random((500, 64)) < 0.1
-    t = O.OracleTree.from_dense(dense, "basic", 33)
+    rng = np.random.default_rng(n + m)
+    dense = rng.random((n, m)) < d
+    t = O.OracleTree.from_dense(dense, part, arity, relax)
+    dev = BRWTDevice.from_tree(t.export())
+    assert dev.layout() == "rows"
+    twin = dev.clone()
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 20000)]).astype(np.uint64)
+    off_o, cols_o = t.get_rows(rows)
+    for cus in (4, 16, 31, 0):
+        for q in (dev, twin):
+            q.set_option(L.MBRWT_OPT_COMPACT_CUS, cus)
+            off_d, cols_d = q.get_rows(rows)
+            np.testing.assert_array_equal(off_d, off_o)
+            np.testing.assert_array_equal(cols_d, cols_o)
+    dev.set_option(L.MBRWT_OPT_COMPACT_CUS, 8)
+    s = torch.cuda.Stream()
+    rt = torch.from_numpy(rows.view(np.int64)).cuda()
+    ot = torch.zeros(len(rows) + 1, dtype=torch.int64, device="cuda")
+    ct = torch.zeros(max(1, len(cols_o)), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    assert dev.get_rows_device(rt, ot, ct, s.cuda_stream) == len(cols_o)
+    s.synchronize()
+    np.testing.assert_array_equal(ot.cpu().numpy().view(np.uint64), off_o)
+    np.testing.assert_array_equal(ct.cpu().numpy().view(np.uint32)[:len(cols_o)], cols_o)
+    for bad in (-1, 32):
+        with pytest.raises(MBRWTError):
+            dev.set_option(L.MBRWT_OPT_COMPACT_CUS, bad)
+
+
+@pytest.mark.parametrize("m,arity", [(40000, 8), (33000, 6), (65536, 16)])
+def test_many_columns_rows(oracle_mod, m, arity):
+    """Row records over 2^15 .. 2^16 columns (r06; < 2^15 before): the RWT
+    table's leaves carry 16-bit columns, the labels stay u16 in the stage."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    n = 1500
+    rng = np.random.default_rng(m)
+    # (about 3.5 labels a row: records of one block request per row, which
+    # AUTO takes -- 12 a row at 40,000 columns made it choose the node images)
+    dense = rng.random((n, m)) < 3.0 / m
+    dense[:, m - 1] |= rng.random(n) < 0.5  # (the last column in use)
+    t = O.OracleTree.from_dense(dense, "basic", arity)
+    dev = BRWTDevice.from_tree(t.export())
+    assert dev.layout() == "rows" and dev.traverse_kernel() == "k_traverse_rows"
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 5000)]).astype(np.uint64)
+    _check_all(t, dev, rows, dense)
+    np.testing.assert_array_equal(_count_labels(dev, rows), dense[rows.astype(np.int64)].sum(axis=0))
+
+
+@pytest.mark.parametrize("m,arity", [(70000, 8), (33000, 2)])
+def test_columns_limit(oracle_mod, m, arity):
+    """Beyond 2^16 columns the u16 label stage no longer holds a label, and a
+    walk table (RWT2, one entry per child of every internal node above the
+    leaf parents) beyond the 8,192 words staged in LDS -- 33,000 columns
+    under a binary tree -- has no record walk: the node layout answers."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice, MBRWTError, _lib as L
+    n = 600
+    rng = np.random.default_rng(3)
+    dense = rng.random((n, m)) < 5.0 / m
+    dense[:, m - 1] = True
+    t = O.OracleTree.from_dense(dense, "basic", arity)
     with pytest.raises(MBRWTError) as ei:
         BRWTDevice.from_tree(t.export(), layout="rows")
     assert ei.value.status == L.MBRWT_ERR_UNSUPPORTED
-    assert BRWTDevice.from_tree(t.export()).layout() == "nodes"
+    d = BRWTDevice.from_tree(t.export())
+    assert d.layout() == "nodes"
+    _check_all(t, d, np.arange(n, dtype=np.uint64), dense, columns=False)
+
+
+def test_arity_limit(oracle_mod):
+    """Nodes wider than 64 children (relax without an arity bound on a dense
+    matrix: 193 children under one node) are outside every layout of this
+    build (masks are held in 64 bits): a clean MBRWT_ERR_UNSUPPORTED."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice, MBRWTError, _lib as L
+    dense = np.random.default_rng(2).random((3000, 200)) < 0.2
+    t = O.OracleTree.from_dense(dense, "greedy", 2, 2**64 - 1)
+    assert int(np.asarray(t.export()["num_children"]).max()) > 64
+    for layout in ("rows", None):
+        with pytest.raises(MBRWTError) as ei:
+            BRWTDevice.from_tree(t.export(), layout=layout) if layout else BRWTDevice.from_tree(t.export())
+        assert ei.value.status == L.MBRWT_ERR_UNSUPPORTED
 
 
 @pytest.mark.parametrize("bs", ["64,1", "64,2", "64,3", "64,5", "64,8", "128,1", "128,3", "128,7", "128,15"])

@@ -13,14 +13,6 @@ B="python -u bench.py --no-e2e --no-probe --traffic off"
 for STAGE in "$@"; do
 O=gpurun_out/r6_$STAGE; mkdir -p $O
 case "$STAGE" in
-onepass)  # the one-pass traversal: row-record tests, then a same-box A/B against the two-kernel path
-  timeout -k 10 700 $PYT tests/test_gpu_rows.py -k "one_pass or odometer or tree_odometer or errors or async or clone or synthetic_c2 or greedy_relax" > $O/pytest_rows.log 2>&1 &&
-  timeout -k 10 300 $B --rows-fused 1 > $O/bench_fused_parity.log 2>&1 &&
-  timeout -k 10 120 $B --no-cpu --rows-fused 0 > $O/bench_twokernel_1.log 2>&1 &&
-  timeout -k 10 120 $B --no-cpu --rows-fused 1 > $O/bench_fused_1.log 2>&1 &&
-  timeout -k 10 120 $B --no-cpu --rows-fused 0 > $O/bench_twokernel_2.log 2>&1 &&
-  timeout -k 10 120 $B --no-cpu --rows-fused 1 > $O/bench_fused_2.log 2>&1
-  ;;
 rows)  # the row-record GPU tests + host pipeline + classes
   timeout -k 10 700 $PYT tests/test_gpu_rows.py tests/test_gpu_hostpipe.py tests/test_gpu_classes.py > $O/pytest_rows.log 2>&1
   ;;
@@ -43,6 +35,18 @@ nib2)  # nibble decode with one 4-byte LDS read: the nibble tests, C4 nibble (pa
   timeout -k 10 400 python -u bench.py --no-e2e --traffic off --rows-code 1 > $O/bench_c4_nib.log 2>&1 &&
   timeout -k 10 200 $B --no-cpu --rows-code 0 > $O/bench_c4_byte.log 2>&1 &&
   timeout -k 10 200 $B --no-cpu --rows-code 1 > $O/bench_c4_nib2.log 2>&1
+  ;;
+wide)  # row records for nodes up to 64 wide and up to 2^16 columns; the row-record suite
+  timeout -k 10 900 $PYT tests/test_gpu_rows.py tests/test_gpu_classes.py tests/test_gpu_files.py tests/test_gpu_parity.py > $O/pytest_rows.log 2>&1
+  ;;
+cumask)  # VERDICT r05 #1a: the compaction on a CU-masked stream -- its test, then ABAB C4 steps
+  timeout -k 10 300 $PYT tests/test_gpu_rows.py -k "compact_cus or async or errors" > $O/pytest_rows.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --compact-cus 0 > $O/bench_c4_cus0_1.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --compact-cus 8 > $O/bench_c4_cus8_1.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --compact-cus 0 > $O/bench_c4_cus0_2.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --compact-cus 8 > $O/bench_c4_cus8_2.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --compact-cus 4 > $O/bench_c4_cus4.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --compact-cus 16 > $O/bench_c4_cus16.log 2>&1
   ;;
 *) echo "unknown stage $STAGE"; exit 2 ;;
 esac || exit $?
