@@ -104,7 +104,7 @@ def parse():
     ap.add_argument("--compact-cus", type=int, default=0,
                     help="row records: run each query stream's compaction on a stream masked to K of every 32 "
                          "CUs (MBRWT_OPT_COMPACT_CUS, VERDICT r05 #1a; 0 = the library default, same stream)")
-    ap.add_argument("--query-streams", type=int, default=2, choices=[1, 2],
+    ap.add_argument("--query-streams", type=int, default=2, choices=[1, 2, 3, 4],
                     help="N = 1: consecutive batches alternate between the context and a clone of it "
                          "(mbrwt_ctx_clone: the same image, separate workspaces) on the default stream and "
                          "a second stream, so batch k+1's traversal overlaps batch k's output pass "
@@ -475,7 +475,7 @@ def main():
     # pack; the all-gather and the unpack run on RCCL's and a side stream)
     Q = a.query_streams if use_async else 1
     qmats, qstreams, qstatus = [mat], [stream], [status_t]
-    if Q == 2:
+    for _ in range(Q - 1):
         qmats.append(mat.clone())
         qstreams.append(torch.cuda.Stream(dev_t))
         qstatus.append(torch.zeros(3, dtype=torch.int64, device=dev_t))
@@ -485,8 +485,9 @@ def main():
     # outputs: step i writes bufs[i mod len]; with two buffers a buffer's next
     # writer is two steps later on the SAME stream, behind this step's readers
     # (its compaction, its pack) -- double-buffered whenever steps overlap
+    # (Q streams: buffer i mod Q is written only by stream i mod Q)
     bufs = [(off_t, cols_t)]
-    if gather or Q == 2:
+    for _ in range(max(Q, 2 if gather else 1) - 1):
         bufs.append((torch.empty_like(off_t), torch.empty_like(cols_t)))
 
     def step():
@@ -636,7 +637,7 @@ def main():
     # alone (one context, one stream, untimed for `value`) is reported
     # beside the roofline as `isolated`
     iso = None
-    if Q == 2:
+    if Q >= 2:
         for _ in range(3):
             mat.get_rows_device_async(rows_ts[0], off_t, cols_t, status_t, sptr)
         torch.cuda.synchronize()
@@ -708,7 +709,7 @@ def main():
     # the other stream's compaction running beside it, so the kernel timed
     # alone on one stream (the isolated pass) is the roofline's time and the
     # overlapped event time is reported beside it
-    kern_ms_overlapped = kern_ms if Q == 2 else None
+    kern_ms_overlapped = kern_ms if Q >= 2 else None
     if iso is not None:
         kern_ms = iso["kernel_ms"]
     kname = mat.traverse_kernel()

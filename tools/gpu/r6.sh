@@ -48,6 +48,13 @@ cumask)  # VERDICT r05 #1a: the compaction on a CU-masked stream -- its test, th
   timeout -k 10 200 $B --no-cpu --compact-cus 4 > $O/bench_c4_cus4.log 2>&1 &&
   timeout -k 10 200 $B --no-cpu --compact-cus 16 > $O/bench_c4_cus16.log 2>&1
   ;;
+qstreams)  # C4 with 2 / 3 / 4 query streams (contexts sharing the image), ABAB
+  timeout -k 10 200 $B --no-cpu --query-streams 2 > $O/bench_c4_q2_1.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --query-streams 3 > $O/bench_c4_q3_1.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --query-streams 2 > $O/bench_c4_q2_2.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --query-streams 3 > $O/bench_c4_q3_2.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --query-streams 4 > $O/bench_c4_q4.log 2>&1
+  ;;
 *) echo "unknown stage $STAGE"; exit 2 ;;
 esac || exit $?
 done
