@@ -55,6 +55,17 @@ qstreams)  # C4 with 2 / 3 / 4 query streams (contexts sharing the image), ABAB
   timeout -k 10 200 $B --no-cpu --query-streams 3 > $O/bench_c4_q3_2.log 2>&1 &&
   timeout -k 10 200 $B --no-cpu --query-streams 4 > $O/bench_c4_q4.log 2>&1
   ;;
+final_tests)  # the round's records, 1/3: every -m gpu test but the full-size ones, smoke
+  timeout -k 10 1000 $PYT -q tests -m "gpu and not slow" -x > $O/pytest_gpu_not_slow.log 2>&1 &&
+  timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+  ;;
+final_slow)  # 2/3: the full-size parity cases (C3, C4, C5, rows >= 2^32)
+  timeout -k 10 1100 $PYT tests -m "gpu and slow" -x > $O/pytest_gpu_slow.log 2>&1
+  ;;
+final_bench)  # 3/3: bench.py (whole-batch parity, CPU baseline, live PMC), its kernel trace + stats
+  timeout -k 10 400 python -u bench.py --traffic-out $O/traffic_c4.json > $O/bench_c4.log 2>&1 &&
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_c4 -o run --output-format csv -- python -u bench.py --no-cpu --no-e2e --no-probe --traffic off > $O/bench_c4_under_rocprof.log 2>&1
+  ;;
 *) echo "unknown stage $STAGE"; exit 2 ;;
 esac || exit $?
 done
