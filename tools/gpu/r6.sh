@@ -66,6 +66,12 @@ final_bench)  # 3/3: bench.py (whole-batch parity, CPU baseline, live PMC), its 
   timeout -k 10 400 python -u bench.py --traffic-out $O/traffic_c4.json > $O/bench_c4.log 2>&1 &&
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_c4 -o run --output-format csv -- python -u bench.py --no-cpu --no-e2e --no-probe --traffic off > $O/bench_c4_under_rocprof.log 2>&1
   ;;
+greedy_sq)  # SQ / TA counters of the greedy + relax traversal at 3.7 B rows (three passes, r05's C4 sets)
+  G="python -u tools/bench_greedy.py --shape-npz tools/data/greedy_relax10_c2_shape.npz --scaled-rows 3700000000 --layout rows --variants 0 --reps 3 --skip-small"
+  timeout -s KILL 400 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS -d $O/sq1 -o run --output-format csv -- $G > $O/sq1.log 2>&1 &&
+  timeout -s KILL 400 rocprofv3 --pmc SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS -d $O/sq2 -o run --output-format csv -- $G > $O/sq2.log 2>&1 &&
+  timeout -s KILL 400 rocprofv3 --pmc GRBM_COUNT GRBM_GUI_ACTIVE SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM_WR TA_BUFFER_WAVEFRONTS_sum TA_TA_BUSY_sum -d $O/sq3 -o run --output-format csv -- $G > $O/sq3.log 2>&1
+  ;;
 *) echo "unknown stage $STAGE"; exit 2 ;;
 esac || exit $?
 done
