@@ -72,6 +72,9 @@ greedy_sq)  # SQ / TA counters of the greedy + relax traversal at 3.7 B rows (th
   timeout -s KILL 400 rocprofv3 --pmc SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS -d $O/sq2 -o run --output-format csv -- $G > $O/sq2.log 2>&1 &&
   timeout -s KILL 400 rocprofv3 --pmc GRBM_COUNT GRBM_GUI_ACTIVE SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM_WR TA_BUFFER_WAVEFRONTS_sum TA_TA_BUSY_sum -d $O/sq3 -o run --output-format csv -- $G > $O/sq3.log 2>&1
   ;;
+rehearsal)  # bench.py's N > 1 step on the final sources: two ranks on one GPU over gloo, 1 B rows (two images fit)
+  timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --dist-backend gloo --rows 1000000000 --steps 10 --warmup 3 --no-e2e > $O/rehearsal_2rank.log 2>&1
+  ;;
 *) echo "unknown stage $STAGE"; exit 2 ;;
 esac || exit $?
 done
