@@ -98,9 +98,9 @@ def parse():
     ap.add_argument("--check-rows", type=int, default=0,
                     help="rows checked element-wise against the oracle (0 = the whole global batch)")
     ap.add_argument("--kernel", type=int, default=0, help="MBRWT_OPT_KERNEL variant (0 = library default)")
-    ap.add_argument("--rows-code", type=int, default=0, choices=[0, 1],
-                    help="row-record masks: 0 bytes (library default), 1 nibble codes (MBRWT_BUILD_ROWS_CODE: the "
-                         "compact image, DESIGN §4g)")
+    ap.add_argument("--rows-code", type=int, default=0, choices=[0, 1, 2, 3],
+                    help="row records (MBRWT_BUILD_ROWS_CODE): 0 the library default (AUTO: terminal records where "
+                         "smaller, DESIGN §4h), 1 nibble codes (§4g), 2 terminal records, 3 byte masks")
     ap.add_argument("--compact-cus", type=int, default=0,
                     help="row records: run each query stream's compaction on a stream masked to K of every 32 "
                          "CUs (MBRWT_OPT_COMPACT_CUS, VERDICT r05 #1a; 0 = the library default, same stream)")
@@ -697,12 +697,15 @@ def main():
         stream_gbs, rnd = probe_ceilings(dev_t, sptr, free, struct_bytes)
 
     # exact work accounting for the algorithmic roofline (untimed diagnostic pass)
-    visits, labels = mat.count_work_device(rows_t, sptr)
+    try:
+        visits, labels = mat.count_work_device(rows_t, sptr)
+    except L.MBRWTError:  # terminal records (--rows-code 2) store no internal masks: no V accounting
+        visits, labels = None, n_lab
     assert labels == n_lab, (labels, n_lab)
     # SURVEY §8(d)'s per-row figure: 64 B per index-bit probe of the
     # reference recursion (BRWT.cpp:30) + row id + offset + 4 B per label --
     # "probe-equivalent": the layouts answer a row without those probes
-    probe_bytes = 64 * visits + 16 * nb + 4 * labels
+    probe_bytes = 64 * visits + 16 * nb + 4 * labels if visits is not None else None
     kern_ms = kern_ms_total / max(1, launches)
     # the roofline's kernel time must fit inside the step:
     # with two query streams the HIP events around one traversal also span
@@ -823,11 +826,13 @@ def main():
             "achieved": alg_bytes / ks / 1e9 if alg_bytes else None,
             "frac": alg_bytes / ks / 1e9 / HBM_PEAK_GBS if alg_bytes else None,
             "alg_bytes_per_launch": alg_bytes, "alg_basis": alg_basis, "traffic": None,
-            "probe_equivalent": {"bytes_per_launch": probe_bytes, "achieved": probe_bytes / ks / 1e9,
-                                 "frac": probe_bytes / ks / 1e9 / HBM_PEAK_GBS,
-                                 "note": "SURVEY §8(d): 64 B x V + 16 + 4 L per row, V = index-bit probes of the "
-                                         "reference recursion; the row-record layouts issue none of these probes"},
-            "visits_per_row": visits / max(1, nb), "labels_per_row": labels / max(1, nb),
+            "probe_equivalent": ({"bytes_per_launch": probe_bytes, "achieved": probe_bytes / ks / 1e9,
+                                  "frac": probe_bytes / ks / 1e9 / HBM_PEAK_GBS,
+                                  "note": "SURVEY §8(d): 64 B x V + 16 + 4 L per row, V = index-bit probes of the "
+                                          "reference recursion; the row-record layouts issue none of these probes"}
+                                 if probe_bytes is not None else None),
+            "visits_per_row": visits / max(1, nb) if visits is not None else None,
+            "labels_per_row": labels / max(1, nb),
             "stream_read_measured": stream_gbs}
     if iso is not None:
         iks = iso["kernel_ms"] / 1e3
@@ -908,7 +913,9 @@ def main():
             "global_batch": G, "batch_per_gpu": nb, "batches": K, "layout": a.layout,
             "api": "mbrwt_get_rows_device_async" if use_async else "mbrwt_get_rows_device",
             "query_streams": Q,
-            "rows_code": "nibble" if a.rows_code else "byte",
+            "rows_code": {0: "auto", 1: "nibble", 2: "terminal", 3: "byte"}[a.rows_code],
+            "records": ("terminal" if rstats and rstats.get("terminal_records") else
+                        "nibble" if rstats and rstats.get("nibble_codes") else "byte"),
             **({"compact_cus_of_32": a.compact_cus} if a.compact_cus else {}),
             "parallelism": f"batch-sharded x{world}, tree replicated" + ("" if world == 1 or a.no_gather
                                                                          else ", all-gatherv over " + ("RCCL" if a.dist_backend == "nccl" else a.dist_backend)

@@ -312,6 +312,7 @@ class BRWTDevice:
         d = dict(zip(keys, [int(v) for v in out]))
         d["uniform_levels"] = (d["height"] >> 32) & 0xFF  # odometer walk when > 0
         d["nibble_codes"] = bool((d["height"] >> 40) & 1)  # masks as nibble codes (MBRWT_BUILD_ROWS_CODE)
+        d["terminal_records"] = bool((d["height"] >> 41) & 1)  # terminal records (MBRWT_BUILD_ROWS_CODE = 2)
         d["variable"] = d["block_bytes"] == 0  # variable-length records (csrc/rows_var.hip)
         d["height"] &= 0xFFFFFFFF
         cl = (C.c_uint64 * 4)()

@@ -560,6 +560,21 @@ int export_var(const Ctx &c, mbrwt_tree &out) {
     cut[T] = R;
     std::vector<std::vector<BitAppend>> part(T, std::vector<BitAppend>(D));
     std::vector<int> prc(T, MBRWT_OK);
+    // terminal records (r06): every dnode's parent below the root, so a
+    // terminal's fields set the children bits of its ancestors
+    std::vector<uint32_t> par;
+    if (im.term) {
+        par.assign(D, ~0u);
+        std::vector<uint32_t> q{rootd};
+        for (size_t h = 0; h < q.size(); ++h) {
+            const DevNode &v = t.nodes[q[h]];
+            if (v.kind == KIND_LEAF) continue;
+            for (uint32_t c = 0; c < v.arity && v.first_child + c < D; ++c) {
+                par[v.first_child + c] = q[h];
+                if (t.nodes[v.first_child + c].kind != KIND_LEAF) q.push_back(v.first_child + c);
+            }
+        }
+    }
     auto work = [&](uint64_t k) {
         std::vector<BitAppend> &cols = part[k];
         std::vector<uint32_t> mask_of(D, 0), touched;
@@ -720,6 +735,21 @@ int export_rows(const Ctx &c, mbrwt_tree &out) {
     cut[T] = R;
     std::vector<std::vector<BitAppend>> part(T, std::vector<BitAppend>(D));
     std::vector<int> prc(T, MBRWT_OK);
+    // terminal records (r06): every dnode's parent below the root, so a
+    // terminal's fields set the children bits of its ancestors
+    std::vector<uint32_t> par;
+    if (im.term) {
+        par.assign(D, ~0u);
+        std::vector<uint32_t> q{rootd};
+        for (size_t h = 0; h < q.size(); ++h) {
+            const DevNode &v = t.nodes[q[h]];
+            if (v.kind == KIND_LEAF) continue;
+            for (uint32_t c = 0; c < v.arity && v.first_child + c < D; ++c) {
+                par[v.first_child + c] = q[h];
+                if (t.nodes[v.first_child + c].kind != KIND_LEAF) q.push_back(v.first_child + c);
+            }
+        }
+    }
     auto work = [&](uint64_t k) {
         std::vector<BitAppend> &cols = part[k];
         std::vector<uint8_t> blk;
@@ -728,6 +758,8 @@ int export_rows(const Ctx &c, mbrwt_tree &out) {
             uint64_t rem;  // children still to visit
         };
         std::vector<Frame> st;
+        std::vector<uint64_t> mk(im.term ? D : 0, 0);  // terminal records: the row's masks by dnode
+        std::vector<uint32_t> touched;
         // one row's record (entry tt of block bp) -> its bits of every index column
         auto row_bits = [&](const uint8_t *bp, uint32_t tt) -> bool {
             const uint32_t e = bp[tt], o = e & 0x7Fu;
@@ -745,12 +777,43 @@ int export_rows(const Ctx &c, mbrwt_tree &out) {
             }
             cols[1].push(count ? 1u : 0u);
             if (!count) return true;
+            if (im.term) {  // the terminals' fields -> the masks of every node they reach
+                for (const uint32_t u : touched) mk[u] = 0;
+                touched.clear();
+                const uint32_t w = im.table3[0] & 0xFFu, ib = (im.table3[0] >> 8) & 0xFFu, nT = im.table3[1];
+                uint32_t left = count, bit = 0;
+                auto set = [&](uint32_t u, uint64_t bits) {
+                    if (!mk[u]) touched.push_back(u);
+                    mk[u] |= bits;
+                };
+                while (left) {
+                    uint64_t x = 0;
+                    for (uint32_t k = 0; 8 * k < (bit & 7) + w; ++k) x |= (uint64_t)rec[(bit >> 3) + k] << (8 * k);
+                    const uint32_t f = (uint32_t)(x >> (bit & 7)) & ((1u << w) - 1u);
+                    bit += w;
+                    const uint32_t id = f & ((1u << ib) - 1u);
+                    if (id >= nT || id >= im.term_dnode.size()) return false;
+                    const uint32_t e = im.table3[4 + id], u = im.term_dnode[id];
+                    const uint32_t m = (e >> 30) == 3u ? f >> ib : 1u;
+                    if (!m || u >= D) return false;
+                    if ((e >> 30) == 3u) set(u, m);
+                    for (uint32_t ch = u; ch != rootd;) {
+                        const uint32_t p = par[ch];
+                        if (p == ~0u) return false;
+                        set(p, 1ull << (ch - t.nodes[p].first_child));
+                        ch = p;
+                    }
+                    left -= std::min<uint32_t>(left, (uint32_t)__builtin_popcount(m));
+                }
+            }
             uint32_t pos = 0;  // (bytes; nibbles for nibble-coded masks, rows_record.hpp RecMasks)
             auto nibble = [&](uint32_t k) { return (uint32_t)(rec[k >> 1] >> ((k & 1u) * 4u)) & 15u; };
             auto visit = [&](uint32_t v) {  // v reached: read its mask, append its children's bits
                 const DevNode &dn = t.nodes[v];
                 uint64_t m;
-                if (im.nib) {
+                if (im.term) {
+                    m = mk[v];
+                } else if (im.nib) {
                     const uint32_t c = nibble(pos);
                     if (c < 8) {
                         m = 1u << c;

@@ -642,7 +642,7 @@ int mbrwt_set_build_option(int option, int64_t value) {
         t.rows_classes = (int)value;
         return MBRWT_OK;
     case MBRWT_BUILD_ROWS_CODE:
-        if (value < 0 || value > 1) break;
+        if (value < 0 || value > 3) break;
         t.rows_code = (int)value;
         return MBRWT_OK;
     default:
@@ -712,7 +712,7 @@ int mbrwt_rows_stats(const mbrwt_ctx *ctx, uint64_t out[8]) {
     out[4] = r.record_bytes;
     out[5] = r.spilled_rows;
     out[6] = r.long_rows;
-    out[7] = r.height | (uint64_t)r.uni << 32 | (uint64_t)(r.nib ? 1 : 0) << 40;
+    out[7] = r.height | (uint64_t)r.uni << 32 | (uint64_t)(r.nib ? 1 : 0) << 40 | (uint64_t)(r.term ? 1 : 0) << 41;
     return MBRWT_OK;
 }
 int mbrwt_rows_classes(const mbrwt_ctx *ctx, uint64_t out[4]) {

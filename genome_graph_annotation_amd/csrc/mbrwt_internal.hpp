@@ -265,6 +265,19 @@ struct RowsImage {
     bool mask1 = false;             // every internal node (leaf parents too) has arity <= 8: one-byte masks
     bool nib = false;               // masks as nibble codes (rows_record.hpp RecMasks; MBRWT_BUILD_ROWS_CODE)
     uint32_t max_arity = 0;         // the widest internal node (masks of (arity + 7) / 8 bytes; r06: up to 64)
+    // terminal records (MBRWT_BUILD_ROWS_CODE = 2, r06; rows_record.hpp
+    // term_walk): the TT table (host, device) the traversal and the one-lane
+    // walks read instead of RWT2 / RWT
+    bool term = false;
+    std::vector<uint32_t> table3;
+    uint32_t *d_table3 = nullptr;
+    std::vector<uint32_t> slot_dnode;  // RWT2 entry -> dnode (entry nE: the root)
+    std::vector<uint32_t> term_dnode;  // terminal id -> dnode (export)
+    // the V accounting of terminal records (rows_count_work): per terminal
+    // its chain of ancestor dnodes from the root and their arities
+    // (WT: [D, nT, 0, 0], nT x D ids, nT x D arities, nT lengths, nT own arities)
+    std::vector<uint32_t> table4;
+    uint32_t *d_table4 = nullptr;
     uint32_t uni = 0;               // K internal levels above leaf parents on every path (rows_walk_uni), else 0
     uint64_t bytes = 0;             // blocks + spill used
     uint32_t occ_cap = 0;           // workgroups per CU of k_traverse_rows (0 = the default; MBRWT_BUILD_ROWS_WGS_PER_CU)
@@ -294,7 +307,8 @@ struct RowsImage {
 // the RWT table of a finished node tree; false (and an empty table) when the
 // shape is outside the row-record kernels' limits
 bool build_rwt_table(const Tree &tree, std::vector<uint32_t> &table, uint32_t &height, uint32_t &max_arity);
-bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &table2, uint32_t &frames);
+bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &table2, uint32_t &frames,
+                      std::vector<uint32_t> *slot_dnode = nullptr);
 uint32_t rwt2_uniform_levels(const std::vector<uint32_t> &table2);
 // the thread's build layout (mbrwt_set_build_option; AUTO when unset)
 int build_layout();
@@ -548,7 +562,7 @@ struct BuildTuning {
     uint64_t shard_rows = 0;     // 0: the default shard size
     uint32_t rows_wgs_per_cu = 0;
     int rows_classes = -1;       // record classes: -1 auto, 0 never, 1 whenever exact
-    int rows_code = 0;           // record masks: 0 bytes, 1 nibble codes (uniform trees of arity <= 8)
+    int rows_code = 0;           // records: 0 AUTO (terminal records where smaller, else byte masks), 1 nibble codes, 2 terminal records, 3 byte masks
 };
 BuildTuning &build_tuning();
 void set_build_tuning(const BuildTuning &t);

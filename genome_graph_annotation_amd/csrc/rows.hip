@@ -139,7 +139,7 @@ bool build_rwt_table(const Tree &tree, std::vector<uint32_t> &table, uint32_t &h
 //     LP list   0xE0000000 | arity << 16 | first u16 of its column list
 //     internal  arity << 16 | first entry of its children
 // so the walk reads ONE table word per visited child.
-bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &t2, uint32_t &frames) {
+bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &t2, uint32_t &frames, std::vector<uint32_t> *slot_dnode) {
     t2.clear();
     frames = 0;
     const auto &N = tree.nodes;
@@ -222,6 +222,13 @@ bool build_rwt2_table(const Tree &tree, std::vector<uint32_t> &t2, uint32_t &fra
         return true;
     };
     t2.assign(4 + nE, 0);
+    if (slot_dnode) {  // (terminal records: the dnode of every entry; slot nE = the root)
+        slot_dnode->assign(nE + 1, ~0u);
+        (*slot_dnode)[nE] = root;
+        if (!root_lp)
+            for (const uint32_t v : order)
+                for (uint32_t c = 0; c < N[v].arity; ++c) (*slot_dnode)[first_of[v] + c] = N[v].first_child + c;
+    }
     if (!entry(root, t2[0])) return false;
     t2[1] = nE;
     t2[2] = frames;
@@ -326,23 +333,204 @@ void append_path_table(std::vector<uint32_t> &t2, uint32_t K) {
         t2.push_back((uint32_t)col[i] | (i + 1 < col.size() ? (uint32_t)col[i + 1] << 16 : 0u));
 }
 
+// TERMINAL records (r06, MBRWT_BUILD_ROWS_CODE = 2; rows_record.hpp
+// term_walk): every RWT2 entry that is a leaf or a leaf parent is a
+// terminal.  TT = [w | ib << 8, nT, 0, 0, nT entry words, the RWT2 column
+// lists]; the build table BT = [root entry, the root's terminal id (a
+// one-level tree), nE, 0, nE entries, nE terminal ids (internal: ~0)] for
+// the build's walk.  False when the fields would not fit 28 bits (more than
+// 4,096 terminals or a leaf parent wider than 16).
+bool build_term_tables(const std::vector<uint32_t> &t2, std::vector<uint32_t> &tt, std::vector<uint32_t> &bt,
+                       std::vector<uint32_t> &term_slot) {
+    tt.clear();
+    bt.clear();
+    term_slot.clear();
+    if (t2.size() < 4) return false;
+    const uint32_t root = t2[0], nE = t2[1];
+    const size_t lists_end = t2[3] ? (size_t)t2[3] : t2.size();
+    if (4 + (size_t)nE > lists_end) return false;
+    std::vector<uint32_t> ent, tid(nE, ~0u);
+    uint32_t mbits = 0;
+    auto is_term = [](uint32_t e) { return (e >> 31) != 0u; };
+    auto lp_arity = [](uint32_t e) { return (e >> 30) == 3u ? (e >> 16) & 0x7Fu : 0u; };
+    if ((root >> 30) == 3u) {  // a one-level tree: the root is the only terminal
+        ent.push_back(root);
+        term_slot.push_back(nE);
+        mbits = lp_arity(root);
+    } else {
+        for (uint32_t i = 0; i < nE; ++i) {
+            const uint32_t e = t2[4 + i];
+            if (!is_term(e)) continue;
+            tid[i] = (uint32_t)ent.size();
+            ent.push_back(e);
+            term_slot.push_back(i);
+            mbits = std::max(mbits, lp_arity(e));
+        }
+    }
+    const uint32_t nT = (uint32_t)ent.size();
+    uint32_t ib = 1;
+    while ((1u << ib) < nT) ++ib;
+    if (nT == 0 || nT > 4096 || mbits > 16 || ib + mbits > 28) return false;
+    const uint32_t w = ib + mbits;
+    tt = {w | ib << 8, nT, 0u, 0u};
+    tt.insert(tt.end(), ent.begin(), ent.end());
+    tt.insert(tt.end(), t2.begin() + 4 + nE, t2.begin() + lists_end);
+    bt = {root, 0u, nE, 0u};
+    bt.insert(bt.end(), t2.begin() + 4, t2.begin() + 4 + nE);
+    bt.insert(bt.end(), tid.begin(), tid.end());
+    return tt.size() <= kRowsMaxTableWords;
+}
+
+// WT (terminal records' V accounting): every terminal's chain of ancestor
+// dnodes from the root down, their arities, the chain's length and the
+// terminal's own arity (a leaf parent's; 0 for a leaf).  The parents come
+// from the logical tree below the root (as build_rwt_table walks it).
+bool build_work_table(const Tree &tree, const std::vector<uint32_t> &term_dnode, std::vector<uint32_t> &wt) {
+    const auto &N = tree.nodes;
+    const uint32_t root = tree.folded ? 0u : 1u;
+    std::vector<uint32_t> parent(N.size(), ~0u), q{root};
+    for (size_t h = 0; h < q.size(); ++h) {
+        const DevNode &v = N[q[h]];
+        if (v.kind == KIND_LEAF) continue;
+        for (uint32_t c = 0; c < v.arity; ++c) {
+            const uint32_t w = v.first_child + c;
+            if (w >= N.size()) return false;
+            parent[w] = q[h];
+            if (N[w].kind != KIND_LEAF) q.push_back(w);
+        }
+    }
+    const uint32_t nT = (uint32_t)term_dnode.size();
+    std::vector<std::vector<uint32_t>> chains(nT);
+    uint32_t D = 1;
+    for (uint32_t t = 0; t < nT; ++t) {
+        const uint32_t u = term_dnode[t];
+        if (u >= N.size()) return false;
+        for (uint32_t a = u == root ? ~0u : parent[u]; a != ~0u; a = a == root ? ~0u : parent[a]) {
+            chains[t].push_back(a);
+            if (chains[t].size() > 32) return false;
+        }
+        std::reverse(chains[t].begin(), chains[t].end());
+        D = std::max<uint32_t>(D, (uint32_t)chains[t].size());
+    }
+    wt.assign(4 + (size_t)nT * (2 * D + 2), 0u);
+    wt[0] = D;
+    wt[1] = nT;
+    for (uint32_t t = 0; t < nT; ++t) {
+        const uint32_t u = term_dnode[t];
+        for (uint32_t k = 0; k < chains[t].size(); ++k) {
+            wt[4 + (size_t)t * D + k] = chains[t][k];
+            wt[4 + (size_t)nT * D + (size_t)t * D + k] = N[chains[t][k]].arity;
+        }
+        wt[4 + (size_t)2 * nT * D + t] = (uint32_t)chains[t].size();
+        wt[4 + (size_t)2 * nT * D + nT + t] = N[u].kind == KIND_LEAF ? 0u : N[u].arity;
+    }
+    return true;
+}
+
 namespace {
+
+// the terminals of row r's descent in pre-order, term(id, children mask):
+// the row's masks (emit_row_masks) walked over the build table BT
+// (build_term_tables).  False when the row has more than kTermMaxMasks masks
+// or its masks do not follow the table.
+constexpr uint32_t kTermMaxMasks = 256;
+template <class Term>
+__device__ bool row_terms(const DevNode *nodes, bool folded, uint32_t r, const uint32_t *bt, Term term,
+                          uint32_t &labels) {
+    uint16_t mb[kTermMaxMasks];
+    uint32_t nm = 0;
+    labels = emit_row_masks(nodes, folded, r, [&](uint64_t mk, uint32_t, uint32_t) {
+        if (nm < kTermMaxMasks) mb[nm] = (uint16_t)mk;
+        ++nm;
+    });
+    if (labels == ~0u || nm > kTermMaxMasks) return false;
+    if (!nm) return labels == 0;
+    const uint32_t root = gld(bt);
+    if ((root >> 30) == 3u) {  // a one-level tree
+        term(gld(bt + 1), (uint32_t)mb[0]);
+        return nm == 1;
+    }
+    const uint32_t nE = gld(bt + 2);
+    const uint32_t *ent = bt + 4, *tid = bt + 4 + nE;
+    uint32_t pos = 1, m = mb[0], f = root & 0xFFFFu;
+    uint32_t sf[kRowsMaxHeight], sm[kRowsMaxHeight];
+    int sp = 0;
+    while (true) {
+        if (!m) {
+            if (!sp) break;
+            --sp;
+            f = sf[sp];
+            m = sm[sp];
+            continue;
+        }
+        const uint32_t c = (uint32_t)__builtin_ctz(m);
+        m &= m - 1u;
+        const uint32_t sl = f + c;
+        if (sl >= nE) return false;
+        const uint32_t e = gld(ent + sl);
+        if ((e >> 31) == 0u) {  // an internal node: its mask, one level down
+            if (pos >= nm || (m && sp == (int)kRowsMaxHeight)) return false;
+            if (m) {
+                sf[sp] = f;
+                sm[sp] = m;
+                ++sp;
+            }
+            f = e & 0xFFFFu;
+            m = mb[pos++];
+        } else if ((e >> 30) == 3u) {  // a leaf parent: a terminal with its mask
+            if (pos >= nm) return false;
+            term(gld(tid + sl), (uint32_t)mb[pos++]);
+        } else {  // a leaf: a terminal of its own
+            term(gld(tid + sl), 0u);
+        }
+    }
+    return pos == nm;
+}
+// row r's terminal fields (w bits: id | mask << ib) from byte p on; the
+// bytes written, or ~0u
+__device__ __forceinline__ uint32_t write_row_terms(const DevNode *nodes, bool folded, uint32_t r, uint8_t *p,
+                                                    const uint32_t *bt, uint32_t w, uint32_t ib, uint32_t &labels) {
+    uint64_t acc = 0;
+    uint32_t nb = 0, wr = 0;
+    const bool ok = row_terms(
+        nodes, folded, r, bt,
+        [&](uint32_t id, uint32_t m) {
+            acc |= (uint64_t)(id | (m << ib)) << nb;
+            nb += w;
+            while (nb >= 8u) {
+                p[wr++] = (uint8_t)acc;
+                acc >>= 8;
+                nb -= 8u;
+            }
+        },
+        labels);
+    if (nb) p[wr++] = (uint8_t)acc;
+    return ok ? wr : ~0u;
+}
 
 // per row of a range: record size (1 + mask bytes, < 2^15) | 0x8000 when the
 // row has >= 255 labels (its count does not fit the inline byte)
 // (nib: the masks as nibble codes, rows_record.hpp RecMasks)
 __global__ __launch_bounds__(256) void k_rows_measure(const DevNode *nodes, uint32_t folded, uint64_t n, uint16_t *sz,
-                                                      unsigned long long *acc, uint32_t nib) {
+                                                      unsigned long long *acc, uint32_t code, const uint32_t *bt,
+                                                      uint32_t w) {
+    const bool nib = code == 1u;
     unsigned long long lab = 0, bytes = 0, bad = 0, bytes1 = 0;
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gs) {
         uint32_t b = 1, nn = 0, b1 = 1;
-        const uint32_t L = emit_row_masks(nodes, folded != 0, (uint32_t)r, [&](uint64_t mk, uint32_t a, uint32_t) {
+        uint32_t L = emit_row_masks(nodes, folded != 0, (uint32_t)r, [&](uint64_t mk, uint32_t a, uint32_t) {
             if (nib) nn += nib_codes((uint32_t)mk);
             else b += rec_mask_bytes(a);
             b1 += rec_mask_bytes(a);
         });
         b += (nn + 1) / 2;
+        if (code == 2u && L != ~0u) {  // terminal records: the fields' bytes
+            uint32_t nt = 0, L2 = 0;
+            b = row_terms(nodes, folded != 0, (uint32_t)r, bt, [&](uint32_t, uint32_t) { ++nt; }, L2) && L2 == L
+                    ? 1u + (nt * w + 7u) / 8u
+                    : 0x8000u;  // (a row the fields cannot hold: bad)
+        }
         bytes1 += b1;
         if (L == ~0u || b >= 0x8000) {
             ++bad;
@@ -454,7 +642,13 @@ __device__ __forceinline__ uint32_t write_row_masks(const DevNode *nodes, bool f
 // one thread per block of the range: header, inline records, spill entries
 __global__ __launch_bounds__(256) void k_rows_write(const DevNode *nodes, uint32_t folded, uint64_t nr_range,
                                                     const uint16_t *sz, uint32_t B, uint32_t S, uint8_t *blocks,
-                                                    uint8_t *spill, unsigned long long *spill_used, uint32_t nib) {
+                                                    uint8_t *spill, unsigned long long *spill_used, uint32_t code,
+                                                    const uint32_t *bt, uint32_t w, uint32_t ib) {
+    const uint32_t nib = code == 1u ? 1u : 0u;
+    auto write = [&](uint32_t r, uint8_t *p, uint32_t &L) -> uint32_t {
+        return code == 2u ? write_row_terms(nodes, folded != 0, r, p, bt, w, ib, L)
+                          : write_row_masks(nodes, folded != 0, r, p, nib, L);
+    };
     const uint64_t nb = (nr_range + S - 1) / S;
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gs) {
@@ -470,9 +664,9 @@ __global__ __launch_bounds__(256) void k_rows_write(const DevNode *nodes, uint32
                 const uint64_t idx = atomicAdd(spill_used, (unsigned long long)spill_units(s[t]));
                 uint8_t *se = spill + idx * 16;
                 uint32_t L = 0;
-                const uint32_t w = write_row_masks(nodes, folded != 0, r, se + 8, nib, L);
+                const uint32_t nw = write(r, se + 8, L);
                 *reinterpret_cast<uint32_t *>(se) = L;
-                *reinterpret_cast<uint32_t *>(se + 4) = w;
+                *reinterpret_cast<uint32_t *>(se + 4) = nw;
                 blk[t] = (uint8_t)(o | 0x80u);
                 blk[o] = (uint8_t)std::min<uint32_t>(L, 255);
                 for (uint32_t k = 0; k < 4; ++k) blk[o + 1 + k] = (uint8_t)(idx >> (8 * k));
@@ -480,9 +674,9 @@ __global__ __launch_bounds__(256) void k_rows_write(const DevNode *nodes, uint32
             } else {
                 blk[t] = (uint8_t)o;
                 uint32_t L = 0;
-                const uint32_t w = write_row_masks(nodes, folded != 0, r, blk + o + 1, nib, L);
+                const uint32_t nw = write(r, blk + o + 1, L);
                 blk[o] = (uint8_t)L;
-                o += 1 + w;
+                o += 1 + nw;
             }
         }
     }
@@ -508,6 +702,7 @@ struct RowsBuild {
     uint16_t *d_sz = nullptr;
     uint64_t sz_cap = 0;
     hipStream_t s = nullptr;
+    uint32_t *d_bt = nullptr;  // terminal records: the build table (build_term_tables)
 };
 
 void free_rows(RowsImage &r) {
@@ -521,6 +716,8 @@ void free_rows(RowsImage &r) {
     if (r.d_spill_used) (void)hipFree(r.d_spill_used);
     if (r.d_table) (void)hipFree(r.d_table);
     if (r.d_table2) (void)hipFree(r.d_table2);
+    if (r.d_table3) (void)hipFree(r.d_table3);
+    if (r.d_table4) (void)hipFree(r.d_table4);
     if (r.classes) (void)hipFree(r.classes);
     r = RowsImage();
 }
@@ -547,6 +744,7 @@ void rows_build_abort(RowsBuild *rb) {
     if (!rb) return;
     if (rb->d_acc) (void)hipFree(rb->d_acc);
     if (rb->d_sz) (void)hipFree(rb->d_sz);
+    if (rb->d_bt) (void)hipFree(rb->d_bt);
     var_free_scratch(rb->vws);
     free_rows(rb->img);
     delete rb;
@@ -592,7 +790,8 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         return MBRWT_ERR_INVALID;
     }
     if (im.table.empty()) {
-        if (!build_rwt_table(range.tree, im.table, im.height, im.max_arity) || !build_rwt2_table(range.tree, im.table2, im.frames)) {
+        if (!build_rwt_table(range.tree, im.table, im.height, im.max_arity) ||
+            !build_rwt2_table(range.tree, im.table2, im.frames, &im.slot_dnode)) {
             im.table.clear();
             set_error("tree shape outside the row-record limits (arity <= 64, columns < 2^16, height <= 16, a walk table of <= 8192 words)");
             return MBRWT_ERR_UNSUPPORTED;
@@ -618,7 +817,32 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
         // path-table odometer and the one-lane walks, so uniform trees of
         // one-byte masks with a path table only (the others keep bytes)
         im.nib = build_tuning().rows_code == 1 && im.uni && im.table2.size() > 3 && im.table2[3] != 0;
+        // terminal records (r06; MBRWT_BUILD_ROWS_CODE 0 = AUTO, the default,
+        // or 2): trees of masks up to 16 bits whose terminals fit the fields
+        im.term = false;
+        // (AUTO, code 0: where they are smaller than byte masks -- decided on
+        // the first range below; code 3 forces byte masks)
+        const int code = build_tuning().rows_code;
+        if ((code == 0 || code == 2) && im.max_arity <= 16) {
+            std::vector<uint32_t> bt, term_slot;
+            bool ok = build_term_tables(im.table2, im.table3, bt, term_slot);
+            if (ok) {
+                im.term_dnode.resize(term_slot.size());
+                for (size_t i = 0; i < term_slot.size(); ++i)
+                    im.term_dnode[i] = term_slot[i] < im.slot_dnode.size() ? im.slot_dnode[term_slot[i]] : ~0u;
+                ok = build_work_table(range.tree, im.term_dnode, im.table4);
+            }
+            if (ok) {
+                if (!rb.d_bt) {
+                    if (hipMalloc(&rb.d_bt, bt.size() * 4) != hipSuccess) return hip_fail(hipGetLastError(), "build table");
+                    MBRWT_HIP(hipMemcpy(rb.d_bt, bt.data(), bt.size() * 4, hipMemcpyHostToDevice));
+                }
+                im.term = true;
+            }
+        }
     }
+    const uint32_t tw = im.term ? im.table3[0] & 0xFFu : 0u, tib = im.term ? (im.table3[0] >> 8) & 0xFFu : 0u;
+    auto code_of = [&]() -> uint32_t { return im.term ? 2u : im.nib ? 1u : 0u; };
     if (nr > rb.sz_cap) {
         if (rb.d_sz) MBRWT_HIP(hipFree(rb.d_sz));
         rb.d_sz = nullptr;
@@ -629,13 +853,20 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
     auto measure = [&]() -> int {
         MBRWT_HIP(hipMemsetAsync(rb.d_acc, 0, 8 * sizeof(unsigned long long), rb.s));
         hipLaunchKernelGGL(k_rows_measure, dim3(build_grid(nr)), dim3(256), 0, rb.s, range.d_nodes,
-                           range.tree.folded ? 1u : 0u, nr, rb.d_sz, rb.d_acc, im.nib ? 1u : 0u);
+                           range.tree.folded ? 1u : 0u, nr, rb.d_sz, rb.d_acc, code_of(), (const uint32_t *)rb.d_bt, tw);
         MBRWT_HIP(hipGetLastError());
         return read_acc(rb, h, 4);
     };
     if (int rc = measure()) return rc;
-    // nibble codes that do not shrink the first range's records (dense rows:
-    // most masks hold several bits) give way to bytes for the whole image
+    // nibble codes or terminal records that do not shrink the first range's
+    // records (dense rows: most masks hold several bits), or terminal
+    // fields a row of the range cannot take, give way to bytes for the
+    // whole image
+    if (im.term && !rb.decided && (h[2] || h[1] >= h[3])) {
+        im.term = false;
+        im.table3.clear();
+        if (int rc = measure()) return rc;
+    }
     if (im.nib && !rb.decided && h[2] == 0 && h[1] >= h[3]) {
         im.nib = false;
         if (int rc = measure()) return rc;
@@ -792,7 +1023,7 @@ int rows_build_range(RowsBuild *rbp, Ctx &range, uint64_t row0) {
     im.spill_bytes += o[1] * 16;
     hipLaunchKernelGGL(k_rows_write, dim3(build_grid((nr + im.S - 1) / im.S)), dim3(256), 0, rb.s, range.d_nodes,
                        range.tree.folded ? 1u : 0u, nr, rb.d_sz, im.B, im.S, im.blocks + (row0 / im.S) * im.B,
-                       im.spill, im.d_spill_used, im.nib ? 1u : 0u);
+                       im.spill, im.d_spill_used, code_of(), (const uint32_t *)rb.d_bt, tw, tib);
     MBRWT_HIP(hipGetLastError());
     MBRWT_HIP(hipStreamSynchronize(rb.s));
     return MBRWT_OK;
@@ -818,6 +1049,12 @@ int rows_build_finish(RowsBuild *rbp) {
                 hipMalloc(&im.d_table2, im.table2.size() * 4) != hipSuccess ||
                 hipMemcpy(im.d_table2, im.table2.data(), im.table2.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
         rc = hip_fail(hipGetLastError(), "row-record table upload");
+    if (!rc && im.term &&
+        (hipMalloc(&im.d_table3, im.table3.size() * 4) != hipSuccess ||
+         hipMemcpy(im.d_table3, im.table3.data(), im.table3.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+         hipMalloc(&im.d_table4, im.table4.size() * 4) != hipSuccess ||
+         hipMemcpy(im.d_table4, im.table4.data(), im.table4.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
+        rc = hip_fail(hipGetLastError(), "terminal table upload");
     if (rc) {
         rows_build_abort(rbp);
         return rc;
@@ -855,6 +1092,7 @@ int rows_build_finish(RowsBuild *rbp) {
     rb.img = RowsImage();  // ownership moved
     if (rb.d_acc) (void)hipFree(rb.d_acc);
     if (rb.d_sz) (void)hipFree(rb.d_sz);
+    if (rb.d_bt) (void)hipFree(rb.d_bt);
     var_free_scratch(rb.vws);
     delete rbp;
     return MBRWT_OK;
@@ -1321,6 +1559,38 @@ __device__ __forceinline__ void rows_walk_tree(const AS_LDS uint8_t *pb, uint32_
     }
 }
 
+// The walk of a TERMINAL record (r06, rows_record.hpp term_walk): no tree
+// to walk -- each field names a leaf parent (its children mask beside) or a
+// leaf, in pre-order, so a lane reads its fields one after the other (two
+// aligned LDS words and a funnel shift per field) until its row's count of
+// labels is out.  The TT table is in LDS: hdr = its word 0, ent its entries,
+// lst its column lists.
+__device__ __forceinline__ void rows_walk_terms(const AS_LDS uint8_t *pb, uint32_t o, bool live, uint32_t cnt,
+                                                uint32_t hdr, const AS_LDS uint32_t *ent, const AS_LDS uint16_t *lst,
+                                                AS_LDS uint16_t *out, uint32_t pos) {
+    const uint32_t w = hdr & 0xFFu, ib = (hdr >> 8) & 0xFFu;
+    const uint32_t fmask = (1u << w) - 1u, imask = (1u << ib) - 1u;
+    const uint32_t a0 = (uint32_t)(uintptr_t)(pb + o);
+    const AS_LDS uint32_t *wp = (const AS_LDS uint32_t *)(uintptr_t)(a0 & ~3u);
+    uint32_t bit = 8u * (a0 & 3u);
+    uint32_t left = live ? cnt : 0u;
+    uint32_t ob = pos * 2u;  // byte offset of the next label
+    while (left) {
+        const uint32_t wi = bit >> 5;
+        const uint32_t f = __builtin_amdgcn_alignbit(wp[wi + 1], wp[wi], bit & 31u) & fmask;
+        bit += w;
+        const uint32_t e = ent[f & imask];
+        uint32_t x = (e >> 30) == 3u ? (f >> ib) : 1u;  // a leaf parent: its set children; a leaf: itself
+        x = x ? x : 1u;  // (a corrupt field: one label, so the loop still ends)
+        do {
+            *(AS_LDS uint16_t *)((uintptr_t)out + ob) = (uint16_t)term_label(e, lst, (uint32_t)__builtin_ctz(x));
+            ob += 2u;
+            x &= x - 1u;
+            --left;
+        } while (x && left);
+    }
+}
+
 // Tiles per wave (r05).  A persistent grid (every wave a fixed share of the
 // tiles) lasts as long as its slowest wave, and its waves are not equally
 // fast: the workgroups dispatched last lose issue arbitration by age (per-wave
@@ -1346,7 +1616,7 @@ constexpr uint32_t kRowsTilesPerWave = 1;
 // against 0.33 ms per C4 step and was retired: profiles/r06/v01_one_pass.)
 // VAR: the record variant -- 0 byte masks, VAR_NIB nibble codes (the path
 // odometer), VAR_WIDE masks of up to 64 bits (the tree odometer, r06)
-enum : uint32_t { VAR_BYTE = 0, VAR_NIB = 1, VAR_WIDE = 2 };
+enum : uint32_t { VAR_BYTE = 0, VAR_NIB = 1, VAR_WIDE = 2, VAR_TERM = 3 };
 template <int B, int WPB, bool NT, uint32_t WALK, uint32_t VAR = VAR_BYTE>
 __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
     constexpr bool NIB = VAR == VAR_NIB;
@@ -1505,7 +1775,9 @@ __global__ __launch_bounds__(64 * WPB) void k_traverse_rows(RowsParams p) {
                 // instead of one scattered 2-byte store per label: the r03
                 // SQ/TA counters showed the texture-address unit as the
                 // busiest unit)
-                if constexpr (WALK == WALK_TREE_ODOMETER) {
+                if constexpr (WALK == WALK_TREE_ODOMETER && VAR == VAR_TERM) {
+                    rows_walk_terms(rec, o, live, cnt, root, ent, lst, stage, pos);
+                } else if constexpr (WALK == WALK_TREE_ODOMETER) {
 #define MBRWT_TREE_CASE(K)                                                              \
     case K:                                                                             \
         if constexpr (VAR == VAR_WIDE)                                                  \
@@ -1705,10 +1977,13 @@ __global__ __launch_bounds__(256) void k_compact_tiles(CompactParams p) {
                 if (j < count) gst(dst + j, col);
                 ++j;
             };
-            const auto mk = rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, p.v.nib);
-            // (masks beyond 16 bits: the frames in registers, not packed in LDS)
-            const bool ok = WIDE ? rwt_walk(p.table, mk, put, [](uint32_t) {})
-                                 : rwt_walk_lds(p.table, mk, put,
+            auto byte = [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); };
+            const auto mk = rec_masks(byte, p.v.nib);
+            // (masks beyond 16 bits: the frames in registers, not packed in
+            // LDS; terminal records: no frames)
+            const bool ok = p.v.term ? term_walk(p.table, byte, count, put)
+                            : WIDE   ? rwt_walk(p.table, mk, put, [](uint32_t) {})
+                                     : rwt_walk_lds(p.table, mk, put,
                                                 (AS_LDS uint32_t *)cstk + (threadIdx.x >> 6) * 128 * p.stk_lim + lane,
                                                 p.stk_lim);
             if (!ok || j != count) publish_status(p.status, MBRWT_ERR_DEVICE);
@@ -1732,10 +2007,7 @@ __global__ __launch_bounds__(256) void k_rows_get(RowsView v, const uint32_t *ta
         uint32_t count;
         rows_locate(v, row, masks, count);
         uint32_t hit = 0;
-        if (count)
-            (void)rwt_walk(
-                table, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
-                [&](uint32_t c) { hit |= c == col; }, [](uint32_t) {});
+        if (count) (void)record_walk(v, table, masks, count, [&](uint32_t c) { hit |= c == col; }, [](uint32_t) {});
         gst(out + i, (uint8_t)hit);
     }
 }
@@ -1746,7 +2018,7 @@ __global__ __launch_bounds__(256) void k_rows_get(RowsView v, const uint32_t *ta
 template <bool WORK>
 __global__ __launch_bounds__(256) void k_rows_count(RowsView v, const uint32_t *table, const uint64_t *rows,
                                                     uint64_t n, unsigned long long *counts,
-                                                    unsigned long long *scalars) {
+                                                    unsigned long long *scalars, const uint32_t *wt) {
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     unsigned long long vis = 0, lab = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
@@ -1760,8 +2032,28 @@ __global__ __launch_bounds__(256) void k_rows_count(RowsView v, const uint32_t *
         rows_locate(v, row, masks, count);
         vis += 1;
         if (!count) continue;
-        (void)rwt_walk(
-            table, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
+        if (WORK && v.term) {  // terminal records: V from the terminals' ancestor chains (WT)
+            const uint32_t D = wt[0], nT = wt[1];
+            const uint32_t *ids = wt + 4, *ars = ids + (size_t)nT * D, *len = ars + (size_t)nT * D, *own = len + nT;
+            uint32_t prev = ~0u;
+            (void)term_walk(
+                table, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, count,
+                [&](uint32_t) { ++lab; },
+                [&](uint32_t id) {
+                    const uint32_t l = len[id];
+                    uint32_t k = 0;
+                    if (prev != ~0u) {  // (the chain shared with the previous terminal: counted already)
+                        const uint32_t lp = len[prev];
+                        while (k < l && k < lp && ids[(size_t)id * D + k] == ids[(size_t)prev * D + k]) ++k;
+                    }
+                    for (; k < l; ++k) vis += ars[(size_t)id * D + k];
+                    vis += own[id];
+                    prev = id;
+                });
+            continue;
+        }
+        (void)record_walk(
+            v, table, masks, count,
             [&](uint32_t c) {
                 if constexpr (WORK) ++lab;
                 else atomicAdd(counts + c, 1ull);
@@ -1794,9 +2086,7 @@ struct RowHasColumn {
         rows_locate(v, row, masks, count);
         if (!count) return false;
         bool hit = false;
-        (void)rwt_walk(
-            table, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
-            [&](uint32_t c) { hit |= c == col; }, [](uint32_t) {});
+        (void)record_walk(v, table, masks, count, [&](uint32_t c) { hit |= c == col; }, [](uint32_t) {});
         return hit;
     }
 };
@@ -1804,6 +2094,9 @@ struct HasColumnCount {
     RowHasColumn f;
     __device__ uint64_t operator()(const uint64_t &row) const { return f(row) ? 1u : 0u; }
 };
+
+// the table the one-lane walks read: RWT, or TT for terminal records
+const uint32_t *walk_table(const RowsImage &im) { return im.term ? im.d_table3 : im.d_table; }
 
 RowsView view_of(const Ctx &c) {
     RowsView v;
@@ -1814,6 +2107,7 @@ RowsView view_of(const Ctx &c) {
     v.B = c.rows.B;
     v.S = c.rows.S;
     v.nib = c.rows.nib ? 1u : 0u;
+    v.term = c.rows.term ? 1u : 0u;
     return v;
 }
 
@@ -1824,7 +2118,8 @@ constexpr uint32_t kRowsWpb = 8;
 // 8-wave workgroups per CU (16 waves); two of 11 waves fit (22)
 constexpr uint32_t kRowsWpbWide = 11;
 template <int B, bool NT>
-RowsFn rows_fn_b(uint32_t walk, uint32_t wpb, bool nib, bool wide) {
+RowsFn rows_fn_b(uint32_t walk, uint32_t wpb, bool nib, bool wide, bool term) {
+    if (term) return k_traverse_rows<B, kRowsWpb, NT, WALK_TREE_ODOMETER, VAR_TERM>;  // (terminal records)
     if (nib) return k_traverse_rows<B, kRowsWpb, NT, WALK_ODOMETER, VAR_NIB>;  // (nibble codes: the path odometer)
     if (wide)  // (masks beyond 16 bits: the tree odometer)
         return wpb == kRowsWpbWide ? k_traverse_rows<B, kRowsWpbWide, NT, WALK_TREE_ODOMETER, VAR_WIDE>
@@ -1837,10 +2132,12 @@ RowsFn rows_fn_b(uint32_t walk, uint32_t wpb, bool nib, bool wide) {
 }
 RowsFn rows_fn(const RowsImage &im, uint32_t walk, uint32_t wpb) {
     const bool nt = im.bytes > (1ull << 30);  // non-temporal block reads for images beyond the caches
-    const bool wide = im.max_arity > 16;
+    const bool wide = im.max_arity > 16, term = im.term;
     if (im.B == 64)
-        return nt ? rows_fn_b<64, true>(walk, wpb, im.nib, wide) : rows_fn_b<64, false>(walk, wpb, im.nib, wide);
-    return nt ? rows_fn_b<128, true>(walk, wpb, im.nib, wide) : rows_fn_b<128, false>(walk, wpb, im.nib, wide);
+        return nt ? rows_fn_b<64, true>(walk, wpb, im.nib, wide, term)
+                  : rows_fn_b<64, false>(walk, wpb, im.nib, wide, term);
+    return nt ? rows_fn_b<128, true>(walk, wpb, im.nib, wide, term)
+              : rows_fn_b<128, false>(walk, wpb, im.nib, wide, term);
 }
 // resident waves per CU with workgroups of w waves: the LDS (160 KiB per CU:
 // the table once per workgroup + per_wave bytes per wave) within the 24-wave cap
@@ -1875,6 +2172,7 @@ struct MaskTile {
 // (MBRWT_OPT_ROWS_WALK = 6 forces the non-odometer walk: tests)
 static uint32_t rows_walk_of(const Ctx &c) {
     const RowsImage &im = c.rows;
+    if (im.term) return WALK_TREE_ODOMETER;  // (terminal records: their own walk, in the tree odometer's slot)
     if (im.nib) return WALK_ODOMETER;       // (nibble codes: only the path odometer reads them)
     if (im.max_arity > 16) return WALK_TREE_ODOMETER;  // (masks beyond 16 bits: the tree odometer only)
     if (im.uni && c.rows_walk != 6 && c.rows_walk != 4 && c.rows_walk != 3)
@@ -1940,8 +2238,9 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     p.spill = (uint64_t)(uintptr_t)im.spill;
     p.magic = im.magic;
     p.S = im.S;
-    p.table_words = (uint32_t)im.table2.size();
-    p.table = im.d_table2;
+    const std::vector<uint32_t> &tab = im.term ? im.table3 : im.table2;  // (terminal records: the TT table)
+    p.table_words = (uint32_t)tab.size();
+    p.table = im.term ? im.d_table3 : im.d_table2;
     p.C = C;
     p.temp = reinterpret_cast<uint8_t *>(c.ws_temp.buf);
     p.tile_counts = d_tc;
@@ -1953,15 +2252,16 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
     p.frames = im.frames;
     p.mask1 = im.mask1 ? 1u : 0u;
 
-    const size_t table_bytes = ((im.table2.size() + 3) & ~size_t(3)) * 4;
+    const size_t table_bytes = ((tab.size() + 3) & ~size_t(3)) * 4;
     const size_t per_wave = 64ull * (im.B + 4) + 256ull * p.stk_words + (walk >= WALK_ODOMETER ? 2ull * C : 0ull);
-    const uint32_t wpb = (walk == WALK_TREE_ODOMETER && !im.occ_cap &&
+    const uint32_t wpb = (walk == WALK_TREE_ODOMETER && !im.term && !im.occ_cap &&
                           rows_waves_per_cu(table_bytes, per_wave, kRowsWpbWide) >
                               rows_waves_per_cu(table_bytes, per_wave, kRowsWpb))
                              ? kRowsWpbWide
                              : kRowsWpb;
     const RowsFn kfn = rows_fn(im, walk, wpb);
-    const size_t lds = table_bytes + wpb * per_wave;
+    // (terminal records: a field's second word may lie past the last wave's stage)
+    const size_t lds = table_bytes + wpb * per_wave + (im.term ? 16 : 0);
     const uint32_t threads = 64 * wpb;
     // at most 24 waves (3 workgroups of 8) per CU: more waves make the walk phase
     // slower than the extra loads in flight gain (C4 0.426 ms at 3 against
@@ -2007,7 +2307,7 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         // tree odometer's table -- 8.8 KB at the greedy + relax shape -- is
         // staged once per workgroup: one tile per wave took 0.518 against
         // 0.458 ms there, profiles/r05)
-        const bool persistent = walk != WALK_ODOMETER;
+        const bool persistent = walk != WALK_ODOMETER && !im.term;  // (terminal records: a small table)
         const uint64_t per_wg = (uint64_t)wpb * kRowsTilesPerWave;
         const uint64_t g = persistent
                                ? std::max<uint64_t>(1, std::min<uint64_t>((nt + wpb - 1) / wpb, (uint64_t)c.rb_blocks))
@@ -2033,7 +2333,7 @@ int rows_get_rows(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_offset
         cp.classes = im.classes;
         cp.class_bits = im.class_bits;
         cp.v = view_of(c);
-        cp.table = im.d_table;
+        cp.table = im.term ? im.d_table3 : im.d_table;
         const uint64_t waves = (nt + kCompactTpw - 1) / kCompactTpw;
         cp.stk_lim = stk_lim;
         // (MBRWT_OPT_COMPACT_CUS: on the CU-masked stream, between two events)
@@ -2098,7 +2398,7 @@ int rows_get_batch(Ctx &c, const uint64_t *d_rows, const uint64_t *d_cols, uint6
         if (int rc = rows_class_map(c, d_rows, n, &d_rows, s)) return rc;
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
     hipLaunchKernelGGL(k_rows_get, dim3((unsigned)simple_grid(n)), dim3(256), 0, s, view_of(c),
-                       (const uint32_t *)c.rows.d_table, d_rows, d_cols, n, c.tree.num_columns, d_out,
+                       (const uint32_t *)walk_table(c.rows), d_rows, d_cols, n, c.tree.num_columns, d_out,
                        reinterpret_cast<unsigned long long *>(c.d_scalars));
     MBRWT_HIP(hipGetLastError());
     MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
@@ -2114,8 +2414,8 @@ int rows_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_co
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
     if (n)
         hipLaunchKernelGGL(k_rows_count<false>, dim3((unsigned)simple_grid(n)), dim3(256), 0, s, view_of(c),
-                           (const uint32_t *)c.rows.d_table, d_rows, n, reinterpret_cast<unsigned long long *>(d_counts),
-                           reinterpret_cast<unsigned long long *>(c.d_scalars));
+                           (const uint32_t *)walk_table(c.rows), d_rows, n, reinterpret_cast<unsigned long long *>(d_counts),
+                           reinterpret_cast<unsigned long long *>(c.d_scalars), (const uint32_t *)c.rows.d_table4);
     MBRWT_HIP(hipGetLastError());
     MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     MBRWT_HIP(hipStreamSynchronize(s));
@@ -2124,13 +2424,14 @@ int rows_count_labels(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *d_co
 
 int rows_count_work(Ctx &c, const uint64_t *d_rows, uint64_t n, uint64_t *visits, uint64_t *labels, hipStream_t s) {
     if (c.rows.var) return var_count(c, d_rows, n, nullptr, visits, labels, s);
+
     if (c.rows.classes)
         if (int rc = rows_class_map(c, d_rows, n, &d_rows, s)) return rc;
     MBRWT_HIP(hipMemsetAsync(c.d_scalars, 0, 8 * sizeof(uint64_t), s));
     if (n)
         hipLaunchKernelGGL(k_rows_count<true>, dim3((unsigned)simple_grid(n)), dim3(256), 0, s, view_of(c),
-                           (const uint32_t *)c.rows.d_table, d_rows, n, nullptr,
-                           reinterpret_cast<unsigned long long *>(c.d_scalars));
+                           (const uint32_t *)walk_table(c.rows), d_rows, n, nullptr,
+                           reinterpret_cast<unsigned long long *>(c.d_scalars), (const uint32_t *)c.rows.d_table4);
     MBRWT_HIP(hipGetLastError());
     MBRWT_HIP(hipMemcpyAsync(c.h_scalars, c.d_scalars, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     MBRWT_HIP(hipStreamSynchronize(s));
@@ -2149,7 +2450,7 @@ int rows_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t rows_cap
     }
     if (c.rows.classes) return rows_class_get_column(c, column, d_rows, rows_cap, rows_needed, s);
     const uint64_t n = c.tree.num_rows;
-    const RowHasColumn f{view_of(c), c.rows.d_table, (uint32_t)column};
+    const RowHasColumn f{view_of(c), walk_table(c.rows), (uint32_t)column};
     hipcub::CountingInputIterator<uint64_t> rows_it(0);
     // the column's size first (a reduce over the rows), then the rows
     hipcub::TransformInputIterator<uint64_t, HasColumnCount, hipcub::CountingInputIterator<uint64_t>> cnt_it(

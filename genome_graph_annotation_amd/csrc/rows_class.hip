@@ -60,15 +60,13 @@ __device__ bool record_of(const RowsView &v, const uint32_t *table, uint64_t r, 
     if (!rr.count) return true;
     uint32_t hi = 0;
     const uint64_t m = rr.masks;
-    const bool ok = rwt_walk(
-        table,
-        rec_masks(
-            [&](uint32_t o) {
-                hi = o + 1 > hi ? o + 1 : hi;
-                return (uint32_t)gld_at<uint8_t>(m + o);
-            },
-            v.nib),
-        [](uint32_t) {}, [](uint32_t) {});
+    const bool ok = record_walk_bytes(
+        v, table,
+        [&](uint32_t o) {
+            hi = o + 1 > hi ? o + 1 : hi;
+            return (uint32_t)gld_at<uint8_t>(m + o);
+        },
+        rr.count, [](uint32_t) {}, [](uint32_t) {});
     rr.len = hi;
     return ok;
 }
@@ -206,10 +204,7 @@ __global__ __launch_bounds__(256) void k_class_has(RowsView v, const uint32_t *t
         uint32_t count;
         rows_locate(v, k, masks, count);
         bool hit = false;
-        if (count)
-            (void)rwt_walk(
-                table, rec_masks([&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, v.nib),
-                [&](uint32_t c) { hit |= c == col; }, [](uint32_t) {});
+        if (count) (void)record_walk(v, table, masks, count, [&](uint32_t c) { hit |= c == col; }, [](uint32_t) {});
         gst(has + k, (uint8_t)(hit ? 1 : 0));
     }
 }
@@ -226,6 +221,8 @@ struct ClassHasCount {
 
 uint64_t grid_of(uint64_t items) { return std::max<uint64_t>(1, std::min<uint64_t>((items + 255) / 256, 65536)); }
 
+// the table the record walks read: RWT, or TT for terminal records (r06)
+const uint32_t *class_table(const RowsImage &im) { return im.term ? im.d_table3 : im.d_table; }
 RowsView block_view(const RowsImage &im, uint64_t records) {
     RowsView v;
     v.blocks = (uint64_t)(uintptr_t)im.blocks;
@@ -235,6 +232,7 @@ RowsView block_view(const RowsImage &im, uint64_t records) {
     v.B = im.B;
     v.S = im.S;
     v.nib = im.nib ? 1u : 0u;
+    v.term = im.term ? 1u : 0u;
     return v;
 }
 
@@ -279,7 +277,7 @@ int rows_classes_build(RowsImage &im, uint64_t n, int mode, uint64_t *sample_dis
         const uint64_t m = kSampleRows, stride = n / m;
         uint64_t *k0 = sc.get<uint64_t>(m), *k1 = sc.get<uint64_t>(m), *d_cnt = sc.get<uint64_t>(1);
         if (!k0 || !k1 || !d_cnt) return MBRWT_OK;
-        hipLaunchKernelGGL(k_class_hash, dim3((unsigned)grid_of(m)), dim3(256), 0, s, v, im.d_table, 0ull, stride, m,
+        hipLaunchKernelGGL(k_class_hash, dim3((unsigned)grid_of(m)), dim3(256), 0, s, v, class_table(im), 0ull, stride, m,
                            k0, (uint64_t *)nullptr, d_err);
         MBRWT_HIP(hipGetLastError());
         size_t tb = 0, rb = 0;
@@ -320,7 +318,7 @@ int rows_classes_build(RowsImage &im, uint64_t n, int mode, uint64_t *sample_dis
     uint64_t *keys_in = sc.get<uint64_t>(n), *vals_in = sc.get<uint64_t>(n);
     uint64_t *keys = sc.get<uint64_t>(n), *rows = sc.get<uint64_t>(n);
     if (!keys_in || !vals_in || !keys || !rows) return MBRWT_OK;
-    hipLaunchKernelGGL(k_class_hash, dim3((unsigned)grid_of(n)), dim3(256), 0, s, v, im.d_table, 0ull, 1ull, n,
+    hipLaunchKernelGGL(k_class_hash, dim3((unsigned)grid_of(n)), dim3(256), 0, s, v, class_table(im), 0ull, 1ull, n,
                        keys_in, vals_in, d_err);
     MBRWT_HIP(hipGetLastError());
     hipcub::CountingInputIterator<uint64_t> it(0);
@@ -346,11 +344,11 @@ int rows_classes_build(RowsImage &im, uint64_t n, int mode, uint64_t *sample_dis
         return MBRWT_OK;
     }
     MBRWT_HIP(hipMemsetAsync(index, 0, index_words * 4, s));
-    hipLaunchKernelGGL(k_class_assign, dim3((unsigned)grid_of(n)), dim3(256), 0, s, v, im.d_table, rows, cid1, rep, n,
+    hipLaunchKernelGGL(k_class_assign, dim3((unsigned)grid_of(n)), dim3(256), 0, s, v, class_table(im), rows, cid1, rep, n,
                        w, index, d_err);
     MBRWT_HIP(hipGetLastError());
     unsigned long long *d_acc = d_err + 1;  // [1] units, [2] spilled, [3] long
-    hipLaunchKernelGGL(k_class_measure, dim3((unsigned)grid_of(D)), dim3(256), 0, s, v, im.d_table, rep, D, d_acc);
+    hipLaunchKernelGGL(k_class_measure, dim3((unsigned)grid_of(D)), dim3(256), 0, s, v, class_table(im), rep, D, d_acc);
     MBRWT_HIP(hipGetLastError());
     MBRWT_HIP(hipMemcpyAsync(h_err, d_err, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     MBRWT_HIP(hipStreamSynchronize(s));
@@ -374,7 +372,7 @@ int rows_classes_build(RowsImage &im, uint64_t n, int mode, uint64_t *sample_dis
     MBRWT_HIP(hipMemsetAsync(dblocks, 0, D * kClassB, s));
     MBRWT_HIP(hipMemsetAsync(dspill, 0, spill_cap, s));
     MBRWT_HIP(hipMemsetAsync(d_acc, 0, sizeof(unsigned long long), s));
-    hipLaunchKernelGGL(k_class_write, dim3((unsigned)grid_of(D)), dim3(256), 0, s, v, im.d_table, rep, D, dblocks,
+    hipLaunchKernelGGL(k_class_write, dim3((unsigned)grid_of(D)), dim3(256), 0, s, v, class_table(im), rep, D, dblocks,
                        dspill, d_acc);
     MBRWT_HIP(hipGetLastError());
     MBRWT_HIP(hipStreamSynchronize(s));
@@ -419,7 +417,7 @@ int rows_class_get_column(Ctx &c, uint64_t column, uint64_t *d_rows, uint64_t ro
     int rc;
     if ((rc = ensure(c.ws_class, D))) return rc;
     uint8_t *has = static_cast<uint8_t *>(c.ws_class.buf);
-    hipLaunchKernelGGL(k_class_has, dim3((unsigned)grid_of(D)), dim3(256), 0, s, block_view(im, D), im.d_table, D,
+    hipLaunchKernelGGL(k_class_has, dim3((unsigned)grid_of(D)), dim3(256), 0, s, block_view(im, D), class_table(im), D,
                        (uint32_t)column, has);
     MBRWT_HIP(hipGetLastError());
     const ClassHas f{im.classes, im.class_bits, has};

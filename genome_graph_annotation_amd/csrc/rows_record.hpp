@@ -16,7 +16,8 @@ namespace mbrwt {
 struct RowsView {
     uint64_t blocks, spill, magic, num_rows;
     uint32_t B, S;
-    uint32_t nib;  // masks stored as nibble codes (RowsImage::nib)
+    uint32_t nib;   // masks stored as nibble codes (RowsImage::nib)
+    uint32_t term;  // terminal records (RowsImage::term): `table` is the TT table
 };
 __device__ __forceinline__ uint64_t rows_block(uint64_t r, uint32_t S, uint64_t magic) {
     return S == 1 ? r : __umul64hi(r, magic);
@@ -134,6 +135,59 @@ __device__ bool rwt_walk(const uint32_t *table, MaskFn mask, LeafFn leaf, InnerF
         first = nw & 0xFFFFFFu;
     }
     return ok;
+}
+
+// TERMINAL records (r06, MBRWT_BUILD_ROWS_CODE = 2; rows.hip
+// build_term_tables): a row's descent as the leaf parents and leaves it
+// reaches ("terminals"), in pre-order, each a w-bit field {terminal id
+// [0, ib), its children mask [ib, w)} packed LSB-first -- the internal
+// nodes' masks are implied by the terminals below them.  The TT table: [0]
+// w | ib << 8, [1] nT, [2..3] 0, nT RWT2 entry words (leaf / leaf parent /
+// listed leaf parent: term_label's forms), then the u16 column lists.  The
+// fields are read until the record's count of labels is reached.
+__device__ __forceinline__ uint32_t tt_label(uint32_t e, const uint16_t *lst, uint32_t bit) {
+    const uint32_t i = (e & 0xFFFFu) + bit;
+    return ((e >> 29) & 1u) ? (uint32_t)lst[i] : i;
+}
+struct NoTerm {
+    __device__ void operator()(uint32_t) const {}
+};
+template <class ByteFn, class LeafFn, class TermFn = NoTerm>
+__device__ bool term_walk(const uint32_t *tt, ByteFn byte, uint32_t count, LeafFn leaf, TermFn onterm = TermFn()) {
+    const uint32_t hdr = tt[0], w = hdr & 0xFFu, ib = (hdr >> 8) & 0xFFu, nT = tt[1];
+    const uint32_t *ent = tt + 4;
+    const uint16_t *lst = reinterpret_cast<const uint16_t *>(ent + nT);
+    uint32_t left = count, bit = 0;
+    while (left) {
+        const uint32_t b0 = bit >> 3, sh = bit & 7u;
+        uint64_t v = 0;
+        for (uint32_t k = 0; 8u * k < sh + w; ++k) v |= (uint64_t)byte(b0 + k) << (8u * k);
+        const uint32_t f = (uint32_t)(v >> sh) & ((1u << w) - 1u);
+        bit += w;
+        const uint32_t id = f & ((1u << ib) - 1u);
+        if (id >= nT) return false;
+        const uint32_t e = ent[id];
+        uint32_t x = (e >> 30) == 3u ? (f >> ib) : 1u;  // a leaf parent: its set children; a leaf: itself
+        if (!x) return false;
+        onterm(id);
+        for (; x && left; x &= x - 1u, --left) leaf(tt_label(e, lst, (uint32_t)__builtin_ctz(x)));
+        if (x) return false;  // (more labels than the record's count)
+    }
+    return true;
+}
+// one record's labels in pre-order, whatever its form: leaf(column) per
+// label, inner(arity) per mask read (the mask forms only)
+template <class ByteFn, class LeafFn, class InnerFn>
+__device__ __forceinline__ bool record_walk_bytes(const RowsView &v, const uint32_t *table, ByteFn byte, uint32_t count,
+                                                  LeafFn leaf, InnerFn inner) {
+    if (v.term) return term_walk(table, byte, count, leaf);
+    return rwt_walk(table, rec_masks(byte, v.nib), leaf, inner);
+}
+template <class LeafFn, class InnerFn>
+__device__ __forceinline__ bool record_walk(const RowsView &v, const uint32_t *table, uint64_t masks, uint32_t count,
+                                            LeafFn leaf, InnerFn inner) {
+    return record_walk_bytes(v, table, [&](uint32_t o) { return (uint32_t)gld_at<uint8_t>(masks + o); }, count, leaf,
+                             inner);
 }
 
 // record classes (rows_class.hip): row r's class, bits [r w, r w + w) of the

@@ -240,14 +240,18 @@ int mbrwt_ctx_clone(mbrwt_ctx *src, mbrwt_ctx **out);
                               and they at least halve the image), 0 never,
                               1 whenever they fit (always exact: every row's
                               record is compared with its class's)
-   MBRWT_BUILD_ROWS_CODE      how a row record stores its masks:
-                              0 (default) one byte per mask, 1 NIBBLE CODES
-                              -- a mask with one bit set as that bit's index
-                              in 4 bits, any other as 12 bits -- for uniform
-                              trees of arity <= 8 (the basic partitioner's:
-                              C2-C4; other trees keep bytes): 15.2 instead of
-                              21.3 bytes per Kingsford-shape record, three
-                              rows per 64-byte block */
+   MBRWT_BUILD_ROWS_CODE      how a row record stores the row's descent
+                              (DESIGN §4g, §4h): 0 (default) AUTO -- TERMINAL
+                              RECORDS where they are smaller than byte masks,
+                              else byte masks; 1 NIBBLE CODES -- a mask with
+                              one bit set as that bit's index in 4 bits, any
+                              other as 12 bits -- for uniform trees of arity
+                              <= 8 (other trees keep bytes); 2 terminal
+                              records where they fit: the leaf parents and
+                              leaves the descent reaches, in pre-order, each
+                              a field {id, its children mask} (masks <= 16
+                              bits, <= 4,096 terminals); 3 one byte per 8
+                              children of every internal node reached */
 #define MBRWT_BUILD_ROWS_VAR 4
 #define MBRWT_BUILD_VAR_LANES 5
 #define MBRWT_BUILD_ROWS_BLOCK 6

@@ -123,11 +123,13 @@ def test_random_matrices_rows(oracle_mod, n, m, d, part, arity, relax, layout):
     (20000, 100, 0.05, 8, 2),      # 100 = 12 x 8 + 4: a short last group is still uniform
     (3000, 7, 1.0, 2, 0),          # singleton groups pass through: mixed depths
 ])
-def test_odometer_walk(oracle_mod, n, m, d, arity, levels):
+def test_odometer_walk(oracle_mod, build_env, n, m, d, arity, levels):
     """rows_walk_path / rows_walk_uni (one lock-step iteration per reached leaf
     parent, with / without the path table) and the general walk
     (MBRWT_OPT_ROWS_WALK = 6) return the oracle's CSR on uniform trees;
-    non-uniform trees report 0 levels and keep the general walk."""
+    non-uniform trees report 0 levels and keep the general walk (byte-mask
+    records: the walks of terminal records are test_terminal_records')."""
+    build_env("MBRWT_ROWS_CODE", 3)
     O = oracle_mod
     from genome_graph_annotation_amd import BRWTDevice
     rng = np.random.default_rng(n + m)
@@ -159,11 +161,12 @@ def test_odometer_walk(oracle_mod, n, m, d, arity, levels):
     (4000, 300, 0.4, "greedy", 2, 10),     # long records: spills and the direct pass
     (3000, 7, 1.0, "basic", 2, 0),         # singleton groups pass through
 ])
-def test_tree_odometer(oracle_mod, n, m, d, part, arity, relax):
+def test_tree_odometer(oracle_mod, build_env, n, m, d, part, arity, relax):
     """rows_walk_tree (the default on non-uniform trees: one lock-step
     iteration per reached leaf parent or leaf, leaf parents at any depth,
     non-consecutive leaf parents walked as internal nodes, masks up to 16
     bits) returns the oracle's CSR, as do the stack walks it replaced."""
+    build_env("MBRWT_ROWS_CODE", 3)  # (byte masks: the odometers)
     O = oracle_mod
     from genome_graph_annotation_amd import BRWTDevice
     from genome_graph_annotation_amd import _lib as L
@@ -347,6 +350,10 @@ def test_every_block_shape(oracle_mod, bs, build_env):
     O = oracle_mod
     from genome_graph_annotation_amd import BRWTDevice
     build_env("MBRWT_ROWS_BS", bs)
+    # (byte masks: a fully dense row's terminal fields outgrow a 64-byte
+    # block where its masks do not, and AUTO then takes the variable-length
+    # records -- terminal records' spills and long rows: test_terminal_records)
+    build_env("MBRWT_ROWS_CODE", 3)
     rng = np.random.default_rng(5)
     n, m = 30000, 300
     # rows of very different lengths: most sparse, some dense (long records)
@@ -555,6 +562,7 @@ def test_nibble_codes(oracle_mod, build_env, n, m, d, arity):
     dense = rng.random((n, m)) < d
     t = O.OracleTree.from_dense(dense, "basic", arity)
     ex = t.export()
+    build_env("MBRWT_ROWS_CODE", 3)  # (byte masks: the baseline)
     plain = BRWTDevice.from_tree(ex, layout="rows")
     build_env("MBRWT_ROWS_CODE", 1)
     dev = BRWTDevice.from_tree(ex, layout="rows")
@@ -589,6 +597,93 @@ def test_nibble_codes(oracle_mod, build_env, n, m, d, arity):
     np.testing.assert_array_equal(cols_a, cols_o)
 
 
+@pytest.mark.parametrize("n,m,d,part,arity,relax", [
+    (20000, 2652, 0.003, "basic", 8, 0),      # the Kingsford shape (uniform)
+    (20000, 600, 0.01, "greedy", 2, 10),      # the reference's production shape: mixed depths, listed leaf parents
+    (20000, 300, 0.05, "greedy", 2, 4),
+    (20000, 256, 0.02, "greedy", 2, 0),       # binary greedy: 8+ internal levels
+    (20000, 250, 0.05, "basic", 12, 0),       # two-byte masks, mixed depths
+    (20000, 9, 0.2, "basic", 3, 0),           # the root's children are leaf parents
+    (2000, 12, 0.3, "basic", 16, 0),          # a one-level tree: the root is the only terminal
+    (3000, 7, 1.0, "basic", 2, 0),            # singleton groups: leaves beside internal nodes
+    (4000, 300, 0.4, "greedy", 2, 10),        # dense rows: long records, direct tiles (or bytes kept)
+])
+def test_terminal_records(oracle_mod, build_env, n, m, d, part, arity, relax):
+    """Terminal records (MBRWT_BUILD_ROWS_CODE = 2; the AUTO default where
+    smaller): each row as the leaf parents and leaves its descent reaches, in
+    pre-order -- every query (ordered CSR, point queries, columns,
+    count_labels, the V/L accounting, the async call) against the oracle and
+    the byte-mask image of the same tree, and the export back into the
+    reference's index columns."""
+    O = oracle_mod
+    import torch
+    from genome_graph_annotation_amd import BRWTDevice, MBRWTError, _lib as L
+    rng = np.random.default_rng(n + m + arity)
+    dense = rng.random((n, m)) < d
+    t = O.OracleTree.from_dense(dense, part, arity, relax)
+    ex = t.export()
+    build_env("MBRWT_ROWS_CODE", 3)  # (byte masks: the baseline)
+    plain = BRWTDevice.from_tree(ex, layout="rows")
+    build_env("MBRWT_ROWS_CODE", 2)
+    dev = BRWTDevice.from_tree(ex, layout="rows")
+    st, sp = dev.rows_stats(), plain.rows_stats()
+    assert not sp["terminal_records"]
+    # terminal fields where they shrink the records (bytes kept otherwise)
+    assert st["record_bytes"] <= sp["record_bytes"], (st, sp)
+    assert st["terminal_records"] == (st["record_bytes"] < sp["record_bytes"]), (st, sp)
+    if d <= 0.05:
+        assert st["terminal_records"], (st, sp)
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 20000)]).astype(np.uint64)
+    off_o, cols_o = _check_all(t, dev, rows, dense)
+    np.testing.assert_array_equal(_count_labels(dev, rows), _count_labels(plain, rows))
+    rt = torch.from_numpy(rows.view(np.int64)).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    stt = torch.zeros(3, dtype=torch.int64, device="cuda")
+    ot = torch.empty(len(rows) + 1, dtype=torch.int64, device="cuda")
+    ct = torch.empty(len(cols_o) + 1, dtype=torch.int32, device="cuda")
+    dev.get_rows_device_async(rt, ot, ct, stt, s)
+    torch.cuda.synchronize()
+    assert stt.cpu().tolist() == [len(cols_o), L.MBRWT_OK, 1 << L.MBRWT_OK]
+    np.testing.assert_array_equal(ot.cpu().numpy().view(np.uint64), off_o)
+    np.testing.assert_array_equal(ct.cpu().numpy().view(np.uint32)[:len(cols_o)], cols_o)
+    # the V accounting (the terminals' ancestor chains) and the export (the
+    # index columns rebuilt from the terminals) equal the byte records'
+    assert dev.count_work_device(rt) == plain.count_work_device(rt)
+    back = dev.export()
+    for k in ("num_children", "first_child", "leaf_column"):
+        np.testing.assert_array_equal(np.asarray(back[k]), np.asarray(ex[k]))
+    again = BRWTDevice.from_tree(back, layout="rows")
+    off_a, cols_a = again.get_rows(rows)
+    np.testing.assert_array_equal(off_a, off_o)
+    np.testing.assert_array_equal(cols_a, cols_o)
+    # out-of-range rows still report MBRWT_ERR_RANGE
+    with pytest.raises(MBRWTError) as ei:
+        dev.get_rows(np.array([n], dtype=np.uint64))
+    assert ei.value.status == L.MBRWT_ERR_RANGE
+
+
+def test_terminal_records_kingsford_synthetic(oracle_mod, build_env):
+    """The C2 shape generated on the device with terminal records: the whole
+    batch against the oracle's independent generator and the image against
+    the byte-coded one."""
+    O = oracle_mod
+    from genome_graph_annotation_amd import BRWTDevice
+    n, m, d = 1_000_000, 2652, 0.003
+    build_env("MBRWT_ROWS_CODE", 3)
+    plain = BRWTDevice.synthetic(n, m, d, 8, 42, layout="rows")
+    build_env("MBRWT_ROWS_CODE", 2)
+    dev = BRWTDevice.synthetic(n, m, d, 8, 42, layout="rows")
+    st = dev.rows_stats()
+    assert st["terminal_records"], st
+    assert dev.device_bytes() < plain.device_bytes(), (dev.device_bytes(), plain.device_bytes())
+    t = O.OracleTree.topdown(n, m, d, 8, 42)
+    rows = np.random.default_rng(42).integers(0, n, 300_000).astype(np.uint64)
+    off_o, cols_o = t.get_rows(rows)
+    off_d, cols_d = dev.get_rows(rows)
+    np.testing.assert_array_equal(off_d, off_o)
+    np.testing.assert_array_equal(cols_d, cols_o)
+
+
 def test_nibble_codes_kingsford_synthetic(oracle_mod, build_env):
     """The C2 shape generated on the device with nibble-coded records: the
     whole batch against the oracle's independent generator, three rows per
@@ -596,6 +691,7 @@ def test_nibble_codes_kingsford_synthetic(oracle_mod, build_env):
     O = oracle_mod
     from genome_graph_annotation_amd import BRWTDevice
     n, m, d = 1_000_000, 2652, 0.003
+    build_env("MBRWT_ROWS_CODE", 3)
     plain = BRWTDevice.synthetic(n, m, d, 8, 42, layout="rows")
     build_env("MBRWT_ROWS_CODE", 1)
     dev = BRWTDevice.synthetic(n, m, d, 8, 42, layout="rows")

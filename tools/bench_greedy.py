@@ -38,7 +38,10 @@ def measure(dev, rows_np, ref, variants, reps):
     s = torch.cuda.current_stream().cuda_stream
     off_o, cols_o = ref
     cols_t = torch.empty(len(cols_o) + 1024, dtype=torch.int32, device="cuda")
-    visits, labels = dev.count_work_device(rows_t, s)
+    try:
+        visits, labels = dev.count_work_device(rows_t, s)
+    except L.MBRWTError:  # terminal records: no V accounting
+        visits, labels = 0, len(ref[1])
     out = {}
     for v in variants:
         if isinstance(v, str):  # "wN": row records with MBRWT_OPT_ROWS_WALK = N
@@ -103,6 +106,9 @@ def main():
     ap.add_argument("--blocks", default="",
                     help="scaled shape: comma-separated row-record block shapes 'B:S' to build and measure one after "
                          "the other (MBRWT_BUILD_ROWS_BLOCK; '' = the automatic choice only, 'auto' names it)")
+    ap.add_argument("--rows-codes", default="0",
+                    help="comma-separated MBRWT_BUILD_ROWS_CODE values for the scaled shape: 0 mask bytes, "
+                         "2 terminal records (DESIGN §4h)")
     ap.add_argument("--layout", default="nodes", choices=["nodes", "rows", "both"],
                     help="device layout (include/mbrwt.h MBRWT_BUILD_LAYOUT)")
     a = ap.parse_args()
@@ -155,27 +161,28 @@ def main():
             from genome_graph_annotation_amd import _lib as LB
             from genome_graph_annotation_amd.brwt import build_option
             ref = None
-            for blk in (a.blocks.split(",") if a.blocks else ["auto"]):
+            for blk, code in [(b, int(c)) for b in (a.blocks.split(",") if a.blocks else ["auto"])
+                              for c in a.rows_codes.split(",")]:
                 t0 = time.time()
                 bs = 0 if blk == "auto" else (int(blk.split(":")[0]) << 8) | int(blk.split(":")[1])
                 with build_option(LB.MBRWT_BUILD_ROWS_FOOTPRINT,
                                   LB.MBRWT_ROWS_COMPACT if a.compact else LB.MBRWT_ROWS_FAST), \
-                        build_option(LB.MBRWT_BUILD_ROWS_BLOCK, bs):
+                        build_option(LB.MBRWT_BUILD_ROWS_BLOCK, bs), build_option(LB.MBRWT_BUILD_ROWS_CODE, code):
                     dev = BRWTDevice.synthetic_shaped(a.scaled_rows, keep, a.density, 42, layout=a.layout)
                 torch.cuda.synchronize()
                 gen_s = time.time() - t0
                 t0 = time.time()
                 if ref is None:
                     ref = O.topdown_get_rows_shaped(a.scaled_rows, keep, a.density, 42, srows)
-                log(f"scaled {shape} (blocks {blk}): {a.scaled_rows:,} rows, {len(nc)} nodes, max arity "
+                log(f"scaled {shape} (blocks {blk}, code {code}): {a.scaled_rows:,} rows, {len(nc)} nodes, max arity "
                     f"{int(nc.max())}, device {dev.device_bytes() / 1e9:.2f} GB (generated in {gen_s:.1f} s), "
                     f"kernel {dev.traverse_kernel()}, rows_stats {dev.rows_stats()}")
                 r = measure(dev, srows, ref, variants, a.reps)
                 r.update({"layout": dev.layout(), "rows_stats": dev.rows_stats(), "nodes": len(nc),
                           "max_arity": int(nc.max()), "device_bytes": int(dev.device_bytes()),
                           "generate_s": gen_s, "rows": a.scaled_rows, "batch": a.scaled_batch,
-                          "num_relations": int(dev.num_relations()), "blocks": blk})
-                res[f"scaled {shape}" + ("" if blk == "auto" else f" blocks {blk}")] = r
+                          "num_relations": int(dev.num_relations()), "blocks": blk, "rows_code": code})
+                res[f"scaled {shape}" + ("" if blk == "auto" else f" blocks {blk}") + (f" code {code}" if code else "")] = r
                 del dev
                 torch.cuda.empty_cache()
     print(json.dumps({"workload": f"C2 columns {a.rows:,} x {a.cols:,} d={a.density} (mt19937 seed 42), batch "

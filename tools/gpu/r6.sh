@@ -75,6 +75,23 @@ greedy_sq)  # SQ / TA counters of the greedy + relax traversal at 3.7 B rows (th
 rehearsal)  # bench.py's N > 1 step on the final sources: two ranks on one GPU over gloo, 1 B rows (two images fit)
   timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --dist-backend gloo --rows 1000000000 --steps 10 --warmup 3 --no-e2e > $O/rehearsal_2rank.log 2>&1
   ;;
+term)  # terminal records: their tests, C4 with them (parity) and ABAB against bytes, the greedy shape with both
+  timeout -k 10 500 $PYT tests/test_gpu_rows.py -k "terminal or nibble or odometer or async or errors or compact_cus" > $O/pytest_rows.log 2>&1 &&
+  timeout -k 10 300 python -u bench.py --no-e2e --no-probe --traffic off --rows-code 2 > $O/bench_c4_term_parity.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --rows-code 0 > $O/bench_c4_byte_1.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --rows-code 2 > $O/bench_c4_term_1.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --rows-code 0 > $O/bench_c4_byte_2.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --rows-code 2 > $O/bench_c4_term_2.log 2>&1 &&
+  timeout -k 10 600 python -u tools/bench_greedy.py --shape-npz tools/data/greedy_relax10_c2_shape.npz --scaled-rows 3700000000 --layout rows --variants 0 --reps 10 --skip-small --rows-codes 0,2 > $O/greedy_codes.log 2>&1
+  ;;
+greedy_default)  # the greedy + relax shape at 3.7 B rows with the library defaults (AUTO records)
+  timeout -k 10 600 python -u tools/bench_greedy.py --shape-npz tools/data/greedy_relax10_c2_shape.npz --scaled-rows 3700000000 --layout rows --variants 0 --reps 10 --skip-small > $O/greedy_default.log 2>&1
+  ;;
+final_rest)  # the files after a first failure in test_gpu_rows.py, smoke, then the full-size cases
+  timeout -k 10 900 $PYT -q tests/test_gpu_rows.py tests/test_gpu_shards.py tests/test_gpu_wire.py -m "gpu and not slow" > $O/pytest_rest.log 2>&1 &&
+  timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
+  timeout -k 10 900 $PYT tests -m "gpu and slow" > $O/pytest_gpu_slow.log 2>&1
+  ;;
 *) echo "unknown stage $STAGE"; exit 2 ;;
 esac || exit $?
 done
