@@ -101,6 +101,8 @@ def parse():
     ap.add_argument("--rows-code", type=int, default=0, choices=[0, 1, 2, 3],
                     help="row records (MBRWT_BUILD_ROWS_CODE): 0 the library default (AUTO: terminal records where "
                          "smaller, DESIGN §4h), 1 nibble codes (§4g), 2 terminal records, 3 byte masks")
+    ap.add_argument("--rows-block", default="",
+                    help="row records: force the block shape B:S (MBRWT_BUILD_ROWS_BLOCK; default: the cost model)")
     ap.add_argument("--compact-cus", type=int, default=0,
                     help="row records: run each query stream's compaction on a stream masked to K of every 32 "
                          "CUs (MBRWT_OPT_COMPACT_CUS, VERDICT r05 #1a; 0 = the library default, same stream)")
@@ -147,10 +149,18 @@ def kernel_source_hash():
     return h.hexdigest()[:16]
 
 
+def rows_block_opt(a):
+    """--rows-block B:S as MBRWT_BUILD_ROWS_BLOCK (B << 8 | S; 0 = the cost model)."""
+    if not a.rows_block:
+        return 0
+    b, s_ = (int(x) for x in a.rows_block.split(":"))
+    return b << 8 | s_
+
+
 def workload_args(a):
     return ["--rows", str(a.rows), "--cols", str(a.cols), "--density", repr(a.density), "--arity", str(a.arity),
             "--batch", str(a.batch), "--seed", str(a.seed), "--kernel", str(a.kernel), "--layout", a.layout,
-            "--rows-code", str(a.rows_code)]
+            "--rows-code", str(a.rows_code)] + (["--rows-block", a.rows_block] if a.rows_block else [])
 
 
 def pmc_pass(a):
@@ -159,7 +169,7 @@ def pmc_pass(a):
     from genome_graph_annotation_amd import BRWTDevice, _lib as L
     from genome_graph_annotation_amd.brwt import build_option
     torch.cuda.set_device(0)
-    with build_option(L.MBRWT_BUILD_ROWS_CODE, a.rows_code):
+    with build_option(L.MBRWT_BUILD_ROWS_CODE, a.rows_code), build_option(L.MBRWT_BUILD_ROWS_BLOCK, rows_block_opt(a)):
         mat = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, device=0, layout=a.layout)
     if a.kernel:
         mat.set_option(L.MBRWT_OPT_KERNEL, a.kernel)
@@ -411,7 +421,7 @@ def main():
 
     dev_t = torch.device("cuda", local)
     t0 = time.time()
-    with build_option(L.MBRWT_BUILD_ROWS_CODE, a.rows_code):
+    with build_option(L.MBRWT_BUILD_ROWS_CODE, a.rows_code), build_option(L.MBRWT_BUILD_ROWS_BLOCK, rows_block_opt(a)):
         mat = BRWTDevice.synthetic(a.rows, a.cols, a.density, a.arity, a.seed, device=local, layout=a.layout)
     setup_s = time.time() - t0
     struct_bytes = mat.device_bytes()
@@ -914,6 +924,7 @@ def main():
             "api": "mbrwt_get_rows_device_async" if use_async else "mbrwt_get_rows_device",
             "query_streams": Q,
             "rows_code": {0: "auto", 1: "nibble", 2: "terminal", 3: "byte"}[a.rows_code],
+            **({"rows_block": a.rows_block} if a.rows_block else {}),
             "records": ("terminal" if rstats and rstats.get("terminal_records") else
                         "nibble" if rstats and rstats.get("nibble_codes") else "byte"),
             **({"compact_cus_of_32": a.compact_cus} if a.compact_cus else {}),

@@ -92,6 +92,13 @@ final_rest)  # the files after a first failure in test_gpu_rows.py, smoke, then 
   timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
   timeout -k 10 900 $PYT tests -m "gpu and slow" > $O/pytest_gpu_slow.log 2>&1
   ;;
+term3)  # C4 terminal records at three rows per block (the compact image) against the cost model's two, ABAB
+  timeout -k 10 300 python -u bench.py --no-e2e --no-probe --traffic off --rows-block 64:3 > $O/bench_c4_s3_parity.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu > $O/bench_c4_s2_1.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --rows-block 64:3 > $O/bench_c4_s3_1.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu > $O/bench_c4_s2_2.log 2>&1 &&
+  timeout -k 10 200 $B --no-cpu --rows-block 64:3 > $O/bench_c4_s3_2.log 2>&1
+  ;;
 *) echo "unknown stage $STAGE"; exit 2 ;;
 esac || exit $?
 done
