@@ -99,6 +99,9 @@ term3)  # C4 terminal records at three rows per block (the compact image) agains
   timeout -k 10 200 $B --no-cpu > $O/bench_c4_s2_2.log 2>&1 &&
   timeout -k 10 200 $B --no-cpu --rows-block 64:3 > $O/bench_c4_s3_2.log 2>&1
   ;;
+footprint)  # device bytes against the reference's RRR bytes at 100 M rows with the r06 defaults (terminal records)
+  timeout -k 10 1100 python -u tools/footprint_scale.py > $O/footprint.jsonl 2> $O/footprint.log
+  ;;
 *) echo "unknown stage $STAGE"; exit 2 ;;
 esac || exit $?
 done
