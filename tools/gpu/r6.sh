@@ -102,6 +102,9 @@ term3)  # C4 terminal records at three rows per block (the compact image) agains
 footprint)  # device bytes against the reference's RRR bytes at 100 M rows with the r06 defaults (terminal records)
   timeout -k 10 1100 python -u tools/footprint_scale.py > $O/footprint.jsonl 2> $O/footprint.log
   ;;
+greedy_term_blocks)  # greedy + relax with terminal records (defaults) at the automatic block shape and 64:3 / 64:2
+  timeout -k 10 900 python -u tools/bench_greedy.py --shape-npz tools/data/greedy_relax10_c2_shape.npz --scaled-rows 3700000000 --layout rows --variants 0 --reps 10 --skip-small --blocks auto,64:3,64:2 > $O/greedy_term_blocks.log 2>&1
+  ;;
 *) echo "unknown stage $STAGE"; exit 2 ;;
 esac || exit $?
 done
