@@ -1575,10 +1575,18 @@ __device__ __forceinline__ void rows_walk_terms(const AS_LDS uint8_t *pb, uint32
     uint32_t bit = 8u * (a0 & 3u);
     uint32_t left = live ? cnt : 0u;
     uint32_t ob = pos * 2u;  // byte offset of the next label
+    // (fixed-width fields: the next field's words are read before this
+    // field's entry and labels, off the dependency chain)
+    uint32_t lo = 0, hi = 0;
+    if (left) {
+        lo = wp[bit >> 5];
+        hi = wp[(bit >> 5) + 1];
+    }
     while (left) {
-        const uint32_t wi = bit >> 5;
-        const uint32_t f = __builtin_amdgcn_alignbit(wp[wi + 1], wp[wi], bit & 31u) & fmask;
+        const uint32_t f = __builtin_amdgcn_alignbit(hi, lo, bit & 31u) & fmask;
         bit += w;
+        lo = wp[bit >> 5];
+        hi = wp[(bit >> 5) + 1];
         const uint32_t e = ent[f & imask];
         uint32_t x = (e >> 30) == 3u ? (f >> ib) : 1u;  // a leaf parent: its set children; a leaf: itself
         x = x ? x : 1u;  // (a corrupt field: one label, so the loop still ends)
