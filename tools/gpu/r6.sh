@@ -116,6 +116,12 @@ prefetch)  # terminal walk reading the next field's words early: tests, then ABA
   timeout -k 10 600 $H python -u tools/bench_greedy.py --shape-npz tools/data/greedy_relax10_c2_shape.npz --scaled-rows 3700000000 --layout rows --variants 0 --reps 10 --skip-small > $O/greedy_head.log 2>&1 &&
   timeout -k 10 600 python -u tools/bench_greedy.py --shape-npz tools/data/greedy_relax10_c2_shape.npz --scaled-rows 3700000000 --layout rows --variants 0 --reps 10 --skip-small > $O/greedy_new.log 2>&1
   ;;
+c4_sq)  # SQ / TA counters of the C4 traversal with terminal records (r05's three passes)
+  C="python -u bench.py --no-cpu --no-e2e --no-probe --traffic off --steps 3 --warmup 1"
+  timeout -s KILL 400 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS -d $O/sq1 -o run --output-format csv -- $C > $O/sq1.log 2>&1 &&
+  timeout -s KILL 400 rocprofv3 --pmc SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS -d $O/sq2 -o run --output-format csv -- $C > $O/sq2.log 2>&1 &&
+  timeout -s KILL 400 rocprofv3 --pmc GRBM_COUNT GRBM_GUI_ACTIVE SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM_WR TA_BUFFER_WAVEFRONTS_sum TA_TA_BUSY_sum -d $O/sq3 -o run --output-format csv -- $C > $O/sq3.log 2>&1
+  ;;
 *) echo "unknown stage $STAGE"; exit 2 ;;
 esac || exit $?
 done
