@@ -106,6 +106,7 @@ greedy_term_blocks)  # greedy + relax with terminal records (defaults) at the au
   timeout -k 10 900 python -u tools/bench_greedy.py --shape-npz tools/data/greedy_relax10_c2_shape.npz --scaled-rows 3700000000 --layout rows --variants 0 --reps 10 --skip-small --blocks auto,64:3,64:2 > $O/greedy_term_blocks.log 2>&1
   ;;
 prefetch)  # terminal walk reading the next field's words early: tests, then ABAB C4 and greedy against the previous build
+  # (needs tools/_ab/libmbrwt_head.so: the previous commit's libmbrwt.so, copied there before the change)
   H="env MBRWT_LIB=tools/_ab/libmbrwt_head.so"
   timeout -k 10 400 $PYT tests/test_gpu_rows.py -k "terminal or async or errors or reference_grids or random_matrices or compact_cus" > $O/pytest_rows.log 2>&1 &&
   timeout -k 10 300 python -u bench.py --no-e2e --no-probe --traffic off > $O/bench_c4_parity.log 2>&1 &&
