@@ -123,6 +123,16 @@ c4_sq)  # SQ / TA counters of the C4 traversal with terminal records (r05's thre
   timeout -s KILL 400 rocprofv3 --pmc SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS -d $O/sq2 -o run --output-format csv -- $C > $O/sq2.log 2>&1 &&
   timeout -s KILL 400 rocprofv3 --pmc GRBM_COUNT GRBM_GUI_ACTIVE SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM_WR TA_BUFFER_WAVEFRONTS_sum TA_TA_BUSY_sum -d $O/sq3 -o run --output-format csv -- $C > $O/sq3.log 2>&1
   ;;
+configs)  # BASELINE configs[1] (C2) and configs[2] (C3) on HEAD: whole-batch parity, live PMC
+  timeout -k 10 400 python -u bench.py --workload c2 --no-e2e > $O/bench_c2.log 2>&1 &&
+  timeout -k 10 600 python -u bench.py --workload c3 --no-e2e > $O/bench_c3.log 2>&1
+  ;;
+c2ab)  # C2 (cache-resident) with terminal records against byte masks, ABAB
+  timeout -k 10 200 $B --workload c2 --no-cpu --rows-code 3 > $O/bench_c2_byte_1.log 2>&1 &&
+  timeout -k 10 200 $B --workload c2 --no-cpu > $O/bench_c2_term_1.log 2>&1 &&
+  timeout -k 10 200 $B --workload c2 --no-cpu --rows-code 3 > $O/bench_c2_byte_2.log 2>&1 &&
+  timeout -k 10 200 $B --workload c2 --no-cpu > $O/bench_c2_term_2.log 2>&1
+  ;;
 *) echo "unknown stage $STAGE"; exit 2 ;;
 esac || exit $?
 done
